@@ -1,0 +1,963 @@
+"""paddle.nn.functional (parity: python/paddle/nn/functional/*.py).
+
+Hot ops route to the HIP kernel registry (``ops.fused``): layer_norm,
+rms_norm, softmax (last axis), softmax_with_cross_entropy / cross_entropy
+(hard labels), gelu(+bias), flash/scaled-dot-product attention. GEMM/conv go to
+hipBLASLt / MIOpen through PyTorch-ROCm.
+"""
+import math
+
+import numpy as np
+import torch
+import torch.nn.functional as TF
+
+from ...framework.core import Tensor, _u, convert_dtype
+from ...ops import fused as K
+
+
+def _t(x):
+    return x._t if isinstance(x, Tensor) else x
+
+
+def _w(t):
+    return Tensor(t)
+
+
+def _opt(x):
+    return None if x is None else _t(x)
+
+
+# =============================================================================
+# activations
+# =============================================================================
+def relu(x, name=None):
+    return _w(torch.relu(_t(x)))
+
+
+def relu_(x, name=None):
+    torch.relu_(x._t)
+    return x
+
+
+def relu6(x, name=None):
+    return _w(TF.relu6(_t(x)))
+
+
+def leaky_relu(x, negative_slope=0.01, name=None):
+    return _w(TF.leaky_relu(_t(x), negative_slope))
+
+
+def elu(x, alpha=1.0, name=None):
+    return _w(TF.elu(_t(x), alpha))
+
+
+def elu_(x, alpha=1.0, name=None):
+    TF.elu_(x._t, alpha)
+    return x
+
+
+def celu(x, alpha=1.0, name=None):
+    return _w(TF.celu(_t(x), alpha))
+
+
+def selu(x, scale=1.0507009873554804934193349852946, alpha=1.6732632423543772848170429916717,
+         name=None):
+    t = _t(x)
+    return _w(scale * torch.where(t > 0, t, alpha * (torch.exp(t) - 1)))
+
+
+def gelu(x, approximate=False, name=None):
+    t = _t(x)
+    if t.is_cuda:
+        return _w(K.bias_gelu(t, None, bool(approximate)))
+    return _w(TF.gelu(t, approximate='tanh' if approximate else 'none'))
+
+
+def fused_bias_gelu(x, bias, approximate=False):
+    return _w(K.bias_gelu(_t(x), _t(bias), bool(approximate)))
+
+
+def silu(x, name=None):
+    return _w(TF.silu(_t(x)))
+
+
+def swish(x, name=None):
+    return _w(TF.silu(_t(x)))
+
+
+def mish(x, name=None):
+    return _w(TF.mish(_t(x)))
+
+
+def sigmoid(x, name=None):
+    return _w(torch.sigmoid(_t(x)))
+
+
+def tanh(x, name=None):
+    return _w(torch.tanh(_t(x)))
+
+
+def tanh_(x, name=None):
+    x._t.tanh_()
+    return x
+
+
+def hardtanh(x, min=-1.0, max=1.0, name=None):
+    return _w(TF.hardtanh(_t(x), min, max))
+
+
+def hardsigmoid(x, slope=0.1666667, offset=0.5, name=None):
+    return _w(torch.clamp(_t(x) * slope + offset, 0, 1))
+
+
+def hardswish(x, name=None):
+    return _w(TF.hardswish(_t(x)))
+
+
+def hardshrink(x, threshold=0.5, name=None):
+    return _w(TF.hardshrink(_t(x), threshold))
+
+
+def softshrink(x, threshold=0.5, name=None):
+    return _w(TF.softshrink(_t(x), threshold))
+
+
+def softsign(x, name=None):
+    return _w(TF.softsign(_t(x)))
+
+
+def softplus(x, beta=1, threshold=20, name=None):
+    return _w(TF.softplus(_t(x), beta, threshold))
+
+
+def tanhshrink(x, name=None):
+    return _w(TF.tanhshrink(_t(x)))
+
+
+def thresholded_relu(x, threshold=1.0, name=None):
+    t = _t(x)
+    return _w(torch.where(t > threshold, t, torch.zeros_like(t)))
+
+
+def log_sigmoid(x, name=None):
+    return _w(TF.logsigmoid(_t(x)))
+
+
+def prelu(x, weight, data_format='NCHW', name=None):
+    t, w = _t(x), _t(weight)
+    if w.numel() > 1 and data_format in ('NHWC', 'NLC', 'NDHWC'):
+        return _w(torch.where(t >= 0, t, t * w))
+    return _w(TF.prelu(t, w))
+
+
+def rrelu(x, lower=1. / 8., upper=1. / 3., training=True, name=None):
+    return _w(TF.rrelu(_t(x), lower, upper, training))
+
+
+def maxout(x, groups, axis=1, name=None):
+    t = _t(x)
+    shp = list(t.shape)
+    c = shp[axis]
+    shp[axis:axis + 1] = [c // groups, groups]
+    return _w(t.reshape(shp).amax(axis + 1))
+
+
+def glu(x, axis=-1, name=None):
+    return _w(TF.glu(_t(x), axis))
+
+
+def softmax(x, axis=-1, dtype=None, name=None):
+    t = _t(x)
+    if dtype is not None:
+        t = t.to(convert_dtype(dtype))
+    if t.is_cuda and (axis == -1 or axis == t.dim() - 1):
+        return _w(K.softmax_lastdim(t))
+    return _w(torch.softmax(t, axis))
+
+
+def softmax_(x, axis=-1, dtype=None, name=None):
+    r = softmax(x, axis, dtype)
+    object.__setattr__(x, '_t', r._t)
+    return x
+
+
+def log_softmax(x, axis=-1, dtype=None, name=None):
+    t = _t(x)
+    if dtype is not None:
+        t = t.to(convert_dtype(dtype))
+    return _w(torch.log_softmax(t, axis))
+
+
+def gumbel_softmax(x, temperature=1.0, hard=False, axis=-1, name=None):
+    return _w(TF.gumbel_softmax(_t(x), tau=temperature, hard=hard, dim=axis))
+
+
+# =============================================================================
+# common
+# =============================================================================
+def linear(x, weight, bias=None, name=None):
+    """y = x @ W + b with paddle's [in, out] weight layout (hipBLASLt GEMM)."""
+    t, w = _t(x), _t(weight)
+    if bias is not None:
+        b = _t(bias)
+        if t.dim() == 2:
+            return _w(torch.addmm(b, t, w))
+        return _w(torch.addmm(b, t.reshape(-1, t.shape[-1]), w).reshape(*t.shape[:-1], w.shape[-1]))
+    return _w(torch.matmul(t, w))
+
+
+def bilinear(x1, x2, weight, bias=None, name=None):
+    return _w(TF.bilinear(_t(x1), _t(x2), _t(weight), None if bias is None else _t(bias).flatten()))
+
+
+def dropout(x, p=0.5, axis=None, training=True, mode='upscale_in_train', name=None):
+    t = _t(x)
+    if not training or p == 0:
+        if mode == 'downscale_in_infer' and not training:
+            return _w(t * (1 - p))
+        return x if isinstance(x, Tensor) else _w(t)
+    if axis is not None:
+        axes = [axis] if isinstance(axis, int) else list(axis)
+        mshape = [t.shape[i] if i in [a % t.dim() for a in axes] else 1 for i in range(t.dim())]
+        mask = (torch.rand(mshape, device=t.device) >= p).to(t.dtype)
+        out = t * mask
+        return _w(out / (1 - p) if mode == 'upscale_in_train' else out)
+    if mode == 'upscale_in_train':
+        return _w(TF.dropout(t, p, True))
+    return _w(t * (torch.rand_like(t, dtype=torch.float32) >= p).to(t.dtype))
+
+
+def dropout2d(x, p=0.5, training=True, data_format='NCHW', name=None):
+    t = _t(x)
+    if data_format == 'NHWC':
+        return _w(TF.dropout2d(t.permute(0, 3, 1, 2), p, training).permute(0, 2, 3, 1))
+    return _w(TF.dropout2d(t, p, training))
+
+
+def dropout3d(x, p=0.5, training=True, data_format='NCDHW', name=None):
+    return _w(TF.dropout3d(_t(x), p, training))
+
+
+def alpha_dropout(x, p=0.5, training=True, name=None):
+    return _w(TF.alpha_dropout(_t(x), p, training))
+
+
+def label_smooth(label, prior_dist=None, epsilon=0.1, name=None):
+    t = _t(label)
+    n = t.shape[-1]
+    pd = (1.0 / n) if prior_dist is None else _t(prior_dist)
+    return _w((1 - epsilon) * t + epsilon * pd)
+
+
+def one_hot(x, num_classes, name=None):
+    return _w(TF.one_hot(_t(x).long(), num_classes).float())
+
+
+def embedding(x, weight, padding_idx=None, sparse=False, name=None):
+    w = _t(weight)
+    if padding_idx is not None and padding_idx < 0:
+        padding_idx += w.shape[0]
+    return _w(TF.embedding(_t(x).long(), w, padding_idx))
+
+
+def pad(x, pad, mode='constant', value=0.0, data_format='NCHW', name=None):
+    t = _t(x)
+    if isinstance(pad, Tensor):
+        pad = pad.tolist()
+    pad = list(pad)
+    nd = t.dim()
+    if len(pad) == 2 * nd:
+        # paddle full-rank pad: [d0_before, d0_after, d1_before, ...] -> torch reversed pairs
+        tp = []
+        for i in reversed(range(nd)):
+            tp += [pad[2 * i], pad[2 * i + 1]]
+        return _w(TF.pad(t, tp, mode=mode if mode != 'edge' else 'replicate', value=value))
+    channel_last = data_format in ('NHWC', 'NLC', 'NDHWC')
+    if channel_last:
+        t = t.movedim(-1, 1)
+    # paddle pads spatial dims as [left, right, top, bottom, front, back] (last dim first)
+    m = {'constant': 'constant', 'reflect': 'reflect', 'replicate': 'replicate', 'edge': 'replicate',
+         'circular': 'circular'}[mode]
+    out = TF.pad(t, pad, mode=m, value=value) if m == 'constant' else TF.pad(t, pad, mode=m)
+    if channel_last:
+        out = out.movedim(1, -1)
+    return _w(out)
+
+
+def zeropad2d(x, padding, data_format='NCHW', name=None):
+    if isinstance(padding, int):
+        padding = [padding] * 4
+    return pad(x, padding, 'constant', 0.0, data_format)
+
+
+def cosine_similarity(x1, x2, axis=1, eps=1e-8):
+    return _w(TF.cosine_similarity(_t(x1), _t(x2), axis, eps))
+
+
+def pairwise_distance(x, y, p=2.0, epsilon=1e-6, keepdim=False, name=None):
+    return _w(TF.pairwise_distance(_t(x), _t(y), p, epsilon, keepdim))
+
+
+def normalize(x, p=2, axis=1, epsilon=1e-12, name=None):
+    return _w(TF.normalize(_t(x), p, axis, epsilon))
+
+
+def interpolate(x, size=None, scale_factor=None, mode='nearest', align_corners=False,
+                align_mode=0, data_format='NCHW', name=None):
+    t = _t(x)
+    cl = data_format in ('NHWC', 'NLC', 'NDHWC')
+    if cl:
+        t = t.movedim(-1, 1)
+    if isinstance(size, Tensor):
+        size = size.tolist()
+    if isinstance(size, (list, tuple)):
+        size = [int(s.item()) if isinstance(s, Tensor) else int(s) for s in size]
+    m = {'nearest': 'nearest', 'bilinear': 'bilinear', 'trilinear': 'trilinear', 'bicubic': 'bicubic',
+         'linear': 'linear', 'area': 'area'}[mode.lower()]
+    kw = {} if m in ('nearest', 'area') else {'align_corners': align_corners}
+    out = TF.interpolate(t, size=size, scale_factor=scale_factor, mode=m, **kw)
+    if cl:
+        out = out.movedim(1, -1)
+    return _w(out)
+
+
+upsample = interpolate
+
+
+def unfold(x, kernel_sizes, strides=1, paddings=0, dilations=1, name=None):
+    if isinstance(paddings, (list, tuple)) and len(paddings) == 4:
+        t = TF.pad(_t(x), [paddings[1], paddings[3], paddings[0], paddings[2]])
+        return _w(TF.unfold(t, kernel_sizes, dilations, 0, strides))
+    return _w(TF.unfold(_t(x), kernel_sizes, dilations, paddings, strides))
+
+
+def fold(x, output_sizes, kernel_sizes, strides=1, paddings=0, dilations=1, name=None):
+    return _w(TF.fold(_t(x), output_sizes, kernel_sizes, dilations, paddings, strides))
+
+
+def pixel_shuffle(x, upscale_factor, data_format='NCHW', name=None):
+    t = _t(x)
+    if data_format == 'NHWC':
+        return _w(TF.pixel_shuffle(t.permute(0, 3, 1, 2), upscale_factor).permute(0, 2, 3, 1))
+    return _w(TF.pixel_shuffle(t, upscale_factor))
+
+
+def pixel_unshuffle(x, downscale_factor, data_format='NCHW', name=None):
+    t = _t(x)
+    if data_format == 'NHWC':
+        return _w(TF.pixel_unshuffle(t.permute(0, 3, 1, 2), downscale_factor).permute(0, 2, 3, 1))
+    return _w(TF.pixel_unshuffle(t, downscale_factor))
+
+
+def channel_shuffle(x, groups, data_format='NCHW', name=None):
+    t = _t(x)
+    if data_format == 'NHWC':
+        return _w(TF.channel_shuffle(t.permute(0, 3, 1, 2), groups).permute(0, 2, 3, 1))
+    return _w(TF.channel_shuffle(t, groups))
+
+
+def affine_grid(theta, out_shape, align_corners=True, name=None):
+    if isinstance(out_shape, Tensor):
+        out_shape = out_shape.tolist()
+    return _w(TF.affine_grid(_t(theta), list(out_shape), align_corners))
+
+
+def grid_sample(x, grid, mode='bilinear', padding_mode='zeros', align_corners=True, name=None):
+    return _w(TF.grid_sample(_t(x), _t(grid), mode, padding_mode, align_corners))
+
+
+def sequence_mask(x, maxlen=None, dtype='int64', name=None):
+    t = _t(x)
+    maxlen = int(t.max().item()) if maxlen is None else int(maxlen)
+    r = torch.arange(maxlen, device=t.device)
+    return _w((r < t.unsqueeze(-1)).to(convert_dtype(dtype)))
+
+
+def diag_embed(input, offset=0, dim1=-2, dim2=-1):
+    return _w(torch.diag_embed(_t(input), offset, dim1, dim2))
+
+
+def temporal_shift(x, seg_num, shift_ratio=0.25, name=None, data_format='NCHW'):
+    t = _t(x)
+    nt, c, h, w = t.shape
+    n = nt // seg_num
+    t = t.reshape(n, seg_num, c, h, w)
+    fold = int(c * shift_ratio)
+    out = torch.zeros_like(t)
+    out[:, :-1, :fold] = t[:, 1:, :fold]
+    out[:, 1:, fold:2 * fold] = t[:, :-1, fold:2 * fold]
+    out[:, :, 2 * fold:] = t[:, :, 2 * fold:]
+    return _w(out.reshape(nt, c, h, w))
+
+
+# =============================================================================
+# conv / pool
+# =============================================================================
+def _ntuple(v, n):
+    if isinstance(v, (list, tuple)):
+        return tuple(v) if len(v) == n else tuple(v) * (n // len(v))
+    return (v,) * n
+
+
+def _conv_padding(padding, n, t=None, ksize=None, stride=None, dilation=None):
+    if isinstance(padding, str):
+        p = padding.upper()
+        if p == 'VALID':
+            return 0, None
+        if p == 'SAME':
+            return 'same', None
+    if isinstance(padding, (list, tuple)):
+        padding = list(padding)
+        if len(padding) == 2 * n and not isinstance(padding[0], (list, tuple)):
+            if all(padding[2 * i] == padding[2 * i + 1] for i in range(n)):
+                return tuple(padding[0::2]), None
+            tp = []
+            for i in reversed(range(n)):
+                tp += [padding[2 * i], padding[2 * i + 1]]
+            return 0, tp
+        if len(padding) == n + 2 and isinstance(padding[0], (list, tuple)):
+            sp = [p for p in padding if list(p) != [0, 0]]
+            padding = [x for p in padding[2:] for x in p] if len(sp) <= n else sp
+            return _conv_padding(padding, n)
+    return _ntuple(padding, n), None
+
+
+def _conv(fn, n, x, weight, bias, stride, padding, dilation, groups, data_format):
+    t = _t(x)
+    cl = data_format in ('NHWC', 'NLC', 'NDHWC')
+    if cl:
+        t = t.movedim(-1, 1)
+    pad_, extra = _conv_padding(padding, n)
+    if extra is not None:
+        t = TF.pad(t, extra)
+    w = _t(weight)
+    if t.dtype != w.dtype:
+        t = t.to(w.dtype)
+    out = fn(t, w, None if bias is None else _t(bias), _ntuple(stride, n), pad_,
+             _ntuple(dilation, n), groups)
+    if cl:
+        out = out.movedim(1, -1)
+    return _w(out)
+
+
+def conv1d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, data_format='NCL',
+           name=None):
+    return _conv(TF.conv1d, 1, x, weight, bias, stride, padding, dilation, groups, data_format)
+
+
+def conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, data_format='NCHW',
+           name=None):
+    return _conv(TF.conv2d, 2, x, weight, bias, stride, padding, dilation, groups, data_format)
+
+
+def conv3d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, data_format='NCDHW',
+           name=None):
+    return _conv(TF.conv3d, 3, x, weight, bias, stride, padding, dilation, groups, data_format)
+
+
+def _conv_t(fn, n, x, weight, bias, stride, padding, output_padding, dilation, groups, output_size,
+            data_format):
+    t = _t(x)
+    cl = data_format in ('NHWC', 'NLC', 'NDHWC')
+    if cl:
+        t = t.movedim(-1, 1)
+    pad_, _ = _conv_padding(padding, n)
+    if pad_ == 'same':
+        pad_ = tuple((k - 1) // 2 for k in _t(weight).shape[2:])
+    st, dl = _ntuple(stride, n), _ntuple(dilation, n)
+    op = _ntuple(output_padding, n)
+    if output_size is not None:
+        if isinstance(output_size, int):
+            output_size = [output_size] * n
+        ks = _t(weight).shape[2:]
+        base = [(t.shape[2 + i] - 1) * st[i] - 2 * pad_[i] + dl[i] * (ks[i] - 1) + 1 for i in range(n)]
+        op = tuple(int(o) - b for o, b in zip(output_size, base))
+    out = fn(t, _t(weight), None if bias is None else _t(bias), st, pad_, op, groups, dl)
+    if cl:
+        out = out.movedim(1, -1)
+    return _w(out)
+
+
+def conv1d_transpose(x, weight, bias=None, stride=1, padding=0, output_padding=0, groups=1,
+                     dilation=1, output_size=None, data_format='NCL', name=None):
+    return _conv_t(TF.conv_transpose1d, 1, x, weight, bias, stride, padding, output_padding, dilation,
+                   groups, output_size, data_format)
+
+
+def conv2d_transpose(x, weight, bias=None, stride=1, padding=0, output_padding=0, dilation=1,
+                     groups=1, output_size=None, data_format='NCHW', name=None):
+    return _conv_t(TF.conv_transpose2d, 2, x, weight, bias, stride, padding, output_padding, dilation,
+                   groups, output_size, data_format)
+
+
+def conv3d_transpose(x, weight, bias=None, stride=1, padding=0, output_padding=0, groups=1,
+                     dilation=1, output_size=None, data_format='NCDHW', name=None):
+    return _conv_t(TF.conv_transpose3d, 3, x, weight, bias, stride, padding, output_padding, dilation,
+                   groups, output_size, data_format)
+
+
+def _pool_pad(padding, n):
+    if isinstance(padding, str):
+        return padding.upper(), None
+    if isinstance(padding, (list, tuple)) and len(padding) == 2 * n:
+        if all(padding[2 * i] == padding[2 * i + 1] for i in range(n)):
+            return tuple(padding[0::2]), None
+        tp = []
+        for i in reversed(range(n)):
+            tp += [padding[2 * i], padding[2 * i + 1]]
+        return 0, tp
+    return _ntuple(padding, n), None
+
+
+def _pool(kind, n, x, kernel_size, stride, padding, ceil_mode, data_format, exclusive=True,
+          return_mask=False, divisor_override=None):
+    t = _t(x)
+    cl = data_format in ('NHWC', 'NLC', 'NDHWC')
+    if cl:
+        t = t.movedim(-1, 1)
+    ks = _ntuple(kernel_size, n)
+    st = ks if stride is None else _ntuple(stride, n)
+    pd, extra = _pool_pad(padding, n)
+    if pd == 'VALID':
+        pd = (0,) * n
+    elif pd == 'SAME':
+        outs = [math.ceil(t.shape[2 + i] / st[i]) for i in range(n)]
+        tot = [max((outs[i] - 1) * st[i] + ks[i] - t.shape[2 + i], 0) for i in range(n)]
+        extra = []
+        for i in reversed(range(n)):
+            extra += [tot[i] // 2, tot[i] - tot[i] // 2]
+        pd = (0,) * n
+    if extra is not None:
+        t = TF.pad(t, extra, value=float('-inf') if kind == 'max' else 0.0)
+    if kind == 'max':
+        fn = {1: TF.max_pool1d, 2: TF.max_pool2d, 3: TF.max_pool3d}[n]
+        r = fn(t, ks, st, pd, 1, ceil_mode, return_mask)
+        if return_mask:
+            out, mask = r
+            return (_w(out.movedim(1, -1) if cl else out), _w(mask))
+        out = r
+    else:
+        fn = {1: TF.avg_pool1d, 2: TF.avg_pool2d, 3: TF.avg_pool3d}[n]
+        kw = {} if n == 1 else {'divisor_override': divisor_override}
+        out = fn(t, ks, st, pd, ceil_mode, not exclusive, **kw)
+    if cl:
+        out = out.movedim(1, -1)
+    return _w(out)
+
+
+def max_pool1d(x, kernel_size, stride=None, padding=0, return_mask=False, ceil_mode=False,
+               name=None):
+    return _pool('max', 1, x, kernel_size, stride, padding, ceil_mode, 'NCL', return_mask=return_mask)
+
+
+def max_pool2d(x, kernel_size, stride=None, padding=0, return_mask=False, ceil_mode=False,
+               data_format='NCHW', name=None):
+    return _pool('max', 2, x, kernel_size, stride, padding, ceil_mode, data_format,
+                 return_mask=return_mask)
+
+
+def max_pool3d(x, kernel_size, stride=None, padding=0, return_mask=False, ceil_mode=False,
+               data_format='NCDHW', name=None):
+    return _pool('max', 3, x, kernel_size, stride, padding, ceil_mode, data_format,
+                 return_mask=return_mask)
+
+
+def avg_pool1d(x, kernel_size, stride=None, padding=0, exclusive=True, ceil_mode=False, name=None):
+    return _pool('avg', 1, x, kernel_size, stride, padding, ceil_mode, 'NCL', exclusive)
+
+
+def avg_pool2d(x, kernel_size, stride=None, padding=0, ceil_mode=False, exclusive=True,
+               divisor_override=None, data_format='NCHW', name=None):
+    return _pool('avg', 2, x, kernel_size, stride, padding, ceil_mode, data_format, exclusive,
+                 divisor_override=divisor_override)
+
+
+def avg_pool3d(x, kernel_size, stride=None, padding=0, ceil_mode=False, exclusive=True,
+               divisor_override=None, data_format='NCDHW', name=None):
+    return _pool('avg', 3, x, kernel_size, stride, padding, ceil_mode, data_format, exclusive,
+                 divisor_override=divisor_override)
+
+
+def _adaptive(fn, x, output_size, data_format, return_mask=False):
+    t = _t(x)
+    cl = data_format in ('NHWC', 'NLC', 'NDHWC')
+    if cl:
+        t = t.movedim(-1, 1)
+    if isinstance(output_size, (list, tuple)):
+        output_size = tuple(t.shape[2 + i] if o is None else o for i, o in enumerate(output_size))
+    r = fn(t, output_size, return_mask) if return_mask else fn(t, output_size)
+    if return_mask:
+        return _w(r[0]), _w(r[1])
+    return _w(r.movedim(1, -1) if cl else r)
+
+
+def adaptive_avg_pool1d(x, output_size, name=None):
+    return _adaptive(TF.adaptive_avg_pool1d, x, output_size, 'NCL')
+
+
+def adaptive_avg_pool2d(x, output_size, data_format='NCHW', name=None):
+    return _adaptive(TF.adaptive_avg_pool2d, x, output_size, data_format)
+
+
+def adaptive_avg_pool3d(x, output_size, data_format='NCDHW', name=None):
+    return _adaptive(TF.adaptive_avg_pool3d, x, output_size, data_format)
+
+
+def adaptive_max_pool1d(x, output_size, return_mask=False, name=None):
+    return _adaptive(TF.adaptive_max_pool1d, x, output_size, 'NCL', return_mask)
+
+
+def adaptive_max_pool2d(x, output_size, return_mask=False, name=None):
+    return _adaptive(TF.adaptive_max_pool2d, x, output_size, 'NCHW', return_mask)
+
+
+def adaptive_max_pool3d(x, output_size, return_mask=False, name=None):
+    return _adaptive(TF.adaptive_max_pool3d, x, output_size, 'NCDHW', return_mask)
+
+
+def max_unpool1d(x, indices, kernel_size, stride=None, padding=0, data_format='NCL',
+                 output_size=None, name=None):
+    return _w(TF.max_unpool1d(_t(x), _t(indices), kernel_size, stride, padding, output_size))
+
+
+def max_unpool2d(x, indices, kernel_size, stride=None, padding=0, data_format='NCHW',
+                 output_size=None, name=None):
+    return _w(TF.max_unpool2d(_t(x), _t(indices), kernel_size, stride, padding, output_size))
+
+
+def max_unpool3d(x, indices, kernel_size, stride=None, padding=0, data_format='NCDHW',
+                 output_size=None, name=None):
+    return _w(TF.max_unpool3d(_t(x), _t(indices), kernel_size, stride, padding, output_size))
+
+
+# =============================================================================
+# norms
+# =============================================================================
+def layer_norm(x, normalized_shape, weight=None, bias=None, epsilon=1e-05, name=None):
+    t = _t(x)
+    if isinstance(normalized_shape, int):
+        normalized_shape = [normalized_shape]
+    w, b = _opt(weight), _opt(bias)
+    n = int(np.prod(normalized_shape))
+    if w is not None and w.dim() > 1:
+        w = w.reshape(-1)
+    if b is not None and b.dim() > 1:
+        b = b.reshape(-1)
+    if t.dtype in (torch.float32, torch.float16, torch.bfloat16) and (w is None or w.numel() == n):
+        shp = t.shape
+        out = K.layer_norm(t.reshape(*shp[:t.dim() - len(normalized_shape)], n), w, b, epsilon)
+        return _w(out.reshape(shp))
+    return _w(TF.layer_norm(t, list(normalized_shape), w, b, epsilon))
+
+
+def rms_norm(x, weight=None, epsilon=1e-6, name=None):
+    return _w(K.rms_norm(_t(x), _opt(weight), epsilon))
+
+
+def batch_norm(x, running_mean, running_var, weight, bias, training=False, momentum=0.9,
+               epsilon=1e-05, data_format='NCHW', use_global_stats=None, name=None):
+    t = _t(x)
+    cl = data_format in ('NHWC', 'NLC', 'NDHWC')
+    if cl:
+        t = t.movedim(-1, 1)
+    if use_global_stats:
+        training = False
+    rm, rv = _t(running_mean), _t(running_var)
+    out = TF.batch_norm(t, rm, rv, _opt(weight), _opt(bias), training, 1 - momentum, epsilon)
+    if cl:
+        out = out.movedim(1, -1)
+    return _w(out)
+
+
+def instance_norm(x, running_mean=None, running_var=None, weight=None, bias=None,
+                  use_input_stats=True, momentum=0.9, eps=1e-05, data_format='NCHW', name=None):
+    return _w(TF.instance_norm(_t(x), _opt(running_mean), _opt(running_var), _opt(weight), _opt(bias),
+                               use_input_stats, 1 - momentum, eps))
+
+
+def group_norm(x, num_groups, epsilon=1e-05, weight=None, bias=None, data_format='NCHW', name=None):
+    t = _t(x)
+    cl = data_format in ('NHWC', 'NLC', 'NDHWC')
+    if cl:
+        t = t.movedim(-1, 1)
+    out = TF.group_norm(t, num_groups, _opt(weight), _opt(bias), epsilon)
+    return _w(out.movedim(1, -1) if cl else out)
+
+
+def local_response_norm(x, size, alpha=1e-4, beta=0.75, k=1.0, data_format='NCHW', name=None):
+    return _w(TF.local_response_norm(_t(x), size, alpha * size, beta, k))
+
+
+# =============================================================================
+# losses
+# =============================================================================
+def _reduce(loss, reduction):
+    if reduction == 'mean':
+        return loss.mean()
+    if reduction == 'sum':
+        return loss.sum()
+    return loss
+
+
+def cross_entropy(input, label, weight=None, ignore_index=-100, reduction='mean', soft_label=False,
+                  axis=-1, use_softmax=True, label_smoothing=0.0, name=None):
+    """Paddle cross_entropy. Hard labels on the HIP device use the fused
+    one-pass softmax+CE kernel (the [N, V] probabilities are never stored)."""
+    x, lab = _t(input), _t(label)
+    nd = x.dim()
+    axis = axis % nd
+    if not use_softmax:
+        logp = torch.log(x.clamp_min(1e-30))
+        if soft_label:
+            loss = -(lab * logp).sum(axis)
+        else:
+            l = lab.squeeze(axis) if lab.dim() == nd else lab
+            loss = TF.nll_loss(logp.movedim(axis, 1) if nd > 2 else logp, l.long(),
+                               None if weight is None else _t(weight), reduction='none',
+                               ignore_index=ignore_index)
+        return _w(_reduce(loss, reduction))
+    if soft_label or (lab.dtype.is_floating_point and lab.shape == x.shape):
+        logp = torch.log_softmax(x.float(), axis)
+        loss = -(lab.float() * logp).sum(axis)
+        if weight is not None:
+            loss = loss * (lab.float() * _t(weight)).sum(axis)
+        return _w(_reduce(loss, reduction).to(x.dtype if x.dtype != torch.bfloat16 else torch.float32))
+    l = lab.squeeze(axis) if (lab.dim() == nd and lab.shape[axis] == 1) else lab
+    l = l.long()
+    if (axis == nd - 1 and weight is None and label_smoothing == 0.0 and
+            x.dtype in (torch.float32, torch.float16, torch.bfloat16)):
+        loss = K.softmax_cross_entropy(x, l, ignore_index)
+        if reduction == 'mean':
+            valid = (l != ignore_index).sum().clamp_min(1)
+            return _w(loss.sum() / valid)
+        return _w(_reduce(loss, reduction))
+    xm = x.movedim(axis, 1) if nd > 2 else x
+    loss = TF.cross_entropy(xm.float(), l, None if weight is None else _t(weight).float(),
+                            ignore_index=ignore_index, reduction=reduction,
+                            label_smoothing=label_smoothing)
+    return _w(loss)
+
+
+def softmax_with_cross_entropy(logits, label, soft_label=False, ignore_index=-100,
+                               numeric_stable_mode=True, return_softmax=False, axis=-1):
+    x, lab = _t(logits), _t(label)
+    nd = x.dim()
+    axis = axis % nd
+    if soft_label:
+        loss = -(lab * torch.log_softmax(x, axis)).sum(axis, keepdim=True)
+    else:
+        l = lab.squeeze(axis) if lab.dim() == nd else lab
+        if axis == nd - 1 and x.dtype in (torch.float32, torch.float16, torch.bfloat16):
+            loss = K.softmax_cross_entropy(x, l.long(), ignore_index).unsqueeze(axis)
+        else:
+            loss = TF.cross_entropy(x.movedim(axis, 1), l.long(), ignore_index=ignore_index,
+                                    reduction='none').unsqueeze(axis)
+    if return_softmax:
+        return _w(loss), _w(torch.softmax(x, axis))
+    return _w(loss)
+
+
+def nll_loss(input, label, weight=None, ignore_index=-100, reduction='mean', name=None):
+    return _w(TF.nll_loss(_t(input), _t(label).long(), _opt(weight), ignore_index=ignore_index,
+                          reduction=reduction))
+
+
+def mse_loss(input, label, reduction='mean', name=None):
+    return _w(TF.mse_loss(_t(input), _t(label), reduction=reduction))
+
+
+def square_error_cost(input, label):
+    return _w((_t(input) - _t(label)) ** 2)
+
+
+def l1_loss(input, label, reduction='mean', name=None):
+    return _w(TF.l1_loss(_t(input), _t(label), reduction=reduction))
+
+
+def smooth_l1_loss(input, label, reduction='mean', delta=1.0, name=None):
+    return _w(TF.huber_loss(_t(input), _t(label), reduction=reduction, delta=delta))
+
+
+def binary_cross_entropy(input, label, weight=None, reduction='mean', name=None):
+    return _w(TF.binary_cross_entropy(_t(input), _t(label), _opt(weight), reduction=reduction))
+
+
+def binary_cross_entropy_with_logits(logit, label, weight=None, reduction='mean', pos_weight=None,
+                                     name=None):
+    return _w(TF.binary_cross_entropy_with_logits(_t(logit), _t(label), _opt(weight),
+                                                  reduction=reduction, pos_weight=_opt(pos_weight)))
+
+
+def kl_div(input, label, reduction='mean', name=None):
+    t, l = _t(input), _t(label)
+    loss = l * (torch.log(l.clamp_min(1e-30)) - t)
+    loss = torch.where(l > 0, loss, torch.zeros_like(loss))
+    if reduction == 'batchmean':
+        return _w(loss.sum() / t.shape[0])
+    return _w(_reduce(loss, reduction))
+
+
+def margin_ranking_loss(input, other, label, margin=0.0, reduction='mean', name=None):
+    return _w(TF.margin_ranking_loss(_t(input), _t(other), _t(label), margin, reduction=reduction))
+
+
+def hinge_embedding_loss(input, label, margin=1.0, reduction='mean', name=None):
+    return _w(TF.hinge_embedding_loss(_t(input), _t(label), margin, reduction=reduction))
+
+
+def cosine_embedding_loss(input1, input2, label, margin=0, reduction='mean', name=None):
+    return _w(TF.cosine_embedding_loss(_t(input1), _t(input2), _t(label), margin, reduction=reduction))
+
+
+def soft_margin_loss(input, label, reduction='mean', name=None):
+    return _w(TF.soft_margin_loss(_t(input), _t(label).to(_t(input).dtype), reduction=reduction))
+
+
+def multi_label_soft_margin_loss(input, label, weight=None, reduction='mean', name=None):
+    return _w(TF.multilabel_soft_margin_loss(_t(input), _t(label), _opt(weight), reduction=reduction))
+
+
+def multi_margin_loss(input, label, p=1, margin=1.0, weight=None, reduction='mean', name=None):
+    return _w(TF.multi_margin_loss(_t(input), _t(label).long(), p, margin, _opt(weight),
+                                   reduction=reduction))
+
+
+def triplet_margin_loss(input, positive, negative, margin=1.0, p=2, epsilon=1e-6, swap=False,
+                        reduction='mean', name=None):
+    return _w(TF.triplet_margin_loss(_t(input), _t(positive), _t(negative), margin, p, epsilon, swap,
+                                     reduction=reduction))
+
+
+def triplet_margin_with_distance_loss(input, positive, negative, distance_function=None, margin=1.0,
+                                      swap=False, reduction='mean', name=None):
+    df = None
+    if distance_function is not None:
+        df = lambda a, b: _t(distance_function(Tensor(a), Tensor(b)))
+    return _w(TF.triplet_margin_with_distance_loss(_t(input), _t(positive), _t(negative),
+                                                   distance_function=df, margin=margin, swap=swap,
+                                                   reduction=reduction))
+
+
+def log_loss(input, label, epsilon=1e-4, name=None):
+    t, l = _t(input), _t(label)
+    return _w(-l * torch.log(t + epsilon) - (1 - l) * torch.log(1 - t + epsilon))
+
+
+def sigmoid_focal_loss(logit, label, normalizer=None, alpha=0.25, gamma=2.0, reduction='sum',
+                       name=None):
+    x, l = _t(logit), _t(label)
+    p = torch.sigmoid(x)
+    ce = TF.binary_cross_entropy_with_logits(x, l, reduction='none')
+    pt = p * l + (1 - p) * (1 - l)
+    loss = ce * ((1 - pt) ** gamma)
+    if alpha >= 0:
+        loss = (alpha * l + (1 - alpha) * (1 - l)) * loss
+    if normalizer is not None:
+        loss = loss / _t(normalizer)
+    return _w(_reduce(loss, reduction))
+
+
+def dice_loss(input, label, epsilon=0.00001, name=None):
+    x = _t(input)
+    l = TF.one_hot(_t(label).long().squeeze(-1), x.shape[-1]).to(x.dtype)
+    red = tuple(range(1, x.dim()))
+    inter = (x * l).sum(red)
+    return _w((1 - 2 * inter / (x.sum(red) + l.sum(red) + epsilon)).mean())
+
+
+def npair_loss(anchor, positive, labels, l2_reg=0.002):
+    a, p, l = _t(anchor), _t(positive), _t(labels).float().reshape(-1, 1)
+    same = (l == l.t()).float()
+    same = same / same.sum(1, keepdim=True)
+    logits = a @ p.t()
+    ce = (-same * torch.log_softmax(logits, 1)).sum(1).mean()
+    reg = l2_reg * ((a ** 2).sum(1).mean() + (p ** 2).sum(1).mean()) * 0.25
+    return _w(ce + reg)
+
+
+def ctc_loss(log_probs, labels, input_lengths, label_lengths, blank=0, reduction='mean',
+             norm_by_times=False):
+    loss = TF.ctc_loss(_t(log_probs), _t(labels), _t(input_lengths), _t(label_lengths), blank,
+                       reduction='none')
+    if reduction == 'mean':
+        return _w((loss / _t(label_lengths).clamp_min(1)).mean())
+    return _w(_reduce(loss, reduction))
+
+
+def rnnt_loss(*a, **k):
+    raise NotImplementedError("rnnt_loss is not available in the MI355X build yet")
+
+
+def hsigmoid_loss(*a, **k):
+    raise NotImplementedError("hsigmoid_loss is not available in the MI355X build yet")
+
+
+def margin_cross_entropy(logits, label, margin1=1.0, margin2=0.5, margin3=0.0, scale=64.0,
+                         group=None, return_softmax=False, reduction='mean'):
+    x, l = _t(logits), _t(label).long().reshape(-1)
+    theta = torch.acos(x.clamp(-1, 1))
+    tgt = torch.cos(margin1 * theta + margin2) - margin3
+    oh = TF.one_hot(l, x.shape[-1]).bool()
+    z = torch.where(oh, tgt, x) * scale
+    loss = TF.cross_entropy(z, l, reduction='none').unsqueeze(-1)
+    loss = _reduce(loss, reduction) if reduction else loss
+    if return_softmax:
+        return _w(loss), _w(torch.softmax(z, -1))
+    return _w(loss)
+
+
+# =============================================================================
+# attention
+# =============================================================================
+def scaled_dot_product_attention(query, key, value, attn_mask=None, dropout_p=0.0, is_causal=False,
+                                 training=True, name=None):
+    """Inputs [batch, seq, heads, head_dim] (paddle layout)."""
+    q, k, v = _t(query), _t(key), _t(value)
+    if attn_mask is None and (dropout_p == 0.0 or not training) and q.is_cuda:
+        return _w(K.flash_attention(q, k, v, causal=is_causal))
+    qt, kt, vt = (t.transpose(1, 2) for t in (q, k, v))
+    o = TF.scaled_dot_product_attention(qt, kt, vt, _opt(attn_mask),
+                                        dropout_p if training else 0.0, is_causal)
+    return _w(o.transpose(1, 2))
+
+
+def flash_attention(query, key, value, dropout=0.0, causal=False, return_softmax=False,
+                    fixed_seed_offset=None, rng_name="", training=True, name=None):
+    """paddle.nn.functional.flash_attention.flash_attention -> (out, softmax|None)."""
+    q, k, v = _t(query), _t(key), _t(value)
+    if dropout > 0 and training:
+        out = scaled_dot_product_attention(query, key, value, None, dropout, causal, training)
+    else:
+        out = _w(K.flash_attention(q, k, v, causal=causal))
+    return out, None
+
+
+def sparse_attention(*a, **k):
+    raise NotImplementedError("sparse_attention is not available in the MI355X build yet")
+
+
+def class_center_sample(label, num_classes, num_samples, group=None):
+    l = _t(label).reshape(-1)
+    pos = torch.unique(l)
+    if pos.numel() < num_samples:
+        others = torch.tensor([i for i in range(num_classes) if i not in set(pos.tolist())],
+                              device=l.device)
+        perm = others[torch.randperm(others.numel(), device=l.device)[:num_samples - pos.numel()]]
+        sampled = torch.cat([pos, perm]).sort().values
+    else:
+        sampled = pos
+    remap = torch.full((num_classes,), -1, dtype=torch.long, device=l.device)
+    remap[sampled] = torch.arange(sampled.numel(), device=l.device)
+    return _w(remap[l]), _w(sampled)
+
+
+def gather_tree(ids, parents):
+    i, p = _t(ids), _t(parents)
+    T = i.shape[0]
+    out = torch.empty_like(i)
+    out[-1] = i[-1]
+    par = p[-1]
+    for t in range(T - 2, -1, -1):
+        out[t] = torch.gather(i[t], -1, par)
+        par = torch.gather(p[t], -1, par)
+    return _w(out)

@@ -1,0 +1,133 @@
+// pybind11 entry points of the _pra_hip kernel library. Arguments are raw device
+// pointers (ints from torch.Tensor.data_ptr()) and the current HIP stream, so the
+// Python side pays one pybind11 call per launch and no tensor marshalling.
+#include <hip/hip_runtime.h>
+#include <pybind11/pybind11.h>
+#include <stdint.h>
+#include <stdexcept>
+#include <string>
+
+namespace py = pybind11;
+typedef uintptr_t P;
+
+extern "C" {
+void pra_layernorm_fwd(const void*, const void*, const void*, void*, float*, float*, int, int, float, int, int,
+                       hipStream_t);
+void pra_layernorm_bwd(const void*, const void*, const void*, const float*, const float*, void*, float*, float*, int,
+                       int, int, int, int, hipStream_t);
+void pra_rmsnorm_fwd(const void*, const void*, void*, float*, int, int, float, int, int, hipStream_t);
+void pra_rmsnorm_bwd(const void*, const void*, const void*, const float*, void*, float*, int, int, int, int, int,
+                     hipStream_t);
+void pra_colsum(const float*, void*, int, int, int, hipStream_t);
+void pra_softmax_fwd(const void*, void*, int, int, int, hipStream_t);
+void pra_softmax_bwd(const void*, const void*, void*, int, int, int, hipStream_t);
+void pra_softmax_ce_fwd(const void*, const int64_t*, float*, float*, int, int, int, int, hipStream_t);
+void pra_softmax_ce_bwd(const void*, const int64_t*, const float*, const float*, void*, int, int, int, int,
+                        hipStream_t);
+void pra_bias_gelu_fwd(const void*, const void*, void*, int64_t, int, int, int, hipStream_t);
+void pra_bias_gelu_bwd(const void*, const void*, const void*, void*, int64_t, int, int, int, hipStream_t);
+void pra_adamw_mt(const int64_t*, const float*, const int64_t*, int, float, float, float, float, float, float, float,
+                  hipStream_t);
+void pra_momentum_mt(const int64_t*, const float*, const int64_t*, int, float, float, int, float, hipStream_t);
+void pra_sumsq_accum(const void*, float*, int64_t, int, hipStream_t);
+void pra_flash_bwd_pre(const void*, const void*, float*, int, int, int, int, int, hipStream_t);
+int pra_flash_fwd(const void*, const void*, const void*, void*, float*, int, int, int, int, int, const int64_t*, float,
+                  int, int, hipStream_t);
+int pra_flash_bwd(const void*, const void*, const void*, const void*, const float*, const float*, void*, void*, void*,
+                  int, int, int, int, int, const int64_t*, float, int, int, hipStream_t);
+}
+
+#define V(x) reinterpret_cast<void*>(x)
+#define CV(x) reinterpret_cast<const void*>(x)
+#define F(x) reinterpret_cast<float*>(x)
+#define CF(x) reinterpret_cast<const float*>(x)
+#define I64(x) reinterpret_cast<const int64_t*>(x)
+#define S(x) reinterpret_cast<hipStream_t>(x)
+
+static void check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+PYBIND11_MODULE(_pra_hip, m) {
+  m.doc() = "paddle_ray_amd gfx950 HIP kernels";
+  m.def("layernorm_fwd", [](P x, P w, P b, P y, P mean, P rstd, int rows, int cols, float eps, int dtx, int dtw, P s) {
+    pra_layernorm_fwd(CV(x), CV(w), CV(b), V(y), F(mean), F(rstd), rows, cols, eps, dtx, dtw, S(s));
+    check_launch("layernorm_fwd");
+  });
+  m.def("layernorm_bwd", [](P dy, P x, P w, P mean, P rstd, P dx, P pw, P pb, int rows, int cols, int nblk, int dtx,
+                            int dtw, P s) {
+    pra_layernorm_bwd(CV(dy), CV(x), CV(w), CF(mean), CF(rstd), V(dx), F(pw), F(pb), rows, cols, nblk, dtx, dtw, S(s));
+    check_launch("layernorm_bwd");
+  });
+  m.def("rmsnorm_fwd", [](P x, P w, P y, P rstd, int rows, int cols, float eps, int dtx, int dtw, P s) {
+    pra_rmsnorm_fwd(CV(x), CV(w), V(y), F(rstd), rows, cols, eps, dtx, dtw, S(s));
+    check_launch("rmsnorm_fwd");
+  });
+  m.def("rmsnorm_bwd", [](P dy, P x, P w, P rstd, P dx, P pw, int rows, int cols, int nblk, int dtx, int dtw, P s) {
+    pra_rmsnorm_bwd(CV(dy), CV(x), CV(w), CF(rstd), V(dx), F(pw), rows, cols, nblk, dtx, dtw, S(s));
+    check_launch("rmsnorm_bwd");
+  });
+  m.def("colsum", [](P part, P out, int nblk, int cols, int dt, P s) {
+    pra_colsum(CF(part), V(out), nblk, cols, dt, S(s));
+    check_launch("colsum");
+  });
+  m.def("softmax_fwd", [](P x, P y, int rows, int cols, int dt, P s) {
+    pra_softmax_fwd(CV(x), V(y), rows, cols, dt, S(s));
+    check_launch("softmax_fwd");
+  });
+  m.def("softmax_bwd", [](P y, P dy, P dx, int rows, int cols, int dt, P s) {
+    pra_softmax_bwd(CV(y), CV(dy), V(dx), rows, cols, dt, S(s));
+    check_launch("softmax_bwd");
+  });
+  m.def("softmax_ce_fwd", [](P logits, P labels, P loss, P lse, int rows, int V_, int ign, int dt, P s) {
+    pra_softmax_ce_fwd(CV(logits), I64(labels), F(loss), F(lse), rows, V_, ign, dt, S(s));
+    check_launch("softmax_ce_fwd");
+  });
+  m.def("softmax_ce_bwd", [](P logits, P labels, P lse, P dloss, P dl, int rows, int V_, int ign, int dt, P s) {
+    pra_softmax_ce_bwd(CV(logits), I64(labels), CF(lse), CF(dloss), V(dl), rows, V_, ign, dt, S(s));
+    check_launch("softmax_ce_bwd");
+  });
+  m.def("bias_gelu_fwd", [](P x, P b, P y, int64_t rows, int cols, int dt, int approx, P s) {
+    pra_bias_gelu_fwd(CV(x), CV(b), V(y), rows, cols, dt, approx, S(s));
+    check_launch("bias_gelu_fwd");
+  });
+  m.def("bias_gelu_bwd", [](P dy, P x, P b, P dx, int64_t rows, int cols, int dt, int approx, P s) {
+    pra_bias_gelu_bwd(CV(dy), CV(x), CV(b), V(dx), rows, cols, dt, approx, S(s));
+    check_launch("bias_gelu_bwd");
+  });
+  m.def("adamw_mt", [](P tab, P ftab, P chunks, int nch, float lr, float b1, float b2, float eps, float bc1, float bc2,
+                       float gs, P s) {
+    pra_adamw_mt(I64(tab), CF(ftab), I64(chunks), nch, lr, b1, b2, eps, bc1, bc2, gs, S(s));
+    check_launch("adamw_mt");
+  });
+  m.def("momentum_mt", [](P tab, P ftab, P chunks, int nch, float lr, float mu, int nesterov, float gs, P s) {
+    pra_momentum_mt(I64(tab), CF(ftab), I64(chunks), nch, lr, mu, nesterov, gs, S(s));
+    check_launch("momentum_mt");
+  });
+  m.def("sumsq_accum", [](P x, P out, int64_t n, int dt, P s) {
+    pra_sumsq_accum(CV(x), F(out), n, dt, S(s));
+    check_launch("sumsq_accum");
+  });
+  m.def("flash_bwd_pre", [](P o, P dO, P delta, int B, int H, int Sq, int D, int dt, P s) {
+    pra_flash_bwd_pre(CV(o), CV(dO), F(delta), B, H, Sq, D, dt, S(s));
+    check_launch("flash_bwd_pre");
+  });
+  m.def("flash_fwd", [](P q, P k, P v, P o, P lse, int B, int H, int Sq, int Sk, int D, int64_t qsb, int64_t qss,
+                        int64_t qsh, int64_t ksb, int64_t kss, int64_t ksh, int64_t vsb, int64_t vss, int64_t vsh,
+                        float scale, int causal, int dt, P s) {
+    int64_t st[9] = {qsb, qss, qsh, ksb, kss, ksh, vsb, vss, vsh};
+    if (pra_flash_fwd(CV(q), CV(k), CV(v), V(o), F(lse), B, H, Sq, Sk, D, st, scale, causal, dt, S(s)) != 0)
+      throw std::invalid_argument("flash_fwd: unsupported head_dim/dtype");
+    check_launch("flash_fwd");
+  });
+  m.def("flash_bwd", [](P q, P k, P v, P dO, P lse, P delta, P dq, P dk, P dv, int B, int H, int Sq, int Sk, int D,
+                        int64_t qsb, int64_t qss, int64_t qsh, int64_t ksb, int64_t kss, int64_t ksh, int64_t vsb,
+                        int64_t vss, int64_t vsh, float scale, int causal, int dt, P s) {
+    int64_t st[9] = {qsb, qss, qsh, ksb, kss, ksh, vsb, vss, vsh};
+    if (pra_flash_bwd(CV(q), CV(k), CV(v), CV(dO), CF(lse), CF(delta), V(dq), V(dk), V(dv), B, H, Sq, Sk, D, st, scale,
+                      causal, dt, S(s)) != 0)
+      throw std::invalid_argument("flash_bwd: unsupported head_dim/dtype");
+    check_launch("flash_bwd");
+  });
+}

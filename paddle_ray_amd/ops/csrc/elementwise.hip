@@ -1,0 +1,233 @@
+// Elementwise / optimizer kernels for gfx950:
+//   bias+GELU fwd/bwd (tanh or erf form), multi-tensor AdamW (one launch for a
+//   whole parameter list, fp32 master weights + low-precision param write-back),
+//   multi-tensor Momentum, sum-of-squares (global-norm clipping), attention
+//   backward preprocess delta = rowsum(dO * O).
+#include "common.h"
+
+namespace pra {
+
+__device__ __forceinline__ float gelu_f(float x, int approx) {
+  if (approx) {
+    const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+    float t = tanhf(k0 * (x + k1 * x * x * x));
+    return 0.5f * x * (1.f + t);
+  }
+  return 0.5f * x * (1.f + erff(x * 0.7071067811865476f));
+}
+__device__ __forceinline__ float gelu_df(float x, int approx) {
+  if (approx) {
+    const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+    float t = tanhf(k0 * (x + k1 * x * x * x));
+    return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k0 * (1.f + 3.f * k1 * x * x);
+  }
+  return 0.5f * (1.f + erff(x * 0.7071067811865476f)) + x * 0.3989422804014327f * __expf(-0.5f * x * x);
+}
+
+template <typename T>
+__global__ void bias_gelu_fwd_k(const T* __restrict__ x, const T* __restrict__ b, T* __restrict__ y, size_t n,
+                                int cols, int approx) {
+  const size_t nv = n / 8;
+  for (size_t v = blockIdx.x * (size_t)blockDim.x + threadIdx.x; v < nv; v += (size_t)gridDim.x * blockDim.x) {
+    float a[8], bb[8];
+    load8<T>(x + v * 8, a);
+    if (b) load8<T>(b + (v * 8) % cols, bb);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a[i] = gelu_f(a[i] + (b ? bb[i] : 0.f), approx);
+    store8<T>(y + v * 8, a);
+  }
+}
+
+template <typename T>
+__global__ void bias_gelu_bwd_k(const T* __restrict__ dy, const T* __restrict__ x, const T* __restrict__ b,
+                                T* __restrict__ dx, size_t n, int cols, int approx) {
+  const size_t nv = n / 8;
+  for (size_t v = blockIdx.x * (size_t)blockDim.x + threadIdx.x; v < nv; v += (size_t)gridDim.x * blockDim.x) {
+    float a[8], g[8], bb[8];
+    load8<T>(x + v * 8, a);
+    load8<T>(dy + v * 8, g);
+    if (b) load8<T>(b + (v * 8) % cols, bb);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a[i] = g[i] * gelu_df(a[i] + (b ? bb[i] : 0.f), approx);
+    store8<T>(dx + v * 8, a);
+  }
+}
+
+template <typename T>
+__global__ void bias_gelu_fwd_scalar(const T* __restrict__ x, const T* __restrict__ b, T* __restrict__ y, size_t n,
+                                     int cols, int approx) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    y[i] = Cvt<T>::from(gelu_f(Cvt<T>::to(x[i]) + (b ? Cvt<T>::to(b[i % cols]) : 0.f), approx));
+}
+template <typename T>
+__global__ void bias_gelu_bwd_scalar(const T* __restrict__ dy, const T* __restrict__ x, const T* __restrict__ b,
+                                     T* __restrict__ dx, size_t n, int cols, int approx) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    dx[i] = Cvt<T>::from(Cvt<T>::to(dy[i]) *
+                         gelu_df(Cvt<T>::to(x[i]) + (b ? Cvt<T>::to(b[i % cols]) : 0.f), approx));
+}
+
+// ---------------------------------------------------------------------------
+// multi-tensor AdamW
+// tab[t] = {master_or_param, grad, m, v, lowp_param (0 if none), n, grad_dtype, param_dtype}
+// ftab[t] = {weight_decay, lr_mul, -, -};  chunks[c] = {tensor, start}
+// ---------------------------------------------------------------------------
+constexpr int kChunk = 65536;
+
+__device__ __forceinline__ float ld_any(const void* p, size_t i, int dt) {
+  if (dt == kF32) return ((const float*)p)[i];
+  if (dt == kBF16) return bf2f(((const uint16_t*)p)[i]);
+  return (float)((const f16*)p)[i];
+}
+__device__ __forceinline__ void st_any(void* p, size_t i, int dt, float v) {
+  if (dt == kF32) ((float*)p)[i] = v;
+  else if (dt == kBF16) ((uint16_t*)p)[i] = f2bf(v);
+  else ((f16*)p)[i] = (f16)v;
+}
+
+__global__ void __launch_bounds__(256) adamw_mt_k(const int64_t* __restrict__ tab, const float* __restrict__ ftab,
+                                                  const int64_t* __restrict__ chunks, float lr, float b1, float b2,
+                                                  float eps, float bc1, float bc2, float gscale) {
+  const int64_t t = chunks[2 * blockIdx.x], start = chunks[2 * blockIdx.x + 1];
+  const int64_t* d = tab + 8 * t;
+  void* master = (void*)d[0];
+  const void* grad = (const void*)d[1];
+  float* m = (float*)d[2];
+  float* v = (float*)d[3];
+  void* lowp = (void*)d[4];
+  const int64_t n = d[5];
+  const int gdt = (int)d[6], pdt = (int)d[7];
+  const int mdt = lowp ? kF32 : pdt;
+  const float wd = ftab[4 * t], lrt = lr * ftab[4 * t + 1];
+  const float decay = 1.f - lrt * wd, step = lrt / bc1, rbc2 = 1.f / bc2;
+  int64_t end = start + kChunk;
+  if (end > n) end = n;
+  for (int64_t i = start + threadIdx.x; i < end; i += blockDim.x) {
+    float g = ld_any(grad, i, gdt) * gscale;
+    float mi = b1 * m[i] + (1.f - b1) * g;
+    float vi = b2 * v[i] + (1.f - b2) * g * g;
+    m[i] = mi;
+    v[i] = vi;
+    float p = ld_any(master, i, mdt) * decay - step * mi / (sqrtf(vi * rbc2) + eps);
+    st_any(master, i, mdt, p);
+    if (lowp) st_any(lowp, i, pdt, p);
+  }
+}
+
+// tab[t] = {master_or_param, grad, velocity, 0, lowp, n, gdt, pdt}; ftab = {wd, lr_mul}
+__global__ void __launch_bounds__(256) momentum_mt_k(const int64_t* __restrict__ tab, const float* __restrict__ ftab,
+                                                     const int64_t* __restrict__ chunks, float lr, float mu,
+                                                     int nesterov, float gscale) {
+  const int64_t t = chunks[2 * blockIdx.x], start = chunks[2 * blockIdx.x + 1];
+  const int64_t* d = tab + 8 * t;
+  void* master = (void*)d[0];
+  const void* grad = (const void*)d[1];
+  float* vel = (float*)d[2];
+  void* lowp = (void*)d[4];
+  const int64_t n = d[5];
+  const int gdt = (int)d[6], pdt = (int)d[7];
+  const int mdt = lowp ? kF32 : pdt;
+  const float wd = ftab[4 * t], lrt = lr * ftab[4 * t + 1];
+  int64_t end = start + kChunk;
+  if (end > n) end = n;
+  for (int64_t i = start + threadIdx.x; i < end; i += blockDim.x) {
+    float p = ld_any(master, i, mdt);
+    float g = ld_any(grad, i, gdt) * gscale + wd * p;
+    float vi = mu * vel[i] + g;
+    vel[i] = vi;
+    p -= lrt * (nesterov ? g + mu * vi : vi);
+    st_any(master, i, mdt, p);
+    if (lowp) st_any(lowp, i, pdt, p);
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) sumsq_k(const T* __restrict__ x, float* __restrict__ out, size_t n) {
+  __shared__ float red[16];
+  float s = 0.f;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    float v = Cvt<T>::to(x[i]);
+    s += v * v;
+  }
+  s = block_sum(s, red);
+  if (threadIdx.x == 0) atomicAdd(out, s);
+}
+
+// delta[b,h,s] = sum_d dO[b,s,h,d] * O[b,s,h,d]   (O, dO contiguous [B,S,H,D]); one wave per row.
+template <typename T>
+__global__ void __launch_bounds__(256) attn_delta_k(const T* __restrict__ o, const T* __restrict__ dO,
+                                                    float* __restrict__ delta, int B, int H, int S, int D) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= (int64_t)B * S * H) return;
+  const T* orow = o + r * D;
+  const T* drow = dO + r * D;
+  float s = 0.f;
+  for (int i = lane; i < D; i += 64) s += Cvt<T>::to(orow[i]) * Cvt<T>::to(drow[i]);
+  s = wave_sum(s);
+  if (lane == 0) {
+    const int64_t h = r % H, bs = r / H, sq = bs % S, b = bs / S;
+    delta[(b * H + h) * S + sq] = s;
+  }
+}
+
+static int grid_for(size_t nv) {
+  size_t g = (nv + 255) / 256;
+  if (g > 4096) g = 4096;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+}  // namespace pra
+
+using namespace pra;
+
+extern "C" {
+void pra_bias_gelu_fwd(const void* x, const void* b, void* y, int64_t rows, int cols, int dt, int approx,
+                       hipStream_t s) {
+  size_t n = (size_t)rows * cols;
+  if (!n) return;
+  if (cols % 8 == 0) {
+    PRA_DISPATCH_FLOAT(dt, T, hipLaunchKernelGGL((bias_gelu_fwd_k<T>), dim3(grid_for(n / 8)), dim3(256), 0, s,
+                                                 (const T*)x, (const T*)b, (T*)y, n, cols, approx));
+  } else {
+    PRA_DISPATCH_FLOAT(dt, T, hipLaunchKernelGGL((bias_gelu_fwd_scalar<T>), dim3(grid_for(n)), dim3(256), 0, s,
+                                                 (const T*)x, (const T*)b, (T*)y, n, cols, approx));
+  }
+}
+void pra_bias_gelu_bwd(const void* dy, const void* x, const void* b, void* dx, int64_t rows, int cols, int dt,
+                       int approx, hipStream_t s) {
+  size_t n = (size_t)rows * cols;
+  if (!n) return;
+  if (cols % 8 == 0) {
+    PRA_DISPATCH_FLOAT(dt, T, hipLaunchKernelGGL((bias_gelu_bwd_k<T>), dim3(grid_for(n / 8)), dim3(256), 0, s,
+                                                 (const T*)dy, (const T*)x, (const T*)b, (T*)dx, n, cols, approx));
+  } else {
+    PRA_DISPATCH_FLOAT(dt, T, hipLaunchKernelGGL((bias_gelu_bwd_scalar<T>), dim3(grid_for(n)), dim3(256), 0, s,
+                                                 (const T*)dy, (const T*)x, (const T*)b, (T*)dx, n, cols, approx));
+  }
+}
+void pra_adamw_mt(const int64_t* tab, const float* ftab, const int64_t* chunks, int nchunks, float lr, float b1,
+                  float b2, float eps, float bc1, float bc2, float gscale, hipStream_t s) {
+  if (!nchunks) return;
+  hipLaunchKernelGGL(adamw_mt_k, dim3(nchunks), dim3(256), 0, s, tab, ftab, chunks, lr, b1, b2, eps, bc1, bc2,
+                     gscale);
+}
+void pra_momentum_mt(const int64_t* tab, const float* ftab, const int64_t* chunks, int nchunks, float lr, float mu,
+                     int nesterov, float gscale, hipStream_t s) {
+  if (!nchunks) return;
+  hipLaunchKernelGGL(momentum_mt_k, dim3(nchunks), dim3(256), 0, s, tab, ftab, chunks, lr, mu, nesterov, gscale);
+}
+void pra_sumsq_accum(const void* x, float* out, int64_t n, int dt, hipStream_t s) {
+  if (!n) return;
+  PRA_DISPATCH_FLOAT(dt, T, hipLaunchKernelGGL((sumsq_k<T>), dim3(grid_for(n) > 1024 ? 1024 : grid_for(n)),
+                                               dim3(256), 0, s, (const T*)x, out, (size_t)n));
+}
+void pra_flash_bwd_pre(const void* o, const void* dO, float* delta, int B, int H, int S, int D, int dt,
+                       hipStream_t s) {
+  int64_t rows = (int64_t)B * S * H;
+  if (!rows) return;
+  PRA_DISPATCH_FLOAT(dt, T, hipLaunchKernelGGL((attn_delta_k<T>), dim3((rows + 3) / 4), dim3(256), 0, s,
+                                               (const T*)o, (const T*)dO, delta, B, H, S, D));
+}
+}

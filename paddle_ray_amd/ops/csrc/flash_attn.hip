@@ -1,0 +1,632 @@
+// Flash attention forward + backward for gfx950 (CDNA4) on v_mfma_f32_32x32x16_{bf16,f16}.
+//
+// Layout: q,k,v,o are [B, S, H, D] with D contiguous (arbitrary b/s/h strides so
+// the GPT fused-QKV projection output is consumed in place); lse/delta are
+// [B, H, S] fp32. D in {64, 128}.
+//
+// "Swapped" formulation (CDNA4 guide §3 'accumulator as next operand', T12):
+//   S^T = K Q^T  -> the 32x32 accumulator holds one QUERY per lane (column),
+//                   keys in registers: softmax row stats are lane-local
+//                   (one __shfl_xor(.,32) for the row max/sum).
+//   O^T += V^T P^T -> P^T's accumulator registers ARE the B operand (k order
+//                   permuted: elem j of lane-half h <-> key 16s+8(j>>2)+4h+(j&3)),
+//                   V^T comes from a transposed LDS image read as 2x ds_read_b64.
+//                   The O^T accumulator is again one query per lane, so the
+//                   online-softmax rescale is lane-local too.
+// Backward = FA2 split into a dK/dV kernel (keys on lanes, sweep queries) and a
+// dQ kernel (queries on lanes, sweep keys): no float atomics (MI355X atomics
+// are ~1.3 TB/s chip-wide; dQ atomics would cost more than the whole backward).
+//
+// Workgroup = 4 waves (256 threads); each wave owns 32 queries (fwd, dQ) or 32
+// keys (dK/dV); K/V (resp. Q/dO) tiles of 64 rows staged through LDS with
+// register prefetch of the next tile (async-STAGE split, guide T14).
+#include "common.h"
+
+namespace pra {
+namespace fa {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+template <typename T> struct V8;
+template <> struct V8<bf16> { typedef __bf16 type __attribute__((ext_vector_type(8))); };
+template <> struct V8<f16> { typedef _Float16 type __attribute__((ext_vector_type(8))); };
+
+template <typename T>
+__device__ __forceinline__ f32x16 mfma(typename V8<T>::type a, typename V8<T>::type b, f32x16 c);
+template <>
+__device__ __forceinline__ f32x16 mfma<bf16>(V8<bf16>::type a, V8<bf16>::type b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+template <>
+__device__ __forceinline__ f32x16 mfma<f16>(V8<f16>::type a, V8<f16>::type b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
+
+template <typename T> __device__ __forceinline__ uint32_t pack2(float a, float b);
+template <> __device__ __forceinline__ uint32_t pack2<bf16>(float a, float b) {
+  return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+}
+template <> __device__ __forceinline__ uint32_t pack2<f16>(float a, float b) {
+  _Float16 x = (_Float16)a, y = (_Float16)b;
+  return (uint32_t)__builtin_bit_cast(uint16_t, x) | ((uint32_t)__builtin_bit_cast(uint16_t, y) << 16);
+}
+template <typename T> __device__ __forceinline__ float lo16(uint32_t w);
+template <typename T> __device__ __forceinline__ float hi16(uint32_t w);
+template <> __device__ __forceinline__ float lo16<bf16>(uint32_t w) { return __uint_as_float(w << 16); }
+template <> __device__ __forceinline__ float hi16<bf16>(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
+template <> __device__ __forceinline__ float lo16<f16>(uint32_t w) {
+  return (float)__builtin_bit_cast(_Float16, (uint16_t)(w & 0xffff));
+}
+template <> __device__ __forceinline__ float hi16<f16>(uint32_t w) {
+  return (float)__builtin_bit_cast(_Float16, (uint16_t)(w >> 16));
+}
+
+template <typename T>
+__device__ __forceinline__ typename V8<T>::type as_v8(u32x4 u) {
+  return __builtin_bit_cast(typename V8<T>::type, u);
+}
+// 8 accumulator registers (floats) -> one MFMA operand fragment
+template <typename T>
+__device__ __forceinline__ typename V8<T>::type pack_frag(const f32x16& acc, int base) {
+  u32x4 u;
+  u[0] = pack2<T>(acc[base + 0], acc[base + 1]);
+  u[1] = pack2<T>(acc[base + 2], acc[base + 3]);
+  u[2] = pack2<T>(acc[base + 4], acc[base + 5]);
+  u[3] = pack2<T>(acc[base + 6], acc[base + 7]);
+  return as_v8<T>(u);
+}
+
+constexpr int kTile = 64;        // rows per staged tile (keys in fwd/dQ, queries in dK/dV)
+constexpr int kTP = kTile + 4;   // transposed-image row length (136 B rows: 8-B aligned, spread banks)
+
+template <int D> struct Geo {
+  static constexpr int RP = D + 8;                 // row-major image row length (odd # of 16-B slots)
+  static constexpr int NPASS = D / 64;             // pair-load passes per thread
+  static constexpr int ROW_IMG = kTile * RP;       // elements
+  static constexpr int TR_IMG = D * kTP;           // elements
+};
+
+// Block-cooperative staged load of a 64-row x D tile, pair mapping:
+// thread t -> rows 2*(t%32), 2*(t%32)+1; 16-B column chunk (t/32) + 8*pass.
+template <typename T, int D>
+struct TileRegs {
+  uint4 r0[Geo<D>::NPASS], r1[Geo<D>::NPASS];
+
+  __device__ __forceinline__ void load(const T* base, int64_t row_stride, int row0, int nrows) {
+    const int t = threadIdx.x, kp = t & 31, dcb = t >> 5;
+    const int ra = row0 + 2 * kp, rb = ra + 1;
+#pragma unroll
+    for (int p = 0; p < Geo<D>::NPASS; ++p) {
+      const int dc = dcb + 8 * p;
+      r0[p] = ra < nrows ? *reinterpret_cast<const uint4*>(base + (int64_t)ra * row_stride + dc * 8)
+                         : make_uint4(0, 0, 0, 0);
+      r1[p] = rb < nrows ? *reinterpret_cast<const uint4*>(base + (int64_t)rb * row_stride + dc * 8)
+                         : make_uint4(0, 0, 0, 0);
+    }
+  }
+  // row-major image [64][D+8]
+  __device__ __forceinline__ void store_rows(T* img) const {
+    const int t = threadIdx.x, kp = t & 31, dcb = t >> 5;
+#pragma unroll
+    for (int p = 0; p < Geo<D>::NPASS; ++p) {
+      const int dc = dcb + 8 * p;
+      *reinterpret_cast<uint4*>(img + (2 * kp) * Geo<D>::RP + dc * 8) = r0[p];
+      *reinterpret_cast<uint4*>(img + (2 * kp + 1) * Geo<D>::RP + dc * 8) = r1[p];
+    }
+  }
+  // transposed image [D][64+4]: dword (row 2kp, row 2kp+1) at [d][2kp]
+  __device__ __forceinline__ void store_tr(T* img) const {
+    const int t = threadIdx.x, kp = t & 31, dcb = t >> 5;
+#pragma unroll
+    for (int p = 0; p < Geo<D>::NPASS; ++p) {
+      const int d0 = (dcb + 8 * p) * 8;
+      const uint32_t a[4] = {r0[p].x, r0[p].y, r0[p].z, r0[p].w};
+      const uint32_t b[4] = {r1[p].x, r1[p].y, r1[p].z, r1[p].w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        uint32_t lo = (a[i] & 0xffffu) | (b[i] << 16);
+        uint32_t hi = (a[i] >> 16) | (b[i] & 0xffff0000u);
+        *reinterpret_cast<uint32_t*>(img + (d0 + 2 * i) * kTP + 2 * kp) = lo;
+        *reinterpret_cast<uint32_t*>(img + (d0 + 2 * i + 1) * kTP + 2 * kp) = hi;
+      }
+    }
+  }
+};
+
+// A operand (row = lane&31) from a row-major image, k-step s over D (16 wide)
+template <typename T, int D>
+__device__ __forceinline__ typename V8<T>::type frag_rows(const T* img, int row, int s, int h) {
+  return *reinterpret_cast<const typename V8<T>::type*>(img + row * Geo<D>::RP + 16 * s + 8 * h);
+}
+// A operand (row = lane&31 of the transposed image) with the permuted k order of an
+// accumulator-derived B operand: elem j <-> k = 16s + 8(j>>2) + 4h + (j&3)
+template <typename T>
+__device__ __forceinline__ typename V8<T>::type frag_tr(const T* img, int row, int s, int h) {
+  const T* p = img + row * kTP + 16 * s + 4 * h;
+  u32x2 a = *reinterpret_cast<const u32x2*>(p);
+  u32x2 b = *reinterpret_cast<const u32x2*>(p + 8);
+  u32x4 u;
+  u[0] = a[0]; u[1] = a[1]; u[2] = b[0]; u[3] = b[1];
+  return as_v8<T>(u);
+}
+// operand fragment straight from global (row pointer + d offset), zero if invalid
+template <typename T>
+__device__ __forceinline__ typename V8<T>::type frag_global(const T* rowp, int d, bool valid) {
+  u32x4 u = {0, 0, 0, 0};
+  if (valid) {
+    uint4 x = *reinterpret_cast<const uint4*>(rowp + d);
+    u[0] = x.x; u[1] = x.y; u[2] = x.z; u[3] = x.w;
+  }
+  return as_v8<T>(u);
+}
+
+__device__ __forceinline__ int acc_row(int reg, int h) { return (reg & 3) + 8 * (reg >> 2) + 4 * h; }
+
+// ============================================================================
+// forward
+// ============================================================================
+template <typename T, int D, bool CAUSAL>
+__global__ void __launch_bounds__(256, 1)
+fwd_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restrict__ v, T* __restrict__ o,
+           float* __restrict__ lse, int H, int Sq, int Sk, int64_t qsb, int64_t qss, int64_t qsh, int64_t ksb,
+           int64_t kss, int64_t ksh, int64_t vsb, int64_t vss, int64_t vsh, float scale_log2) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  T* Ks = reinterpret_cast<T*>(smem);
+  T* Vt = Ks + Geo<D>::ROW_IMG;
+  constexpr int NS = D / 16, ND = D / 32;
+
+  const int nqb = gridDim.x;
+  const int qb = CAUSAL ? (nqb - 1 - blockIdx.x) : blockIdx.x;
+  const int bh = blockIdx.y, b = bh / H, hh = bh % H;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+  const int q0 = qb * 128;
+  const int myq = q0 + wave * 32 + r;
+  const int off = Sk - Sq;
+
+  const T* qb_ = q + b * qsb + hh * qsh;
+  const T* kb_ = k + b * ksb + hh * ksh;
+  const T* vb_ = v + b * vsb + hh * vsh;
+
+  typename V8<T>::type qf[NS];
+  {
+    const bool valid = myq < Sq;
+    const T* rowp = qb_ + (int64_t)(valid ? myq : 0) * qss;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) qf[s] = frag_global<T>(rowp, 16 * s + 8 * h, valid);
+  }
+
+  f32x16 acc_o[ND];
+#pragma unroll
+  for (int i = 0; i < ND; ++i) acc_o[i] = f32x16{};
+  float m_run = -INFINITY, l_run = 0.f;
+
+  int n_end = Sk;
+  if (CAUSAL) n_end = min(Sk, q0 + 128 + off);
+  const int ntiles = n_end > 0 ? (n_end + kTile - 1) / kTile : 0;
+
+  TileRegs<T, D> kr, vr;
+  if (ntiles > 0) {
+    kr.load(kb_, kss, 0, Sk);
+    vr.load(vb_, vss, 0, Sk);
+    kr.store_rows(Ks);
+    vr.store_tr(Vt);
+  }
+  __syncthreads();
+
+  for (int kt = 0; kt < ntiles; ++kt) {
+    const int k0 = kt * kTile;
+    if (kt + 1 < ntiles) {  // issue next tile's global loads; written after the compute
+      kr.load(kb_, kss, k0 + kTile, Sk);
+      vr.load(vb_, vss, k0 + kTile, Sk);
+    }
+    // S^T = K Q^T : two 32-key tiles
+    f32x16 s_acc[2];
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) {
+      s_acc[mt] = f32x16{};
+#pragma unroll
+      for (int s = 0; s < NS; ++s)
+        s_acc[mt] = mfma<T>(frag_rows<T, D>(Ks, 32 * mt + r, s, h), qf[s], s_acc[mt]);
+    }
+    // scale + mask + online softmax (lane-local per query)
+    float mx = -INFINITY;
+    const bool need_mask = (k0 + kTile > Sk) || (CAUSAL && (k0 + kTile - 1 > q0 + off));
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        float x = s_acc[mt][i] * scale_log2;
+        if (need_mask) {
+          const int key = k0 + 32 * mt + acc_row(i, h);
+          if (key >= Sk || (CAUSAL && key > myq + off)) x = -INFINITY;
+        }
+        s_acc[mt][i] = x;
+        mx = fmaxf(mx, x);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float m_new = fmaxf(m_run, mx);
+    const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
+    const float alpha = exp2f(m_run - m_use);
+    float ps = 0.f;
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        float p = exp2f(s_acc[mt][i] - m_use);
+        s_acc[mt][i] = p;
+        ps += p;
+      }
+    ps += __shfl_xor(ps, 32, 64);
+    l_run = l_run * alpha + ps;
+    m_run = m_new;
+#pragma unroll
+    for (int dt = 0; dt < ND; ++dt) acc_o[dt] *= alpha;
+    // O^T += V^T P^T
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const typename V8<T>::type pf = pack_frag<T>(s_acc[ks >> 1], 8 * (ks & 1));
+#pragma unroll
+      for (int dt = 0; dt < ND; ++dt) acc_o[dt] = mfma<T>(frag_tr<T>(Vt, 32 * dt + r, ks, h), pf, acc_o[dt]);
+    }
+    __syncthreads();
+    if (kt + 1 < ntiles) {
+      kr.store_rows(Ks);
+      vr.store_tr(Vt);
+    }
+    __syncthreads();
+  }
+
+  if (myq < Sq) {
+    const float inv = l_run > 0.f ? 1.f / l_run : 0.f;
+    T* orow = o + ((int64_t)b * Sq + myq) * ((int64_t)H * D) + (int64_t)hh * D;
+#pragma unroll
+    for (int dt = 0; dt < ND; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int d = 32 * dt + 8 * g + 4 * h;
+        uint2 w;
+        w.x = pack2<T>(acc_o[dt][4 * g + 0] * inv, acc_o[dt][4 * g + 1] * inv);
+        w.y = pack2<T>(acc_o[dt][4 * g + 2] * inv, acc_o[dt][4 * g + 3] * inv);
+        *reinterpret_cast<uint2*>(orow + d) = w;
+      }
+    if (h == 0) {
+      const float l2 = l_run > 0.f ? (m_run + log2f(l_run)) : INFINITY;
+      lse[(int64_t)bh * Sq + myq] = l2 * 0.6931471805599453f;
+    }
+  }
+}
+
+// ============================================================================
+// backward: dQ (queries on lanes, sweep key tiles)
+// ============================================================================
+template <typename T, int D, bool CAUSAL>
+__global__ void __launch_bounds__(256, 1)
+bwd_dq_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restrict__ v, const T* __restrict__ dO,
+              const float* __restrict__ lse, const float* __restrict__ delta, T* __restrict__ dq, int H, int Sq,
+              int Sk, int64_t qsb, int64_t qss, int64_t qsh, int64_t ksb, int64_t kss, int64_t ksh, int64_t vsb,
+              int64_t vss, int64_t vsh, float scale, float scale_log2) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  T* Ks = reinterpret_cast<T*>(smem);
+  T* Vs = Ks + Geo<D>::ROW_IMG;
+  T* Kt = Vs + Geo<D>::ROW_IMG;
+  constexpr int NS = D / 16, ND = D / 32;
+  const float LOG2E = 1.4426950408889634f;
+
+  const int nqb = gridDim.x;
+  const int qb = CAUSAL ? (nqb - 1 - blockIdx.x) : blockIdx.x;
+  const int bh = blockIdx.y, b = bh / H, hh = bh % H;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+  const int q0 = qb * 128;
+  const int myq = q0 + wave * 32 + r;
+  const int off = Sk - Sq;
+  const bool qvalid = myq < Sq;
+
+  const T* qb_ = q + b * qsb + hh * qsh;
+  const T* kb_ = k + b * ksb + hh * ksh;
+  const T* vb_ = v + b * vsb + hh * vsh;
+  const int64_t HD = (int64_t)H * D;
+  const T* dob_ = dO + (int64_t)b * Sq * HD + (int64_t)hh * D;
+
+  typename V8<T>::type qf[NS], df[NS];
+  {
+    const int qq = qvalid ? myq : 0;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      qf[s] = frag_global<T>(qb_ + (int64_t)qq * qss, 16 * s + 8 * h, qvalid);
+      df[s] = frag_global<T>(dob_ + (int64_t)qq * HD, 16 * s + 8 * h, qvalid);
+    }
+  }
+  const float lse2 = qvalid ? lse[(int64_t)bh * Sq + myq] * LOG2E : INFINITY;
+  const float dlt = qvalid ? delta[(int64_t)bh * Sq + myq] : 0.f;
+
+  f32x16 acc_q[ND];
+#pragma unroll
+  for (int i = 0; i < ND; ++i) acc_q[i] = f32x16{};
+
+  int n_end = Sk;
+  if (CAUSAL) n_end = min(Sk, q0 + 128 + off);
+  const int ntiles = n_end > 0 ? (n_end + kTile - 1) / kTile : 0;
+
+  TileRegs<T, D> kr, vr;
+  if (ntiles > 0) {
+    kr.load(kb_, kss, 0, Sk);
+    vr.load(vb_, vss, 0, Sk);
+    kr.store_rows(Ks);
+    kr.store_tr(Kt);
+    vr.store_rows(Vs);
+  }
+  __syncthreads();
+
+  for (int kt = 0; kt < ntiles; ++kt) {
+    const int k0 = kt * kTile;
+    if (kt + 1 < ntiles) {
+      kr.load(kb_, kss, k0 + kTile, Sk);
+      vr.load(vb_, vss, k0 + kTile, Sk);
+    }
+    f32x16 s_acc[2], dp_acc[2];
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) {
+      s_acc[mt] = f32x16{};
+      dp_acc[mt] = f32x16{};
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        s_acc[mt] = mfma<T>(frag_rows<T, D>(Ks, 32 * mt + r, s, h), qf[s], s_acc[mt]);
+        dp_acc[mt] = mfma<T>(frag_rows<T, D>(Vs, 32 * mt + r, s, h), df[s], dp_acc[mt]);
+      }
+    }
+    const bool need_mask = (k0 + kTile > Sk) || (CAUSAL && (k0 + kTile - 1 > q0 + off));
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        float p = exp2f(s_acc[mt][i] * scale_log2 - lse2);
+        if (need_mask) {
+          const int key = k0 + 32 * mt + acc_row(i, h);
+          if (key >= Sk || (CAUSAL && key > myq + off)) p = 0.f;
+        }
+        s_acc[mt][i] = p * (dp_acc[mt][i] - dlt);  // dS^T (unscaled)
+      }
+    // dQ^T += K^T dS^T
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const typename V8<T>::type sf = pack_frag<T>(s_acc[ks >> 1], 8 * (ks & 1));
+#pragma unroll
+      for (int dt = 0; dt < ND; ++dt) acc_q[dt] = mfma<T>(frag_tr<T>(Kt, 32 * dt + r, ks, h), sf, acc_q[dt]);
+    }
+    __syncthreads();
+    if (kt + 1 < ntiles) {
+      kr.store_rows(Ks);
+      kr.store_tr(Kt);
+      vr.store_rows(Vs);
+    }
+    __syncthreads();
+  }
+
+  if (qvalid) {
+    T* row = dq + ((int64_t)b * Sq + myq) * HD + (int64_t)hh * D;
+#pragma unroll
+    for (int dt = 0; dt < ND; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int d = 32 * dt + 8 * g + 4 * h;
+        uint2 w;
+        w.x = pack2<T>(acc_q[dt][4 * g + 0] * scale, acc_q[dt][4 * g + 1] * scale);
+        w.y = pack2<T>(acc_q[dt][4 * g + 2] * scale, acc_q[dt][4 * g + 3] * scale);
+        *reinterpret_cast<uint2*>(row + d) = w;
+      }
+  }
+}
+
+// ============================================================================
+// backward: dK, dV (keys on lanes, sweep query tiles)
+// S = Q K^T with the 32x32 tile [q rows in registers, key = lane]:
+//   A = Q (row-major LDS image), B = K^T (K fragments in registers)
+// dV^T += dO^T P,  dK^T += Q^T dS  (A from transposed images, B = accumulators)
+// ============================================================================
+template <typename T, int D, bool CAUSAL>
+__global__ void __launch_bounds__(256, 1)
+bwd_dkdv_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restrict__ v, const T* __restrict__ dO,
+                const float* __restrict__ lse, const float* __restrict__ delta, T* __restrict__ dk,
+                T* __restrict__ dv, int H, int Sq, int Sk, int64_t qsb, int64_t qss, int64_t qsh, int64_t ksb,
+                int64_t kss, int64_t ksh, int64_t vsb, int64_t vss, int64_t vsh, float scale, float scale_log2) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  T* Qs = reinterpret_cast<T*>(smem);
+  T* Qt = Qs + Geo<D>::ROW_IMG;
+  T* Ds = Qt + Geo<D>::TR_IMG;
+  T* Dt = Ds + Geo<D>::ROW_IMG;
+  float* Ls = reinterpret_cast<float*>(Dt + Geo<D>::TR_IMG);  // [64] lse*log2e
+  float* Dl = Ls + kTile;                                      // [64] delta
+  constexpr int NS = D / 16, ND = D / 32;
+  const float LOG2E = 1.4426950408889634f;
+
+  const int nkb = gridDim.x;
+  const int kb = CAUSAL ? blockIdx.x : blockIdx.x;  // causal: later key blocks have less work
+  (void)nkb;
+  const int bh = blockIdx.y, b = bh / H, hh = bh % H;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+  const int kblk0 = kb * 128;
+  const int mykey = kblk0 + wave * 32 + r;
+  const int off = Sk - Sq;
+  const bool kvalid = mykey < Sk;
+
+  const T* qb_ = q + b * qsb + hh * qsh;
+  const T* kb_ = k + b * ksb + hh * ksh;
+  const T* vb_ = v + b * vsb + hh * vsh;
+  const int64_t HD = (int64_t)H * D;
+  const T* dob_ = dO + (int64_t)b * Sq * HD + (int64_t)hh * D;
+
+  typename V8<T>::type kf[NS], vf[NS];
+  {
+    const int kk = kvalid ? mykey : 0;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      kf[s] = frag_global<T>(kb_ + (int64_t)kk * kss, 16 * s + 8 * h, kvalid);
+      vf[s] = frag_global<T>(vb_ + (int64_t)kk * vss, 16 * s + 8 * h, kvalid);
+    }
+  }
+  f32x16 acc_k[ND], acc_v[ND];
+#pragma unroll
+  for (int i = 0; i < ND; ++i) { acc_k[i] = f32x16{}; acc_v[i] = f32x16{}; }
+
+  int q_begin = 0;
+  if (CAUSAL) q_begin = max(0, kblk0 - off) / kTile * kTile;
+  const int ntiles = q_begin < Sq ? (Sq - q_begin + kTile - 1) / kTile : 0;
+
+  TileRegs<T, D> qr, dr;
+  float lreg = 0.f, dreg = 0.f;
+  auto load_tile = [&](int qs0) {
+    qr.load(qb_, qss, qs0, Sq);
+    dr.load(dob_, HD, qs0, Sq);
+    if (threadIdx.x < kTile) {
+      const int qq = qs0 + threadIdx.x;
+      lreg = qq < Sq ? lse[(int64_t)bh * Sq + qq] * LOG2E : INFINITY;
+      dreg = qq < Sq ? delta[(int64_t)bh * Sq + qq] : 0.f;
+    }
+  };
+  auto store_tile = [&]() {
+    qr.store_rows(Qs);
+    qr.store_tr(Qt);
+    dr.store_rows(Ds);
+    dr.store_tr(Dt);
+    if (threadIdx.x < kTile) { Ls[threadIdx.x] = lreg; Dl[threadIdx.x] = dreg; }
+  };
+  if (ntiles > 0) { load_tile(q_begin); store_tile(); }
+  __syncthreads();
+
+  for (int it = 0; it < ntiles; ++it) {
+    const int qs0 = q_begin + it * kTile;
+    if (it + 1 < ntiles) load_tile(qs0 + kTile);
+    const bool need_mask = (qs0 + kTile > Sq) || (CAUSAL && (kblk0 + 127 > qs0 + off));
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {  // two 32-query halves of the tile
+      f32x16 s_acc = f32x16{}, dp_acc = f32x16{};
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        s_acc = mfma<T>(frag_rows<T, D>(Qs, 32 * nt + r, s, h), kf[s], s_acc);
+        dp_acc = mfma<T>(frag_rows<T, D>(Ds, 32 * nt + r, s, h), vf[s], dp_acc);
+      }
+      // rows (queries) in registers: q = 32nt + acc_row(i,h)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int qr0 = 32 * nt + 8 * g + 4 * h;
+        const float4 l4 = *reinterpret_cast<const float4*>(Ls + qr0);
+        const float4 d4 = *reinterpret_cast<const float4*>(Dl + qr0);
+        const float la[4] = {l4.x, l4.y, l4.z, l4.w};
+        const float da[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const int i = 4 * g + c;
+          float p = exp2f(s_acc[i] * scale_log2 - la[c]);
+          if (need_mask) {
+            const int qq = qs0 + qr0 + c;
+            if (qq >= Sq || (CAUSAL && mykey > qq + off)) p = 0.f;
+          }
+          s_acc[i] = p;
+          dp_acc[i] = p * (dp_acc[i] - da[c]);
+        }
+      }
+      // dV^T += dO^T P ; dK^T += Q^T dS   (k = queries of this 32-half, 2 steps of 16)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const typename V8<T>::type pf = pack_frag<T>(s_acc, 8 * ks);
+        const typename V8<T>::type sf = pack_frag<T>(dp_acc, 8 * ks);
+#pragma unroll
+        for (int dt = 0; dt < ND; ++dt) {
+          acc_v[dt] = mfma<T>(frag_tr<T>(Dt, 32 * dt + r, 2 * nt + ks, h), pf, acc_v[dt]);
+          acc_k[dt] = mfma<T>(frag_tr<T>(Qt, 32 * dt + r, 2 * nt + ks, h), sf, acc_k[dt]);
+        }
+      }
+    }
+    __syncthreads();
+    if (it + 1 < ntiles) store_tile();
+    __syncthreads();
+  }
+
+  if (kvalid) {
+    T* krow = dk + ((int64_t)b * Sk + mykey) * HD + (int64_t)hh * D;
+    T* vrow = dv + ((int64_t)b * Sk + mykey) * HD + (int64_t)hh * D;
+#pragma unroll
+    for (int dt = 0; dt < ND; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int d = 32 * dt + 8 * g + 4 * h;
+        uint2 wk, wv;
+        wk.x = pack2<T>(acc_k[dt][4 * g + 0] * scale, acc_k[dt][4 * g + 1] * scale);
+        wk.y = pack2<T>(acc_k[dt][4 * g + 2] * scale, acc_k[dt][4 * g + 3] * scale);
+        wv.x = pack2<T>(acc_v[dt][4 * g + 0], acc_v[dt][4 * g + 1]);
+        wv.y = pack2<T>(acc_v[dt][4 * g + 2], acc_v[dt][4 * g + 3]);
+        *reinterpret_cast<uint2*>(krow + d) = wk;
+        *reinterpret_cast<uint2*>(vrow + d) = wv;
+      }
+  }
+}
+
+template <typename T, int D, bool C>
+static void launch_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B, int H, int Sq,
+                       int Sk, const int64_t* st, float scale, hipStream_t s) {
+  const size_t lds = (Geo<D>::ROW_IMG + Geo<D>::TR_IMG) * sizeof(T);
+  auto kern = fwd_kernel<T, D, C>;
+  hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  dim3 grid((Sq + 127) / 128, B * H);
+  hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, (const T*)q, (const T*)k, (const T*)v, (T*)o, lse, H, Sq, Sk,
+                     st[0], st[1], st[2], st[3], st[4], st[5], st[6], st[7], st[8], scale * 1.4426950408889634f);
+}
+
+template <typename T, int D, bool C>
+static void launch_bwd(const void* q, const void* k, const void* v, const void* dO, const float* lse,
+                       const float* delta, void* dq, void* dk, void* dv, int B, int H, int Sq, int Sk,
+                       const int64_t* st, float scale, hipStream_t s) {
+  const float sl2 = scale * 1.4426950408889634f;
+  {
+    const size_t lds = (2 * Geo<D>::ROW_IMG + Geo<D>::TR_IMG) * sizeof(T);
+    auto kern = bwd_dq_kernel<T, D, C>;
+    hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(kern, dim3((Sq + 127) / 128, B * H), dim3(256), lds, s, (const T*)q, (const T*)k,
+                       (const T*)v, (const T*)dO, lse, delta, (T*)dq, H, Sq, Sk, st[0], st[1], st[2], st[3], st[4],
+                       st[5], st[6], st[7], st[8], scale, sl2);
+  }
+  {
+    const size_t lds = (2 * Geo<D>::ROW_IMG + 2 * Geo<D>::TR_IMG) * sizeof(T) + 2 * kTile * sizeof(float);
+    auto kern = bwd_dkdv_kernel<T, D, C>;
+    hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(kern, dim3((Sk + 127) / 128, B * H), dim3(256), lds, s, (const T*)q, (const T*)k,
+                       (const T*)v, (const T*)dO, lse, delta, (T*)dk, (T*)dv, H, Sq, Sk, st[0], st[1], st[2],
+                       st[3], st[4], st[5], st[6], st[7], st[8], scale, sl2);
+  }
+}
+
+}  // namespace fa
+}  // namespace pra
+
+using namespace pra;
+
+#define PRA_FA_DISPATCH(FN, ...)                                                                  \
+  do {                                                                                             \
+    if (dt == kBF16) {                                                                             \
+      if (D == 128) { if (causal) fa::FN<bf16, 128, true>(__VA_ARGS__); else fa::FN<bf16, 128, false>(__VA_ARGS__); } \
+      else { if (causal) fa::FN<bf16, 64, true>(__VA_ARGS__); else fa::FN<bf16, 64, false>(__VA_ARGS__); } \
+    } else {                                                                                       \
+      if (D == 128) { if (causal) fa::FN<f16, 128, true>(__VA_ARGS__); else fa::FN<f16, 128, false>(__VA_ARGS__); } \
+      else { if (causal) fa::FN<f16, 64, true>(__VA_ARGS__); else fa::FN<f16, 64, false>(__VA_ARGS__); } \
+    }                                                                                              \
+  } while (0)
+
+extern "C" {
+int pra_flash_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B, int H, int Sq, int Sk,
+                  int D, const int64_t* strides, float scale, int causal, int dt, hipStream_t s) {
+  if (!(D == 64 || D == 128) || !(dt == kBF16 || dt == kF16)) return -1;
+  if (B * H == 0 || Sq == 0) return 0;
+  PRA_FA_DISPATCH(launch_fwd, q, k, v, o, lse, B, H, Sq, Sk, strides, scale, s);
+  return 0;
+}
+int pra_flash_bwd(const void* q, const void* k, const void* v, const void* dO, const float* lse, const float* delta,
+                  void* dq, void* dk, void* dv, int B, int H, int Sq, int Sk, int D, const int64_t* strides,
+                  float scale, int causal, int dt, hipStream_t s) {
+  if (!(D == 64 || D == 128) || !(dt == kBF16 || dt == kF16)) return -1;
+  if (B * H == 0 || Sq == 0) return 0;
+  PRA_FA_DISPATCH(launch_bwd, q, k, v, dO, lse, delta, dq, dk, dv, B, H, Sq, Sk, strides, scale, s);
+  return 0;
+}
+}

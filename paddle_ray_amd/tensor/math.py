@@ -1,0 +1,635 @@
+"""Math / logic / search / stat API.
+
+Parity: python/paddle/tensor/{math.py,logic.py,search.py,stat.py}. Elementwise
+and reduction ops map onto PyTorch-ROCm's fused elementwise engine; hot fused
+ops (norms, softmax, CE, attention, optimizers) live in ``paddle_ray_amd.ops``.
+"""
+import builtins
+import numbers
+
+import numpy as np
+import torch
+
+from ..framework.core import Tensor, _u, convert_dtype, _default_device
+
+
+def _t(x, like=None):
+    if isinstance(x, Tensor):
+        return x._t
+    if isinstance(x, torch.Tensor):
+        return x
+    if like is not None and isinstance(x, (numbers.Number, bool)):
+        return x
+    return torch.as_tensor(np.asarray(x), device=_default_device())
+
+
+def _ax(axis):
+    if axis is None:
+        return None
+    if isinstance(axis, Tensor):
+        axis = axis._t.tolist()
+    if isinstance(axis, (list, tuple)):
+        if len(axis) == 0:
+            return None
+        return tuple(int(a) for a in axis)
+    return int(axis)
+
+
+def _binary(fn):
+    def op(x, y, name=None):
+        a = _t(x)
+        b = _t(y, like=a)
+        return Tensor(fn(a, b))
+    return op
+
+
+def _unary(fn):
+    def op(x, name=None):
+        return Tensor(fn(_t(x)))
+    return op
+
+
+def _inplace_unary(fn):
+    def op(x, name=None):
+        fn(x._t)
+        return x
+    return op
+
+
+# -- elementwise binary -------------------------------------------------------
+add = _binary(torch.add)
+subtract = _binary(torch.sub)
+multiply = _binary(torch.mul)
+maximum = _binary(torch.maximum)
+minimum = _binary(torch.minimum)
+fmax = _binary(torch.fmax)
+fmin = _binary(torch.fmin)
+atan2 = _binary(torch.atan2)
+heaviside = _binary(torch.heaviside)
+gcd = _binary(torch.gcd)
+lcm = _binary(torch.lcm)
+bitwise_and = _binary(torch.bitwise_and)
+bitwise_or = _binary(torch.bitwise_or)
+bitwise_xor = _binary(torch.bitwise_xor)
+logical_and = _binary(torch.logical_and)
+logical_or = _binary(torch.logical_or)
+logical_xor = _binary(torch.logical_xor)
+equal = _binary(torch.eq)
+not_equal = _binary(torch.ne)
+less_than = _binary(torch.lt)
+less_equal = _binary(torch.le)
+greater_than = _binary(torch.gt)
+greater_equal = _binary(torch.ge)
+
+
+def divide(x, y, name=None):
+    a = _t(x)
+    b = _t(y, like=a)
+    if not a.is_floating_point() and not (isinstance(b, torch.Tensor) and b.is_floating_point()) \
+            and not isinstance(b, float):
+        return Tensor(torch.div(a, b, rounding_mode='trunc'))
+    return Tensor(torch.div(a, b))
+
+
+def floor_divide(x, y, name=None):
+    a = _t(x)
+    return Tensor(torch.div(a, _t(y, like=a), rounding_mode='floor'))
+
+
+def remainder(x, y, name=None):
+    a = _t(x)
+    return Tensor(torch.remainder(a, _t(y, like=a)))
+
+
+mod = remainder
+floor_mod = remainder
+
+
+def pow(x, y, name=None):
+    a = _t(x)
+    return Tensor(torch.pow(a, _t(y, like=a)))
+
+
+def add_(x, y, name=None):
+    x._t.add_(_t(y, like=x._t))
+    return x
+
+
+def subtract_(x, y, name=None):
+    x._t.sub_(_t(y, like=x._t))
+    return x
+
+
+def multiply_(x, y, name=None):
+    x._t.mul_(_t(y, like=x._t))
+    return x
+
+
+def scale(x, scale=1.0, bias=0.0, bias_after_scale=True, act=None, name=None):
+    t = _t(x)
+    s = scale.item() if isinstance(scale, Tensor) else scale
+    out = t * s + bias if bias_after_scale else (t + bias) * s
+    if act == 'relu':
+        out = torch.relu(out)
+    elif act == 'tanh':
+        out = torch.tanh(out)
+    return Tensor(out)
+
+
+def scale_(x, scale=1.0, bias=0.0, bias_after_scale=True, act=None, name=None):
+    with torch.no_grad() if x._t.is_leaf and x._t.requires_grad else _null():
+        if bias_after_scale:
+            x._t.mul_(scale).add_(bias)
+        else:
+            x._t.add_(bias).mul_(scale)
+    return x
+
+
+class _null:
+    def __enter__(self):
+        pass
+
+    def __exit__(self, *a):
+        pass
+
+
+def lerp(x, y, weight, name=None):
+    return Tensor(torch.lerp(_t(x), _t(y), _t(weight, like=_t(x))))
+
+
+def logit(x, eps=None, name=None):
+    return Tensor(torch.logit(_t(x), eps))
+
+
+def stanh(x, scale_a=0.67, scale_b=1.7159, name=None):
+    return Tensor(scale_b * torch.tanh(scale_a * _t(x)))
+
+
+def clip(x, min=None, max=None, name=None):
+    t = _t(x)
+    mn = min.item() if isinstance(min, Tensor) else min
+    mx = max.item() if isinstance(max, Tensor) else max
+    return Tensor(torch.clamp(t, mn, mx))
+
+
+def clip_(x, min=None, max=None, name=None):
+    x._t.clamp_(min, max)
+    return x
+
+
+def increment(x, value=1.0, name=None):
+    x._t.add_(value)
+    return x
+
+
+def addmm(input, x, y, beta=1.0, alpha=1.0, name=None):
+    return Tensor(torch.addmm(_t(input), _t(x), _t(y), beta=beta, alpha=alpha))
+
+
+def inner(x, y, name=None):
+    return Tensor(torch.inner(_t(x), _t(y)))
+
+
+def outer(x, y, name=None):
+    return Tensor(torch.outer(_t(x).flatten(), _t(y).flatten()))
+
+
+def kron(x, y, name=None):
+    return Tensor(torch.kron(_t(x), _t(y)))
+
+
+def add_n(inputs, name=None):
+    if isinstance(inputs, Tensor):
+        return inputs
+    out = _t(inputs[0])
+    for i in inputs[1:]:
+        out = out + _t(i)
+    return Tensor(out)
+
+
+def nan_to_num(x, nan=0.0, posinf=None, neginf=None, name=None):
+    return Tensor(torch.nan_to_num(_t(x), nan, posinf, neginf))
+
+
+def diff(x, n=1, axis=-1, prepend=None, append=None, name=None):
+    return Tensor(torch.diff(_t(x), n, axis, None if prepend is None else _t(prepend),
+                             None if append is None else _t(append)))
+
+
+def frexp(x, name=None):
+    m, e = torch.frexp(_t(x))
+    return Tensor(m), Tensor(e.to(_t(x).dtype))
+
+
+def renorm(x, p, axis, max_norm):
+    return Tensor(torch.renorm(_t(x), p, axis, max_norm))
+
+
+# -- elementwise unary ---------------------------------------------------------
+for _n, _f in dict(abs=torch.abs, acos=torch.acos, asin=torch.asin, atan=torch.atan, cos=torch.cos,
+                   sin=torch.sin, tan=torch.tan, cosh=torch.cosh, sinh=torch.sinh, tanh=torch.tanh,
+                   acosh=torch.acosh, asinh=torch.asinh, atanh=torch.atanh, exp=torch.exp,
+                   expm1=torch.expm1, log=torch.log, log2=torch.log2, log10=torch.log10,
+                   log1p=torch.log1p, sqrt=torch.sqrt, rsqrt=torch.rsqrt, square=torch.square,
+                   ceil=torch.ceil, floor=torch.floor, round=torch.round, trunc=torch.trunc,
+                   frac=torch.frac, reciprocal=torch.reciprocal, sign=torch.sign, sgn=torch.sgn,
+                   neg=torch.neg, erf=torch.erf, erfinv=torch.erfinv, lgamma=torch.lgamma,
+                   digamma=torch.digamma, isnan=torch.isnan, isinf=torch.isinf,
+                   isfinite=torch.isfinite, logical_not=torch.logical_not,
+                   bitwise_not=torch.bitwise_not, conj=torch.conj_physical, real=torch.real,
+                   imag=torch.imag, angle=torch.angle, deg2rad=torch.deg2rad,
+                   rad2deg=torch.rad2deg, sigmoid=torch.sigmoid, i0=torch.i0).items():
+    globals()[_n] = _unary(_f)
+for _n, _f in dict(tanh_=torch.Tensor.tanh_, exp_=torch.Tensor.exp_, sqrt_=torch.Tensor.sqrt_,
+                   rsqrt_=torch.Tensor.rsqrt_, ceil_=torch.Tensor.ceil_,
+                   floor_=torch.Tensor.floor_, round_=torch.Tensor.round_,
+                   reciprocal_=torch.Tensor.reciprocal_, abs_=torch.Tensor.abs_,
+                   neg_=torch.Tensor.neg_, sigmoid_=torch.Tensor.sigmoid_,
+                   zero_=torch.Tensor.zero_).items():
+    globals()[_n] = _inplace_unary(_f)
+
+
+def fill_(x, value):
+    x._t.fill_(value)
+    return x
+
+
+def as_complex(x, name=None):
+    return Tensor(torch.view_as_complex(_t(x)))
+
+
+def as_real(x, name=None):
+    return Tensor(torch.view_as_real(_t(x)))
+
+
+def is_complex(x):
+    return _t(x).is_complex()
+
+
+def is_floating_point(x):
+    return _t(x).is_floating_point()
+
+
+def is_integer(x):
+    t = _t(x)
+    return not t.is_floating_point() and not t.is_complex() and t.dtype != torch.bool
+
+
+def is_empty(x, name=None):
+    return Tensor(torch.tensor(_t(x).numel() == 0))
+
+
+# -- reductions ----------------------------------------------------------------
+def _red_dtype(t, dtype):
+    if dtype is not None:
+        return convert_dtype(dtype)
+    if t.dtype in (torch.bool, torch.int32, torch.int16, torch.int8, torch.uint8):
+        return torch.int64
+    return None
+
+
+def sum(x, axis=None, dtype=None, keepdim=False, name=None):
+    t = _t(x)
+    a = _ax(axis)
+    d = _red_dtype(t, dtype)
+    if a is None:
+        out = t.sum(dtype=d)
+        if keepdim:
+            out = out.reshape([1] * t.dim())
+        return Tensor(out)
+    return Tensor(t.sum(a, keepdim=keepdim, dtype=d))
+
+
+def nansum(x, axis=None, dtype=None, keepdim=False, name=None):
+    t = _t(x)
+    a = _ax(axis)
+    return Tensor(torch.nansum(t, a, keepdim=keepdim, dtype=convert_dtype(dtype)) if a is not None
+                  else torch.nansum(t, dtype=convert_dtype(dtype)))
+
+
+def mean(x, axis=None, keepdim=False, name=None):
+    t = _t(x)
+    a = _ax(axis)
+    if a is None:
+        out = t.mean()
+        return Tensor(out.reshape([1] * t.dim()) if keepdim else out)
+    return Tensor(t.mean(a, keepdim=keepdim))
+
+
+def nanmean(x, axis=None, keepdim=False, name=None):
+    t = _t(x)
+    a = _ax(axis)
+    return Tensor(torch.nanmean(t, a, keepdim=keepdim))
+
+
+def prod(x, axis=None, keepdim=False, dtype=None, name=None):
+    t = _t(x)
+    a = _ax(axis)
+    d = convert_dtype(dtype)
+    if a is None:
+        return Tensor(t.prod(dtype=d))
+    if isinstance(a, tuple):
+        out = t
+        for ax in sorted([ax % t.dim() for ax in a], reverse=True):
+            out = out.prod(ax, keepdim=keepdim, dtype=d)
+        return Tensor(out)
+    return Tensor(t.prod(a, keepdim=keepdim, dtype=d))
+
+
+def _minmax(fn):
+    def op(x, axis=None, keepdim=False, name=None):
+        t = _t(x)
+        a = _ax(axis)
+        if a is None:
+            out = fn(t)
+            return Tensor(out.reshape([1] * t.dim()) if keepdim else out)
+        return Tensor(fn(t, dim=a, keepdim=keepdim))
+    return op
+
+
+max = _minmax(torch.amax)
+min = _minmax(torch.amin)
+amax = max
+amin = min
+
+
+def all(x, axis=None, keepdim=False, name=None):
+    t = _t(x)
+    a = _ax(axis)
+    if a is None:
+        return Tensor(t.all())
+    if isinstance(a, tuple):
+        out = t
+        for ax in sorted([ax % t.dim() for ax in a], reverse=True):
+            out = out.all(ax, keepdim=keepdim)
+        return Tensor(out)
+    return Tensor(t.all(a, keepdim=keepdim))
+
+
+def any(x, axis=None, keepdim=False, name=None):
+    t = _t(x)
+    a = _ax(axis)
+    if a is None:
+        return Tensor(t.any())
+    if isinstance(a, tuple):
+        out = t
+        for ax in sorted([ax % t.dim() for ax in a], reverse=True):
+            out = out.any(ax, keepdim=keepdim)
+        return Tensor(out)
+    return Tensor(t.any(a, keepdim=keepdim))
+
+
+def logsumexp(x, axis=None, keepdim=False, name=None):
+    t = _t(x)
+    a = _ax(axis)
+    if a is None:
+        a = tuple(range(t.dim()))
+    return Tensor(torch.logsumexp(t, a, keepdim=keepdim))
+
+
+def cumsum(x, axis=None, dtype=None, name=None):
+    t = _t(x)
+    if axis is None:
+        t, axis = t.flatten(), 0
+    return Tensor(torch.cumsum(t, axis, dtype=convert_dtype(dtype)))
+
+
+def cumprod(x, dim=None, dtype=None, name=None):
+    t = _t(x)
+    if dim is None:
+        t, dim = t.flatten(), 0
+    return Tensor(torch.cumprod(t, dim, dtype=convert_dtype(dtype)))
+
+
+def logcumsumexp(x, axis=None, dtype=None, name=None):
+    t = _t(x)
+    if axis is None:
+        t, axis = t.flatten(), 0
+    if dtype is not None:
+        t = t.to(convert_dtype(dtype))
+    return Tensor(torch.logcumsumexp(t, axis))
+
+
+def count_nonzero(x, axis=None, keepdim=False, name=None):
+    t = _t(x)
+    a = _ax(axis)
+    out = torch.count_nonzero(t, a)
+    if keepdim and a is not None:
+        for ax in sorted([a] if isinstance(a, int) else a):
+            out = out.unsqueeze(ax % t.dim())
+    return Tensor(out)
+
+
+def trace(x, offset=0, axis1=0, axis2=1, name=None):
+    return Tensor(torch.diagonal(_t(x), offset, axis1, axis2).sum(-1))
+
+
+def diagonal(x, offset=0, axis1=0, axis2=1, name=None):
+    return Tensor(torch.diagonal(_t(x), offset, axis1, axis2))
+
+
+# -- stat ----------------------------------------------------------------------
+def var(x, axis=None, unbiased=True, keepdim=False, name=None):
+    t = _t(x)
+    a = _ax(axis)
+    return Tensor(torch.var(t, a, correction=1 if unbiased else 0, keepdim=keepdim))
+
+
+def std(x, axis=None, unbiased=True, keepdim=False, name=None):
+    t = _t(x)
+    a = _ax(axis)
+    return Tensor(torch.std(t, a, correction=1 if unbiased else 0, keepdim=keepdim))
+
+
+def median(x, axis=None, keepdim=False, name=None):
+    t = _t(x)
+    if axis is None:
+        s = t.flatten().sort().values
+        n = s.numel()
+        m = (s[(n - 1) // 2] + s[n // 2]) / 2 if n % 2 == 0 else s[n // 2]
+        return Tensor(m.reshape([1] * t.dim()) if keepdim else m)
+    return Tensor(torch.quantile(t.float(), 0.5, dim=axis, keepdim=keepdim).to(t.dtype)
+                  if t.is_floating_point() else torch.median(t, axis, keepdim).values)
+
+
+def nanmedian(x, axis=None, keepdim=True, name=None):
+    t = _t(x)
+    if axis is None:
+        return Tensor(torch.nanquantile(t.flatten().float(), 0.5))
+    return Tensor(torch.nanquantile(t.float(), 0.5, dim=axis, keepdim=keepdim))
+
+
+def quantile(x, q, axis=None, keepdim=False):
+    t = _t(x)
+    qq = torch.as_tensor(q, dtype=t.dtype, device=t.device)
+    if axis is None:
+        return Tensor(torch.quantile(t.flatten(), qq))
+    if isinstance(axis, (list, tuple)):
+        axs = [a % t.dim() for a in axis]
+        rest = [i for i in range(t.dim()) if i not in axs]
+        tp = t.permute(rest + axs).reshape([t.shape[i] for i in rest] + [-1])
+        out = torch.quantile(tp, qq, dim=-1)
+        if keepdim:
+            for a in sorted(axs):
+                out = out.unsqueeze(a + (1 if qq.dim() else 0))
+        return Tensor(out)
+    return Tensor(torch.quantile(t, qq, dim=axis, keepdim=keepdim))
+
+
+def nanquantile(x, q, axis=None, keepdim=False):
+    t = _t(x)
+    qq = torch.as_tensor(q, dtype=t.dtype, device=t.device)
+    if axis is None:
+        return Tensor(torch.nanquantile(t.flatten(), qq))
+    return Tensor(torch.nanquantile(t, qq, dim=axis, keepdim=keepdim))
+
+
+def numel(x, name=None):
+    return Tensor(torch.tensor(_t(x).numel(), dtype=torch.int64))
+
+
+# -- logic ---------------------------------------------------------------------
+def allclose(x, y, rtol=1e-05, atol=1e-08, equal_nan=False, name=None):
+    return Tensor(torch.tensor(torch.allclose(_t(x), _t(y), rtol, atol, equal_nan)))
+
+
+def isclose(x, y, rtol=1e-05, atol=1e-08, equal_nan=False, name=None):
+    return Tensor(torch.isclose(_t(x), _t(y), rtol, atol, equal_nan))
+
+
+def equal_all(x, y, name=None):
+    return Tensor(torch.tensor(torch.equal(_t(x), _t(y))))
+
+
+def is_tensor(x):
+    return isinstance(x, Tensor)
+
+
+# -- search --------------------------------------------------------------------
+def argmax(x, axis=None, keepdim=False, dtype='int64', name=None):
+    t = _t(x)
+    out = torch.argmax(t.flatten() if axis is None else t, None if axis is None else int(axis),
+                       keepdim=keepdim and axis is not None)
+    return Tensor(out.to(convert_dtype(dtype)))
+
+
+def argmin(x, axis=None, keepdim=False, dtype='int64', name=None):
+    t = _t(x)
+    out = torch.argmin(t.flatten() if axis is None else t, None if axis is None else int(axis),
+                       keepdim=keepdim and axis is not None)
+    return Tensor(out.to(convert_dtype(dtype)))
+
+
+def argsort(x, axis=-1, descending=False, stable=False, name=None):
+    return Tensor(torch.argsort(_t(x), dim=axis, descending=descending, stable=True))
+
+
+def sort(x, axis=-1, descending=False, stable=False, name=None):
+    return Tensor(torch.sort(_t(x), dim=axis, descending=descending, stable=True).values)
+
+
+def topk(x, k, axis=-1, largest=True, sorted=True, name=None):
+    k = k.item() if isinstance(k, Tensor) else k
+    v, i = torch.topk(_t(x), int(k), dim=axis, largest=largest, sorted=sorted)
+    return Tensor(v), Tensor(i)
+
+
+def kthvalue(x, k, axis=-1, keepdim=False, name=None):
+    v, i = torch.kthvalue(_t(x), k, axis, keepdim)
+    return Tensor(v), Tensor(i)
+
+
+def mode(x, axis=-1, keepdim=False, name=None):
+    v, i = torch.mode(_t(x), axis, keepdim)
+    return Tensor(v), Tensor(i)
+
+
+def nonzero(x, as_tuple=False):
+    t = _t(x)
+    if as_tuple:
+        return tuple(Tensor(i.unsqueeze(-1)) for i in torch.nonzero(t, as_tuple=True))
+    return Tensor(torch.nonzero(t))
+
+
+def where(condition, x=None, y=None, name=None):
+    c = _t(condition)
+    if x is None and y is None:
+        return nonzero(condition, as_tuple=True)
+    a = _t(x) if isinstance(x, (Tensor, torch.Tensor)) else x
+    b = _t(y) if isinstance(y, (Tensor, torch.Tensor)) else y
+    return Tensor(torch.where(c, a, b))
+
+
+def masked_select(x, mask, name=None):
+    return Tensor(torch.masked_select(_t(x), _t(mask)))
+
+
+def searchsorted(sorted_sequence, values, out_int32=False, right=False, name=None):
+    return Tensor(torch.searchsorted(_t(sorted_sequence), _t(values), out_int32=out_int32,
+                                     right=right))
+
+
+def bucketize(x, sorted_sequence, out_int32=False, right=False, name=None):
+    return Tensor(torch.bucketize(_t(x), _t(sorted_sequence), out_int32=out_int32, right=right))
+
+
+def index_sample(x, index):
+    return Tensor(torch.gather(_t(x), 1, _t(index)))
+
+
+def unique(x, return_index=False, return_inverse=False, return_counts=False, axis=None,
+           dtype='int64', name=None):
+    t = _t(x)
+    u, inv, cnt = torch.unique(t, sorted=True, return_inverse=True, return_counts=True, dim=axis)
+    outs = [Tensor(u)]
+    if return_index:
+        flat = t.flatten() if axis is None else t
+        n = flat.shape[0] if axis is not None else flat.numel()
+        perm = torch.arange(n, device=t.device)
+        invf = inv.flatten()
+        idx = torch.full((u.shape[0] if axis is not None else u.numel(),), n, dtype=torch.int64,
+                         device=t.device)
+        idx = idx.scatter_reduce(0, invf, perm, reduce='amin')
+        outs.append(Tensor(idx.to(convert_dtype(dtype))))
+    if return_inverse:
+        outs.append(Tensor(inv.flatten().to(convert_dtype(dtype)) if axis is None
+                           else inv.to(convert_dtype(dtype))))
+    if return_counts:
+        outs.append(Tensor(cnt.to(convert_dtype(dtype))))
+    return outs[0] if len(outs) == 1 else tuple(outs)
+
+
+def unique_consecutive(x, return_inverse=False, return_counts=False, axis=None, dtype='int64',
+                       name=None):
+    u, inv, cnt = torch.unique_consecutive(_t(x), return_inverse=True, return_counts=True, dim=axis)
+    outs = [Tensor(u)]
+    if return_inverse:
+        outs.append(Tensor(inv.to(convert_dtype(dtype))))
+    if return_counts:
+        outs.append(Tensor(cnt.to(convert_dtype(dtype))))
+    return outs[0] if len(outs) == 1 else tuple(outs)
+
+
+def bincount(x, weights=None, minlength=0, name=None):
+    return Tensor(torch.bincount(_t(x), None if weights is None else _t(weights), minlength))
+
+
+def histogram(input, bins=100, min=0, max=0, name=None):
+    t = _t(input).float()
+    if min == 0 and max == 0:
+        min, max = t.min().item(), t.max().item()
+    return Tensor(torch.histc(t, bins, min, max).to(torch.int64))
+
+
+def multiplex(inputs, index, name=None):
+    st = torch.stack([_t(i) for i in inputs], 0)
+    idx = _t(index).flatten()
+    return Tensor(st[idx, torch.arange(idx.numel(), device=idx.device)])
+
+
+def dist(x, y, p=2, name=None):
+    return Tensor(torch.dist(_t(x), _t(y), p))
+
+
+def broadcast_shape(x_shape, y_shape):
+    return list(torch.broadcast_shapes(tuple(x_shape), tuple(y_shape)))

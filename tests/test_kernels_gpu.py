@@ -1,0 +1,196 @@
+"""Numerics of every gfx950 HIP kernel vs a PyTorch fp32 reference of the same op."""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from paddle_ray_amd.ops import fused as F  # noqa: E402
+from paddle_ray_amd.ops import registry as R  # noqa: E402
+from paddle_ray_amd.ops import _native  # noqa: E402
+
+DEV = 'cuda'
+
+
+def test_native_loaded():
+    assert _native.available(), _native.load_error()
+
+
+def _tol(dt):
+    return {torch.float32: 2e-5, torch.float16: 2e-3, torch.bfloat16: 2e-2}[dt]
+
+
+@pytest.mark.parametrize('dt', [torch.float32, torch.bfloat16, torch.float16])
+@pytest.mark.parametrize('cols', [2048, 1000, 768, 8192])
+def test_layer_norm(dt, cols):
+    torch.manual_seed(0)
+    x = torch.randn(37, cols, device=DEV, dtype=dt, requires_grad=True)
+    w = torch.randn(cols, device=DEV, dtype=dt, requires_grad=True)
+    b = torch.randn(cols, device=DEV, dtype=dt, requires_grad=True)
+    y = F.layer_norm(x, w, b, 1e-5)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    xr, wr, br = (t.detach().float().requires_grad_() for t in (x, w, b))
+    yr = torch.nn.functional.layer_norm(xr, (cols,), wr, br, 1e-5)
+    yr.backward(dy.float())
+    tol = _tol(dt)
+    assert torch.allclose(y.float(), yr, atol=tol * 4, rtol=tol)
+    assert torch.allclose(x.grad.float(), xr.grad, atol=tol * 8, rtol=tol * 4)
+    assert torch.allclose(w.grad.float(), wr.grad, atol=tol * 40, rtol=tol * 4)
+    assert torch.allclose(b.grad.float(), br.grad, atol=tol * 40, rtol=tol * 4)
+
+
+@pytest.mark.parametrize('dt', [torch.float32, torch.bfloat16])
+def test_rms_norm(dt):
+    x = torch.randn(64, 4096, device=DEV, dtype=dt, requires_grad=True)
+    w = torch.randn(4096, device=DEV, dtype=dt, requires_grad=True)
+    y = F.rms_norm(x, w, 1e-6)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    xr, wr = (t.detach().float().requires_grad_() for t in (x, w))
+    yr = xr * torch.rsqrt(xr.pow(2).mean(-1, keepdim=True) + 1e-6) * wr
+    yr.backward(dy.float())
+    tol = _tol(dt)
+    assert torch.allclose(y.float(), yr, atol=tol * 4, rtol=tol)
+    assert torch.allclose(x.grad.float(), xr.grad, atol=tol * 8, rtol=tol * 4)
+    assert torch.allclose(w.grad.float(), wr.grad, atol=tol * 40, rtol=tol * 4)
+
+
+@pytest.mark.parametrize('dt', [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize('cols', [1024, 50304, 333])
+def test_softmax(dt, cols):
+    x = torch.randn(19, cols, device=DEV, dtype=dt, requires_grad=True)
+    y = F.softmax_lastdim(x)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    xr = x.detach().float().requires_grad_()
+    yr = torch.softmax(xr, -1)
+    yr.backward(dy.float())
+    tol = _tol(dt)
+    assert torch.allclose(y.float(), yr, atol=tol, rtol=tol)
+    assert torch.allclose(x.grad.float(), xr.grad, atol=tol, rtol=tol * 4)
+
+
+@pytest.mark.parametrize('dt', [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize('V', [50304, 1001])
+def test_softmax_ce(dt, V):
+    N = 67
+    x = (torch.randn(N, V, device=DEV) * 3).to(dt).requires_grad_()
+    lab = torch.randint(0, V, (N,), device=DEV)
+    lab[3] = -100
+    loss = F.softmax_cross_entropy(x, lab, -100)
+    g = torch.rand(N, device=DEV)
+    loss.backward(g)
+    xr = x.detach().float().requires_grad_()
+    lr = torch.nn.functional.cross_entropy(xr, lab, ignore_index=-100, reduction='none')
+    lr.backward(g)
+    assert torch.allclose(loss, lr, atol=1e-3, rtol=1e-4)
+    tol = _tol(dt)
+    assert torch.allclose(x.grad.float(), xr.grad, atol=tol * 0.1, rtol=tol * 4)
+
+
+@pytest.mark.parametrize('dt', [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize('approx', [True, False])
+def test_bias_gelu(dt, approx):
+    x = torch.randn(33, 8192, device=DEV, dtype=dt, requires_grad=True)
+    b = torch.randn(8192, device=DEV, dtype=dt, requires_grad=True)
+    y = F.bias_gelu(x, b, approx)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    xr, br = (t.detach().float().requires_grad_() for t in (x, b))
+    yr = torch.nn.functional.gelu(xr + br, approximate='tanh' if approx else 'none')
+    yr.backward(dy.float())
+    tol = _tol(dt)
+    assert torch.allclose(y.float(), yr, atol=tol, rtol=tol)
+    assert torch.allclose(x.grad.float(), xr.grad, atol=tol * 2, rtol=tol * 2)
+    assert torch.allclose(b.grad.float(), br.grad, atol=tol * 40, rtol=tol * 4)
+
+
+def _attn_ref(q, k, v, causal, scale):
+    qf, kf, vf = (t.float().permute(0, 2, 1, 3) for t in (q, k, v))
+    s = qf @ kf.transpose(-1, -2) * scale
+    if causal:
+        Sq, Sk = s.shape[-2:]
+        m = torch.ones(Sq, Sk, dtype=torch.bool, device=s.device).triu(Sk - Sq + 1)
+        s = s.masked_fill(m, float('-inf'))
+    return (torch.softmax(s, -1) @ vf).permute(0, 2, 1, 3)
+
+
+@pytest.mark.parametrize('dt', [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize('D', [64, 128])
+@pytest.mark.parametrize('causal', [True, False])
+@pytest.mark.parametrize('S', [256, 200])
+def test_flash_attention(dt, D, causal, S):
+    torch.manual_seed(1)
+    B, H = 2, 3
+    qkv = torch.randn(B, S, 3, H, D, device=DEV, dtype=dt)
+    q, k, v = qkv.unbind(2)  # strided views, like the GPT fused projection
+    q, k, v = (t.detach().requires_grad_() for t in (q, k, v))
+    scale = 1.0 / math.sqrt(D)
+    o = F.flash_attention(q, k, v, causal=causal, scale=scale)
+    do = torch.randn_like(o)
+    o.backward(do)
+    qr, kr, vr = (t.detach().float().requires_grad_() for t in (q, k, v))
+    orf = _attn_ref(qr, kr, vr, causal, scale)
+    orf.backward(do.float())
+    tol = 2e-2 if dt == torch.bfloat16 else 4e-3
+    assert (o.float() - orf).abs().max().item() < tol * 2, (o.float() - orf).abs().max()
+    for g, gr in ((q.grad, qr.grad), (k.grad, kr.grad), (v.grad, vr.grad)):
+        err = (g.float() - gr).abs().max().item()
+        assert err < tol * 4 * max(1.0, gr.abs().max().item()), err
+
+
+def test_flash_attention_spike_rows():
+    """A spiked key forces the online-softmax rescale path (CDNA guide rule 26)."""
+    B, S, H, D = 1, 256, 2, 128
+    q = torch.randn(B, S, H, D, device=DEV, dtype=torch.bfloat16)
+    k = torch.randn(B, S, H, D, device=DEV, dtype=torch.bfloat16)
+    v = torch.randn(B, S, H, D, device=DEV, dtype=torch.bfloat16)
+    k[:, 200] *= 30
+    o = F.flash_attention(q, k, v, causal=True)
+    ref = _attn_ref(q, k, v, True, 1 / math.sqrt(D))
+    assert (o.float() - ref).abs().max().item() < 5e-2
+
+
+@pytest.mark.parametrize('master', [True, False])
+def test_adamw_multi_tensor(master):
+    torch.manual_seed(0)
+    shapes = [(1000,), (70000,), (3, 5)]
+    pdt = torch.bfloat16 if master else torch.float32
+    ps = [torch.randn(s, device=DEV).to(pdt) for s in shapes]
+    gs = [torch.randn(s, device=DEV).to(pdt) for s in shapes]
+    ms = [torch.zeros(s, device=DEV) for s in shapes]
+    vs = [torch.zeros(s, device=DEV) for s in shapes]
+    mas = [p.float().clone() for p in ps] if master else [None] * 3
+    wds, lrm = [0.1, 0.0, 0.01], [1.0, 0.5, 1.0]
+    ref_p = [p.clone() for p in ps]
+    ref_m = [m.clone() for m in ms]
+    ref_v = [v.clone() for v in vs]
+    ref_ma = [m.clone() for m in mas] if master else [None] * 3
+    mt = F.MultiTensorAdamW(ps, lambda: gs, ms, vs, mas, wds, lrm)
+    for step in (1, 2, 3):
+        mt.step(1e-2, 0.9, 0.999, 1e-8, step, grad_scale=0.5)
+        F.adamw_ref(ref_p, gs, ref_m, ref_v, ref_ma, 1e-2, 0.9, 0.999, 1e-8, wds, lrm, step, 0.5)
+    torch.cuda.synchronize()
+    for a, b in zip(ps, ref_p):
+        assert torch.allclose(a.float(), b.float(), atol=1e-2 if master else 1e-5)
+    for a, b in zip(ms, ref_m):
+        assert torch.allclose(a, b, atol=1e-5)
+    if master:
+        for a, b in zip(mas, ref_ma):
+            assert torch.allclose(a, b, atol=1e-5)
+
+
+def test_sumsq():
+    ts = [torch.randn(1000, device=DEV), torch.randn(77, 3, device=DEV).bfloat16()]
+    got = F.global_l2_norm_sq(ts)
+    ref = sum((t.float() ** 2).sum() for t in ts)
+    assert torch.allclose(got, ref, rtol=1e-4)
+
+
+def test_registry_uses_hip():
+    R.reset_stats()
+    x = torch.randn(4, 64, device=DEV)
+    F.layer_norm(x, None, None, 1e-5)
+    assert R.stats().get(('layer_norm_fwd', 'hip'), 0) == 1
