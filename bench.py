@@ -1,0 +1,174 @@
+#!/usr/bin/env python
+"""Headline benchmark (BASELINE.json): GPT-3 1.3B pretraining step with Fleet sharding
+stage 3 ('p_g_os') over N MI355X GPUs (one process per GPU, RCCL over xGMI), bf16
+compute, fp32 master weights + AdamW moments (sharded), synthetic token data,
+random-init weights. Weak scaling: ``--micro-batch`` sequences of ``--seq`` tokens
+per GPU per step.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+Prints ONE JSON line on rank 0. ``--model resnet50`` runs the secondary headline
+(ResNet50 bf16 images/s, DP).
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+BASELINE = None  # BASELINE.json "published" is empty: no reference number to divide by
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument('--gpus', type=int, default=1)
+    p.add_argument('--steps', type=int, default=10)
+    p.add_argument('--warmup', type=int, default=3)
+    p.add_argument('--model', default='gpt3-1.3b')
+    p.add_argument('--micro-batch', type=int, default=16)
+    p.add_argument('--seq', type=int, default=1024)
+    p.add_argument('--level', default='p_g_os')
+    p.add_argument('--dropout', type=float, default=0.1)
+    p.add_argument('--recompute', action='store_true')
+    p.add_argument('--profile-dir', default=None)
+    return p.parse_args()
+
+
+def main():
+    a = parse()
+    import torch
+    import torch.distributed as dist
+    import paddle_ray_amd as paddle
+    from paddle_ray_amd.distributed import collective as C
+
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    if world > 1:
+        C.init_parallel_env()
+    rank = C.get_rank()
+    dev = torch.device('cuda', torch.cuda.current_device()) if torch.cuda.is_available() \
+        else torch.device('cpu')
+    if dev.type == 'cuda':
+        paddle.set_device(f'gpu:{dev.index}')
+    paddle.seed(1234 + rank)
+
+    if a.model.startswith('gpt'):
+        result = bench_gpt(a, paddle, torch, dist, C, world, rank, dev)
+    else:
+        result = bench_resnet(a, paddle, torch, dist, C, world, rank, dev)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def _timed(step_fn, a, torch, dist, world, dev):
+    for _ in range(a.warmup):
+        step_fn()
+    if world > 1:
+        dist.barrier()
+    if dev.type == 'cuda':
+        torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step_fn()
+    if dev.type == 'cuda':
+        torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    return dt
+
+
+def bench_gpt(a, paddle, torch, dist, C, world, rank, dev):
+    from paddle_ray_amd.models import gpt_config, GPTForPretraining, gpt_flops_per_token
+    from paddle_ray_amd.distributed.sharding import group_sharded_parallel
+    paddle.set_default_dtype('bfloat16')
+    cfg = gpt_config(a.model, max_seq_len=max(a.seq, 1024), hidden_dropout=a.dropout,
+                     recompute=a.recompute)
+    model = GPTForPretraining(cfg)
+    paddle.set_default_dtype('float32')
+    clip = paddle.nn.ClipGradByGlobalNorm(1.0)
+    sched = paddle.optimizer.lr.CosineAnnealingDecay(1e-4, T_max=100000)
+    opt = paddle.optimizer.AdamW(learning_rate=sched, parameters=model.parameters(),
+                                 weight_decay=0.01, grad_clip=clip, multi_precision=True,
+                                 apply_decay_param_fun=lambda n: not ('norm' in n or '.b' in n))
+    model, opt, _ = group_sharded_parallel(model, opt, a.level)
+    g = torch.Generator(device=dev).manual_seed(rank)
+    tokens = torch.randint(0, cfg.vocab_size, (a.micro_batch, a.seq + 1), device=dev, generator=g)
+    inp = paddle.Tensor(tokens[:, :-1].contiguous())
+    lab = paddle.Tensor(tokens[:, 1:].contiguous())
+    losses = []
+
+    def step():
+        loss = model(inp, lab)
+        loss.backward()
+        opt.step()
+        opt.clear_grad()
+        sched.step()
+        losses.append(loss.detach())
+
+    prof = None
+    if a.profile_dir:
+        prof = torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CPU,
+                                                  torch.profiler.ProfilerActivity.CUDA])
+    dt = _timed(step, a, torch, dist, world, dev)
+    last_loss = float(losses[-1].item())
+    tok = a.micro_batch * a.seq * world * a.steps
+    tps = tok / dt
+    fpt = gpt_flops_per_token(cfg, a.seq)
+    mfu = tps / world * fpt / 2.5e15
+    return {"metric": "tokens/sec GPT-3-1.3B Fleet sharding-3", "value": round(tps, 2),
+            "unit": "tokens/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+            "ms_per_step": round(dt / a.steps * 1000, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None if BASELINE is None else tps / BASELINE,
+            "dtype": "bf16", "data": "synthetic (random tokens, random-init weights)",
+            "config": {"model": "GPT-3-1.3B" if a.model == 'gpt3-1.3b' else a.model,
+                       "global_batch": a.micro_batch * world, "seq_len": a.seq,
+                       "parallelism": f"sharding{ {'os': 1, 'os_g': 2, 'p_g_os': 3}[a.level] }"
+                                      f"_dp{world}",
+                       "micro_batch_per_gpu": a.micro_batch, "hidden_dropout": a.dropout,
+                       "optimizer": "AdamW fp32-master, global-norm clip"},
+            "tokens_per_sec_per_gpu": round(tps / world, 2),
+            "mfu_bf16_dense": round(mfu, 4), "final_loss": round(last_loss, 4)}
+
+
+def bench_resnet(a, paddle, torch, dist, C, world, rank, dev):
+    from paddle_ray_amd.vision.models import resnet50
+    model = resnet50(data_format='NHWC')
+    model = paddle.amp.decorate(model, level='O2', dtype='bfloat16')
+    opt = paddle.optimizer.Momentum(0.1, 0.9, parameters=model.parameters(), weight_decay=1e-4,
+                                    multi_precision=True)
+    if world > 1:
+        model = paddle.DataParallel(model)
+    bs = a.micro_batch if a.micro_batch != 16 else 256
+    x = paddle.Tensor(torch.randn(bs, 224, 224, 3, device=dev, dtype=torch.bfloat16))
+    y = paddle.Tensor(torch.randint(0, 1000, (bs,), device=dev))
+    ce = paddle.nn.CrossEntropyLoss()
+
+    def step():
+        loss = ce(model(x), y)
+        loss.backward()
+        opt.step()
+        opt.clear_grad()
+
+    dt = _timed(step, a, torch, dist, world, dev)
+    ips = bs * world * a.steps / dt
+    return {"metric": "samples/sec ResNet50 bf16", "value": round(ips, 2), "unit": "images/s",
+            "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+            "ms_per_step": round(dt / a.steps * 1000, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
+            "config": {"model": "ResNet50", "global_batch": bs * world, "seq_len": None,
+                       "parallelism": f"dp{world}"},
+            "samples_per_sec_per_gpu": round(ips / world, 2)}
+
+
+if __name__ == '__main__':
+    main()

@@ -1,0 +1,37 @@
+"""paddle.device (parity: python/paddle/device/__init__.py). 'gpu' == the HIP device."""
+import torch
+
+from ..framework.core import (set_device, get_device, is_compiled_with_cuda, is_compiled_with_rocm,  # noqa
+                              is_compiled_with_xpu)
+from . import cuda  # noqa
+
+
+def get_all_device_type():
+    return ['cpu'] + (['gpu'] if torch.cuda.is_available() else [])
+
+
+def get_all_custom_device_type():
+    return []
+
+
+def get_available_device():
+    return ['cpu'] + [f'gpu:{i}' for i in range(torch.cuda.device_count())]
+
+
+def get_cudnn_version():
+    return None
+
+
+def synchronize(device=None):
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+
+
+def is_compiled_with_cinn():
+    return False
+
+
+Stream = cuda.Stream
+Event = cuda.Event
+current_stream = cuda.current_stream
+stream_guard = cuda.stream_guard

@@ -1,0 +1,76 @@
+import argparse
+import os
+import signal
+import socket
+import subprocess
+import sys
+import time
+
+
+def _parse(argv=None):
+    p = argparse.ArgumentParser('paddle_ray_amd.distributed.launch')
+    p.add_argument('--gpus', '--devices', dest='devices', default=None)
+    p.add_argument('--nproc_per_node', type=int, default=None)
+    p.add_argument('--master', default=None)
+    p.add_argument('--nnodes', default='1')
+    p.add_argument('--rank', type=int, default=0)
+    p.add_argument('--log_dir', default='log')
+    p.add_argument('--job_id', default='default')
+    p.add_argument('training_script')
+    p.add_argument('training_script_args', nargs=argparse.REMAINDER)
+    return p.parse_args(argv)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch(argv=None):
+    a = _parse(argv)
+    if a.devices:
+        devs = [d for d in a.devices.split(',') if d != '']
+    else:
+        n = a.nproc_per_node or int(os.environ.get('PRA_NPROC', '1'))
+        devs = [str(i) for i in range(n)]
+    n = len(devs)
+    if a.master:
+        addr, port = a.master.split(':')
+    else:
+        addr, port = '127.0.0.1', str(_free_port())
+    os.makedirs(a.log_dir, exist_ok=True)
+    procs = []
+    eps = ','.join(f'{addr}:{int(port) + i}' for i in range(n))
+    for r, d in enumerate(devs):
+        env = dict(os.environ)
+        env.update({'RANK': str(r), 'LOCAL_RANK': str(r), 'WORLD_SIZE': str(n),
+                    'MASTER_ADDR': addr, 'MASTER_PORT': str(port),
+                    'PADDLE_TRAINER_ID': str(r), 'PADDLE_TRAINERS_NUM': str(n),
+                    'PADDLE_TRAINER_ENDPOINTS': eps, 'PADDLE_CURRENT_ENDPOINT': eps.split(',')[r],
+                    'FLAGS_selected_gpus': str(d)})
+        log = open(os.path.join(a.log_dir, f'workerlog.{r}'), 'w')
+        cmd = [sys.executable, '-u', a.training_script] + a.training_script_args
+        procs.append((subprocess.Popen(cmd, env=env, stdout=log if r else None,
+                                       stderr=subprocess.STDOUT if r else None), log))
+    code = 0
+    try:
+        while procs:
+            for p, log in list(procs):
+                rc = p.poll()
+                if rc is None:
+                    continue
+                procs.remove((p, log))
+                log.close()
+                if rc != 0 and code == 0:
+                    code = rc
+                    for q, _ in procs:  # a failed rank takes the job down
+                        q.send_signal(signal.SIGTERM)
+            time.sleep(0.2)
+    except KeyboardInterrupt:
+        for q, _ in procs:
+            q.send_signal(signal.SIGTERM)
+        code = 130
+    sys.exit(code)

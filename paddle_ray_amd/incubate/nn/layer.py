@@ -1,0 +1,165 @@
+"""Fused layer classes (parity: python/paddle/incubate/nn/layer/*)."""
+import math
+
+from ...nn.layer.layers import Layer
+from ...nn import initializer as I
+from . import functional as FF
+
+
+class FusedLinear(Layer):
+    def __init__(self, in_features, out_features, weight_attr=None, bias_attr=None,
+                 transpose_weight=False, name=None):
+        super().__init__()
+        shape = [out_features, in_features] if transpose_weight else [in_features, out_features]
+        self.weight = self.create_parameter(shape, weight_attr)
+        self.bias = self.create_parameter([out_features], bias_attr, is_bias=True)
+        self.transpose_weight = transpose_weight
+
+    def forward(self, x):
+        return FF.fused_linear(x, self.weight, self.bias, self.transpose_weight)
+
+
+class FusedDropoutAdd(Layer):
+    def __init__(self, p=0.5, mode="upscale_in_train", name=None):
+        super().__init__()
+        self.p, self.mode = p, mode
+
+    def forward(self, x, y):
+        return FF.fused_dropout_add(x, y, self.p, self.training, self.mode)
+
+
+class FusedBiasDropoutResidualLayerNorm(Layer):
+    def __init__(self, embed_dim, dropout_rate=0.5, weight_attr=None, bias_attr=None,
+                 epsilon=1e-5, name=None):
+        super().__init__()
+        self.linear_bias = self.create_parameter([embed_dim], bias_attr, is_bias=True)
+        self.ln_scale = self.create_parameter([embed_dim], weight_attr,
+                                              default_initializer=I.Constant(1.0))
+        self.ln_bias = self.create_parameter([embed_dim], bias_attr, is_bias=True)
+        self.dropout_rate, self.epsilon = dropout_rate, epsilon
+
+    def forward(self, x, residual):
+        return FF.fused_bias_dropout_residual_layer_norm(x, residual, self.linear_bias,
+                                                         self.ln_scale, self.ln_bias,
+                                                         self.dropout_rate, self.epsilon,
+                                                         self.training)
+
+
+class FusedMultiHeadAttention(Layer):
+    def __init__(self, embed_dim, num_heads, dropout_rate=0.5, attn_dropout_rate=0.5, kdim=None,
+                 vdim=None, normalize_before=False, need_weights=False, qkv_weight_attr=None,
+                 qkv_bias_attr=None, linear_weight_attr=None, linear_bias_attr=None,
+                 pre_ln_scale_attr=None, pre_ln_bias_attr=None, ln_scale_attr=None,
+                 ln_bias_attr=None, epsilon=1e-5, nranks=1, ring_id=-1, transpose_qkv_wb=False,
+                 name=None):
+        super().__init__()
+        self.embed_dim, self.num_heads = embed_dim, num_heads
+        self.head_dim = embed_dim // num_heads
+        self.normalize_before, self.epsilon = normalize_before, epsilon
+        self.dropout_rate, self.attn_dropout_rate = dropout_rate, attn_dropout_rate
+        self.transpose_qkv_wb = transpose_qkv_wb
+        qshape = [embed_dim, 3 * embed_dim] if transpose_qkv_wb else \
+            [3, num_heads, self.head_dim, embed_dim]
+        self.qkv_weight = self.create_parameter(qshape, qkv_weight_attr)
+        self.qkv_bias = self.create_parameter([3 * embed_dim] if transpose_qkv_wb else
+                                              [3, num_heads, self.head_dim], qkv_bias_attr,
+                                              is_bias=True)
+        self.linear_weight = self.create_parameter([embed_dim, embed_dim], linear_weight_attr)
+        self.linear_bias = self.create_parameter([embed_dim], linear_bias_attr, is_bias=True)
+        one = I.Constant(1.0)
+        self.pre_ln_scale = self.create_parameter([embed_dim], pre_ln_scale_attr,
+                                                  default_initializer=one)
+        self.pre_ln_bias = self.create_parameter([embed_dim], pre_ln_bias_attr, is_bias=True)
+        self.ln_scale = self.create_parameter([embed_dim], ln_scale_attr, default_initializer=one)
+        self.ln_bias = self.create_parameter([embed_dim], ln_bias_attr, is_bias=True)
+
+    def forward(self, query, key=None, value=None, attn_mask=None, cache=None):
+        return FF.fused_multi_head_attention(
+            query, self.qkv_weight, self.linear_weight, self.normalize_before, self.pre_ln_scale,
+            self.pre_ln_bias, self.ln_scale, self.ln_bias, self.epsilon, self.qkv_bias,
+            self.linear_bias, cache, attn_mask, self.dropout_rate, self.attn_dropout_rate,
+            self.epsilon, self.training, num_heads=self.num_heads,
+            transpose_qkv_wb=self.transpose_qkv_wb)
+
+
+class FusedFeedForward(Layer):
+    def __init__(self, d_model, dim_feedforward, dropout_rate=0.1, epsilon=1e-05,
+                 activation="relu", act_dropout_rate=None, normalize_before=False,
+                 linear1_weight_attr=None, linear1_bias_attr=None, linear2_weight_attr=None,
+                 linear2_bias_attr=None, ln1_scale_attr=None, ln1_bias_attr=None,
+                 ln2_scale_attr=None, ln2_bias_attr=None, nranks=1, ring_id=-1, name=None):
+        super().__init__()
+        self.dropout_rate = dropout_rate
+        self.act_dropout_rate = dropout_rate if act_dropout_rate is None else act_dropout_rate
+        self.activation, self.normalize_before, self.epsilon = activation, normalize_before, \
+            epsilon
+        self.linear1_weight = self.create_parameter([d_model, dim_feedforward], linear1_weight_attr)
+        self.linear1_bias = self.create_parameter([dim_feedforward], linear1_bias_attr,
+                                                  is_bias=True)
+        self.linear2_weight = self.create_parameter([dim_feedforward, d_model], linear2_weight_attr)
+        self.linear2_bias = self.create_parameter([d_model], linear2_bias_attr, is_bias=True)
+        one = I.Constant(1.0)
+        self.ln1_scale = self.create_parameter([d_model], ln1_scale_attr, default_initializer=one)
+        self.ln1_bias = self.create_parameter([d_model], ln1_bias_attr, is_bias=True)
+        self.ln2_scale = self.create_parameter([d_model], ln2_scale_attr, default_initializer=one)
+        self.ln2_bias = self.create_parameter([d_model], ln2_bias_attr, is_bias=True)
+
+    def forward(self, src, cache=None):
+        return FF.fused_feedforward(src, self.linear1_weight, self.linear2_weight,
+                                    self.linear1_bias, self.linear2_bias, self.ln1_scale,
+                                    self.ln1_bias, self.ln2_scale, self.ln2_bias,
+                                    self.act_dropout_rate, self.dropout_rate, self.activation,
+                                    self.epsilon, self.epsilon, self.normalize_before,
+                                    self.training)
+
+
+class FusedTransformerEncoderLayer(Layer):
+    def __init__(self, d_model, nhead, dim_feedforward, dropout_rate=0.1, activation="relu",
+                 attn_dropout_rate=None, act_dropout_rate=None, normalize_before=False,
+                 weight_attr=None, bias_attr=None):
+        super().__init__()
+        adr = dropout_rate if attn_dropout_rate is None else attn_dropout_rate
+        self.fused_attn = FusedMultiHeadAttention(d_model, nhead, dropout_rate, adr,
+                                                  normalize_before=normalize_before)
+        self.ffn = FusedFeedForward(d_model, dim_feedforward, dropout_rate, activation=activation,
+                                    act_dropout_rate=act_dropout_rate,
+                                    normalize_before=normalize_before)
+
+    def forward(self, src, src_mask=None, cache=None):
+        return self.ffn(self.fused_attn(src, attn_mask=src_mask))
+
+
+class FusedMultiTransformer(Layer):
+    def __init__(self, embed_dim, num_heads, dim_feedforward, dropout_rate=0.0, activation="gelu",
+                 normalize_before=True, num_layers=1, epsilon=1e-5, **kw):
+        super().__init__()
+        self.layers = [FusedTransformerEncoderLayer(embed_dim, num_heads, dim_feedforward,
+                                                    dropout_rate, activation,
+                                                    normalize_before=normalize_before)
+                       for _ in range(num_layers)]
+        for i, l in enumerate(self.layers):
+            self.add_sublayer(str(i), l)
+
+    def forward(self, src, attn_mask=None, caches=None, time_step=None):
+        for l in self.layers:
+            src = l(src, attn_mask)
+        return src
+
+
+class FusedEcMoe(Layer):
+    def __init__(self, hidden_size, inter_size, num_experts, act_type, weight_attr=None,
+                 bias_attr=None):
+        super().__init__()
+        self.bmm_weight0 = self.create_parameter([num_experts, hidden_size, inter_size],
+                                                 weight_attr)
+        self.bmm_bias0 = self.create_parameter([num_experts, 1, inter_size], bias_attr,
+                                               is_bias=True)
+        self.bmm_weight1 = self.create_parameter([num_experts, inter_size, hidden_size],
+                                                 weight_attr)
+        self.bmm_bias1 = self.create_parameter([num_experts, 1, hidden_size], bias_attr,
+                                               is_bias=True)
+        self.act_type = act_type
+
+    def forward(self, x, gate):
+        return FF.fused_ec_moe(x, gate, self.bmm_weight0, self.bmm_bias0, self.bmm_weight1,
+                               self.bmm_bias1, self.act_type)

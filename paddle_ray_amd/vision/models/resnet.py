@@ -1,0 +1,174 @@
+"""ResNet family (parity: python/paddle/vision/models/resnet.py).
+
+``data_format='NHWC'`` keeps activations channels-last end to end, the layout
+MIOpen's fast bf16 conv kernels want on MI355X (no NCHW<->NHWC transposes).
+"""
+from ... import nn
+
+
+class BasicBlock(nn.Layer):
+    expansion = 1
+
+    def __init__(self, inplanes, planes, stride=1, downsample=None, groups=1, base_width=64,
+                 dilation=1, norm_layer=None, data_format='NCHW'):
+        super().__init__()
+        norm_layer = norm_layer or nn.BatchNorm2D
+        df = data_format
+        self.conv1 = nn.Conv2D(inplanes, planes, 3, padding=1, stride=stride, bias_attr=False,
+                               data_format=df)
+        self.bn1 = norm_layer(planes, data_format=df)
+        self.relu = nn.ReLU()
+        self.conv2 = nn.Conv2D(planes, planes, 3, padding=1, bias_attr=False, data_format=df)
+        self.bn2 = norm_layer(planes, data_format=df)
+        self.downsample = downsample
+        self.stride = stride
+
+    def forward(self, x):
+        identity = x
+        out = self.relu(self.bn1(self.conv1(x)))
+        out = self.bn2(self.conv2(out))
+        if self.downsample is not None:
+            identity = self.downsample(x)
+        return self.relu(out + identity)
+
+
+class BottleneckBlock(nn.Layer):
+    expansion = 4
+
+    def __init__(self, inplanes, planes, stride=1, downsample=None, groups=1, base_width=64,
+                 dilation=1, norm_layer=None, data_format='NCHW'):
+        super().__init__()
+        norm_layer = norm_layer or nn.BatchNorm2D
+        df = data_format
+        width = int(planes * (base_width / 64.)) * groups
+        self.conv1 = nn.Conv2D(inplanes, width, 1, bias_attr=False, data_format=df)
+        self.bn1 = norm_layer(width, data_format=df)
+        self.conv2 = nn.Conv2D(width, width, 3, padding=dilation, stride=stride, groups=groups,
+                               dilation=dilation, bias_attr=False, data_format=df)
+        self.bn2 = norm_layer(width, data_format=df)
+        self.conv3 = nn.Conv2D(width, planes * self.expansion, 1, bias_attr=False, data_format=df)
+        self.bn3 = norm_layer(planes * self.expansion, data_format=df)
+        self.relu = nn.ReLU()
+        self.downsample = downsample
+        self.stride = stride
+
+    def forward(self, x):
+        identity = x
+        out = self.relu(self.bn1(self.conv1(x)))
+        out = self.relu(self.bn2(self.conv2(out)))
+        out = self.bn3(self.conv3(out))
+        if self.downsample is not None:
+            identity = self.downsample(x)
+        return self.relu(out + identity)
+
+
+class ResNet(nn.Layer):
+    def __init__(self, block, depth=50, width=64, num_classes=1000, with_pool=True, groups=1,
+                 data_format='NCHW'):
+        super().__init__()
+        layer_cfg = {18: [2, 2, 2, 2], 34: [3, 4, 6, 3], 50: [3, 4, 6, 3], 101: [3, 4, 23, 3],
+                     152: [3, 8, 36, 3]}
+        layers = layer_cfg[depth]
+        self.groups, self.base_width = groups, width
+        self.num_classes, self.with_pool = num_classes, with_pool
+        self._norm_layer = nn.BatchNorm2D
+        self.data_format = df = data_format
+        self.inplanes, self.dilation = 64, 1
+        self.conv1 = nn.Conv2D(3, self.inplanes, 7, stride=2, padding=3, bias_attr=False,
+                               data_format=df)
+        self.bn1 = self._norm_layer(self.inplanes, data_format=df)
+        self.relu = nn.ReLU()
+        self.maxpool = nn.MaxPool2D(3, stride=2, padding=1, data_format=df)
+        self.layer1 = self._make_layer(block, 64, layers[0])
+        self.layer2 = self._make_layer(block, 128, layers[1], stride=2)
+        self.layer3 = self._make_layer(block, 256, layers[2], stride=2)
+        self.layer4 = self._make_layer(block, 512, layers[3], stride=2)
+        if with_pool:
+            self.avgpool = nn.AdaptiveAvgPool2D((1, 1), data_format=df)
+        if num_classes > 0:
+            self.fc = nn.Linear(512 * block.expansion, num_classes)
+
+    def _make_layer(self, block, planes, blocks, stride=1, dilate=False):
+        df = self.data_format
+        downsample = None
+        if stride != 1 or self.inplanes != planes * block.expansion:
+            downsample = nn.Sequential(
+                nn.Conv2D(self.inplanes, planes * block.expansion, 1, stride=stride,
+                          bias_attr=False, data_format=df),
+                self._norm_layer(planes * block.expansion, data_format=df))
+        layers = [block(self.inplanes, planes, stride, downsample, self.groups, self.base_width,
+                        1, self._norm_layer, df)]
+        self.inplanes = planes * block.expansion
+        for _ in range(1, blocks):
+            layers.append(block(self.inplanes, planes, groups=self.groups,
+                                base_width=self.base_width, norm_layer=self._norm_layer,
+                                data_format=df))
+        return nn.Sequential(*layers)
+
+    def forward(self, x):
+        x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
+        x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
+        if self.with_pool:
+            x = self.avgpool(x)
+        if self.num_classes > 0:
+            x = x.flatten(1)
+            x = self.fc(x)
+        return x
+
+
+def _resnet(block, depth, pretrained=False, **kw):
+    if pretrained:
+        raise ValueError("pretrained weights are not downloadable in this environment")
+    return ResNet(block, depth, **kw)
+
+
+def resnet18(pretrained=False, **kw):
+    return _resnet(BasicBlock, 18, pretrained, **kw)
+
+
+def resnet34(pretrained=False, **kw):
+    return _resnet(BasicBlock, 34, pretrained, **kw)
+
+
+def resnet50(pretrained=False, **kw):
+    return _resnet(BottleneckBlock, 50, pretrained, **kw)
+
+
+def resnet101(pretrained=False, **kw):
+    return _resnet(BottleneckBlock, 101, pretrained, **kw)
+
+
+def resnet152(pretrained=False, **kw):
+    return _resnet(BottleneckBlock, 152, pretrained, **kw)
+
+
+def resnext50_32x4d(pretrained=False, **kw):
+    return _resnet(BottleneckBlock, 50, pretrained, groups=32, width=4, **kw)
+
+
+def resnext50_64x4d(pretrained=False, **kw):
+    return _resnet(BottleneckBlock, 50, pretrained, groups=64, width=4, **kw)
+
+
+def resnext101_32x4d(pretrained=False, **kw):
+    return _resnet(BottleneckBlock, 101, pretrained, groups=32, width=4, **kw)
+
+
+def resnext101_64x4d(pretrained=False, **kw):
+    return _resnet(BottleneckBlock, 101, pretrained, groups=64, width=4, **kw)
+
+
+def resnext152_32x4d(pretrained=False, **kw):
+    return _resnet(BottleneckBlock, 152, pretrained, groups=32, width=4, **kw)
+
+
+def resnext152_64x4d(pretrained=False, **kw):
+    return _resnet(BottleneckBlock, 152, pretrained, groups=64, width=4, **kw)
+
+
+def wide_resnet50_2(pretrained=False, **kw):
+    return _resnet(BottleneckBlock, 50, pretrained, width=128, **kw)
+
+
+def wide_resnet101_2(pretrained=False, **kw):
+    return _resnet(BottleneckBlock, 101, pretrained, width=128, **kw)
