@@ -106,6 +106,22 @@ class GPTAttention(nn.Layer):
             self.out_proj = nn.Linear(h, h, nn.ParamAttr(initializer=out_init))
         self.attn_dropout = cfg.attention_dropout
 
+    def _core(self, x):
+        qkv = _u(self.qkv_proj(x))
+        B, S = qkv.shape[0], qkv.shape[1]
+        qkv = qkv.view(B, S, 3, self.num_heads, self.head_dim)
+        if self.attn_dropout > 0 and self.training:
+            q, k, v = qkv.unbind(2)
+            o = F.scaled_dot_product_attention(Tensor(q), Tensor(k), Tensor(v), None,
+                                               self.attn_dropout, True, True)._t
+        else:
+            o = K.flash_attention_qkvpacked(qkv, causal=True)
+        return o.reshape(B, S, self.num_heads * self.head_dim)
+
+    def forward_nobias(self, x):
+        """attention output projection WITHOUT its bias (fused into the next kernel)."""
+        return Tensor(torch.matmul(self._core(x), self.out_proj.weight._t))
+
     def forward(self, x):
         qkv = _u(self.qkv_proj(x))
         B, S = qkv.shape[0], qkv.shape[1]
@@ -138,6 +154,11 @@ class GPTMLP(nn.Layer):
             self.fc2 = nn.Linear(f, h, nn.ParamAttr(initializer=out_init))
             self._fused = True
 
+    def forward_nobias(self, x):
+        t = _u(x)
+        hdn = K.bias_gelu(torch.matmul(t, self.fc1.weight._t), self.fc1.bias._t, self.approx)
+        return Tensor(torch.matmul(hdn, self.fc2.weight._t))
+
     def forward(self, x):
         if self._fused:
             # GEMM without bias, then the fused bias+GELU HIP kernel (one pass over [T, 4h])
@@ -156,6 +177,8 @@ class GPTBlock(nn.Layer):
         self.ln2 = nn.LayerNorm(cfg.hidden_size, cfg.layer_norm_eps)
         self.mlp = GPTMLP(cfg)
         self.p = cfg.hidden_dropout
+        self.eps = cfg.layer_norm_eps
+        self.fused = cfg.mp_degree == 1
 
     def _drop(self, t):
         if self.p > 0 and self.training:
@@ -163,10 +186,22 @@ class GPTBlock(nn.Layer):
         return t
 
     def forward(self, x):
+        """Unfused reference path: x -> x + attn(ln1 x) -> + mlp(ln2 .)"""
         t = _u(x)
         t = t + self._drop(_u(self.attn(self.ln1(Tensor(t)))))
         t = t + self._drop(_u(self.mlp(self.ln2(Tensor(t)))))
         return Tensor(t)
+
+    def forward_fused(self, r, y, next_ln):
+        """(r, y=ln1(r)) -> (r', next_ln(r')) with both residual adds, dropouts, out-proj /
+        fc2 bias-adds and the following LayerNorms done by the fused HIP kernel."""
+        p = self.p if self.training else 0.0
+        a = _u(self.attn.forward_nobias(Tensor(y)))
+        r1, y1 = K.add_dropout_layer_norm(r, a, self.attn.out_proj.bias._t, self.ln2.weight._t,
+                                          self.ln2.bias._t, p, self.eps)
+        m = _u(self.mlp.forward_nobias(Tensor(y1)))
+        return K.add_dropout_layer_norm(r1, m, self.mlp.fc2.bias._t, next_ln.weight._t,
+                                        next_ln.bias._t, p, self.eps)
 
 
 class GPTModel(nn.Layer):
@@ -179,12 +214,27 @@ class GPTModel(nn.Layer):
 
     def forward(self, input_ids, position_ids=None):
         x = self.embeddings(input_ids, position_ids)
+        blocks = list(self.layers)
+        if blocks and blocks[0].fused:
+            r = _u(x)
+            y = _u(blocks[0].ln1(x))
+            for i, blk in enumerate(blocks):
+                nxt = blocks[i + 1].ln1 if i + 1 < len(blocks) else self.final_norm
+                if self.cfg.recompute and self.training:
+                    from ..parallel.recompute import recompute
+                    r, y = recompute(lambda a, b, blk=blk, nxt=nxt: tuple(
+                        Tensor(t) for t in blk.forward_fused(_u(a), _u(b), nxt)),
+                        Tensor(r), Tensor(y))
+                    r, y = _u(r), _u(y)
+                else:
+                    r, y = blk.forward_fused(r, y, nxt)
+            return Tensor(y)
         if self.cfg.recompute and self.training:
             from ..parallel.recompute import recompute
-            for blk in self.layers:
+            for blk in blocks:
                 x = recompute(blk, x)
         else:
-            for blk in self.layers:
+            for blk in blocks:
                 x = blk(x)
         return self.final_norm(x)
 

@@ -3,6 +3,8 @@
 // Python side pays one pybind11 call per launch and no tensor marshalling.
 #include <hip/hip_runtime.h>
 #include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+#include <vector>
 #include <stdint.h>
 #include <stdexcept>
 #include <string>
@@ -31,6 +33,12 @@ void pra_adamw_mt(const int64_t*, const float*, const int64_t*, int, float, floa
 void pra_momentum_mt(const int64_t*, const float*, const int64_t*, int, float, float, int, float, hipStream_t);
 void pra_sumsq_accum(const void*, float*, int64_t, int, hipStream_t);
 void pra_flash_bwd_pre(const void*, const void*, float*, int, int, int, int, int, hipStream_t);
+int pra_adl_supported(int);
+void pra_adl_fwd(const void*, const void*, const void*, const void*, const void*, void*, void*, float*, float*, int,
+                 int, float, float, uint64_t, uint64_t, int, int, hipStream_t);
+void pra_adl_bwd(const void*, const void*, const void*, const void*, const float*, const float*, void*, void*, float*,
+                 float*, float*, int, int, int, float, uint64_t, uint64_t, int, int, hipStream_t);
+void pra_colsum16(const float*, void*, int, int, int, hipStream_t);
 int pra_flash_fwd(const void*, const void*, const void*, void*, float*, int, int, int, int, int, const int64_t*, float,
                   int, int, hipStream_t);
 int pra_flash_bwd(const void*, const void*, const void*, const void*, const float*, const float*, void*, void*, void*,
@@ -109,6 +117,23 @@ PYBIND11_MODULE(_pra_hip, m) {
     pra_sumsq_accum(CV(x), F(out), n, dt, S(s));
     check_launch("sumsq_accum");
   });
+  m.def("adl_supported", [](int cols) { return pra_adl_supported(cols); });
+  m.def("adl_fwd", [](P x, P h, P hb, P w, P b, P r, P y, P mean, P rstd, int rows, int cols, float eps, float p,
+                      uint64_t seed, uint64_t off, int dt, int dtw, P s) {
+    pra_adl_fwd(CV(x), CV(h), CV(hb), CV(w), CV(b), V(r), V(y), F(mean), F(rstd), rows, cols, eps, p, seed, off, dt,
+                dtw, S(s));
+    check_launch("adl_fwd");
+  });
+  m.def("adl_bwd", [](P dy, P dro, P r, P w, P mean, P rstd, P dri, P dh, P pw, P pb, P pbias, int rows, int cols,
+                      int nblk, float p, uint64_t seed, uint64_t off, int dt, int dtw, P s) {
+    pra_adl_bwd(CV(dy), CV(dro), CV(r), CV(w), CF(mean), CF(rstd), V(dri), V(dh), F(pw), F(pb), F(pbias), rows, cols,
+                nblk, p, seed, off, dt, dtw, S(s));
+    check_launch("adl_bwd");
+  });
+  m.def("colsum16", [](P part, P out, int nblk, int cols, int dt, P s) {
+    pra_colsum16(CF(part), V(out), nblk, cols, dt, S(s));
+    check_launch("colsum16");
+  });
   m.def("flash_bwd_pre", [](P o, P dO, P delta, int B, int H, int Sq, int D, int dt, P s) {
     pra_flash_bwd_pre(CV(o), CV(dO), F(delta), B, H, Sq, D, dt, S(s));
     check_launch("flash_bwd_pre");
@@ -122,11 +147,10 @@ PYBIND11_MODULE(_pra_hip, m) {
     check_launch("flash_fwd");
   });
   m.def("flash_bwd", [](P q, P k, P v, P dO, P lse, P delta, P dq, P dk, P dv, int B, int H, int Sq, int Sk, int D,
-                        int64_t qsb, int64_t qss, int64_t qsh, int64_t ksb, int64_t kss, int64_t ksh, int64_t vsb,
-                        int64_t vss, int64_t vsh, float scale, int causal, int dt, P s) {
-    int64_t st[9] = {qsb, qss, qsh, ksb, kss, ksh, vsb, vss, vsh};
-    if (pra_flash_bwd(CV(q), CV(k), CV(v), CV(dO), CF(lse), CF(delta), V(dq), V(dk), V(dv), B, H, Sq, Sk, D, st, scale,
-                      causal, dt, S(s)) != 0)
+                        std::vector<int64_t> st, float scale, int causal, int dt, P s) {
+    if (st.size() != 18) throw std::invalid_argument("flash_bwd: need 18 strides");
+    if (pra_flash_bwd(CV(q), CV(k), CV(v), CV(dO), CF(lse), CF(delta), V(dq), V(dk), V(dv), B, H, Sq, Sk, D, st.data(),
+                      scale, causal, dt, S(s)) != 0)
       throw std::invalid_argument("flash_bwd: unsupported head_dim/dtype");
     check_launch("flash_bwd");
   });

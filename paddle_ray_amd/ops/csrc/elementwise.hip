@@ -142,6 +142,23 @@ __global__ void __launch_bounds__(256) momentum_mt_k(const int64_t* __restrict__
 }
 
 template <typename T>
+__global__ void __launch_bounds__(256) sumsq_vec_k(const T* __restrict__ x, float* __restrict__ out, size_t n) {
+  __shared__ float red[16];
+  float s = 0.f;
+  const size_t nv = n / 8;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < nv; i += (size_t)gridDim.x * blockDim.x) {
+    float v[8];
+    load8<T>(x + i * 8, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s += v[j] * v[j];
+  }
+  if (blockIdx.x == 0)
+    for (size_t i = nv * 8 + threadIdx.x; i < n; i += blockDim.x) { float v = Cvt<T>::to(x[i]); s += v * v; }
+  s = block_sum(s, red);
+  if (threadIdx.x == 0) atomicAdd(out, s);
+}
+
+template <typename T>
 __global__ void __launch_bounds__(256) sumsq_k(const T* __restrict__ x, float* __restrict__ out, size_t n) {
   __shared__ float red[16];
   float s = 0.f;
@@ -220,8 +237,15 @@ void pra_momentum_mt(const int64_t* tab, const float* ftab, const int64_t* chunk
 }
 void pra_sumsq_accum(const void* x, float* out, int64_t n, int dt, hipStream_t s) {
   if (!n) return;
-  PRA_DISPATCH_FLOAT(dt, T, hipLaunchKernelGGL((sumsq_k<T>), dim3(grid_for(n) > 1024 ? 1024 : grid_for(n)),
-                                               dim3(256), 0, s, (const T*)x, out, (size_t)n));
+  if (((uintptr_t)x & 15) == 0) {
+    int g = grid_for((size_t)n / 8);
+    if (g > 2048) g = 2048;
+    PRA_DISPATCH_FLOAT(dt, T, hipLaunchKernelGGL((sumsq_vec_k<T>), dim3(g), dim3(256), 0, s, (const T*)x, out,
+                                                 (size_t)n));
+  } else {
+    PRA_DISPATCH_FLOAT(dt, T, hipLaunchKernelGGL((sumsq_k<T>), dim3(grid_for(n) > 1024 ? 1024 : grid_for(n)),
+                                                 dim3(256), 0, s, (const T*)x, out, (size_t)n));
+  }
 }
 void pra_flash_bwd_pre(const void* o, const void* dO, float* delta, int B, int H, int S, int D, int dt,
                        hipStream_t s) {

@@ -306,7 +306,7 @@ __global__ void __launch_bounds__(256, 1)
 bwd_dq_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restrict__ v, const T* __restrict__ dO,
               const float* __restrict__ lse, const float* __restrict__ delta, T* __restrict__ dq, int H, int Sq,
               int Sk, int64_t qsb, int64_t qss, int64_t qsh, int64_t ksb, int64_t kss, int64_t ksh, int64_t vsb,
-              int64_t vss, int64_t vsh, float scale, float scale_log2) {
+              int64_t vss, int64_t vsh, int64_t dqsb, int64_t dqss, int64_t dqsh, float scale, float scale_log2) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   T* Ks = reinterpret_cast<T*>(smem);
   T* Vs = Ks + Geo<D>::ROW_IMG;
@@ -405,7 +405,7 @@ bwd_dq_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restr
   }
 
   if (qvalid) {
-    T* row = dq + ((int64_t)b * Sq + myq) * HD + (int64_t)hh * D;
+    T* row = dq + (int64_t)b * dqsb + (int64_t)myq * dqss + (int64_t)hh * dqsh;
 #pragma unroll
     for (int dt = 0; dt < ND; ++dt)
 #pragma unroll
@@ -430,7 +430,8 @@ __global__ void __launch_bounds__(256, 1)
 bwd_dkdv_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restrict__ v, const T* __restrict__ dO,
                 const float* __restrict__ lse, const float* __restrict__ delta, T* __restrict__ dk,
                 T* __restrict__ dv, int H, int Sq, int Sk, int64_t qsb, int64_t qss, int64_t qsh, int64_t ksb,
-                int64_t kss, int64_t ksh, int64_t vsb, int64_t vss, int64_t vsh, float scale, float scale_log2) {
+                int64_t kss, int64_t ksh, int64_t vsb, int64_t vss, int64_t vsh, int64_t dksb, int64_t dkss,
+                int64_t dksh, int64_t dvsb, int64_t dvss, int64_t dvsh, float scale, float scale_log2) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   T* Qs = reinterpret_cast<T*>(smem);
   T* Qt = Qs + Geo<D>::ROW_IMG;
@@ -545,8 +546,8 @@ bwd_dkdv_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __res
   }
 
   if (kvalid) {
-    T* krow = dk + ((int64_t)b * Sk + mykey) * HD + (int64_t)hh * D;
-    T* vrow = dv + ((int64_t)b * Sk + mykey) * HD + (int64_t)hh * D;
+    T* krow = dk + (int64_t)b * dksb + (int64_t)mykey * dkss + (int64_t)hh * dksh;
+    T* vrow = dv + (int64_t)b * dvsb + (int64_t)mykey * dvss + (int64_t)hh * dvsh;
 #pragma unroll
     for (int dt = 0; dt < ND; ++dt)
 #pragma unroll
@@ -585,7 +586,7 @@ static void launch_bwd(const void* q, const void* k, const void* v, const void* 
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(kern, dim3((Sq + 127) / 128, B * H), dim3(256), lds, s, (const T*)q, (const T*)k,
                        (const T*)v, (const T*)dO, lse, delta, (T*)dq, H, Sq, Sk, st[0], st[1], st[2], st[3], st[4],
-                       st[5], st[6], st[7], st[8], scale, sl2);
+                       st[5], st[6], st[7], st[8], st[9], st[10], st[11], scale, sl2);
   }
   {
     const size_t lds = (2 * Geo<D>::ROW_IMG + 2 * Geo<D>::TR_IMG) * sizeof(T) + 2 * kTile * sizeof(float);
@@ -593,7 +594,8 @@ static void launch_bwd(const void* q, const void* k, const void* v, const void* 
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(kern, dim3((Sk + 127) / 128, B * H), dim3(256), lds, s, (const T*)q, (const T*)k,
                        (const T*)v, (const T*)dO, lse, delta, (T*)dk, (T*)dv, H, Sq, Sk, st[0], st[1], st[2],
-                       st[3], st[4], st[5], st[6], st[7], st[8], scale, sl2);
+                       st[3], st[4], st[5], st[6], st[7], st[8], st[12], st[13], st[14], st[15], st[16], st[17],
+                       scale, sl2);
   }
 }
 

@@ -66,6 +66,14 @@ def _colsum_nblk(rows):
     return max(1, min(rows, 256))
 
 
+def _adl_ok(cols):
+    return cols % 8 == 0 and cols <= 4096
+
+
+def _adl_nblk(rows):
+    return max(1, min(512, (rows + 7) // 8))
+
+
 @R.register_kernel('layer_norm_fwd', 'hip')
 def _ln_fwd_hip(x2, w, b, eps):
     L = _native.lib()
@@ -73,8 +81,13 @@ def _ln_fwd_hip(x2, w, b, eps):
     y = torch.empty_like(x2)
     mean = torch.empty(rows, device=x2.device, dtype=torch.float32)
     rstd = torch.empty(rows, device=x2.device, dtype=torch.float32)
-    L.layernorm_fwd(_ptr(x2), _ptr(w), _ptr(b), _ptr(y), _ptr(mean), _ptr(rstd), rows, cols,
-                    float(eps), _dt(x2), _dt(w) if w is not None else _dt(x2), _stream())
+    dtw = _dt(w) if w is not None else _dt(x2)
+    if _adl_ok(cols):
+        L.adl_fwd(_ptr(x2), 0, 0, _ptr(w), _ptr(b), 0, _ptr(y), _ptr(mean), _ptr(rstd), rows, cols,
+                  float(eps), 0.0, 0, 0, _dt(x2), dtw, _stream())
+    else:
+        L.layernorm_fwd(_ptr(x2), _ptr(w), _ptr(b), _ptr(y), _ptr(mean), _ptr(rstd), rows, cols,
+                        float(eps), _dt(x2), dtw, _stream())
     return y, mean, rstd
 
 
@@ -83,19 +96,30 @@ def _ln_bwd_hip(dy, x2, w, mean, rstd, need_dw, need_db):
     L = _native.lib()
     rows, cols = x2.shape
     dx = torch.empty_like(x2)
-    nblk = _colsum_nblk(rows)
-    part = torch.empty((2, nblk, cols), device=x2.device, dtype=torch.float32)
-    L.layernorm_bwd(_ptr(dy.contiguous()), _ptr(x2), _ptr(w), _ptr(mean), _ptr(rstd), _ptr(dx),
-                    _ptr(part[0]), _ptr(part[1]), rows, cols, nblk, _dt(x2),
-                    _dt(w) if w is not None else _dt(x2), _stream())
-    dw = db = None
     pdt = w.dtype if w is not None else x2.dtype
+    dtw = _dt(w) if w is not None else _dt(x2)
+    dy = dy.contiguous()
+    if _adl_ok(cols):
+        nblk = _adl_nblk(rows)
+        part = torch.empty((2, nblk, cols), device=x2.device, dtype=torch.float32)
+        L.adl_bwd(_ptr(dy), 0, _ptr(x2), _ptr(w), _ptr(mean), _ptr(rstd), _ptr(dx), 0,
+                  _ptr(part[0]) if (need_dw and w is not None) else 0,
+                  _ptr(part[1]) if need_db else 0, 0, rows, cols, nblk, 0.0, 0, 0, _dt(x2), dtw,
+                  _stream())
+        red = L.colsum16
+    else:
+        nblk = _colsum_nblk(rows)
+        part = torch.empty((2, nblk, cols), device=x2.device, dtype=torch.float32)
+        L.layernorm_bwd(_ptr(dy), _ptr(x2), _ptr(w), _ptr(mean), _ptr(rstd), _ptr(dx),
+                        _ptr(part[0]), _ptr(part[1]), rows, cols, nblk, _dt(x2), dtw, _stream())
+        red = L.colsum
+    dw = db = None
     if need_dw and w is not None:
         dw = torch.empty(cols, device=x2.device, dtype=pdt)
-        L.colsum(_ptr(part[0]), _ptr(dw), nblk, cols, _DT[pdt], _stream())
+        red(_ptr(part[0]), _ptr(dw), nblk, cols, _DT[pdt], _stream())
     if need_db:
         db = torch.empty(cols, device=x2.device, dtype=pdt)
-        L.colsum(_ptr(part[1]), _ptr(db), nblk, cols, _DT[pdt], _stream())
+        red(_ptr(part[1]), _ptr(db), nblk, cols, _DT[pdt], _stream())
     return dx, dw, db
 
 
@@ -122,6 +146,134 @@ class LayerNormFn(torch.autograd.Function):
 
 def layer_norm(x, w, b, eps=1e-5):
     return LayerNormFn.apply(x, w, b, eps)
+
+
+# =============================================================================
+# Fused residual add + dropout(+bias) + LayerNorm:  r = x + drop(h + hb);  y = LN(r)
+# =============================================================================
+def _dropout_seed():
+    # drawn from the host generator: follows paddle.seed and recompute's RNG restore
+    return int(torch.randint(0, 2 ** 62, (1,)).item())
+
+
+def _hash_keep_ref(n, p, seed, device):
+    """Reference of the kernel's counter-hash keep mask (for CPU + tests)."""
+    import numpy as np
+    i = np.arange(n, dtype=np.uint64)
+    c = (i >> np.uint64(1)).astype(np.uint64)
+    M = np.uint64(0xffffffff)
+
+    def mix(x):
+        x = x & M
+        x ^= x >> np.uint64(16); x = (x * np.uint64(0x7feb352d)) & M
+        x ^= x >> np.uint64(15); x = (x * np.uint64(0x846ca68b)) & M
+        x ^= x >> np.uint64(16)
+        return x
+    s = np.uint64(seed)
+    a = mix((c & M) ^ (s & M))
+    r = mix(a ^ (c >> np.uint64(32)) ^ (s >> np.uint64(32)) ^ np.uint64(0x9e3779b9))
+    u = np.where(i % np.uint64(2) == 0, r & np.uint64(0xffff), r >> np.uint64(16))
+    thr = np.uint64(int(p * 65536 + 0.5))
+    return torch.from_numpy((u >= thr).astype(np.bool_)).to(device)
+
+
+@R.register_kernel('add_dropout_ln_fwd', 'ref')
+def _adl_fwd_ref(x2, h2, hb, w, b, p, eps, seed):
+    t = h2.float() + (hb.float() if hb is not None else 0)
+    if p > 0:
+        keep = _hash_keep_ref(h2.numel(), p, seed, h2.device).view(h2.shape)
+        t = torch.where(keep, t / (1 - p), torch.zeros_like(t))
+    r = (x2.float() + t).to(x2.dtype)
+    y, mean, rstd = _ln_fwd_ref(r, w, b, eps)
+    return r, y, mean, rstd
+
+
+@R.register_kernel('add_dropout_ln_bwd', 'ref')
+def _adl_bwd_ref(dy, dr_out, r, w, mean, rstd, p, seed, need_dw, need_db, need_dhb):
+    dx, dw, db = _ln_bwd_ref(dy, r, w, mean, rstd, need_dw, need_db)
+    dri = dx.float() + (dr_out.float() if dr_out is not None else 0)
+    dh = dri
+    if p > 0:
+        keep = _hash_keep_ref(r.numel(), p, seed, r.device).view(r.shape)
+        dh = torch.where(keep, dri / (1 - p), torch.zeros_like(dri))
+    dhb = dh.sum(0).to(r.dtype) if need_dhb else None
+    return dri.to(r.dtype), dh.to(r.dtype), dw, db, dhb
+
+
+@R.register_kernel('add_dropout_ln_fwd', 'hip')
+def _adl_fwd_hip(x2, h2, hb, w, b, p, eps, seed):
+    rows, cols = x2.shape
+    if not _adl_ok(cols):
+        return _adl_fwd_ref(x2, h2, hb, w, b, p, eps, seed)
+    r = torch.empty_like(x2)
+    y = torch.empty_like(x2)
+    mean = torch.empty(rows, device=x2.device, dtype=torch.float32)
+    rstd = torch.empty(rows, device=x2.device, dtype=torch.float32)
+    _native.lib().adl_fwd(_ptr(x2), _ptr(h2), _ptr(hb), _ptr(w), _ptr(b), _ptr(r), _ptr(y),
+                          _ptr(mean), _ptr(rstd), rows, cols, float(eps), float(p), seed, 0,
+                          _dt(x2), _dt(w) if w is not None else _dt(x2), _stream())
+    return r, y, mean, rstd
+
+
+@R.register_kernel('add_dropout_ln_bwd', 'hip')
+def _adl_bwd_hip(dy, dr_out, r, w, mean, rstd, p, seed, need_dw, need_db, need_dhb):
+    rows, cols = r.shape
+    if not _adl_ok(cols):
+        return _adl_bwd_ref(dy, dr_out, r, w, mean, rstd, p, seed, need_dw, need_db, need_dhb)
+    L = _native.lib()
+    dri = torch.empty_like(r)
+    dh = torch.empty_like(r)
+    nblk = _adl_nblk(rows)
+    part = torch.empty((3, nblk, cols), device=r.device, dtype=torch.float32)
+    pdt = w.dtype if w is not None else r.dtype
+    L.adl_bwd(_ptr(dy), _ptr(dr_out), _ptr(r), _ptr(w), _ptr(mean), _ptr(rstd), _ptr(dri),
+              _ptr(dh), _ptr(part[0]) if need_dw else 0, _ptr(part[1]) if need_db else 0,
+              _ptr(part[2]) if need_dhb else 0, rows, cols, nblk, float(p), seed, 0, _dt(r),
+              _dt(w) if w is not None else _dt(r), _stream())
+    outs = []
+    for need, i, dt in ((need_dw, 0, pdt), (need_db, 1, pdt), (need_dhb, 2, r.dtype)):
+        if need:
+            o = torch.empty(cols, device=r.device, dtype=dt)
+            L.colsum16(_ptr(part[i]), _ptr(o), nblk, cols, _DT[dt], _stream())
+            outs.append(o)
+        else:
+            outs.append(None)
+    return (dri, dh) + tuple(outs)
+
+
+class AddDropoutLNFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, h, hb, w, b, p, eps):
+        shp = x.shape
+        cols = shp[-1]
+        x2 = x.contiguous().view(-1, cols)
+        h2 = h.contiguous().view(-1, cols)
+        if hb is not None and hb.dtype != x.dtype:
+            hb = hb.to(x.dtype)
+        seed = _dropout_seed() if p > 0 else 0
+        r, y, mean, rstd = R.dispatch('add_dropout_ln_fwd', x2, x2, h2, hb, w, b, p, eps, seed)
+        ctx.save_for_backward(r, w, mean, rstd)
+        ctx.p, ctx.seed, ctx.shp = p, seed, shp
+        ctx.has_b, ctx.has_hb = b is not None, hb is not None
+        return r.view(shp), y.view(shp)
+
+    @staticmethod
+    def backward(ctx, g_r, g_y):
+        r, w, mean, rstd = ctx.saved_tensors
+        cols = ctx.shp[-1]
+        if g_y is None:
+            g_y = torch.zeros_like(r)
+        dr_out = None if g_r is None else g_r.contiguous().view(-1, cols)
+        dri, dh, dw, db, dhb = R.dispatch(
+            'add_dropout_ln_bwd', r, g_y.contiguous().view(-1, cols), dr_out, r, w, mean, rstd,
+            ctx.p, ctx.seed, w is not None and ctx.needs_input_grad[3],
+            ctx.has_b and ctx.needs_input_grad[4], ctx.has_hb and ctx.needs_input_grad[2])
+        return dri.view(ctx.shp), dh.view(ctx.shp), dhb, dw, db, None, None
+
+
+def add_dropout_layer_norm(x, h, hbias, w, b, p=0.0, eps=1e-5, training=True):
+    """(r, y) with r = x + dropout(h + hbias), y = LayerNorm(r)·w + b."""
+    return AddDropoutLNFn.apply(x, h, hbias, w, b, p if training else 0.0, eps)
 
 
 # =============================================================================
@@ -443,7 +595,7 @@ def _fa_fwd_hip(q, k, v, causal, scale):
 
 
 @R.register_kernel('flash_attn_bwd', 'hip')
-def _fa_bwd_hip(do, q, k, v, o, lse, causal, scale):
+def _fa_bwd_hip(do, q, k, v, o, lse, causal, scale, dq=None, dk=None, dv=None):
     if not _fa_supported(q, k, v):
         return _fa_bwd_ref(do, q, k, v, o, lse, causal, scale)
     L = _native.lib()
@@ -452,16 +604,47 @@ def _fa_bwd_hip(do, q, k, v, o, lse, causal, scale):
     do = do.contiguous()
     delta = torch.empty((B, H, Sq), device=q.device, dtype=torch.float32)
     L.flash_bwd_pre(_ptr(o), _ptr(do), _ptr(delta), B, H, Sq, D, _dt(q), _stream())
-    dq = torch.empty((B, Sq, H, D), device=q.device, dtype=q.dtype)
-    dk = torch.empty((B, Sk, H, D), device=q.device, dtype=q.dtype)
-    dv = torch.empty((B, Sk, H, D), device=q.device, dtype=q.dtype)
+    if dq is None:
+        dq = torch.empty((B, Sq, H, D), device=q.device, dtype=q.dtype)
+        dk = torch.empty((B, Sk, H, D), device=q.device, dtype=q.dtype)
+        dv = torch.empty((B, Sk, H, D), device=q.device, dtype=q.dtype)
+    st = [q.stride(0), q.stride(1), q.stride(2), k.stride(0), k.stride(1), k.stride(2),
+          v.stride(0), v.stride(1), v.stride(2), dq.stride(0), dq.stride(1), dq.stride(2),
+          dk.stride(0), dk.stride(1), dk.stride(2), dv.stride(0), dv.stride(1), dv.stride(2)]
     L.flash_bwd(_ptr(q), _ptr(k), _ptr(v), _ptr(do), _ptr(lse), _ptr(delta), _ptr(dq), _ptr(dk),
-                _ptr(dv), B, H, Sq, Sk, D,
-                q.stride(0), q.stride(1), q.stride(2),
-                k.stride(0), k.stride(1), k.stride(2),
-                v.stride(0), v.stride(1), v.stride(2),
-                float(scale), int(causal), _dt(q), _stream())
+                _ptr(dv), B, H, Sq, Sk, D, st, float(scale), int(causal), _dt(q), _stream())
     return dq, dk, dv
+
+
+class FlashAttnQKVPackedFn(torch.autograd.Function):
+    """qkv [B, S, 3, H, D] -> o [B, S, H, D]; backward writes dq/dk/dv straight into one
+    packed [B, S, 3, H, D] gradient (no stack/cat of the three grads)."""
+
+    @staticmethod
+    def forward(ctx, qkv, causal, scale):
+        q, k, v = qkv.unbind(2)
+        o, lse = R.dispatch('flash_attn_fwd', qkv, q, k, v, causal, scale)
+        ctx.save_for_backward(qkv, o, lse)
+        ctx.causal, ctx.scale = causal, scale
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        qkv, o, lse = ctx.saved_tensors
+        q, k, v = qkv.unbind(2)
+        if R.select_backend(qkv, 'flash_attn_bwd') == 'hip' and _fa_supported(q, k, v):
+            dqkv = torch.empty_like(qkv)
+            dq, dk, dv = dqkv.unbind(2)
+            _fa_bwd_hip(do, q, k, v, o, lse, ctx.causal, ctx.scale, dq, dk, dv)
+            return dqkv, None, None
+        dq, dk, dv = _fa_bwd_ref(do, q, k, v, o, lse, ctx.causal, ctx.scale)
+        return torch.stack([dq, dk, dv], 2), None, None
+
+
+def flash_attention_qkvpacked(qkv, causal=False, scale=None):
+    if scale is None:
+        scale = 1.0 / math.sqrt(qkv.shape[-1])
+    return FlashAttnQKVPackedFn.apply(qkv, causal, scale)
 
 
 class FlashAttnFn(torch.autograd.Function):

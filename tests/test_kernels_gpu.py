@@ -194,3 +194,61 @@ def test_registry_uses_hip():
     x = torch.randn(4, 64, device=DEV)
     F.layer_norm(x, None, None, 1e-5)
     assert R.stats().get(('layer_norm_fwd', 'hip'), 0) == 1
+
+
+@pytest.mark.parametrize('p', [0.0, 0.1])
+@pytest.mark.parametrize('cols', [2048, 1024, 776])
+def test_add_dropout_layer_norm(p, cols):
+    torch.manual_seed(0)
+    dt = torch.bfloat16
+    x = torch.randn(67, cols, device=DEV, dtype=dt, requires_grad=True)
+    h = torch.randn(67, cols, device=DEV, dtype=dt, requires_grad=True)
+    hb = torch.randn(cols, device=DEV, dtype=dt, requires_grad=True)
+    w = torch.randn(cols, device=DEV, dtype=dt, requires_grad=True)
+    b = torch.randn(cols, device=DEV, dtype=dt, requires_grad=True)
+    torch.manual_seed(5)
+    r, y = F.add_dropout_layer_norm(x, h, hb, w, b, p, 1e-5)
+    gr, gy = torch.randn_like(r), torch.randn_like(y)
+    (r.float() * gr.float()).sum().add((y.float() * gy.float()).sum()).backward()
+    # reference with the SAME counter-hash mask
+    torch.manual_seed(5)
+    seed = F._dropout_seed() if p > 0 else 0
+    xr, hr, hbr, wr, br = (t.detach().float().requires_grad_() for t in (x, h, hb, w, b))
+    t = hr + hbr
+    if p > 0:
+        keep = F._hash_keep_ref(t.numel(), p, seed, DEV).view(t.shape)
+        t = torch.where(keep, t / (1 - p), torch.zeros_like(t))
+    rr = xr + t
+    yr = torch.nn.functional.layer_norm(rr, (cols,), wr, br, 1e-5)
+    (rr * gr.float()).sum().add((yr * gy.float()).sum()).backward()
+    assert torch.allclose(r.float(), rr, atol=5e-2, rtol=2e-2)
+    assert torch.allclose(y.float(), yr, atol=1e-1, rtol=5e-2)
+    for a, bb, tol in ((x.grad, xr.grad, 0.15), (h.grad, hr.grad, 0.15), (w.grad, wr.grad, 2.0),
+                       (b.grad, br.grad, 2.0), (hb.grad, hbr.grad, 2.0)):
+        assert (a.float() - bb).abs().max().item() < tol * max(1, bb.abs().max().item() * 0.05), \
+            (a.float() - bb).abs().max()
+
+
+def test_dropout_rate():
+    x = torch.zeros(256, 2048, device=DEV, dtype=torch.bfloat16)
+    h = torch.ones(256, 2048, device=DEV, dtype=torch.bfloat16)
+    r, _ = F.add_dropout_layer_norm(x, h, None, None, None, 0.1, 1e-5)
+    frac = (r == 0).float().mean().item()
+    assert abs(frac - 0.1) < 0.005, frac
+
+
+@pytest.mark.parametrize('D', [64, 128])
+def test_flash_attention_qkvpacked(D):
+    torch.manual_seed(3)
+    B, S, H = 2, 192, 4
+    qkv = torch.randn(B, S, 3, H, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    o = F.flash_attention_qkvpacked(qkv, causal=True)
+    do = torch.randn_like(o)
+    o.backward(do)
+    ref = qkv.detach().float().requires_grad_()
+    q, k, v = ref.unbind(2)
+    orf = _attn_ref(q, k, v, True, 1 / math.sqrt(D))
+    orf.backward(do.float())
+    assert (o.float() - orf).abs().max().item() < 4e-2
+    err = (qkv.grad.float() - ref.grad).abs().max().item()
+    assert err < 8e-2 * max(1.0, ref.grad.abs().max().item()), err
