@@ -12,11 +12,13 @@ struct bf16 { uint16_t v; };
 using f16 = _Float16;
 
 __device__ __forceinline__ float bf2f(uint16_t u) { return __uint_as_float(((uint32_t)u) << 16); }
-__device__ __forceinline__ uint16_t f2bf(float f) {
-  uint32_t u = __float_as_uint(f);
-  if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40);  // NaN stays NaN
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return (uint16_t)(u >> 16);
+// hardware RNE conversion (v_cvt_pk_bf16_f32 on gfx950; NaN-preserving, branch-free)
+typedef float pra_f2 __attribute__((ext_vector_type(2)));
+typedef __bf16 pra_b2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint16_t f2bf(float f) { return __builtin_bit_cast(uint16_t, (__bf16)f); }
+__device__ __forceinline__ uint32_t pack_bf2(float a, float b) {
+  pra_f2 v = {a, b};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, pra_b2));
 }
 
 template <typename T> struct Cvt;
@@ -63,10 +65,10 @@ template <> __device__ __forceinline__ void store8<float>(float* p, const float*
 }
 template <> __device__ __forceinline__ void store8<bf16>(bf16* p, const float* o) {
   uint4 u;
-  u.x = (uint32_t)f2bf(o[0]) | ((uint32_t)f2bf(o[1]) << 16);
-  u.y = (uint32_t)f2bf(o[2]) | ((uint32_t)f2bf(o[3]) << 16);
-  u.z = (uint32_t)f2bf(o[4]) | ((uint32_t)f2bf(o[5]) << 16);
-  u.w = (uint32_t)f2bf(o[6]) | ((uint32_t)f2bf(o[7]) << 16);
+  u.x = pack_bf2(o[0], o[1]);
+  u.y = pack_bf2(o[2], o[3]);
+  u.z = pack_bf2(o[4], o[5]);
+  u.w = pack_bf2(o[6], o[7]);
   *reinterpret_cast<uint4*>(p) = u;
 }
 template <> __device__ __forceinline__ void store8<f16>(f16* p, const float* o) {

@@ -25,6 +25,8 @@
 namespace pra {
 namespace fa {
 
+__device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
@@ -45,9 +47,7 @@ __device__ __forceinline__ f32x16 mfma<f16>(V8<f16>::type a, V8<f16>::type b, f3
 }
 
 template <typename T> __device__ __forceinline__ uint32_t pack2(float a, float b);
-template <> __device__ __forceinline__ uint32_t pack2<bf16>(float a, float b) {
-  return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
-}
+template <> __device__ __forceinline__ uint32_t pack2<bf16>(float a, float b) { return pack_bf2(a, b); }
 template <> __device__ __forceinline__ uint32_t pack2<f16>(float a, float b) {
   _Float16 x = (_Float16)a, y = (_Float16)b;
   return (uint32_t)__builtin_bit_cast(uint16_t, x) | ((uint32_t)__builtin_bit_cast(uint16_t, y) << 16);
@@ -83,53 +83,57 @@ constexpr int kTP = kTile + 4;   // transposed-image row length (136 B rows: 8-B
 
 template <int D> struct Geo {
   static constexpr int RP = D + 8;                 // row-major image row length (odd # of 16-B slots)
-  static constexpr int NPASS = D / 64;             // pair-load passes per thread
   static constexpr int ROW_IMG = kTile * RP;       // elements
   static constexpr int TR_IMG = D * kTP;           // elements
 };
 
-// Block-cooperative staged load of a 64-row x D tile, pair mapping:
-// thread t -> rows 2*(t%32), 2*(t%32)+1; 16-B column chunk (t/32) + 8*pass.
-template <typename T, int D>
+// Block-cooperative staged load of a 64-row x D tile by NT threads, pair mapping:
+// pair-chunk pc = t + NT*p -> rows 2*(pc%32), 2*(pc%32)+1, 16-B column chunk pc/32.
+template <typename T, int D, int NT>
 struct TileRegs {
-  uint4 r0[Geo<D>::NPASS], r1[Geo<D>::NPASS];
+  static constexpr int NCH = D / 8;                          // 16-B chunks per row
+  static constexpr int NPASS = (32 * NCH + NT - 1) / NT;
+  uint4 r0[NPASS], r1[NPASS];
 
   __device__ __forceinline__ void load(const T* base, int64_t row_stride, int row0, int nrows) {
-    const int t = threadIdx.x, kp = t & 31, dcb = t >> 5;
-    const int ra = row0 + 2 * kp, rb = ra + 1;
 #pragma unroll
-    for (int p = 0; p < Geo<D>::NPASS; ++p) {
-      const int dc = dcb + 8 * p;
-      r0[p] = ra < nrows ? *reinterpret_cast<const uint4*>(base + (int64_t)ra * row_stride + dc * 8)
-                         : make_uint4(0, 0, 0, 0);
-      r1[p] = rb < nrows ? *reinterpret_cast<const uint4*>(base + (int64_t)rb * row_stride + dc * 8)
-                         : make_uint4(0, 0, 0, 0);
+    for (int p = 0; p < NPASS; ++p) {
+      const int pc = threadIdx.x + NT * p, kp = pc & 31, dc = pc >> 5;
+      const int ra = row0 + 2 * kp, rb = ra + 1;
+      const bool ok = dc < NCH;
+      r0[p] = (ok && ra < nrows) ? *reinterpret_cast<const uint4*>(base + (int64_t)ra * row_stride + dc * 8)
+                                 : make_uint4(0, 0, 0, 0);
+      r1[p] = (ok && rb < nrows) ? *reinterpret_cast<const uint4*>(base + (int64_t)rb * row_stride + dc * 8)
+                                 : make_uint4(0, 0, 0, 0);
     }
   }
   // row-major image [64][D+8]
   __device__ __forceinline__ void store_rows(T* img) const {
-    const int t = threadIdx.x, kp = t & 31, dcb = t >> 5;
 #pragma unroll
-    for (int p = 0; p < Geo<D>::NPASS; ++p) {
-      const int dc = dcb + 8 * p;
-      *reinterpret_cast<uint4*>(img + (2 * kp) * Geo<D>::RP + dc * 8) = r0[p];
-      *reinterpret_cast<uint4*>(img + (2 * kp + 1) * Geo<D>::RP + dc * 8) = r1[p];
+    for (int p = 0; p < NPASS; ++p) {
+      const int pc = threadIdx.x + NT * p, kp = pc & 31, dc = pc >> 5;
+      if (dc < NCH) {
+        *reinterpret_cast<uint4*>(img + (2 * kp) * Geo<D>::RP + dc * 8) = r0[p];
+        *reinterpret_cast<uint4*>(img + (2 * kp + 1) * Geo<D>::RP + dc * 8) = r1[p];
+      }
     }
   }
   // transposed image [D][64+4]: dword (row 2kp, row 2kp+1) at [d][2kp]
   __device__ __forceinline__ void store_tr(T* img) const {
-    const int t = threadIdx.x, kp = t & 31, dcb = t >> 5;
 #pragma unroll
-    for (int p = 0; p < Geo<D>::NPASS; ++p) {
-      const int d0 = (dcb + 8 * p) * 8;
-      const uint32_t a[4] = {r0[p].x, r0[p].y, r0[p].z, r0[p].w};
-      const uint32_t b[4] = {r1[p].x, r1[p].y, r1[p].z, r1[p].w};
+    for (int p = 0; p < NPASS; ++p) {
+      const int pc = threadIdx.x + NT * p, kp = pc & 31, dc = pc >> 5;
+      if (dc < NCH) {
+        const int d0 = dc * 8;
+        const uint32_t a[4] = {r0[p].x, r0[p].y, r0[p].z, r0[p].w};
+        const uint32_t b[4] = {r1[p].x, r1[p].y, r1[p].z, r1[p].w};
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        uint32_t lo = (a[i] & 0xffffu) | (b[i] << 16);
-        uint32_t hi = (a[i] >> 16) | (b[i] & 0xffff0000u);
-        *reinterpret_cast<uint32_t*>(img + (d0 + 2 * i) * kTP + 2 * kp) = lo;
-        *reinterpret_cast<uint32_t*>(img + (d0 + 2 * i + 1) * kTP + 2 * kp) = hi;
+        for (int i = 0; i < 4; ++i) {
+          uint32_t lo = (a[i] & 0xffffu) | (b[i] << 16);
+          uint32_t hi = (a[i] >> 16) | (b[i] & 0xffff0000u);
+          *reinterpret_cast<uint32_t*>(img + (d0 + 2 * i) * kTP + 2 * kp) = lo;
+          *reinterpret_cast<uint32_t*>(img + (d0 + 2 * i + 1) * kTP + 2 * kp) = hi;
+        }
       }
     }
   }
@@ -167,21 +171,21 @@ __device__ __forceinline__ int acc_row(int reg, int h) { return (reg & 3) + 8 * 
 // ============================================================================
 // forward
 // ============================================================================
-template <typename T, int D, bool CAUSAL>
-__global__ void __launch_bounds__(256, 1)
+template <typename T, int D, bool CAUSAL, int NW>
+__global__ void __launch_bounds__(NW * 64, NW / 4)
 fwd_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restrict__ v, T* __restrict__ o,
            float* __restrict__ lse, int H, int Sq, int Sk, int64_t qsb, int64_t qss, int64_t qsh, int64_t ksb,
            int64_t kss, int64_t ksh, int64_t vsb, int64_t vss, int64_t vsh, float scale_log2) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   T* Ks = reinterpret_cast<T*>(smem);
   T* Vt = Ks + Geo<D>::ROW_IMG;
-  constexpr int NS = D / 16, ND = D / 32;
+  constexpr int NS = D / 16, ND = D / 32, BM = NW * 32;
 
   const int nqb = gridDim.x;
-  const int qb = CAUSAL ? (nqb - 1 - blockIdx.x) : blockIdx.x;
+  const int qb = CAUSAL ? (nqb - 1 - blockIdx.x) : blockIdx.x;  // heaviest causal blocks first
   const int bh = blockIdx.y, b = bh / H, hh = bh % H;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
-  const int q0 = qb * 128;
+  const int q0 = qb * BM;
   const int myq = q0 + wave * 32 + r;
   const int off = Sk - Sq;
 
@@ -200,13 +204,13 @@ fwd_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restrict
   f32x16 acc_o[ND];
 #pragma unroll
   for (int i = 0; i < ND; ++i) acc_o[i] = f32x16{};
-  float m_run = -INFINITY, l_run = 0.f;
+  float m_run = -INFINITY, l_run = 0.f;  // m in the scaled log2 domain
 
   int n_end = Sk;
-  if (CAUSAL) n_end = min(Sk, q0 + 128 + off);
+  if (CAUSAL) n_end = min(Sk, q0 + BM + off);
   const int ntiles = n_end > 0 ? (n_end + kTile - 1) / kTile : 0;
 
-  TileRegs<T, D> kr, vr;
+  TileRegs<T, D, NW * 64> kr, vr;
   if (ntiles > 0) {
     kr.load(kb_, kss, 0, Sk);
     vr.load(vb_, vss, 0, Sk);
@@ -221,7 +225,7 @@ fwd_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restrict
       kr.load(kb_, kss, k0 + kTile, Sk);
       vr.load(vb_, vss, k0 + kTile, Sk);
     }
-    // S^T = K Q^T : two 32-key tiles
+    // S^T = K Q^T : two 32-key tiles (raw scores)
     f32x16 s_acc[2];
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt) {
@@ -230,39 +234,43 @@ fwd_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restrict
       for (int s = 0; s < NS; ++s)
         s_acc[mt] = mfma<T>(frag_rows<T, D>(Ks, 32 * mt + r, s, h), qf[s], s_acc[mt]);
     }
-    // scale + mask + online softmax (lane-local per query)
-    float mx = -INFINITY;
     const bool need_mask = (k0 + kTile > Sk) || (CAUSAL && (k0 + kTile - 1 > q0 + off));
+    if (need_mask) {
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int key = k0 + 32 * mt + acc_row(i, h);
+          const bool bad = key >= Sk || (CAUSAL && key > myq + off);
+          s_acc[mt][i] = bad ? -INFINITY : s_acc[mt][i];
+        }
+    }
+    float mx = -INFINITY;
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        float x = s_acc[mt][i] * scale_log2;
-        if (need_mask) {
-          const int key = k0 + 32 * mt + acc_row(i, h);
-          if (key >= Sk || (CAUSAL && key > myq + off)) x = -INFINITY;
-        }
-        s_acc[mt][i] = x;
-        mx = fmaxf(mx, x);
-      }
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      for (int i = 0; i < 16; ++i) mx = fmaxf(mx, s_acc[mt][i]);
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64)) * scale_log2;
     const float m_new = fmaxf(m_run, mx);
     const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
-    const float alpha = exp2f(m_run - m_use);
+    if (__any(m_new > m_run)) {  // exact: lanes whose max did not grow get alpha = 1
+      const float alpha = fexp2(m_run - m_use);
+      l_run *= alpha;
+#pragma unroll
+      for (int dt = 0; dt < ND; ++dt) acc_o[dt] *= alpha;
+    }
+    m_run = m_new;
     float ps = 0.f;
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        float p = exp2f(s_acc[mt][i] - m_use);
+        float p = fexp2(fmaf(s_acc[mt][i], scale_log2, -m_use));
         s_acc[mt][i] = p;
         ps += p;
       }
     ps += __shfl_xor(ps, 32, 64);
-    l_run = l_run * alpha + ps;
-    m_run = m_new;
-#pragma unroll
-    for (int dt = 0; dt < ND; ++dt) acc_o[dt] *= alpha;
+    l_run += ps;
     // O^T += V^T P^T
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
@@ -301,8 +309,8 @@ fwd_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restrict
 // ============================================================================
 // backward: dQ (queries on lanes, sweep key tiles)
 // ============================================================================
-template <typename T, int D, bool CAUSAL>
-__global__ void __launch_bounds__(256, 1)
+template <typename T, int D, bool CAUSAL, int NW>
+__global__ void __launch_bounds__(NW * 64, NW / 4)
 bwd_dq_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restrict__ v, const T* __restrict__ dO,
               const float* __restrict__ lse, const float* __restrict__ delta, T* __restrict__ dq, int H, int Sq,
               int Sk, int64_t qsb, int64_t qss, int64_t qsh, int64_t ksb, int64_t kss, int64_t ksh, int64_t vsb,
@@ -311,14 +319,14 @@ bwd_dq_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restr
   T* Ks = reinterpret_cast<T*>(smem);
   T* Vs = Ks + Geo<D>::ROW_IMG;
   T* Kt = Vs + Geo<D>::ROW_IMG;
-  constexpr int NS = D / 16, ND = D / 32;
+  constexpr int NS = D / 16, ND = D / 32, BM = NW * 32;
   const float LOG2E = 1.4426950408889634f;
 
   const int nqb = gridDim.x;
   const int qb = CAUSAL ? (nqb - 1 - blockIdx.x) : blockIdx.x;
   const int bh = blockIdx.y, b = bh / H, hh = bh % H;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
-  const int q0 = qb * 128;
+  const int q0 = qb * BM;
   const int myq = q0 + wave * 32 + r;
   const int off = Sk - Sq;
   const bool qvalid = myq < Sq;
@@ -346,10 +354,10 @@ bwd_dq_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restr
   for (int i = 0; i < ND; ++i) acc_q[i] = f32x16{};
 
   int n_end = Sk;
-  if (CAUSAL) n_end = min(Sk, q0 + 128 + off);
+  if (CAUSAL) n_end = min(Sk, q0 + BM + off);
   const int ntiles = n_end > 0 ? (n_end + kTile - 1) / kTile : 0;
 
-  TileRegs<T, D> kr, vr;
+  TileRegs<T, D, NW * 64> kr, vr;
   if (ntiles > 0) {
     kr.load(kb_, kss, 0, Sk);
     vr.load(vb_, vss, 0, Sk);
@@ -381,7 +389,7 @@ bwd_dq_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restr
     for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        float p = exp2f(s_acc[mt][i] * scale_log2 - lse2);
+        float p = fexp2(fmaf(s_acc[mt][i], scale_log2, -lse2));
         if (need_mask) {
           const int key = k0 + 32 * mt + acc_row(i, h);
           if (key >= Sk || (CAUSAL && key > myq + off)) p = 0.f;
@@ -475,7 +483,7 @@ bwd_dkdv_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __res
   if (CAUSAL) q_begin = max(0, kblk0 - off) / kTile * kTile;
   const int ntiles = q_begin < Sq ? (Sq - q_begin + kTile - 1) / kTile : 0;
 
-  TileRegs<T, D> qr, dr;
+  TileRegs<T, D, 256> qr, dr;
   float lreg = 0.f, dreg = 0.f;
   auto load_tile = [&](int qs0) {
     qr.load(qb_, qss, qs0, Sq);
@@ -519,7 +527,7 @@ bwd_dkdv_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __res
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
           const int i = 4 * g + c;
-          float p = exp2f(s_acc[i] * scale_log2 - la[c]);
+          float p = fexp2(fmaf(s_acc[i], scale_log2, -la[c]));
           if (need_mask) {
             const int qq = qs0 + qr0 + c;
             if (qq >= Sq || (CAUSAL && mykey > qq + off)) p = 0.f;
@@ -568,10 +576,11 @@ template <typename T, int D, bool C>
 static void launch_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B, int H, int Sq,
                        int Sk, const int64_t* st, float scale, hipStream_t s) {
   const size_t lds = (Geo<D>::ROW_IMG + Geo<D>::TR_IMG) * sizeof(T);
-  auto kern = fwd_kernel<T, D, C>;
+  constexpr int NW = 8;
+  auto kern = fwd_kernel<T, D, C, NW>;
   hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  dim3 grid((Sq + 127) / 128, B * H);
-  hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, (const T*)q, (const T*)k, (const T*)v, (T*)o, lse, H, Sq, Sk,
+  dim3 grid((Sq + NW * 32 - 1) / (NW * 32), B * H);
+  hipLaunchKernelGGL(kern, grid, dim3(NW * 64), lds, s, (const T*)q, (const T*)k, (const T*)v, (T*)o, lse, H, Sq, Sk,
                      st[0], st[1], st[2], st[3], st[4], st[5], st[6], st[7], st[8], scale * 1.4426950408889634f);
 }
 
@@ -582,9 +591,10 @@ static void launch_bwd(const void* q, const void* k, const void* v, const void* 
   const float sl2 = scale * 1.4426950408889634f;
   {
     const size_t lds = (2 * Geo<D>::ROW_IMG + Geo<D>::TR_IMG) * sizeof(T);
-    auto kern = bwd_dq_kernel<T, D, C>;
+    constexpr int NW = 8;
+    auto kern = bwd_dq_kernel<T, D, C, NW>;
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(kern, dim3((Sq + 127) / 128, B * H), dim3(256), lds, s, (const T*)q, (const T*)k,
+    hipLaunchKernelGGL(kern, dim3((Sq + NW * 32 - 1) / (NW * 32), B * H), dim3(NW * 64), lds, s, (const T*)q, (const T*)k,
                        (const T*)v, (const T*)dO, lse, delta, (T*)dq, H, Sq, Sk, st[0], st[1], st[2], st[3], st[4],
                        st[5], st[6], st[7], st[8], st[9], st[10], st[11], scale, sl2);
   }
