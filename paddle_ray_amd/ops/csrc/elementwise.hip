@@ -170,19 +170,25 @@ __global__ void __launch_bounds__(256) sumsq_k(const T* __restrict__ x, float* _
   if (threadIdx.x == 0) atomicAdd(out, s);
 }
 
-// delta[b,h,s] = sum_d dO[b,s,h,d] * O[b,s,h,d]   (O, dO contiguous [B,S,H,D]); one wave per row.
+// delta[b,h,s] = sum_d dO[b,s,h,d] * O[b,s,h,d]   (O, dO contiguous [B,S,H,D]).
+// D/8 lanes per row with 16-B loads (D=128: 16 lanes, 4 rows per wave).
 template <typename T>
 __global__ void __launch_bounds__(256) attn_delta_k(const T* __restrict__ o, const T* __restrict__ dO,
                                                     float* __restrict__ delta, int B, int H, int S, int D) {
-  const int lane = threadIdx.x & 63;
-  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (r >= (int64_t)B * S * H) return;
-  const T* orow = o + r * D;
-  const T* drow = dO + r * D;
+  const int lpr = D / 8;  // lanes per row (power of two, <= 64)
+  const int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / lpr;
+  const int sub = threadIdx.x % lpr;
+  const bool valid = r < (int64_t)B * S * H;
   float s = 0.f;
-  for (int i = lane; i < D; i += 64) s += Cvt<T>::to(orow[i]) * Cvt<T>::to(drow[i]);
-  s = wave_sum(s);
-  if (lane == 0) {
+  if (valid) {
+    float a[8], g[8];
+    load8<T>(o + r * D + sub * 8, a);
+    load8<T>(dO + r * D + sub * 8, g);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s += a[i] * g[i];
+  }
+  for (int off = lpr / 2; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+  if (valid && sub == 0) {
     const int64_t h = r % H, bs = r / H, sq = bs % S, b = bs / S;
     delta[(b * H + h) * S + sq] = s;
   }
@@ -251,7 +257,8 @@ void pra_flash_bwd_pre(const void* o, const void* dO, float* delta, int B, int H
                        hipStream_t s) {
   int64_t rows = (int64_t)B * S * H;
   if (!rows) return;
-  PRA_DISPATCH_FLOAT(dt, T, hipLaunchKernelGGL((attn_delta_k<T>), dim3((rows + 3) / 4), dim3(256), 0, s,
+  const int64_t threads = rows * (D / 8);
+  PRA_DISPATCH_FLOAT(dt, T, hipLaunchKernelGGL((attn_delta_k<T>), dim3((threads + 255) / 256), dim3(256), 0, s,
                                                (const T*)o, (const T*)dO, delta, B, H, S, D));
 }
 }
