@@ -330,7 +330,21 @@ def alltoall(in_tensor_list, out_tensor_list, group=None, sync_op=True):
         out_tensor_list.extend(Tensor(t.clone()) for t in ins)
         return _Task()
     outs = [torch.empty_like(t) for t in ins]
-    w = dist.all_to_all(outs, ins, _pg(group), async_op=True)
+    if dist.get_backend(_pg(group)) == 'gloo':  # gloo has no alltoall: pairwise p2p exchange
+        me = get_rank(group) if group is not None else dist.get_rank()
+        ranks = group.ranks if group is not None else list(range(dist.get_world_size()))
+        ops = []
+        for j, peer in enumerate(ranks):
+            if j == me:
+                outs[j].copy_(ins[j])
+                continue
+            ops.append(dist.P2POp(dist.isend, ins[j], peer, _pg(group)))
+            ops.append(dist.P2POp(dist.irecv, outs[j], peer, _pg(group)))
+        for w_ in dist.batch_isend_irecv(ops):
+            w_.wait()
+        w = None
+    else:
+        w = dist.all_to_all(outs, ins, _pg(group), async_op=True)
 
     def post():
         out_tensor_list.clear()

@@ -263,6 +263,7 @@ class PipelineParallel(Layer):
             self.total_loss = torch.stack(losses).sum()
             return self.total_loss
         p2p.sent_meta = False
+        p2p.recv_meta = None  # both sides re-exchange activation meta every batch
         nst, st = p2p.nstages, p2p.stage
         warmup = min(nst - st - 1, M)
         remaining = M - warmup

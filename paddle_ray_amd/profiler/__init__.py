@@ -132,6 +132,7 @@ class Profiler:
         self.record_shapes, self.profile_memory = record_shapes, profile_memory
         self._host_events = []
         self._tp = None
+        self._recording = False
         self.step_num = 0
         self._step_times = []
         self._t_step = None
@@ -143,7 +144,11 @@ class Profiler:
                                                  ProfilerState.RECORD_AND_RETURN)
 
     def _open(self):
-        if self._tp is not None or self.timer_only:
+        if self._recording:
+            return
+        self._recording = True
+        _active.append(self)
+        if self.timer_only:
             return
         acts = [torch.profiler.ProfilerActivity.CPU]
         if ProfilerTarget.GPU in self.targets and torch.cuda.is_available():
@@ -151,14 +156,15 @@ class Profiler:
         self._tp = torch.profiler.profile(activities=acts, record_shapes=self.record_shapes,
                                           profile_memory=self.profile_memory)
         self._tp.__enter__()
-        _active.append(self)
 
     def _close(self):
-        if self._tp is None:
+        if not self._recording:
             return
-        self._tp.__exit__(None, None, None)
+        self._recording = False
         if self in _active:
             _active.remove(self)
+        if self._tp is not None:
+            self._tp.__exit__(None, None, None)
         if self.on_trace_ready is not None:
             self.on_trace_ready(self)
 
@@ -177,11 +183,10 @@ class Profiler:
         self._t_step = now
         self.step_num += 1
         rec = self._want_record()
-        if rec and self._tp is None:
+        if rec and not self._recording:
             self._open()
-        elif not rec and self._tp is not None:
+        elif not rec and self._recording:
             self._close()
-            self._tp = None
 
     def step_info(self, unit=None):
         if not self._step_times:
