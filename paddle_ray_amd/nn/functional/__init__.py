@@ -663,7 +663,10 @@ def batch_norm(x, running_mean, running_var, weight, bias, training=False, momen
     if use_global_stats:
         training = False
     rm, rv = _t(running_mean), _t(running_var)
-    out = TF.batch_norm(t, rm, rv, _opt(weight), _opt(bias), training, 1 - momentum, epsilon)
+    w = _opt(weight)
+    if rm.dtype != t.dtype and not (w is not None and w.dtype == torch.float32):
+        rm, rv = rm.to(t.dtype), rv.to(t.dtype)  # (mixed bf16-in/fp32-param runs natively)
+    out = TF.batch_norm(t, rm, rv, w, _opt(bias), training, 1 - momentum, epsilon)
     if cl:
         out = out.movedim(1, -1)
     return _w(out)

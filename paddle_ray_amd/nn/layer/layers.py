@@ -271,6 +271,14 @@ class Layer:
         raise NotImplementedError
 
     def __call__(self, *inputs, **kwargs):
+        from ...static import _STATIC
+        if _STATIC[0]:
+            from ...static.graph import _has_var, record_layer_call
+            if _has_var(inputs) or _has_var(kwargs):
+                return record_layer_call(self, inputs, kwargs)
+        return self._call_impl(*inputs, **kwargs)
+
+    def _call_impl(self, *inputs, **kwargs):
         if self._forward_pre_hooks:
             for h in list(self._forward_pre_hooks.values()):
                 r = h(self, inputs)

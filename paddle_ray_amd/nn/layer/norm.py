@@ -62,25 +62,9 @@ class _BatchNormBase(Layer):
         self.register_buffer('_variance', Tensor(torch.ones(num_features, dtype=dt, device=dev)))
 
     def forward(self, x):
-        t = _u(x)
-        w = None if self.weight is None else self.weight._t
-        b = None if self.bias is None else self.bias._t
-        cl = self._data_format in ('NHWC', 'NLC', 'NDHWC')
-        if cl:
-            t = t.movedim(-1, 1)
         training = self.training and not self._use_global_stats
-        rm, rv = self._mean._t, self._variance._t
-        if t.dtype != torch.float32 and w is not None and w.dtype == torch.float32:
-            # mixed precision: MIOpen bf16 in / fp32 params
-            out = torch.nn.functional.batch_norm(t, rm, rv, w, b, training, 1 - self._momentum,
-                                                 self._epsilon)
-        else:
-            out = torch.nn.functional.batch_norm(t, rm.to(t.dtype) if rm.dtype != t.dtype else rm,
-                                                 rv.to(t.dtype) if rv.dtype != t.dtype else rv, w, b,
-                                                 training, 1 - self._momentum, self._epsilon)
-        if cl:
-            out = out.movedim(1, -1)
-        return Tensor(out)
+        return F.batch_norm(x, self._mean, self._variance, self.weight, self.bias, training,
+                            self._momentum, self._epsilon, self._data_format)
 
     def extra_repr(self):
         return f'num_features={self._num_features}, momentum={self._momentum}, epsilon={self._epsilon}'

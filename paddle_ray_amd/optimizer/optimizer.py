@@ -146,7 +146,7 @@ class Optimizer:
     def minimize(self, loss, startup_program=None, parameters=None, no_grad_set=None):
         from ..static import _static_mode_enabled
         if _static_mode_enabled():
-            from ..static.program import _static_minimize
+            from ..static.graph import _static_minimize
             return _static_minimize(self, loss, parameters)
         loss.backward()
         self.step()

