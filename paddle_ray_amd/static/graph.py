@@ -601,13 +601,31 @@ class Executor:
             if isinstance(f, str):
                 f = blk.var(f) if blk.has_var(f) else prog._params[f]
             fetch_vars.append(f)
+        names = list(feed.keys())
+        vals = [_as_tensor_feed(feed[n], blk.var(n)) for n in names]
+        has_train = any(op.type in ('backward', 'optimize', 'gradients') for op in blk.ops)
+        if use_graph and not has_train and torch.cuda.is_available() and vals and \
+                all(v._t.is_cuda for v in vals):
+            from ..jit.api import _GraphEntry, _signature
+            key = (prog._version, tuple(names), _signature(tuple(vals), {}),
+                   tuple(id(f) for f in fetch_vars))
+            cache = prog.__dict__.setdefault('_graph_cache', {})
+            g = cache.get(key)
+            if g is None:
+                fn = lambda *fv: self._execute(prog, names, fv, fetch_vars)  # noqa: E731
+                with torch.no_grad():
+                    g = cache[key] = _GraphEntry(fn, tuple(vals), {})
+            outs = [Tensor(o._t.clone()) for o in g(tuple(vals), {})]
+        else:
+            outs = self._execute(prog, names, vals, fetch_vars)
+        return [t.numpy() if return_numpy else t for t in outs]
+
+    def _execute(self, prog, names, vals, fetch_vars):
+        blk = prog.global_block()
         required = [f.vid for f in fetch_vars if isinstance(f, Variable) and
                     not isinstance(f, GradVar)]
         order, free_after = self._plan(prog, required)
-        env = {}
-        for name, val in feed.items():
-            var = blk.var(name)
-            env[var.vid] = _as_tensor_feed(val, var)
+        env = {blk.var(n).vid: v for n, v in zip(names, vals)}
         prev = _STATIC[0]
         _STATIC[0] = False
         try:
@@ -633,7 +651,7 @@ class Executor:
                 t = env[f.vid]
             else:
                 t = f
-            results.append(t.numpy() if return_numpy else t)
+            results.append(t)
         return results
 
 

@@ -166,3 +166,27 @@ def test_save_load_inference_model(static_mode, tmp_path):
     assert feed_names == ['img']
     r, = exe.run(prog, feed={'img': xv}, fetch_list=fetch_targets)
     np.testing.assert_allclose(r, ref, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.gpu
+def test_executor_hip_graph_replay():
+    paddle.set_device('gpu')
+    paddle.enable_static()
+    try:
+        main = static.Program()
+        with static.program_guard(main):
+            x = static.data('x', [None, 16], 'float32')
+            y = F.gelu(static.nn.fc(x, 32)) * 3.0
+        cp = static.CompiledProgram(main)
+        cp._build_strategy.use_hip_graph = True
+        exe = static.Executor()
+        xv = np.random.rand(4, 16).astype('float32')
+        a, = exe.run(main, feed={'x': xv}, fetch_list=[y])
+        b, = exe.run(cp, feed={'x': xv}, fetch_list=[y])
+        c, = exe.run(cp, feed={'x': xv * 2}, fetch_list=[y])
+        d, = exe.run(main, feed={'x': xv * 2}, fetch_list=[y])
+        np.testing.assert_allclose(a, b, rtol=1e-5)
+        np.testing.assert_allclose(c, d, rtol=1e-5)
+        assert len(main._graph_cache) == 1
+    finally:
+        paddle.disable_static()
