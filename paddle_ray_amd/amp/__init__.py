@@ -172,3 +172,4 @@ def is_float16_supported(device=None):
 
 def is_bfloat16_supported(device=None):
     return True
+from . import debugging  # noqa: E402

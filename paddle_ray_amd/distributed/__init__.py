@@ -23,3 +23,4 @@ class ParallelMode:
 
 
 from . import io  # noqa
+from . import watchdog  # noqa: E402

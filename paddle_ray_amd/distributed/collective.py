@@ -14,6 +14,8 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
+from . import watchdog as _watchdog
+
 from ..framework.core import Tensor, _u, _default_device
 
 
@@ -207,13 +209,18 @@ def _single(group):
 
 
 class _Task:
-    def __init__(self, work=None, post=None):
+    def __init__(self, work=None, post=None, name=None):
         self._work, self._post = work, post
+        self._wd = None
+        if work is not None and _watchdog.enabled():
+            self._wd = _watchdog.get_watchdog().track(name or 'collective', work)
 
     def wait(self):
         if self._work is not None:
             self._work.wait()
             self._work = None
+            if self._wd is not None:
+                _watchdog.get_watchdog().done(self._wd)
         if self._post is not None:
             self._post()
             self._post = None
@@ -224,7 +231,8 @@ class _Task:
 
 
 def _ret(work, sync_op, post=None):
-    t = _Task(work, post)
+    import sys
+    t = _Task(work, post, sys._getframe(1).f_code.co_name)
     if sync_op:
         t.wait()
     return t

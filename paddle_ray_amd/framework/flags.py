@@ -44,6 +44,16 @@ def set_flags(flags):
         if k == 'FLAGS_cudnn_deterministic':
             import torch
             torch.backends.cudnn.deterministic = bool(v)
+        if k in ('FLAGS_check_nan_inf', 'FLAGS_check_nan_inf_level'):
+            _apply_nan_inf()
+
+
+def _apply_nan_inf():
+    from . import nan_inf
+    if _FLAGS['FLAGS_check_nan_inf']:
+        nan_inf.enable(_FLAGS['FLAGS_check_nan_inf_level'])
+    else:
+        nan_inf.disable()
 
 
 def get_flags(flags):
@@ -60,3 +70,7 @@ def get_flags(flags):
 
 def flag(name):
     return _FLAGS.get(name)
+
+
+if _FLAGS['FLAGS_check_nan_inf']:
+    _apply_nan_inf()

@@ -13,6 +13,8 @@ import os
 
 import torch
 
+from ..framework import nan_inf as _nan_inf
+
 _KERNELS = {}
 _STATS = collections.Counter()
 _FORCE_REF = os.environ.get('PRA_FORCE_REF', '0') == '1'
@@ -53,7 +55,10 @@ def select_backend(t: torch.Tensor, op=None):
 
 
 def dispatch(op, t, *args, **kwargs):
-    return _KERNELS[(op, select_backend(t, op))](*args, **kwargs)
+    out = _KERNELS[(op, select_backend(t, op))](*args, **kwargs)
+    if _nan_inf._state['mode'] is not None:
+        _nan_inf.check_outputs(op, out)
+    return out
 
 
 def stats():

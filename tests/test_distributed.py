@@ -270,3 +270,30 @@ def test_pipeline_parallel_1f1b(tmp_path):
         ref.append(tot)
     np.testing.assert_allclose(res[0]['losses'], ref, rtol=1e-4)
     np.testing.assert_allclose(res[1]['losses'], ref, rtol=1e-4)
+
+
+# ---------------------------------------------------------------------------------------------
+def _watchdog_worker(rank, world):
+    import time
+    import paddle_ray_amd as paddle
+    import paddle_ray_amd.distributed as dist
+    from paddle_ray_amd.distributed import watchdog
+    wd = watchdog.get_watchdog()
+    wd.timeout_s, wd.poll_s = 0.5, 0.1
+    hb = watchdog.Heartbeat(interval=0.2).start()
+    time.sleep(0.3)
+    alive = hb.dead_ranks(stale_s=5.0)
+    if rank == 1:
+        time.sleep(2.0)  # straggler: rank 0's all_reduce stays in flight
+    t = paddle.to_tensor([1.0])
+    dist.all_reduce(t)
+    hb.stop()
+    return {'reports': list(wd.reports), 'dead': alive, 'sum': float(t)}
+
+
+def test_comm_watchdog_and_heartbeat(tmp_path):
+    res = run_ranks(_watchdog_worker, 2, tmp_path)
+    assert res[0]['sum'] == 2.0 and res[1]['sum'] == 2.0
+    assert any("all_reduce" in m for m in res[0]['reports']), res[0]['reports']
+    assert not res[1]['reports']
+    assert res[0]['dead'] == [] and res[1]['dead'] == []
