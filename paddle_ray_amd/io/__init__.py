@@ -235,7 +235,7 @@ def default_collate_fn(batch):
     if isinstance(s, Tensor):
         return np.stack([b.numpy() for b in batch])
     if isinstance(s, np.ndarray):
-        return np.stack(batch)
+        return _stack_native(batch)
     if isinstance(s, (int, np.integer)):
         return np.array(batch, dtype=np.int64)
     if isinstance(s, (float, np.floating)):
@@ -247,6 +247,22 @@ def default_collate_fn(batch):
     if isinstance(s, (list, tuple)):
         return [default_collate_fn(list(x)) for x in zip(*batch)]
     return batch
+
+
+def _stack_native(arrs):
+    """np.stack via the native multi-threaded row copy for large same-shape batches."""
+    s = arrs[0]
+    nbytes = s.nbytes * len(arrs)
+    if nbytes < (4 << 20) or not all(a.shape == s.shape and a.dtype == s.dtype for a in arrs):
+        return np.stack(arrs)
+    from ..native import runtime
+    rt = runtime()
+    if rt is None:
+        return np.stack(arrs)
+    arrs = [np.ascontiguousarray(a) for a in arrs]
+    out = np.empty((len(arrs),) + s.shape, dtype=s.dtype)
+    rt.stack_rows([a.ctypes.data for a in arrs], s.nbytes, out.ctypes.data, 8)
+    return out
 
 
 def default_convert_fn(batch):
@@ -445,3 +461,6 @@ class _GeneratorLoader:
         dev = _default_device()
         for b in self._gen():
             yield _to_device_tree(b, dev)
+
+
+from .gpt_dataset import GPTDataset, NativeTokenLoader, write_token_dataset  # noqa: E402

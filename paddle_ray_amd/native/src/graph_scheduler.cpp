@@ -122,8 +122,11 @@ static Plan build_plan(const std::vector<std::vector<int>>& ins, const std::vect
   return plan;
 }
 
+void pra_register_data(py::module& m);  // data_ring.cpp
+
 PYBIND11_MODULE(_pra_runtime, m) {
-  m.doc() = "paddle_ray_amd native runtime: static-graph scheduler";
+  m.doc() = "paddle_ray_amd native runtime: static-graph scheduler + data pipeline";
+  pra_register_data(m);
   m.def("build_plan",
         [](const std::vector<std::vector<int>>& ins, const std::vector<std::vector<int>>& outs,
            const std::vector<int>& required, const std::vector<int>& persistable) {
