@@ -176,18 +176,18 @@ class BertLayer(nn.Layer):
 
     def _ffn_hidden(self, y):
         if self.act == 'gelu' and self.fused:
-            return K.bias_gelu(torch.matmul(_u(y), self.fc1.weight._t), self.fc1.bias._t, False)
+            return K.bias_gelu(K.linear(_u(y), self.fc1.weight._t), self.fc1.bias._t, False)
         return _u(getattr(F, self.act)(self.fc1(y)))
 
     def forward(self, x, attn_mask=None):
         p = self.p if self.training else 0.0
         if self.fused:
             t = _u(x)
-            a = torch.matmul(self.attn.context(x, attn_mask), self.attn.out_proj.weight._t)
+            a = K.linear(self.attn.context(x, attn_mask), self.attn.out_proj.weight._t)
             _, y1 = K.add_dropout_layer_norm(t, a, self.attn.out_proj.bias._t,
                                              self.ln1.weight._t, self.ln1.bias._t, p, self.eps)
             hdn = self._ffn_hidden(Tensor(y1))
-            m = torch.matmul(hdn, self.fc2.weight._t)
+            m = K.linear(hdn, self.fc2.weight._t)
             _, y2 = K.add_dropout_layer_norm(y1, m, self.fc2.bias._t, self.ln2.weight._t,
                                              self.ln2.bias._t, p, self.eps)
             return Tensor(y2)

@@ -120,7 +120,7 @@ class GPTAttention(nn.Layer):
 
     def forward_nobias(self, x):
         """attention output projection WITHOUT its bias (fused into the next kernel)."""
-        return Tensor(torch.matmul(self._core(x), self.out_proj.weight._t))
+        return Tensor(K.linear(self._core(x), self.out_proj.weight._t))
 
     def forward(self, x):
         qkv = _u(self.qkv_proj(x))
@@ -156,14 +156,14 @@ class GPTMLP(nn.Layer):
 
     def forward_nobias(self, x):
         t = _u(x)
-        hdn = K.bias_gelu(torch.matmul(t, self.fc1.weight._t), self.fc1.bias._t, self.approx)
-        return Tensor(torch.matmul(hdn, self.fc2.weight._t))
+        hdn = K.bias_gelu(K.linear(t, self.fc1.weight._t), self.fc1.bias._t, self.approx)
+        return Tensor(K.linear(hdn, self.fc2.weight._t))
 
     def forward(self, x):
         if self._fused:
             # GEMM without bias, then the fused bias+GELU HIP kernel (one pass over [T, 4h])
             t = _u(x)
-            hdn = torch.matmul(t, self.fc1.weight._t)
+            hdn = K.linear(t, self.fc1.weight._t)
             hdn = K.bias_gelu(hdn, self.fc1.bias._t, self.approx)
             return self.fc2(Tensor(hdn))
         return self.fc2(F.gelu(self.fc1(x), approximate=self.approx))

@@ -198,6 +198,9 @@ def gumbel_softmax(x, temperature=1.0, hard=False, axis=-1, name=None):
 def linear(x, weight, bias=None, name=None):
     """y = x @ W + b with paddle's [in, out] weight layout (hipBLASLt GEMM)."""
     t, w = _t(x), _t(weight)
+    if w.dim() == 2 and t.dim() >= 2 and t.dtype == w.dtype:
+        from ...ops import fused as _K
+        return _w(_K.linear(t, w, None if bias is None else _t(bias)))
     if bias is not None:
         b = _t(bias)
         if t.dim() == 2:

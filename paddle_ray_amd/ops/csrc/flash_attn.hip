@@ -27,6 +27,12 @@ namespace fa {
 
 __device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
+// s_waitcnt vmcnt(0) (expcnt/lgkmcnt left at max). Placed right after the per-wave
+// register fragments are loaded in the prologue: without it the waitcnt pass cannot prove
+// at the loop header that those prologue loads retired and puts a vmcnt(0) in front of the
+// FIRST MFMA of every iteration -- which then also waits for the NEXT tile's prefetch.
+__device__ __forceinline__ void wait_vmem_all() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
@@ -200,6 +206,7 @@ fwd_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restrict
 #pragma unroll
     for (int s = 0; s < NS; ++s) qf[s] = frag_global<T>(rowp, 16 * s + 8 * h, valid);
   }
+  wait_vmem_all();
 
   f32x16 acc_o[ND];
 #pragma unroll
@@ -348,6 +355,7 @@ bwd_dq_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restr
   }
   const float lse2 = qvalid ? lse[(int64_t)bh * Sq + myq] * LOG2E : INFINITY;
   const float dlt = qvalid ? delta[(int64_t)bh * Sq + myq] : 0.f;
+  wait_vmem_all();
 
   f32x16 acc_q[ND];
 #pragma unroll
@@ -475,6 +483,7 @@ bwd_dkdv_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __res
       vf[s] = frag_global<T>(vb_ + (int64_t)kk * vss, 16 * s + 8 * h, kvalid);
     }
   }
+  wait_vmem_all();
   f32x16 acc_k[ND], acc_v[ND];
 #pragma unroll
   for (int i = 0; i < ND; ++i) { acc_k[i] = f32x16{}; acc_v[i] = f32x16{}; }
@@ -490,7 +499,7 @@ bwd_dkdv_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __res
     dr.load(dob_, HD, qs0, Sq);
     if (threadIdx.x < kTile) {
       const int qq = qs0 + threadIdx.x;
-      lreg = qq < Sq ? lse[(int64_t)bh * Sq + qq] * LOG2E : INFINITY;
+      lreg = qq < Sq ? lse[(int64_t)bh * Sq + qq] : INFINITY;  // scaled at store (no wait here)
       dreg = qq < Sq ? delta[(int64_t)bh * Sq + qq] : 0.f;
     }
   };
@@ -499,7 +508,7 @@ bwd_dkdv_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __res
     qr.store_tr(Qt);
     dr.store_rows(Ds);
     dr.store_tr(Dt);
-    if (threadIdx.x < kTile) { Ls[threadIdx.x] = lreg; Dl[threadIdx.x] = dreg; }
+    if (threadIdx.x < kTile) { Ls[threadIdx.x] = lreg * LOG2E; Dl[threadIdx.x] = dreg; }
   };
   if (ntiles > 0) { load_tile(q_begin); store_tile(); }
   __syncthreads();

@@ -670,6 +670,57 @@ def flash_attention(q, k, v, causal=False, scale=None):
 
 
 # =============================================================================
+# Linear with fused weight-gradient accumulation
+# =============================================================================
+class LinearFn(torch.autograd.Function):
+    """y = x @ W (+ b) with paddle's [in, out] weight. The backward accumulates dW
+    straight into W's existing ``.grad`` (the flat DP/sharding gradient buffer, or the
+    zeroed grad after ``clear_grad``) with ONE beta=1 GEMM -- hipBLASLt reads C in its
+    epilogue -- instead of materialising dW and running AccumulateGrad's separate add
+    kernel. W's AccumulateGrad node still runs (with no gradient to add) and fires the
+    post-accumulate-grad hooks that trigger the bucketed all-reduce / reduce-scatter."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        x2 = x.reshape(-1, x.shape[-1])
+        y = torch.addmm(b, x2, w) if b is not None else torch.mm(x2, w)
+        ctx.save_for_backward(x)
+        ctx.w = w
+        ctx.has_b = b is not None
+        return y.view(*x.shape[:-1], w.shape[-1])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, = ctx.saved_tensors
+        w = ctx.w
+        dy2 = dy.reshape(-1, dy.shape[-1])
+        x2 = x.reshape(-1, x.shape[-1])
+        dx = torch.mm(dy2, w.t()).view(x.shape) if ctx.needs_input_grad[0] else None
+        dw = None
+        if ctx.needs_input_grad[1]:
+            g = w.grad
+            if (g is not None and not torch.is_grad_enabled() and g.shape == w.shape
+                    and g.dtype == dy2.dtype and g.is_contiguous()):
+                # returning None still runs W's AccumulateGrad node, which fires its
+                # post-accumulate hooks after this in-place accumulation
+                g.addmm_(x2.t(), dy2)
+            else:
+                dw = torch.mm(x2.t(), dy2)
+        db = dy2.sum(0) if ctx.has_b and ctx.needs_input_grad[2] else None
+        return dx, dw, db
+
+
+def linear(x, w, b=None):
+    """[.., in] @ [in, out] (+ b) with fused dW accumulation (see LinearFn)."""
+    if w.requires_grad and torch.is_grad_enabled() and w.is_leaf and x.dtype == w.dtype and \
+            not torch.is_autocast_enabled(x.device.type):
+        return LinearFn.apply(x, w, b)
+    x2 = x.reshape(-1, x.shape[-1])
+    y = torch.addmm(b, x2, w) if b is not None else torch.mm(x2, w)
+    return y.view(*x.shape[:-1], w.shape[-1])
+
+
+# =============================================================================
 # Multi-tensor fused AdamW / Adam / Momentum (one launch for all params)
 # =============================================================================
 def adamw_ref(params, grads, ms, vs, masters, lr, b1, b2, eps, wds, lr_muls, step, grad_scale=1.0):

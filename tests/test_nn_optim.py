@@ -300,3 +300,23 @@ def test_safe_loader_refuses_code(tmp_path):
         pickle.dump({'x': Evil()}, f)
     with pytest.raises(pickle.UnpicklingError):
         paddle.load(str(tmp_path / 'evil.pdparams'))
+
+
+def test_linear_fused_wgrad_accumulation_matches():
+    """LinearFn accumulates dW into an existing .grad (beta=1 GEMM) and fires hooks."""
+    import torch
+    from paddle_ray_amd.ops import fused as K
+    torch.manual_seed(0)
+    x = torch.randn(6, 5, 4, requires_grad=True)
+    w = torch.randn(4, 3, requires_grad=True)
+    b = torch.randn(3, requires_grad=True)
+    fired = []
+    w.register_post_accumulate_grad_hook(lambda t: fired.append(1))
+    w.grad = torch.full_like(w, 0.5)  # pre-existing grad (flat buffer / micro-batch accum)
+    K.linear(x, w, b).square().sum().backward()
+    xr, wr, br = (t.detach().clone().requires_grad_() for t in (x, w, b))
+    (xr @ wr + br).square().sum().backward()
+    torch.testing.assert_close(w.grad, wr.grad + 0.5)
+    torch.testing.assert_close(x.grad, xr.grad)
+    torch.testing.assert_close(b.grad, br.grad)
+    assert fired == [1]
