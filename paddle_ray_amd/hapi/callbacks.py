@@ -166,3 +166,18 @@ class ReduceLROnPlateau(Callback):
                 opt = self.model._optimizer
                 opt.set_lr(max(opt.get_lr() * self.factor, self.min_lr))
                 self.wait = 0
+
+
+class WandbCallback(Callback):
+    """Weights & Biases logging (wandb is not installed here: logs into ``self.history``)."""
+
+    def __init__(self, project=None, entity=None, name=None, dir=None, mode=None, job_type=None,
+                 **kwargs):
+        super().__init__()
+        self.history = []
+
+    def on_train_batch_end(self, step, logs=None):
+        self.history.append(dict(logs or {}))
+
+    def on_eval_end(self, logs=None):
+        self.history.append({'eval': dict(logs or {})})
