@@ -3,7 +3,8 @@
 Flags are seeded from ``FLAGS_*`` environment variables at import.
 Recognised: FLAGS_check_nan_inf (NaN/Inf checker on layer outputs and grads),
 FLAGS_cudnn_deterministic, FLAGS_eager_delete_tensor_gb, FLAGS_allocator_strategy,
-FLAGS_fraction_of_gpu_memory_to_use, FLAGS_call_stack_level, FLAGS_use_hip_kernels.
+FLAGS_fraction_of_gpu_memory_to_use, FLAGS_call_stack_level, FLAGS_use_hip_kernels,
+FLAGS_cudnn_exhaustive_search (MIOpen find-mode conv algorithm search, cached per shape).
 """
 import os
 
@@ -18,6 +19,7 @@ _FLAGS = {
     'FLAGS_use_hip_kernels': True,
     'FLAGS_embedding_deterministic': 0,
     'FLAGS_benchmark': False,
+    'FLAGS_cudnn_exhaustive_search': False,
 }
 
 
@@ -44,6 +46,9 @@ def set_flags(flags):
         if k == 'FLAGS_cudnn_deterministic':
             import torch
             torch.backends.cudnn.deterministic = bool(v)
+        if k == 'FLAGS_cudnn_exhaustive_search':
+            import torch
+            torch.backends.cudnn.benchmark = bool(v)
         if k in ('FLAGS_check_nan_inf', 'FLAGS_check_nan_inf_level'):
             _apply_nan_inf()
 

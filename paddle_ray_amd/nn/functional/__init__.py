@@ -6,6 +6,7 @@ rms_norm, softmax (last axis), softmax_with_cross_entropy / cross_entropy
 hipBLASLt / MIOpen through PyTorch-ROCm.
 """
 import math
+import os
 
 import numpy as np
 import torch
@@ -425,12 +426,36 @@ def _conv_padding(padding, n, t=None, ksize=None, stride=None, dilation=None):
     return _ntuple(padding, n), None
 
 
+# opt-in: measured slower on MI355X for ResNet50 (hipBLASLt has no split-K for the huge-K
+# wgrad GEMMs: 710 us vs MIOpen's 96 us), kept for A/B
+_CONV1X1_GEMM = os.environ.get('PRA_CONV1X1_GEMM', '0') == '1'
+
+
+def _conv1x1_gemm(t, w, bias, st):
+    """Channels-last 1x1 conv (pad 0, dilation 1, groups 1) as one hipBLASLt GEMM
+    [N*Ho*Wo, Cin] @ [Cin, Cout]: dgrad and wgrad are plain GEMMs too (no split-K atomics,
+    no workspace zero-fill), and the NHWC activation is read in place."""
+    if st != (1, 1):
+        t = t[:, ::st[0], ::st[1], :]
+    n, h, wd, cin = t.shape
+    cout = w.shape[0]
+    y = torch.mm(t.reshape(-1, cin), w.view(cout, cin).t())
+    if bias is not None:
+        y = y + bias
+    return y.view(n, h, wd, cout)
+
+
 def _conv(fn, n, x, weight, bias, stride, padding, dilation, groups, data_format):
     t = _t(x)
     cl = data_format in ('NHWC', 'NLC', 'NDHWC')
+    pad_, extra = _conv_padding(padding, n)
+    if (_CONV1X1_GEMM and n == 2 and cl and t.is_cuda and groups == 1 and extra is None
+            and _t(weight).shape[2:] == (1, 1) and _ntuple(dilation, 2) == (1, 1)
+            and pad_ in (0, (0, 0), [0, 0]) and t.dtype == _t(weight).dtype):
+        return _w(_conv1x1_gemm(t, _t(weight), None if bias is None else _t(bias),
+                                _ntuple(stride, 2)))
     if cl:
         t = t.movedim(-1, 1)
-    pad_, extra = _conv_padding(padding, n)
     if extra is not None:
         t = TF.pad(t, extra)
     w = _t(weight)
@@ -660,12 +685,16 @@ def rms_norm(x, weight=None, epsilon=1e-6, name=None):
 def batch_norm(x, running_mean, running_var, weight, bias, training=False, momentum=0.9,
                epsilon=1e-05, data_format='NCHW', use_global_stats=None, name=None):
     t = _t(x)
-    cl = data_format in ('NHWC', 'NLC', 'NDHWC')
-    if cl:
-        t = t.movedim(-1, 1)
+    cl = data_format in ('NHWC', 'NLC', 'NDHWC') or t.dim() == 2
     if use_global_stats:
         training = False
     rm, rv = _t(running_mean), _t(running_var)
+    if cl and t.is_cuda and t.shape[-1] % 8 == 0 and rm.dtype == torch.float32:
+        # channels-last on the device: gfx950 BN kernel (ops/csrc/bn.hip)
+        return _w(K.batch_norm_act(t, None, _opt(weight), _opt(bias), rm, rv, training,
+                                   momentum, epsilon, False))
+    if cl:
+        t = t.movedim(-1, 1)
     w = _opt(weight)
     if rm.dtype != t.dtype and not (w is not None and w.dtype == torch.float32):
         rm, rv = rm.to(t.dtype), rv.to(t.dtype)  # (mixed bf16-in/fp32-param runs natively)
@@ -673,6 +702,27 @@ def batch_norm(x, running_mean, running_var, weight, bias, training=False, momen
     if cl:
         out = out.movedim(1, -1)
     return _w(out)
+
+
+def fused_bn_add_act(x, z, running_mean, running_var, weight, bias, training=False, momentum=0.9,
+                     epsilon=1e-05, act='relu', data_format='NHWC'):
+    """act(batch_norm(x) + z) in one pass (parity: fluid/operators/fused/
+    fused_bn_add_activation_op.cu; ``z=None`` is fused_bn_activation). Channels-last on the
+    device runs the gfx950 kernel; other layouts compose."""
+    if act not in (None, 'relu', 'identity'):
+        raise ValueError(f"fused_bn_add_act: unsupported act {act!r}")
+    relu = act == 'relu'
+    t = _t(x)
+    rm, rv = _t(running_mean), _t(running_var)
+    cl = data_format in ('NHWC', 'NLC', 'NDHWC') or t.dim() == 2
+    if cl and rm.dtype == torch.float32 and (t.shape[-1] % 8 == 0 or not t.is_cuda):
+        return _w(K.batch_norm_act(t, _opt(z), _opt(weight), _opt(bias), rm, rv, training,
+                                   momentum, epsilon, relu))
+    out = _t(batch_norm(x, running_mean, running_var, weight, bias, training, momentum, epsilon,
+                        data_format))
+    if z is not None:
+        out = out + _t(z)
+    return _w(torch.relu(out) if relu else out)
 
 
 def instance_norm(x, running_mean=None, running_var=None, weight=None, bias=None,

@@ -43,6 +43,13 @@ int pra_flash_fwd(const void*, const void*, const void*, void*, float*, int, int
                   int, int, hipStream_t);
 int pra_flash_bwd(const void*, const void*, const void*, const void*, const float*, const float*, void*, void*, void*,
                   int, int, int, int, int, const int64_t*, float, int, int, hipStream_t);
+int pra_bn_nrb(int, int);
+void pra_bn_fwd_train(const void*, const void*, const void*, const void*, float*, float*, void*, uint8_t*, float*,
+                      float*, float*, float*, int, int, int, float, float, int, int, int, hipStream_t);
+void pra_bn_fwd_infer(const void*, const void*, const void*, const void*, const float*, const float*, void*, float*,
+                      int, int, float, int, int, int, hipStream_t);
+void pra_bn_bwd(const void*, const void*, const uint8_t*, const void*, const void*, const float*, const float*, void*,
+                void*, void*, void*, float*, float*, int, int, int, int, int, int, hipStream_t);
 }
 
 #define V(x) reinterpret_cast<void*>(x)
@@ -153,5 +160,23 @@ PYBIND11_MODULE(_pra_hip, m) {
                       scale, causal, dt, S(s)) != 0)
       throw std::invalid_argument("flash_bwd: unsupported head_dim/dtype");
     check_launch("flash_bwd");
+  });
+  m.def("bn_nrb", [](int M, int C) { return pra_bn_nrb(M, C); });
+  m.def("bn_fwd_train", [](P x, P z, P w, P b, P rm, P rv, P y, P mask, P mean, P invstd, P part, P coef, int M,
+                           int C, int nrb, float eps, float mom, int relu, int dt, int dtw, P s) {
+    pra_bn_fwd_train(CV(x), CV(z), CV(w), CV(b), F(rm), F(rv), V(y), reinterpret_cast<uint8_t*>(mask), F(mean),
+                     F(invstd), F(part), F(coef), M, C, nrb, eps, mom, relu, dt, dtw, S(s));
+    check_launch("bn_fwd_train");
+  });
+  m.def("bn_fwd_infer", [](P x, P z, P w, P b, P rm, P rv, P y, P coef, int M, int C, float eps, int relu, int dt,
+                           int dtw, P s) {
+    pra_bn_fwd_infer(CV(x), CV(z), CV(w), CV(b), CF(rm), CF(rv), V(y), F(coef), M, C, eps, relu, dt, dtw, S(s));
+    check_launch("bn_fwd_infer");
+  });
+  m.def("bn_bwd", [](P dy, P y, P mask, P x, P w, P mean, P invstd, P dx, P dz, P dw, P db, P part, P coef, int M,
+                     int C, int nrb, int relu, int dt, int dtw, P s) {
+    pra_bn_bwd(CV(dy), CV(y), reinterpret_cast<const uint8_t*>(mask), CV(x), CV(w), CF(mean), CF(invstd), V(dx), V(dz),
+               V(dw), V(db), F(part), F(coef), M, C, nrb, relu, dt, dtw, S(s));
+    check_launch("bn_bwd");
   });
 }

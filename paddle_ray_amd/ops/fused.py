@@ -827,3 +827,149 @@ def global_l2_norm_sq(tensors):
             L.sumsq_accum(_ptr(t), _ptr(out), t.numel(), _dt(t), _stream())
         return out[0]
     return sum((t.float() ** 2).sum() for t in tensors)
+
+
+# =============================================================================
+# BatchNorm (+ residual add + ReLU), channels-last [M, C]
+# parity: paddle/phi/kernels/gpu/batch_norm_kernel.cu, batch_norm_grad_kernel.cu,
+#         paddle/fluid/operators/fused/fused_bn_add_activation_op.cu (y = act(BN(x) + z))
+# =============================================================================
+@R.register_kernel('batch_norm_fwd', 'ref')
+def _bn_fwd_ref(x2, z2, w, b, rmean, rvar, training, momentum, eps, relu):
+    xf = x2.float()
+    if training:
+        mean = xf.mean(0)
+        var = xf.var(0, unbiased=False)
+        if rmean is not None:
+            m = x2.shape[0]
+            with torch.no_grad():
+                rmean.mul_(momentum).add_(mean, alpha=1 - momentum)
+                rvar.mul_(momentum).add_(var * (m / max(m - 1, 1)), alpha=1 - momentum)
+    else:
+        mean, var = rmean.float(), rvar.float()
+    invstd = torch.rsqrt(var + eps)
+    y = (xf - mean) * invstd
+    if w is not None:
+        y = y * w.float()
+    if b is not None:
+        y = y + b.float()
+    if z2 is not None:
+        y = y + z2.float()
+    if relu:
+        y = torch.relu(y)
+    return y.to(x2.dtype), mean, invstd, None
+
+
+@R.register_kernel('batch_norm_bwd', 'ref')
+def _bn_bwd_ref(dy, y, mask, x2, w, mean, invstd, relu, need_dz):
+    g = dy.float()
+    if relu:
+        g = torch.where(y > 0, g, torch.zeros_like(g))
+    xhat = (x2.float() - mean) * invstd
+    m = x2.shape[0]
+    s1 = g.sum(0)
+    s2 = (g * xhat).sum(0)
+    a = (w.float() if w is not None else 1.0) * invstd
+    dx = a * (g - s1 / m - xhat * s2 / m)
+    pdt = w.dtype if w is not None else torch.float32
+    dz = g.to(x2.dtype) if need_dz else None
+    return dx.to(x2.dtype), dz, s2.to(pdt), s1.to(pdt)
+
+
+def _bn_hip_ok(x2):
+    return x2.shape[1] % 8 == 0 and x2.numel() // 8 < 2 ** 32 and x2.is_contiguous()
+
+
+@R.register_kernel('batch_norm_fwd', 'hip')
+def _bn_fwd_hip(x2, z2, w, b, rmean, rvar, training, momentum, eps, relu):
+    """Returns (y, mean, invstd, relu keep-mask bytes or None)."""
+    if not _bn_hip_ok(x2):
+        return _bn_fwd_ref(x2, z2, w, b, rmean, rvar, training, momentum, eps, relu)
+    L = _native.lib()
+    M, C = x2.shape
+    dev = x2.device
+    y = torch.empty_like(x2)
+    dtw = _dt(w) if w is not None else 0
+    z2 = z2.contiguous() if z2 is not None else None
+    if training:
+        nrb = L.bn_nrb(M, C)
+        part = torch.empty((2, nrb, C), device=dev, dtype=torch.float32)
+        stat = torch.empty((4, C), device=dev, dtype=torch.float32)  # mean | invstd | scale | shift
+        mask = torch.empty(M * C // 8, device=dev, dtype=torch.uint8) if relu else None
+        L.bn_fwd_train(_ptr(x2), _ptr(z2), _ptr(w), _ptr(b), _ptr(rmean), _ptr(rvar), _ptr(y),
+                       _ptr(mask), _ptr(stat[0]), _ptr(stat[1]), _ptr(part), _ptr(stat[2]), M, C,
+                       nrb, float(eps), float(momentum), int(relu), _dt(x2), dtw, _stream())
+        return y, stat[0], stat[1], mask
+    coef = torch.empty((2, C), device=dev, dtype=torch.float32)
+    L.bn_fwd_infer(_ptr(x2), _ptr(z2), _ptr(w), _ptr(b), _ptr(rmean), _ptr(rvar), _ptr(y),
+                   _ptr(coef), M, C, float(eps), int(relu), _dt(x2), dtw, _stream())
+    mean = rmean.float()
+    return y, mean, torch.rsqrt(rvar.float() + eps), None
+
+
+@R.register_kernel('batch_norm_bwd', 'hip')
+def _bn_bwd_hip(dy, y, mask, x2, w, mean, invstd, relu, need_dz):
+    if not _bn_hip_ok(x2):
+        return _bn_bwd_ref(dy, y, mask, x2, w, mean, invstd, relu, need_dz)
+    L = _native.lib()
+    M, C = x2.shape
+    dev = x2.device
+    dy = dy.contiguous()
+    dx = torch.empty_like(x2)
+    dz = None
+    if need_dz:
+        dz = torch.empty_like(x2) if relu else dy
+    pdt = w.dtype if w is not None else torch.float32
+    dwb = torch.empty((2, C), device=dev, dtype=pdt)
+    nrb = L.bn_nrb(M, C)
+    part = torch.empty((2, nrb, C), device=dev, dtype=torch.float32)
+    coef = torch.empty((3, C), device=dev, dtype=torch.float32)
+    L.bn_bwd(_ptr(dy), _ptr(y) if relu else 0, _ptr(mask) if relu else 0, _ptr(x2), _ptr(w), _ptr(mean), _ptr(invstd),
+             _ptr(dx), _ptr(dz) if (need_dz and relu) else 0, _ptr(dwb[0]), _ptr(dwb[1]),
+             _ptr(part), _ptr(coef), M, C, nrb, int(relu), _dt(x2), _DT[pdt], _stream())
+    return dx, dz, dwb[0], dwb[1]
+
+
+class BatchNormActFn(torch.autograd.Function):
+    """y = act(BN(x) + z) over channels-last x[..., C]; running stats updated in place."""
+
+    @staticmethod
+    def forward(ctx, x, z, w, b, rmean, rvar, training, momentum, eps, relu):
+        shp = x.shape
+        C = shp[-1]
+        x2 = x.contiguous().view(-1, C)
+        z2 = z.reshape(-1, C) if z is not None else None
+        y, mean, invstd, mask = R.dispatch('batch_norm_fwd', x2, x2, z2, w, b, rmean, rvar,
+                                           training, momentum, eps, relu)
+        # ReLU backward needs only the keep-bits (1 B per 8 channels) when the kernel wrote them
+        ctx.save_for_backward(x2, y if (relu and mask is None) else None, mask, w, mean, invstd)
+        ctx.relu, ctx.shp, ctx.has_z = relu, shp, z is not None
+        ctx.has_b, ctx.training = b is not None, training
+        return y.view(shp)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, y, mask, w, mean, invstd = ctx.saved_tensors
+        dy2 = dy.contiguous().view(x2.shape)
+        if not ctx.training:  # frozen statistics: dx = dy * w * invstd
+            g = dy2.float()
+            if ctx.relu:
+                g = torch.where(y > 0, g, torch.zeros_like(g))
+            a = invstd * (w.float() if w is not None else 1.0)
+            pdt = w.dtype if w is not None else torch.float32
+            dw = (g * (x2.float() - mean) * invstd).sum(0).to(pdt)
+            dz = g.to(x2.dtype).view(ctx.shp) if ctx.has_z else None
+            return ((g * a).to(x2.dtype).view(ctx.shp), dz, dw if w is not None else None,
+                    g.sum(0).to(pdt) if ctx.has_b else None, None, None, None, None, None, None)
+        dx, dz, dw, db = R.dispatch('batch_norm_bwd', x2, dy2, y, mask, x2, w, mean, invstd, ctx.relu,
+                                    ctx.has_z and ctx.needs_input_grad[1])
+        return (dx.view(ctx.shp), dz.view(ctx.shp) if dz is not None else None,
+                dw if (w is not None and ctx.needs_input_grad[2]) else None,
+                db if (ctx.has_b and ctx.needs_input_grad[3]) else None,
+                None, None, None, None, None, None)
+
+
+def batch_norm_act(x, z, w, b, rmean, rvar, training, momentum=0.9, eps=1e-5, relu=False):
+    """Channels-last BatchNorm with optional fused residual add and ReLU (paddle momentum
+    convention: running = momentum * running + (1 - momentum) * batch)."""
+    return BatchNormActFn.apply(x, z, w, b, rmean, rvar, training, momentum, eps, relu)

@@ -4,6 +4,20 @@
 MIOpen's fast bf16 conv kernels want on MI355X (no NCHW<->NHWC transposes).
 """
 from ... import nn
+from ...nn import functional as F
+
+
+def _bn_act(bn, x, z=None, act='relu'):
+    """act(bn(x) + z) through the fused BN(+add)(+ReLU) op (one read of x, one write of y on
+    the gfx950 channels-last path; parity: fused_bn_add_activation_op)."""
+    if isinstance(bn, nn.SyncBatchNorm) or not isinstance(bn, nn.layer.norm._BatchNormBase):
+        out = bn(x)
+        if z is not None:
+            out = out + z
+        return F.relu(out) if act == 'relu' else out
+    return F.fused_bn_add_act(x, z, bn._mean, bn._variance, bn.weight, bn.bias,
+                              bn.training and not bn._use_global_stats, bn._momentum, bn._epsilon,
+                              act, bn._data_format)
 
 
 class BasicBlock(nn.Layer):
@@ -25,11 +39,10 @@ class BasicBlock(nn.Layer):
 
     def forward(self, x):
         identity = x
-        out = self.relu(self.bn1(self.conv1(x)))
-        out = self.bn2(self.conv2(out))
+        out = _bn_act(self.bn1, self.conv1(x))
         if self.downsample is not None:
             identity = self.downsample(x)
-        return self.relu(out + identity)
+        return _bn_act(self.bn2, self.conv2(out), identity)
 
 
 class BottleneckBlock(nn.Layer):
@@ -54,12 +67,11 @@ class BottleneckBlock(nn.Layer):
 
     def forward(self, x):
         identity = x
-        out = self.relu(self.bn1(self.conv1(x)))
-        out = self.relu(self.bn2(self.conv2(out)))
-        out = self.bn3(self.conv3(out))
+        out = _bn_act(self.bn1, self.conv1(x))
+        out = _bn_act(self.bn2, self.conv2(out))
         if self.downsample is not None:
             identity = self.downsample(x)
-        return self.relu(out + identity)
+        return _bn_act(self.bn3, self.conv3(out), identity)
 
 
 class ResNet(nn.Layer):
@@ -106,7 +118,7 @@ class ResNet(nn.Layer):
         return nn.Sequential(*layers)
 
     def forward(self, x):
-        x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
+        x = self.maxpool(_bn_act(self.bn1, self.conv1(x)))
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         if self.with_pool:
             x = self.avgpool(x)

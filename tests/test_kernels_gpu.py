@@ -252,3 +252,88 @@ def test_flash_attention_qkvpacked(D):
     assert (o.float() - orf).abs().max().item() < 4e-2
     err = (qkv.grad.float() - ref.grad).abs().max().item()
     assert err < 8e-2 * max(1.0, ref.grad.abs().max().item()), err
+
+
+def _bn_ref(x, z, w, b, relu, eps):
+    xf = x.float()
+    mean = xf.mean(0)
+    var = xf.var(0, unbiased=False)
+    y = (xf - mean) * torch.rsqrt(var + eps) * w + b
+    if z is not None:
+        y = y + z.float()
+    return torch.relu(y) if relu else y, mean, var
+
+
+@pytest.mark.parametrize('dt', [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize('M,C', [(4096, 64), (3 * 7 * 7, 2048), (1000, 256), (50, 24)])
+@pytest.mark.parametrize('relu,res', [(False, False), (True, False), (True, True)])
+def test_batch_norm_act(dt, M, C, relu, res):
+    torch.manual_seed(0)
+    x = (torch.randn(M, C, device=DEV) * 2 + 3).to(dt).requires_grad_()
+    z = torch.randn(M, C, device=DEV, dtype=dt, requires_grad=True) if res else None
+    w = torch.rand(C, device=DEV, requires_grad=True)
+    b = torch.randn(C, device=DEV, requires_grad=True)
+    rm, rv = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+    R.reset_stats()
+    y = F.batch_norm_act(x, z, w, b, rm, rv, True, 0.9, 1e-5, relu)
+    if C % 8 == 0:
+        assert R.stats().get(('batch_norm_fwd', 'hip'), 0) == 1
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    xr = x.detach().float().requires_grad_()
+    zr = z.detach().float().requires_grad_() if res else None
+    wr, br = w.detach().clone().requires_grad_(), b.detach().clone().requires_grad_()
+    yr, mean, var = _bn_ref(xr, zr, wr, br, relu, 1e-5)
+    yr.backward(dy.float())
+    tol = _tol(dt)
+    assert torch.allclose(y.float(), yr, atol=tol * 4, rtol=tol)
+    assert torch.allclose(rm, 0.1 * mean, atol=1e-4, rtol=1e-4)
+    assert torch.allclose(rv, 0.9 + 0.1 * var * M / (M - 1), atol=1e-4, rtol=1e-4)
+    assert torch.allclose(x.grad.float(), xr.grad, atol=tol * 8, rtol=tol * 4)
+    assert torch.allclose(w.grad, wr.grad, atol=tol * 40 * math.sqrt(M) / 8, rtol=tol * 4)
+    assert torch.allclose(b.grad, br.grad, atol=tol * 40 * math.sqrt(M) / 8, rtol=tol * 4)
+    if res:
+        assert torch.allclose(z.grad.float(), zr.grad, atol=tol * 4, rtol=tol)
+
+
+def test_batch_norm_infer():
+    C = 128
+    x = torch.randn(300, C, device=DEV, dtype=torch.bfloat16)
+    w, b = torch.rand(C, device=DEV), torch.randn(C, device=DEV)
+    rm, rv = torch.randn(C, device=DEV), torch.rand(C, device=DEV) + 0.5
+    y = F.batch_norm_act(x, None, w, b, rm, rv, False, 0.9, 1e-5, True)
+    yr = torch.relu((x.float() - rm) * torch.rsqrt(rv + 1e-5) * w + b)
+    assert torch.allclose(y.float(), yr, atol=0.05, rtol=0.02)
+
+
+def test_resnet_block_uses_fused_bn():
+    import paddle_ray_amd as paddle
+    from paddle_ray_amd.vision.models import resnet50
+    paddle.set_device('gpu:0')
+    m = resnet50(data_format='NHWC', num_classes=10)
+    m = paddle.amp.decorate(m, level='O2', dtype='bfloat16')
+    x = paddle.Tensor(torch.randn(4, 64, 64, 3, device=DEV, dtype=torch.bfloat16))
+    R.reset_stats()
+    out = m(x)
+    out.sum().backward()
+    st = R.stats()
+    assert st.get(('batch_norm_fwd', 'hip'), 0) == 53 and st.get(('batch_norm_bwd', 'hip'), 0) == 53, st
+
+
+@pytest.mark.parametrize('stride', [1, 2])
+def test_conv1x1_gemm_path(stride, monkeypatch):
+    import paddle_ray_amd as paddle
+    import paddle_ray_amd.nn.functional as PF
+    monkeypatch.setattr(PF, '_CONV1X1_GEMM', True)
+    x = torch.randn(4, 14, 14, 64, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    w = torch.randn(128, 64, 1, 1, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    y = PF.conv2d(paddle.Tensor(x), paddle.Tensor(w), stride=stride, data_format='NHWC')._t
+    yr = torch.nn.functional.conv2d(x.float().permute(0, 3, 1, 2), w.float(), stride=stride)
+    yr = yr.permute(0, 2, 3, 1)
+    assert y.shape == yr.shape
+    assert torch.allclose(y.float(), yr, atol=0.1, rtol=0.02)
+    dy = torch.randn_like(y)
+    gx, gw = torch.autograd.grad(y, [x, w], dy)
+    gxr, gwr = torch.autograd.grad(yr, [x, w], dy.float())
+    assert torch.allclose(gx.float(), gxr.float(), atol=0.1, rtol=0.02)
+    assert torch.allclose(gw.float(), gwr.float(), atol=0.5, rtol=0.02)

@@ -320,3 +320,24 @@ def test_linear_fused_wgrad_accumulation_matches():
     torch.testing.assert_close(x.grad, xr.grad)
     torch.testing.assert_close(b.grad, br.grad)
     assert fired == [1]
+
+
+def test_fused_bn_add_act_matches_composition():
+    import paddle_ray_amd as paddle
+    import paddle_ray_amd.nn.functional as F
+    paddle.seed(0)
+    bn = paddle.nn.BatchNorm2D(16, data_format='NHWC')
+    bn2 = paddle.nn.BatchNorm2D(16, data_format='NHWC')
+    bn2.set_state_dict(bn.state_dict())
+    x = paddle.randn([4, 5, 5, 16])
+    z = paddle.randn([4, 5, 5, 16])
+    x.stop_gradient = False
+    y1 = F.fused_bn_add_act(x, z, bn._mean, bn._variance, bn.weight, bn.bias, True, 0.9, 1e-5,
+                            'relu', 'NHWC')
+    y2 = F.relu(bn2(x) + z)
+    np.testing.assert_allclose(y1.numpy(), y2.numpy(), rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(bn._mean.numpy(), bn2._mean.numpy(), rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(bn._variance.numpy(), bn2._variance.numpy(), rtol=1e-5, atol=1e-6)
+    g1 = paddle.grad(y1.sum(), [x])[0]
+    g2 = paddle.grad(y2.sum(), [x])[0]
+    np.testing.assert_allclose(g1.numpy(), g2.numpy(), rtol=1e-4, atol=1e-5)
