@@ -34,6 +34,8 @@ def parse():
     p.add_argument('--dropout', type=float, default=0.1)
     p.add_argument('--recompute', action='store_true')
     p.add_argument('--profile-dir', default=None)
+    p.add_argument('--no-tuned-gemms', action='store_true',
+                   help='skip the committed MI355X TunableOp GEMM solutions')
     return p.parse_args()
 
 
@@ -53,6 +55,9 @@ def main():
     if dev.type == 'cuda':
         paddle.set_device(f'gpu:{dev.index}')
     paddle.seed(1234 + rank)
+    if dev.type == 'cuda' and not a.no_tuned_gemms:
+        from paddle_ray_amd.incubate import autotune
+        autotune.use_tuned_gemms()  # paddle_ray_amd/tuning/gemm_gfx950.csv (if present)
 
     if a.model.startswith('gpt'):
         result = bench_gpt(a, paddle, torch, dist, C, world, rank, dev)

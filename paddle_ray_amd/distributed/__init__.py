@@ -24,3 +24,5 @@ class ParallelMode:
 
 from . import io  # noqa
 from . import watchdog  # noqa: E402
+from . import models  # noqa: E402
+from . import utils  # noqa: E402

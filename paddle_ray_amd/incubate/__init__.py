@@ -1,7 +1,14 @@
 """paddle.incubate (parity: python/paddle/incubate/__init__.py)."""
 from . import nn  # noqa
 from . import autograd  # noqa
+from . import autotune  # noqa
+from . import distributed  # noqa
+from . import optimizer  # noqa
+from .optimizer import LookAhead, ModelAverage, DistributedFusedLamb  # noqa
 from .nn.functional import fused_dropout_add  # noqa
+from ..geometric import (segment_sum, segment_mean, segment_max, segment_min,  # noqa
+                         send_u_recv as graph_send_recv, reindex_graph as graph_reindex,
+                         sample_neighbors as graph_sample_neighbors)
 
 
 def softmax_mask_fuse(x, mask, name=None):

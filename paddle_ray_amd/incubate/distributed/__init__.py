@@ -1,0 +1,2 @@
+"""paddle.incubate.distributed (parity: python/paddle/incubate/distributed/)."""
+from . import models  # noqa: F401

@@ -123,6 +123,8 @@ class Optimizer:
         if clip is None:
             return None
         from ..nn.clip import ClipGradByGlobalNorm
+        if hasattr(clip, 'coefficient_from_params'):  # e.g. MoE clip: needs param identity
+            return clip.coefficient_from_params([(p, p._t.grad) for p, g in pgs])
         if isinstance(clip, ClipGradByGlobalNorm):
             grads = [p._t.grad for p, g in pgs if getattr(p, 'need_clip', True)]
             return clip.coefficient(grads)
