@@ -258,10 +258,12 @@ def one_hot(x, num_classes, name=None):
 
 
 def embedding(x, weight, padding_idx=None, sparse=False, name=None):
+    """Row lookup (gfx950 kernel on the device; rows of ``padding_idx`` read as zeros and
+    receive no gradient, as in paddle's lookup_table_v2)."""
     w = _t(weight)
     if padding_idx is not None and padding_idx < 0:
         padding_idx += w.shape[0]
-    return _w(TF.embedding(_t(x).long(), w, padding_idx))
+    return _w(K.embedding(_t(x).long(), w, padding_idx))
 
 
 def pad(x, pad, mode='constant', value=0.0, data_format='NCHW', name=None):

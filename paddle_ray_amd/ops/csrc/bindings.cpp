@@ -43,6 +43,9 @@ int pra_flash_fwd(const void*, const void*, const void*, void*, float*, int, int
                   int, int, hipStream_t);
 int pra_flash_bwd(const void*, const void*, const void*, const void*, const float*, const float*, void*, void*, void*,
                   int, int, int, int, int, const int64_t*, float, int, int, hipStream_t);
+int pra_embedding_fwd(const int64_t*, const void*, void*, int64_t, int, int64_t, int64_t, int, hipStream_t);
+int pra_embedding_bwd(const int64_t*, const int64_t*, const void*, void*, int64_t, int, int64_t, int64_t, int, int,
+                      int, hipStream_t);
 int pra_bn_nrb(int, int);
 void pra_bn_fwd_train(const void*, const void*, const void*, const void*, float*, float*, void*, uint8_t*, float*,
                       float*, float*, float*, int, int, int, float, float, int, int, int, hipStream_t);
@@ -178,5 +181,16 @@ PYBIND11_MODULE(_pra_hip, m) {
     pra_bn_bwd(CV(dy), CV(y), reinterpret_cast<const uint8_t*>(mask), CV(x), CV(w), CF(mean), CF(invstd), V(dx), V(dz),
                V(dw), V(db), F(part), F(coef), M, C, nrb, relu, dt, dtw, S(s));
     check_launch("bn_bwd");
+  });
+  m.def("embedding_fwd", [](P ids, P w, P out, int64_t n, int D, int64_t V, int64_t pad, int dt, P s) {
+    if (pra_embedding_fwd(I64(ids), CV(w), V(out), n, D, V, pad, dt, S(s)) != 0)
+      throw std::invalid_argument("embedding_fwd: unsupported D/dtype");
+    check_launch("embedding_fwd");
+  });
+  m.def("embedding_bwd", [](P sids, P perm, P dy, P dw, int64_t n, int D, int64_t V, int64_t pad, int dtg, int dtw,
+                            int acc, P s) {
+    if (pra_embedding_bwd(I64(sids), I64(perm), CV(dy), V(dw), n, D, V, pad, dtg, dtw, acc, S(s)) != 0)
+      throw std::invalid_argument("embedding_bwd: unsupported D/dtype");
+    check_launch("embedding_bwd");
   });
 }

@@ -973,3 +973,93 @@ def batch_norm_act(x, z, w, b, rmean, rvar, training, momentum=0.9, eps=1e-5, re
     """Channels-last BatchNorm with optional fused residual add and ReLU (paddle momentum
     convention: running = momentum * running + (1 - momentum) * batch)."""
     return BatchNormActFn.apply(x, z, w, b, rmean, rvar, training, momentum, eps, relu)
+
+
+# =============================================================================
+# Embedding lookup (parity: paddle/phi/kernels/gpu/embedding_kernel.cu,
+# embedding_grad_kernel.cu); ids outside [0, V) or == padding_idx read as zero rows
+# =============================================================================
+@R.register_kernel('embedding_fwd', 'ref')
+def _emb_fwd_ref(ids, w, pad):
+    V = w.shape[0]
+    ok = (ids >= 0) & (ids < V)
+    if pad is not None and pad >= 0:
+        ok = ok & (ids != pad)
+    out = torch.nn.functional.embedding(torch.where(ok, ids, torch.zeros_like(ids)), w)
+    return out * ok.unsqueeze(-1).to(out.dtype)
+
+
+@R.register_kernel('embedding_bwd', 'ref')
+def _emb_bwd_ref(ids, dy, w_shape, w_dtype, pad, into=None):
+    V, D = w_shape
+    flat = ids.reshape(-1)
+    ok = (flat >= 0) & (flat < V)
+    if pad is not None and pad >= 0:
+        ok = ok & (flat != pad)
+    g = torch.zeros(w_shape, dtype=torch.float32, device=dy.device)
+    g.index_add_(0, flat[ok], dy.reshape(-1, D)[ok].float())
+    if into is not None:
+        into.add_(g.to(into.dtype))
+        return into
+    return g.to(w_dtype)
+
+
+@R.register_kernel('embedding_fwd', 'hip')
+def _emb_fwd_hip(ids, w, pad):
+    D = w.shape[1]
+    if D % 8 != 0 or not w.is_contiguous():
+        return _emb_fwd_ref(ids, w, pad)
+    ids_c = ids.reshape(-1).contiguous().long()
+    out = torch.empty((ids_c.numel(), D), device=w.device, dtype=w.dtype)
+    _native.lib().embedding_fwd(_ptr(ids_c), _ptr(w), _ptr(out), ids_c.numel(), D, w.shape[0],
+                                -1 if pad is None else int(pad), _dt(w), _stream())
+    return out.view(*ids.shape, D)
+
+
+@R.register_kernel('embedding_bwd', 'hip')
+def _emb_bwd_hip(ids, dy, w_shape, w_dtype, pad, into=None):
+    V, D = w_shape
+    tgt_dt = into.dtype if into is not None else w_dtype
+    if D % 8 != 0 or D > 4096 or (dy.dtype, tgt_dt) not in (
+            (torch.bfloat16, torch.bfloat16), (torch.bfloat16, torch.float32),
+            (torch.float32, torch.float32), (torch.float16, torch.float16),
+            (torch.float16, torch.float32)):
+        return _emb_bwd_ref(ids, dy, w_shape, w_dtype, pad, into)
+    flat = ids.reshape(-1).long()
+    sids, perm = torch.sort(flat, stable=True)
+    dy2 = dy.reshape(-1, D).contiguous()
+    out = into if into is not None else torch.zeros(w_shape, dtype=w_dtype, device=dy.device)
+    _native.lib().embedding_bwd(_ptr(sids), _ptr(perm), _ptr(dy2), _ptr(out), flat.numel(), D, V,
+                                -1 if pad is None else int(pad), _dt(dy2), _DT[out.dtype],
+                                1, _stream())
+    return out
+
+
+class EmbeddingFn(torch.autograd.Function):
+    """Lookup whose backward adds straight into the table's existing ``.grad`` (the flat
+    DP/sharding grad buffer) when there is one, like LinearFn: no dense [V, D] gradient
+    temporary, no AccumulateGrad add pass."""
+
+    @staticmethod
+    def forward(ctx, ids, w, pad):
+        ctx.save_for_backward(ids)
+        ctx.w, ctx.pad = w, pad
+        return R.dispatch('embedding_fwd', w, ids, w, pad)
+
+    @staticmethod
+    def backward(ctx, dy):
+        ids, = ctx.saved_tensors
+        w = ctx.w
+        g = w.grad
+        if (g is not None and not torch.is_grad_enabled() and g.shape == w.shape and
+                g.is_contiguous()):
+            R.dispatch('embedding_bwd', w, ids, dy, tuple(w.shape), w.dtype, ctx.pad, g)
+            return None, None, None
+        return None, R.dispatch('embedding_bwd', w, ids, dy, tuple(w.shape), w.dtype, ctx.pad), \
+            None
+
+
+def embedding(ids, w, padding_idx=None):
+    if w.requires_grad and torch.is_grad_enabled():
+        return EmbeddingFn.apply(ids, w, padding_idx)
+    return R.dispatch('embedding_fwd', w, ids, w, padding_idx)

@@ -337,3 +337,41 @@ def test_conv1x1_gemm_path(stride, monkeypatch):
     gxr, gwr = torch.autograd.grad(yr, [x, w], dy.float())
     assert torch.allclose(gx.float(), gxr.float(), atol=0.1, rtol=0.02)
     assert torch.allclose(gw.float(), gwr.float(), atol=0.5, rtol=0.02)
+
+
+@pytest.mark.parametrize('dt', [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize('D', [2048, 64, 1000])
+def test_embedding_fwd_bwd(dt, D):
+    torch.manual_seed(0)
+    V = 300
+    ids = torch.randint(0, V, (6, 50), device=DEV)
+    ids[0, :10] = 7          # a long run of one id
+    ids[1, 0] = 5            # padding row
+    w = torch.randn(V, D, device=DEV, dtype=dt, requires_grad=True)
+    R.reset_stats()
+    out = F.embedding(ids, w, 5)
+    if D % 8 == 0:
+        assert R.stats().get(('embedding_fwd', 'hip'), 0) == 1
+    keep = (ids != 5).unsqueeze(-1)
+    ref = torch.nn.functional.embedding(ids, w.detach().float()) * keep
+    assert torch.equal(out.float(), ref)
+    dy = torch.randn_like(out)
+    out.backward(dy)
+    gref = torch.zeros(V, D, device=DEV)
+    gref.index_add_(0, ids.reshape(-1), (dy.float() * keep).reshape(-1, D))
+    tol = _tol(dt) * 10
+    assert torch.allclose(w.grad.float(), gref, atol=tol, rtol=tol)
+    # second backward accumulates into the existing grad in place
+    out2 = F.embedding(ids, w, 5)
+    with torch.no_grad():
+        g0 = w.grad.clone()
+    out2.backward(dy)
+    assert torch.allclose(w.grad.float(), g0.float() + gref, atol=2 * tol, rtol=tol)
+
+
+def test_embedding_out_of_range_reads_zero():
+    w = torch.randn(10, 16, device=DEV)
+    ids = torch.tensor([[0, 9, 10, -1, 1000]], device=DEV)
+    out = F.embedding(ids, w, None)
+    assert torch.equal(out[0, 2:], torch.zeros(3, 16, device=DEV))
+    assert torch.equal(out[0, :2], w[[0, 9]])
