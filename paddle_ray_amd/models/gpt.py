@@ -256,7 +256,7 @@ class GPTForPretraining(nn.Layer):
             h = _u(_mp()._c_identity(Tensor(h), self.gpt.embeddings.word_embeddings
                                      .model_parallel_group))
         B, S, H = h.shape
-        logits = torch.matmul(h.reshape(B * S, H), w.t())
+        logits = K.linear_nt(h.reshape(B * S, H), w)  # tied head, dW accumulated in place
         if labels is None:
             return Tensor(logits.view(B, S, -1))
         lab = _u(labels).reshape(-1)

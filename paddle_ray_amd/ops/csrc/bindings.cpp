@@ -29,8 +29,9 @@ void pra_softmax_ce_bwd(const void*, const int64_t*, const float*, const float*,
 void pra_bias_gelu_fwd(const void*, const void*, void*, int64_t, int, int, int, hipStream_t);
 void pra_bias_gelu_bwd(const void*, const void*, const void*, void*, int64_t, int, int, int, hipStream_t);
 void pra_adamw_mt(const int64_t*, const float*, const int64_t*, int, float, float, float, float, float, float, float,
-                  hipStream_t);
-void pra_momentum_mt(const int64_t*, const float*, const int64_t*, int, float, float, int, float, hipStream_t);
+                  const float*, hipStream_t);
+void pra_momentum_mt(const int64_t*, const float*, const int64_t*, int, float, float, int, float, const float*,
+                     hipStream_t);
 void pra_sumsq_accum(const void*, float*, int64_t, int, hipStream_t);
 void pra_flash_bwd_pre(const void*, const void*, float*, int, int, int, int, int, hipStream_t);
 int pra_adl_supported(int);
@@ -46,6 +47,8 @@ int pra_flash_bwd(const void*, const void*, const void*, const void*, const floa
 int pra_embedding_fwd(const int64_t*, const void*, void*, int64_t, int, int64_t, int64_t, int, hipStream_t);
 int pra_embedding_bwd(const int64_t*, const int64_t*, const void*, void*, int64_t, int, int64_t, int64_t, int, int,
                       int, hipStream_t);
+void pra_bias_gelu_bwd_db(const void*, const void*, const void*, void*, float*, int, int, int, int, int,
+                          hipStream_t);
 int pra_bn_nrb(int, int);
 void pra_bn_fwd_train(const void*, const void*, const void*, const void*, float*, float*, void*, uint8_t*, float*,
                       float*, float*, float*, int, int, int, float, float, int, int, int, hipStream_t);
@@ -115,12 +118,13 @@ PYBIND11_MODULE(_pra_hip, m) {
     check_launch("bias_gelu_bwd");
   });
   m.def("adamw_mt", [](P tab, P ftab, P chunks, int nch, float lr, float b1, float b2, float eps, float bc1, float bc2,
-                       float gs, P s) {
-    pra_adamw_mt(I64(tab), CF(ftab), I64(chunks), nch, lr, b1, b2, eps, bc1, bc2, gs, S(s));
+                       float gs, P s, P gsp) {
+    pra_adamw_mt(I64(tab), CF(ftab), I64(chunks), nch, lr, b1, b2, eps, bc1, bc2, gs, CF(gsp), S(s));
     check_launch("adamw_mt");
   });
-  m.def("momentum_mt", [](P tab, P ftab, P chunks, int nch, float lr, float mu, int nesterov, float gs, P s) {
-    pra_momentum_mt(I64(tab), CF(ftab), I64(chunks), nch, lr, mu, nesterov, gs, S(s));
+  m.def("momentum_mt", [](P tab, P ftab, P chunks, int nch, float lr, float mu, int nesterov, float gs, P s,
+                          P gsp) {
+    pra_momentum_mt(I64(tab), CF(ftab), I64(chunks), nch, lr, mu, nesterov, gs, CF(gsp), S(s));
     check_launch("momentum_mt");
   });
   m.def("sumsq_accum", [](P x, P out, int64_t n, int dt, P s) {
@@ -192,5 +196,10 @@ PYBIND11_MODULE(_pra_hip, m) {
     if (pra_embedding_bwd(I64(sids), I64(perm), CV(dy), V(dw), n, D, V, pad, dtg, dtw, acc, S(s)) != 0)
       throw std::invalid_argument("embedding_bwd: unsupported D/dtype");
     check_launch("embedding_bwd");
+  });
+  m.def("bias_gelu_bwd_db", [](P dy, P x, P b, P dx, P part, int rows, int cols, int nrb, int dt, int approx,
+                               P s) {
+    pra_bias_gelu_bwd_db(CV(dy), CV(x), CV(b), V(dx), F(part), rows, cols, nrb, dt, approx, S(s));
+    check_launch("bias_gelu_bwd_db");
   });
 }

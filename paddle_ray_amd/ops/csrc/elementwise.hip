@@ -53,6 +53,59 @@ __global__ void bias_gelu_bwd_k(const T* __restrict__ dy, const T* __restrict__ 
   }
 }
 
+// Backward with the bias gradient fused in: grid = (column tiles of 256 x 8 columns, nrb
+// row blocks); each lane owns 8 columns, walks its row block (2 rows in flight), writes dx and
+// keeps the column sums of dx (= d bias) in registers -> part[nrb, cols] fp32, reduced by
+// `colsum`. Removes the separate [rows, cols] re-read of dx for db.
+template <typename T>
+__global__ void __launch_bounds__(256) bias_gelu_bwd_db_k(const T* __restrict__ dy, const T* __restrict__ x,
+                                                          const T* __restrict__ b, T* __restrict__ dx,
+                                                          float* __restrict__ part, int rows, int cols, int rpb,
+                                                          int approx) {
+  const int cv = blockIdx.x * 256 + threadIdx.x;
+  if (cv * 8 >= cols) return;
+  const int c = cv * 8;
+  float bb[8], db[8];
+  if (b) load8<T>(b + c, bb);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { db[i] = 0.f; if (!b) bb[i] = 0.f; }
+  const int r0 = blockIdx.y * rpb, r1 = min(rows, r0 + rpb);
+  int r = r0;
+  for (; r + 1 < r1; r += 2) {
+    float a0[8], g0[8], a1[8], g1[8];
+    const size_t o0 = (size_t)r * cols + c, o1 = o0 + cols;
+    load8<T>(x + o0, a0);
+    load8<T>(dy + o0, g0);
+    load8<T>(x + o1, a1);
+    load8<T>(dy + o1, g1);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      a0[i] = g0[i] * gelu_df(a0[i] + bb[i], approx);
+      a1[i] = g1[i] * gelu_df(a1[i] + bb[i], approx);
+    }
+    store8<T>(dx + o0, a0);
+    store8<T>(dx + o1, a1);
+    // d bias from the ROUNDED dx values (what a separate colsum(dx) would read)
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      db[i] += Cvt<T>::to(Cvt<T>::from(a0[i])) + Cvt<T>::to(Cvt<T>::from(a1[i]));
+  }
+  if (r < r1) {
+    float a0[8], g0[8];
+    const size_t o0 = (size_t)r * cols + c;
+    load8<T>(x + o0, a0);
+    load8<T>(dy + o0, g0);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a0[i] = g0[i] * gelu_df(a0[i] + bb[i], approx);
+    store8<T>(dx + o0, a0);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) db[i] += Cvt<T>::to(Cvt<T>::from(a0[i]));
+  }
+  float* p = part + (size_t)blockIdx.y * cols + c;
+  *reinterpret_cast<float4*>(p) = make_float4(db[0], db[1], db[2], db[3]);
+  *reinterpret_cast<float4*>(p + 4) = make_float4(db[4], db[5], db[6], db[7]);
+}
+
 template <typename T>
 __global__ void bias_gelu_fwd_scalar(const T* __restrict__ x, const T* __restrict__ b, T* __restrict__ y, size_t n,
                                      int cols, int approx) {
@@ -85,10 +138,50 @@ __device__ __forceinline__ void st_any(void* p, size_t i, int dt, float v) {
   else ((f16*)p)[i] = (f16)v;
 }
 
+// Vector body of the common mixed-precision case (bf16 or fp32 grad, fp32 master, optional
+// bf16 low-precision param copy): 4 elements per lane per step, 16-B fp32 accesses.
+template <bool BF16G, bool LOWP>
+__device__ __forceinline__ void adamw_vec4(float* __restrict__ master, const void* __restrict__ grad,
+                                           float* __restrict__ m, float* __restrict__ v, uint16_t* __restrict__ lowp,
+                                           int64_t start, int64_t end, float b1, float b2, float eps, float decay,
+                                           float step, float rbc2, float gscale) {
+  for (int64_t i = start + 4 * threadIdx.x; i + 3 < end; i += 4 * blockDim.x) {
+    float g[4];
+    if (BF16G) {
+      const uint2 u = *reinterpret_cast<const uint2*>((const uint16_t*)grad + i);
+      g[0] = __uint_as_float(u.x << 16); g[1] = __uint_as_float(u.x & 0xffff0000u);
+      g[2] = __uint_as_float(u.y << 16); g[3] = __uint_as_float(u.y & 0xffff0000u);
+    } else {
+      const float4 u = *reinterpret_cast<const float4*>((const float*)grad + i);
+      g[0] = u.x; g[1] = u.y; g[2] = u.z; g[3] = u.w;
+    }
+    float4 mv = *reinterpret_cast<float4*>(m + i);
+    float4 vv = *reinterpret_cast<float4*>(v + i);
+    float4 pv = *reinterpret_cast<float4*>(master + i);
+    float mm[4] = {mv.x, mv.y, mv.z, mv.w}, vq[4] = {vv.x, vv.y, vv.z, vv.w}, pp[4] = {pv.x, pv.y, pv.z, pv.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float gk = g[k] * gscale;
+      mm[k] = b1 * mm[k] + (1.f - b1) * gk;
+      vq[k] = b2 * vq[k] + (1.f - b2) * gk * gk;
+      pp[k] = pp[k] * decay - step * mm[k] / (sqrtf(vq[k] * rbc2) + eps);
+    }
+    *reinterpret_cast<float4*>(m + i) = make_float4(mm[0], mm[1], mm[2], mm[3]);
+    *reinterpret_cast<float4*>(v + i) = make_float4(vq[0], vq[1], vq[2], vq[3]);
+    *reinterpret_cast<float4*>(master + i) = make_float4(pp[0], pp[1], pp[2], pp[3]);
+    if (LOWP) *reinterpret_cast<uint2*>(lowp + i) = make_uint2(pack_bf2(pp[0], pp[1]), pack_bf2(pp[2], pp[3]));
+  }
+}
+
+// gscale_ptr (device, nullable): global-norm clip coefficient read in-kernel, so the clip
+// needs no separate pass over the gradients.
 __global__ void __launch_bounds__(256) adamw_mt_k(const int64_t* __restrict__ tab, const float* __restrict__ ftab,
                                                   const int64_t* __restrict__ chunks, float lr, float b1, float b2,
-                                                  float eps, float bc1, float bc2, float gscale) {
-  const int64_t t = chunks[2 * blockIdx.x], start = chunks[2 * blockIdx.x + 1];
+                                                  float eps, float bc1, float bc2, float gscale,
+                                                  const float* __restrict__ gscale_ptr) {
+  if (gscale_ptr) gscale *= *gscale_ptr;
+  const int64_t t = chunks[2 * blockIdx.x];
+  int64_t start = chunks[2 * blockIdx.x + 1];
   const int64_t* d = tab + 8 * t;
   void* master = (void*)d[0];
   const void* grad = (const void*)d[1];
@@ -102,6 +195,23 @@ __global__ void __launch_bounds__(256) adamw_mt_k(const int64_t* __restrict__ ta
   const float decay = 1.f - lrt * wd, step = lrt / bc1, rbc2 = 1.f / bc2;
   int64_t end = start + kChunk;
   if (end > n) end = n;
+  const bool aligned = ((start & 3) == 0) && ((((uintptr_t)master | (uintptr_t)m | (uintptr_t)v) & 15) == 0) &&
+                       ((((uintptr_t)grad | (uintptr_t)lowp) & 7) == 0);
+  if (aligned && mdt == kF32 && (gdt == kBF16 || gdt == kF32) && (!lowp || pdt == kBF16)) {
+    const int64_t vend = start + ((end - start) & ~(int64_t)3);
+    if (gdt == kBF16) {
+      if (lowp) adamw_vec4<true, true>((float*)master, grad, m, v, (uint16_t*)lowp, start, vend, b1, b2, eps,
+                                       decay, step, rbc2, gscale);
+      else adamw_vec4<true, false>((float*)master, grad, m, v, nullptr, start, vend, b1, b2, eps, decay, step,
+                                   rbc2, gscale);
+    } else {
+      if (lowp) adamw_vec4<false, true>((float*)master, grad, m, v, (uint16_t*)lowp, start, vend, b1, b2, eps,
+                                        decay, step, rbc2, gscale);
+      else adamw_vec4<false, false>((float*)master, grad, m, v, nullptr, start, vend, b1, b2, eps, decay, step,
+                                    rbc2, gscale);
+    }
+    start = vend;  // scalar tail below
+  }
   for (int64_t i = start + threadIdx.x; i < end; i += blockDim.x) {
     float g = ld_any(grad, i, gdt) * gscale;
     float mi = b1 * m[i] + (1.f - b1) * g;
@@ -117,7 +227,9 @@ __global__ void __launch_bounds__(256) adamw_mt_k(const int64_t* __restrict__ ta
 // tab[t] = {master_or_param, grad, velocity, 0, lowp, n, gdt, pdt}; ftab = {wd, lr_mul}
 __global__ void __launch_bounds__(256) momentum_mt_k(const int64_t* __restrict__ tab, const float* __restrict__ ftab,
                                                      const int64_t* __restrict__ chunks, float lr, float mu,
-                                                     int nesterov, float gscale) {
+                                                     int nesterov, float gscale,
+                                                     const float* __restrict__ gscale_ptr) {
+  if (gscale_ptr) gscale *= *gscale_ptr;
   const int64_t t = chunks[2 * blockIdx.x], start = chunks[2 * blockIdx.x + 1];
   const int64_t* d = tab + 8 * t;
   void* master = (void*)d[0];
@@ -231,15 +343,16 @@ void pra_bias_gelu_bwd(const void* dy, const void* x, const void* b, void* dx, i
   }
 }
 void pra_adamw_mt(const int64_t* tab, const float* ftab, const int64_t* chunks, int nchunks, float lr, float b1,
-                  float b2, float eps, float bc1, float bc2, float gscale, hipStream_t s) {
+                  float b2, float eps, float bc1, float bc2, float gscale, const float* gscale_ptr, hipStream_t s) {
   if (!nchunks) return;
   hipLaunchKernelGGL(adamw_mt_k, dim3(nchunks), dim3(256), 0, s, tab, ftab, chunks, lr, b1, b2, eps, bc1, bc2,
-                     gscale);
+                     gscale, gscale_ptr);
 }
 void pra_momentum_mt(const int64_t* tab, const float* ftab, const int64_t* chunks, int nchunks, float lr, float mu,
-                     int nesterov, float gscale, hipStream_t s) {
+                     int nesterov, float gscale, const float* gscale_ptr, hipStream_t s) {
   if (!nchunks) return;
-  hipLaunchKernelGGL(momentum_mt_k, dim3(nchunks), dim3(256), 0, s, tab, ftab, chunks, lr, mu, nesterov, gscale);
+  hipLaunchKernelGGL(momentum_mt_k, dim3(nchunks), dim3(256), 0, s, tab, ftab, chunks, lr, mu, nesterov, gscale,
+                     gscale_ptr);
 }
 void pra_sumsq_accum(const void* x, float* out, int64_t n, int dt, hipStream_t s) {
   if (!n) return;
@@ -260,5 +373,13 @@ void pra_flash_bwd_pre(const void* o, const void* dO, float* delta, int B, int H
   const int64_t threads = rows * (D / 8);
   PRA_DISPATCH_FLOAT(dt, T, hipLaunchKernelGGL((attn_delta_k<T>), dim3((threads + 255) / 256), dim3(256), 0, s,
                                                (const T*)o, (const T*)dO, delta, B, H, S, D));
+}
+void pra_bias_gelu_bwd_db(const void* dy, const void* x, const void* b, void* dx, float* part, int rows, int cols,
+                          int nrb, int dt, int approx, hipStream_t s) {
+  if (!rows || cols % 8) return;
+  const int rpb = (rows + nrb - 1) / nrb;
+  const dim3 grid((cols / 8 + 255) / 256, nrb);
+  PRA_DISPATCH_FLOAT(dt, T, hipLaunchKernelGGL((bias_gelu_bwd_db_k<T>), grid, dim3(256), 0, s, (const T*)dy,
+                                               (const T*)x, (const T*)b, (T*)dx, part, rows, cols, rpb, approx));
 }
 }

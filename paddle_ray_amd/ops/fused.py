@@ -499,6 +499,9 @@ def _bg_fwd_hip(x2, b, approximate):
     return y
 
 
+R.register_kernel('bias_gelu_bwd_db', 'hip')(lambda *a: None)  # dispatch-stats marker
+
+
 @R.register_kernel('bias_gelu_bwd', 'hip')
 def _bg_bwd_hip(dy2, x2, b, approximate):
     dx = torch.empty_like(x2)
@@ -523,8 +526,21 @@ class BiasGeluFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x2, b = ctx.saved_tensors
-        dx = R.dispatch('bias_gelu_bwd', x2, dy.contiguous().view(x2.shape), x2, b,
-                        ctx.approximate)
+        dy2 = dy.contiguous().view(x2.shape)
+        rows, cols = x2.shape
+        if (b is not None and ctx.needs_input_grad[1] and x2.is_cuda and cols % 8 == 0
+                and R.select_backend(x2, 'bias_gelu_bwd_db') == 'hip'):
+            # dx and d(bias) in one pass (bias grad = column sums kept in registers)
+            L = _native.lib()
+            nrb = max(1, min(256, rows // 16))
+            part = torch.empty((nrb, cols), device=x2.device, dtype=torch.float32)
+            dx = torch.empty_like(x2)
+            L.bias_gelu_bwd_db(_ptr(dy2), _ptr(x2), _ptr(b), _ptr(dx), _ptr(part), rows, cols, nrb,
+                               _dt(x2), int(ctx.approximate), _stream())
+            db = torch.empty(cols, device=x2.device, dtype=b.dtype)
+            L.colsum16(_ptr(part), _ptr(db), nrb, cols, _dt(db), _stream())
+            return dx.view(ctx.shp), db, None
+        dx = R.dispatch('bias_gelu_bwd', x2, dy2, x2, b, ctx.approximate)
         db = dx.sum(0) if (b is not None and ctx.needs_input_grad[1]) else None
         return dx.view(ctx.shp), db, None
 
@@ -720,6 +736,41 @@ def linear(x, w, b=None):
     return y.view(*x.shape[:-1], w.shape[-1])
 
 
+class LinearNTFn(torch.autograd.Function):
+    """y = x @ W^T for a [out, in] weight (the tied LM head: W is the [vocab, hidden] word
+    embedding). dW = dy^T @ x is accumulated in place into W's existing grad (one beta=1
+    GEMM) like LinearFn."""
+
+    @staticmethod
+    def forward(ctx, x, w):
+        ctx.save_for_backward(x)
+        ctx.w = w
+        return torch.mm(x, w.t())
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, = ctx.saved_tensors
+        w = ctx.w
+        dx = torch.mm(dy, w) if ctx.needs_input_grad[0] else None
+        dw = None
+        if ctx.needs_input_grad[1]:
+            g = w.grad
+            if (g is not None and not torch.is_grad_enabled() and g.shape == w.shape
+                    and g.dtype == dy.dtype and g.is_contiguous()):
+                g.addmm_(dy.t(), x)
+            else:
+                dw = torch.mm(dy.t(), x)
+        return dx, dw
+
+
+def linear_nt(x2, w):
+    """[T, in] @ [out, in]^T with fused dW accumulation (see LinearNTFn)."""
+    if w.requires_grad and torch.is_grad_enabled() and w.is_leaf and x2.dtype == w.dtype and \
+            not torch.is_autocast_enabled(x2.device.type):
+        return LinearNTFn.apply(x2, w)
+    return torch.mm(x2, w.t())
+
+
 # =============================================================================
 # Multi-tensor fused AdamW / Adam / Momentum (one launch for all params)
 # =============================================================================
@@ -792,7 +843,9 @@ class MultiTensorAdamW:
         self._plan = _mt_table(cols, n, [self.wds, self.lr_muls], dev)
         self._gptrs = tuple(g.data_ptr() for g in grads)
 
-    def step(self, lr, b1, b2, eps, step, grad_scale=1.0):
+    def step(self, lr, b1, b2, eps, step, grad_scale=1.0, scale_tensor=None):
+        """``scale_tensor``: optional 0-d fp32 device tensor (the global-norm clip
+        coefficient) multiplied into every gradient inside the kernel."""
         grads = self.grads_getter()
         if self._plan is None or tuple(g.data_ptr() for g in grads) != self._gptrs:
             self._build(grads)
@@ -801,7 +854,7 @@ class MultiTensorAdamW:
         bc2 = 1 - b2 ** step
         _native.lib().adamw_mt(_ptr(tab), _ptr(ftab), _ptr(ch), nch, float(lr), float(b1),
                                float(b2), float(eps), float(bc1), float(bc2), float(grad_scale),
-                               _stream())
+                               _stream(), _ptr(scale_tensor))
 
 
 def momentum_ref(params, grads, vels, masters, lr, mu, wds, use_nesterov, grad_scale=1.0):

@@ -247,16 +247,14 @@ class Momentum(Optimizer):
         lrm = [self._lr_for(p, g) / lr if lr else 1.0 for p, g in pgs]
         gs = 1.0 * self._rescale_grad
         if ps[0]._t.is_cuda and _native.available():
-            if coef is not None:
-                for p in ps:
-                    p._t.grad.mul_(coef.to(p._t.grad.dtype))
-            self._mt_momentum(ps, vels, masters, wds, lrm, lr, gs)
+            scale_t = None if coef is None else coef.to(torch.float32).reshape(()).contiguous()
+            self._mt_momentum(ps, vels, masters, wds, lrm, lr, gs, scale_t)
         else:
             grads = [p._t.grad * (coef if coef is not None else 1.0) for p in ps]
             K.momentum_ref([p._t for p in ps], grads, vels, masters, lr, self._momentum,
                            [w for w in wds], self._use_nesterov, gs)
 
-    def _mt_momentum(self, ps, vels, masters, wds, lrm, lr, gs):
+    def _mt_momentum(self, ps, vels, masters, wds, lrm, lr, gs, scale_t=None):
         key = tuple(p._t.grad.data_ptr() for p in ps) + tuple(p._t.data_ptr() for p in ps)
         if self._fused_plan is None or self._fused_plan[0] != key:
             n = [p._t.numel() for p in ps]
@@ -272,7 +270,7 @@ class Momentum(Optimizer):
         tab, ftab, ch, nch = self._fused_plan[1]
         _native.lib().momentum_mt(tab.data_ptr(), ftab.data_ptr(), ch.data_ptr(), nch, float(lr),
                                   float(self._momentum), int(self._use_nesterov), float(gs),
-                                  K._stream())
+                                  K._stream(), 0 if scale_t is None else scale_t.data_ptr())
 
 
 class Adam(Optimizer):
@@ -313,18 +311,22 @@ class Adam(Optimizer):
         for p in ps:  # keep reference-compatible pow accumulators
             self._acc('beta1_pow_acc', p, 1.0, shape=[1]).fill_(b1 ** step)
             self._acc('beta2_pow_acc', p, 1.0, shape=[1]).fill_(b2 ** step)
-        if not self._decoupled and any(wds):
-            # Adam + L2: coupled decay folded into the gradient
+        coupled = not self._decoupled and any(wds)
+        if coupled:
+            # Adam + L2: clip first, then the coupled decay folded into the gradient
+            if coef is not None:
+                for p in ps:
+                    p._t.grad.mul_(coef.to(p._t.grad.dtype))
+                coef = None
             for p, w, m in zip(ps, wds, masters):
                 if w:
                     p._t.grad.add_((m if m is not None else p._t).to(p._t.grad.dtype), alpha=w)
             wds = [0.0] * len(ps)
         if ps[0]._t.is_cuda and _native.available():
             gscale = 1.0
-            if coef is not None:
-                # the plan takes a host scalar; the coefficient stays on device via pre-scaling
-                for p in ps:
-                    p._t.grad.mul_(coef.to(p._t.grad.dtype))
+            scale_t = None
+            if coef is not None:  # the clip coefficient is applied inside the update kernel
+                scale_t = coef.to(torch.float32).reshape(()).contiguous()
             key = tuple(p._t.grad.data_ptr() for p in ps) + tuple(p._t.data_ptr() for p in ps) + \
                 tuple(wds) + tuple(lrm)
             if self._fused_plan is None or self._fused_plan[0] != key:
@@ -333,7 +335,7 @@ class Adam(Optimizer):
                 self._fused_plan = (key, plan)
             plan = self._fused_plan[1]
             plan.grads_getter = lambda: [p._t.grad for p in ps]
-            plan.step(lr, b1, b2, self._epsilon, step, gscale)
+            plan.step(lr, b1, b2, self._epsilon, step, gscale, scale_t)
         else:
             grads = [p._t.grad if coef is None else p._t.grad * coef for p in ps]
             K.adamw_ref([p._t for p in ps], grads, ms, vs, masters, lr, b1, b2, self._epsilon, wds,

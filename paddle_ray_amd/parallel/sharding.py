@@ -208,15 +208,21 @@ class ShardedOptimizer:
         o = self._inner
         o._step_count = self._step
         coef = self._clip_coef()
-        if coef is not None:
-            for s in st.shard_grads:
-                s.mul_(coef.to(s.dtype))
         lr = o.get_lr()
         dev = st.groups[0].device if st.groups else None
-        if dev is not None and dev.type == 'cuda' and _native.available():
-            self._step_hip(lr)
+        coupled = self._kind == 'Adam' and o._weight_decay
+        if dev is not None and dev.type == 'cuda' and _native.available() and not coupled:
+            # the clip coefficient is read by the update kernel: no extra pass over the grads
+            self._step_hip(lr, None if coef is None else
+                           coef.to(torch.float32).reshape(()).contiguous())
         else:
-            self._step_ref(lr)
+            if coef is not None:
+                for s in st.shard_grads:
+                    s.mul_(coef.to(s.dtype))
+            if dev is not None and dev.type == 'cuda' and _native.available():
+                self._step_hip(lr)
+            else:
+                self._step_ref(lr)
         st.after_step()
 
     def _piece_views(self, gi, lo, hi):
@@ -246,7 +252,7 @@ class ShardedOptimizer:
                                [None if lowp is None else master], lr * lrm, mu, [self._wd(p)],
                                getattr(o, '_use_nesterov', False))
 
-    def _step_hip(self, lr):
+    def _step_hip(self, lr, scale_t=None):
         o = self._inner
         if self._plan is None:
             cols = [[], [], [], [], [], [], [], []]
@@ -279,11 +285,12 @@ class ShardedOptimizer:
             _native.lib().adamw_mt(tab.data_ptr(), ftab.data_ptr(), ch.data_ptr(), nch, float(lr),
                                    float(b1), float(b2), float(o._epsilon),
                                    float(1 - b1 ** self._step), float(1 - b2 ** self._step), 1.0,
-                                   K._stream())
+                                   K._stream(), 0 if scale_t is None else scale_t.data_ptr())
         else:
             _native.lib().momentum_mt(tab.data_ptr(), ftab.data_ptr(), ch.data_ptr(), nch, float(lr),
                                       float(getattr(o, '_momentum', 0.0)),
-                                      int(getattr(o, '_use_nesterov', False)), 1.0, K._stream())
+                                      int(getattr(o, '_use_nesterov', False)), 1.0, K._stream(),
+                                      0 if scale_t is None else scale_t.data_ptr())
 
     def minimize(self, loss, *a, **k):
         loss.backward()

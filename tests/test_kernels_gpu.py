@@ -92,9 +92,10 @@ def test_softmax_ce(dt, V):
 
 @pytest.mark.parametrize('dt', [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize('approx', [True, False])
-def test_bias_gelu(dt, approx):
-    x = torch.randn(33, 8192, device=DEV, dtype=dt, requires_grad=True)
-    b = torch.randn(8192, device=DEV, dtype=dt, requires_grad=True)
+@pytest.mark.parametrize('rows,cols', [(33, 8192), (1000, 2048)])
+def test_bias_gelu(dt, approx, rows, cols):
+    x = torch.randn(rows, cols, device=DEV, dtype=dt, requires_grad=True)
+    b = torch.randn(cols, device=DEV, dtype=dt, requires_grad=True)
     y = F.bias_gelu(x, b, approx)
     dy = torch.randn_like(y)
     y.backward(dy)
@@ -104,7 +105,8 @@ def test_bias_gelu(dt, approx):
     tol = _tol(dt)
     assert torch.allclose(y.float(), yr, atol=tol, rtol=tol)
     assert torch.allclose(x.grad.float(), xr.grad, atol=tol * 2, rtol=tol * 2)
-    assert torch.allclose(b.grad.float(), br.grad, atol=tol * 40, rtol=tol * 4)
+    assert torch.allclose(b.grad.float(), br.grad, atol=tol * 40 * max(1, rows // 100),
+                          rtol=tol * 4)
 
 
 def _attn_ref(q, k, v, causal, scale):
