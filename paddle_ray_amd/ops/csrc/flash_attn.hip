@@ -21,6 +21,8 @@
 // keys (dK/dV); K/V (resp. Q/dO) tiles of 64 rows staged through LDS with
 // register prefetch of the next tile (async-STAGE split, guide T14).
 #include "common.h"
+#include <stdlib.h>
+#include <type_traits>
 
 namespace pra {
 namespace fa {
@@ -178,7 +180,7 @@ __device__ __forceinline__ int acc_row(int reg, int h) { return (reg & 3) + 8 * 
 // forward
 // ============================================================================
 template <typename T, int D, bool CAUSAL, int NW>
-__global__ void __launch_bounds__(NW * 64, NW / 4)
+__global__ void __launch_bounds__(NW * 64, 2)
 fwd_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restrict__ v, T* __restrict__ o,
            float* __restrict__ lse, int H, int Sq, int Sk, int64_t qsb, int64_t qss, int64_t qsh, int64_t ksb,
            int64_t kss, int64_t ksh, int64_t vsb, int64_t vss, int64_t vsh, float scale_log2) {
@@ -232,14 +234,25 @@ fwd_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restrict
       kr.load(kb_, kss, k0 + kTile, Sk);
       vr.load(vb_, vss, k0 + kTile, Sk);
     }
-    // S^T = K Q^T : two 32-key tiles (raw scores)
+    // S^T = K Q^T : two 32-key tiles (raw scores). All 2*NS K fragments are read from LDS
+    // before the first MFMA so the reads overlap each other instead of one LDS round trip
+    // per MFMA (hipcc otherwise reuses one fragment register: read, wait, mfma, read, ...).
     f32x16 s_acc[2];
+    {
+      typename V8<T>::type kfr[2][NS];
 #pragma unroll
-    for (int mt = 0; mt < 2; ++mt) {
-      s_acc[mt] = f32x16{};
+      for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
-      for (int s = 0; s < NS; ++s)
-        s_acc[mt] = mfma<T>(frag_rows<T, D>(Ks, 32 * mt + r, s, h), qf[s], s_acc[mt]);
+        for (int s = 0; s < NS; ++s) kfr[mt][s] = frag_rows<T, D>(Ks, 32 * mt + r, s, h);
+      // nothing crosses this point: every read is issued before the first MFMA, and the
+      // waitcnt pass then counts them down (lgkmcnt(N)) one MFMA at a time
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) {
+        s_acc[mt] = f32x16{};
+#pragma unroll
+        for (int s = 0; s < NS; ++s) s_acc[mt] = mfma<T>(kfr[mt][s], qf[s], s_acc[mt]);
+      }
     }
     const bool need_mask = (k0 + kTile > Sk) || (CAUSAL && (k0 + kTile - 1 > q0 + off));
     if (need_mask) {
@@ -317,7 +330,7 @@ fwd_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restrict
 // backward: dQ (queries on lanes, sweep key tiles)
 // ============================================================================
 template <typename T, int D, bool CAUSAL, int NW>
-__global__ void __launch_bounds__(NW * 64, NW / 4)
+__global__ void __launch_bounds__(NW * 64, 2)
 bwd_dq_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restrict__ v, const T* __restrict__ dO,
               const float* __restrict__ lse, const float* __restrict__ delta, T* __restrict__ dq, int H, int Sq,
               int Sk, int64_t qsb, int64_t qss, int64_t qsh, int64_t ksb, int64_t kss, int64_t ksh, int64_t vsb,
@@ -386,10 +399,29 @@ bwd_dq_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restr
     for (int mt = 0; mt < 2; ++mt) {
       s_acc[mt] = f32x16{};
       dp_acc[mt] = f32x16{};
+      // fragments read in groups of 4, one group ahead of the MFMAs that consume them
+      // (8 fragments live at most: this kernel is at the 256-VGPR occupancy-2 limit)
+      constexpr int G = 4, NG = 2 * NS / G;  // groups over the K (first NS) then V fragments
+      typename V8<T>::type fr[2][G];
 #pragma unroll
-      for (int s = 0; s < NS; ++s) {
-        s_acc[mt] = mfma<T>(frag_rows<T, D>(Ks, 32 * mt + r, s, h), qf[s], s_acc[mt]);
-        dp_acc[mt] = mfma<T>(frag_rows<T, D>(Vs, 32 * mt + r, s, h), df[s], dp_acc[mt]);
+      for (int g = 0; g <= NG; ++g) {
+        if (g < NG) {
+#pragma unroll
+          for (int j = 0; j < G; ++j) {
+            const int f = g * G + j;
+            fr[g & 1][j] = f < NS ? frag_rows<T, D>(Ks, 32 * mt + r, f, h)
+                                  : frag_rows<T, D>(Vs, 32 * mt + r, f - NS, h);
+          }
+        }
+        if (g > 0) {
+#pragma unroll
+          for (int j = 0; j < G; ++j) {
+            const int f = (g - 1) * G + j;
+            if (f < NS) s_acc[mt] = mfma<T>(fr[(g - 1) & 1][j], qf[f], s_acc[mt]);
+            else dp_acc[mt] = mfma<T>(fr[(g - 1) & 1][j], df[f - NS], dp_acc[mt]);
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
     const bool need_mask = (k0 + kTile > Sk) || (CAUSAL && (k0 + kTile - 1 > q0 + off));
@@ -520,10 +552,21 @@ bwd_dkdv_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __res
 #pragma unroll
     for (int nt = 0; nt < 2; ++nt) {  // two 32-query halves of the tile
       f32x16 s_acc = f32x16{}, dp_acc = f32x16{};
+      {
+        // all 2*NS row fragments in flight before the MFMAs (one wave per SIMD here: an LDS
+        // round trip per MFMA would be fully exposed)
+        typename V8<T>::type qfr[NS], dfr[NS];
 #pragma unroll
-      for (int s = 0; s < NS; ++s) {
-        s_acc = mfma<T>(frag_rows<T, D>(Qs, 32 * nt + r, s, h), kf[s], s_acc);
-        dp_acc = mfma<T>(frag_rows<T, D>(Ds, 32 * nt + r, s, h), vf[s], dp_acc);
+        for (int s = 0; s < NS; ++s) {
+          qfr[s] = frag_rows<T, D>(Qs, 32 * nt + r, s, h);
+          dfr[s] = frag_rows<T, D>(Ds, 32 * nt + r, s, h);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+          s_acc = mfma<T>(qfr[s], kf[s], s_acc);
+          dp_acc = mfma<T>(dfr[s], vf[s], dp_acc);
+        }
       }
       // rows (queries) in registers: q = 32nt + acc_row(i,h)
 #pragma unroll
@@ -548,12 +591,19 @@ bwd_dkdv_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __res
       // dV^T += dO^T P ; dK^T += Q^T dS   (k = queries of this 32-half, 2 steps of 16)
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
-        const typename V8<T>::type pf = pack_frag<T>(s_acc, 8 * ks);
-        const typename V8<T>::type sf = pack_frag<T>(dp_acc, 8 * ks);
+        typename V8<T>::type dtr[ND], qtr[ND];
 #pragma unroll
         for (int dt = 0; dt < ND; ++dt) {
-          acc_v[dt] = mfma<T>(frag_tr<T>(Dt, 32 * dt + r, 2 * nt + ks, h), pf, acc_v[dt]);
-          acc_k[dt] = mfma<T>(frag_tr<T>(Qt, 32 * dt + r, 2 * nt + ks, h), sf, acc_k[dt]);
+          dtr[dt] = frag_tr<T>(Dt, 32 * dt + r, 2 * nt + ks, h);
+          qtr[dt] = frag_tr<T>(Qt, 32 * dt + r, 2 * nt + ks, h);
+        }
+        const typename V8<T>::type pf = pack_frag<T>(s_acc, 8 * ks);
+        const typename V8<T>::type sf = pack_frag<T>(dp_acc, 8 * ks);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int dt = 0; dt < ND; ++dt) {
+          acc_v[dt] = mfma<T>(dtr[dt], pf, acc_v[dt]);
+          acc_k[dt] = mfma<T>(qtr[dt], sf, acc_k[dt]);
         }
       }
     }
@@ -581,16 +631,22 @@ bwd_dkdv_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __res
   }
 }
 
-template <typename T, int D, bool C>
-static void launch_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B, int H, int Sq,
-                       int Sk, const int64_t* st, float scale, hipStream_t s) {
+template <typename T, int D, bool C, int NW>
+static void launch_fwd_nw(const void* q, const void* k, const void* v, void* o, float* lse, int B, int H, int Sq,
+                          int Sk, const int64_t* st, float scale, hipStream_t s) {
   const size_t lds = (Geo<D>::ROW_IMG + Geo<D>::TR_IMG) * sizeof(T);
-  constexpr int NW = 8;
   auto kern = fwd_kernel<T, D, C, NW>;
   hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   dim3 grid((Sq + NW * 32 - 1) / (NW * 32), B * H);
   hipLaunchKernelGGL(kern, grid, dim3(NW * 64), lds, s, (const T*)q, (const T*)k, (const T*)v, (T*)o, lse, H, Sq, Sk,
                      st[0], st[1], st[2], st[3], st[4], st[5], st[6], st[7], st[8], scale * 1.4426950408889634f);
+}
+
+// 8 waves = one 256-query block per CU (4-wave blocks, two per CU, measured the same)
+template <typename T, int D, bool C>
+static void launch_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B, int H, int Sq,
+                       int Sk, const int64_t* st, float scale, hipStream_t s) {
+  launch_fwd_nw<T, D, C, 8>(q, k, v, o, lse, B, H, Sq, Sk, st, scale, s);
 }
 
 template <typename T, int D, bool C>
@@ -600,12 +656,15 @@ static void launch_bwd(const void* q, const void* k, const void* v, const void* 
   const float sl2 = scale * 1.4426950408889634f;
   {
     const size_t lds = (2 * Geo<D>::ROW_IMG + Geo<D>::TR_IMG) * sizeof(T);
-    constexpr int NW = 8;
-    auto kern = bwd_dq_kernel<T, D, C, NW>;
-    hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(kern, dim3((Sq + NW * 32 - 1) / (NW * 32), B * H), dim3(NW * 64), lds, s, (const T*)q, (const T*)k,
-                       (const T*)v, (const T*)dO, lse, delta, (T*)dq, H, Sq, Sk, st[0], st[1], st[2], st[3], st[4],
-                       st[5], st[6], st[7], st[8], st[9], st[10], st[11], scale, sl2);
+    auto go = [&](auto nwc) {
+      constexpr int NW = decltype(nwc)::value;
+      auto kern = bwd_dq_kernel<T, D, C, NW>;
+      hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      hipLaunchKernelGGL(kern, dim3((Sq + NW * 32 - 1) / (NW * 32), B * H), dim3(NW * 64), lds, s, (const T*)q,
+                         (const T*)k, (const T*)v, (const T*)dO, lse, delta, (T*)dq, H, Sq, Sk, st[0], st[1], st[2],
+                         st[3], st[4], st[5], st[6], st[7], st[8], st[9], st[10], st[11], scale, sl2);
+    };
+    go(std::integral_constant<int, 8>{});
   }
   {
     const size_t lds = (2 * Geo<D>::ROW_IMG + 2 * Geo<D>::TR_IMG) * sizeof(T) + 2 * kTile * sizeof(float);
