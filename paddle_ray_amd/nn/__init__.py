@@ -25,3 +25,4 @@ from .layer.rnn import (RNNCellBase, SimpleRNNCell, LSTMCell, GRUCell, RNN, BiRN
                         LSTM, GRU)
 from .clip import ClipGradByValue, ClipGradByNorm, ClipGradByGlobalNorm  # noqa
 from . import utils  # noqa
+from . import quant  # noqa: E402
