@@ -95,6 +95,15 @@ template <int D> struct Geo {
   static constexpr int TR_IMG = D * kTP;           // elements
 };
 
+// Swizzled tile image [64][D] (no padding), element offset of 16-B chunk ch of row `row`:
+// 8-row x 32-column subtiles of 512 B, chunk (ch&3) XOR-ed with (row>>2)&3. One image serves
+// row fragments (ds_read_b128) and transposed fragments (ds_read_b64_tr_b16) bank-conflict
+// free, and the reads of one fragment set differ by immediates from 2 base registers.
+template <int D>
+__device__ __forceinline__ int swz(int row, int ch) {
+  return (row >> 3) * (8 * D) + (ch >> 2) * 256 + (row & 7) * 32 + 8 * ((ch & 3) ^ ((row >> 2) & 3));
+}
+
 // Block-cooperative staged load of a 64-row x D tile by NT threads, pair mapping:
 // pair-chunk pc = t + NT*p -> rows 2*(pc%32), 2*(pc%32)+1, 16-B column chunk pc/32.
 template <typename T, int D, int NT>
@@ -123,6 +132,17 @@ struct TileRegs {
       if (dc < NCH) {
         *reinterpret_cast<uint4*>(img + (2 * kp) * Geo<D>::RP + dc * 8) = r0[p];
         *reinterpret_cast<uint4*>(img + (2 * kp + 1) * Geo<D>::RP + dc * 8) = r1[p];
+      }
+    }
+  }
+  // swizzled row image [64][D] (see swz)
+  __device__ __forceinline__ void store_swz(T* img) const {
+#pragma unroll
+    for (int p = 0; p < NPASS; ++p) {
+      const int pc = threadIdx.x + NT * p, kp = pc & 31, dc = pc >> 5;
+      if (dc < NCH) {
+        *reinterpret_cast<uint4*>(img + swz<D>(2 * kp, dc)) = r0[p];
+        *reinterpret_cast<uint4*>(img + swz<D>(2 * kp + 1, dc)) = r1[p];
       }
     }
   }
@@ -175,6 +195,34 @@ __device__ __forceinline__ typename V8<T>::type frag_global(const T* rowp, int d
 }
 
 __device__ __forceinline__ int acc_row(int reg, int h) { return (reg & 3) + 8 * (reg >> 2) + 4 * h; }
+
+// Row fragment from a swizzled image: a tile is staged once (no transposed copy built from
+// scattered 4-B writes) and read both ways.
+template <typename T, int D>
+__device__ __forceinline__ typename V8<T>::type frag_rows_swz(const T* img, int row, int s, int h) {
+  return *reinterpret_cast<const typename V8<T>::type*>(img + swz<D>(row, 2 * s + h));
+}
+typedef short v4i16 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
+// Transposed A fragment (row = column 32*dt + (lane&31) of the image) over the k-step S of
+// the image's rows, in the permuted k order of an accumulator-derived B operand:
+// elem j <-> image row 16S + 8(j>>2) + 4h + (j&3). Two ds_read_b64_tr_b16: lane 4q+p of each
+// 16-lane group addresses row (base+q), columns 4p..4p+3 of the group's 16 columns and
+// receives its own column of the 4 rows. EXEC must be full (every lane takes part).
+template <typename T, int D>
+__device__ __forceinline__ typename V8<T>::type frag_trr(const T* img, int dt, int S, int h, int lane) {
+  const int g = (lane >> 4) & 1, q = (lane >> 2) & 3, p = lane & 3;
+  const int c = 4 * dt + 2 * g + (p >> 1);
+  const int ra = 16 * S + 4 * h + q;
+  const T* pa = img + swz<D>(ra, c) + 4 * (p & 1);
+  const T* pb = img + swz<D>(ra + 8, c) + 4 * (p & 1);
+  const v4i16 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)pa);
+  const v4i16 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)pb);
+  const u32x2 ua = __builtin_bit_cast(u32x2, a), ub = __builtin_bit_cast(u32x2, b);
+  u32x4 u;
+  u[0] = ua[0]; u[1] = ua[1]; u[2] = ub[0]; u[3] = ub[1];
+  return as_v8<T>(u);
+}
 
 // ============================================================================
 // forward
@@ -335,10 +383,9 @@ bwd_dq_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restr
               const float* __restrict__ lse, const float* __restrict__ delta, T* __restrict__ dq, int H, int Sq,
               int Sk, int64_t qsb, int64_t qss, int64_t qsh, int64_t ksb, int64_t kss, int64_t ksh, int64_t vsb,
               int64_t vss, int64_t vsh, int64_t dqsb, int64_t dqss, int64_t dqsh, float scale, float scale_log2) {
+  // double-buffered {K, V} swizzled row images; K^T fragments by transposed reads of K
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  T* Ks = reinterpret_cast<T*>(smem);
-  T* Vs = Ks + Geo<D>::ROW_IMG;
-  T* Kt = Vs + Geo<D>::ROW_IMG;
+  T* img0 = reinterpret_cast<T*>(smem);  // [2][2][64*D]
   constexpr int NS = D / 16, ND = D / 32, BM = NW * 32;
   const float LOG2E = 1.4426950408889634f;
 
@@ -382,14 +429,15 @@ bwd_dq_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restr
   if (ntiles > 0) {
     kr.load(kb_, kss, 0, Sk);
     vr.load(vb_, vss, 0, Sk);
-    kr.store_rows(Ks);
-    kr.store_tr(Kt);
-    vr.store_rows(Vs);
+    kr.store_swz(img0);
+    vr.store_swz(img0 + kTile * D);
   }
   __syncthreads();
 
   for (int kt = 0; kt < ntiles; ++kt) {
     const int k0 = kt * kTile;
+    const T* Ks = img0 + (2 * (kt & 1)) * kTile * D;
+    const T* Vs = Ks + kTile * D;
     if (kt + 1 < ntiles) {
       kr.load(kb_, kss, k0 + kTile, Sk);
       vr.load(vb_, vss, k0 + kTile, Sk);
@@ -401,7 +449,7 @@ bwd_dq_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restr
       dp_acc[mt] = f32x16{};
       // fragments read in groups of 4, one group ahead of the MFMAs that consume them
       // (8 fragments live at most: this kernel is at the 256-VGPR occupancy-2 limit)
-      constexpr int G = 4, NG = 2 * NS / G;  // groups over the K (first NS) then V fragments
+      constexpr int G = 2, NG = 2 * NS / G;  // groups over the K (first NS) then V fragments
       typename V8<T>::type fr[2][G];
 #pragma unroll
       for (int g = 0; g <= NG; ++g) {
@@ -409,8 +457,8 @@ bwd_dq_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restr
 #pragma unroll
           for (int j = 0; j < G; ++j) {
             const int f = g * G + j;
-            fr[g & 1][j] = f < NS ? frag_rows<T, D>(Ks, 32 * mt + r, f, h)
-                                  : frag_rows<T, D>(Vs, 32 * mt + r, f - NS, h);
+            fr[g & 1][j] = f < NS ? frag_rows_swz<T, D>(Ks, 32 * mt + r, f, h)
+                                  : frag_rows_swz<T, D>(Vs, 32 * mt + r, f - NS, h);
           }
         }
         if (g > 0) {
@@ -441,13 +489,12 @@ bwd_dq_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restr
     for (int ks = 0; ks < 4; ++ks) {
       const typename V8<T>::type sf = pack_frag<T>(s_acc[ks >> 1], 8 * (ks & 1));
 #pragma unroll
-      for (int dt = 0; dt < ND; ++dt) acc_q[dt] = mfma<T>(frag_tr<T>(Kt, 32 * dt + r, ks, h), sf, acc_q[dt]);
+      for (int dt = 0; dt < ND; ++dt) acc_q[dt] = mfma<T>(frag_trr<T, D>(Ks, dt, ks, h, lane), sf, acc_q[dt]);
     }
-    __syncthreads();
-    if (kt + 1 < ntiles) {
-      kr.store_rows(Ks);
-      kr.store_tr(Kt);
-      vr.store_rows(Vs);
+    if (kt + 1 < ntiles) {  // idle buffer: last read before the previous barrier
+      T* nb = img0 + (2 * ((kt + 1) & 1)) * kTile * D;
+      kr.store_swz(nb);
+      vr.store_swz(nb + kTile * D);
     }
     __syncthreads();
   }
@@ -480,19 +527,17 @@ bwd_dkdv_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __res
                 T* __restrict__ dv, int H, int Sq, int Sk, int64_t qsb, int64_t qss, int64_t qsh, int64_t ksb,
                 int64_t kss, int64_t ksh, int64_t vsb, int64_t vss, int64_t vsh, int64_t dksb, int64_t dkss,
                 int64_t dksh, int64_t dvsb, int64_t dvss, int64_t dvsh, float scale, float scale_log2) {
+  // Double-buffered LDS: buffer b = {Q image, dO image} (swizzled rows, read both row-wise and
+  // transposed) + lse/delta of the tile's 64 queries. The next tile is written into the idle
+  // buffer right after the current tile's MFMAs are issued: one barrier per tile.
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  T* Qs = reinterpret_cast<T*>(smem);
-  T* Qt = Qs + Geo<D>::ROW_IMG;
-  T* Ds = Qt + Geo<D>::TR_IMG;
-  T* Dt = Ds + Geo<D>::ROW_IMG;
-  float* Ls = reinterpret_cast<float*>(Dt + Geo<D>::TR_IMG);  // [64] lse*log2e
-  float* Dl = Ls + kTile;                                      // [64] delta
+  T* img0 = reinterpret_cast<T*>(smem);                               // [2][2][64*D]
+  float* Lsb = reinterpret_cast<float*>(img0 + 4 * kTile * D);        // [2][64] lse*log2e
+  float* Dlb = Lsb + 2 * kTile;                                       // [2][64] delta
   constexpr int NS = D / 16, ND = D / 32;
   const float LOG2E = 1.4426950408889634f;
 
-  const int nkb = gridDim.x;
-  const int kb = CAUSAL ? blockIdx.x : blockIdx.x;  // causal: later key blocks have less work
-  (void)nkb;
+  const int kb = blockIdx.x;
   const int bh = blockIdx.y, b = bh / H, hh = bh % H;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
   const int kblk0 = kb * 128;
@@ -535,17 +580,23 @@ bwd_dkdv_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __res
       dreg = qq < Sq ? delta[(int64_t)bh * Sq + qq] : 0.f;
     }
   };
-  auto store_tile = [&]() {
-    qr.store_rows(Qs);
-    qr.store_tr(Qt);
-    dr.store_rows(Ds);
-    dr.store_tr(Dt);
-    if (threadIdx.x < kTile) { Ls[threadIdx.x] = lreg * LOG2E; Dl[threadIdx.x] = dreg; }
+  auto store_tile = [&](int buf) {
+    qr.store_swz(img0 + (2 * buf) * kTile * D);
+    dr.store_swz(img0 + (2 * buf + 1) * kTile * D);
+    if (threadIdx.x < kTile) {
+      Lsb[buf * kTile + threadIdx.x] = lreg * LOG2E;
+      Dlb[buf * kTile + threadIdx.x] = dreg;
+    }
   };
-  if (ntiles > 0) { load_tile(q_begin); store_tile(); }
+  if (ntiles > 0) { load_tile(q_begin); store_tile(0); }
   __syncthreads();
 
   for (int it = 0; it < ntiles; ++it) {
+    const int buf = it & 1;
+    const T* Qs = img0 + (2 * buf) * kTile * D;
+    const T* Ds = Qs + kTile * D;
+    const float* Ls = Lsb + buf * kTile;
+    const float* Dl = Dlb + buf * kTile;
     const int qs0 = q_begin + it * kTile;
     if (it + 1 < ntiles) load_tile(qs0 + kTile);
     const bool need_mask = (qs0 + kTile > Sq) || (CAUSAL && (kblk0 + 127 > qs0 + off));
@@ -558,8 +609,8 @@ bwd_dkdv_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __res
         typename V8<T>::type qfr[NS], dfr[NS];
 #pragma unroll
         for (int s = 0; s < NS; ++s) {
-          qfr[s] = frag_rows<T, D>(Qs, 32 * nt + r, s, h);
-          dfr[s] = frag_rows<T, D>(Ds, 32 * nt + r, s, h);
+          qfr[s] = frag_rows_swz<T, D>(Qs, 32 * nt + r, s, h);
+          dfr[s] = frag_rows_swz<T, D>(Ds, 32 * nt + r, s, h);
         }
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -588,14 +639,15 @@ bwd_dkdv_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __res
           dp_acc[i] = p * (dp_acc[i] - da[c]);
         }
       }
-      // dV^T += dO^T P ; dK^T += Q^T dS   (k = queries of this 32-half, 2 steps of 16)
+      // dV^T += dO^T P ; dK^T += Q^T dS   (k = queries of this 32-half, 2 steps of 16);
+      // the transposed operands come straight from the row images (ds_read_b64_tr_b16)
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
         typename V8<T>::type dtr[ND], qtr[ND];
 #pragma unroll
         for (int dt = 0; dt < ND; ++dt) {
-          dtr[dt] = frag_tr<T>(Dt, 32 * dt + r, 2 * nt + ks, h);
-          qtr[dt] = frag_tr<T>(Qt, 32 * dt + r, 2 * nt + ks, h);
+          dtr[dt] = frag_trr<T, D>(Ds, dt, 2 * nt + ks, h, lane);
+          qtr[dt] = frag_trr<T, D>(Qs, dt, 2 * nt + ks, h, lane);
         }
         const typename V8<T>::type pf = pack_frag<T>(s_acc, 8 * ks);
         const typename V8<T>::type sf = pack_frag<T>(dp_acc, 8 * ks);
@@ -607,8 +659,8 @@ bwd_dkdv_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __res
         }
       }
     }
-    __syncthreads();
-    if (it + 1 < ntiles) store_tile();
+    // the idle buffer was last read before the previous barrier: fill it now
+    if (it + 1 < ntiles) store_tile(buf ^ 1);
     __syncthreads();
   }
 
@@ -655,7 +707,7 @@ static void launch_bwd(const void* q, const void* k, const void* v, const void* 
                        const int64_t* st, float scale, hipStream_t s) {
   const float sl2 = scale * 1.4426950408889634f;
   {
-    const size_t lds = (2 * Geo<D>::ROW_IMG + Geo<D>::TR_IMG) * sizeof(T);
+    const size_t lds = 4 * kTile * D * sizeof(T);
     auto go = [&](auto nwc) {
       constexpr int NW = decltype(nwc)::value;
       auto kern = bwd_dq_kernel<T, D, C, NW>;
@@ -667,7 +719,7 @@ static void launch_bwd(const void* q, const void* k, const void* v, const void* 
     go(std::integral_constant<int, 8>{});
   }
   {
-    const size_t lds = (2 * Geo<D>::ROW_IMG + 2 * Geo<D>::TR_IMG) * sizeof(T) + 2 * kTile * sizeof(float);
+    const size_t lds = 4 * kTile * D * sizeof(T) + 4 * kTile * sizeof(float);
     auto kern = bwd_dkdv_kernel<T, D, C>;
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(kern, dim3((Sk + 127) / 128, B * H), dim3(256), lds, s, (const T*)q, (const T*)k,
