@@ -87,13 +87,6 @@ __device__ __forceinline__ typename V8<T>::type pack_frag(const f32x16& acc, int
 }
 
 constexpr int kTile = 64;        // rows per staged tile (keys in fwd/dQ, queries in dK/dV)
-constexpr int kTP = kTile + 4;   // transposed-image row length (136 B rows: 8-B aligned, spread banks)
-
-template <int D> struct Geo {
-  static constexpr int RP = D + 8;                 // row-major image row length (odd # of 16-B slots)
-  static constexpr int ROW_IMG = kTile * RP;       // elements
-  static constexpr int TR_IMG = D * kTP;           // elements
-};
 
 // Swizzled tile image [64][D] (no padding), element offset of 16-B chunk ch of row `row`:
 // 8-row x 32-column subtiles of 512 B, chunk (ch&3) XOR-ed with (row>>2)&3. One image serves
@@ -124,17 +117,6 @@ struct TileRegs {
                                  : make_uint4(0, 0, 0, 0);
     }
   }
-  // row-major image [64][D+8]
-  __device__ __forceinline__ void store_rows(T* img) const {
-#pragma unroll
-    for (int p = 0; p < NPASS; ++p) {
-      const int pc = threadIdx.x + NT * p, kp = pc & 31, dc = pc >> 5;
-      if (dc < NCH) {
-        *reinterpret_cast<uint4*>(img + (2 * kp) * Geo<D>::RP + dc * 8) = r0[p];
-        *reinterpret_cast<uint4*>(img + (2 * kp + 1) * Geo<D>::RP + dc * 8) = r1[p];
-      }
-    }
-  }
   // swizzled row image [64][D] (see swz)
   __device__ __forceinline__ void store_swz(T* img) const {
 #pragma unroll
@@ -146,43 +128,8 @@ struct TileRegs {
       }
     }
   }
-  // transposed image [D][64+4]: dword (row 2kp, row 2kp+1) at [d][2kp]
-  __device__ __forceinline__ void store_tr(T* img) const {
-#pragma unroll
-    for (int p = 0; p < NPASS; ++p) {
-      const int pc = threadIdx.x + NT * p, kp = pc & 31, dc = pc >> 5;
-      if (dc < NCH) {
-        const int d0 = dc * 8;
-        const uint32_t a[4] = {r0[p].x, r0[p].y, r0[p].z, r0[p].w};
-        const uint32_t b[4] = {r1[p].x, r1[p].y, r1[p].z, r1[p].w};
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          uint32_t lo = (a[i] & 0xffffu) | (b[i] << 16);
-          uint32_t hi = (a[i] >> 16) | (b[i] & 0xffff0000u);
-          *reinterpret_cast<uint32_t*>(img + (d0 + 2 * i) * kTP + 2 * kp) = lo;
-          *reinterpret_cast<uint32_t*>(img + (d0 + 2 * i + 1) * kTP + 2 * kp) = hi;
-        }
-      }
-    }
-  }
 };
 
-// A operand (row = lane&31) from a row-major image, k-step s over D (16 wide)
-template <typename T, int D>
-__device__ __forceinline__ typename V8<T>::type frag_rows(const T* img, int row, int s, int h) {
-  return *reinterpret_cast<const typename V8<T>::type*>(img + row * Geo<D>::RP + 16 * s + 8 * h);
-}
-// A operand (row = lane&31 of the transposed image) with the permuted k order of an
-// accumulator-derived B operand: elem j <-> k = 16s + 8(j>>2) + 4h + (j&3)
-template <typename T>
-__device__ __forceinline__ typename V8<T>::type frag_tr(const T* img, int row, int s, int h) {
-  const T* p = img + row * kTP + 16 * s + 4 * h;
-  u32x2 a = *reinterpret_cast<const u32x2*>(p);
-  u32x2 b = *reinterpret_cast<const u32x2*>(p + 8);
-  u32x4 u;
-  u[0] = a[0]; u[1] = a[1]; u[2] = b[0]; u[3] = b[1];
-  return as_v8<T>(u);
-}
 // operand fragment straight from global (row pointer + d offset), zero if invalid
 template <typename T>
 __device__ __forceinline__ typename V8<T>::type frag_global(const T* rowp, int d, bool valid) {
@@ -232,9 +179,9 @@ __global__ void __launch_bounds__(NW * 64, 2)
 fwd_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restrict__ v, T* __restrict__ o,
            float* __restrict__ lse, int H, int Sq, int Sk, int64_t qsb, int64_t qss, int64_t qsh, int64_t ksb,
            int64_t kss, int64_t ksh, int64_t vsb, int64_t vss, int64_t vsh, float scale_log2) {
+  // double-buffered {K, V} swizzled images; V^T fragments by transposed reads of V
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  T* Ks = reinterpret_cast<T*>(smem);
-  T* Vt = Ks + Geo<D>::ROW_IMG;
+  T* img0 = reinterpret_cast<T*>(smem);  // [2][2][64*D]
   constexpr int NS = D / 16, ND = D / 32, BM = NW * 32;
 
   const int nqb = gridDim.x;
@@ -271,13 +218,15 @@ fwd_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restrict
   if (ntiles > 0) {
     kr.load(kb_, kss, 0, Sk);
     vr.load(vb_, vss, 0, Sk);
-    kr.store_rows(Ks);
-    vr.store_tr(Vt);
+    kr.store_swz(img0);
+    vr.store_swz(img0 + kTile * D);
   }
   __syncthreads();
 
   for (int kt = 0; kt < ntiles; ++kt) {
     const int k0 = kt * kTile;
+    const T* Ks = img0 + (2 * (kt & 1)) * kTile * D;
+    const T* Vs = Ks + kTile * D;
     if (kt + 1 < ntiles) {  // issue next tile's global loads; written after the compute
       kr.load(kb_, kss, k0 + kTile, Sk);
       vr.load(vb_, vss, k0 + kTile, Sk);
@@ -291,7 +240,7 @@ fwd_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restrict
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
-        for (int s = 0; s < NS; ++s) kfr[mt][s] = frag_rows<T, D>(Ks, 32 * mt + r, s, h);
+        for (int s = 0; s < NS; ++s) kfr[mt][s] = frag_rows_swz<T, D>(Ks, 32 * mt + r, s, h);
       // nothing crosses this point: every read is issued before the first MFMA, and the
       // waitcnt pass then counts them down (lgkmcnt(N)) one MFMA at a time
       __builtin_amdgcn_sched_barrier(0);
@@ -344,12 +293,12 @@ fwd_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restrict
     for (int ks = 0; ks < 4; ++ks) {
       const typename V8<T>::type pf = pack_frag<T>(s_acc[ks >> 1], 8 * (ks & 1));
 #pragma unroll
-      for (int dt = 0; dt < ND; ++dt) acc_o[dt] = mfma<T>(frag_tr<T>(Vt, 32 * dt + r, ks, h), pf, acc_o[dt]);
+      for (int dt = 0; dt < ND; ++dt) acc_o[dt] = mfma<T>(frag_trr<T, D>(Vs, dt, ks, h, lane), pf, acc_o[dt]);
     }
-    __syncthreads();
-    if (kt + 1 < ntiles) {
-      kr.store_rows(Ks);
-      vr.store_tr(Vt);
+    if (kt + 1 < ntiles) {  // idle buffer: last read before the previous barrier
+      T* nb = img0 + (2 * ((kt + 1) & 1)) * kTile * D;
+      kr.store_swz(nb);
+      vr.store_swz(nb + kTile * D);
     }
     __syncthreads();
   }
@@ -686,7 +635,7 @@ bwd_dkdv_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __res
 template <typename T, int D, bool C, int NW>
 static void launch_fwd_nw(const void* q, const void* k, const void* v, void* o, float* lse, int B, int H, int Sq,
                           int Sk, const int64_t* st, float scale, hipStream_t s) {
-  const size_t lds = (Geo<D>::ROW_IMG + Geo<D>::TR_IMG) * sizeof(T);
+  const size_t lds = 4 * kTile * D * sizeof(T);
   auto kern = fwd_kernel<T, D, C, NW>;
   hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   dim3 grid((Sq + NW * 32 - 1) / (NW * 32), B * H);
