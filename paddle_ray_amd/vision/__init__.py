@@ -1,5 +1,5 @@
 """paddle.vision (parity: python/paddle/vision/__init__.py)."""
-from . import models, transforms, datasets  # noqa
+from . import models, transforms, datasets, ops  # noqa
 from .models import *  # noqa
 
 
