@@ -251,6 +251,15 @@ fwd_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restrict
         for (int s = 0; s < NS; ++s) s_acc[mt] = mfma<T>(kfr[mt][s], qf[s], s_acc[mt]);
       }
     }
+    // V^T fragments of the PV product, issued right behind the S MFMAs (the K fragment
+    // registers are free again) so the transposed LDS reads land under the softmax VALU
+    // (the first two k-steps only: all four would exceed the 256-VGPR occupancy-2 budget)
+    typename V8<T>::type vfr[2][ND];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int dt = 0; dt < ND; ++dt) vfr[ks][dt] = frag_trr<T, D>(Vs, dt, ks, h, lane);
+    __builtin_amdgcn_sched_barrier(0);
     const bool need_mask = (k0 + kTile > Sk) || (CAUSAL && (k0 + kTile - 1 > q0 + off));
     if (need_mask) {
 #pragma unroll
@@ -293,7 +302,8 @@ fwd_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restrict
     for (int ks = 0; ks < 4; ++ks) {
       const typename V8<T>::type pf = pack_frag<T>(s_acc[ks >> 1], 8 * (ks & 1));
 #pragma unroll
-      for (int dt = 0; dt < ND; ++dt) acc_o[dt] = mfma<T>(frag_trr<T, D>(Vs, dt, ks, h, lane), pf, acc_o[dt]);
+      for (int dt = 0; dt < ND; ++dt)
+        acc_o[dt] = mfma<T>(ks < 2 ? vfr[ks & 1][dt] : frag_trr<T, D>(Vs, dt, ks, h, lane), pf, acc_o[dt]);
     }
     if (kt + 1 < ntiles) {  // idle buffer: last read before the previous barrier
       T* nb = img0 + (2 * ((kt + 1) & 1)) * kTile * D;
