@@ -25,7 +25,7 @@ from .framework.io import save, load  # noqa
 from .framework import flags as _flags  # noqa
 from .framework.flags import set_flags, get_flags  # noqa
 from . import nn, optimizer, autograd, amp, io, static, jit, distributed, incubate, vision, metric  # noqa
-from . import audio, text, quantization, reader, dataset  # noqa: E402
+from . import audio, text, quantization, reader, dataset, cost_model  # noqa: E402
 from . import linalg, fft, device, utils, profiler, hapi, sparse, distribution, signal, models  # noqa
 from . import framework, inference, geometric, regularizer, callbacks, sysconfig, hub, onnx  # noqa
 from .autograd import grad, PyLayer  # noqa

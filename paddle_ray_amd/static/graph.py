@@ -19,6 +19,7 @@ import importlib
 import itertools
 import json
 import os
+import time
 
 import numpy as np
 import torch
@@ -565,6 +566,15 @@ class Executor:
 
     def __init__(self, place=None):
         self.place = place
+        self._op_costs = None  # list of (op type, ms) when per-op timing is on (CostModel)
+
+    def enable_op_timing(self, on=True):
+        """Record every executed op's wall time (device-synchronized) in ``op_costs``."""
+        self._op_costs = [] if on else None
+
+    @property
+    def op_costs(self):
+        return list(self._op_costs or [])
 
     def close(self):
         pass
@@ -630,9 +640,18 @@ class Executor:
         _STATIC[0] = False
         try:
             ops = blk.ops
+            timing = self._op_costs is not None
+            sync = torch.cuda.synchronize if timing and torch.cuda.is_available() else \
+                (lambda: None)
             for pos, oi in enumerate(order):
                 op = ops[oi]
+                if timing:
+                    sync()
+                    t0 = time.perf_counter()
                 res = op.fn(*_materialize(op.args, env), **_materialize(op.kwargs, env))
+                if timing:
+                    sync()
+                    self._op_costs.append((op.type, (time.perf_counter() - t0) * 1e3))
                 if op.out_vids:
                     flat, _ = _flatten_out(res)
                     for vid, t in zip(op.out_vids, flat):

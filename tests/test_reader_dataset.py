@@ -93,3 +93,20 @@ def test_dataset_image_helpers():
     out = I.simple_transform(im, 32, 24, is_train=False, mean=[1.0, 2.0, 3.0])
     assert out.shape == (3, 24, 24) and out.dtype == np.float32
     assert I.random_crop(im, 10).shape == (10, 10, 3)
+
+
+def test_cost_model():
+    cm = paddle.cost_model.CostModel()
+    s, m = cm.build_program()
+    try:
+        r = cm.profile_measure(s, m, device='cpu')
+    finally:
+        paddle.disable_static()
+    assert r['time'] > 0 and 'backward' in r['op_time'] and len(r['ops']) >= 3
+    data = cm.static_cost_data()  # measured on MI355X by scripts/op_benchmark.py
+    assert any(d['op'] == 'flash_attention' for d in data)
+    fwd = cm.get_static_op_time('matmul', forward=True, dtype='bfloat16')
+    bwd = cm.get_static_op_time('matmul', forward=False, dtype='bfloat16')
+    assert fwd['op_time'] > 0 and bwd['op_time'] > 0 and 'bfloat16' in fwd['config']
+    with pytest.raises(ValueError):
+        cm.get_static_op_time(None)
