@@ -10,16 +10,21 @@
 //                   (one __shfl_xor(.,32) for the row max/sum).
 //   O^T += V^T P^T -> P^T's accumulator registers ARE the B operand (k order
 //                   permuted: elem j of lane-half h <-> key 16s+8(j>>2)+4h+(j&3)),
-//                   V^T comes from a transposed LDS image read as 2x ds_read_b64.
+//                   V^T comes from the same swizzled V tile image through
+//                   ds_read_b64_tr_b16 (hardware transposed read, guide T10).
 //                   The O^T accumulator is again one query per lane, so the
 //                   online-softmax rescale is lane-local too.
 // Backward = FA2 split into a dK/dV kernel (keys on lanes, sweep queries) and a
 // dQ kernel (queries on lanes, sweep keys): no float atomics (MI355X atomics
 // are ~1.3 TB/s chip-wide; dQ atomics would cost more than the whole backward).
 //
-// Workgroup = 4 waves (256 threads); each wave owns 32 queries (fwd, dQ) or 32
-// keys (dK/dV); K/V (resp. Q/dO) tiles of 64 rows staged through LDS with
-// register prefetch of the next tile (async-STAGE split, guide T14).
+// Tiles of 64 rows (K/V in fwd and dQ, Q/dO in dK/dV) are staged ONCE per tile into a
+// swizzled LDS image (8x32 subtiles, XOR chunk swizzle) that serves both row fragments
+// (ds_read_b128) and transposed fragments; two LDS buffers alternate so the next tile is
+// written right after the current tile's MFMAs (one barrier per tile), with its global
+// loads issued at the top of the iteration (async-STAGE split, guide T14).
+// fwd / dQ: 8 waves, 32 queries per wave (2 waves per SIMD); dK/dV: 4 waves, 32 keys per
+// wave (one wave per SIMD, 256 + accumulator registers).
 #include "common.h"
 #include <stdlib.h>
 #include <type_traits>

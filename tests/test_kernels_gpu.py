@@ -377,3 +377,23 @@ def test_embedding_out_of_range_reads_zero():
     out = F.embedding(ids, w, None)
     assert torch.equal(out[0, 2:], torch.zeros(3, 16, device=DEV))
     assert torch.equal(out[0, :2], w[[0, 9]])
+
+
+def test_memory_efficient_attention_block_diagonal_gpu():
+    """Packed variable-length sequences run the HIP flash kernel per block (causal and not)."""
+    import paddle_ray_amd as paddle
+    from paddle_ray_amd.incubate.nn import attn_bias as AB, memory_efficient_attention
+    torch.manual_seed(0)
+    lens = [64, 128, 40]
+    q, k, v = (torch.randn(1, sum(lens), 4, 128, device=DEV, dtype=torch.bfloat16)
+               for _ in range(3))
+    for bias in (AB.BlockDiagonalMask.from_seqlens(lens),
+                 AB.BlockDiagonalMask.from_seqlens(lens).make_causal()):
+        R.reset_stats()
+        out = memory_efficient_attention(paddle.Tensor(q), paddle.Tensor(k), paddle.Tensor(v),
+                                         bias)._t
+        assert R.stats().get(('flash_attn_fwd', 'hip'), 0) == len(lens)
+        dense = bias.materialize([1, 4, sum(lens), sum(lens)])._t.to(DEV)
+        s = torch.einsum('bmhk,bnhk->bhmn', q.float(), k.float()) / math.sqrt(128) + dense
+        ref = torch.einsum('bhmn,bnhk->bmhk', torch.softmax(s, -1), v.float())
+        assert (out.float() - ref).abs().max().item() < 2e-2
