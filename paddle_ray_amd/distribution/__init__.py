@@ -92,11 +92,23 @@ class TransformedDistribution(Distribution):
         self._d = D.TransformedDistribution(base._d, [t._t for t in transforms])
 
 
+_KL_REGISTRY = {}
+
+
 def kl_divergence(p, q):
+    """KL(p || q): user registrations (register_kl) first, then the closed forms."""
+    for (cp, cq), fn in _KL_REGISTRY.items():
+        if isinstance(p, cp) and isinstance(q, cq):
+            return fn(p, q)
     return Tensor(D.kl_divergence(p._d, q._d))
 
 
 def register_kl(cls_p, cls_q):
+    """Decorator registering ``fn(p, q)`` as KL(p || q) for the two distribution classes."""
     def deco(fn):
+        _KL_REGISTRY[(cls_p, cls_q)] = fn
         return fn
     return deco
+
+from . import transform  # noqa: E402
+from .transform import *  # noqa: E402,F401,F403

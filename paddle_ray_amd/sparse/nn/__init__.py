@@ -1,16 +1,221 @@
+"""paddle.sparse.nn (parity: python/paddle/sparse/nn/{layer,functional}).
+
+Sparse COO tensors here are torch sparse tensors whose sparse dims are (N, D, H, W) and
+whose dense dim is the channel (NDHWC, values [nnz, C]) -- the reference's layout for 3-D
+point-cloud / voxel networks. Convolutions compute on the densified grid and keep the
+sparse-conv output pattern: a regular Conv3D activates every output site reached by an
+active input site, a submanifold conv keeps exactly the input's active sites.
+"""
 import torch
+import torch.nn.functional as TF
 
 from ...framework.core import Tensor, _u
 from ...nn.layer.layers import Layer
+from ...nn import initializer as I
 
 
-class ReLU(Layer):
-    def forward(self, x):
-        t = _u(x).coalesce()
-        return Tensor(torch.sparse_coo_tensor(t.indices(), torch.relu(t.values()), t.shape))
+def _coo(x):
+    t = _u(x)
+    return t.coalesce() if t.layout == torch.sparse_coo else t.to_sparse_coo().coalesce()
+
+
+def _like(t, values):
+    return Tensor(torch.sparse_coo_tensor(t.indices(), values, t.shape).coalesce())
+
+
+def _triple(v):
+    return (v, v, v) if isinstance(v, int) else tuple(v)
+
+
+def _from_dense(dense_ndhwc, active):
+    """Sparse COO of ``dense`` at the boolean ``active`` [N, D, H, W] sites."""
+    idx = active.nonzero().t()
+    vals = dense_ndhwc[active]
+    return Tensor(torch.sparse_coo_tensor(idx, vals, dense_ndhwc.shape).coalesce())
 
 
 class functional:
     @staticmethod
-    def relu(x):
-        return ReLU()(x)
+    def relu(x, name=None):
+        t = _coo(x)
+        return _like(t, torch.relu(t.values()))
+
+    @staticmethod
+    def relu6(x, name=None):
+        t = _coo(x)
+        return _like(t, torch.clamp(t.values(), 0, 6))
+
+    @staticmethod
+    def leaky_relu(x, negative_slope=0.01, name=None):
+        t = _coo(x)
+        return _like(t, TF.leaky_relu(t.values(), negative_slope))
+
+    @staticmethod
+    def softmax(x, axis=-1, name=None):
+        """Softmax over the stored entries of each row (missing entries are -inf)."""
+        t = _u(x)
+        csr = t.layout == torch.sparse_csr
+        coo = t.to_sparse_coo().coalesce() if csr else t.coalesce()
+        out = torch.sparse.softmax(coo, dim=axis if axis >= 0 else coo.dim() + axis)
+        return Tensor(out.to_sparse_csr() if csr else out)
+
+    @staticmethod
+    def _conv(x, weight, bias, stride, padding, dilation, groups, subm):
+        t = _coo(x)
+        dense = t.to_dense()  # [N, D, H, W, C]
+        w = _u(weight)  # [kD, kH, kW, Cin/groups, Cout]
+        stride, padding, dilation = _triple(stride), _triple(padding), _triple(dilation)
+        if subm:
+            stride = (1, 1, 1)
+            padding = tuple(d * (k - 1) // 2 for d, k in zip(dilation, w.shape[:3]))
+        inp = dense.permute(0, 4, 1, 2, 3)
+        out = TF.conv3d(inp, w.permute(4, 3, 0, 1, 2), None, stride, padding, dilation, groups)
+        out = out.permute(0, 2, 3, 4, 1)
+        if bias is not None:
+            out = out + _u(bias)
+        occ = torch.zeros(dense.shape[:4], dtype=dense.dtype, device=dense.device)
+        occ[tuple(t.indices())] = 1.0
+        if subm:
+            active = occ > 0
+        else:
+            k = torch.ones((1, 1) + tuple(w.shape[:3]), dtype=occ.dtype, device=occ.device)
+            active = TF.conv3d(occ[:, None], k, None, stride, padding, dilation)[:, 0] > 0
+        return _from_dense(out, active)
+
+    @staticmethod
+    def conv3d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1,
+               data_format='NDHWC', name=None):
+        return functional._conv(x, weight, bias, stride, padding, dilation, groups, False)
+
+    @staticmethod
+    def subm_conv3d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1,
+                    data_format='NDHWC', key=None, name=None):
+        return functional._conv(x, weight, bias, stride, padding, dilation, groups, True)
+
+    @staticmethod
+    def max_pool3d(x, kernel_size, stride=None, padding=0, ceil_mode=False,
+                   data_format='NDHWC', name=None):
+        """Max over the ACTIVE sites of each window; windows without one stay inactive."""
+        t = _coo(x)
+        dense = t.to_dense()
+        occ = torch.zeros(dense.shape[:4], dtype=torch.bool, device=dense.device)
+        occ[tuple(t.indices())] = True
+        neg = torch.finfo(dense.dtype).min
+        filled = torch.where(occ[..., None], dense, torch.full_like(dense, neg))
+        k = _triple(kernel_size)
+        s = _triple(stride) if stride is not None else k
+        p = _triple(padding)
+        out = TF.max_pool3d(filled.permute(0, 4, 1, 2, 3), k, s, p, ceil_mode=ceil_mode)
+        act = TF.max_pool3d(occ[:, None].float(), k, s, p, ceil_mode=ceil_mode)[:, 0] > 0
+        return _from_dense(out.permute(0, 2, 3, 4, 1), act)
+
+    @staticmethod
+    def attention(query, key, value, sparse_mask, key_padding_mask=None, attn_mask=None,
+                  name=None):
+        """softmax(QK^T / sqrt(d)) V restricted to the sparsity pattern of ``sparse_mask``
+        ([B*H, S, S] CSR); q/k/v are [B, H, S, D]."""
+        q, k, v = _u(query), _u(key), _u(value)
+        B, H, S, Dh = q.shape
+        m = _u(sparse_mask)
+        m = (m.to_dense() if m.layout != torch.strided else m).reshape(B, H, S, S) != 0
+        s = torch.matmul(q, k.transpose(-1, -2)) / (Dh ** 0.5)
+        s = s.masked_fill(~m, float('-inf'))
+        if key_padding_mask is not None:
+            s = s.masked_fill(_u(key_padding_mask).reshape(B, 1, 1, S) == 0, float('-inf'))
+        if attn_mask is not None:
+            s = s.masked_fill(_u(attn_mask).reshape(1, 1, S, S) == 0, float('-inf'))
+        a = torch.nan_to_num(torch.softmax(s, -1))
+        return Tensor(torch.matmul(a, v))
+
+
+class ReLU(Layer):
+    def forward(self, x):
+        return functional.relu(x)
+
+
+class ReLU6(Layer):
+    def forward(self, x):
+        return functional.relu6(x)
+
+
+class LeakyReLU(Layer):
+    def __init__(self, negative_slope=0.01, name=None):
+        super().__init__()
+        self._slope = negative_slope
+
+    def forward(self, x):
+        return functional.leaky_relu(x, self._slope)
+
+
+class Softmax(Layer):
+    def __init__(self, axis=-1, name=None):
+        super().__init__()
+        self._axis = axis
+
+    def forward(self, x):
+        return functional.softmax(x, self._axis)
+
+
+class _Conv3DBase(Layer):
+    _subm = False
+
+    def __init__(self, in_channels, out_channels, kernel_size, stride=1, padding=0, dilation=1,
+                 groups=1, padding_mode='zeros', key=None, weight_attr=None, bias_attr=None,
+                 data_format='NDHWC'):
+        super().__init__()
+        k = _triple(kernel_size)
+        self._stride, self._padding, self._dilation, self._groups = stride, padding, dilation, \
+            groups
+        fan_in = in_channels // groups * k[0] * k[1] * k[2]
+        self.weight = self.create_parameter(
+            [k[0], k[1], k[2], in_channels // groups, out_channels], attr=weight_attr,
+            default_initializer=I.Normal(0.0, (2.0 / fan_in) ** 0.5))
+        self.bias = None if bias_attr is False else self.create_parameter(
+            [out_channels], attr=bias_attr, is_bias=True)
+
+    def forward(self, x):
+        fn = functional.subm_conv3d if self._subm else functional.conv3d
+        return fn(x, self.weight, self.bias, self._stride, self._padding, self._dilation,
+                  self._groups)
+
+
+class Conv3D(_Conv3DBase):
+    pass
+
+
+class SubmConv3D(_Conv3DBase):
+    _subm = True
+
+
+class MaxPool3D(Layer):
+    def __init__(self, kernel_size, stride=None, padding=0, return_mask=False, ceil_mode=False,
+                 data_format='NDHWC', name=None):
+        super().__init__()
+        self._k, self._s, self._p, self._ceil = kernel_size, stride, padding, ceil_mode
+
+    def forward(self, x):
+        return functional.max_pool3d(x, self._k, self._s, self._p, self._ceil)
+
+
+class BatchNorm(Layer):
+    """BatchNorm over the channel of the stored values ([nnz, C]) of a sparse tensor."""
+
+    def __init__(self, num_features, momentum=0.9, epsilon=1e-05, weight_attr=None,
+                 bias_attr=None, data_format='NDHWC', use_global_stats=None, name=None):
+        super().__init__()
+        from ...nn import BatchNorm1D
+        self._bn = BatchNorm1D(num_features, momentum, epsilon, weight_attr, bias_attr)
+
+    def forward(self, x):
+        t = _coo(x)
+        return _like(t, _u(self._bn(Tensor(t.values()))))
+
+
+class SyncBatchNorm(BatchNorm):
+    """Cross-rank statistics come from the dense SyncBatchNorm when a process group is up."""
+
+    def __init__(self, num_features, momentum=0.9, epsilon=1e-05, weight_attr=None,
+                 bias_attr=None, data_format='NDHWC', name=None):
+        Layer.__init__(self)
+        from ...nn import SyncBatchNorm as _Sync
+        self._bn = _Sync(num_features, momentum, epsilon, weight_attr, bias_attr, 'NCL')
