@@ -50,6 +50,8 @@ int pra_embedding_bwd(const int64_t*, const int64_t*, const void*, void*, int64_
 void pra_bias_gelu_bwd_db(const void*, const void*, const void*, void*, float*, int, int, int, int, int,
                           hipStream_t);
 int pra_bn_nrb(int, int);
+int pra_gemm_bias_act(const void*, const void*, const void*, void*, void*, int, int, int, int, int, int, int, int,
+                      hipStream_t);
 void pra_bn_fwd_train(const void*, const void*, const void*, const void*, float*, float*, void*, uint8_t*, float*,
                       float*, float*, float*, int, int, int, float, float, int, int, int, hipStream_t);
 void pra_bn_fwd_infer(const void*, const void*, const void*, const void*, const float*, const float*, void*, float*,
@@ -72,6 +74,12 @@ static void check_launch(const char* what) {
 
 PYBIND11_MODULE(_pra_hip, m) {
   m.doc() = "paddle_ray_amd gfx950 HIP kernels";
+  m.def("gemm_bias_act", [](P a, P b, P bias, P c, P z, int M, int N, int K, int lda, int ldb, int ldc, int dt, int act,
+                            P s) {
+    if (pra_gemm_bias_act(CV(a), CV(b), CV(bias), V(c), V(z), M, N, K, lda, ldb, ldc, dt, act, S(s)) != 0)
+      throw std::invalid_argument("gemm_bias_act: unsupported shape/stride/dtype");
+    check_launch("gemm_bias_act");
+  });
   m.def("layernorm_fwd", [](P x, P w, P b, P y, P mean, P rstd, int rows, int cols, float eps, int dtx, int dtw, P s) {
     pra_layernorm_fwd(CV(x), CV(w), CV(b), V(y), F(mean), F(rstd), rows, cols, eps, dtx, dtw, S(s));
     check_launch("layernorm_fwd");

@@ -1116,3 +1116,99 @@ def embedding(ids, w, padding_idx=None):
     if w.requires_grad and torch.is_grad_enabled():
         return EmbeddingFn.apply(ids, w, padding_idx)
     return R.dispatch('embedding_fwd', w, ids, w, padding_idx)
+
+
+# =============================================================================
+# GEMM + bias + activation (MFMA kernel, gemm.hip). Parity: reference
+# paddle/phi/kernels/fusion/gpu/fused_gemm_epilogue_kernel.cu (cublasLt BIAS / GELU / RELU
+# epilogues) behind python/paddle/incubate/nn/functional/fused_matmul_bias.py.
+# =============================================================================
+_ACT = {None: 0, 'none': 0, 'gelu': 1, 'gelu_tanh': 2, 'relu': 3}
+
+
+def _act_ref(z, act):
+    if act == 1:
+        return torch.nn.functional.gelu(z)
+    if act == 2:
+        return torch.nn.functional.gelu(z, approximate='tanh')
+    if act == 3:
+        return torch.relu(z)
+    return z
+
+
+@R.register_kernel('gemm_bias_act', 'ref')
+def _gba_ref(x2, w, b, act, want_z):
+    z = x2.float() @ w.float()
+    if b is not None:
+        z = z + b.float()
+    y = _act_ref(z, act).to(x2.dtype)
+    return y, (z.to(x2.dtype) if want_z and act else None)
+
+
+@R.register_kernel('gemm_bias_act', 'hip')
+def _gba_hip(x2, w, b, act, want_z):
+    M, K = x2.shape
+    N = w.shape[1]
+    y = torch.empty(M, N, dtype=x2.dtype, device=x2.device)
+    z = torch.empty_like(y) if (want_z and act) else None
+    _native.lib().gemm_bias_act(_ptr(x2), _ptr(w), _ptr(b), _ptr(y), _ptr(z), M, N, K, x2.stride(0),
+                                w.stride(0), N, _dt(x2), act, _stream())
+    return y, z
+
+
+def gemm_supported(x2, w):
+    """Shapes/layouts the MFMA kernel takes: 2-byte dtypes, 16-B aligned row-major rows."""
+    return (x2.dtype in (torch.bfloat16, torch.float16) and w.dtype == x2.dtype and x2.dim() == 2
+            and w.dim() == 2 and x2.stride(1) == 1 and w.stride(1) == 1 and x2.shape[1] == w.shape[0]
+            and x2.shape[1] % 8 == 0 and w.shape[1] % 8 == 0 and x2.stride(0) % 8 == 0
+            and w.stride(0) % 8 == 0 and x2.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0)
+
+
+class GemmBiasActFn(torch.autograd.Function):
+    """y = act(x @ w + b) with the epilogue fused into the MFMA GEMM; backward keeps the
+    pre-activation the kernel wrote alongside y and runs hipBLASLt for dX / dW."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, act):
+        shp = x.shape
+        x2 = x.reshape(-1, shp[-1])
+        if x2.stride(-1) != 1 or x2.stride(0) % 8 or x2.data_ptr() % 16:
+            x2 = x2.contiguous()  # row pitch may exceed K (lda), rows must stay 16-B aligned
+        if b is not None:
+            b = b.to(x.dtype).contiguous()
+            if b.data_ptr() % 8:
+                b = b.clone()
+        need = any(ctx.needs_input_grad[:3])
+        y, z = R.dispatch('gemm_bias_act', x2, x2, w, b, act, need)
+        ctx.save_for_backward(x2, w, z)
+        ctx.act, ctx.has_b, ctx.shp = act, b is not None, shp
+        return y.view(*shp[:-1], w.shape[1])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w, z = ctx.saved_tensors
+        dy2 = dy.reshape(-1, w.shape[1])
+        if ctx.act in (1, 2):  # GELU': the elementwise HIP kernel on the saved pre-activation
+            dy2 = dy2.contiguous()
+            dz = R.dispatch('bias_gelu_bwd', dy2, dy2, z, None, ctx.act == 2)
+        elif ctx.act:
+            with torch.enable_grad():
+                zf = z.detach().requires_grad_(True)
+                (dz,) = torch.autograd.grad(_act_ref(zf, ctx.act), zf, dy2)
+        else:
+            dz = dy2
+        dx = (dz @ w.t()).view(ctx.shp) if ctx.needs_input_grad[0] else None
+        dw = x2.t() @ dz if ctx.needs_input_grad[1] else None
+        db = dz.sum(0, dtype=torch.float32).to(dz.dtype) if (ctx.has_b and ctx.needs_input_grad[2]) else None
+        return dx, dw, db, None
+
+
+def gemm_bias_act(x, w, b=None, act=None):
+    """act(x @ w + b) for x [..., K], w [K, N] (Paddle Linear layout). On the GPU this is one
+    MFMA kernel launch (gemm.hip); unsupported layouts fall back to matmul + epilogue."""
+    a = _ACT[act] if not isinstance(act, int) else act
+    x2 = x.reshape(-1, x.shape[-1])
+    if x.is_cuda and not gemm_supported(x2 if x2.is_contiguous() else x2.contiguous(), w):
+        z = torch.matmul(x, w)
+        return _act_ref(z if b is None else z + b, a)
+    return GemmBiasActFn.apply(x, w, b, a)
