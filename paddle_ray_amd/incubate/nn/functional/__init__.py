@@ -42,6 +42,20 @@ def fused_linear(x, weight, bias=None, transpose_weight=False, name=None):
     return fused_matmul_bias(x, weight, bias, False, transpose_weight)
 
 
+def fused_linear_activation(x, y, bias, trans_x=False, trans_y=False, activation=None):
+    """act(x @ y + bias) with the epilogue fused into one gfx950 MFMA GEMM launch
+    (ops/csrc/gemm.hip; parity: reference python/paddle/incubate/nn/functional/
+    fused_matmul_bias.py `fused_linear_activation`, activation in {None, 'none', 'gelu', 'relu'})."""
+    a, b = _u(x), _u(y)
+    if trans_x:
+        a = a.transpose(-1, -2)
+    if trans_y:
+        b = b.t().contiguous()
+    if activation not in (None, 'none', 'gelu', 'gelu_tanh', 'relu'):
+        raise ValueError(f"fused_linear_activation: unsupported activation {activation!r}")
+    return Tensor(K.gemm_bias_act(a, b, _t(bias), activation))
+
+
 def fused_dropout_add(x, y, p=0.5, training=True, mode='upscale_in_train', name=None):
     return Tensor(_drop(_u(x), p, training, mode) + _u(y))
 

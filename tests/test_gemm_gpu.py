@@ -61,3 +61,18 @@ def test_gemm_bias_act_backward(act):
     for a, r in ((x.grad, xr.grad), (w.grad, wr.grad), (b.grad, br.grad)):
         scale = r.abs().max().item() + 1e-6
         assert (a.float() - r).abs().max().item() / scale < 3e-2
+
+
+def test_fused_linear_activation_runs_mfma():
+    import paddle_ray_amd as paddle
+    from paddle_ray_amd.incubate.nn import functional as IF
+    _native.require()
+    x = torch.randn(64, 256, device='cuda', dtype=torch.bfloat16)
+    w = torch.randn(512, 256, device='cuda', dtype=torch.bfloat16) / 16
+    b = torch.randn(512, device='cuda', dtype=torch.bfloat16)
+    R.reset_stats()
+    y = IF.fused_linear_activation(paddle.Tensor(x), paddle.Tensor(w), paddle.Tensor(b), trans_y=True,
+                                   activation='gelu')
+    assert R.stats().get(('gemm_bias_act', 'hip'), 0) == 1
+    ref = torch.nn.functional.gelu(x.float() @ w.float().t() + b.float())
+    torch.testing.assert_close(y._t.float(), ref, atol=2e-2, rtol=2e-2)

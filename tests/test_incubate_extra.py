@@ -149,3 +149,18 @@ def test_multiprocessing_shares_cpu_tensors():
         if p.is_alive():
             p.kill()
     assert mp is not None and float(t.numpy().sum()) == 4.0
+
+
+def test_fused_linear_activation_cpu():
+    import paddle_ray_amd as paddle
+    from paddle_ray_amd.incubate.nn import functional as IF
+    x = paddle.randn([3, 5, 16])
+    w = paddle.randn([16, 24])
+    b = paddle.randn([24])
+    for act in (None, 'gelu', 'relu'):
+        y = IF.fused_linear_activation(x, w, b, activation=act)
+        z = x._t @ w._t + b._t
+        ref = {None: z, 'gelu': torch.nn.functional.gelu(z), 'relu': torch.relu(z)}[act]
+        assert torch.allclose(y._t, ref, atol=1e-5)
+    y = IF.fused_linear_activation(x, paddle.Tensor(w._t.t().contiguous()), b, trans_y=True, activation='relu')
+    assert torch.allclose(y._t, torch.relu(x._t @ w._t + b._t), atol=1e-5)
