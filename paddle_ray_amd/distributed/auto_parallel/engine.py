@@ -1,0 +1,260 @@
+"""auto_parallel.Engine (parity: reference python/paddle/distributed/auto_parallel/engine.py:
+Engine(model, loss, optimizer, metrics, cluster, strategy) with fit/evaluate/predict/save/load).
+
+Eager MI355X design: no program completion/partitioning. Batches are split over mesh axis 0
+(DistributedBatchSampler with that axis' size/coordinate); after backward every gradient is
+all-reduced (mean) over the mesh axes its parameter is replicated on and data is split over —
+one flat bucket per step so RCCL sees a single large collective; sharded (tensor-parallel)
+parameters keep their shard-local gradient on the other axes. Strategy sections honoured:
+amp (bf16/fp16 auto_cast + GradScaler for fp16), recompute (whole-model recompute),
+gradient_merge (k_steps accumulation), seed.
+"""
+import numpy as np
+import torch
+
+from ...framework.core import Tensor, _u
+from .. import collective as C
+from . import ProcessMesh, dist_attr, _fetches, _world_mesh
+from .strategy import Strategy
+
+
+def _to_list(x):
+    if x is None:
+        return []
+    return list(x) if isinstance(x, (list, tuple)) else [x]
+
+
+class Engine:
+    def __init__(self, model=None, loss=None, optimizer=None, metrics=None, cluster=None, strategy=None):
+        self._model, self._loss, self._optimizer = model, loss, optimizer
+        self._metrics = _to_list(metrics)
+        self._strategy = strategy if strategy is not None else Strategy()
+        self._mesh = None
+        self._scaler = None
+        self.history = None
+        self._merge_count = 0
+        if self._strategy.seed is not None:
+            from ... import seed as _seed
+            _seed(self._strategy.seed)
+
+    # ------------------------------------------------------------------ placement
+    def _resolve_mesh(self):
+        if self._mesh is not None:
+            return self._mesh
+        for p in self._model.parameters():
+            a = dist_attr(p)
+            if a is not None:
+                self._mesh = a.process_mesh
+                break
+        if self._mesh is None:
+            self._mesh = _world_mesh()
+        return self._mesh
+
+    def _dp(self):
+        """(group, size, coordinate) of mesh axis 0, the data-parallel axis."""
+        mesh = self._resolve_mesh()
+        coord = mesh.coord()
+        if coord is None or C.get_world_size() == 1:
+            return None, 1, 0
+        return mesh.axis_group(0), mesh.shape[0], coord[0]
+
+    def _sync_grads(self):
+        group, n, _ = self._dp()
+        if n == 1:
+            return
+        grads = []
+        for p in self._model.parameters():
+            g = p._t.grad
+            if g is None:
+                continue
+            a = dist_attr(p)
+            if a is not None and a.process_mesh == self._mesh and 0 in a.dims_mapping:
+                continue  # sharded over the batch axis: its gradient is already shard-local
+            grads.append(g)
+        if not grads:
+            return
+        flat = torch.cat([g.reshape(-1).float() for g in grads])
+        torch.distributed.all_reduce(flat, group=group.process_group)
+        flat /= n
+        off = 0
+        for g in grads:
+            k = g.numel()
+            g.copy_(flat[off:off + k].view_as(g).to(g.dtype))
+            off += k
+
+    # ------------------------------------------------------------------ data
+    def _loader(self, data, batch_size, shuffle, collate_fn, drop_last=False):
+        from ...io import DataLoader, DistributedBatchSampler, Dataset
+        if data is None:
+            return None
+        if not isinstance(data, Dataset) and hasattr(data, '__iter__') and not hasattr(data, '__getitem__'):
+            return data
+        _, n, r = self._dp()
+        if not self._strategy.split_data:
+            n, r = 1, 0
+        bs = DistributedBatchSampler(data, batch_size, num_replicas=n, rank=r, shuffle=shuffle,
+                                     drop_last=drop_last)
+        return DataLoader(data, batch_sampler=bs, collate_fn=collate_fn)
+
+    @staticmethod
+    def _split(batch, sample_split):
+        batch = _to_list(batch)
+        if sample_split is None:
+            sample_split = len(batch) - 1 if len(batch) > 1 else len(batch)
+        return batch[:sample_split], batch[sample_split:]
+
+    # ------------------------------------------------------------------ steps
+    def _forward(self, inputs):
+        amp = self._strategy.amp
+        fwd = self._model
+        if self._strategy.recompute.enable:
+            from . import recompute
+            fwd = recompute(self._model)
+        if amp.enable:
+            from ...amp import auto_cast
+            with auto_cast(True, level=amp.level.upper(), dtype=amp.dtype):
+                return fwd(*inputs)
+        return fwd(*inputs)
+
+    def _compute_loss(self, outs, labels):
+        if self._loss is None:
+            return outs[0] if isinstance(outs, (list, tuple)) else outs
+        return self._loss(*(_to_list(outs) + labels))
+
+    def _update_metrics(self, outs, labels):
+        res = {}
+        for m in self._metrics:
+            r = m.compute(*(_to_list(outs) + labels))
+            m.update(*[x.numpy() if isinstance(x, Tensor) else x for x in _to_list(r)])
+            acc = m.accumulate()
+            names = _to_list(m.name())
+            for nme, v in zip(names, _to_list(acc)):
+                res[nme] = v
+        return res
+
+    def _train_step(self, inputs, labels):
+        gm = self._strategy.gradient_merge
+        k = gm.k_steps if gm.enable else 1
+        outs = self._forward(inputs)
+        loss = self._compute_loss(outs, labels)
+        scaled = loss / k if (k > 1 and gm.avg) else loss
+        if self._strategy.amp.enable and self._strategy.amp.dtype == 'float16':
+            if self._scaler is None:
+                from ...amp import GradScaler
+                self._scaler = GradScaler(init_loss_scaling=self._strategy.amp.init_loss_scaling)
+            self._scaler.scale(scaled).backward()
+        else:
+            scaled.backward()
+        self._merge_count += 1
+        if self._merge_count % k == 0:
+            self._sync_grads()
+            if self._scaler is not None:
+                self._scaler.step(self._optimizer)
+                self._scaler.update()
+            else:
+                self._optimizer.step()
+            self._optimizer.clear_grad()
+        return loss, outs
+
+    def _fetch_logs(self):
+        out = {}
+        for name, (t, _) in _fetches.items():
+            out[name] = t.numpy() if isinstance(t, Tensor) else t
+        return out
+
+    # ------------------------------------------------------------------ public API
+    def prepare(self, inputs_spec=None, labels_spec=None, inputs=None, labels=None, main_program=None,
+                startup_program=None, mode='train'):
+        self._resolve_mesh()
+        return self
+
+    def fit(self, train_data, train_sample_split=None, batch_size=1, epochs=1, steps_per_epoch=None,
+            log_freq=10, save_dir=None, save_freq=1, valid_data=None, valid_sample_split=None, valid_freq=1,
+            valid_steps=None, collate_fn=None, callbacks=None, verbose=2, nvprof_range=None):
+        assert self._optimizer is not None, "fit() needs an optimizer"
+        self._model.train()
+        loader = self._loader(train_data, batch_size, False, collate_fn)
+        history = {'loss': []}
+        for epoch in range(epochs):
+            for m in self._metrics:
+                m.reset()
+            for step, batch in enumerate(loader):
+                if steps_per_epoch is not None and step >= steps_per_epoch:
+                    break
+                inputs, labels = self._split(batch, train_sample_split)
+                loss, outs = self._train_step(inputs, labels)
+                history['loss'].append(float(loss))
+                logs = self._update_metrics(outs, labels) if self._metrics else {}
+                logs.update(self._fetch_logs())
+                for kk, v in logs.items():
+                    history.setdefault(kk, []).append(v)
+                if verbose and log_freq and step % log_freq == 0 and C.get_rank() == 0:
+                    print(f"[Engine] epoch {epoch} step {step} loss {float(loss):.6f}")
+            if save_dir is not None and (epoch + 1) % save_freq == 0:
+                self.save(f"{save_dir}/epoch{epoch}")
+            if valid_data is not None and (epoch + 1) % valid_freq == 0:
+                ev = self.evaluate(valid_data, valid_sample_split, batch_size, valid_steps,
+                                   collate_fn=collate_fn, verbose=0)
+                for kk, v in ev.items():
+                    history.setdefault('eval_' + kk, []).append(v)
+                self._model.train()
+        self.history = history
+        return history
+
+    @torch.no_grad()
+    def evaluate(self, valid_data, valid_sample_split=None, batch_size=1, steps=None, log_freq=10,
+                 collate_fn=None, callbacks=None, verbose=2):
+        self._model.eval()
+        loader = self._loader(valid_data, batch_size, False, collate_fn)
+        for m in self._metrics:
+            m.reset()
+        losses, logs = [], {}
+        for step, batch in enumerate(loader):
+            if steps is not None and step >= steps:
+                break
+            inputs, labels = self._split(batch, valid_sample_split)
+            outs = self._forward(inputs)
+            if self._loss is not None:
+                losses.append(float(self._compute_loss(outs, labels)))
+            if self._metrics:
+                logs = self._update_metrics(outs, labels)
+        res = dict(logs)
+        if losses:
+            res['loss'] = float(np.mean(losses))
+        return res
+
+    @torch.no_grad()
+    def predict(self, test_data, test_sample_split=None, batch_size=1, steps=None, collate_fn=None,
+                callbacks=None, verbose=2):
+        self._model.eval()
+        loader = self._loader(test_data, batch_size, False, collate_fn)
+        outputs = []
+        for step, batch in enumerate(loader):
+            if steps is not None and step >= steps:
+                break
+            inputs, _ = self._split(batch, test_sample_split if test_sample_split is not None
+                                    else len(_to_list(batch)))
+            outs = self._forward(inputs)
+            outputs.append([o.numpy() for o in _to_list(outs)])
+        return outputs
+
+    def save(self, path, training=True):
+        from ...framework.io import save
+        save(self._model.state_dict(), path + '.pdparams')
+        if training and self._optimizer is not None:
+            save(self._optimizer.state_dict(), path + '.pdopt')
+
+    def load(self, path, strict=True, load_optimizer=True):
+        import os
+        from ...framework.io import load
+        self._model.set_state_dict(load(path + '.pdparams'))
+        if load_optimizer and self._optimizer is not None and os.path.exists(path + '.pdopt'):
+            self._optimizer.set_state_dict(load(path + '.pdopt'))
+
+    @property
+    def main_program(self):
+        return None
+
+    @property
+    def mode(self):
+        return 'train' if self._model.training else 'eval'
