@@ -89,7 +89,10 @@ __global__ __launch_bounds__(CF::NT) void gemm_bias_act_kernel(const uint16_t* _
   const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;
   const int nb = gridDim.x;
   int pid = blockIdx.x;
-  if ((nb & 7) == 0) pid = (pid & 7) * (nb >> 3) + (pid >> 3);  // contiguous tile run per XCD
+  {  // contiguous tile run per XCD; bijective for any grid (the first r XCDs take q+1 tiles)
+    const int q = nb >> 3, r = nb & 7, xcd = pid & 7;
+    pid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (pid >> 3);
+  }
   const int group = 8 * tiles_n, g = pid / group, first_m = g * 8;
   const int gm = min(tiles_m - first_m, 8);
   const int tm = first_m + (pid % group) % gm, tn = (pid % group) / gm;
@@ -219,8 +222,9 @@ void launch_cfg(const uint16_t* pa, const uint16_t* pb, const uint16_t* pbias, u
   }
 }
 
-// Large tiles (1 workgroup/CU) once there are >= 3 rounds of them over the 256 CUs; small otherwise
-// (M=16384,N=2048: 512 large tiles 222 us vs 2048 small tiles 201 us).
+// Large tiles (1 workgroup/CU) once there are >= 3 rounds of them over the 256 CUs, or 2 rounds
+// with a long K loop; small otherwise. Measured at M=16384, N=2048 (512 large tiles):
+// K=2048 large 222 us vs small 201 us; K=8192 large 634 us vs small 672 us.
 template <typename T>
 void launch(const void* A, const void* B, const void* bias, void* C, void* Z, int M, int N, int K, int lda, int ldb,
             int ldc, int a, hipStream_t s) {
@@ -230,7 +234,7 @@ void launch(const void* A, const void* B, const void* bias, void* C, void* Z, in
   auto* pc = static_cast<uint16_t*>(C);
   auto* pz = static_cast<uint16_t*>(Z);
   const int64_t big = (int64_t)((M + 255) / 256) * ((N + 255) / 256);
-  if (big >= 768) launch_cfg<T, Large>(pa, pb, pbias, pc, pz, M, N, K, lda, ldb, ldc, a, s);
+  if (big >= 768 || (big >= 512 && K >= 4096)) launch_cfg<T, Large>(pa, pb, pbias, pc, pz, M, N, K, lda, ldb, ldc, a, s);
   else launch_cfg<T, Small>(pa, pb, pbias, pc, pz, M, N, K, lda, ldb, ldc, a, s);
 }
 
