@@ -18,7 +18,8 @@ def _ref(x, w, b, act):
 
 @pytest.mark.parametrize('dtype', [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize('shape', [(256, 512, 384), (77, 200, 136), (1, 8, 8), (1000, 1024, 2048),
-                                   (130, 72, 4104), (12296, 4104, 136)])
+                                   (130, 72, 4104), (12296, 4104, 136),
+                                   (8192, 4096, 4096)])
 @pytest.mark.parametrize('act', [None, 'gelu', 'gelu_tanh', 'relu'])
 def test_gemm_bias_act_fwd(dtype, shape, act):
     _native.require()
