@@ -39,14 +39,47 @@ def parse():
     return p.parse_args()
 
 
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(('127.0.0.1', 0))
+        return s.getsockname()[1]
+
+
+def _spawn_ranks(n):
+    """``--gpus N`` without a launcher: start N fresh rank processes (one per GPU) and
+    exit with the worst child status. Runs before this process imports torch or touches
+    the GPU, so every rank initialises HIP in a clean process (no fork after HIP init,
+    no exec from a GPU process)."""
+    import subprocess
+    port = str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR='127.0.0.1', MASTER_PORT=port,
+                   HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get('HSA_ENABLE_IPC_MODE_LEGACY', '0'))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env))
+    rc = 0
+    for p in procs:
+        c = p.wait()
+        rc = rc or c
+    return rc
+
+
 def main():
     a = parse()
+    if a.gpus > 1 and 'WORLD_SIZE' not in os.environ:
+        sys.exit(_spawn_ranks(a.gpus))
     import torch
     import torch.distributed as dist
     import paddle_ray_amd as paddle
     from paddle_ray_amd.distributed import collective as C
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
+    if world != a.gpus:
+        raise SystemExit(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world}; launch one rank per GPU "
+                         f"(torchrun --nproc-per-node {a.gpus}) or drop WORLD_SIZE to self-spawn")
     if world > 1:
         C.init_parallel_env()
     rank = C.get_rank()
@@ -63,6 +96,8 @@ def main():
         result = bench_gpt(a, paddle, torch, dist, C, world, rank, dev)
     else:
         result = bench_resnet(a, paddle, torch, dist, C, world, rank, dev)
+    result['backend'] = dist.get_backend() if world > 1 else 'none'
+    result['world_size'] = world
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
