@@ -185,31 +185,86 @@ class Fleet:
         return self._hcg
 
     # -- wrapping ----------------------------------------------------------------------------
+    def _sharding_level(self):
+        st = self._strategy
+        stage = int(st.sharding_configs.get('stage', 1)) if st.sharding_configs else 1
+        return {1: 'os', 2: 'os_g', 3: 'p_g_os'}[stage]
+
     def distributed_model(self, model):
+        """Wrap ``model`` for the active hybrid mode (parity: fleet/model.py:30-140).
+
+        * sharding_degree > 1 (alone, with dp, or with mp): ``ShardedModel`` over the sharding
+          group (stage from ``sharding_configs['stage']``, default 1 as in the reference's
+          DygraphShardingOptimizer), gradients additionally averaged over the dp group;
+        * ``strategy.recompute``: every repeated block (LayerList / Sequential member, or the
+          sublayers named in ``recompute_configs['checkpoints']``) runs under recompute;
+        * ``strategy.amp``: forward under ``auto_cast`` (O2 decorate with use_pure_fp16)."""
         hcg, st = self._hcg, self._strategy
         if hcg is None:
             self.init(is_collective=True)
             hcg, st = self._hcg, self._strategy
+        self._sharded_state = None
+        if st.amp:
+            model = _apply_amp(model, st)
+        if st.recompute:
+            _apply_recompute(model, st.recompute_configs.get('checkpoints') or [])
         mode = hcg.get_parallel_mode()
+        sh = hcg.get_sharding_parallel_world_size()
         if mode == ParallelMode.PIPELINE_PARALLEL:
-            return _pp.PipelineParallel(model, hcg, st)
+            if sh > 1:
+                raise NotImplementedError("pipeline x sharding: use sharding_degree=1 with pp>1")
+            return _wrap_amp(_pp.PipelineParallel(model, hcg, st), st)
+        if sh > 1:
+            from ...parallel.sharding import ShardedState, ShardedModel
+            if hcg.get_model_parallel_world_size() > 1:
+                _broadcast_mp_replicated(model, hcg)
+            dpg = hcg.get_data_parallel_group()
+            state = ShardedState(model, self._sharding_level(), hcg.get_sharding_parallel_group(),
+                                 dp_group=dpg if dpg.nranks > 1 else None,
+                                 segment_bytes=int(st.fuse_grad_size_in_MB) << 20)
+            self._sharded_state = state
+            return _wrap_amp(ShardedModel(model, state), st)
         if mode == ParallelMode.TENSOR_PARALLEL:
-            return TensorParallel(model, hcg, st)
-        if mode == ParallelMode.SHARDING_PARALLEL:
-            return model  # sharding wrapper is applied together with the optimizer
+            return _wrap_amp(TensorParallel(model, hcg, st), st)
         from ...parallel.data_parallel import DataParallel
         if C.get_world_size() > 1:
-            return DataParallel(model, comm_buffer_size=st.fuse_grad_size_in_MB,
-                                find_unused_parameters=st.find_unused_parameters,
-                                group=hcg.get_data_parallel_group())
-        return model
+            return _wrap_amp(DataParallel(model, comm_buffer_size=st.fuse_grad_size_in_MB,
+                                          find_unused_parameters=st.find_unused_parameters,
+                                          group=hcg.get_data_parallel_group()), st)
+        return _wrap_amp(model, st)
 
     def distributed_optimizer(self, optimizer, strategy=None):
+        """HybridParallelOptimizer / sharding optimizer (parity:
+        hybrid_parallel_optimizer.py:243-313); ``strategy.gradient_merge`` wraps the result."""
         if strategy is not None:
             self._strategy = strategy
         if self._hcg is None:
             return optimizer
-        return HybridParallelOptimizer(optimizer, self._hcg, self._strategy)
+        hcg, st = self._hcg, self._strategy
+        state = getattr(self, '_sharded_state', None)
+        if state is not None:
+            from ...parallel.sharding import ShardedOptimizer
+            ppg = hcg.get_pipe_parallel_group()
+            opt = ShardedOptimizer(optimizer, state, mp_group=hcg.get_model_parallel_group(),
+                                   norm_groups=[ppg])
+        else:
+            opt = HybridParallelOptimizer(optimizer, hcg, st)
+        if st.gradient_merge and int(st.gradient_merge_configs.get('k_steps', 1)) > 1:
+            opt = GradientMergeOptimizer(opt, int(st.gradient_merge_configs['k_steps']),
+                                         bool(st.gradient_merge_configs.get('avg', True)))
+        return opt
+
+    def distributed_scaler(self, scaler):
+        """HybridParallelGradScaler: found_inf is MAX-reduced over every hybrid group."""
+        hcg = self._hcg
+        if hcg is None:
+            return scaler
+        from ...amp import _uniq
+        pgs = [g.process_group for g in (hcg.get_data_parallel_group(), hcg.get_model_parallel_group(),
+                                         hcg.get_pipe_parallel_group(),
+                                         hcg.get_sharding_parallel_group()) if g.nranks > 1]
+        scaler._extra_pgs = _uniq(list(scaler._extra_pgs) + pgs)
+        return scaler
 
     # -- checkpoints ---------------------------------------------------------------------------
     def save_persistables(self, executor, dirname, main_program=None, mode=0):
@@ -220,25 +275,132 @@ class Fleet:
         return {}
 
 
-class TensorParallel(torch.nn.Module if False else object):
-    pass
-
-
 from ...nn.layer.layers import Layer  # noqa: E402
 
 
-class TensorParallel(Layer):  # noqa: F811
+def _broadcast_mp_replicated(layers, hcg):
+    mpg = hcg.get_model_parallel_group()
+    if mpg.nranks > 1:
+        for p in layers.parameters():
+            if not getattr(p, 'is_distributed', False):
+                dist.broadcast(p._t.data, mpg.ranks[0], group=mpg.process_group)
+
+
+def _apply_recompute(model, checkpoints):
+    """strategy.recompute for dygraph: run the chosen blocks under activation recompute."""
+    from ...parallel.sharding import _find_units
+    if checkpoints:
+        named = dict(model.named_sublayers())
+        blocks = [named[n] for n in checkpoints if n in named]
+    else:
+        blocks = _find_units(model)
+    for blk in blocks:
+        if getattr(blk, '_pra_recompute', False):
+            continue
+        fwd = blk.forward
+
+        def run(*a, _f=fwd, **k):
+            if not blk.training or not torch.is_grad_enabled():
+                return _f(*a, **k)
+            return _recompute(_f, *a, **k)
+        blk.__dict__['forward'] = run
+        blk.__dict__['_pra_recompute'] = True
+
+
+def _apply_amp(model, st):
+    cfg = st.amp_configs
+    if cfg.get('use_pure_fp16') or cfg.get('use_fp16_guard') is False and cfg.get('level') == 'O2':
+        from ... import amp
+        amp.decorate(model, level='O2', dtype='bfloat16' if cfg.get('use_bf16') else 'float16')
+    return model
+
+
+class _AmpForward(Layer):
+    def __init__(self, inner, st):
+        super().__init__()
+        self._layers = inner
+        cfg = st.amp_configs
+        self.__dict__['_amp_kw'] = dict(
+            level='O2' if cfg.get('use_pure_fp16') else 'O1',
+            dtype='bfloat16' if cfg.get('use_bf16') else 'float16',
+            custom_white_list=cfg.get('custom_white_list'),
+            custom_black_list=cfg.get('custom_black_list'))
+
+    def forward(self, *a, **k):
+        from ... import amp
+        with amp.auto_cast(True, **self._amp_kw):
+            return self._layers(*a, **k)
+
+    def __getattr__(self, name):
+        try:
+            return super().__getattr__(name)
+        except AttributeError:
+            return getattr(self.__dict__['_sub_layers']['_layers'], name)
+
+    def state_dict(self, *a, **k):
+        return self._layers.state_dict(*a, **k)
+
+    def set_state_dict(self, *a, **k):
+        return self._layers.set_state_dict(*a, **k)
+
+    def parameters(self, include_sublayers=True):
+        return self._layers.parameters(include_sublayers)
+
+
+def _wrap_amp(model, st):
+    return _AmpForward(model, st) if st.amp else model
+
+
+class GradientMergeOptimizer:
+    """strategy.gradient_merge (parity: meta_optimizers/gradient_merge_optimizer.py): gradients
+    accumulate over ``k_steps`` backward passes; the inner step runs on every k-th call
+    (grads averaged when ``avg``) and only then are grads cleared."""
+
+    def __init__(self, inner, k_steps, avg=True):
+        self._inner_opt = inner
+        self.k_steps = k_steps
+        self.avg = avg
+        self._calls = 0
+
+    def _grads(self):
+        g = getattr(self._inner_opt, '_scaler_grads', None)
+        if g is not None:
+            return g()
+        return [p._t.grad for p in self._inner_opt._parameter_list if p._t.grad is not None]
+
+    def step(self):
+        self._calls += 1
+        if self._calls % self.k_steps:
+            return
+        if self.avg:
+            with torch.no_grad():
+                for g in self._grads():
+                    g.div_(self.k_steps)
+        self._inner_opt.step()
+        self._merged_ready = True
+
+    def clear_grad(self, set_to_zero=True):
+        if self._calls % self.k_steps == 0:
+            self._inner_opt.clear_grad(set_to_zero)
+
+    clear_gradients = clear_grad
+
+    def minimize(self, loss, *a, **k):
+        loss.backward()
+        self.step()
+
+    def __getattr__(self, k):
+        return getattr(self._inner_opt, k)
+
+
+class TensorParallel(Layer):
     """Broadcast non-distributed params inside the mp group; DP all-reduce over dp group."""
 
     def __init__(self, layers, hcg, strategy=None):
         super().__init__()
         self._layers = layers
         self._hcg = hcg
-        mpg = hcg.get_model_parallel_group()
-        if mpg.nranks > 1:
-            for p in layers.parameters():
-                if not getattr(p, 'is_distributed', False):
-                    dist.broadcast(p._t.data, mpg.ranks[0], group=mpg.process_group)
+        _broadcast_mp_replicated(layers, hcg)
         dpg = hcg.get_data_parallel_group()
         self._dp = None
         if dpg.nranks > 1:
@@ -309,6 +471,7 @@ init = fleet.init
 distributed_model = fleet.distributed_model
 distributed_optimizer = fleet.distributed_optimizer
 get_hybrid_communicate_group = fleet.get_hybrid_communicate_group
+distributed_scaler = fleet.distributed_scaler
 is_first_worker = fleet.is_first_worker
 worker_index = fleet.worker_index
 worker_num = fleet.worker_num

@@ -160,3 +160,31 @@ class Heartbeat:
         stale_s = stale_s if stale_s is not None else 3 * self.interval
         now = time.time()
         return [r for r, t in self.last_seen().items() if t is None or now - t > stale_s]
+
+
+class TrackedWork:
+    """An async RCCL work registered with the watchdog until ``wait()`` returns — used by the
+    hot-path reducers (DataParallel buckets, sharding reduce-scatter / all-gather, pipeline
+    p2p) that call ``torch.distributed`` directly."""
+
+    __slots__ = ('work', 'tid')
+
+    def __init__(self, name, work, nranks=None):
+        self.work = work
+        self.tid = get_watchdog().track(name, work, nranks) if (work is not None and enabled()) \
+            else None
+
+    def wait(self):
+        if self.work is not None:
+            self.work.wait()
+        if self.tid is not None:
+            get_watchdog().done(self.tid)
+            self.tid = None
+        return True
+
+    def is_completed(self):
+        return self.work is None or self.work.is_completed()
+
+
+def track(name, work, nranks=None):
+    return TrackedWork(name, work, nranks)

@@ -185,8 +185,12 @@ class GPTBlock(nn.Layer):
             return torch.nn.functional.dropout(t, self.p, True)
         return t
 
-    def forward(self, x):
-        """Unfused reference path: x -> x + attn(ln1 x) -> + mlp(ln2 .)"""
+    def forward(self, x, y=None, next_ln=None):
+        """Unfused reference path: x -> x + attn(ln1 x) -> + mlp(ln2 .). With ``y`` given this
+        is the fused path ``forward_fused(x, y, next_ln)``; both are reached through
+        ``__call__`` so forward hooks (ZeRO-3 gather/release, recompute) see every block."""
+        if y is not None:
+            return self.forward_fused(_u(x), _u(y), next_ln)
         t = _u(x)
         t = t + self._drop(_u(self.attn(self.ln1(Tensor(t)))))
         t = t + self._drop(_u(self.mlp(self.ln2(Tensor(t)))))
@@ -223,11 +227,10 @@ class GPTModel(nn.Layer):
                 if self.cfg.recompute and self.training:
                     from ..parallel.recompute import recompute
                     r, y = recompute(lambda a, b, blk=blk, nxt=nxt: tuple(
-                        Tensor(t) for t in blk.forward_fused(_u(a), _u(b), nxt)),
-                        Tensor(r), Tensor(y))
+                        Tensor(t) for t in blk(a, b, nxt)), Tensor(r), Tensor(y))
                     r, y = _u(r), _u(y)
                 else:
-                    r, y = blk.forward_fused(r, y, nxt)
+                    r, y = blk(r, y, nxt)
             return Tensor(y)
         if self.cfg.recompute and self.training:
             from ..parallel.recompute import recompute

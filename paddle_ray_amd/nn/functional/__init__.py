@@ -14,6 +14,7 @@ import torch.nn.functional as TF
 
 from ...framework.core import Tensor, _u, convert_dtype
 from ...ops import fused as K
+from ...amp import amp_op as _amp_op
 
 
 def _t(x):
@@ -31,6 +32,7 @@ def _opt(x):
 # =============================================================================
 # activations
 # =============================================================================
+@_amp_op('relu')
 def relu(x, name=None):
     return _w(torch.relu(_t(x)))
 
@@ -67,6 +69,7 @@ def selu(x, scale=1.0507009873554804934193349852946, alpha=1.6732632423543772848
     return _w(scale * torch.where(t > 0, t, alpha * (torch.exp(t) - 1)))
 
 
+@_amp_op('gelu')
 def gelu(x, approximate=False, name=None):
     t = _t(x)
     if t.is_cuda:
@@ -90,6 +93,7 @@ def mish(x, name=None):
     return _w(TF.mish(_t(x)))
 
 
+@_amp_op('sigmoid')
 def sigmoid(x, name=None):
     return _w(torch.sigmoid(_t(x)))
 
@@ -167,6 +171,7 @@ def glu(x, axis=-1, name=None):
     return _w(TF.glu(_t(x), axis))
 
 
+@_amp_op('softmax')
 def softmax(x, axis=-1, dtype=None, name=None):
     t = _t(x)
     if dtype is not None:
@@ -182,6 +187,7 @@ def softmax_(x, axis=-1, dtype=None, name=None):
     return x
 
 
+@_amp_op('log_softmax')
 def log_softmax(x, axis=-1, dtype=None, name=None):
     t = _t(x)
     if dtype is not None:
@@ -196,6 +202,7 @@ def gumbel_softmax(x, temperature=1.0, hard=False, axis=-1, name=None):
 # =============================================================================
 # common
 # =============================================================================
+@_amp_op('linear')
 def linear(x, weight, bias=None, name=None):
     """y = x @ W + b with paddle's [in, out] weight layout (hipBLASLt GEMM)."""
     t, w = _t(x), _t(weight)
@@ -470,16 +477,19 @@ def _conv(fn, n, x, weight, bias, stride, padding, dilation, groups, data_format
     return _w(out)
 
 
+@_amp_op('conv1d')
 def conv1d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, data_format='NCL',
            name=None):
     return _conv(TF.conv1d, 1, x, weight, bias, stride, padding, dilation, groups, data_format)
 
 
+@_amp_op('conv2d')
 def conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, data_format='NCHW',
            name=None):
     return _conv(TF.conv2d, 2, x, weight, bias, stride, padding, dilation, groups, data_format)
 
 
+@_amp_op('conv3d')
 def conv3d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, data_format='NCDHW',
            name=None):
     return _conv(TF.conv3d, 3, x, weight, bias, stride, padding, dilation, groups, data_format)
@@ -663,6 +673,7 @@ def max_unpool3d(x, indices, kernel_size, stride=None, padding=0, data_format='N
 # =============================================================================
 # norms
 # =============================================================================
+@_amp_op('layer_norm')
 def layer_norm(x, normalized_shape, weight=None, bias=None, epsilon=1e-05, name=None):
     t = _t(x)
     if isinstance(normalized_shape, int):
@@ -684,6 +695,7 @@ def rms_norm(x, weight=None, epsilon=1e-6, name=None):
     return _w(K.rms_norm(_t(x), _opt(weight), epsilon))
 
 
+@_amp_op('batch_norm')
 def batch_norm(x, running_mean, running_var, weight, bias, training=False, momentum=0.9,
                epsilon=1e-05, data_format='NCHW', use_global_stats=None, name=None):
     t = _t(x)
@@ -757,6 +769,7 @@ def _reduce(loss, reduction):
     return loss
 
 
+@_amp_op('cross_entropy')
 def cross_entropy(input, label, weight=None, ignore_index=-100, reduction='mean', soft_label=False,
                   axis=-1, use_softmax=True, label_smoothing=0.0, name=None):
     """Paddle cross_entropy. Hard labels on the HIP device use the fused
@@ -796,6 +809,7 @@ def cross_entropy(input, label, weight=None, ignore_index=-100, reduction='mean'
     return _w(loss)
 
 
+@_amp_op('softmax_with_cross_entropy')
 def softmax_with_cross_entropy(logits, label, soft_label=False, ignore_index=-100,
                                numeric_stable_mode=True, return_softmax=False, axis=-1):
     x, lab = _t(logits), _t(label)
@@ -820,6 +834,7 @@ def nll_loss(input, label, weight=None, ignore_index=-100, reduction='mean', nam
                           reduction=reduction))
 
 
+@_amp_op('mse_loss')
 def mse_loss(input, label, reduction='mean', name=None):
     return _w(TF.mse_loss(_t(input), _t(label), reduction=reduction))
 

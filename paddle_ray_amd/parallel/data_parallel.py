@@ -20,6 +20,7 @@ import torch.distributed as dist
 from ..framework.core import Tensor
 from ..nn.layer.layers import Layer
 from .flat import FlatGroup, group_params_into_buckets
+from ..distributed import watchdog as _watchdog
 
 
 def _avg_supported(pg):
@@ -30,15 +31,26 @@ def _avg_supported(pg):
 
 
 class GradBucketReducer:
-    """Shared by DataParallel (all-reduce) and sharding stage 1 (all-reduce) / 2,3 (reduce-scatter)."""
+    """Shared by DataParallel (all-reduce) and sharding stage 1 (all-reduce) / 2,3 (reduce-scatter).
 
-    def __init__(self, groups, pg, world, mode='allreduce', shard_grads=None):
+    ``dp_pg``: in hybrid dp x sharding, the owned (already sharding-reduced) gradient shard
+    is then averaged over the data-parallel group. ``on_launch(gi)`` / ``on_finalize()`` let
+    ZeRO-3 free a bucket's gathered parameters as soon as its gradients are complete.
+    Every RCCL work is registered with the collective watchdog until it is waited on.
+    """
+
+    def __init__(self, groups, pg, world, mode='allreduce', shard_grads=None, dp_pg=None,
+                 dp_world=1, on_launch=None, on_finalize=None, name='dp_bucket'):
         self.groups = groups
         self.pg = pg
         self.world = world
         self.mode = mode
         self.shard_grads = shard_grads  # for reduce_scatter: per-group output buffers
         self.avg = _avg_supported(pg)
+        self.dp_pg, self.dp_world = dp_pg, dp_world
+        self.dp_avg = _avg_supported(dp_pg) if dp_pg is not None else False
+        self.on_launch, self.on_finalize = on_launch, on_finalize
+        self.name = name
         self.counts = [0] * len(groups)
         self.launched = [False] * len(groups)
         self.works = []
@@ -46,11 +58,10 @@ class GradBucketReducer:
         self._cb_queued = False
         self._hooks = []
         for gi, g in enumerate(groups):
-            for p in g.params:
-                if p._t.requires_grad:
-                    self._hooks.append(p._t.register_post_accumulate_grad_hook(
-                        self._make_hook(gi)))
-        self.n_req = [sum(1 for p in g.params if p._t.requires_grad) for g in groups]
+            for t in g.leaves:
+                if t.requires_grad:
+                    self._hooks.append(t.register_post_accumulate_grad_hook(self._make_hook(gi)))
+        self.n_req = [sum(1 for t in g.leaves if t.requires_grad) for g in groups]
 
     def _make_hook(self, gi):
         def hook(t):
@@ -58,25 +69,32 @@ class GradBucketReducer:
                 return
             if not self._cb_queued:
                 self._cb_queued = True
-                torch.autograd.Variable._execution_engine.queue_callback(self.finalize)
+                from .recompute import queue_outer_callback
+                queue_outer_callback(self.finalize)
             self.counts[gi] += 1
             if self.counts[gi] == self.n_req[gi]:
                 self._launch(gi)
         return hook
 
     def _launch(self, gi):
-        if self.launched[gi] or self.world == 1:
-            self.launched[gi] = True
+        if self.launched[gi]:
             return
-        g = self.groups[gi]
-        op = dist.ReduceOp.AVG if self.avg else dist.ReduceOp.SUM
-        if self.mode == 'allreduce':
-            w = dist.all_reduce(g.grad_buf, op=op, group=self.pg, async_op=True)
-        else:
-            w = dist.reduce_scatter_tensor(self.shard_grads[gi], g.grad_buf, op=op, group=self.pg,
-                                           async_op=True)
-        self.works.append((gi, w))
         self.launched[gi] = True
+        if self.world > 1:
+            g = self.groups[gi]
+            op = dist.ReduceOp.AVG if self.avg else dist.ReduceOp.SUM
+            if self.mode == 'allreduce':
+                w = dist.all_reduce(g.grad_buf, op=op, group=self.pg, async_op=True)
+            else:
+                w = dist.reduce_scatter_tensor(self.shard_grads[gi], g.grad_buf, op=op,
+                                               group=self.pg, async_op=True)
+            self.works.append((gi, _watchdog.track(f'{self.name}.{self.mode}[{gi}]', w,
+                                                   self.world)))
+        if self.on_launch is not None:
+            self.on_launch(gi)
+
+    def _shard_out(self, gi):
+        return self.groups[gi].grad_buf if self.mode == 'allreduce' else self.shard_grads[gi]
 
     def finalize(self):
         for gi in range(len(self.groups)):
@@ -85,16 +103,29 @@ class GradBucketReducer:
         for gi, w in self.works:
             w.wait()
             if not self.avg and self.world > 1:
-                (self.groups[gi].grad_buf if self.mode == 'allreduce'
-                 else self.shard_grads[gi]).div_(self.world)
+                self._shard_out(gi).div_(self.world)
         if self.world == 1 and self.mode != 'allreduce':
             for gi, g in enumerate(self.groups):
                 if self.shard_grads[gi].data_ptr() != g.grad_buf.data_ptr():
-                    self.shard_grads[gi].copy_(g.grad_buf)
+                    self.shard_grads[gi].copy_(g.shard(g.grad_buf))
+        if self.dp_pg is not None and self.dp_world > 1:
+            # hybrid dp x sharding: average the owned shard over the replicas
+            op = dist.ReduceOp.AVG if self.dp_avg else dist.ReduceOp.SUM
+            dws = []
+            for gi, g in enumerate(self.groups):
+                out = self.shard_grads[gi] if self.shard_grads is not None else g.grad_buf
+                dws.append((out, _watchdog.track(f'{self.name}.dp_allreduce[{gi}]', dist.all_reduce(
+                    out, op=op, group=self.dp_pg, async_op=True), self.dp_world)))
+            for out, w in dws:
+                w.wait()
+                if not self.dp_avg:
+                    out.div_(self.dp_world)
         self.works.clear()
         self.counts = [0] * len(self.groups)
         self.launched = [False] * len(self.groups)
         self._cb_queued = False
+        if self.on_finalize is not None:
+            self.on_finalize()
 
     def remove(self):
         for h in self._hooks:
@@ -126,7 +157,7 @@ class DataParallel(Layer):
 
     def forward(self, *inputs, **kwargs):
         for g in self._groups:
-            if any(p._t.grad is None for p in g.params if p._t.requires_grad):
+            if g.grads_missing():
                 g.grad_buf.zero_()
                 g.reattach_grads()
         return self._layers(*inputs, **kwargs)

@@ -33,10 +33,12 @@ class FlatGroup:
         assert all(p._t.dtype == self.dtype for p in self.params), "FlatGroup needs one dtype"
         self.world, self.rank = world, rank
         self.offsets = []
+        self.shapes = [tuple(p._t.shape) for p in self.params]
+        self.numels = [p._t.numel() for p in self.params]
         off = 0
-        for p in self.params:
+        for n in self.numels:
             self.offsets.append(off)
-            off += _round_up(p._t.numel(), align)
+            off += _round_up(n, align)
         self.numel = _round_up(max(off, 1), align * world)
         self.shard_numel = self.numel // world
         self.param_buf = torch.zeros(self.numel, dtype=self.dtype, device=self.device)
@@ -46,28 +48,82 @@ class FlatGroup:
             for p, o in zip(self.params, self.offsets):
                 n = p._t.numel()
                 self.param_buf[o:o + n].copy_(p._t.detach().reshape(-1))
+        self._shard_store = None
+        self.params_released = False
+        self.grads_released = False
+        self.leaves = []
         self.attach()
 
     # -- views -------------------------------------------------------------------------
     def attach(self):
-        """(Re)point every param to its slice of the flat buffers."""
-        for p, o in zip(self.params, self.offsets):
-            shape = p._t.shape
-            n = p._t.numel()
+        """(Re)point every param to its slice of the flat buffers.
+
+        Each leaf is built with ``set_`` on the flat storage instead of as a view, so it has
+        its own autograd version counter: collectives writing into ``param_buf`` (the ZeRO-3
+        re-gather in the middle of backward) do not invalidate tensors saved for backward."""
+        self.leaves = []
+        st = self.param_buf.untyped_storage()
+        for p, o, shape, n in zip(self.params, self.offsets, self.shapes, self.numels):
             rg = not p.stop_gradient
-            v = self.param_buf[o:o + n].view(shape)
-            leaf = v.detach()
+            leaf = torch.empty(0, dtype=self.dtype, device=self.device)
+            leaf.set_(st, o, shape, torch.empty(shape, device='meta').stride())
             if rg:
                 leaf.requires_grad_(True)
                 leaf.grad = self.grad_buf[o:o + n].view(shape)
             object.__setattr__(p, '_t', leaf)
+            self.leaves.append(leaf)
 
     def reattach_grads(self):
-        for p, o in zip(self.params, self.offsets):
-            t = p._t
+        if self.grads_released:
+            return
+        for t, o in zip(self.leaves, self.offsets):
             if t.requires_grad and (t.grad is None or t.grad.data_ptr() != self.grad_buf[o:].data_ptr()):
                 n = t.numel()
                 t.grad = self.grad_buf[o:o + n].view(t.shape)
+
+    def grads_missing(self):
+        return any(t.grad is None for t in self.leaves if t.requires_grad)
+
+    # -- ZeRO-3 residency (parity: group_sharded_stage3.py _release_param / _allgather_buffer) --
+    def own_shard(self):
+        """Move the owned parameter shard into its own storage so the full buffer can be freed."""
+        if self._shard_store is None:
+            self._shard_store = self.shard(self.param_buf).clone()
+
+    def release_params(self):
+        """Free the gathered full buffer. Parameters point at an empty placeholder (a use while
+        released fails with a shape error on the host, never a device fault); tensors autograd
+        saved keep the storage object and see the data again after ``materialize_params``."""
+        if self.params_released:
+            return
+        assert self._shard_store is not None, "release_params needs own_shard() first"
+        for p in self.params:
+            object.__setattr__(p, '_t', torch.empty(0, dtype=self.dtype, device=self.device))
+        self.param_buf.untyped_storage().resize_(0)
+        self.params_released = True
+
+    def materialize_params(self):
+        """Re-allocate the full buffer (contents undefined until gathered); re-point params."""
+        if not self.params_released:
+            return
+        self.param_buf.untyped_storage().resize_(self.numel * self.param_buf.element_size())
+        for p, leaf in zip(self.params, self.leaves):
+            object.__setattr__(p, '_t', leaf)
+        self.params_released = False
+
+    def release_grads(self):
+        if not self.grads_released:
+            self.grad_buf.untyped_storage().resize_(0)
+            self.grads_released = True
+
+    def materialize_grads(self):
+        if self.grads_released:
+            self.grad_buf.untyped_storage().resize_(self.numel * self.grad_buf.element_size())
+            self.grad_buf.zero_()
+            self.grads_released = False
+
+    def resident_bytes(self):
+        return self.param_buf.untyped_storage().nbytes() + self.grad_buf.untyped_storage().nbytes()
 
     # -- shards ------------------------------------------------------------------------
     def shard(self, buf, rank=None):
@@ -76,6 +132,8 @@ class FlatGroup:
 
     @property
     def param_shard(self):
+        if self._shard_store is not None:
+            return self._shard_store
         return self.shard(self.param_buf)
 
     def params_in_shard(self, rank=None):
@@ -83,8 +141,7 @@ class FlatGroup:
         r = self.rank if rank is None else rank
         lo, hi = r * self.shard_numel, (r + 1) * self.shard_numel
         out = []
-        for p, o in zip(self.params, self.offsets):
-            n = p._t.numel()
+        for p, o, n in zip(self.params, self.offsets, self.numels):
             a, b = max(o, lo), min(o + n, hi)
             if a < b:
                 out.append((p, a - lo, b - lo, a - o))

@@ -10,6 +10,21 @@ from ..framework.core import Tensor, _u
 from .tensor_parallel import get_rng_state_tracker
 
 
+_DEPTH = [0]
+_DEFERRED = []
+
+
+def queue_outer_callback(cb):
+    """Queue ``cb`` to run when the OUTERMOST backward finishes. Inside a recompute backward
+    (a nested, reentrant ``torch.autograd.backward``) the engine's callback queue belongs to
+    the nested graph task, which ends after one block — the gradient reducers' end-of-backward
+    hooks must wait for the outer one."""
+    if _DEPTH[0] > 0:
+        _DEFERRED.append(cb)
+    else:
+        torch.autograd.Variable._execution_engine.queue_callback(cb)
+
+
 def _wrap(x):
     if isinstance(x, torch.Tensor):
         return Tensor(x)
@@ -82,7 +97,16 @@ class _RecomputeFn(torch.autograd.Function):
         pairs = [(o, g) for o, g in zip(outs, grads)
                  if isinstance(o, torch.Tensor) and o.requires_grad and g is not None]
         if pairs:
-            torch.autograd.backward([p[0] for p in pairs], [p[1] for p in pairs])
+            _DEPTH[0] += 1
+            try:
+                torch.autograd.backward([p[0] for p in pairs], [p[1] for p in pairs])
+            finally:
+                _DEPTH[0] -= 1
+            if _DEPTH[0] == 0 and _DEFERRED:
+                cbs = list(_DEFERRED)
+                _DEFERRED.clear()
+                for cb in cbs:  # now on the outer graph task
+                    torch.autograd.Variable._execution_engine.queue_callback(cb)
         in_grads = tuple(a.grad if isinstance(a, torch.Tensor) else None for a in args)
         return (None, None, None) + in_grads
 

@@ -32,14 +32,81 @@ from ..ops import fused as K
 from ..ops import _native
 from .data_parallel import GradBucketReducer, _avg_supported
 from .flat import FlatGroup, group_params_into_buckets
+from ..distributed import watchdog as _watchdog
 
 LEVELS = {'os': 1, 'os_g': 2, 'p_g_os': 3}
 
 
-class ShardedState:
-    """Flat buckets + owned-shard optimizer state for one model."""
+def _find_units(layer, exclude=()):
+    """ZeRO-3 units: the members of the outermost LayerList / Sequential containers (the
+    repeated blocks), in forward order. Parameters outside every unit (embeddings, heads,
+    final norms) belong to the root and stay gathered for the whole step (FSDP-root style)."""
+    from ..nn.layer.common import LayerList, Sequential
+    units = []
 
-    def __init__(self, layer, level, group=None, segment_bytes=128 << 20, grad_fp32=False):
+    def walk(m):
+        for child in m.children():
+            if isinstance(child, exclude):
+                continue
+            if isinstance(child, (LayerList, Sequential)):
+                units.extend(c for c in child.children() if not isinstance(c, exclude))
+            else:
+                walk(child)
+    if isinstance(layer, (LayerList, Sequential)):
+        units.extend(layer.children())
+    else:
+        walk(layer)
+    return units
+
+
+def _tensors_in(obj):
+    if isinstance(obj, torch.Tensor):
+        yield obj
+    elif isinstance(obj, Tensor):
+        yield obj._t
+    elif isinstance(obj, (list, tuple)):
+        for o in obj:
+            yield from _tensors_in(o)
+    elif isinstance(obj, dict):
+        for o in obj.values():
+            yield from _tensors_in(o)
+
+
+def _in_backward():
+    return torch._C._current_graph_task_id() != -1
+
+
+class _Unit:
+    __slots__ = ('index', 'layer', 'gids')
+
+    def __init__(self, index, layer, gids):
+        self.index, self.layer, self.gids = index, layer, gids
+
+
+class ShardedState:
+    """Flat buckets + owned-shard optimizer state for one model.
+
+    Stage 3 (``p_g_os``) with more than one rank is real ZeRO-3 (parity:
+    group_sharded_stage3.py ``_release_param`` :925, ``_allgather_buffer`` :985,
+    ``_register_forward_hooks`` / ``_register_backward_hooks``):
+      * every parameter of a unit (a repeated block) larger than ``segment_size`` elements
+        lives in a per-unit flat buffer of which a rank keeps ONLY its owned shard; the
+        full buffer exists only while the unit runs;
+      * forward: the unit's pre-hook waits for its all-gather and prefetches the next unit's
+        on the RCCL stream; its post-hook frees the gathered buffer again and hooks the
+        unit's outputs so that, in backward, the gradient arriving at them re-gathers the
+        unit (prefetching the previous one) before the unit's backward kernels run;
+      * backward: once the unit's gradients are accumulated the reduce-scatter is launched
+        and the gathered buffer is freed; after the reduce-scatter completes the full
+        gradient buffer is freed too — only owned shards stay resident between steps.
+    Small parameters (biases, norms, ``<= segment_size``) and parameters outside units
+    stay resident (gathered once per step after the optimizer update, like stage 2).
+    ``dp_group``: hybrid dp x sharding — shard gradients are then averaged over the replicas.
+    """
+
+    def __init__(self, layer, level, group=None, segment_bytes=128 << 20, grad_fp32=False,
+                 dp_group=None, segment_size=2 ** 20, exclude_layer=None,
+                 release_after_forward=True):
         from ..distributed import collective as C
         self.layer = layer
         self.stage = LEVELS[level] if isinstance(level, str) else int(level)
@@ -47,55 +114,199 @@ class ShardedState:
         self.pg = None if group is None else group.process_group
         self.world = C.get_world_size(group)
         self.rank = C.get_rank(group)
+        self.dp_group = dp_group
+        self.dp_pg = None if dp_group is None else dp_group.process_group
+        self.dp_world = 1 if dp_group is None else dp_group.nranks
         params = [p for p in layer.parameters() if not p.stop_gradient]
-        if self.world > 1:
-            src = group.ranks[0] if group is not None else 0
-            for t in [p._t for p in layer.parameters()] + [b._t for b in layer.buffers()]:
-                dist.broadcast(t.data, src, group=self.pg)
-        buckets = group_params_into_buckets(params, segment_bytes)
+        if self.world > 1 or self.dp_world > 1:
+            for grp, pg in ((group, self.pg), (dp_group, self.dp_pg)):
+                if grp is not None and grp.nranks == 1:
+                    continue
+                if grp is None and self.world == 1:
+                    continue
+                src = grp.ranks[0] if grp is not None else 0
+                for t in [p._t for p in layer.parameters()] + [b._t for b in layer.buffers()]:
+                    dist.broadcast(t.data, src, group=pg)
+        self.zero3 = self.stage == 3 and self.world > 1
+        self.units = []
+        unit_of = {}
+        if self.zero3:
+            excl = tuple(exclude_layer) if exclude_layer else ()
+            for u in _find_units(layer, excl):
+                for p in u.parameters():
+                    if not p.stop_gradient and p._t.numel() > segment_size:
+                        unit_of.setdefault(id(p), len(self.units))
+                self.units.append(u)
+        resident = [p for p in params if id(p) not in unit_of]
+        buckets = group_params_into_buckets(resident, segment_bytes)
+        unit_buckets = []
+        for ui in range(len(self.units)):
+            ps = [p for p in params if unit_of.get(id(p)) == ui]
+            # one bucket per unit (or a few when a unit exceeds the bucket size)
+            unit_buckets.append(group_params_into_buckets(ps, max(segment_bytes, 1), reverse=False)
+                                if ps else [])
         self.groups = [FlatGroup(b, self.world, self.rank) for b in buckets]
+        self.n_resident = len(self.groups)
+        self.unit_meta = []
+        for ui, ub in enumerate(unit_buckets):
+            gids = []
+            for b in ub:
+                g = FlatGroup(b, self.world, self.rank)
+                g.own_shard()
+                gids.append(len(self.groups))
+                self.groups.append(g)
+            self.unit_meta.append(_Unit(ui, self.units[ui], gids))
+        self.unit_meta = [u for u in self.unit_meta if u.gids]
+        for i, u in enumerate(self.unit_meta):
+            u.index = i
+        self.release_after_forward = release_after_forward
         self.shard_grads = [g.shard(g.grad_buf) if self.world == 1 else
                             torch.zeros(g.shard_numel, dtype=g.grad_dtype, device=g.device)
                             for g in self.groups]
-        mode = 'allreduce' if self.stage == 1 else 'reduce_scatter'
-        self.reducer = GradBucketReducer(self.groups, self.pg, self.world, mode,
-                                         self.shard_grads) if self.stage > 1 or self.world > 1 \
-            else None
         if self.stage == 1:
             # stage 1 reduces the full grad buffer; the owned slice of it is the shard grad
             self.shard_grads = [g.shard(g.grad_buf) for g in self.groups]
+        mode = 'allreduce' if self.stage == 1 else 'reduce_scatter'
+        self.reducer = GradBucketReducer(
+            self.groups, self.pg, self.world, mode, self.shard_grads, dp_pg=self.dp_pg,
+            dp_world=self.dp_world, on_launch=self._on_grads_launched if self.zero3 else None,
+            on_finalize=self._on_backward_done if self.zero3 else None,
+            name=f'sharding{self.stage}') \
+            if self.stage > 1 or self.world > 1 or self.dp_world > 1 else None
         self.gather_works = {}
         self.params_stale = False
         self._param_bucket = {}
         for gi, g in enumerate(self.groups):
             for p in g.params:
                 self._param_bucket[id(p)] = gi
-        self._pre_hooks = []
-        if self.stage == 3 and self.world > 1:
-            for sub in layer.sublayers(include_self=True):
-                mine = sorted({self._param_bucket[id(p)] for p in sub._parameters.values()
-                               if p is not None and id(p) in self._param_bucket})
-                if mine:
-                    self._pre_hooks.append(sub.register_forward_pre_hook(self._make_wait(mine)))
+        self._unit_gid = {}
+        for u in self.unit_meta:
+            for gi in u.gids:
+                self._unit_gid[gi] = u
+        self._hooks = []
+        self._rs_window = []
+        self.peak_resident_bytes = 0
+        self.on_params_loaded = []
+        if self.zero3:
+            for u in self.unit_meta:
+                self._hooks.append(u.layer.register_forward_pre_hook(self._make_pre(u)))
+                self._hooks.append(u.layer.register_forward_post_hook(self._make_post(u)))
+                for gi in u.gids:
+                    self.groups[gi].release_params()
+                    self.groups[gi].release_grads()
 
-    # -- params all-gather -------------------------------------------------------------
-    def _make_wait(self, gids):
-        def hook(layer, inputs):
-            for gi in gids:
+    # -- memory accounting ----------------------------------------------------------------
+    def resident_bytes(self):
+        return sum(g.resident_bytes() for g in self.groups)
+
+    def _note_peak(self):
+        b = self.resident_bytes()
+        if b > self.peak_resident_bytes:
+            self.peak_resident_bytes = b
+
+    def full_bytes(self):
+        return sum(g.numel * (g.param_buf.element_size() + g.grad_buf.element_size())
+                   for g in self.groups)
+
+    # -- ZeRO-3 unit residency -----------------------------------------------------------------
+    def _gather_group(self, gi):
+        g = self.groups[gi]
+        if not g.params_released or gi in self.gather_works:
+            return
+        g.materialize_params()
+        self.gather_works[gi] = _watchdog.track(f'sharding3.all_gather[{gi}]', dist.all_gather_into_tensor(
+            g.param_buf, g.param_shard, group=self.pg, async_op=True), self.world)
+        self._note_peak()
+
+    def _gather_unit(self, u, wait):
+        for gi in u.gids:
+            self._gather_group(gi)
+        if wait:
+            for gi in u.gids:
                 w = self.gather_works.pop(gi, None)
                 if w is not None:
                     w.wait()
+
+    def _release_unit(self, u):
+        for gi in u.gids:
+            w = self.gather_works.pop(gi, None)
+            if w is not None:
+                w.wait()
+            self.groups[gi].release_params()
+
+    def _prepare_backward(self, u):
+        self._gather_unit(u, wait=True)
+        for gi in u.gids:
+            self.groups[gi].materialize_grads()
+            self.groups[gi].reattach_grads()
+        if u.index > 0:
+            self._gather_unit(self.unit_meta[u.index - 1], wait=False)
+        self._note_peak()
+
+    def _make_pre(self, u):
+        def hook(layer, inputs):
+            if _in_backward():  # recompute re-running the unit inside backward
+                self._prepare_backward(u)
+                return
+            self._gather_unit(u, wait=True)
+            if u.index + 1 < len(self.unit_meta):
+                self._gather_unit(self.unit_meta[u.index + 1], wait=False)
         return hook
 
+    def _make_post(self, u):
+        def hook(layer, inputs, outputs):
+            if _in_backward():
+                return
+            if torch.is_grad_enabled():
+                fired = [False]
+
+                def grad_hook(grad, u=u, fired=fired):
+                    if not fired[0]:
+                        fired[0] = True
+                        self._prepare_backward(u)
+                for t in _tensors_in(outputs):
+                    if t.requires_grad:
+                        t.register_hook(grad_hook)
+            if self.release_after_forward:
+                self._note_peak()
+                self._release_unit(u)
+        return hook
+
+    def _on_grads_launched(self, gi):
+        if gi in self._unit_gid and _in_backward():
+            # every gradient of this bucket is final: its gathered parameters are dead
+            self.groups[gi].release_params()
+            # keep at most two reduce-scatters in flight; older ones are complete on the
+            # compute stream's timeline (wait = stream dependency, no host sync), so their
+            # full gradient buffers can go back to the allocator
+            self._rs_window.append(gi)
+            while len(self._rs_window) > 2:
+                old = self._rs_window.pop(0)
+                for g2, w in self.reducer.works:
+                    if g2 == old:
+                        w.wait()
+                self._note_peak()
+                self.groups[old].release_grads()
+
+    def _on_backward_done(self):
+        self._rs_window = []
+        self._note_peak()
+        for u in self.unit_meta:
+            for gi in u.gids:
+                self.groups[gi].release_params()
+                self.groups[gi].release_grads()
+
+    # -- params all-gather (resident groups) ------------------------------------------------
     def launch_gathers(self, order=None):
         if self.world == 1:
             self.params_stale = False
             return
-        order = range(len(self.groups) - 1, -1, -1) if order is None else order
+        n = self.n_resident
+        order = range(n - 1, -1, -1) if order is None else order
         for gi in order:  # buckets are in backward order: gather forward-first buckets first
             g = self.groups[gi]
-            self.gather_works[gi] = dist.all_gather_into_tensor(
-                g.param_buf, g.param_shard, group=self.pg, async_op=True)
+            self.gather_works[gi] = _watchdog.track(f'sharding.all_gather[{gi}]', dist.all_gather_into_tensor(
+                g.param_buf, g.param_shard, group=self.pg, async_op=True), self.world)
         self.params_stale = False
 
     def wait_gathers(self):
@@ -104,32 +315,55 @@ class ShardedState:
 
     def before_forward(self):
         for g in self.groups:
-            if any(p._t.grad is None for p in g.params if p._t.requires_grad):
+            if not g.grads_released and g.grads_missing():
                 g.grad_buf.zero_()
                 g.reattach_grads()
         if self.params_stale:
             self.launch_gathers()
-            if self.stage != 3:
-                self.wait_gathers()
+            self.wait_gathers()
+        if self.zero3 and self.unit_meta:
+            self._gather_unit(self.unit_meta[0], wait=False)  # prefetch the first unit
 
     def after_step(self):
         self.params_stale = True
+        if self.zero3:
+            for u in self.unit_meta:  # gathered copies (e.g. from state_dict) are stale now
+                self._release_unit(u)
         if self.stage in (1, 2):
             self.launch_gathers()
             self.wait_gathers()
 
     def sync_params(self):
+        """Make every parameter hold its full current value (resident and unit groups)."""
         if self.params_stale:
             self.launch_gathers()
+        for u in self.unit_meta:
+            self._gather_unit(u, wait=False)
         self.wait_gathers()
+
+    def release_all(self):
+        for u in self.unit_meta:
+            self._release_unit(u)
 
     def zero_grad(self):
         for g in self.groups:
+            if g.grads_released:
+                continue
             g.grad_buf.zero_()
             g.reattach_grads()
         if self.stage > 1 and self.world > 1:
             for s in self.shard_grads:
                 s.zero_()
+
+    def params_loaded(self):
+        """Full parameter values were written into the gathered buffers (set_state_dict):
+        refresh the owned shards and the optimizer's fp32 masters from them."""
+        for gi in range(self.n_resident, len(self.groups)):
+            g = self.groups[gi]
+            if not g.params_released:
+                g.param_shard.copy_(g.shard(g.param_buf))
+        for cb in self.on_params_loaded:
+            cb()
 
 
 class ShardedOptimizer:
@@ -139,25 +373,38 @@ class ShardedOptimizer:
     apply_decay_param_fun, grad_clip) are taken from the user's optimizer.
     """
 
-    def __init__(self, optimizer, state: ShardedState):
+    def __init__(self, optimizer, state: ShardedState, offload=False, mp_group=None,
+                 norm_groups=()):
         self._inner = optimizer
         self.state = state
         self._kind = type(optimizer).__name__
         if self._kind not in ('Adam', 'AdamW', 'Momentum', 'SGD'):
             raise NotImplementedError(f"sharding does not support {self._kind} yet")
+        self._offload = bool(offload)
+        self._mp_pg = None if mp_group is None or mp_group.nranks == 1 else mp_group.process_group
+        self._norm_pgs = [g.process_group for g in norm_groups if g is not None and g.nranks > 1]
         self._pieces = []
         self._masters, self._m, self._v = [], [], []
         for gi, g in enumerate(state.groups):
             shard = g.param_shard
-            master = shard.detach().float().clone() if shard.dtype != torch.float32 else None
+            sdev = torch.device('cpu') if self._offload else g.device
+            master = shard.detach().float().clone().to(sdev) \
+                if (shard.dtype != torch.float32 or self._offload) else None
             self._masters.append(master)
-            self._m.append(torch.zeros(g.shard_numel, dtype=torch.float32, device=g.device))
-            self._v.append(torch.zeros(g.shard_numel, dtype=torch.float32, device=g.device)
+            self._m.append(torch.zeros(g.shard_numel, dtype=torch.float32, device=sdev))
+            self._v.append(torch.zeros(g.shard_numel, dtype=torch.float32, device=sdev)
                            if self._kind in ('Adam', 'AdamW') else None)
             for (p, lo, hi, plo) in g.params_in_shard():
                 self._pieces.append((gi, p, lo, hi, plo))
         self._plan = None
         self._step = 0
+        state.on_params_loaded.append(self._refresh_masters)
+
+    def _refresh_masters(self):
+        with torch.no_grad():
+            for gi, g in enumerate(self.state.groups):
+                if self._masters[gi] is not None:
+                    self._masters[gi].copy_(g.param_shard.float())
 
     # -- paddle optimizer surface ----------------------------------------------------------
     def get_lr(self):
@@ -177,6 +424,14 @@ class ShardedOptimizer:
     def clear_grad(self, set_to_zero=True):
         self.state.zero_grad()
 
+    def _scaler_grads(self):
+        return list(self.state.shard_grads)
+
+    def _found_inf_groups(self):
+        st = self.state
+        return [pg for pg, n in ((st.pg, st.world), (st.dp_pg, st.dp_world)) if n > 1] + \
+            ([self._mp_pg] if self._mp_pg is not None else []) + list(self._norm_pgs)
+
     clear_gradients = clear_grad
 
     def _wd(self, p):
@@ -195,10 +450,32 @@ class ShardedOptimizer:
             return None
         if not isinstance(clip, ClipGradByGlobalNorm):
             raise NotImplementedError("sharding supports ClipGradByGlobalNorm only")
+        st = self.state
+        dev = st.shard_grads[0].device if st.shard_grads else torch.device('cpu')
+
+        def nsq(ts):
+            return K.global_l2_norm_sq(ts).reshape(1).float() if ts else \
+                torch.zeros(1, device=dev)
         # owned shards partition the gradients: local sum of squares + one all-reduce
-        sq = K.global_l2_norm_sq(self.state.shard_grads)
-        if self.state.world > 1:
-            dist.all_reduce(sq, group=self.state.pg)
+        if self._mp_pg is None:
+            sq = nsq(st.shard_grads)
+            if st.world > 1:
+                dist.all_reduce(sq, group=st.pg)
+        else:
+            # TP-split parameters are summed over the mp group, replicated ones counted once
+            gs = st.shard_grads
+            d = [gs[gi][lo:hi] for gi, p, lo, hi, _ in self._pieces if getattr(p, 'is_distributed', False)]
+            r = [gs[gi][lo:hi] for gi, p, lo, hi, _ in self._pieces
+                 if not getattr(p, 'is_distributed', False)]
+            both = torch.cat([nsq(d), nsq(r)])
+            if st.world > 1:
+                dist.all_reduce(both, group=st.pg)
+            sd = both[:1].contiguous()
+            dist.all_reduce(sd, group=self._mp_pg)
+            sq = sd + both[1:]
+        for pg in self._norm_pgs:  # pipeline stages own disjoint parameters
+            dist.all_reduce(sq, group=pg)
+        sq = sq.reshape(())
         return clip.clip_norm / torch.clamp(torch.sqrt(sq), min=clip.clip_norm)
 
     @torch.no_grad()
@@ -211,7 +488,9 @@ class ShardedOptimizer:
         lr = o.get_lr()
         dev = st.groups[0].device if st.groups else None
         coupled = self._kind == 'Adam' and o._weight_decay
-        if dev is not None and dev.type == 'cuda' and _native.available() and not coupled:
+        if self._offload:
+            self._step_offload(lr, coef)
+        elif dev is not None and dev.type == 'cuda' and _native.available() and not coupled:
             # the clip coefficient is read by the update kernel: no extra pass over the grads
             self._step_hip(lr, None if coef is None else
                            coef.to(torch.float32).reshape(()).contiguous())
@@ -224,6 +503,35 @@ class ShardedOptimizer:
             else:
                 self._step_ref(lr)
         st.after_step()
+
+    def _step_offload(self, lr, coef):
+        """Host-resident master/moments (group_sharded offload=True): owned grads go to the
+        host, the update runs there, the new low-precision shard is copied back."""
+        st = self.state
+        o = self._inner
+        c = None if coef is None else float(coef)
+        for gi, g in enumerate(st.groups):
+            gh = st.shard_grads[gi].detach().to('cpu', torch.float32)
+            if c is not None:
+                gh.mul_(c)
+            master = self._masters[gi]
+            for gj, p, lo, hi, plo in self._pieces:
+                if gj != gi:
+                    continue
+                lrm = p.optimize_attr.get('learning_rate', 1.0)
+                if self._kind in ('Adam', 'AdamW'):
+                    wd = self._wd(p)
+                    grad = gh[lo:hi]
+                    if self._kind == 'Adam' and wd:
+                        grad = grad + wd * master[lo:hi]
+                        wd = 0.0
+                    K.adamw_ref([master[lo:hi]], [grad], [self._m[gi][lo:hi]], [self._v[gi][lo:hi]],
+                                [None], lr, o._beta1, o._beta2, o._epsilon, [wd], [lrm], self._step)
+                else:
+                    K.momentum_ref([master[lo:hi]], [gh[lo:hi]], [self._m[gi][lo:hi]], [None],
+                                   lr * lrm, getattr(o, '_momentum', 0.0), [self._wd(p)],
+                                   getattr(o, '_use_nesterov', False))
+            g.param_shard.copy_(master.to(g.dtype), non_blocking=False)
 
     def _piece_views(self, gi, lo, hi):
         g = self.state.groups[gi]
@@ -344,11 +652,27 @@ class ShardedModel(Layer):
         return self._layer(*inputs, **kwargs)
 
     def state_dict(self, *a, **k):
-        self._state.sync_params()
-        return self._layer.state_dict(*a, **k)
+        st = self._state
+        st.sync_params()
+        sd = self._layer.state_dict(*a, **k)
+        if st.zero3:
+            # unit parameters are freed again after this call: hand out copies
+            unit_ids = {id(p) for u in st.unit_meta for gi in u.gids for p in st.groups[gi].params}
+            for key, v in list(sd.items()):
+                if id(v) in unit_ids:
+                    c = Parameter(v._t.detach().clone())
+                    c.name = v.name
+                    sd[key] = c
+            st.release_all()
+        return sd
 
     def set_state_dict(self, sd, use_structured_name=True):
+        st = self._state
+        st.sync_params()
         r = self._layer.set_state_dict(sd, use_structured_name)
+        st.params_loaded()
+        if st.zero3:
+            st.release_all()
         return r
 
     set_dict = set_state_dict
@@ -361,19 +685,31 @@ class ShardedModel(Layer):
         return self._layer.named_parameters(prefix, include_sublayers)
 
     def get_all_parameters(self, convert2cpu=False):
+        """Gather every parameter (stays gathered until the next forward/step releases it)."""
         self._state.sync_params()
-        return self._layer.parameters()
+        ps = self._layer.parameters()
+        if convert2cpu:
+            return [Parameter(p._t.detach().cpu()) for p in ps]
+        return ps
 
 
 def group_sharded_parallel(model, optimizer, level, scaler=None, group=None, offload=False,
                            sync_buffers=False, buffer_max_size=2 ** 23, segment_size=2 ** 20,
                            sync_comm=False, dp_group=None, exclude_layer=None,
                            bucket_mb=128):
+    """paddle.distributed.sharding.group_sharded_parallel (parity:
+    python/paddle/distributed/sharding/group_sharded.py). ``offload=True`` keeps the fp32
+    master weights and optimizer moments in host memory (the update runs on the CPU)."""
     if level not in LEVELS:
         raise ValueError(f"level must be one of {list(LEVELS)}")
-    st = ShardedState(model, level, group, segment_bytes=bucket_mb << 20)
+    st = ShardedState(model, level, group, segment_bytes=bucket_mb << 20, dp_group=dp_group,
+                      segment_size=segment_size, exclude_layer=exclude_layer)
     # the (bucketed, flat) params were re-pointed in place: the inner optimizer's list stays valid
-    return ShardedModel(model, st), ShardedOptimizer(optimizer, st), scaler
+    sopt = ShardedOptimizer(optimizer, st, offload=offload)
+    if scaler is not None:
+        from ..amp import ShardedGradScaler
+        scaler = ShardedGradScaler.wrap(scaler, st)
+    return ShardedModel(model, st), sopt, scaler
 
 
 def save_group_sharded_model(model, output, optimizer=None):

@@ -7,12 +7,14 @@ fused-epilogue variants on our MFMA kernels.
 import torch
 
 from ..framework.core import Tensor, _u
+from ..amp import amp_op as _amp_op
 
 
 def _t(x):
     return x._t if isinstance(x, Tensor) else torch.as_tensor(x)
 
 
+@_amp_op('matmul')
 def matmul(x, y, transpose_x=False, transpose_y=False, name=None):
     a, b = _t(x), _t(y)
     if transpose_x:
@@ -22,10 +24,12 @@ def matmul(x, y, transpose_x=False, transpose_y=False, name=None):
     return Tensor(torch.matmul(a, b))
 
 
+@_amp_op('mm')
 def mm(input, mat2, name=None):
     return Tensor(torch.matmul(_t(input), _t(mat2)))
 
 
+@_amp_op('bmm')
 def bmm(x, y, name=None):
     return Tensor(torch.bmm(_t(x), _t(y)))
 
