@@ -155,7 +155,12 @@ class GPTMLP(nn.Layer):
             self._fused = True
 
     def forward_nobias(self, x):
+        """fc2(gelu(fc1 x)) without fc2's bias (fused into the next kernel). On the device the
+        bias+GELU and its backward live in the GEMM epilogues (K.mlp_gelu)."""
         t = _u(x)
+        if t.is_cuda:
+            return Tensor(K.mlp_gelu(t, self.fc1.weight._t, self.fc1.bias._t, self.fc2.weight._t,
+                                     self.approx))
         hdn = K.bias_gelu(K.linear(t, self.fc1.weight._t), self.fc1.bias._t, self.approx)
         return Tensor(K.linear(hdn, self.fc2.weight._t))
 

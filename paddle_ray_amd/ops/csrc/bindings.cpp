@@ -52,6 +52,10 @@ void pra_bias_gelu_bwd_db(const void*, const void*, const void*, void*, float*, 
 int pra_bn_nrb(int, int);
 int pra_gemm_bias_act(const void*, const void*, const void*, void*, void*, int, int, int, int, int, int, int, int,
                       hipStream_t);
+int pra_gemm_lds(int, const void*, const void*, const void*, void*, void*, float*, int, int, int, int, int, int, int,
+                 int, int, int, int, float*, hipStream_t);
+int pra_gemm_lds_splits(int, int, int);
+int pra_colsum_partials(const float*, void*, int, int, int, hipStream_t);
 void pra_bn_fwd_train(const void*, const void*, const void*, const void*, float*, float*, void*, uint8_t*, float*,
                       float*, float*, float*, int, int, int, float, float, int, int, int, hipStream_t);
 void pra_bn_fwd_infer(const void*, const void*, const void*, const void*, const float*, const float*, void*, float*,
@@ -79,6 +83,19 @@ PYBIND11_MODULE(_pra_hip, m) {
     if (pra_gemm_bias_act(CV(a), CV(b), CV(bias), V(c), V(z), M, N, K, lda, ldb, ldc, dt, act, S(s)) != 0)
       throw std::invalid_argument("gemm_bias_act: unsupported shape/stride/dtype");
     check_launch("gemm_bias_act");
+  });
+  m.def("gemm_lds_splits", [](int M, int N, int K) { return pra_gemm_lds_splits(M, N, K); });
+  m.def("gemm_lds", [](int layout, P a, P b, P bias, P c, P z, P colsum, int M, int N, int K, int lda, int ldb,
+                       int ldc, int ldz, int dt, int epi, int beta, int splits, P ws, P s) {
+    if (pra_gemm_lds(layout, CV(a), CV(b), CV(bias), V(c), V(z), F(colsum), M, N, K, lda, ldb, ldc, ldz, dt, epi, beta,
+                     splits, F(ws), S(s)) != 0)
+      throw std::invalid_argument("gemm_lds: unsupported shape/stride/dtype");
+    check_launch("gemm_lds");
+  });
+  m.def("colsum_partials", [](P part, P out, int P_, int N, int dt, P s) {
+    if (pra_colsum_partials(CF(part), V(out), P_, N, dt, S(s)) != 0)
+      throw std::invalid_argument("colsum_partials: unsupported dtype");
+    check_launch("colsum_partials");
   });
   m.def("layernorm_fwd", [](P x, P w, P b, P y, P mean, P rstd, int rows, int cols, float eps, int dtx, int dtw, P s) {
     pra_layernorm_fwd(CV(x), CV(w), CV(b), V(y), F(mean), F(rstd), rows, cols, eps, dtx, dtw, S(s));

@@ -1,0 +1,569 @@
+// LDS-DMA pipelined MFMA GEMM for gfx950 (CDNA4) — the framework's training GEMM.
+//
+//   C[M,N] (=|+=) epi( A[M,K] · B[K,N] )     bf16/f16 operands, fp32 accumulation
+//
+// Operand layouts (template flags), covering the three GEMMs of a Linear layer with Paddle's
+// [in, out] weight (reference python/paddle/nn/functional/common.py `linear`; the fused
+// epilogues follow paddle/phi/kernels/fusion/gpu/fused_gemm_epilogue_kernel.cu semantics):
+//   AK = true : A stored [M][K] (row pitch lda)  — "K-contiguous"
+//   AK = false: A stored [K][M] (row pitch lda)  — "M-contiguous"
+//   BK = true : B stored [N][K] (row pitch ldb)
+//   BK = false: B stored [K][N] (row pitch ldb)
+//   forward  y = x·W        : AK=1, BK=0     dgrad dx = dy·Wᵀ : AK=1, BK=1
+//   wgrad   dW = xᵀ·dy      : AK=0, BK=0     (tied LM head: logits = h·Eᵀ is AK=1, BK=1)
+//
+// Structure (cdna_hip_programming.md §5: glds staging pipeline, counted vmcnt, raw barrier):
+//   * 256x256 output tile per 512-thread workgroup (8 wave64 = 2(M) x 4(N), 128x64 per wave,
+//     8x4 accumulators of v_mfma_f32_16x16x32_{bf16,f16}); 1 workgroup per CU.
+//   * K is staged 64 deep per step (whole 128-B lines of every row) into 2 LDS slots (2 x 64 KB) by
+//     global_load_lds_dwordx4 (LDS-DMA: no VGPR staging, no ds_write). The step-(k+2) DMA is
+//     issued under step k's second k-half; fragments are register double-buffered per 32-deep
+//     k-half so every LDS read runs under the previous half's MFMAs; one raw s_barrier per
+//     K-step (no __syncthreads: its fence would drain the DMA).
+//   * LDS images are lane-linear (what LDS-DMA writes); bank swizzles are applied by permuting
+//     each lane's GLOBAL source chunk and reading with the same permutation:
+//       K-contiguous operand -> image [row][32 k] (64-B rows), 16-B chunk ^= kc_swz(row),
+//                               fragments by ds_read_b128 (conflict-free in its lane groups);
+//       MN-contiguous operand -> image [k][256] (512-B rows), chunk ^= 2*((k&3)|((k>>1)&4)),
+//                               fragments by 2 x ds_read_b64_tr_b16 (hardware transpose).
+//   * MFMAs are issued as (B-frag, A-frag) so each lane's accumulator holds 4 consecutive
+//     output COLUMNS of one row -> packed 8-byte epilogue stores.
+//   * XCD-aware bijective tile remap + 8-row tile grouping for L2 reuse.
+// Epilogue (in registers on the accumulators): + bias[N], activation (GELU tanh/erf, ReLU)
+// with the pre-activation optionally stored to Z, or dGELU: C = acc * gelu'(Z) with per-tile
+// column partial sums written to `colsum` (the bias gradient, reduced by pra_colsum_partials);
+// `beta=1` accumulates into C (dW += xᵀ·dy straight into the flat gradient buffer).
+#include "common.h"
+
+namespace pra {
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+template <typename T> struct V8;
+template <> struct V8<bf16> { typedef __bf16 type __attribute__((ext_vector_type(8))); };
+template <> struct V8<f16> { typedef _Float16 type __attribute__((ext_vector_type(8))); };
+
+template <typename T>
+__device__ __forceinline__ f32x4 mma(typename V8<T>::type a, typename V8<T>::type b, f32x4 c);
+template <>
+__device__ __forceinline__ f32x4 mma<bf16>(V8<bf16>::type a, V8<bf16>::type b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+template <>
+__device__ __forceinline__ f32x4 mma<f16>(V8<f16>::type a, V8<f16>::type b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+
+template <typename T> __device__ __forceinline__ float to_f(uint16_t u);
+template <> __device__ __forceinline__ float to_f<bf16>(uint16_t u) { return bf2f(u); }
+template <> __device__ __forceinline__ float to_f<f16>(uint16_t u) { return (float)__builtin_bit_cast(_Float16, u); }
+template <typename T> __device__ __forceinline__ uint32_t pack2(float a, float b);
+template <> __device__ __forceinline__ uint32_t pack2<bf16>(float a, float b) { return pack_bf2(a, b); }
+template <> __device__ __forceinline__ uint32_t pack2<f16>(float a, float b) {
+  return (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)a) | ((uint32_t)__builtin_bit_cast(uint16_t, (_Float16)b) << 16);
+}
+
+enum Epi : int { kNone = 0, kGeluErf = 1, kGeluTanh = 2, kRelu = 3, kDGeluErf = 4, kDGeluTanh = 5 };
+
+__device__ __forceinline__ float gelu_tanh(float x) {
+  const float u = 0.79788456080286536f * (x + 0.044715f * x * x * x);
+  return 0.5f * x * (1.f + tanhf(u));
+}
+__device__ __forceinline__ float dgelu_tanh(float x) {
+  const float u = 0.79788456080286536f * (x + 0.044715f * x * x * x);
+  const float t = tanhf(u);
+  return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * 0.79788456080286536f * (1.f + 0.134145f * x * x);
+}
+__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
+__device__ __forceinline__ float dgelu_erf(float x) {
+  return 0.5f * (1.f + erff(x * 0.70710678118654752f)) + x * 0.3989422804014327f * __expf(-0.5f * x * x);
+}
+
+template <int E>
+__device__ __forceinline__ float act(float x) {
+  if (E == kGeluErf) return gelu_erf(x);
+  if (E == kGeluTanh) return gelu_tanh(x);
+  if (E == kRelu) return fmaxf(x, 0.f);
+  return x;
+}
+
+constexpr int BM = 256, BN = 256, BKT = 64, NT = 512;
+constexpr int IMG = BM * BKT * 2;       // 32 KB per operand image
+constexpr int SLOT = 2 * IMG;           // A image + B image
+constexpr int LDS_BYTES = 2 * SLOT + 128 * 4 * 4;  // double-buffered 128 KB (+2 KB: epilogue image pitch)
+constexpr int NDMA = IMG / (NT * 16);   // LDS-DMA instructions per thread per operand per K-step (4)
+
+typedef short v4i16 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+// MC image [64 k][256] (512-B rows): 16-B chunk ^= mc_swz(k) makes the two ds_read_b64_tr_b16
+// of a 32-lane half (k rows 8g+q, g = 0,1, q = 0..3) hit 16 distinct slots of the bank row.
+__device__ __forceinline__ int mc_swz(int k) { return 2 * ((k & 3) | ((k >> 1) & 4)); }
+// KC image [256 rows][64 k] (128-B rows): 16-B chunk ^= (row>>1)&7. ds_read_b128 serves lanes in
+// the groups {0-3,12-15,20-27}, {4-11,16-19,28-31} (+32); with this XOR each group's 16 lanes hit
+// 16 distinct 16-B slots (conflict-free).
+__device__ __forceinline__ int kc_swz(int row) { return (row >> 1) & 7; }
+
+// Per-thread DMA plan for one operand image (NDMA glds per thread per K-step). A K-step moves
+// whole 128-B lines of every row (BK = 64 bf16), so each L2 line is requested once.
+// KC image: position P (16-B chunk 0..2047) = row P>>3, slot P&7 holds global chunk (P&7)^kc_swz(row).
+// MC image: position P = k-row P>>5, slot P&31 holds global chunk (P&31)^mc_swz(k).
+template <bool KC>
+struct Dma {
+  uint32_t voff[NDMA];  // per-lane byte offsets of the chunks this thread stages
+  uint64_t base;        // wave-uniform operand base (SGPRs); advanced per K-step
+  uint64_t step;        // bytes per K-step
+  __device__ __forceinline__ void init(const uint16_t* b, int ld, int r0, int rmax, int tid) {
+#pragma unroll
+    for (int n = 0; n < NDMA; ++n) {
+      const int P = n * NT + tid;
+      if (KC) {
+        const int row = P >> 3, c = (P & 7) ^ kc_swz(row);
+        const int r = min(r0 + row, rmax);
+        voff[n] = (uint32_t)(((int64_t)r * ld + 8 * c) * 2);
+      } else {
+        const int k = P >> 5, c = (P & 31) ^ mc_swz(k);
+        const int col = min(r0 + 8 * c, rmax);  // rmax = last valid 8-aligned chunk start
+        voff[n] = (uint32_t)(((int64_t)k * ld + col) * 2);
+      }
+    }
+    base = (uint64_t)b;
+    step = KC ? (uint64_t)BKT * 2 : (uint64_t)BKT * ld * 2;
+  }
+  __device__ __forceinline__ void issue1(uint32_t lds_img, int wave, int kt, int n) {
+    const uint64_t g = base + (uint64_t)kt * step;
+    // readfirstlane returns int: go through uint32_t so the low word is ZERO-extended
+    const uint64_t gs = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(g >> 32)) << 32) |
+                        (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)g);
+    // wave-uniform LDS base in M0; the hardware adds lane*16. Issued from inline asm so the
+    // compiler's waitcnt model does not see an LDS write in flight and never drains it with
+    // vmcnt(0) ahead of the fragment reads: the explicit vmcnt in the K loop is the only wait.
+    const uint32_t dst = __builtin_amdgcn_readfirstlane(lds_img + (n * NT + wave * 64) * 16);
+    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff[n]), "s"(gs), "s"(dst)
+                 : "memory");
+  }
+};
+
+// Fragment for rows [r0, r0+16) (row = lane&15), k = 32*s + 8*(lane>>4) + j of a K-step.
+template <typename T, bool KC>
+__device__ __forceinline__ typename V8<T>::type frag(const char* img, int r0, int s, int lane) {
+  typedef typename V8<T>::type v8;
+  if (KC) {
+    const int row = r0 + (lane & 15), c = (4 * s + (lane >> 4)) ^ kc_swz(row);
+    return *reinterpret_cast<const v8*>(img + row * 128 + c * 16);
+  } else {
+    // ds_read_b64_tr_b16: lane 4q+p of each 16-lane group g addresses k-row 32s+8g+q (+4),
+    // columns r0+4p..+3, and receives its own column's 4 k-values.
+    const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+    const int k = 32 * s + 8 * g + q, x = mc_swz(k);  // mc_swz(k) == mc_swz(k + 4)
+    const int c = ((r0 >> 3) + (p >> 1)) ^ x;
+    const char* a0 = img + k * 512 + c * 16 + 8 * (p & 1);
+    const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)a0);
+    const v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(a0 + 4 * 512));
+    const u32x2 ul = __builtin_bit_cast(u32x2, lo), uh = __builtin_bit_cast(u32x2, hi);
+    const u32x4 u = {ul[0], ul[1], uh[0], uh[1]};
+    return __builtin_bit_cast(v8, u);
+  }
+}
+
+template <typename T, bool AK, bool BK, int E, bool BETA, bool SPLIT>
+__global__ __launch_bounds__(NT, 1) void gemm_lds_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
+                                                          const uint16_t* __restrict__ bias, uint16_t* __restrict__ C,
+                                                          uint16_t* __restrict__ Z, float* __restrict__ colsum,
+                                                          int M, int N, int K, int lda, int ldb, int ldc, int ldz,
+                                                          int splits, float* __restrict__ ws) {
+  __shared__ __attribute__((aligned(1024))) char lds[LDS_BYTES];
+  typedef typename V8<T>::type v8;
+  const uint32_t lds_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)lds;
+
+  const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;
+  const int nb = gridDim.x;
+  int pid = blockIdx.x;
+  {  // contiguous tile run per XCD (bijective for any grid size)
+    const int q = nb >> 3, r = nb & 7, xcd = pid & 7;
+    pid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (pid >> 3);
+  }
+  // split-K: the splits of one tile are adjacent ids (same XCD); each covers a K range and
+  // writes an fp32 partial tile that splitk_reduce_k combines
+  const int split = SPLIT ? pid % splits : 0;
+  if (SPLIT) pid /= splits;
+  const int group = 8 * tiles_n, gi = pid / group, first_m = gi * 8;
+  const int gm = min(tiles_m - first_m, 8);
+  const int tm = first_m + (pid % group) % gm, tn = (pid % group) / gm;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wr = wave >> 2, wc = wave & 3;
+
+  Dma<AK> da;
+  Dma<BK> db;
+  if (AK) da.init(A, lda, m0, M - 1, tid); else da.init(A, lda, m0, M - 8, tid);
+  if (BK) db.init(B, ldb, n0, N - 1, tid); else db.init(B, ldb, n0, N - 8, tid);
+  int nk = K / BKT;
+  if (SPLIT) {
+    const int per = (nk + splits - 1) / splits, kb = split * per;
+    nk = max(0, min(nk, kb + per) - kb);
+    da.base += (uint64_t)kb * da.step;
+    db.base += (uint64_t)kb * db.step;
+  }
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  v8 fa0[8], fb0[4], fa1[8], fb1[4];
+  auto read_frags = [&](v8 (&fa)[8], v8 (&fb)[4], int kt, int s) {
+    const char* ai = lds + (kt & 1) * SLOT;
+    const char* bi = ai + IMG;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) fb[j] = frag<T, BK>(bi, wc * 64 + j * 16, s, lane);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) fa[i] = frag<T, AK>(ai, wr * 128 + i * 16, s, lane);
+  };
+  // 32 MFMAs of one k-half, interleaved segment by segment with (optionally) the fragment reads
+  // of the next k-half and one LDS-DMA instruction of the next K-step every other segment, so
+  // DMA issue and LDS reads hide under the wave's own matrix work.
+  auto half = [&](v8 (&ca)[8], v8 (&cb)[4], v8 (&na)[8], v8 (&nb)[4], bool rd, int rkt, int rs, bool dma,
+                  int dkt) {
+    const uint32_t so = lds_base + (dkt & 1) * SLOT;
+    const char* ai = lds + (rkt & 1) * SLOT;
+    const char* bi = ai + IMG;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      if (dma) {
+        if (i < NDMA) da.issue1(so, wave, dkt, i);
+        else db.issue1(so + IMG, wave, dkt, i - NDMA);
+      }
+      if (rd) {
+        if (i < 4) nb[i] = frag<T, BK>(bi, wc * 64 + i * 16, rs, lane);
+        na[i] = frag<T, AK>(ai, wr * 128 + i * 16, rs, lane);
+      }
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = mma<T>(cb[j], ca[i], acc[i][j]);
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+
+  // prologue: K-steps 0 and 1 in flight, k-half 0 of step 0 in registers
+  if (nk > 0) {
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    if (t < nk) {
+#pragma unroll
+      for (int n = 0; n < NDMA; ++n) da.issue1(lds_base + t * SLOT, wave, t, n);
+#pragma unroll
+      for (int n = 0; n < NDMA; ++n) db.issue1(lds_base + t * SLOT + IMG, wave, t, n);
+    }
+  }
+  if (nk >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+  read_frags(fa0, fb0, 0, 0);
+
+  // K-step kt (slot kt&1): half 0 computes (kt,0) from F0 while reading (kt,1) into F1; then the
+  // barrier that retires step kt+1's DMA and every wave's reads of slot kt; half 1 refills slot kt
+  // with step kt+2 (DMA) and computes (kt,1) from F1 while reading (kt+1,0) into F0.
+  for (int kt = 0; kt < nk; ++kt) {
+    half(fa0, fb0, fa1, fb1, true, kt, 1, false, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): (kt,1) fragments landed; slot kt reads done
+    if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // step kt+1 landed (this wave)
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    half(fa1, fb1, fa0, fb0, kt + 1 < nk, kt + 1, 0, kt + 2 < nk, kt + 2);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // (kt+1,0) fragments landed
+  }
+  }  // nk > 0
+
+  if (SPLIT) {
+    float* wsp = ws + (int64_t)split * M * N;
+    const int mrow = m0 + wr * 128 + (lane & 15);
+    const int ncol = n0 + wc * 64 + 4 * (lane >> 4);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int m = mrow + i * 16;
+      if (m >= M) continue;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = ncol + j * 16;
+        if (n < N)
+          *reinterpret_cast<float4*>(wsp + (int64_t)m * N + n) =
+              make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+      }
+    }
+    return;
+  }
+
+  // Epilogue through LDS (the K loop is done with it): for each 128-row half the waves that own
+  // it park their fp32 accumulators in an [128][256+4] image (ds_write_b128, conflict-free pitch),
+  // then all 8 waves stream it out row-major: 8 columns per lane, whole 512-B row segments per 32
+  // lanes, so the bias/activation/pre-activation/beta/dGELU traffic is 16-B coalesced loads and
+  // stores instead of 8-B scatters across 16 rows.
+  // acc[i][j][r] = C[m0 + wr*128 + i*16 + (lane&15)][n0 + wc*64 + j*16 + 4*(lane>>4) + r]
+  float* img = reinterpret_cast<float*>(lds);
+  constexpr int PITCH = BN + 4;  // floats
+  // this thread's output units: row u>>5 (+16 per q), 8 columns at (u&31)*8 (fixed per thread)
+  const int ucol = (tid & 31) * 8, urow = tid >> 5;
+  const int n = n0 + ucol;
+  const bool ncol_ok = n < N;  // N % 8 == 0: a unit is all-in or all-out
+  float bv[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) bv[e] = 0.f;
+  if (bias && ncol_ok) {
+    const uint4 bb = *reinterpret_cast<const uint4*>(bias + n);
+    const uint32_t w4[4] = {bb.x, bb.y, bb.z, bb.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { bv[2 * e] = to_f<T>(w4[e] & 0xffff); bv[2 * e + 1] = to_f<T>(w4[e] >> 16); }
+  }
+  float cs[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) cs[e] = 0.f;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __syncthreads();  // (h=0) every wave is done reading K-loop tiles; (h=1) half 0 streamed out
+    if (wr == h) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int r = i * 16 + (lane & 15), c = wc * 64 + j * 16 + 4 * (lane >> 4);
+          *reinterpret_cast<f32x4*>(img + r * PITCH + c) = acc[i][j];
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int rr = urow + 16 * q, m = m0 + h * 128 + rr;
+      if (m >= M || !ncol_ok) continue;
+      const f32x4 lo = *reinterpret_cast<const f32x4*>(img + rr * PITCH + ucol);
+      const f32x4 hi = *reinterpret_cast<const f32x4*>(img + rr * PITCH + ucol + 4);
+      float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += bv[e];
+      if (E == kDGeluErf || E == kDGeluTanh) {
+        const uint4 zz = *reinterpret_cast<const uint4*>(Z + (int64_t)m * ldz + n);
+        const uint32_t w4[4] = {zz.x, zz.y, zz.z, zz.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float z0 = to_f<T>(w4[e] & 0xffff), z1 = to_f<T>(w4[e] >> 16);
+          v[2 * e] *= (E == kDGeluErf) ? dgelu_erf(z0) : dgelu_tanh(z0);
+          v[2 * e + 1] *= (E == kDGeluErf) ? dgelu_erf(z1) : dgelu_tanh(z1);
+        }
+      } else if (E != kNone) {
+        if (Z) {
+          uint4 o;
+          o.x = pack2<T>(v[0], v[1]); o.y = pack2<T>(v[2], v[3]);
+          o.z = pack2<T>(v[4], v[5]); o.w = pack2<T>(v[6], v[7]);
+          *reinterpret_cast<uint4*>(Z + (int64_t)m * ldz + n) = o;
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = act<E>(v[e]);
+      }
+      uint16_t* cp = C + (int64_t)m * ldc + n;
+      if (BETA) {
+        const uint4 cc = *reinterpret_cast<const uint4*>(cp);
+        const uint32_t w4[4] = {cc.x, cc.y, cc.z, cc.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { v[2 * e] += to_f<T>(w4[e] & 0xffff); v[2 * e + 1] += to_f<T>(w4[e] >> 16); }
+      }
+      uint4 o;
+      o.x = pack2<T>(v[0], v[1]); o.y = pack2<T>(v[2], v[3]);
+      o.z = pack2<T>(v[4], v[5]); o.w = pack2<T>(v[6], v[7]);
+      *reinterpret_cast<uint4*>(cp) = o;
+      if (colsum) {
+        // the bias gradient sums the ROUNDED output (what a separate reduction would read)
+        const uint32_t w4[4] = {o.x, o.y, o.z, o.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { cs[2 * e] += to_f<T>(w4[e] & 0xffff); cs[2 * e + 1] += to_f<T>(w4[e] >> 16); }
+      }
+    }
+  }
+  if (colsum) {
+    // threads sharing (tid & 31) own the same 8 columns: lanes l, l^32 then the 8 waves via LDS
+#pragma unroll
+    for (int e = 0; e < 8; ++e) cs[e] += __shfl_xor(cs[e], 32, 64);
+    __syncthreads();
+    if (lane < 32) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) img[wave * 256 + lane * 8 + e] = cs[e];
+    }
+    __syncthreads();
+    if (tid < 256) {
+      float t = 0.f;
+#pragma unroll
+      for (int w = 0; w < 8; ++w) t += img[w * 256 + tid];
+      const int nn = n0 + tid;
+      if (nn < N) colsum[(int64_t)tm * N + nn] = t;
+    }
+  }
+}
+
+// split-K combine: C[m][n..n+3] = epi(sum_s ws[s][m][n..n+3] + bias) (+ C if BETA)
+template <typename T, int E, bool BETA>
+__global__ void splitk_reduce_k(const float* __restrict__ ws, int splits, const uint16_t* __restrict__ bias,
+                                uint16_t* __restrict__ C, uint16_t* __restrict__ Z, int M, int N, int ldc, int ldz) {
+  const int64_t idx = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (idx >= (int64_t)M * N) return;
+  const int m = (int)(idx / N), n = (int)(idx % N);
+  float4 a = *reinterpret_cast<const float4*>(ws + idx);
+  for (int s = 1; s < splits; ++s) {
+    const float4 b = *reinterpret_cast<const float4*>(ws + (int64_t)s * M * N + idx);
+    a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+  }
+  float v[4] = {a.x, a.y, a.z, a.w};
+  if (bias) {
+    const uint2 bb = *reinterpret_cast<const uint2*>(bias + n);
+    v[0] += to_f<T>(bb.x & 0xffff); v[1] += to_f<T>(bb.x >> 16);
+    v[2] += to_f<T>(bb.y & 0xffff); v[3] += to_f<T>(bb.y >> 16);
+  }
+  if (E != kNone) {
+    if (Z) {
+      uint2 o;
+      o.x = pack2<T>(v[0], v[1]);
+      o.y = pack2<T>(v[2], v[3]);
+      *reinterpret_cast<uint2*>(Z + (int64_t)m * ldz + n) = o;
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = act<E>(v[r]);
+  }
+  uint16_t* c = C + (int64_t)m * ldc + n;
+  if (BETA) {
+    const uint2 cc = *reinterpret_cast<const uint2*>(c);
+    v[0] += to_f<T>(cc.x & 0xffff); v[1] += to_f<T>(cc.x >> 16);
+    v[2] += to_f<T>(cc.y & 0xffff); v[3] += to_f<T>(cc.y >> 16);
+  }
+  uint2 o;
+  o.x = pack2<T>(v[0], v[1]);
+  o.y = pack2<T>(v[2], v[3]);
+  *reinterpret_cast<uint2*>(c) = o;
+}
+
+// sum of P partial rows [P][N] fp32 -> out[N] (dtype T)
+template <typename T>
+__global__ void colsum_partials_k(const float* __restrict__ part, T* __restrict__ out, int P, int N) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  float s = 0.f;
+  for (int p = 0; p < P; ++p) s += part[(int64_t)p * N + n];
+  out[n] = Cvt<T>::from(s);
+}
+
+template <typename T, bool AK, bool BK, int E>
+void launch_e(const void* A, const void* B, const void* bias, void* C, void* Z, float* colsum, int M, int N, int K,
+              int lda, int ldb, int ldc, int ldz, int beta, int splits, float* ws, hipStream_t s) {
+  const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  auto pa = static_cast<const uint16_t*>(A);
+  auto pb = static_cast<const uint16_t*>(B);
+  auto pbias = static_cast<const uint16_t*>(bias);
+  auto pc = static_cast<uint16_t*>(C);
+  auto pz = static_cast<uint16_t*>(Z);
+  if (splits > 1) {
+    gemm_lds_kernel<T, AK, BK, kNone, false, true><<<tiles * splits, NT, 0, s>>>(
+        pa, pb, nullptr, nullptr, nullptr, nullptr, M, N, K, lda, ldb, ldc, ldz, splits, ws);
+    const int64_t quads = (int64_t)M * N / 4;
+    const int blocks = (int)((quads + 255) / 256);
+    if (beta) splitk_reduce_k<T, E, true><<<blocks, 256, 0, s>>>(ws, splits, pbias, pc, pz, M, N, ldc, ldz);
+    else splitk_reduce_k<T, E, false><<<blocks, 256, 0, s>>>(ws, splits, pbias, pc, pz, M, N, ldc, ldz);
+    return;
+  }
+  if (beta)
+    gemm_lds_kernel<T, AK, BK, E, true, false><<<tiles, NT, 0, s>>>(pa, pb, pbias, pc, pz, colsum, M, N, K, lda, ldb,
+                                                                    ldc, ldz, 1, nullptr);
+  else
+    gemm_lds_kernel<T, AK, BK, E, false, false><<<tiles, NT, 0, s>>>(pa, pb, pbias, pc, pz, colsum, M, N, K, lda, ldb,
+                                                                     ldc, ldz, 1, nullptr);
+}
+
+template <typename T, bool AK, bool BK>
+int launch_l(const void* A, const void* B, const void* bias, void* C, void* Z, float* colsum, int M, int N, int K,
+             int lda, int ldb, int ldc, int ldz, int epi, int beta, int splits, float* ws, hipStream_t s) {
+  switch (epi) {
+    case kNone: launch_e<T, AK, BK, kNone>(A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, beta, splits, ws, s); break;
+    case kGeluErf: launch_e<T, AK, BK, kGeluErf>(A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, beta, splits, ws, s); break;
+    case kGeluTanh: launch_e<T, AK, BK, kGeluTanh>(A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, beta, splits, ws, s); break;
+    case kRelu: launch_e<T, AK, BK, kRelu>(A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, beta, splits, ws, s); break;
+    case kDGeluErf: launch_e<T, AK, BK, kDGeluErf>(A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, beta, splits, ws, s); break;
+    case kDGeluTanh: launch_e<T, AK, BK, kDGeluTanh>(A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, beta, splits, ws, s); break;
+    default: return -1;
+  }
+  return 0;
+}
+
+template <typename T>
+int launch_t(int layout, const void* A, const void* B, const void* bias, void* C, void* Z, float* colsum, int M, int N,
+             int K, int lda, int ldb, int ldc, int ldz, int epi, int beta, int splits, float* ws, hipStream_t s) {
+  switch (layout) {
+    case 0: return launch_l<T, true, false>(A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, epi, beta, splits, ws, s);
+    case 1: return launch_l<T, true, true>(A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, epi, beta, splits, ws, s);
+    case 2: return launch_l<T, false, false>(A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, epi, beta, splits, ws, s);
+    default: return -1;
+  }
+}
+
+}  // namespace
+}  // namespace pra
+
+// layout: 0 = A[M][K]·B[K][N] (forward), 1 = A[M][K]·B[N][K]ᵀ (dgrad / NT), 2 = A[K][M]ᵀ·B[K][N] (wgrad).
+// epi: 0 none, 1 gelu(erf), 2 gelu(tanh), 3 relu (Z receives the pre-activation if given),
+//      4/5 dgelu(erf/tanh): C = acc * gelu'(Z) (Z required). colsum (optional, fp32
+//      [ceil(M/256)][N]) receives per-tile column partial sums of the stored C.
+// Returns -1 (nothing launched) for shapes outside what the kernel assumes: K % 64, N % 8 and every
+// leading dimension % 8 (16-B rows), M-contiguous operands need their MN extent >= 8.
+// Split-K factor for a problem: 1 unless the tile grid leaves CUs idle (fewer than ~256 tiles on
+// a long K loop); then the factor that best fills whole rounds of 256 workgroups.
+extern "C" int pra_gemm_lds_splits(int M, int N, int K) {
+  const int tiles = ((M + 255) / 256) * ((N + 255) / 256), nk = K / 64;
+  if (tiles >= 224 || nk < 16) return 1;
+  int best = 1;
+  double best_eff = 0.0;
+  for (int sp = 1; sp <= 8; ++sp) {
+    if (nk / sp < 8) break;
+    const double w = (double)tiles * sp / 256.0;
+    const double eff = w / __builtin_ceil(w) * (1.0 - 0.03 * (sp - 1));
+    if (eff > best_eff + 1e-9) { best_eff = eff; best = sp; }
+  }
+  return best;
+}
+
+// layout: 0 = A[M][K]·B[K][N] (forward), 1 = A[M][K]·B[N][K]ᵀ (dgrad / NT), 2 = A[K][M]ᵀ·B[K][N] (wgrad).
+// epi: 0 none, 1 gelu(erf), 2 gelu(tanh), 3 relu (Z receives the pre-activation if given),
+//      4/5 dgelu(erf/tanh): C = acc * gelu'(Z) (Z required). colsum (optional, fp32
+//      [ceil(M/256)][N]) receives per-tile column partial sums of the stored C.
+// splits > 1: split-K through the fp32 workspace ws [splits][M][N] (not with dgelu/colsum).
+// Returns -1 (nothing launched) for shapes outside what the kernel assumes: K % 64, N % 8 and every
+// leading dimension % 8 (16-B rows), M-contiguous operands need their MN extent >= 8.
+extern "C" int pra_gemm_lds(int layout, const void* A, const void* B, const void* bias, void* C, void* Z, float* colsum,
+                            int M, int N, int K, int lda, int ldb, int ldc, int ldz, int dtype, int epi, int beta,
+                            int splits, float* ws, hipStream_t s) {
+  if (M <= 0 || N <= 0 || K <= 0 || (K & 63) || (N & 7) || (lda & 7) || (ldb & 7) || (ldc & 7) || (ldz & 7)) return -1;
+  if (layout == 2 && (M < 8 || (M & 7))) return -1;
+  if ((layout == 0 || layout == 2) && N < 8) return -1;
+  if ((epi == 4 || epi == 5) && !Z) return -1;
+  if (splits > 1 && (!ws || epi >= 4 || colsum || ldc != N)) return -1;
+  // K-contiguous operands are addressed with 32-bit per-lane byte offsets from their base
+  if ((layout == 0 || layout == 1) && (int64_t)M * lda * 2 >= (int64_t)1 << 32) return -1;
+  if (layout == 1 && (int64_t)N * ldb * 2 >= (int64_t)1 << 32) return -1;
+  if (splits < 1) splits = 1;
+  if (dtype == pra::kBF16)
+    return pra::launch_t<pra::bf16>(layout, A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, epi, beta, splits, ws, s);
+  if (dtype == pra::kF16)
+    return pra::launch_t<pra::f16>(layout, A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, epi, beta, splits, ws, s);
+  return -1;
+}
+
+extern "C" int pra_colsum_partials(const float* part, void* out, int P, int N, int dtype, hipStream_t s) {
+  const int blocks = (N + 255) / 256;
+  if (dtype == pra::kBF16) pra::colsum_partials_k<pra::bf16><<<blocks, 256, 0, s>>>(part, (pra::bf16*)out, P, N);
+  else if (dtype == pra::kF16) pra::colsum_partials_k<pra::f16><<<blocks, 256, 0, s>>>(part, (pra::f16*)out, P, N);
+  else if (dtype == pra::kF32) pra::colsum_partials_k<float><<<blocks, 256, 0, s>>>(part, (float*)out, P, N);
+  else return -1;
+  return 0;
+}

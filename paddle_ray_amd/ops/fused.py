@@ -686,20 +686,140 @@ def flash_attention(q, k, v, causal=False, scale=None):
 
 
 # =============================================================================
+# MFMA GEMM (ops/csrc/gemm_lds.hip): the training GEMMs of every Linear
+# =============================================================================
+GEMM_FWD, GEMM_NT, GEMM_TN = 0, 1, 2  # x·W, dy·Wᵀ (or h·Eᵀ), xᵀ·dy
+EPI = {None: 0, 'gelu': 1, 'gelu_tanh': 2, 'relu': 3, 'dgelu': 4, 'dgelu_tanh': 5}
+_GEMM_MODE = __import__('os').environ.get('PRA_GEMM', 'mfma')  # 'blas' = hipBLASLt A/B baseline
+
+
+def _gemm_operand_ok(t):
+    return t.is_cuda and t.dtype in (torch.bfloat16, torch.float16) and t.dim() == 2 and \
+        t.stride(1) == 1 and t.stride(0) % 8 == 0 and t.data_ptr() % 16 == 0
+
+
+@R.register_kernel('gemm', 'ref')
+def _gemm_ref(layout, a, b, out=None, bias=None, z=None, epi=None, beta=0, want_colsum=False):
+    af, bf = a.float(), b.float()
+    y = af @ bf if layout == GEMM_FWD else (af @ bf.t() if layout == GEMM_NT else af.t() @ bf)
+    if bias is not None:
+        y = y + bias.float()
+    cs = None
+    if epi in ('dgelu', 'dgelu_tanh'):
+        zf = z.float().requires_grad_(True)
+        with torch.enable_grad():
+            g = torch.nn.functional.gelu(zf, approximate='tanh' if epi == 'dgelu_tanh' else 'none')
+            d, = torch.autograd.grad(g, zf, y)
+        y = d
+    elif epi is not None:
+        if z is not None:
+            z.copy_(y.to(z.dtype))
+        y = torch.nn.functional.gelu(y, approximate='tanh' if epi == 'gelu_tanh' else 'none') \
+            if epi.startswith('gelu') else torch.relu(y)
+    if beta and out is not None:
+        y = y + out.float()
+    yo = y.to(a.dtype)
+    if want_colsum:
+        cs = yo.float().sum(0)
+    if out is not None:
+        out.copy_(yo)
+        yo = out
+    return (yo, cs) if want_colsum else yo
+
+
+@R.register_kernel('gemm', 'hip')
+def _gemm_hip(layout, a, b, out=None, bias=None, z=None, epi=None, beta=0, want_colsum=False):
+    """One MFMA GEMM launch (+ split-K reduce when the tile grid would leave CUs idle).
+    Returns None when the shape/layout is outside what the kernel assumes (caller falls back)."""
+    if _GEMM_MODE == 'blas' or not (_gemm_operand_ok(a) and _gemm_operand_ok(b)) or a.dtype != b.dtype:
+        return None
+    if layout == GEMM_FWD:
+        M, K = a.shape
+        N = b.shape[1]
+    elif layout == GEMM_NT:
+        M, K = a.shape
+        N = b.shape[0]
+    else:
+        K, M = a.shape
+        N = b.shape[1]
+    if out is None:
+        out = torch.empty((M, N), device=a.device, dtype=a.dtype)
+    elif not _gemm_operand_ok(out) or out.dtype != a.dtype or tuple(out.shape) != (M, N):
+        return None
+    if z is not None and (not _gemm_operand_ok(z) or tuple(z.shape) != (M, N)):
+        return None
+    if bias is not None and (bias.dtype != a.dtype or not bias.is_contiguous()):
+        bias = bias.to(a.dtype).contiguous()
+    L = _native.lib()
+    e = EPI[epi]
+    part = None
+    if want_colsum:
+        part = torch.empty(((M + 255) // 256, N), device=a.device, dtype=torch.float32)
+    splits = 1 if (want_colsum or e >= 4 or out.stride(0) != N) else L.gemm_lds_splits(M, N, K)
+    ws = torch.empty((splits, M, N), device=a.device, dtype=torch.float32) if splits > 1 else None
+    try:
+        L.gemm_lds(layout, a.data_ptr(), b.data_ptr(), _ptr(bias), out.data_ptr(), _ptr(z), _ptr(part),
+                   M, N, K, a.stride(0), b.stride(0), out.stride(0), N if z is None else z.stride(0),
+                   _dt(a), e, int(beta), splits, _ptr(ws), _stream())
+    except ValueError:
+        return None
+    if want_colsum:
+        cs = torch.empty(N, device=a.device, dtype=torch.float32)
+        L.colsum_partials(part.data_ptr(), cs.data_ptr(), part.shape[0], N, 0, _stream())
+        return out, cs
+    return out
+
+
+def gemm(layout, a, b, out=None, bias=None, z=None, epi=None, beta=0, want_colsum=False):
+    """C (=|+=) epi(op(a)·op(b) + bias). layout: GEMM_FWD a[M,K]·b[K,N]; GEMM_NT a[M,K]·b[N,K]ᵀ;
+    GEMM_TN a[K,M]ᵀ·b[K,N]. On the device this is the in-tree MFMA kernel; shapes it does not
+    take (K % 64, ragged strides) go to hipBLASLt through torch and are counted as 'gemm'/'ref'."""
+    if a.is_cuda and R.select_backend(a, 'gemm') == 'hip':
+        r = _gemm_hip(layout, a, b, out, bias, z, epi, beta, want_colsum)
+        if r is not None:
+            return r
+        R._STATS[('gemm', 'fallback')] += 1
+    return _gemm_ref_fast(layout, a, b, out, bias, z, epi, beta, want_colsum)
+
+
+def _gemm_ref_fast(layout, a, b, out, bias, z, epi, beta, want_colsum):
+    """Library path (hipBLASLt via torch on the device, BLAS on the host) for what the MFMA
+    kernel does not take; epilogues composed."""
+    if epi is None and not want_colsum:
+        bb = b.t() if layout == GEMM_NT else b
+        aa = a if layout != GEMM_TN else a.t()
+        if out is not None and beta:
+            if bias is not None:
+                out.add_(bias)
+            return out.addmm_(aa, bb)
+        y = torch.addmm(bias, aa, bb) if bias is not None else torch.mm(aa, bb)
+        if out is not None:
+            out.copy_(y)
+            return out
+        return y
+    return _gemm_ref(layout, a, b, out, bias, z, epi, beta, want_colsum)
+
+
+# =============================================================================
 # Linear with fused weight-gradient accumulation
 # =============================================================================
+def _acc_grad_ok(g, w, dt):
+    return (g is not None and not torch.is_grad_enabled() and g.shape == w.shape
+            and g.dtype == dt and g.is_contiguous())
+
+
 class LinearFn(torch.autograd.Function):
-    """y = x @ W (+ b) with paddle's [in, out] weight. The backward accumulates dW
-    straight into W's existing ``.grad`` (the flat DP/sharding gradient buffer, or the
-    zeroed grad after ``clear_grad``) with ONE beta=1 GEMM -- hipBLASLt reads C in its
-    epilogue -- instead of materialising dW and running AccumulateGrad's separate add
-    kernel. W's AccumulateGrad node still runs (with no gradient to add) and fires the
-    post-accumulate-grad hooks that trigger the bucketed all-reduce / reduce-scatter."""
+    """y = x @ W (+ b) with paddle's [in, out] weight, all three GEMMs on the MFMA kernel:
+    forward x·W with the bias in its epilogue; dx = dy·Wᵀ; dW = xᵀ·dy accumulated straight into
+    W's existing ``.grad`` (the flat DP/sharding gradient buffer) by the kernel's beta=1
+    epilogue instead of materialising dW and running AccumulateGrad's separate add. W's
+    AccumulateGrad node still runs (with no gradient to add) and fires the post-accumulate-grad
+    hooks that trigger the bucketed all-reduce / reduce-scatter."""
 
     @staticmethod
     def forward(ctx, x, w, b):
         x2 = x.reshape(-1, x.shape[-1])
-        y = torch.addmm(b, x2, w) if b is not None else torch.mm(x2, w)
+        y = gemm(GEMM_FWD, x2, w, bias=b)
         ctx.save_for_backward(x)
         ctx.w = w
         ctx.has_b = b is not None
@@ -710,18 +830,19 @@ class LinearFn(torch.autograd.Function):
         x, = ctx.saved_tensors
         w = ctx.w
         dy2 = dy.reshape(-1, dy.shape[-1])
+        if not dy2.is_contiguous():
+            dy2 = dy2.contiguous()
         x2 = x.reshape(-1, x.shape[-1])
-        dx = torch.mm(dy2, w.t()).view(x.shape) if ctx.needs_input_grad[0] else None
+        dx = gemm(GEMM_NT, dy2, w).view(x.shape) if ctx.needs_input_grad[0] else None
         dw = None
         if ctx.needs_input_grad[1]:
             g = w.grad
-            if (g is not None and not torch.is_grad_enabled() and g.shape == w.shape
-                    and g.dtype == dy2.dtype and g.is_contiguous()):
+            if _acc_grad_ok(g, w, dy2.dtype):
                 # returning None still runs W's AccumulateGrad node, which fires its
                 # post-accumulate hooks after this in-place accumulation
-                g.addmm_(x2.t(), dy2)
+                gemm(GEMM_TN, x2, dy2, out=g, beta=1)
             else:
-                dw = torch.mm(x2.t(), dy2)
+                dw = gemm(GEMM_TN, x2, dy2)
         db = dy2.sum(0) if ctx.has_b and ctx.needs_input_grad[2] else None
         return dx, dw, db
 
@@ -732,34 +853,37 @@ def linear(x, w, b=None):
             not torch.is_autocast_enabled(x.device.type):
         return LinearFn.apply(x, w, b)
     x2 = x.reshape(-1, x.shape[-1])
-    y = torch.addmm(b, x2, w) if b is not None else torch.mm(x2, w)
+    if x2.is_cuda and x.dtype == w.dtype and not torch.is_autocast_enabled(x.device.type):
+        y = gemm(GEMM_FWD, x2, w, bias=b)
+    else:
+        y = torch.addmm(b, x2, w) if b is not None else torch.mm(x2, w)
     return y.view(*x.shape[:-1], w.shape[-1])
 
 
 class LinearNTFn(torch.autograd.Function):
     """y = x @ W^T for a [out, in] weight (the tied LM head: W is the [vocab, hidden] word
-    embedding). dW = dy^T @ x is accumulated in place into W's existing grad (one beta=1
-    GEMM) like LinearFn."""
+    embedding). dx = dy·W and dW += dyᵀ·x (beta=1 into W's grad) on the MFMA kernel."""
 
     @staticmethod
     def forward(ctx, x, w):
         ctx.save_for_backward(x)
         ctx.w = w
-        return torch.mm(x, w.t())
+        return gemm(GEMM_NT, x, w)
 
     @staticmethod
     def backward(ctx, dy):
         x, = ctx.saved_tensors
         w = ctx.w
-        dx = torch.mm(dy, w) if ctx.needs_input_grad[0] else None
+        if not dy.is_contiguous():
+            dy = dy.contiguous()
+        dx = gemm(GEMM_FWD, dy, w) if ctx.needs_input_grad[0] else None
         dw = None
         if ctx.needs_input_grad[1]:
             g = w.grad
-            if (g is not None and not torch.is_grad_enabled() and g.shape == w.shape
-                    and g.dtype == dy.dtype and g.is_contiguous()):
-                g.addmm_(dy.t(), x)
+            if _acc_grad_ok(g, w, dy.dtype):
+                gemm(GEMM_TN, dy, x, out=g, beta=1)
             else:
-                dw = torch.mm(dy.t(), x)
+                dw = gemm(GEMM_TN, dy, x)
         return dx, dw
 
 
@@ -768,7 +892,63 @@ def linear_nt(x2, w):
     if w.requires_grad and torch.is_grad_enabled() and w.is_leaf and x2.dtype == w.dtype and \
             not torch.is_autocast_enabled(x2.device.type):
         return LinearNTFn.apply(x2, w)
+    if x2.is_cuda and x2.dtype == w.dtype:
+        return gemm(GEMM_NT, x2, w)
     return torch.mm(x2, w.t())
+
+
+class MlpGeluFn(torch.autograd.Function):
+    """y = gelu(x·W1 + b1)·W2 (fc2 bias left to the caller's fused residual kernel).
+
+    Forward: ONE GEMM with bias+GELU in its epilogue that also stores the pre-activation Z, then
+    the fc2 GEMM. Backward: the fc2 dgrad GEMM applies gelu'(Z) in its epilogue and emits the
+    fc1 bias gradient as per-tile column sums, so no separate bias-GELU pass exists in either
+    direction; both weight gradients accumulate in place (beta=1)."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, approximate):
+        x2 = x.reshape(-1, x.shape[-1])
+        M, F = x2.shape[0], w1.shape[1]
+        z = torch.empty((M, F), device=x.device, dtype=x.dtype)
+        h = gemm(GEMM_FWD, x2, w1, bias=b1, z=z, epi='gelu_tanh' if approximate else 'gelu')
+        y = gemm(GEMM_FWD, h, w2)
+        ctx.save_for_backward(x, z, h)
+        ctx.w1, ctx.w2 = w1, w2
+        ctx.approximate = approximate
+        return y.view(*x.shape[:-1], w2.shape[1])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, z, h = ctx.saved_tensors
+        w1, w2 = ctx.w1, ctx.w2
+        dy2 = dy.reshape(-1, dy.shape[-1])
+        if not dy2.is_contiguous():
+            dy2 = dy2.contiguous()
+        x2 = x.reshape(-1, x.shape[-1])
+        dz, db1 = gemm(GEMM_NT, dy2, w2, z=z, epi='dgelu_tanh' if ctx.approximate else 'dgelu',
+                       want_colsum=True)
+        dw1 = dw2 = None
+        g2 = w2.grad
+        if _acc_grad_ok(g2, w2, dy2.dtype):
+            gemm(GEMM_TN, h, dy2, out=g2, beta=1)
+        else:
+            dw2 = gemm(GEMM_TN, h, dy2)
+        dx = gemm(GEMM_NT, dz, w1).view(x.shape)
+        g1 = w1.grad
+        if _acc_grad_ok(g1, w1, dz.dtype):
+            gemm(GEMM_TN, x2, dz, out=g1, beta=1)
+        else:
+            dw1 = gemm(GEMM_TN, x2, dz)
+        return dx, dw1, db1.to(dz.dtype), dw2, None
+
+
+def mlp_gelu(x, w1, b1, w2, approximate=True):
+    """gelu(x·W1 + b1)·W2 with the bias+GELU (and its backward) inside the GEMM epilogues."""
+    if all(t.requires_grad for t in (w1, b1, w2)) and torch.is_grad_enabled() and \
+            all(t.is_leaf for t in (w1, b1, w2)) and x.dtype == w1.dtype and x.is_cuda and \
+            not torch.is_autocast_enabled(x.device.type):
+        return MlpGeluFn.apply(x, w1, b1, w2, approximate)
+    return linear(bias_gelu(linear(x, w1), b1, approximate), w2)
 
 
 # =============================================================================

@@ -1,0 +1,105 @@
+"""LDS-DMA MFMA GEMM (ops/csrc/gemm_lds.hip) vs hipBLASLt (torch.mm) on the GPT-3 1.3B training
+GEMMs (M = 16 x 1024 tokens): correctness vs an fp32 reference, then interleaved timing rounds in
+one process (median of per-round means).
+
+    python scripts/gemm_lds_bench.py [--quick]
+"""
+import statistics
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, __import__('os').path.dirname(__import__('os').path.dirname(__import__('os').path.abspath(__file__))))
+from paddle_ray_amd.ops import _native  # noqa: E402
+
+L = _native.lib()
+T = 16384
+SHAPES = [  # (name, layout, M, N, K)
+    ('qkv.fwd', 0, T, 6144, 2048), ('out.fwd', 0, T, 2048, 2048), ('fc1.fwd', 0, T, 8192, 2048),
+    ('fc2.fwd', 0, T, 2048, 8192),
+    ('qkv.dgrad', 1, T, 2048, 6144), ('out.dgrad', 1, T, 2048, 2048), ('fc1.dgrad', 1, T, 2048, 8192),
+    ('fc2.dgrad', 1, T, 8192, 2048),
+    ('qkv.wgrad', 2, 2048, 6144, T), ('out.wgrad', 2, 2048, 2048, T), ('fc1.wgrad', 2, 2048, 8192, T),
+    ('fc2.wgrad', 2, 8192, 2048, T),
+    ('head.fwd', 1, T, 50304, 2048), ('head.dgrad', 0, T, 2048, 50304), ('head.wgrad', 2, 50304, 2048, T),
+]
+
+
+def operands(layout, M, N, K, dev):
+    g = torch.Generator(device=dev).manual_seed(M * 7 + N * 3 + K)
+    def r(*s):
+        return (torch.rand(*s, device=dev, generator=g) * 2 - 1).to(torch.bfloat16)
+    if layout == 0:
+        return r(M, K), r(K, N)
+    if layout == 1:
+        return r(M, K), r(N, K)
+    return r(K, M), r(K, N)
+
+
+def ref_mm(layout, a, b):
+    if layout == 0:
+        return torch.mm(a, b)
+    if layout == 1:
+        return torch.mm(a, b.t())
+    return torch.mm(a.t(), b)
+
+
+def ours(layout, a, b, c, M, N, K, bias=None, z=None, colsum=None, epi=0, beta=0):
+    from paddle_ray_amd.ops import fused as F
+    r = F._gemm_hip(layout, a, b, out=c)  # includes the split-K choice for small grids
+    assert r is not None
+
+
+def check(name, layout, M, N, K, dev):
+    a, b = operands(layout, M, N, K, dev)
+    c = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    ours(layout, a, b, c, M, N, K)
+    ref = ref_mm(layout, a.float(), b.float())
+    err = (c.float() - ref).abs().max().item()
+    scale = ref.abs().max().item()
+    return err / scale
+
+
+def timeit(fn, iters):
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters
+
+
+def main():
+    dev = torch.device('cuda')
+    quick = '--quick' in sys.argv
+    shapes = SHAPES[:1] + SHAPES[4:5] + SHAPES[8:9] if quick else SHAPES
+    print("| GEMM | layout | M | N | K | rel err | ours us | ours PF/s | hipBLASLt us | hipBLASLt PF/s | ratio |")
+    print("|---|---|---|---|---|---|---|---|---|---|---|", flush=True)
+    tot_o = tot_h = 0.0
+    for name, layout, M, N, K in shapes:
+        rel = check(name, layout, M, N, K, dev)
+        a, b = operands(layout, M, N, K, dev)
+        c = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        fo = lambda: ours(layout, a, b, c, M, N, K)  # noqa: E731
+        fh = lambda: ref_mm(layout, a, b)  # noqa: E731
+        for f in (fo, fh):
+            f()
+        torch.cuda.synchronize()
+        it = 5 if M * N * K > 1e12 else 20
+        to, th = [], []
+        for _ in range(5):
+            to.append(timeit(fo, it))
+            th.append(timeit(fh, it))
+        mo, mh = statistics.median(to), statistics.median(th)
+        fl = 2.0 * M * N * K
+        tot_o += mo
+        tot_h += mh
+        print(f"| {name} | {layout} | {M} | {N} | {K} | {rel:.1e} | {mo * 1e3:.1f} | {fl / mo / 1e12:.3f} | "
+              f"{mh * 1e3:.1f} | {fl / mh / 1e12:.3f} | {mh / mo:.3f} |", flush=True)
+    print(f"\ntotal ours {tot_o:.3f} ms, hipBLASLt {tot_h:.3f} ms")
+
+
+if __name__ == '__main__':
+    main()

@@ -1,0 +1,149 @@
+"""GPU numerics for the LDS-DMA MFMA GEMM (ops/csrc/gemm_lds.hip) against fp32 PyTorch references:
+every layout (x·W, dy·Wᵀ, xᵀ·dy), ragged M/N edges, bias / GELU / ReLU epilogues with the
+pre-activation output, dGELU + bias-gradient column sums, beta=1 accumulation, split-K, and the
+autograd wrappers (Linear, tied LM head, fused MLP) built on it."""
+import pytest
+import torch
+
+from paddle_ray_amd.ops import fused as K
+from paddle_ray_amd.ops import registry as R
+
+pytestmark = pytest.mark.gpu
+
+
+def _r(*s, scale=1.0):
+    return ((torch.rand(*s, device='cuda') * 2 - 1) * scale).to(torch.bfloat16)
+
+
+def _operands(layout, M, N, Kd):
+    if layout == K.GEMM_FWD:
+        return _r(M, Kd), _r(Kd, N)
+    if layout == K.GEMM_NT:
+        return _r(M, Kd), _r(N, Kd)
+    return _r(Kd, M), _r(Kd, N)
+
+
+def _ref(layout, a, b):
+    a, b = a.float(), b.float()
+    return a @ b if layout == K.GEMM_FWD else (a @ b.t() if layout == K.GEMM_NT else a.t() @ b)
+
+
+def _close(x, ref, tol=2e-2):
+    err = (x.float() - ref).abs().max().item()
+    assert err <= tol * max(ref.abs().max().item(), 1e-3), (err, ref.abs().max().item())
+
+
+@pytest.mark.parametrize('layout', [0, 1, 2])
+@pytest.mark.parametrize('M,N,Kd', [(512, 512, 256), (300, 264, 128), (1000, 776, 192), (256, 2048, 1024)])
+def test_layouts_and_edges(layout, M, N, Kd):
+    if layout == 2 and M % 8:
+        pytest.skip("wgrad needs M % 8 == 0")
+    torch.manual_seed(0)
+    a, b = _operands(layout, M, N, Kd)
+    y = K._gemm_hip(layout, a, b)
+    assert y is not None
+    _close(y, _ref(layout, a, b))
+
+
+@pytest.mark.parametrize('epi', ['gelu', 'gelu_tanh', 'relu'])
+def test_bias_act_epilogue_with_preact(epi):
+    torch.manual_seed(1)
+    a, b = _operands(0, 520, 392, 256)
+    bias = _r(392)
+    z = torch.empty(520, 392, device='cuda', dtype=torch.bfloat16)
+    y = K._gemm_hip(0, a, b, bias=bias, z=z, epi=epi)
+    pre = _ref(0, a, b) + bias.float()
+    _close(z, pre)
+    if epi == 'relu':
+        act = torch.relu(pre)
+    else:
+        act = torch.nn.functional.gelu(pre, approximate='tanh' if epi == 'gelu_tanh' else 'none')
+    _close(y, act)
+
+
+@pytest.mark.parametrize('epi', ['dgelu', 'dgelu_tanh'])
+def test_dgelu_epilogue_and_bias_grad(epi):
+    torch.manual_seed(2)
+    dy, w = _r(600, 384), _r(264, 384)          # dz = (dy · wᵀ) * gelu'(z): [600, 264]
+    z = _r(600, 264, scale=3.0)
+    out, cs = K._gemm_hip(1, dy, w, z=z, epi=epi, want_colsum=True)
+    zf = z.float().requires_grad_(True)
+    g = torch.nn.functional.gelu(zf, approximate='tanh' if epi == 'dgelu_tanh' else 'none')
+    ref, = torch.autograd.grad(g, zf, _ref(1, dy, w))
+    _close(out, ref)
+    _close(cs, out.float().sum(0), tol=1e-3)
+
+
+def test_beta_accumulate_and_split_k():
+    torch.manual_seed(3)
+    # 2048 x 2048 output with K = 16384: 64 tiles -> split-K path
+    a, b = _operands(2, 2048, 2048, 16384)
+    c0 = _r(2048, 2048)
+    c = c0.clone()
+    from paddle_ray_amd.ops import _native
+    assert _native.lib().gemm_lds_splits(2048, 2048, 16384) > 1
+    K._gemm_hip(2, a, b, out=c, beta=1)
+    _close(c, _ref(2, a, b) + c0.float())
+    # no split-K for a full grid; beta with the in-kernel epilogue
+    a, b = _operands(1, 1024, 512, 512)
+    c0 = _r(1024, 512)
+    c = c0.clone()
+    K._gemm_hip(1, a, b, out=c, beta=1)
+    _close(c, _ref(1, a, b) + c0.float())
+
+
+def test_linear_fn_grads():
+    torch.manual_seed(4)
+    x = _r(4, 128, 256).requires_grad_(True)
+    w = _r(256, 384).requires_grad_(True)
+    bias = _r(384).requires_grad_(True)
+    R.reset_stats()
+    y = K.linear(x, w, bias)
+    gy = _r(4, 128, 384)
+    y.backward(gy)
+    assert R.stats().get(('gemm', 'hip'), 0) >= 3 and ('gemm', 'fallback') not in R.stats()
+    xf, wf, bf = (t.detach().float().requires_grad_(True) for t in (x, w, bias))
+    yf = xf @ wf + bf
+    yf.backward(gy.float())
+    _close(y, yf)
+    _close(x.grad, xf.grad)
+    _close(w.grad, wf.grad)
+    _close(bias.grad, bf.grad)
+
+
+def test_linear_nt_head_grads():
+    torch.manual_seed(5)
+    h = _r(512, 256).requires_grad_(True)
+    e = _r(1000, 256).requires_grad_(True)     # vocab 1000 (ragged N)
+    e.grad = torch.zeros_like(e)               # dE accumulates in place (beta = 1)
+    with torch.no_grad():
+        e.grad.copy_(_r(1000, 256))
+    g0 = e.grad.clone()
+    y = K.linear_nt(h, e)
+    gy = _r(512, 1000)
+    y.backward(gy)
+    hf, ef = h.detach().float().requires_grad_(True), e.detach().float().requires_grad_(True)
+    (hf @ ef.t()).backward(gy.float())
+    _close(y, hf.detach() @ ef.detach().t())
+    _close(h.grad, hf.grad)
+    _close(e.grad, ef.grad + g0.float())
+
+
+@pytest.mark.parametrize('approx', [True, False])
+def test_mlp_gelu_fused(approx):
+    torch.manual_seed(6)
+    x = _r(2, 256, 256).requires_grad_(True)
+    w1, b1, w2 = _r(256, 1024).requires_grad_(True), _r(1024).requires_grad_(True), \
+        _r(1024, 256, scale=0.5).requires_grad_(True)
+    R.reset_stats()
+    y = K.mlp_gelu(x, w1, b1, w2, approx)
+    gy = _r(2, 256, 256)
+    y.backward(gy)
+    st = R.stats()
+    assert ('bias_gelu_fwd', 'hip') not in st and ('gemm', 'fallback') not in st
+    xf, w1f, b1f, w2f = (t.detach().float().requires_grad_(True) for t in (x, w1, b1, w2))
+    yf = torch.nn.functional.gelu(xf @ w1f + b1f, approximate='tanh' if approx else 'none') @ w2f
+    yf.backward(gy.float())
+    _close(y, yf)
+    for got, ref in ((x.grad, xf.grad), (w1.grad, w1f.grad), (b1.grad, b1f.grad), (w2.grad, w2f.grad)):
+        _close(got, ref, tol=3e-2)
