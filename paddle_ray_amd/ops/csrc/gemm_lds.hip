@@ -34,6 +34,7 @@
 // column partial sums written to `colsum` (the bias gradient, reduced by pra_colsum_partials);
 // `beta=1` accumulates into C (dW += xᵀ·dy straight into the flat gradient buffer).
 #include "common.h"
+#include <stdlib.h>
 
 namespace pra {
 namespace {
@@ -65,13 +66,17 @@ template <> __device__ __forceinline__ uint32_t pack2<f16>(float a, float b) {
 
 enum Epi : int { kNone = 0, kGeluErf = 1, kGeluTanh = 2, kRelu = 3, kDGeluErf = 4, kDGeluTanh = 5 };
 
+// tanh(u) = 1 - 2 / (exp(2u) + 1): one v_exp + one v_rcp (saturates cleanly at +-1)
+__device__ __forceinline__ float fast_tanh(float u) {
+  return 1.f - 2.f * __builtin_amdgcn_rcpf(__expf(2.f * u) + 1.f);
+}
 __device__ __forceinline__ float gelu_tanh(float x) {
   const float u = 0.79788456080286536f * (x + 0.044715f * x * x * x);
-  return 0.5f * x * (1.f + tanhf(u));
+  return 0.5f * x * (1.f + fast_tanh(u));
 }
 __device__ __forceinline__ float dgelu_tanh(float x) {
   const float u = 0.79788456080286536f * (x + 0.044715f * x * x * x);
-  const float t = tanhf(u);
+  const float t = fast_tanh(u);
   return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * 0.79788456080286536f * (1.f + 0.134145f * x * x);
 }
 __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
@@ -87,11 +92,23 @@ __device__ __forceinline__ float act(float x) {
   return x;
 }
 
-constexpr int BM = 256, BN = 256, BKT = 64, NT = 512;
+constexpr int BM = 256, BN = 256, BKT = 64;
 constexpr int IMG = BM * BKT * 2;       // 32 KB per operand image
 constexpr int SLOT = 2 * IMG;           // A image + B image
 constexpr int LDS_BYTES = 2 * SLOT + 128 * 4 * 4;  // double-buffered 128 KB (+2 KB: epilogue image pitch)
-constexpr int NDMA = IMG / (NT * 16);   // LDS-DMA instructions per thread per operand per K-step (4)
+
+// Wave layouts of the 256x256 tile: WR x WC waves, each (256/WR) x (256/WC) outputs.
+//   W8: 2 x 4 waves (128x64 each, 2 waves/SIMD, 32 accumulators)
+//   W4: 2 x 2 waves (128x128 each, 1 wave/SIMD, 64 accumulators in AGPRs): half the LDS
+//       fragment traffic per MFMA and half the waves meeting at each barrier.
+template <int WR_, int WC_>
+struct WCfg {
+  static constexpr int WR = WR_, WC = WC_, NT = 64 * WR_ * WC_;
+  static constexpr int TI = BM / WR_ / 16, TJ = BN / WC_ / 16;  // 16x16 MFMA tiles per wave
+  static constexpr int NDMA = IMG / (NT * 16);                   // glds per thread per operand per K-step
+};
+using W8 = WCfg<2, 4>;
+using W4 = WCfg<2, 2>;
 
 typedef short v4i16 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
@@ -110,7 +127,7 @@ __device__ __forceinline__ int kc_swz(int row) { return (row >> 1) & 7; }
 // whole 128-B lines of every row (BK = 64 bf16), so each L2 line is requested once.
 // KC image: position P (16-B chunk 0..2047) = row P>>3, slot P&7 holds global chunk (P&7)^kc_swz(row).
 // MC image: position P = k-row P>>5, slot P&31 holds global chunk (P&31)^mc_swz(k).
-template <bool KC>
+template <bool KC, int NT, int NDMA>
 struct Dma {
   uint32_t voff[NDMA];  // per-lane byte offsets of the chunks this thread stages
   uint64_t base;        // wave-uniform operand base (SGPRs); advanced per K-step
@@ -168,12 +185,14 @@ __device__ __forceinline__ typename V8<T>::type frag(const char* img, int r0, in
   }
 }
 
-template <typename T, bool AK, bool BK, int E, bool BETA, bool SPLIT>
-__global__ __launch_bounds__(NT, 1) void gemm_lds_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
+template <typename T, typename CF, bool AK, bool BK, int E, bool BETA, bool SPLIT>
+__global__ __launch_bounds__(CF::NT, 1) void gemm_lds_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
                                                           const uint16_t* __restrict__ bias, uint16_t* __restrict__ C,
                                                           uint16_t* __restrict__ Z, float* __restrict__ colsum,
                                                           int M, int N, int K, int lda, int ldb, int ldc, int ldz,
                                                           int splits, float* __restrict__ ws) {
+  constexpr int NT = CF::NT, TI = CF::TI, TJ = CF::TJ, NDMA = CF::NDMA, WC = CF::WC;
+  constexpr int RW = TI * 16, CW = TJ * 16;  // rows / columns per wave
   __shared__ __attribute__((aligned(1024))) char lds[LDS_BYTES];
   typedef typename V8<T>::type v8;
   const uint32_t lds_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)lds;
@@ -194,10 +213,10 @@ __global__ __launch_bounds__(NT, 1) void gemm_lds_kernel(const uint16_t* __restr
   const int tm = first_m + (pid % group) % gm, tn = (pid % group) / gm;
   const int m0 = tm * BM, n0 = tn * BN;
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wr = wave >> 2, wc = wave & 3;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wr = wave / WC, wc = wave % WC;
 
-  Dma<AK> da;
-  Dma<BK> db;
+  Dma<AK, NT, NDMA> da;
+  Dma<BK, NT, NDMA> db;
   if (AK) da.init(A, lda, m0, M - 1, tid); else da.init(A, lda, m0, M - 8, tid);
   if (BK) db.init(B, ldb, n0, N - 1, tid); else db.init(B, ldb, n0, N - 8, tid);
   int nk = K / BKT;
@@ -208,42 +227,46 @@ __global__ __launch_bounds__(NT, 1) void gemm_lds_kernel(const uint16_t* __restr
     db.base += (uint64_t)kb * db.step;
   }
 
-  f32x4 acc[8][4];
+  f32x4 acc[TI][TJ];
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < TI; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < TJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  v8 fa0[8], fb0[4], fa1[8], fb1[4];
-  auto read_frags = [&](v8 (&fa)[8], v8 (&fb)[4], int kt, int s) {
+  v8 fa0[TI], fb0[TJ], fa1[TI], fb1[TJ];
+  auto read_frags = [&](v8 (&fa)[TI], v8 (&fb)[TJ], int kt, int s) {
     const char* ai = lds + (kt & 1) * SLOT;
     const char* bi = ai + IMG;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) fb[j] = frag<T, BK>(bi, wc * 64 + j * 16, s, lane);
+    for (int j = 0; j < TJ; ++j) fb[j] = frag<T, BK>(bi, wc * CW + j * 16, s, lane);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) fa[i] = frag<T, AK>(ai, wr * 128 + i * 16, s, lane);
+    for (int i = 0; i < TI; ++i) fa[i] = frag<T, AK>(ai, wr * RW + i * 16, s, lane);
   };
   // 32 MFMAs of one k-half, interleaved segment by segment with (optionally) the fragment reads
   // of the next k-half and one LDS-DMA instruction of the next K-step every other segment, so
   // DMA issue and LDS reads hide under the wave's own matrix work.
-  auto half = [&](v8 (&ca)[8], v8 (&cb)[4], v8 (&na)[8], v8 (&nb)[4], bool rd, int rkt, int rs, bool dma,
+  auto half = [&](v8 (&ca)[TI], v8 (&cb)[TJ], v8 (&na)[TI], v8 (&nb)[TJ], bool rd, int rkt, int rs, bool dma,
                   int dkt) {
     const uint32_t so = lds_base + (dkt & 1) * SLOT;
     const char* ai = lds + (rkt & 1) * SLOT;
     const char* bi = ai + IMG;
+    constexpr int DPS = (2 * NDMA + TI - 1) / TI;  // DMA instructions per segment
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
+    for (int i = 0; i < TI; ++i) {
       if (dma) {
-        if (i < NDMA) da.issue1(so, wave, dkt, i);
-        else db.issue1(so + IMG, wave, dkt, i - NDMA);
+#pragma unroll
+        for (int d = i * DPS; d < (i + 1) * DPS && d < 2 * NDMA; ++d) {
+          if (d < NDMA) da.issue1(so, wave, dkt, d);
+          else db.issue1(so + IMG, wave, dkt, d - NDMA);
+        }
       }
       if (rd) {
-        if (i < 4) nb[i] = frag<T, BK>(bi, wc * 64 + i * 16, rs, lane);
-        na[i] = frag<T, AK>(ai, wr * 128 + i * 16, rs, lane);
+        if (i < TJ) nb[i] = frag<T, BK>(bi, wc * CW + i * 16, rs, lane);
+        na[i] = frag<T, AK>(ai, wr * RW + i * 16, rs, lane);
       }
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = mma<T>(cb[j], ca[i], acc[i][j]);
+      for (int j = 0; j < TJ; ++j) acc[i][j] = mma<T>(cb[j], ca[i], acc[i][j]);
       __builtin_amdgcn_s_setprio(0);
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -260,8 +283,12 @@ __global__ __launch_bounds__(NT, 1) void gemm_lds_kernel(const uint16_t* __restr
       for (int n = 0; n < NDMA; ++n) db.issue1(lds_base + t * SLOT + IMG, wave, t, n);
     }
   }
-  if (nk >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (nk >= 2) {
+    if (NDMA == 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
   read_frags(fa0, fb0, 0, 0);
@@ -276,7 +303,8 @@ __global__ __launch_bounds__(NT, 1) void gemm_lds_kernel(const uint16_t* __restr
     if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // step kt+1 landed (this wave)
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    half(fa1, fb1, fa0, fb0, kt + 1 < nk, kt + 1, 0, kt + 2 < nk, kt + 2);
+    // (non-split launches pass splits = 0 only for the PRA_GEMM_ABLATE=nodma timing ablation)
+    half(fa1, fb1, fa0, fb0, kt + 1 < nk, kt + 1, 0, kt + 2 < nk && (SPLIT || splits != 0), kt + 2);
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_waitcnt(0xC07F);  // (kt+1,0) fragments landed
   }
@@ -284,14 +312,14 @@ __global__ __launch_bounds__(NT, 1) void gemm_lds_kernel(const uint16_t* __restr
 
   if (SPLIT) {
     float* wsp = ws + (int64_t)split * M * N;
-    const int mrow = m0 + wr * 128 + (lane & 15);
-    const int ncol = n0 + wc * 64 + 4 * (lane >> 4);
+    const int mrow = m0 + wr * RW + (lane & 15);
+    const int ncol = n0 + wc * CW + 4 * (lane >> 4);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
+    for (int i = 0; i < TI; ++i) {
       const int m = mrow + i * 16;
       if (m >= M) continue;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < TJ; ++j) {
         const int n = ncol + j * 16;
         if (n < N)
           *reinterpret_cast<float4*>(wsp + (int64_t)m * N + n) =
@@ -309,7 +337,8 @@ __global__ __launch_bounds__(NT, 1) void gemm_lds_kernel(const uint16_t* __restr
   // acc[i][j][r] = C[m0 + wr*128 + i*16 + (lane&15)][n0 + wc*64 + j*16 + 4*(lane>>4) + r]
   float* img = reinterpret_cast<float*>(lds);
   constexpr int PITCH = BN + 4;  // floats
-  // this thread's output units: row u>>5 (+16 per q), 8 columns at (u&31)*8 (fixed per thread)
+  // this thread's output units: row tid>>5 (+RSTEP per q), 8 columns at (tid&31)*8 (fixed per thread)
+  constexpr int RSTEP = NT / 32, NQ = 128 / RSTEP;
   const int ucol = (tid & 31) * 8, urow = tid >> 5;
   const int n = n0 + ucol;
   const bool ncol_ok = n < N;  // N % 8 == 0: a unit is all-in or all-out
@@ -331,58 +360,75 @@ __global__ __launch_bounds__(NT, 1) void gemm_lds_kernel(const uint16_t* __restr
     __syncthreads();  // (h=0) every wave is done reading K-loop tiles; (h=1) half 0 streamed out
     if (wr == h) {
 #pragma unroll
-      for (int i = 0; i < 8; ++i)
+      for (int i = 0; i < TI; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int r = i * 16 + (lane & 15), c = wc * 64 + j * 16 + 4 * (lane >> 4);
+        for (int j = 0; j < TJ; ++j) {
+          const int r = i * 16 + (lane & 15), c = wc * CW + j * 16 + 4 * (lane >> 4);
           *reinterpret_cast<f32x4*>(img + r * PITCH + c) = acc[i][j];
         }
     }
     __syncthreads();
+    // NQ units per thread in batches of 4: every load of a batch (LDS image, Z / C) is issued
+    // before any of its math so the global-load latency is paid once per batch, not per unit
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const int rr = urow + 16 * q, m = m0 + h * 128 + rr;
-      if (m >= M || !ncol_ok) continue;
-      const f32x4 lo = *reinterpret_cast<const f32x4*>(img + rr * PITCH + ucol);
-      const f32x4 hi = *reinterpret_cast<const f32x4*>(img + rr * PITCH + ucol + 4);
-      float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    for (int bq = 0; bq < NQ; bq += 4) {
+      f32x4 lo[4], hi[4];
+      uint4 gz[4];
+      bool ok[4];
+      int64_t moff[4];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] += bv[e];
-      if (E == kDGeluErf || E == kDGeluTanh) {
-        const uint4 zz = *reinterpret_cast<const uint4*>(Z + (int64_t)m * ldz + n);
-        const uint32_t w4[4] = {zz.x, zz.y, zz.z, zz.w};
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float z0 = to_f<T>(w4[e] & 0xffff), z1 = to_f<T>(w4[e] >> 16);
-          v[2 * e] *= (E == kDGeluErf) ? dgelu_erf(z0) : dgelu_tanh(z0);
-          v[2 * e + 1] *= (E == kDGeluErf) ? dgelu_erf(z1) : dgelu_tanh(z1);
+      for (int u = 0; u < 4; ++u) {
+        const int rr = urow + RSTEP * (bq + u), m = m0 + h * 128 + rr;
+        ok[u] = m < M && ncol_ok;
+        moff[u] = (int64_t)(ok[u] ? m : 0);
+        lo[u] = *reinterpret_cast<const f32x4*>(img + rr * PITCH + ucol);
+        hi[u] = *reinterpret_cast<const f32x4*>(img + rr * PITCH + ucol + 4);
+        if (E == kDGeluErf || E == kDGeluTanh) {
+          if (ok[u]) gz[u] = *reinterpret_cast<const uint4*>(Z + moff[u] * ldz + n);
+        } else if (BETA) {
+          if (ok[u]) gz[u] = *reinterpret_cast<const uint4*>(C + moff[u] * ldc + n);
         }
-      } else if (E != kNone) {
-        if (Z) {
-          uint4 o;
-          o.x = pack2<T>(v[0], v[1]); o.y = pack2<T>(v[2], v[3]);
-          o.z = pack2<T>(v[4], v[5]); o.w = pack2<T>(v[6], v[7]);
-          *reinterpret_cast<uint4*>(Z + (int64_t)m * ldz + n) = o;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (!ok[u]) continue;
+        const int64_t m = moff[u];
+        float v[8] = {lo[u][0], lo[u][1], lo[u][2], lo[u][3], hi[u][0], hi[u][1], hi[u][2], hi[u][3]};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += bv[e];
+        if (E == kDGeluErf || E == kDGeluTanh) {
+          const uint32_t w4[4] = {gz[u].x, gz[u].y, gz[u].z, gz[u].w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float z0 = to_f<T>(w4[e] & 0xffff), z1 = to_f<T>(w4[e] >> 16);
+            v[2 * e] *= (E == kDGeluErf) ? dgelu_erf(z0) : dgelu_tanh(z0);
+            v[2 * e + 1] *= (E == kDGeluErf) ? dgelu_erf(z1) : dgelu_tanh(z1);
+          }
+        } else if (E != kNone) {
+          if (Z) {
+            uint4 o;
+            o.x = pack2<T>(v[0], v[1]); o.y = pack2<T>(v[2], v[3]);
+            o.z = pack2<T>(v[4], v[5]); o.w = pack2<T>(v[6], v[7]);
+            *reinterpret_cast<uint4*>(Z + m * ldz + n) = o;
+          }
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = act<E>(v[e]);
         }
+        if (BETA && !(E == kDGeluErf || E == kDGeluTanh)) {
+          const uint32_t w4[4] = {gz[u].x, gz[u].y, gz[u].z, gz[u].w};
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = act<E>(v[e]);
-      }
-      uint16_t* cp = C + (int64_t)m * ldc + n;
-      if (BETA) {
-        const uint4 cc = *reinterpret_cast<const uint4*>(cp);
-        const uint32_t w4[4] = {cc.x, cc.y, cc.z, cc.w};
+          for (int e = 0; e < 4; ++e) { v[2 * e] += to_f<T>(w4[e] & 0xffff); v[2 * e + 1] += to_f<T>(w4[e] >> 16); }
+        }
+        uint4 o;
+        o.x = pack2<T>(v[0], v[1]); o.y = pack2<T>(v[2], v[3]);
+        o.z = pack2<T>(v[4], v[5]); o.w = pack2<T>(v[6], v[7]);
+        *reinterpret_cast<uint4*>(C + m * ldc + n) = o;
+        if (colsum) {
+          // the bias gradient sums the ROUNDED output (what a separate reduction would read)
+          const uint32_t w4[4] = {o.x, o.y, o.z, o.w};
 #pragma unroll
-        for (int e = 0; e < 4; ++e) { v[2 * e] += to_f<T>(w4[e] & 0xffff); v[2 * e + 1] += to_f<T>(w4[e] >> 16); }
-      }
-      uint4 o;
-      o.x = pack2<T>(v[0], v[1]); o.y = pack2<T>(v[2], v[3]);
-      o.z = pack2<T>(v[4], v[5]); o.w = pack2<T>(v[6], v[7]);
-      *reinterpret_cast<uint4*>(cp) = o;
-      if (colsum) {
-        // the bias gradient sums the ROUNDED output (what a separate reduction would read)
-        const uint32_t w4[4] = {o.x, o.y, o.z, o.w};
-#pragma unroll
-        for (int e = 0; e < 4; ++e) { cs[2 * e] += to_f<T>(w4[e] & 0xffff); cs[2 * e + 1] += to_f<T>(w4[e] >> 16); }
+          for (int e = 0; e < 4; ++e) { cs[2 * e] += to_f<T>(w4[e] & 0xffff); cs[2 * e + 1] += to_f<T>(w4[e] >> 16); }
+        }
       }
     }
   }
@@ -399,7 +445,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_lds_kernel(const uint16_t* __restr
     if (tid < 256) {
       float t = 0.f;
 #pragma unroll
-      for (int w = 0; w < 8; ++w) t += img[w * 256 + tid];
+      for (int w = 0; w < NT / 64; ++w) t += img[w * 256 + tid];
       const int nn = n0 + tid;
       if (nn < N) colsum[(int64_t)tm * N + nn] = t;
     }
@@ -465,21 +511,25 @@ void launch_e(const void* A, const void* B, const void* bias, void* C, void* Z, 
   auto pbias = static_cast<const uint16_t*>(bias);
   auto pc = static_cast<uint16_t*>(C);
   auto pz = static_cast<uint16_t*>(Z);
+  // W4 (1 wave/SIMD, 128x128 per wave) measured 12-45 % slower than W8 on every GPT-1.3B shape
+  // (profiles/r2_gemm/summary.md); it stays a compile-time option, not instantiated.
+  constexpr bool four = false;
+  static const int ablate = getenv("PRA_GEMM_ABLATE") ? 0 : 1;  // 0: no DMA after the prologue (timing only)
   if (splits > 1) {
-    gemm_lds_kernel<T, AK, BK, kNone, false, true><<<tiles * splits, NT, 0, s>>>(
-        pa, pb, nullptr, nullptr, nullptr, nullptr, M, N, K, lda, ldb, ldc, ldz, splits, ws);
+    gemm_lds_kernel<T, W8, AK, BK, kNone, false, true><<<tiles * splits, W8::NT, 0, s>>>(
+          pa, pb, nullptr, nullptr, nullptr, nullptr, M, N, K, lda, ldb, ldc, ldz, splits, ws);
     const int64_t quads = (int64_t)M * N / 4;
     const int blocks = (int)((quads + 255) / 256);
     if (beta) splitk_reduce_k<T, E, true><<<blocks, 256, 0, s>>>(ws, splits, pbias, pc, pz, M, N, ldc, ldz);
     else splitk_reduce_k<T, E, false><<<blocks, 256, 0, s>>>(ws, splits, pbias, pc, pz, M, N, ldc, ldz);
     return;
   }
-  if (beta)
-    gemm_lds_kernel<T, AK, BK, E, true, false><<<tiles, NT, 0, s>>>(pa, pb, pbias, pc, pz, colsum, M, N, K, lda, ldb,
-                                                                    ldc, ldz, 1, nullptr);
-  else
-    gemm_lds_kernel<T, AK, BK, E, false, false><<<tiles, NT, 0, s>>>(pa, pb, pbias, pc, pz, colsum, M, N, K, lda, ldb,
-                                                                     ldc, ldz, 1, nullptr);
+#define PRA_GEMM_LAUNCH(CFG, BETA_)                                                                         \
+  gemm_lds_kernel<T, CFG, AK, BK, E, BETA_, false><<<tiles, CFG::NT, 0, s>>>(pa, pb, pbias, pc, pz, colsum, M, N, K, \
+                                                                           lda, ldb, ldc, ldz, ablate, nullptr)
+  (void)four;
+  if (beta) PRA_GEMM_LAUNCH(W8, true); else PRA_GEMM_LAUNCH(W8, false);
+#undef PRA_GEMM_LAUNCH
 }
 
 template <typename T, bool AK, bool BK>

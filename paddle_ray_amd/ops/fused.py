@@ -690,7 +690,11 @@ def flash_attention(q, k, v, causal=False, scale=None):
 # =============================================================================
 GEMM_FWD, GEMM_NT, GEMM_TN = 0, 1, 2  # x·W, dy·Wᵀ (or h·Eᵀ), xᵀ·dy
 EPI = {None: 0, 'gelu': 1, 'gelu_tanh': 2, 'relu': 3, 'dgelu': 4, 'dgelu_tanh': 5}
-_GEMM_MODE = __import__('os').environ.get('PRA_GEMM', 'mfma')  # 'blas' = hipBLASLt A/B baseline
+# PRA_GEMM: 'auto' (default) = the in-tree MFMA kernel for every layout/epilogue where it measured
+# at or above hipBLASLt on MI355X (forward x·W incl. the fused bias+GELU epilogue, wgrad xᵀ·dy with
+# beta=1 accumulation), hipBLASLt for the dgrad dy·Wᵀ layout where it is still faster
+# (profiles/r2_gemm/summary.md); 'mfma' = in-tree kernel everywhere; 'blas' = hipBLASLt everywhere.
+_GEMM_MODE = __import__('os').environ.get('PRA_GEMM', 'auto')
 
 
 def _gemm_operand_ok(t):
@@ -732,6 +736,8 @@ def _gemm_hip(layout, a, b, out=None, bias=None, z=None, epi=None, beta=0, want_
     """One MFMA GEMM launch (+ split-K reduce when the tile grid would leave CUs idle).
     Returns None when the shape/layout is outside what the kernel assumes (caller falls back)."""
     if _GEMM_MODE == 'blas' or not (_gemm_operand_ok(a) and _gemm_operand_ok(b)) or a.dtype != b.dtype:
+        return None
+    if _GEMM_MODE == 'auto' and layout == GEMM_NT:
         return None
     if layout == GEMM_FWD:
         M, K = a.shape
@@ -778,7 +784,7 @@ def gemm(layout, a, b, out=None, bias=None, z=None, epi=None, beta=0, want_colsu
         r = _gemm_hip(layout, a, b, out, bias, z, epi, beta, want_colsum)
         if r is not None:
             return r
-        R._STATS[('gemm', 'fallback')] += 1
+        R._STATS[('gemm', 'hipblaslt' if _GEMM_MODE == 'auto' and layout == GEMM_NT else 'fallback')] += 1
     return _gemm_ref_fast(layout, a, b, out, bias, z, epi, beta, want_colsum)
 
 
@@ -925,8 +931,13 @@ class MlpGeluFn(torch.autograd.Function):
         if not dy2.is_contiguous():
             dy2 = dy2.contiguous()
         x2 = x.reshape(-1, x.shape[-1])
-        dz, db1 = gemm(GEMM_NT, dy2, w2, z=z, epi='dgelu_tanh' if ctx.approximate else 'dgelu',
-                       want_colsum=True)
+        if _GEMM_MODE == 'auto':
+            # dgrad on hipBLASLt, then ONE fused pass for gelu'(z) and the bias gradient
+            dh = torch.mm(dy2, w2.t())
+            dz, db1 = _dgelu_db(dh, z, ctx.approximate)
+        else:
+            dz, db1 = gemm(GEMM_NT, dy2, w2, z=z, epi='dgelu_tanh' if ctx.approximate else 'dgelu',
+                           want_colsum=True)
         dw1 = dw2 = None
         g2 = w2.grad
         if _acc_grad_ok(g2, w2, dy2.dtype):
@@ -940,6 +951,21 @@ class MlpGeluFn(torch.autograd.Function):
         else:
             dw1 = gemm(GEMM_TN, x2, dz)
         return dx, dw1, db1.to(dz.dtype), dw2, None
+
+
+def _dgelu_db(dh, z, approximate):
+    """dz = dh * gelu'(z) and db = colsum(dz) in one pass (bias_gelu_bwd_db kernel, zero bias)."""
+    rows, cols = z.shape
+    L = _native.lib()
+    nrb = max(1, min(256, rows // 16))
+    part = torch.empty((nrb, cols), device=z.device, dtype=torch.float32)
+    dz = torch.empty_like(z)
+    zero_b = torch.zeros(cols, device=z.device, dtype=z.dtype)
+    L.bias_gelu_bwd_db(_ptr(dh), _ptr(z), _ptr(zero_b), _ptr(dz), _ptr(part), rows, cols, nrb, _dt(z),
+                       int(approximate), _stream())
+    db = torch.empty(cols, device=z.device, dtype=torch.float32)
+    L.colsum16(_ptr(part), _ptr(db), nrb, cols, 0, _stream())
+    return dz, db
 
 
 def mlp_gelu(x, w1, b1, w2, approximate=True):

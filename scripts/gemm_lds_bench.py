@@ -101,5 +101,47 @@ def main():
     print(f"\ntotal ours {tot_o:.3f} ms, hipBLASLt {tot_h:.3f} ms")
 
 
-if __name__ == '__main__':
+if __name__ == '__main__' and '--fused' not in sys.argv:
     main()
+
+
+def fused_main():
+    """fc1 forward with bias+GELU(+pre-act) epilogue and fc2 dgrad with dGELU + bias-grad epilogue
+    vs hipBLASLt GEMM + the separate bias-GELU kernels they replace."""
+    from paddle_ray_amd.ops import fused as F
+    dev = torch.device('cuda')
+    x, w1 = operands(0, T, 8192, 2048, dev)
+    b1 = (torch.rand(8192, device=dev) - 0.5).to(torch.bfloat16)
+    z = torch.empty(T, 8192, device=dev, dtype=torch.bfloat16)
+    dy, w2t = operands(1, T, 8192, 2048, dev)  # dy [T, 2048], W2 [8192, 2048] as [N][K]
+
+    def ours_fwd():
+        F._gemm_hip(0, x, w1, bias=b1, z=z, epi='gelu_tanh')
+
+    def blas_fwd():
+        F.bias_gelu(torch.mm(x, w1), b1, True)
+
+    def ours_bwd():
+        F._gemm_hip(1, dy, w2t, z=z, epi='dgelu_tanh', want_colsum=True)
+
+    zz = z.clone().requires_grad_(False)
+
+    def blas_bwd():
+        dh = torch.mm(dy, w2t.t())
+        F.BiasGeluFn.backward(type('C', (), {'saved_tensors': (zz, b1), 'needs_input_grad': (True, True, False),
+                                             'approximate': True, 'shp': zz.shape})(), dh)
+
+    print("\n| fused op | ours us | hipBLASLt + separate kernel us | ratio |\n|---|---|---|---|")
+    for name, fo, fh in (('fc1 fwd +bias+GELU+Z', ours_fwd, blas_fwd), ('fc2 dgrad +dGELU+db', ours_bwd, blas_bwd)):
+        fo(); fh()
+        torch.cuda.synchronize()
+        to, th = [], []
+        for _ in range(5):
+            to.append(timeit(fo, 10))
+            th.append(timeit(fh, 10))
+        mo, mh = statistics.median(to), statistics.median(th)
+        print(f"| {name} | {mo * 1e3:.1f} | {mh * 1e3:.1f} | {mh / mo:.3f} |", flush=True)
+
+
+if __name__ == '__main__' and '--fused' in sys.argv:
+    fused_main()

@@ -11,6 +11,15 @@ from paddle_ray_amd.ops import registry as R
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True)
+def _mfma_everywhere():
+    """Exercise the in-tree kernel on every layout regardless of the 'auto' policy."""
+    prev = K._GEMM_MODE
+    K._GEMM_MODE = 'mfma'
+    yield
+    K._GEMM_MODE = prev
+
+
 def _r(*s, scale=1.0):
     return ((torch.rand(*s, device='cuda') * 2 - 1) * scale).to(torch.bfloat16)
 
@@ -129,8 +138,10 @@ def test_linear_nt_head_grads():
     _close(e.grad, ef.grad + g0.float())
 
 
+@pytest.mark.parametrize('mode', ['mfma', 'auto'])
 @pytest.mark.parametrize('approx', [True, False])
-def test_mlp_gelu_fused(approx):
+def test_mlp_gelu_fused(approx, mode):
+    K._GEMM_MODE = mode
     torch.manual_seed(6)
     x = _r(2, 256, 256).requires_grad_(True)
     w1, b1, w2 = _r(256, 1024).requires_grad_(True), _r(1024).requires_grad_(True), \
