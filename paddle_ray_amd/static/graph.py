@@ -10,12 +10,24 @@ argument template); output shapes/dtypes are inferred by running the very same o
 program through the same kernel registry (HIP kernels / hipBLASLt / MIOpen) in the
 order chosen by the native C++ scheduler (``native/src/graph_scheduler.cpp``:
 dependency DAG, dead-op pruning against the fetch list, last-use GC points), with
-optional HIP-graph capture of the whole replay for static shapes. Training programs
-carry ``backward`` / ``optimize`` ops appended by ``minimize``; the backward runs on the
-eager autograd tape built during the replay.
+optional HIP-graph capture of the whole replay for static shapes.
+
+Backward is part of the IR (parity: python/paddle/fluid/backward.py:1826 append_backward):
+``append_backward`` walks the forward ops in reverse and emits one ``<type>_grad`` OpDesc
+per differentiable op (reading the forward op's saved context var and its output grads,
+writing its input / parameter grads), ``sum`` ops where a var or parameter feeds several
+ops, and a ``fill_grad_seed`` op for the loss. At replay each forward op that has a grad op
+runs on leaf copies of its inputs and keeps its OWN small autograd graph in the context
+var; its grad op differentiates exactly that graph (torch.autograd.grad), so dropout masks
+and AMP casts match the forward. ``optimize`` consumes the ``param@GRAD`` vars. Forward +
+backward of a training program can be captured as ONE HIP graph
+(``BuildStrategy.use_hip_graph``); the optimizer step runs after the replay.
+
+Serialized programs (``.pdmodel``) name ops only by their registered op type; loading
+resolves names through the static op table and refuses anything else.
 """
+import collections
 import contextlib
-import importlib
 import itertools
 import json
 import os
@@ -107,12 +119,22 @@ class _VarRef:
 
 
 class OpDesc:
-    def __init__(self, type, fn, args, kwargs, in_vids, out_vids, out_template):
+    """One op of a Block (parity: framework.proto OpDesc: type, inputs, outputs, attrs).
+
+    ``role`` is 'forward', 'backward' (grad / sum / seed ops from append_backward) or
+    'optimize'; a forward op that has a grad op also writes a context var ``ctx_vid``."""
+
+    def __init__(self, type, fn, args, kwargs, in_vids, out_vids, out_template, role='forward'):
         self.type, self.fn = type, fn
         self.args, self.kwargs = args, kwargs
         self.in_vids, self.out_vids = in_vids, out_vids
         self.out_template = out_template
         self.attrs = {}
+        self.role = role
+        self.ctx_vid = None
+
+    def all_outputs(self):
+        return self.out_vids + ([self.ctx_vid] if self.ctx_vid is not None else [])
 
     def __repr__(self):
         return f'{{Out={self.out_vids}}} = {self.type}(inputs={self.in_vids})'
@@ -181,11 +203,14 @@ class Program:
         p = Program()
         ops = []
         for op in self.global_block().ops:
-            if for_test and op.type in ('backward', 'optimize'):
+            if for_test and op.role != 'forward':
                 continue
-            if for_test and isinstance(op.kwargs, dict) and op.kwargs.get('training') is True:
-                op = OpDesc(op.type, op.fn, op.args, dict(op.kwargs, training=False),
-                            op.in_vids, op.out_vids, op.out_template)
+            if for_test:
+                kw = dict(op.kwargs, training=False) if isinstance(op.kwargs, dict) and \
+                    op.kwargs.get('training') is True else op.kwargs
+                nop = OpDesc(op.type, op.fn, op.args, kw, op.in_vids, op.out_vids, op.out_template)
+                nop.attrs = dict(op.attrs)
+                op = nop
             ops.append(op)
         p.blocks[0].ops = ops
         p.blocks[0].vars = dict(self.global_block().vars)
@@ -384,6 +409,8 @@ def record_op(op_type, fn, args, kwargs):
         blk.vars[v.vid] = v
         out_vars.append(v)
     op = OpDesc(op_type, fn, targs, tkw, in_vids, [v.vid for v in out_vars], tmpl)
+    op.attrs['params'] = [p for p in params if isinstance(p, Parameter)]
+    _record_amp(op)
     for v in out_vars:
         v.__dict__['op'] = op
     blk.ops.append(op)
@@ -391,8 +418,27 @@ def record_op(op_type, fn, args, kwargs):
     return _rebuild(tmpl, iter(out_vars))
 
 
+def _record_amp(op):
+    """Ops recorded inside ``paddle.amp.auto_cast`` replay under the same AMP policy."""
+    from ..amp import amp_state
+    st = amp_state()
+    if st['enabled']:
+        op.attrs['amp'] = {'dtype': st['dtype'], 'level': st['level'], 'white': set(st['white']),
+                           'black': set(st['black'])}
+
+
+_OP_TABLE = {}  # op type -> eager function (the only things a .pdmodel may name)
+
+
+def register_static_op(name, fn):
+    _OP_TABLE[name] = fn
+    return fn
+
+
 def static_op(name, fn):
     """Wrap an eager API function so that it records when given static Variables."""
+    register_static_op(name, fn)
+
     def wrapper(*args, **kwargs):
         if _STATIC[0] and (_has_var(args) or _has_var(kwargs)):
             return record_op(name, fn, args, kwargs)
@@ -417,41 +463,177 @@ def _op_binary(name):
 
 
 # =============================================================================
-# backward / optimize markers
+# backward: grad OpDescs (parity: python/paddle/fluid/backward.py append_backward :1826,
+# gradients; paddle/fluid/framework grad op makers)
 # =============================================================================
-def _backward_fn(loss):
-    loss.backward()
-    return None
+class _Ctx:
+    """A forward op's saved autograd context (its leaf inputs, parameters and outputs)."""
+    __slots__ = ('leaves', 'params', 'outs')
+
+    def __init__(self, leaves, params, outs):
+        self.leaves, self.params, self.outs = leaves, params, outs
 
 
-def _optimize_fn(opt):
-    opt.step()
-    opt.clear_grad()
-    return None
+def _vjp(ctx, *out_grads):
+    """Generic grad kernel: differentiate the forward op's own graph."""
+    targets = list(ctx.leaves) + list(ctx.params)
+    pairs = [(o, g) for o, g in zip(ctx.outs, out_grads)
+             if g is not None and isinstance(o, torch.Tensor) and o.requires_grad]
+    if pairs:
+        gs = torch.autograd.grad([o for o, _ in pairs], targets,
+                                 [(_u(g) if isinstance(g, Tensor) else g).to(o.dtype) for o, g in pairs],
+                                 allow_unused=True)
+    else:
+        gs = [None] * len(targets)
+    ctx.outs = ()  # the graph is consumed: free it
+    return [Tensor(g if g is not None else torch.zeros_like(t)) for g, t in zip(gs, targets)]
+
+
+def _sum_grads(*gs):
+    t = _u(gs[0])
+    for g in gs[1:]:
+        t = t + _u(g).to(t.dtype)
+    return Tensor(t)
+
+
+def _seed(target, scale=1.0):
+    return Tensor(torch.full_like(_u(target), float(scale)))
+
+
+for _n, _f in (('grad', _vjp), ('sum', _sum_grads), ('fill_grad_seed', _seed)):
+    register_static_op(_n, _f)
+
+
+def _new_var(blk, like_shape, dtype, name=None):
+    v = Variable(blk, like_shape, dtype, name=name, stop_gradient=False)
+    blk.vars[v.vid] = v
+    return v
+
+
+def _build_backward(prog, targets, inputs=(), target_grads=None, no_grad_set=None,
+                    params=None, loss_scale=1.0):
+    """Emit grad ops for ``targets`` w.r.t. ``inputs`` (Variables) and the trainable
+    parameters. Returns ({input vid: grad var}, {param name: grad var})."""
+    blk = prog.global_block()
+    no_grad = {getattr(x, 'name', x) for x in (no_grad_set or ())}
+    fwd = [op for op in blk.ops if op.role == 'forward']
+    req = {v.vid for v in blk.vars.values() if v.is_data and not v.stop_gradient}
+    req |= {x.vid for x in inputs}
+    allowed = None if params is None else {id(p) for p in params}
+
+    def diff_params(op):
+        return [p for p in op.attrs.get('params', [])
+                if not p.stop_gradient and p.name not in no_grad and
+                (allowed is None or id(p) in allowed)]
+    for op in fwd:
+        if any(i in req for i in op.in_vids) or diff_params(op):
+            for o in op.out_vids:
+                v = blk.vars.get(o)
+                if v is not None and (v.dtype.is_floating_point or v.dtype.is_complex):
+                    req.add(o)
+    needed = {t.vid for t in targets}
+    path = []
+    for op in reversed(fwd):
+        if any(o in needed for o in op.out_vids) and \
+                (any(i in req for i in op.in_vids) or diff_params(op)):
+            path.append(op)
+            needed.update(i for i in op.in_vids if i in req)
+    partial = {}
+    final = {}
+
+    def add_partial(key, gv):
+        partial.setdefault(key, []).append(gv)
+
+    def final_grad(key, name=None):
+        if key in final:
+            return final[key]
+        gs = partial.get(key, [])
+        if not gs:
+            final[key] = None
+        elif len(gs) == 1:
+            final[key] = gs[0]
+        else:
+            ref = blk.vars[gs[0]]
+            out = _new_var(blk, ref.shape, ref.dtype, name)
+            blk.ops.append(OpDesc('sum', _sum_grads, [_VarRef(g) for g in gs], {}, list(gs),
+                                  [out.vid], 'T', role='backward'))
+            final[key] = out.vid
+        return final[key]
+
+    for i, t in enumerate(targets):
+        if target_grads is not None and i < len(target_grads) and target_grads[i] is not None:
+            add_partial(t.vid, target_grads[i].vid)
+            continue
+        g = _new_var(blk, t.shape, t.dtype, t.name + '@GRAD')
+        blk.ops.append(OpDesc('fill_grad_seed', _seed, [_VarRef(t.vid), loss_scale], {},
+                              [t.vid], [g.vid], 'T', role='backward'))
+        add_partial(t.vid, g.vid)
+    for op in path:
+        ogs = [final_grad(o) for o in op.out_vids]
+        if all(g is None for g in ogs):
+            continue
+        diff_in = []
+        for i in op.in_vids:
+            if i in req and i not in diff_in:
+                diff_in.append(i)
+        dps = diff_params(op)
+        if not diff_in and not dps:
+            continue
+        if op.ctx_vid is None:
+            cv = Variable(blk, [], 'float32', name=f'{op.type}@CTX')
+            blk.vars[cv.vid] = cv
+            op.ctx_vid = cv.vid
+        op.attrs['diff_in'] = diff_in
+        op.attrs['diff_params'] = dps
+        outs = []
+        for i in diff_in:
+            v = blk.vars[i]
+            outs.append(_new_var(blk, v.shape, v.dtype).vid)
+        for p in dps:
+            outs.append(_new_var(blk, list(_u(p).shape), _u(p).dtype).vid)
+        args = [_VarRef(op.ctx_vid)] + [None if g is None else _VarRef(g) for g in ogs]
+        gop = OpDesc(op.type + '_grad', _vjp, args, {},
+                     [op.ctx_vid] + [g for g in ogs if g is not None], outs,
+                     ('list', ['T'] * len(outs)), role='backward')
+        gop.attrs['fwd'] = op
+        if 'amp' in op.attrs:
+            gop.attrs['amp'] = op.attrs['amp']
+        blk.ops.append(gop)
+        for i, gv in zip(diff_in, outs[:len(diff_in)]):
+            add_partial(i, gv)
+        for p, gv in zip(dps, outs[len(diff_in):]):
+            add_partial(('param', p.name), gv)
+            prog._register_param(p)
+    in_grads = {x.vid: final_grad(x.vid, x.name + '@GRAD') for x in inputs}
+    p_grads = {}
+    for key in list(partial):
+        if isinstance(key, tuple) and key[0] == 'param':
+            p_grads[key[1]] = final_grad(key, key[1] + '@GRAD')
+    prog._bump()
+    return in_grads, p_grads
 
 
 def append_backward(loss, parameter_list=None, no_grad_set=None, callbacks=None,
-                    checkpoints=None):
+                    checkpoints=None, loss_scale=1.0):
+    """Append grad ops for ``loss``; returns [(param, param@GRAD var)]."""
     prog = loss.block.program
     blk = prog.global_block()
-    blk.ops.append(OpDesc('backward', _backward_fn, [_VarRef(loss.vid)], {}, [loss.vid], [],
-                          'C'))
-    prog._bump()
-    params = parameter_list or [p for p in prog.all_parameters() if not p.stop_gradient]
-    params = [prog._params[p] if isinstance(p, str) else p for p in params]
+    params = None
+    if parameter_list:
+        params = [prog._params[p] if isinstance(p, str) else p for p in parameter_list]
+    _, p_grads = _build_backward(prog, [loss], no_grad_set=no_grad_set, params=params,
+                                 loss_scale=loss_scale)
     out = []
-    for p in params:
-        g = GradVar(blk, p)
-        blk.vars[g.vid] = g
+    for name, gvid in p_grads.items():
+        if gvid is None:
+            continue
+        p = prog._params[name]
+        g = blk.vars[gvid]
+        g.name = name + '@GRAD'
+        g.__dict__['param'] = p
         out.append((p, g))
+    prog.__dict__['_param_grads'] = {id(p): g for p, g in out}
     return out
-
-
-def _grad_fn(targets, inputs):
-    ts = [_u(t) for t in targets]
-    xs = [_u(i) for i in inputs]
-    gs = torch.autograd.grad(ts, xs, allow_unused=True, retain_graph=True)
-    return [Tensor(g) if g is not None else Tensor(torch.zeros_like(x)) for g, x in zip(gs, xs)]
 
 
 def gradients(targets, inputs, target_gradients=None, no_grad_set=None):
@@ -459,29 +641,54 @@ def gradients(targets, inputs, target_gradients=None, no_grad_set=None):
     inputs = inputs if isinstance(inputs, (list, tuple)) else [inputs]
     prog = default_main_program()
     blk = prog.global_block()
-    in_vids = []
-    targs = _template((list(targets), list(inputs)), in_vids, [])
+    tg = None if target_gradients is None else (
+        target_gradients if isinstance(target_gradients, (list, tuple)) else [target_gradients])
+    in_grads, _ = _build_backward(prog, list(targets), inputs=list(inputs), target_grads=tg,
+                                  no_grad_set=no_grad_set, params=[])
     outs = []
     for x in inputs:
-        g = Variable(blk, x.shape, x.dtype, name=x.name + '@GRAD', stop_gradient=False)
-        blk.vars[g.vid] = g
-        outs.append(g)
-    op = OpDesc('gradients', _grad_fn, list(targs), {}, in_vids, [g.vid for g in outs],
-                ('list', ['T'] * len(outs)))
-    blk.ops.append(op)
+        gv = in_grads.get(x.vid)
+        if gv is None:  # no path: a zeros op keeps the fetch valid
+            g = _new_var(blk, x.shape, x.dtype, x.name + '@GRAD')
+            blk.ops.append(OpDesc('fill_grad_seed', _seed, [_VarRef(x.vid), 0.0], {}, [x.vid],
+                                  [g.vid], 'T', role='backward'))
+            outs.append(g)
+        else:
+            outs.append(blk.vars[gv])
     prog._bump()
     return outs
 
 
-def _static_minimize(opt, loss, parameters=None):
+def _optimize_fn(opt, params, *grads, scaler=None):
+    """Apply ``param@GRAD`` vars through the eager optimizer (fused multi-tensor kernels)."""
+    for p, g in zip(params, grads):
+        gt = _u(g)
+        p._t.grad = gt.to(p._t.dtype) if gt.dtype != p._t.dtype else gt
+    if scaler is not None:
+        scaler.step(opt)
+        scaler.update()
+    else:
+        opt.step()
+    opt.clear_grad(set_to_zero=False)
+    return None
+
+
+register_static_op('optimize', _optimize_fn)
+
+
+def _static_minimize(opt, loss, parameters=None, scaler=None, loss_scale=1.0):
     prog = loss.block.program
     if not opt._parameter_list:
         ps = parameters or [p for p in prog.all_parameters() if not p.stop_gradient]
         opt._param_groups = []
         opt._add_param_group({'params': list(ps)})
-    pg = append_backward(loss, parameters)
+    pg = append_backward(loss, parameters, loss_scale=loss_scale)
     blk = prog.global_block()
-    blk.ops.append(OpDesc('optimize', _optimize_fn, [opt], {}, [], [], 'C'))
+    params = [p for p, _ in pg]
+    gvars = [g for _, g in pg]
+    op = OpDesc('optimize', _optimize_fn, [opt, params] + [_VarRef(g.vid) for g in gvars],
+                {'scaler': scaler}, [g.vid for g in gvars], [], 'C', role='optimize')
+    blk.ops.append(op)
     prog._bump()
     return None, pg
 
@@ -586,7 +793,7 @@ class Executor:
             from ..native import build_plan
             ops = prog.global_block().ops
             ins = [op.in_vids for op in ops]
-            outs = [op.out_vids for op in ops]
+            outs = [op.all_outputs() for op in ops]
             persist = [v.vid for v in prog.global_block().vars.values() if v.persistable]
             order, free_after, level, pruned = build_plan(ins, outs, list(required), persist)
             plan = (order, free_after)
@@ -613,24 +820,74 @@ class Executor:
             fetch_vars.append(f)
         names = list(feed.keys())
         vals = [_as_tensor_feed(feed[n], blk.var(n)) for n in names]
-        has_train = any(op.type in ('backward', 'optimize', 'gradients') for op in blk.ops)
-        if use_graph and not has_train and torch.cuda.is_available() and vals and \
-                all(v._t.is_cuda for v in vals):
+        has_opt = any(op.role == 'optimize' for op in blk.ops)
+        if use_graph and torch.cuda.is_available() and vals and all(v._t.is_cuda for v in vals):
             from ..jit.api import _GraphEntry, _signature
             key = (prog._version, tuple(names), _signature(tuple(vals), {}),
                    tuple(id(f) for f in fetch_vars))
             cache = prog.__dict__.setdefault('_graph_cache', {})
             g = cache.get(key)
+            opt_ops = [op for op in blk.ops if op.role == 'optimize']
+            opt_in = [blk.vars[v] for op in opt_ops for v in op.in_vids]
+            nf = len(fetch_vars)
             if g is None:
-                fn = lambda *fv: self._execute(prog, names, fv, fetch_vars)  # noqa: E731
-                with torch.no_grad():
+                # forward + backward (grad ops) captured as ONE HIP graph; the optimizer
+                # step (host-side LR / loss-scale state) runs eagerly after each replay
+                fn = lambda *fv: self._execute(prog, names, fv, fetch_vars + opt_in,  # noqa: E731
+                                               skip_optimize=True)
+                if has_opt:
                     g = cache[key] = _GraphEntry(fn, tuple(vals), {})
-            outs = [Tensor(o._t.clone()) for o in g(tuple(vals), {})]
+                else:
+                    with torch.no_grad():
+                        g = cache[key] = _GraphEntry(fn, tuple(vals), {})
+            res = g(tuple(vals), {})
+            outs = [Tensor(o._t.clone()) for o in res[:nf]]
+            if opt_ops:
+                genv = {v.vid: t for v, t in zip(opt_in, res[nf:])}
+                prev = _STATIC[0]
+                _STATIC[0] = False
+                try:
+                    for op in opt_ops:
+                        op.fn(*_materialize(op.args, genv), **_materialize(op.kwargs, genv))
+                finally:
+                    _STATIC[0] = prev
         else:
             outs = self._execute(prog, names, vals, fetch_vars)
         return [t.numpy() if return_numpy else t for t in outs]
 
-    def _execute(self, prog, names, vals, fetch_vars):
+    def _run_op(self, op, env, ctx_needed, explicit_bwd):
+        amp_cfg = op.attrs.get('amp')
+        amp_ctx = contextlib.nullcontext()
+        if amp_cfg is not None:
+            from ..amp import auto_cast
+            amp_ctx = auto_cast(True, amp_cfg['white'], amp_cfg['black'], amp_cfg['level'],
+                                amp_cfg['dtype'])
+        with amp_ctx:
+            if op.role == 'forward' and op.ctx_vid is not None and ctx_needed:
+                # run on leaf copies of the differentiable inputs and keep this op's own graph
+                diff_in = op.attrs.get('diff_in', [])
+                dps = op.attrs.get('diff_params', [])
+                overlay = {}
+                for vid in diff_in:
+                    t = _u(env[vid]).detach()
+                    if t.is_floating_point() or t.is_complex():
+                        t.requires_grad_(True)
+                    overlay[vid] = Tensor(t)
+                view = collections.ChainMap(overlay, env)
+                with torch.enable_grad():
+                    res = op.fn(*_materialize(op.args, view), **_materialize(op.kwargs, view))
+                flat, _ = _flatten_out(res)
+                env[op.ctx_vid] = _Ctx([overlay[v]._t for v in diff_in], [p._t for p in dps],
+                                       [t._t for t in flat])
+                return [Tensor(t._t.detach()) for t in flat]
+            if op.role == 'optimize' or not explicit_bwd:
+                # programs without grad ops (inference, TranslatedLayer fine-tuning) keep the
+                # ambient autograd mode so eager backward can flow through them
+                return op.fn(*_materialize(op.args, env), **_materialize(op.kwargs, env))
+            with torch.no_grad():
+                return op.fn(*_materialize(op.args, env), **_materialize(op.kwargs, env))
+
+    def _execute(self, prog, names, vals, fetch_vars, skip_optimize=False):
         blk = prog.global_block()
         required = [f.vid for f in fetch_vars if isinstance(f, Variable) and
                     not isinstance(f, GradVar)]
@@ -640,15 +897,19 @@ class Executor:
         _STATIC[0] = False
         try:
             ops = blk.ops
+            live = {v for oi in order for v in ops[oi].in_vids}
+            explicit_bwd = any(ops[oi].role == 'backward' for oi in order)
             timing = self._op_costs is not None
             sync = torch.cuda.synchronize if timing and torch.cuda.is_available() else \
                 (lambda: None)
             for pos, oi in enumerate(order):
                 op = ops[oi]
+                if skip_optimize and op.role == 'optimize':
+                    continue
                 if timing:
                     sync()
                     t0 = time.perf_counter()
-                res = op.fn(*_materialize(op.args, env), **_materialize(op.kwargs, env))
+                res = self._run_op(op, env, op.ctx_vid in live, explicit_bwd)
                 if timing:
                     sync()
                     self._op_costs.append((op.type, (time.perf_counter() - t0) * 1e3))
@@ -687,12 +948,19 @@ def _qualname(fn, op_type=None):
     return f'{f.__module__}:{f.__qualname__}'
 
 
-def _resolve(q):
-    mod, name = q.split(':')
-    obj = importlib.import_module(mod)
-    for part in name.split('.'):
-        obj = getattr(obj, part)
-    return obj
+_NOT_LOADABLE = {'py_func', 'Print'}
+
+
+def _resolve(op_type):
+    """A .pdmodel names ops ONLY by registered op type (the static op table filled by
+    ``install_static_hooks``); anything else -- e.g. a crafted 'os:system' -- is refused
+    instead of being imported (parity: OpDesc.type resolved through the OpInfoMap)."""
+    install_static_hooks()
+    fn = _OP_TABLE.get(op_type)
+    if fn is None or op_type in _NOT_LOADABLE:
+        raise ValueError(f"op type {op_type!r} is not a registered paddle_ray_amd op; refusing "
+                         "to load this program")
+    return fn
 
 
 def _encode(obj, params):
@@ -753,18 +1021,20 @@ def serialize_program(feed_vars, fetch_vars, program=None):
     blk = prog.global_block()
     required = [v.vid for v in fetch_vars]
     from ..native import build_plan
-    ops = [op for op in blk.ops if op.type not in ('backward', 'optimize')]
+    ops = [op for op in blk.ops if op.role == 'forward']
     order, _, _, _ = build_plan([o.in_vids for o in ops], [o.out_vids for o in ops], required, [])
     params = {}
     enc_ops = []
     for oi in order:
         op = ops[oi]
-        enc_ops.append({'type': op.type, 'fn': _qualname(op.fn, op.type),
-                        'args': _encode(op.args, params), 'kwargs': _encode(op.kwargs, params),
-                        'in': op.in_vids, 'out': op.out_vids})
+        qn = _qualname(op.fn, op.type)
+        if qn not in _OP_TABLE:
+            raise TypeError(f"op {op.type!r} is not a registered static op; cannot serialize")
+        enc_ops.append({'type': qn, 'args': _encode(op.args, params),
+                        'kwargs': _encode(op.kwargs, params), 'in': op.in_vids, 'out': op.out_vids})
     vars_ = {str(v.vid): {'name': v.name, 'shape': v.shape, 'dtype': dtype_to_str(v.dtype)}
              for v in blk.vars.values()}
-    desc = {'version': 1, 'feeds': [v.vid for v in feed_vars], 'fetches': required,
+    desc = {'version': 2, 'feeds': [v.vid for v in feed_vars], 'fetches': required,
             'ops': enc_ops, 'vars': vars_, 'params': sorted(params)}
     return json.dumps(desc).encode(), params
 
@@ -808,7 +1078,7 @@ def deserialize_program(data, params=None):
     for p in params.values():
         prog._register_param(p)
     for o in desc['ops']:
-        fn = _resolve(o['fn'])
+        fn = _resolve(o['type'])
         op = OpDesc(o['type'], fn, _decode(o['args'], params), _decode(o['kwargs'], params),
                     o['in'], o['out'], None)
         blk.ops.append(op)
@@ -897,7 +1167,11 @@ def Print(input, first_n=-1, message=None, summarize=20, print_tensor_name=True,
 
 def py_func(func, x, out, backward_func=None, skip_vars_in_backward_input=None):
     xs = x if isinstance(x, (list, tuple)) else [x]
-    return static_op('py_func', lambda *a: func(*a))(*xs)
+    def run(*a):
+        return func(*a)
+    if _STATIC[0] and _has_var(xs):
+        return record_op('py_func', run, xs, {})  # runs in-process; never serialized
+    return run(*xs)
 
 
 def cpu_places(device_count=None):
@@ -1062,6 +1336,8 @@ def record_layer_call(layer, inputs, kwargs):
     op = OpDesc(f'layer:{type(layer).__name__}', call, targs, tkw, in_vids,
                 [v.vid for v in out_vars], tmpl)
     op.attrs['layer'] = layer
+    op.attrs['params'] = list(layer.parameters())
+    _record_amp(op)
     blk.ops.append(op)
     prog._bump()
     return _rebuild(tmpl, iter(out_vars))
