@@ -32,6 +32,20 @@ def _ptr(t):
     return 0 if t is None else t.data_ptr()
 
 
+def _like(t, dtype):
+    """Cast ``t`` to ``dtype`` when they differ (autocast regions mix bf16 activations with
+    fp32 residuals / parameters; every HIP kernel reads its operands with ONE dtype code)."""
+    return t if t is None or t.dtype == dtype else t.to(dtype)
+
+
+def _check_dtypes(op, *pairs):
+    """Host-side guard before a launch: a kernel given mismatched operand dtypes would read
+    past the end of the narrower buffer."""
+    for a, b in pairs:
+        if a is not None and b is not None and a.dtype != b.dtype:
+            raise TypeError(f"{op}: operand dtypes differ ({a.dtype} vs {b.dtype})")
+
+
 # =============================================================================
 # LayerNorm (last-dim normalisation over `cols`)
 # =============================================================================
@@ -76,6 +90,7 @@ def _adl_nblk(rows):
 
 @R.register_kernel('layer_norm_fwd', 'hip')
 def _ln_fwd_hip(x2, w, b, eps):
+    _check_dtypes('layer_norm', (w, b))
     L = _native.lib()
     rows, cols = x2.shape
     y = torch.empty_like(x2)
@@ -129,6 +144,8 @@ class LayerNormFn(torch.autograd.Function):
         shp = x.shape
         cols = w.numel() if w is not None else shp[-1]
         x2 = x.contiguous().view(-1, cols)
+        if w is not None:
+            b = _like(b, w.dtype)
         y, mean, rstd = R.dispatch('layer_norm_fwd', x2, x2, w, b, eps)
         ctx.save_for_backward(x2, w, mean, rstd)
         ctx.has_b = b is not None
@@ -138,7 +155,7 @@ class LayerNormFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x2, w, mean, rstd = ctx.saved_tensors
-        dy2 = dy.contiguous().view(x2.shape)
+        dy2 = _like(dy, x2.dtype).contiguous().view(x2.shape)
         dx, dw, db = R.dispatch('layer_norm_bwd', x2, dy2, x2, w, mean, rstd,
                                 ctx.needs_input_grad[1], ctx.has_b and ctx.needs_input_grad[2])
         return dx.view(ctx.shp), dw, db, None
@@ -202,6 +219,7 @@ def _adl_bwd_ref(dy, dr_out, r, w, mean, rstd, p, seed, need_dw, need_db, need_d
 
 @R.register_kernel('add_dropout_ln_fwd', 'hip')
 def _adl_fwd_hip(x2, h2, hb, w, b, p, eps, seed):
+    _check_dtypes('add_dropout_layer_norm', (x2, h2), (x2, hb), (w, b))
     rows, cols = x2.shape
     if not _adl_ok(cols):
         return _adl_fwd_ref(x2, h2, hb, w, b, p, eps, seed)
@@ -217,6 +235,7 @@ def _adl_fwd_hip(x2, h2, hb, w, b, p, eps, seed):
 
 @R.register_kernel('add_dropout_ln_bwd', 'hip')
 def _adl_bwd_hip(dy, dr_out, r, w, mean, rstd, p, seed, need_dw, need_db, need_dhb):
+    _check_dtypes('add_dropout_layer_norm_grad', (r, dy), (r, dr_out))
     rows, cols = r.shape
     if not _adl_ok(cols):
         return _adl_bwd_ref(dy, dr_out, r, w, mean, rstd, p, seed, need_dw, need_db, need_dhb)
@@ -247,9 +266,10 @@ class AddDropoutLNFn(torch.autograd.Function):
         shp = x.shape
         cols = shp[-1]
         x2 = x.contiguous().view(-1, cols)
-        h2 = h.contiguous().view(-1, cols)
-        if hb is not None and hb.dtype != x.dtype:
-            hb = hb.to(x.dtype)
+        h2 = _like(h, x.dtype).contiguous().view(-1, cols)
+        hb = _like(hb, x.dtype)
+        if w is not None:
+            b = _like(b, w.dtype)
         seed = _dropout_seed() if p > 0 else 0
         r, y, mean, rstd = R.dispatch('add_dropout_ln_fwd', x2, x2, h2, hb, w, b, p, eps, seed)
         ctx.save_for_backward(r, w, mean, rstd)
@@ -263,9 +283,10 @@ class AddDropoutLNFn(torch.autograd.Function):
         cols = ctx.shp[-1]
         if g_y is None:
             g_y = torch.zeros_like(r)
-        dr_out = None if g_r is None else g_r.contiguous().view(-1, cols)
+        dr_out = None if g_r is None else _like(g_r, r.dtype).contiguous().view(-1, cols)
         dri, dh, dw, db, dhb = R.dispatch(
-            'add_dropout_ln_bwd', r, g_y.contiguous().view(-1, cols), dr_out, r, w, mean, rstd,
+            'add_dropout_ln_bwd', r, _like(g_y, r.dtype).contiguous().view(-1, cols), dr_out, r, w,
+            mean, rstd,
             ctx.p, ctx.seed, w is not None and ctx.needs_input_grad[3],
             ctx.has_b and ctx.needs_input_grad[4], ctx.has_hb and ctx.needs_input_grad[2])
         return dri.view(ctx.shp), dh.view(ctx.shp), dhb, dw, db, None, None
@@ -340,7 +361,7 @@ class RMSNormFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x2, w, rstd = ctx.saved_tensors
-        dx, dw = R.dispatch('rms_norm_bwd', x2, dy.contiguous().view(x2.shape), x2, w, rstd,
+        dx, dw = R.dispatch('rms_norm_bwd', x2, _like(dy, x2.dtype).contiguous().view(x2.shape), x2, w, rstd,
                             ctx.needs_input_grad[1])
         return dx.view(ctx.shp), dw, None
 
@@ -390,7 +411,7 @@ class SoftmaxFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         (y,) = ctx.saved_tensors
-        return R.dispatch('softmax_bwd', y, y, dy.contiguous().view(y.shape)).view(ctx.shp)
+        return R.dispatch('softmax_bwd', y, y, _like(dy, y.dtype).contiguous().view(y.shape)).view(ctx.shp)
 
 
 def softmax_lastdim(x):
@@ -526,7 +547,7 @@ class BiasGeluFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x2, b = ctx.saved_tensors
-        dy2 = dy.contiguous().view(x2.shape)
+        dy2 = _like(dy, x2.dtype).contiguous().view(x2.shape)
         rows, cols = x2.shape
         if (b is not None and ctx.needs_input_grad[1] and x2.is_cuda and cols % 8 == 0
                 and R.select_backend(x2, 'bias_gelu_bwd_db') == 'hip'):
@@ -596,6 +617,7 @@ def _fa_supported(q, k, v):
 
 @R.register_kernel('flash_attn_fwd', 'hip')
 def _fa_fwd_hip(q, k, v, causal, scale):
+    _check_dtypes('flash_attention', (q, k), (q, v))
     if not _fa_supported(q, k, v):
         return _fa_fwd_ref(q, k, v, causal, scale)
     B, Sq, H, D = q.shape
@@ -612,6 +634,8 @@ def _fa_fwd_hip(q, k, v, causal, scale):
 
 @R.register_kernel('flash_attn_bwd', 'hip')
 def _fa_bwd_hip(do, q, k, v, o, lse, causal, scale, dq=None, dk=None, dv=None):
+    do = _like(do, q.dtype)
+    _check_dtypes('flash_attention_grad', (q, k), (q, v), (q, o))
     if not _fa_supported(q, k, v):
         return _fa_bwd_ref(do, q, k, v, o, lse, causal, scale)
     L = _native.lib()
@@ -666,6 +690,7 @@ def flash_attention_qkvpacked(qkv, causal=False, scale=None):
 class FlashAttnFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, q, k, v, causal, scale):
+        k, v = _like(k, q.dtype), _like(v, q.dtype)
         o, lse = R.dispatch('flash_attn_fwd', q, q, k, v, causal, scale)
         ctx.save_for_backward(q, k, v, o, lse)
         ctx.causal, ctx.scale = causal, scale
@@ -1141,6 +1166,7 @@ def _bn_hip_ok(x2):
 
 @R.register_kernel('batch_norm_fwd', 'hip')
 def _bn_fwd_hip(x2, z2, w, b, rmean, rvar, training, momentum, eps, relu):
+    _check_dtypes('batch_norm', (x2, z2), (w, b))
     """Returns (y, mean, invstd, relu keep-mask bytes or None)."""
     if not _bn_hip_ok(x2):
         return _bn_fwd_ref(x2, z2, w, b, rmean, rvar, training, momentum, eps, relu)
@@ -1197,7 +1223,9 @@ class BatchNormActFn(torch.autograd.Function):
         shp = x.shape
         C = shp[-1]
         x2 = x.contiguous().view(-1, C)
-        z2 = z.reshape(-1, C) if z is not None else None
+        z2 = _like(z, x.dtype).reshape(-1, C) if z is not None else None
+        if w is not None:
+            b = _like(b, w.dtype)
         y, mean, invstd, mask = R.dispatch('batch_norm_fwd', x2, x2, z2, w, b, rmean, rvar,
                                            training, momentum, eps, relu)
         # ReLU backward needs only the keep-bits (1 B per 8 channels) when the kernel wrote them
@@ -1209,7 +1237,7 @@ class BatchNormActFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x2, y, mask, w, mean, invstd = ctx.saved_tensors
-        dy2 = dy.contiguous().view(x2.shape)
+        dy2 = _like(dy, x2.dtype).contiguous().view(x2.shape)
         if not ctx.training:  # frozen statistics: dx = dy * w * invstd
             g = dy2.float()
             if ctx.relu:
@@ -1396,7 +1424,8 @@ class GemmBiasActFn(torch.autograd.Function):
         dy2 = dy.reshape(-1, w.shape[1])
         if ctx.act in (1, 2):  # GELU': the elementwise HIP kernel on the saved pre-activation
             dy2 = dy2.contiguous()
-            dz = R.dispatch('bias_gelu_bwd', dy2, dy2, z, None, ctx.act == 2)
+            dy2 = _like(dy2, z.dtype)
+            dz = R.dispatch("bias_gelu_bwd", dy2, dy2, z, None, ctx.act == 2)
         elif ctx.act:
             with torch.enable_grad():
                 zf = z.detach().requires_grad_(True)
