@@ -403,6 +403,23 @@ class _PipeHead(nn.Layer):
         return self.decoder(self.layer_norm(F.gelu(self.transform(x))))
 
 
+class _PipeHeadTransform(nn.Layer):
+    def __init__(self, cfg):
+        super().__init__()
+        self.transform = nn.Linear(cfg.hidden_size, cfg.hidden_size, _init(cfg))
+        self.layer_norm = nn.LayerNorm(cfg.hidden_size, cfg.layer_norm_eps)
+
+    def forward(self, x):
+        return self.layer_norm(F.gelu(self.transform(x)))
+
+
+def _tied_decoder(emb, x):
+    """MLM logits against the (pipeline-shared) word-embedding matrix."""
+    h = _u(x)
+    w = emb.word_embeddings.weight._t
+    return Tensor(K.linear_nt(h.reshape(-1, h.shape[-1]), w).view(*h.shape[:-1], w.shape[0]))
+
+
 class _MLMLoss(nn.Layer):
     def forward(self, scores, labels):
         s = _u(scores)
@@ -410,10 +427,20 @@ class _MLMLoss(nn.Layer):
                                               _u(labels).reshape(-1), -1).mean())
 
 
-def ernie_pipe(cfg, num_stages=None, topology=None, **kw):
+def ernie_pipe(cfg, num_stages=None, topology=None, tie_word_embeddings=False, **kw):
     """ERNIE/BERT MLM model as a ``PipelineLayer`` (layers split over pipeline stages;
-    TP inside each layer when ``cfg.mp_degree > 1``)."""
-    from ..parallel.pipeline import LayerDesc, PipelineLayer
+    TP inside each layer when ``cfg.mp_degree > 1``). ``tie_word_embeddings``: the MLM
+    decoder reuses the input word embedding across the first and last stage
+    (``SharedLayerDesc('embed')``: broadcast at build, gradient all-reduced per batch)."""
+    from ..parallel.pipeline import LayerDesc, PipelineLayer, SharedLayerDesc
+    if tie_word_embeddings and cfg.mp_degree == 1:
+        attr = 'word_embeddings.weight'
+        descs = [SharedLayerDesc('embed', _PipeEmbeddings, None, attr, cfg)]
+        descs += [LayerDesc(_PipeLayer, cfg) for _ in range(cfg.num_hidden_layers)]
+        descs += [LayerDesc(_PipeHeadTransform, cfg),
+                  SharedLayerDesc('embed', _PipeEmbeddings, _tied_decoder, attr, cfg)]
+        return PipelineLayer(descs, num_stages=num_stages, topology=topology,
+                             loss_fn=_MLMLoss(), **kw)
     descs = [LayerDesc(_PipeEmbeddings, cfg)]
     descs += [LayerDesc(_PipeLayer, cfg) for _ in range(cfg.num_hidden_layers)]
     descs.append(LayerDesc(_PipeHead, cfg))

@@ -56,6 +56,7 @@ class GradBucketReducer:
         self.works = []
         self.enabled = True
         self._cb_queued = False
+        self.finalize_count = 0
         self._hooks = []
         for gi, g in enumerate(groups):
             for t in g.leaves:
@@ -124,6 +125,7 @@ class GradBucketReducer:
         self.counts = [0] * len(self.groups)
         self.launched = [False] * len(self.groups)
         self._cb_queued = False
+        self.finalize_count += 1
         if self.on_finalize is not None:
             self.on_finalize()
 

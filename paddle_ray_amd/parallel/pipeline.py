@@ -1,21 +1,31 @@
 """Pipeline parallelism (parity: python/paddle/distributed/fleet/meta_parallel/
 {parallel_layers/pp_layers.py, pipeline_parallel.py, pp_utils/p2p_communication.py}).
 
-PipelineLayer builds only the local stage's layers from LayerDesc lists
-(uniform or parameter-balanced segmentation, SharedLayerDesc for tied
-embeddings). PipelineParallel.train_batch runs the 1F1B schedule; the steady
-state pairs send/recv with batched isend/irecv so neighbouring stages never
-deadlock; activations go point-to-point over RCCL (xGMI peer link).
+* ``PipelineLayer`` builds only this stage's layers from ``LayerDesc`` lists (uniform,
+  ``layer:<Name>`` or parameter-balanced segmentation). With
+  ``num_virtual_pipeline_stages = V`` the model is cut into ``stages * V`` chunks and stage
+  ``s`` holds chunks ``s, s + stages, ...`` (interleaved placement, pp_layers.py
+  ``_construct_shared_comm`` / virtual stages).
+* ``SharedLayerDesc``: a layer used on several stages (tied input embedding / LM head) is
+  built on every owning stage, broadcast from the first owning stage at construction and its
+  gradient is all-reduced over the owning stages after each batch
+  (pp_layers.py ``_synchronize_shared_weights`` :485, ``allreduce_shared_weight_gradients`` :498).
+* ``PipelineParallel.train_batch``: 1F1B (V = 1) or the interleaved schedule over virtual
+  chunks (V > 1, ``PipelineParallelWithInterleave``); activations may be tuples of tensors;
+  point-to-point isend/irecv over RCCL (xGMI peer links), every transfer registered with the
+  collective watchdog. Data-parallel gradients live in flat buckets: with 1F1B the bucket
+  all-reduces are launched from the gradient hooks of the LAST micro-batch's backward, so they
+  overlap the rest of it; the interleaved schedule reduces all buckets after the schedule.
 """
 import math
 
-import numpy as np
 import torch
 import torch.distributed as dist
 
 from ..framework.core import Tensor, _u
 from ..nn.layer.layers import Layer
 from ..nn.layer.common import LayerList
+from ..distributed import watchdog as _watchdog
 from .recompute import recompute
 
 
@@ -58,52 +68,125 @@ class SegmentLayers:
         return [int(round(per * i)) for i in range(self.num_parts)] + [n]
 
 
+def _as_list(x):
+    if x is None:
+        return []
+    if isinstance(x, (list, tuple)):
+        return [_u(t) if isinstance(t, Tensor) else t for t in x]
+    return [_u(x) if isinstance(x, Tensor) else x]
+
+
+def _wrap_acts(ts):
+    ts = [Tensor(t) if isinstance(t, torch.Tensor) else t for t in ts]
+    return ts[0] if len(ts) == 1 else tuple(ts)
+
+
 class PipelineLayer(Layer):
     def __init__(self, layers, num_stages=None, topology=None, loss_fn=None, seg_method="uniform",
                  recompute_interval=0, recompute_ctx=None, num_virtual_pipeline_stages=None):
         super().__init__()
         from ..distributed import fleet
         hcg = fleet.get_hybrid_communicate_group() if fleet.fleet._hcg is not None else None
+        self._hcg = hcg
         self._num_stages = num_stages or (hcg.get_pipe_parallel_world_size() if hcg else 1)
         self._stage_id = hcg.get_stage_id() if hcg else 0
+        self._num_virtual = max(1, int(num_virtual_pipeline_stages or 1))
         self._loss_fn = loss_fn
         self._recompute_interval = recompute_interval
         self._layers_desc = list(layers)
-        self.segment_parts = SegmentLayers(self._layers_desc, self._num_stages,
-                                           seg_method).do_segment()
-        lo, hi = self.segment_parts[self._stage_id], self.segment_parts[self._stage_id + 1]
-        self.run_function = []
+        nparts = self._num_stages * self._num_virtual
+        self.segment_parts = SegmentLayers(self._layers_desc, nparts, seg_method).do_segment()
         self.shared_layers = {}
+        self._chunks = []          # run functions per local virtual chunk
         built = LayerList()
-        for i in range(lo, hi):
-            d = self._layers_desc[i]
-            if isinstance(d, SharedLayerDesc):
-                if d.layer_name not in self.shared_layers:
-                    self.shared_layers[d.layer_name] = d.build_layer()
-                    built.append(self.shared_layers[d.layer_name])
-                l = self.shared_layers[d.layer_name]
-                fn = (lambda layer, f: (lambda x: f(layer, x)))(l, d.forward_func) \
-                    if d.forward_func else l
-                self.run_function.append(fn)
-            elif isinstance(d, LayerDesc):
-                l = d.build_layer()
-                built.append(l)
-                self.run_function.append(l)
-            elif isinstance(d, Layer):
-                built.append(d)
-                self.run_function.append(d)
-            else:
-                self.run_function.append(d)
+        for v in range(self._num_virtual):
+            part = v * self._num_stages + self._stage_id
+            lo, hi = self.segment_parts[part], self.segment_parts[part + 1]
+            fns = []
+            for i in range(lo, hi):
+                d = self._layers_desc[i]
+                if isinstance(d, SharedLayerDesc):
+                    if d.layer_name not in self.shared_layers:
+                        self.shared_layers[d.layer_name] = d.build_layer()
+                        built.append(self.shared_layers[d.layer_name])
+                    l = self.shared_layers[d.layer_name]
+                    fns.append((lambda layer, f: (lambda x: f(layer, x)))(l, d.forward_func)
+                               if d.forward_func else l)
+                elif isinstance(d, LayerDesc):
+                    l = d.build_layer()
+                    built.append(l)
+                    fns.append(l)
+                elif isinstance(d, Layer):
+                    built.append(d)
+                    fns.append(d)
+                else:
+                    fns.append(d)
+            self._chunks.append(fns)
+        self.run_function = [f for c in self._chunks for f in c]
         self.run_layers = built
+        self._shared_comm = {}
+        if self._num_stages > 1 and hcg is not None:
+            self._build_shared_comm(hcg)
+            self._synchronize_shared_weights()
 
+    # -- shared (tied) layers across stages -----------------------------------------------------
+    def _owning_stages(self):
+        owners = {}
+        for part in range(len(self.segment_parts) - 1):
+            stage = part % self._num_stages
+            for i in range(self.segment_parts[part], self.segment_parts[part + 1]):
+                d = self._layers_desc[i]
+                if isinstance(d, SharedLayerDesc):
+                    owners.setdefault(d.layer_name, set()).add(stage)
+        return {k: sorted(v) for k, v in owners.items()}
+
+    def _build_shared_comm(self, hcg):
+        """One group per shared key and per pipe group, over the stages owning that key;
+        every rank creates every group in the same order (collective new_group)."""
+        from ..distributed import collective as C
+        me = C.get_rank()
+        attr_of = {d.layer_name: d.shared_weight_attr for d in self._layers_desc
+                   if isinstance(d, SharedLayerDesc)}
+        for key, stages in sorted(self._owning_stages().items()):
+            if len(stages) < 2:
+                continue
+            for pipe_ranks in hcg.topology().get_comm_list('pipe'):
+                ranks = [pipe_ranks[s] for s in stages]
+                g = C.new_group(ranks)
+                if me in ranks and key in self.shared_layers:
+                    self._shared_comm[key] = (g, ranks, attr_of[key])
+
+    def _shared_params(self, key):
+        _, _, attr = self._shared_comm[key]
+        layer = self.shared_layers[key]
+        names = attr if isinstance(attr, (list, tuple)) else [attr]
+        out = []
+        for n in names:  # dotted paths reach into sublayers ('word_embeddings.weight')
+            obj = layer
+            for part in n.split('.'):
+                obj = getattr(obj, part)
+            out.append(obj)
+        return out
+
+    def _synchronize_shared_weights(self):
+        for key, (g, ranks, _) in self._shared_comm.items():
+            for p in self._shared_params(key):
+                dist.broadcast(p._t.data, ranks[0], group=g.process_group)
+
+    def allreduce_shared_weight_gradients(self):
+        for key, (g, ranks, _) in self._shared_comm.items():
+            for p in self._shared_params(key):
+                if p._t.grad is not None:
+                    _watchdog.track(f'pp.shared[{key}]', dist.all_reduce(
+                        p._t.grad, group=g.process_group, async_op=True), len(ranks)).wait()
+
+    # -- forward -------------------------------------------------------------------------------
     def get_stage_from_index(self, idx):
-        for s in range(self._num_stages):
-            if self.segment_parts[s] <= idx < self.segment_parts[s + 1]:
-                return s
+        for part in range(len(self.segment_parts) - 1):
+            if self.segment_parts[part] <= idx < self.segment_parts[part + 1]:
+                return part % self._num_stages
 
-    def forward(self, input):
-        x = input
-        fns = self.run_function
+    def _run(self, fns, x):
         if self._recompute_interval > 0 and self.training:
             k = self._recompute_interval
             for lo in range(0, len(fns), k):
@@ -120,88 +203,89 @@ class PipelineLayer(Layer):
             x = f(x)
         return x
 
+    def forward(self, input, chunk_id=None):
+        if chunk_id is not None:
+            return self._run(self._chunks[chunk_id], input)
+        return self._run(self.run_function, input)
 
-_DT_CODES = [torch.float32, torch.float16, torch.bfloat16, torch.int64, torch.int32, torch.bool]
+
+_DT_CODES = [torch.float32, torch.float16, torch.bfloat16, torch.int64, torch.int32, torch.bool,
+             torch.uint8, torch.float64]
+_META_LEN = 64
 
 
 class _P2P:
+    """Point-to-point activation / gradient exchange on the pipe group's ring (the wrap
+    from the last stage to the first is used by the interleaved schedule). Activations may
+    be tuples; only floating tensors carry gradients back."""
+
     def __init__(self, hcg):
         self.hcg = hcg
         self.stage = hcg.get_stage_id()
         self.nstages = hcg.get_pipe_parallel_world_size()
         g = hcg.get_pipe_parallel_group()
         self.pg = g.process_group
-        self.prev = g.ranks[self.stage - 1] if self.stage > 0 else None
-        self.next = g.ranks[self.stage + 1] if self.stage < self.nstages - 1 else None
+        self.ranks = g.ranks
+        self.prev = g.ranks[(self.stage - 1) % self.nstages]
+        self.next = g.ranks[(self.stage + 1) % self.nstages]
         self.dev = torch.device('cuda', torch.cuda.current_device()) \
             if torch.cuda.is_available() and dist.get_backend(self.pg) == 'nccl' else \
             torch.device('cpu')
-        self.recv_meta = None
-        self.sent_meta = False
+        self.meta_from = {}   # peer -> [(shape, dtype)] of what that peer sends us
+        self.meta_sent = set()
+        self.pending = []     # (work, tensor) isends to wait for before the batch ends
 
-    def _send_meta(self, t):
-        m = torch.zeros(16, dtype=torch.int64, device=self.dev)
-        m[0] = t.dim()
-        m[1] = _DT_CODES.index(t.dtype)
-        m[2:2 + t.dim()] = torch.tensor(list(t.shape))
-        dist.send(m, self.next, group=self.pg)
+    def _isend(self, t, peer, what):
+        t = t.detach().contiguous()
+        w = _watchdog.track(f'pp.{what}', dist.isend(t, peer, group=self.pg), 2)
+        self.pending.append((w, t))
 
-    def _recv_meta(self):
-        m = torch.zeros(16, dtype=torch.int64, device=self.dev)
-        dist.recv(m, self.prev, group=self.pg)
-        nd = int(m[0])
-        self.recv_meta = (tuple(int(v) for v in m[2:2 + nd]), _DT_CODES[int(m[1])])
-
-    def send_fwd(self, t):
-        if self.next is None:
-            return
-        if not self.sent_meta:
-            self._send_meta(t)
-            self.sent_meta = True
-        dist.send(t.detach().contiguous(), self.next, group=self.pg)
-
-    def recv_fwd(self):
-        if self.prev is None:
-            return None
-        if self.recv_meta is None:
-            self._recv_meta()
-        shp, dt = self.recv_meta
-        t = torch.empty(shp, dtype=dt, device=self.dev)
-        dist.recv(t, self.prev, group=self.pg)
-        return t.requires_grad_(t.is_floating_point())
-
-    def send_bwd(self, g):
-        if self.prev is None or g is None:
-            return
-        dist.send(g.contiguous(), self.prev, group=self.pg)
-
-    def recv_bwd(self, like):
-        if self.next is None:
-            return None
-        t = torch.empty_like(like)
-        dist.recv(t, self.next, group=self.pg)
+    def _recv(self, t, peer, what):
+        _watchdog.track(f'pp.{what}', dist.irecv(t, peer, group=self.pg), 2).wait()
         return t
 
-    def send_fwd_recv_bwd(self, y):
-        if self.next is None:
-            return None
-        g = torch.empty_like(y)
-        ops = [dist.P2POp(dist.isend, y.detach().contiguous(), self.next, self.pg),
-               dist.P2POp(dist.irecv, g, self.next, self.pg)]
-        for w in dist.batch_isend_irecv(ops):
-            w.wait()
-        return g
+    def send_acts(self, acts, peer):
+        ts = [t for t in acts if isinstance(t, torch.Tensor)]
+        if peer not in self.meta_sent:
+            m = torch.zeros(_META_LEN, dtype=torch.int64, device=self.dev)
+            m[0] = len(ts)
+            k = 1
+            for t in ts:
+                m[k], m[k + 1] = t.dim(), _DT_CODES.index(t.dtype)
+                m[k + 2:k + 2 + t.dim()] = torch.tensor(list(t.shape))
+                k += 2 + t.dim()
+            self._isend(m, peer, 'meta')
+            self.meta_sent.add(peer)
+        for t in ts:
+            self._isend(t, peer, 'send_fwd')
 
-    def send_bwd_recv_fwd(self, dx):
-        if self.prev is None:
-            return None
-        shp, dt = self.recv_meta
-        x = torch.empty(shp, dtype=dt, device=self.dev)
-        ops = [dist.P2POp(dist.isend, dx.contiguous(), self.prev, self.pg),
-               dist.P2POp(dist.irecv, x, self.prev, self.pg)]
-        for w in dist.batch_isend_irecv(ops):
+    def recv_acts(self, peer):
+        if peer not in self.meta_from:
+            m = self._recv(torch.zeros(_META_LEN, dtype=torch.int64, device=self.dev), peer, 'meta')
+            n, k, meta = int(m[0]), 1, []
+            for _ in range(n):
+                nd, dt = int(m[k]), _DT_CODES[int(m[k + 1])]
+                meta.append((tuple(int(v) for v in m[k + 2:k + 2 + nd]), dt))
+                k += 2 + nd
+            self.meta_from[peer] = meta
+        out = []
+        for shp, dt in self.meta_from[peer]:
+            t = self._recv(torch.empty(shp, dtype=dt, device=self.dev), peer, 'recv_fwd')
+            out.append(t.requires_grad_(t.is_floating_point()))
+        return out
+
+    def send_grads(self, grads, peer):
+        for g in grads:
+            self._isend(g, peer, 'send_bwd')
+
+    def recv_grads(self, like, peer):
+        return [self._recv(torch.empty_like(t), peer, 'recv_bwd') for t in like
+                if t.is_floating_point()]
+
+    def flush(self):
+        for w, _ in self.pending:
             w.wait()
-        return x.requires_grad_(x.is_floating_point())
+        self.pending.clear()
 
 
 class PipelineParallel(Layer):
@@ -216,8 +300,25 @@ class PipelineParallel(Layer):
         self.is_last = hcg.is_last_stage()
         self._p2p = _P2P(hcg) if hcg.get_pipe_parallel_world_size() > 1 else None
         self.total_loss = None
-        # DP over the data-parallel axis: gradient all-reduce after the schedule
         self._dp_group = hcg.get_data_parallel_group()
+        self._dp_reducer = None
+        if self._dp_group is not None and self._dp_group.nranks > 1:
+            self._build_dp_buckets(strategy)
+
+    def _build_dp_buckets(self, strategy):
+        """Flat gradient buckets over this stage's parameters, all-reduced over the dp group
+        (GradBucketReducer: one RCCL call per bucket, watchdog-tracked)."""
+        from .data_parallel import GradBucketReducer
+        from .flat import FlatGroup, group_params_into_buckets
+        g = self._dp_group
+        params = [p for p in self._layers.parameters() if not p.stop_gradient]
+        for p in self._layers.parameters():
+            dist.broadcast(p._t.data, g.ranks[0], group=g.process_group)
+        mb = getattr(strategy, 'fuse_grad_size_in_MB', 64) if strategy is not None else 64
+        self._dp_groups = [FlatGroup(b) for b in group_params_into_buckets(params, int(mb) << 20)]
+        self._dp_reducer = GradBucketReducer(self._dp_groups, g.process_group, g.nranks,
+                                             'allreduce', name='pp.dp_bucket')
+        self._dp_reducer.enabled = False
 
     def forward(self, *a, **k):
         return self._layers(*a, **k)
@@ -231,23 +332,33 @@ class PipelineParallel(Layer):
         t = _u(data)
         return t[i * mb:(i + 1) * mb]
 
-    def _fwd(self, x, labels):
-        out = self._layers(Tensor(x) if isinstance(x, torch.Tensor) else x)
-        if self.is_last:
+    def _run_chunk(self, acts, labels, chunk, last_chunk):
+        out = self._layers(_wrap_acts(acts), chunk_id=chunk) if self._layers._num_virtual > 1 \
+            else self._layers(_wrap_acts(acts))
+        if self.is_last and last_chunk:
             loss = self._layers._loss_fn(out, Tensor(labels) if isinstance(labels, torch.Tensor)
                                          else labels)
             lt = _u(loss)
             if lt.dim():
                 lt = lt.mean()
-            return lt / self.accumulate_steps
-        return _u(out)
+            return [lt / self.accumulate_steps]
+        return _as_list(out)
 
-    def _bwd(self, x, y, dy):
-        if self.is_last:
-            y.backward()
-        else:
-            torch.autograd.backward(y, dy)
-        return x.grad if isinstance(x, torch.Tensor) and x.requires_grad else None
+    @staticmethod
+    def _backward(xs, ys, gys):
+        outs, grads = [], []
+        for y, g in zip([y for y in ys if y.is_floating_point()], gys):
+            if y.requires_grad:
+                outs.append(y)
+                grads.append(g)
+        if outs:
+            torch.autograd.backward(outs, grads if any(g is not None for g in grads) else None)
+        return [x.grad if (x.requires_grad and x.grad is not None) else torch.zeros_like(x)
+                for x in xs if isinstance(x, torch.Tensor) and x.is_floating_point()]
+
+    def _first_inputs(self, inputs, i):
+        x = self._micro(inputs, i)
+        return [t for t in (x if isinstance(x, tuple) else (x,))]
 
     def forward_backward_pipeline(self, data, scaler=None):
         inputs, labels = data if isinstance(data, (list, tuple)) and len(data) == 2 else (data, None)
@@ -256,79 +367,126 @@ class PipelineParallel(Layer):
         if p2p is None:
             losses = []
             for i in range(M):
-                x = self._micro(inputs, i)
-                y = self._fwd(x, self._micro(labels, i))
+                if self._dp_reducer is not None:
+                    self._dp_reducer.enabled = i == M - 1
+                y = self._run_chunk(self._first_inputs(inputs, i), self._micro(labels, i), 0, True)[0]
+                if scaler is not None:
+                    y = _u(scaler.scale(Tensor(y)))
                 y.backward()
                 losses.append(y.detach())
             self.total_loss = torch.stack(losses).sum()
             return self.total_loss
-        p2p.sent_meta = False
-        p2p.recv_meta = None  # both sides re-exchange activation meta every batch
-        nst, st = p2p.nstages, p2p.stage
-        warmup = min(nst - st - 1, M)
-        remaining = M - warmup
-        pending, losses = [], []
-
-        def get_x(i):
-            if self.is_first:
-                x = self._micro(inputs, i)
-                return x
-            return None
-
-        for i in range(warmup):
-            x = get_x(i) if self.is_first else p2p.recv_fwd()
-            y = self._fwd(x, self._micro(labels, i))
-            p2p.send_fwd(y)
-            pending.append((x, y))
-            if self.is_last:
-                losses.append(y.detach())
-        x = None
-        if remaining > 0:
-            x = get_x(warmup) if self.is_first else p2p.recv_fwd()
-        for i in range(remaining):
-            y = self._fwd(x, self._micro(labels, warmup + i))
-            if self.is_last:
-                losses.append(y.detach())
-                dy = None
-            else:
-                dy = p2p.send_fwd_recv_bwd(y)
-            pending.append((x, y))
-            x0, y0 = pending.pop(0)
-            dx = self._bwd(x0, y0, dy if not self.is_last else None) if True else None
-            if i == remaining - 1:
-                p2p.send_bwd(dx)
-            else:
-                if self.is_first:
-                    x = get_x(warmup + i + 1)
-                else:
-                    x = p2p.send_bwd_recv_fwd(dx)
-                if self.is_first:
-                    pass
-        for i in range(warmup):
-            x0, y0 = pending.pop(0)
-            dy = p2p.recv_bwd(y0) if not self.is_last else None
-            dx = self._bwd(x0, y0, dy)
-            p2p.send_bwd(dx)
-        # last stage owns the loss; broadcast it over the pipe group for reporting
+        p2p.meta_from.clear()
+        p2p.meta_sent.clear()  # both sides re-exchange activation meta every batch
+        if self._layers._num_virtual > 1:
+            losses = self._interleaved(inputs, labels, M, scaler)
+        else:
+            losses = self._one_f_one_b(inputs, labels, M, scaler)
+        p2p.flush()
         loss = torch.stack(losses).sum() if losses else torch.zeros((), device=p2p.dev)
         loss = loss.to(p2p.dev).float()
-        dist.broadcast(loss, p2p.hcg.get_pipe_parallel_group().ranks[-1], group=p2p.pg)
+        if scaler is not None and losses:
+            loss = loss / scaler.get_loss_scaling()
+        dist.broadcast(loss, p2p.ranks[-1], group=p2p.pg)
         self.total_loss = loss
         return loss
 
-    def _dp_allreduce(self):
-        g = self._dp_group
-        if g is None or g.nranks <= 1:
+    # -- 1F1B ----------------------------------------------------------------------------------
+    def _one_f_one_b(self, inputs, labels, M, scaler):
+        p2p = self._p2p
+        nst, st = p2p.nstages, p2p.stage
+        warmup = min(nst - st - 1, M)
+        pending, losses = [], []
+        nb = [0]
+
+        def fwd(i):
+            xs = self._first_inputs(inputs, i) if self.is_first else p2p.recv_acts(p2p.prev)
+            ys = self._run_chunk(xs, self._micro(labels, i), 0, True)
+            if self.is_last:
+                if scaler is not None:
+                    ys = [_u(scaler.scale(Tensor(ys[0])))]
+                losses.append(ys[0].detach())
+            else:
+                p2p.send_acts(ys, p2p.next)
+            pending.append((xs, ys))
+
+        def bwd():
+            xs, ys = pending.pop(0)
+            gys = [None] if self.is_last else p2p.recv_grads(ys, p2p.next)
+            nb[0] += 1
+            if self._dp_reducer is not None:
+                self._dp_reducer.enabled = nb[0] == M  # last micro-batch: launch bucket reduces
+            dxs = self._backward(xs, ys, gys)
+            if not self.is_first:
+                p2p.send_grads(dxs, p2p.prev)
+
+        for i in range(warmup):
+            fwd(i)
+        for i in range(M - warmup):
+            fwd(warmup + i)
+            bwd()
+        for _ in range(warmup):
+            bwd()
+        return losses
+
+    # -- interleaved (virtual stages) ----------------------------------------------------------
+    def _interleaved(self, inputs, labels, M, scaler):
+        """Depth-first over virtual chunks: every stage runs chunk v for all micro-batches,
+        handing activations around the ring (last stage -> first stage between chunks), then
+        the backward in exactly the reverse order. Sends are asynchronous, receives block, and
+        every peer pair sees one consistent order, so no cycle of waits can form."""
+        p2p = self._p2p
+        V = self._layers._num_virtual
+        nst, st = p2p.nstages, p2p.stage
+        bufs, losses = {}, []
+        for v in range(V):
+            first_chunk = st == 0 and v == 0
+            last_chunk = st == nst - 1 and v == V - 1
+            for m in range(M):
+                xs = self._first_inputs(inputs, m) if first_chunk else p2p.recv_acts(p2p.prev)
+                ys = self._run_chunk(xs, self._micro(labels, m), v, v == V - 1)
+                if last_chunk:
+                    if scaler is not None:
+                        ys = [_u(scaler.scale(Tensor(ys[0])))]
+                    losses.append(ys[0].detach())
+                else:
+                    p2p.send_acts(ys, p2p.next)
+                bufs[(v, m)] = (xs, ys)
+        for v in reversed(range(V)):
+            first_chunk = st == 0 and v == 0
+            last_chunk = st == nst - 1 and v == V - 1
+            for m in range(M):
+                xs, ys = bufs.pop((v, m))
+                gys = [None] if last_chunk else p2p.recv_grads(ys, p2p.next)
+                dxs = self._backward(xs, ys, gys)
+                if not first_chunk:
+                    p2p.send_grads(dxs, p2p.prev)
+        return losses
+
+    # -- gradient reduction + step --------------------------------------------------------------
+    def _reduce_dp(self):
+        r = self._dp_reducer
+        if r is None:
             return
-        for p in self._layers.parameters():
-            if p._t.grad is not None:
-                dist.all_reduce(p._t.grad, group=g.process_group)
-                p._t.grad.div_(g.nranks)
+        r.enabled = True
+        for gi in range(len(r.groups)):
+            r._launch(gi)
+        r.finalize()
 
     def train_batch(self, data, optimizer, lr_scheduler=None, scaler=None):
         self._layers.train()
+        if self._dp_reducer is not None:
+            for g in self._dp_groups:
+                if g.grads_missing():
+                    g.grad_buf.zero_()
+                    g.reattach_grads()
+        before = self._dp_reducer.finalize_count if self._dp_reducer is not None else 0
         loss = self.forward_backward_pipeline(data, scaler)
-        self._dp_allreduce()
+        if self._dp_reducer is not None and self._dp_reducer.finalize_count == before:
+            self._reduce_dp()  # interleaved schedule (or no hook fired): reduce all buckets now
+        self._layers.allreduce_shared_weight_gradients()
+        if self._dp_reducer is not None:
+            self._dp_reducer.enabled = False
         if scaler is not None:
             scaler.step(optimizer)
             scaler.update()
@@ -347,3 +505,6 @@ class PipelineParallel(Layer):
             if compute_loss and self._layers._loss_fn is not None:
                 return self._layers._loss_fn(out, labels)
             return out
+
+
+PipelineParallelWithInterleave = PipelineParallel
