@@ -29,7 +29,14 @@ def _stream(t=None):
 
 
 def _ptr(t):
-    return 0 if t is None else t.data_ptr()
+    """Device address of a HIP kernel operand. A host or meta tensor here (e.g. a symbolic
+    static-graph Variable reaching a kernel selected by another operand's device) would hand
+    the kernel a host / null address and fault the GPU: refuse on the host instead."""
+    if t is None:
+        return 0
+    if not t.is_cuda:
+        raise TypeError(f"HIP kernel operand on {t.device}, expected the GPU")
+    return t.data_ptr()
 
 
 def _like(t, dtype):
@@ -1331,7 +1338,7 @@ class EmbeddingFn(torch.autograd.Function):
     def forward(ctx, ids, w, pad):
         ctx.save_for_backward(ids)
         ctx.w, ctx.pad = w, pad
-        return R.dispatch('embedding_fwd', w, ids, w, pad)
+        return R.dispatch('embedding_fwd', ids if not ids.is_cuda else w, ids, w, pad)
 
     @staticmethod
     def backward(ctx, dy):
