@@ -292,12 +292,16 @@ def is_grad_enabled():
 # ----------------------------------------------------------------------------
 # Tensor
 # ----------------------------------------------------------------------------
-_name_counter = [0]
+# per-prefix counters, like the reference's paddle.utils.unique_name (``linear_0.w_0``);
+# ``paddle.utils.unique_name.guard()`` swaps in a fresh table
+_NAME_COUNTERS = [__import__('collections').defaultdict(int)]
 
 
 def _unique_name(prefix='generated_tensor'):
-    _name_counter[0] += 1
-    return f'{prefix}_{_name_counter[0]}'
+    c = _NAME_COUNTERS[0]
+    n = c[prefix]
+    c[prefix] += 1
+    return f'{prefix}_{n}'
 
 
 class Tensor:

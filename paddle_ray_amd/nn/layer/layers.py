@@ -71,8 +71,7 @@ class Layer:
         d['_forward_post_hooks'] = collections.OrderedDict()
         d['_hook_id'] = 0
         scope = name_scope or re.sub(r'(?<!^)(?=[A-Z])', '_', type(self).__name__).lower()
-        d['_full_name'] = f'{scope}_{_layer_name_counts[scope]}'
-        _layer_name_counts[scope] += 1
+        d['_full_name'] = _unique_name(scope)
 
     # -- construction ----------------------------------------------------------
     def full_name(self):

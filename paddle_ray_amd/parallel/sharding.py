@@ -605,38 +605,112 @@ class ShardedOptimizer:
         self.step()
 
     # -- checkpoint ------------------------------------------------------------------------
-    def state_dict(self):
-        """Owned-shard state (each rank saves its own .pdopt shard)."""
+    def _acc_keys(self):
+        return ('moment1', 'moment2') if self._kind in ('Adam', 'AdamW') else ('velocity', None)
+
+    def _gather_full(self, buf, g):
+        """All-gather one group's owned shards into the full flat buffer (host copy)."""
+        st = self.state
+        if st.world == 1:
+            return buf.detach().float().cpu()
+        dev = g.device if (g.device.type == 'cuda' and dist.get_backend(st.pg) == 'nccl') \
+            else torch.device('cpu')
+        src = buf.detach().float().to(dev).contiguous()
+        out = torch.empty(src.numel() * st.world, dtype=src.dtype, device=dev)
+        _watchdog.track('sharding.ckpt_gather', dist.all_gather_into_tensor(
+            out, src, group=st.pg, async_op=True), st.world).wait()
+        return out.cpu()
+
+    def state_dict(self, full=True):
+        """Optimizer state in the reference's per-parameter layout (``{param}_moment1_0``,
+        ``{param}_moment2_0`` / ``{param}_velocity_0``, ``{param}_beta{1,2}_pow_acc_0``,
+        ``master_weights``, ``LR_Scheduler``), gathered from every rank's owned shard: a
+        ``.pdopt`` written here resumes under ANY sharding degree (or none: the plain optimizer
+        reads the same keys). ``full=False`` returns this rank's raw shards only."""
+        st = self.state
         sd = {}
-        for gi in range(len(self.state.groups)):
-            sd[f'shard{gi}_moment1'] = Tensor(self._m[gi])
-            if self._v[gi] is not None:
-                sd[f'shard{gi}_moment2'] = Tensor(self._v[gi])
-            if self._masters[gi] is not None:
-                sd[f'shard{gi}_master'] = Tensor(self._masters[gi])
+        if not full:
+            for gi in range(len(st.groups)):
+                sd[f'shard{gi}_moment1'] = Tensor(self._m[gi])
+                if self._v[gi] is not None:
+                    sd[f'shard{gi}_moment2'] = Tensor(self._v[gi])
+                if self._masters[gi] is not None:
+                    sd[f'shard{gi}_master'] = Tensor(self._masters[gi])
+            sd['@rank'], sd['@world'] = st.rank, st.world
+        else:
+            k1, k2 = self._acc_keys()
+            masters = {}
+            for gi, g in enumerate(st.groups):
+                bufs = [(k1, self._m[gi]), (k2, self._v[gi]), ('master', self._masters[gi])]
+                for key, buf in bufs:
+                    if key is None or buf is None:
+                        continue
+                    flat = self._gather_full(buf, g)
+                    for p, o, n, shp in zip(g.params, g.offsets, g.numels, g.shapes):
+                        v = Tensor(flat[o:o + n].view(shp).clone())
+                        if key == 'master':
+                            masters[p.name] = v
+                        else:
+                            sd[f'{p.name}_{key}_0'] = v
+                if self._kind in ('Adam', 'AdamW'):
+                    o = self._inner
+                    for p in g.params:
+                        sd[f'{p.name}_beta1_pow_acc_0'] = Tensor(
+                            torch.tensor([o._beta1 ** self._step], dtype=torch.float32))
+                        sd[f'{p.name}_beta2_pow_acc_0'] = Tensor(
+                            torch.tensor([o._beta2 ** self._step], dtype=torch.float32))
+            if masters:
+                sd['master_weights'] = masters
         sd['@step'] = self._step
-        sd['@rank'] = self.state.rank
-        sd['@world'] = self.state.world
         from ..optimizer.lr import LRScheduler
         if isinstance(self._inner._learning_rate, LRScheduler):
             sd['LR_Scheduler'] = self._inner._learning_rate.state_dict()
         return sd
 
     def set_state_dict(self, sd):
-        for gi in range(len(self.state.groups)):
-            for key, buf in ((f'shard{gi}_moment1', self._m[gi]), (f'shard{gi}_moment2', self._v[gi]),
-                             (f'shard{gi}_master', self._masters[gi])):
-                if key in sd and buf is not None:
-                    buf.copy_(_u(sd[key]).to(buf.device))
-        self._step = int(sd.get('@step', self._step))
+        st = self.state
+        k1, k2 = self._acc_keys()
+        per_param = any(isinstance(k, str) and k.endswith(f'_{k1}_0') for k in sd)
+        masters_sd = sd.get('master_weights', {})
+        with torch.no_grad():
+            for gi, g in enumerate(st.groups):
+                if per_param:
+                    # slice this rank's owned pieces out of the full per-parameter tensors
+                    for p, lo, hi, plo in g.params_in_shard():
+                        for key, buf in ((k1, self._m[gi]), (k2, self._v[gi])):
+                            name = f'{p.name}_{key}_0'
+                            if key is None or buf is None or name not in sd:
+                                continue
+                            src = _u(sd[name]).reshape(-1)[plo:plo + (hi - lo)]
+                            buf[lo:hi].copy_(src.to(device=buf.device, dtype=buf.dtype))
+                        if self._masters[gi] is not None and p.name in masters_sd:
+                            src = _u(masters_sd[p.name]).reshape(-1)[plo:plo + (hi - lo)]
+                            self._masters[gi][lo:hi].copy_(src.to(self._masters[gi].device,
+                                                                  torch.float32))
+                else:
+                    for key, buf in ((f'shard{gi}_moment1', self._m[gi]),
+                                     (f'shard{gi}_moment2', self._v[gi]),
+                                     (f'shard{gi}_master', self._masters[gi])):
+                        if key in sd and buf is not None:
+                            buf.copy_(_u(sd[key]).to(buf.device))
+        step = sd.get('@step')
+        if step is None and self._kind in ('Adam', 'AdamW'):
+            b1 = [v for k, v in sd.items() if isinstance(k, str) and k.endswith('_beta1_pow_acc_0')]
+            if b1:
+                step = int(round(math.log(float(_u(b1[0]).reshape(-1)[0])) /
+                                 math.log(self._inner._beta1)))
+        if step is not None:
+            self._step = int(step)
         if 'LR_Scheduler' in sd:
             self._inner._learning_rate.set_state_dict(sd['LR_Scheduler'])
         # refresh the owned low-precision shard from the restored master
-        for gi, g in enumerate(self.state.groups):
+        for gi, g in enumerate(st.groups):
             if self._masters[gi] is not None:
-                g.param_shard.copy_(self._masters[gi])
-        self.state.params_stale = True
-        self.state.sync_params()
+                g.param_shard.copy_(self._masters[gi].to(g.param_shard.device))
+        st.params_stale = True
+        st.sync_params()
+        if st.zero3:
+            st.release_all()
 
 
 class ShardedModel(Layer):
@@ -713,12 +787,17 @@ def group_sharded_parallel(model, optimizer, level, scaler=None, group=None, off
 
 
 def save_group_sharded_model(model, output, optimizer=None):
+    """Save the FULL model (``model.pdparams``) and the FULL, per-parameter optimizer state
+    (``model.pdopt``) from rank 0 (parity: distributed/sharding/group_sharded.py
+    save_group_sharded_model); every rank takes part in the gathers. The files load into
+    a sharded run of any degree or into a plain single-process optimizer."""
     import os
     from ..framework.io import save
     from ..distributed import collective as C
     os.makedirs(output, exist_ok=True)
     sd = model.state_dict()
+    osd = optimizer.state_dict() if optimizer is not None else None
     if C.get_rank() == 0:
         save(sd, os.path.join(output, 'model.pdparams'))
-    if optimizer is not None:
-        save(optimizer.state_dict(), os.path.join(output, f'model.rank{C.get_rank()}.pdopt'))
+        if osd is not None:
+            save(osd, os.path.join(output, 'model.pdopt'))

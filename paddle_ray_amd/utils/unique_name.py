@@ -1,21 +1,22 @@
 import collections
 import contextlib
 
-_counters = collections.defaultdict(int)
+import importlib
+
+_core = importlib.import_module('paddle_ray_amd.framework.core')
 
 
 def generate(key):
-    n = _counters[key]
-    _counters[key] += 1
-    return f'{key}_{n}'
+    return _core._unique_name(key)
 
 
 @contextlib.contextmanager
 def guard(new_generator=None):
-    global _counters
-    old = _counters
-    _counters = collections.defaultdict(int)
+    """Fresh name counters for layers / parameters / tensors created inside (parity:
+    python/paddle/utils/unique_name.py guard)."""
+    old = _core._NAME_COUNTERS[0]
+    _core._NAME_COUNTERS[0] = collections.defaultdict(int)
     try:
         yield
     finally:
-        _counters = old
+        _core._NAME_COUNTERS[0] = old
