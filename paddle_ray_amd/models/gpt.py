@@ -8,7 +8,12 @@ MI355X mapping per block:
   fused) -> fc2 GEMM -> residual. Logits = h @ E^T (tied) -> fused one-pass
   softmax-CE (HIP) — the [tokens, vocab] probability matrix is never stored.
 Tensor parallel (mp_degree > 1) swaps in Column/RowParallelLinear,
-VocabParallelEmbedding and ParallelCrossEntropy.
+VocabParallelEmbedding and ParallelCrossEntropy and keeps every fusion: the block input
+enters the TP region through an identity/all-reduce-grad op, the rank-local QKV GEMM +
+flash attention + out-proj (and fc1 GEMM+bias+GELU + fc2) produce partial sums that are
+all-reduced ONCE, and the fused add+dropout+LayerNorm kernel adds the replicated bias,
+residual and next LN after the all-reduce. The embedding is the HIP lookup on shifted ids
+and the loss is the one-pass vocab-parallel softmax-CE kernel.
 """
 import math
 from dataclasses import dataclass
@@ -105,6 +110,7 @@ class GPTAttention(nn.Layer):
             self.qkv_proj = nn.Linear(h, 3 * h, nn.ParamAttr(initializer=init))
             self.out_proj = nn.Linear(h, h, nn.ParamAttr(initializer=out_init))
         self.attn_dropout = cfg.attention_dropout
+        self.mp = cfg.mp_degree
 
     def _core(self, x):
         qkv = _u(self.qkv_proj(x))
@@ -119,8 +125,12 @@ class GPTAttention(nn.Layer):
         return o.reshape(B, S, self.num_heads * self.head_dim)
 
     def forward_nobias(self, x):
-        """attention output projection WITHOUT its bias (fused into the next kernel)."""
-        return Tensor(K.linear(self._core(x), self.out_proj.weight._t))
+        """attention output projection WITHOUT its bias (fused into the next kernel). Under
+        TP the row-parallel partial sums are all-reduced here (bias added after, once)."""
+        a = K.linear(self._core(x), self.out_proj.weight._t)
+        if self.mp > 1:
+            a = _mp()._AllReduce.apply(a, self.out_proj.model_parallel_group)
+        return Tensor(a)
 
     def forward(self, x):
         qkv = _u(self.qkv_proj(x))
@@ -153,16 +163,23 @@ class GPTMLP(nn.Layer):
             self.fc1 = nn.Linear(h, f, nn.ParamAttr(initializer=init))
             self.fc2 = nn.Linear(f, h, nn.ParamAttr(initializer=out_init))
             self._fused = True
+        self.mp = cfg.mp_degree
 
     def forward_nobias(self, x):
         """fc2(gelu(fc1 x)) without fc2's bias (fused into the next kernel). On the device the
-        bias+GELU and its backward live in the GEMM epilogues (K.mlp_gelu)."""
+        bias+GELU and its backward live in the GEMM epilogues (K.mlp_gelu). Under TP fc1/fc2
+        are the rank's column/row shards: identity-in (grad all-reduce), all-reduce out."""
         t = _u(x)
+        if self.mp > 1:
+            t = _mp()._Identity.apply(t, self.fc1.model_parallel_group)
         if t.is_cuda:
-            return Tensor(K.mlp_gelu(t, self.fc1.weight._t, self.fc1.bias._t, self.fc2.weight._t,
-                                     self.approx))
-        hdn = K.bias_gelu(K.linear(t, self.fc1.weight._t), self.fc1.bias._t, self.approx)
-        return Tensor(K.linear(hdn, self.fc2.weight._t))
+            o = K.mlp_gelu(t, self.fc1.weight._t, self.fc1.bias._t, self.fc2.weight._t, self.approx)
+        else:
+            hdn = K.bias_gelu(K.linear(t, self.fc1.weight._t), self.fc1.bias._t, self.approx)
+            o = K.linear(hdn, self.fc2.weight._t)
+        if self.mp > 1:
+            o = _mp()._AllReduce.apply(o, self.fc2.model_parallel_group)
+        return Tensor(o)
 
     def forward(self, x):
         if self._fused:
@@ -183,7 +200,7 @@ class GPTBlock(nn.Layer):
         self.mlp = GPTMLP(cfg)
         self.p = cfg.hidden_dropout
         self.eps = cfg.layer_norm_eps
-        self.fused = cfg.mp_degree == 1
+        self.fused = True
 
     def _drop(self, t):
         if self.p > 0 and self.training:

@@ -26,6 +26,10 @@ void pra_softmax_bwd(const void*, const void*, void*, int, int, int, hipStream_t
 void pra_softmax_ce_fwd(const void*, const int64_t*, float*, float*, int, int, int, int, hipStream_t);
 void pra_softmax_ce_bwd(const void*, const int64_t*, const float*, const float*, void*, int, int, int, int,
                         hipStream_t);
+void pra_vp_ce_part_fwd(const void*, const int64_t*, float*, int, int, int64_t, int, hipStream_t);
+void pra_vp_ce_final(const float*, const int64_t*, float*, float*, int, int, int64_t, int, hipStream_t);
+void pra_vp_ce_bwd(const void*, const int64_t*, const float*, const float*, void*, int, int, int64_t, int64_t, int,
+                   int, hipStream_t);
 void pra_bias_gelu_fwd(const void*, const void*, void*, int64_t, int, int, int, hipStream_t);
 void pra_bias_gelu_bwd(const void*, const void*, const void*, void*, int64_t, int, int, int, hipStream_t);
 void pra_adamw_mt(const int64_t*, const float*, const int64_t*, int, float, float, float, float, float, float, float,
@@ -133,6 +137,19 @@ PYBIND11_MODULE(_pra_hip, m) {
   m.def("softmax_ce_bwd", [](P logits, P labels, P lse, P dloss, P dl, int rows, int V_, int ign, int dt, P s) {
     pra_softmax_ce_bwd(CV(logits), I64(labels), CF(lse), CF(dloss), V(dl), rows, V_, ign, dt, S(s));
     check_launch("softmax_ce_bwd");
+  });
+  m.def("vp_ce_part_fwd", [](P logits, P labels, P stats, int rows, int V_, int64_t start, int dt, P s) {
+    pra_vp_ce_part_fwd(CV(logits), I64(labels), F(stats), rows, V_, start, dt, S(s));
+    check_launch("vp_ce_part_fwd");
+  });
+  m.def("vp_ce_final", [](P stats, P labels, P loss, P lse, int rows, int world, int64_t vtot, int ign, P s) {
+    pra_vp_ce_final(CF(stats), I64(labels), F(loss), F(lse), rows, world, vtot, ign, S(s));
+    check_launch("vp_ce_final");
+  });
+  m.def("vp_ce_bwd", [](P logits, P labels, P lse, P dloss, P dl, int rows, int V_, int64_t start, int64_t vtot,
+                        int ign, int dt, P s) {
+    pra_vp_ce_bwd(CV(logits), I64(labels), CF(lse), CF(dloss), V(dl), rows, V_, start, vtot, ign, dt, S(s));
+    check_launch("vp_ce_bwd");
   });
   m.def("bias_gelu_fwd", [](P x, P b, P y, int64_t rows, int cols, int dt, int approx, P s) {
     pra_bias_gelu_fwd(CV(x), CV(b), V(y), rows, cols, dt, approx, S(s));

@@ -129,16 +129,58 @@ __global__ void __launch_bounds__(256) ce_fwd_k(const T* __restrict__ logits, co
   }
 }
 
+// Vocab-parallel CE, pass 1: this rank's slice [start, start + V) of each row gives its
+// partial (max, sum exp(x - max), picked logit) — 3 floats/row, all-gathered over the TP
+// group (a [world, rows, 3] tensor) instead of reducing [rows, V] probabilities.
 template <typename T>
-__global__ void __launch_bounds__(256) ce_bwd_k(const T* __restrict__ logits, const int64_t* __restrict__ labels,
+__global__ void __launch_bounds__(256) ce_part_fwd_k(const T* __restrict__ logits, const int64_t* __restrict__ labels,
+                                                     float* __restrict__ stats, int V, int64_t start) {
+  __shared__ float red[32];
+  const size_t row = blockIdx.x;
+  const T* xr = logits + row * V;
+  float m, s;
+  row_ms<T>(xr, V, m, s);
+  block_ms(m, s, red);
+  if (threadIdx.x == 0) {
+    const int64_t lab = labels[row] - start;
+    stats[row * 3 + 0] = m;
+    stats[row * 3 + 1] = s;
+    stats[row * 3 + 2] = (lab >= 0 && lab < V) ? Cvt<T>::to(xr[lab]) : 0.f;
+  }
+}
+
+// pass 2: combine the world's partials per row -> loss, lse (one thread per row).
+__global__ void __launch_bounds__(256) ce_part_final_k(const float* __restrict__ stats, const int64_t* __restrict__ labels,
+                                                       float* __restrict__ loss, float* __restrict__ lse_out, int rows,
+                                                       int world, int64_t vtot, int ignore_index) {
+  const int row = blockIdx.x * blockDim.x + threadIdx.x;
+  if (row >= rows) return;
+  float m = -INFINITY, s = 0.f, picked = 0.f;
+  for (int r = 0; r < world; ++r) {
+    const float* st = stats + ((size_t)r * rows + row) * 3;
+    ms_combine(m, s, st[0], st[1]);
+    picked += st[2];
+  }
+  const float lse = m + __logf(s);
+  lse_out[row] = lse;
+  const int64_t lab = labels[row];
+  loss[row] = (lab == ignore_index || lab < 0 || lab >= vtot) ? 0.f : lse - picked;
+}
+
+// dlogits = (exp(x - lse) - onehot(label - start)) * dloss for this rank's V columns
+// (start = 0, vtot = V for the unsharded op). dl may alias logits (each element is read and
+// written by the same lane).
+template <typename T>
+__global__ void __launch_bounds__(256) ce_bwd_k(const T* logits, const int64_t* __restrict__ labels,
                                                 const float* __restrict__ lse, const float* __restrict__ dloss,
-                                                T* __restrict__ dl, int V, int ignore_index, int gx) {
+                                                T* dl, int V, int ignore_index, int gx, int64_t start, int64_t vtot) {
   const size_t row = blockIdx.x / gx;
   const int part = blockIdx.x % gx;
   const T* xr = logits + row * V;
   T* gr = dl + row * V;
-  const int64_t lab = labels[row];
-  const bool valid = !(lab == ignore_index || lab < 0 || lab >= V);
+  const int64_t glab = labels[row];
+  const bool valid = !(glab == ignore_index || glab < 0 || glab >= vtot);
+  const int64_t lab = glab - start;
   const float g = valid ? dloss[row] : 0.f;
   const float L = lse[row];
   const int stride = gx * blockDim.x * 8;
@@ -196,6 +238,28 @@ void pra_softmax_ce_bwd(const void* logits, const int64_t* labels, const float* 
   if (gx > 8) gx = 8;
   if (gx < 1) gx = 1;
   PRA_DISPATCH_FLOAT(dt, T, hipLaunchKernelGGL((ce_bwd_k<T>), dim3(gx * rows), dim3(256), 0, s, (const T*)logits,
-                                               labels, lse, dloss, (T*)dl, V, ignore_index, gx));
+                                               labels, lse, dloss, (T*)dl, V, ignore_index, gx, (int64_t)0,
+                                               (int64_t)V));
+}
+void pra_vp_ce_part_fwd(const void* logits, const int64_t* labels, float* stats, int rows, int V, int64_t start,
+                        int dt, hipStream_t s) {
+  if (!rows) return;
+  PRA_DISPATCH_FLOAT(dt, T, hipLaunchKernelGGL((ce_part_fwd_k<T>), dim3(rows), dim3(256), 0, s, (const T*)logits,
+                                               labels, stats, V, start));
+}
+void pra_vp_ce_final(const float* stats, const int64_t* labels, float* loss, float* lse, int rows, int world,
+                     int64_t vtot, int ignore_index, hipStream_t s) {
+  if (!rows) return;
+  hipLaunchKernelGGL(ce_part_final_k, dim3((rows + 255) / 256), dim3(256), 0, s, stats, labels, loss, lse, rows,
+                     world, vtot, ignore_index);
+}
+void pra_vp_ce_bwd(const void* logits, const int64_t* labels, const float* lse, const float* dloss, void* dl,
+                   int rows, int V, int64_t start, int64_t vtot, int ignore_index, int dt, hipStream_t s) {
+  if (!rows) return;
+  int gx = (V / 8 + 255) / 256;
+  if (gx > 8) gx = 8;
+  if (gx < 1) gx = 1;
+  PRA_DISPATCH_FLOAT(dt, T, hipLaunchKernelGGL((ce_bwd_k<T>), dim3(gx * rows), dim3(256), 0, s, (const T*)logits,
+                                               labels, lse, dloss, (T*)dl, V, ignore_index, gx, start, vtot));
 }
 }

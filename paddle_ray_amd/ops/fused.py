@@ -498,6 +498,114 @@ def softmax_cross_entropy(logits, labels, ignore_index=-100):
 
 
 # =============================================================================
+# Vocab-parallel softmax + cross-entropy (parity: reference
+# paddle/fluid/operators/collective/c_softmax_with_cross_entropy_op.cu). Each TP rank holds
+# logits[:, start:start+V]; pass 1 reduces its slice to (max, sum-exp, picked) per row, the
+# [rows, 3] partials are all-gathered (3 floats/row/rank instead of any [rows, V] tensor),
+# pass 2 combines them into loss / lse, backward writes (softmax - onehot) * dloss for the
+# local slice in one pass. No fp32 probabilities, no one-hot.
+# =============================================================================
+@R.register_kernel('vp_ce_part_fwd', 'ref')
+def _vp_part_ref(logits, labels, start):
+    lf = logits.float()
+    m = lf.max(-1).values
+    s = torch.exp(lf - m[:, None]).sum(-1)
+    V = lf.shape[1]
+    loc = labels - start
+    inr = (loc >= 0) & (loc < V)
+    picked = lf.gather(-1, loc.clamp(0, V - 1)[:, None]).squeeze(-1) * inr.float()
+    return torch.stack([m, s, picked], -1).contiguous()
+
+
+@R.register_kernel('vp_ce_part_fwd', 'hip')
+def _vp_part_hip(logits, labels, start):
+    rows, V = logits.shape
+    st = torch.empty(rows, 3, device=logits.device, dtype=torch.float32)
+    _native.lib().vp_ce_part_fwd(_ptr(logits), _ptr(labels), _ptr(st), rows, V, int(start),
+                                 _dt(logits), _stream())
+    return st
+
+
+@R.register_kernel('vp_ce_final', 'ref')
+def _vp_final_ref(stats, labels, vtot, ignore_index):
+    m, s, picked = stats[..., 0], stats[..., 1], stats[..., 2]   # [world, rows]
+    M = m.max(0).values
+    lse = M + torch.log((s * torch.exp(m - M)).sum(0))
+    valid = (labels != ignore_index) & (labels >= 0) & (labels < vtot)
+    return torch.where(valid, lse - picked.sum(0), torch.zeros_like(lse)), lse
+
+
+@R.register_kernel('vp_ce_final', 'hip')
+def _vp_final_hip(stats, labels, vtot, ignore_index):
+    world, rows = stats.shape[0], stats.shape[1]
+    loss = torch.empty(rows, device=stats.device, dtype=torch.float32)
+    lse = torch.empty_like(loss)
+    _native.lib().vp_ce_final(_ptr(stats), _ptr(labels), _ptr(loss), _ptr(lse), rows, world,
+                              int(vtot), int(ignore_index), _stream())
+    return loss, lse
+
+
+@R.register_kernel('vp_ce_bwd', 'ref')
+def _vp_bwd_ref(logits, labels, lse, dloss, start, vtot, ignore_index):
+    V = logits.shape[1]
+    g = torch.exp(logits.float() - lse[:, None])
+    loc = labels - start
+    inr = (loc >= 0) & (loc < V)
+    g.scatter_add_(-1, loc.clamp(0, V - 1)[:, None], -inr.float()[:, None])
+    valid = (labels != ignore_index) & (labels >= 0) & (labels < vtot)
+    return (g * (dloss.float() * valid.float())[:, None]).to(logits.dtype)
+
+
+@R.register_kernel('vp_ce_bwd', 'hip')
+def _vp_bwd_hip(logits, labels, lse, dloss, start, vtot, ignore_index):
+    rows, V = logits.shape
+    dl = torch.empty_like(logits)
+    _native.lib().vp_ce_bwd(_ptr(logits), _ptr(labels), _ptr(lse), _ptr(dloss.float().contiguous()),
+                            _ptr(dl), rows, V, int(start), int(vtot), int(ignore_index),
+                            _dt(logits), _stream())
+    return dl
+
+
+class VocabParallelCEFn(torch.autograd.Function):
+    """loss over a vocab dimension sharded across ``pg`` (rank r holds columns
+    [r*V, (r+1)*V)); ``world == 1`` degenerates to the plain fused softmax-CE."""
+
+    @staticmethod
+    def forward(ctx, logits, labels, pg, world, rank, ignore_index):
+        import torch.distributed as dist
+        shp = logits.shape
+        l2 = logits.contiguous().view(-1, shp[-1])
+        lab = labels.contiguous().view(-1).to(torch.int64)
+        V = l2.shape[1]
+        start, vtot = rank * V, world * V
+        part = R.dispatch('vp_ce_part_fwd', l2, l2, lab, start)
+        if world > 1:
+            allp = torch.empty((world,) + tuple(part.shape), dtype=part.dtype, device=part.device)
+            if part.is_cuda:
+                dist.all_gather_into_tensor(allp, part, group=pg)
+            else:  # gloo has no all_gather_into_tensor
+                dist.all_gather(list(allp.unbind(0)), part, group=pg)
+        else:
+            allp = part.unsqueeze(0)
+        loss, lse = R.dispatch('vp_ce_final', allp, allp, lab, vtot, ignore_index)
+        ctx.save_for_backward(l2, lab, lse)
+        ctx.meta = (start, vtot, ignore_index, shp)
+        return loss.view(shp[:-1])
+
+    @staticmethod
+    def backward(ctx, dloss):
+        l2, lab, lse = ctx.saved_tensors
+        start, vtot, ignore_index, shp = ctx.meta
+        g = R.dispatch('vp_ce_bwd', l2, l2, lab, lse, dloss.contiguous().view(-1), start, vtot,
+                       ignore_index)
+        return g.view(shp), None, None, None, None, None
+
+
+def vocab_parallel_cross_entropy(logits, labels, pg=None, world=1, rank=0, ignore_index=-100):
+    return VocabParallelCEFn.apply(logits, labels, pg, world, rank, ignore_index)
+
+
+# =============================================================================
 # bias + GELU
 # =============================================================================
 def _gelu_ref(x, approximate):

@@ -15,6 +15,7 @@ from ..nn.layer.layers import Layer
 from ..nn import functional as F
 from ..nn import initializer as I
 from ..distributed import collective as C
+from ..ops import fused as K
 
 
 def _pg(group):
@@ -194,7 +195,9 @@ def model_parallel_random_seed(seed=None):
     seed = 2048 if seed is None else seed
     _RNG_TRACKER.reset()
     _RNG_TRACKER.add(MODEL_PARALLEL_RNG, seed * 1024 + rank * 100 + 1)
-    torch.manual_seed(seed + 1024 + rank)
+    # the global stream stays identical across the TP group (random.py:104): dropout on the
+    # replicated residual stream must draw the same mask on every mp rank
+    torch.manual_seed(seed)
 
 
 # -- layers -------------------------------------------------------------------------------
@@ -217,11 +220,9 @@ class VocabParallelEmbedding(Layer):
         ids = _u(x)
         if self.world_size == 1:
             return F.embedding(x, self.weight)
-        per = self._size[0]
-        local = ids - self.vocab_start_index
-        mask = (local < 0) | (local >= per)
-        out = torch.nn.functional.embedding(local.masked_fill(mask, 0), self.weight._t)
-        out = out.masked_fill(mask.unsqueeze(-1), 0)
+        # the lookup kernel reads ids outside [0, per) as zero rows and skips them in the
+        # weight gradient: shifting by vocab_start_index IS the vocab-range mask
+        out = K.embedding(ids - self.vocab_start_index, self.weight._t)
         return Tensor(_AllReduce.apply(out, self.model_parallel_group))
 
 
@@ -277,42 +278,6 @@ class RowParallelLinear(Layer):
         return out
 
 
-class _VocabParallelCE(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, logits, labels, group, ignore_index):
-        lf = logits.float()
-        per = lf.shape[-1]
-        start = _rank(group) * per
-        m = lf.max(-1).values
-        if _ws(group) > 1:
-            dist.all_reduce(m, dist.ReduceOp.MAX, group=_pg(group))
-        e = torch.exp(lf - m.unsqueeze(-1))
-        s = e.sum(-1)
-        local = labels - start
-        inr = (local >= 0) & (local < per)
-        picked = torch.where(inr, lf.gather(-1, local.clamp(0, per - 1).unsqueeze(-1)).squeeze(-1),
-                             torch.zeros_like(m))
-        if _ws(group) > 1:
-            dist.all_reduce(s, group=_pg(group))
-            dist.all_reduce(picked, group=_pg(group))
-        loss = torch.log(s) + m - picked
-        valid = labels != ignore_index
-        loss = torch.where(valid, loss, torch.zeros_like(loss))
-        ctx.save_for_backward(e, s, local, inr, valid)
-        ctx.dtype = logits.dtype
-        return loss
-
-    @staticmethod
-    def backward(ctx, g):
-        e, s, local, inr, valid = ctx.saved_tensors
-        p = e / s.unsqueeze(-1)
-        per = p.shape[-1]
-        onehot = torch.nn.functional.one_hot(local.clamp(0, per - 1), per).to(p.dtype) * \
-            inr.unsqueeze(-1).to(p.dtype)
-        grad = (p - onehot) * (g * valid.to(g.dtype)).unsqueeze(-1)
-        return grad.to(ctx.dtype), None, None, None
-
-
 class ParallelCrossEntropy(Layer):
     def __init__(self, mp_group=None, name=None, ignore_index=-100):
         super().__init__()
@@ -323,8 +288,9 @@ class ParallelCrossEntropy(Layer):
         lab = _u(label)
         if lab.dim() == _u(input).dim():
             lab = lab.squeeze(-1)
-        loss = _VocabParallelCE.apply(_u(input), lab.long(), self.model_parallel_group,
-                                      self.ignore_index)
+        g = self.model_parallel_group
+        loss = K.vocab_parallel_cross_entropy(_u(input), lab.long(), _pg(g), _ws(g), _rank(g),
+                                              self.ignore_index)
         return Tensor(loss.unsqueeze(-1))
 
 
