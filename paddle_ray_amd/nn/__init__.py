@@ -25,4 +25,5 @@ from .layer.rnn import (RNNCellBase, SimpleRNNCell, LSTMCell, GRUCell, RNN, BiRN
                         LSTM, GRU)
 from .clip import ClipGradByValue, ClipGradByNorm, ClipGradByGlobalNorm  # noqa
 from . import utils  # noqa
+from .decode import BeamSearchDecoder, dynamic_decode, Decoder  # noqa: E402
 from . import quant  # noqa: E402

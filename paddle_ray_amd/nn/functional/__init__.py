@@ -957,12 +957,89 @@ def ctc_loss(log_probs, labels, input_lengths, label_lengths, blank=0, reduction
     return _w(_reduce(loss, reduction))
 
 
-def rnnt_loss(*a, **k):
-    raise NotImplementedError("rnnt_loss is not available in the MI355X build yet")
+def rnnt_loss(input, label, input_lengths, label_lengths, blank=0, fastemit_lambda=0.001,
+              reduction='mean', name=None):
+    """RNN-Transducer loss (parity: python/paddle/nn/functional/loss.py:1818 rnnt_loss over
+    warp-transducer). ``input`` [B, T, U+1, V] are unnormalised joint-network outputs
+    (log-softmax is applied here, as the reference's GPU path does).
+
+    Forward variable in log space, one vectorised update per time step: within a row t the
+    label recursion alpha[t,u] = logaddexp(alpha[t-1,u] + blank[t-1,u], alpha[t,u-1] +
+    emit[t,u-1]) is a linear recurrence, solved as E[u] + logcumsumexp(a[u] - E[u]) with E
+    the running sum of emission log-probs — T batched kernels instead of T*U scalar steps.
+    Gradients come from autograd through the recursion. FastEmit (arXiv 2010.11148) scales
+    the emission-path gradient by (1 + lambda) and leaves the loss value unchanged."""
+    x = _t(input)
+    lab = _t(label).long()
+    tl, ul = _t(input_lengths).long().to(x.device), _t(label_lengths).long().to(x.device)
+    B, T, U1, V = x.shape
+    lp = torch.log_softmax(x.float() if x.dtype in (torch.float16, torch.bfloat16) else x, -1)
+    blank_lp = lp[..., blank]                                            # [B, T, U+1]
+    U = U1 - 1
+    if U > 0:
+        emit = torch.gather(lp[:, :, :U, :], 3,
+                            lab[:, None, :U, None].expand(B, T, U, 1).clamp_min(0)).squeeze(-1)
+    else:
+        emit = lp.new_zeros(B, T, 0)
+    if fastemit_lambda:
+        emit = emit + fastemit_lambda * (emit - emit.detach())
+    ninf = torch.finfo(lp.dtype).min / 4
+    E = torch.cat([emit.new_zeros(B, T, 1), torch.cumsum(emit, -1)], -1)  # [B, T, U+1]
+    alphas = []
+    a = torch.full((B, U1), ninf, dtype=lp.dtype, device=lp.device)
+    a[:, 0] = 0.0
+    for t in range(T):
+        if t > 0:
+            a = alphas[-1] + blank_lp[:, t - 1]
+        alpha = E[:, t] + torch.logcumsumexp(a - E[:, t], -1)
+        alphas.append(alpha)
+    alpha = torch.stack(alphas, 1)                                        # [B, T, U+1]
+    bi = torch.arange(B, device=lp.device)
+    tT = (tl - 1).clamp_min(0)
+    loss = -(alpha[bi, tT, ul] + blank_lp[bi, tT, ul])
+    if reduction == 'mean':
+        return _w(loss.sum() / B)
+    if reduction == 'sum':
+        return _w(loss.sum())
+    return _w(loss)
 
 
-def hsigmoid_loss(*a, **k):
-    raise NotImplementedError("hsigmoid_loss is not available in the MI355X build yet")
+def _hs_default_paths(lab, num_classes):
+    """Default complete-binary-tree codes (matrix_bit_code.h SimpleCode): code = label +
+    num_classes; step j visits node (code >> (j+1)) - 1 with target bit (code >> j) & 1."""
+    L = max(int(num_classes - 1).bit_length(), 1)
+    code = lab + num_classes
+    j = torch.arange(L, device=lab.device)
+    node = (code[:, None] >> (j + 1)) - 1
+    bit = (code[:, None] >> j) & 1
+    valid = node >= 0
+    return node, bit, valid
+
+
+def hsigmoid_loss(input, label, num_classes, weight, bias=None, path_table=None,
+                  path_code=None, is_sparse=False, name=None):
+    """Hierarchical sigmoid (parity: python/paddle/nn/functional/loss.py hsigmoid_loss over
+    phi hierarchical_sigmoid kernel). Returns [N, 1]: per sample the sum over its tree path
+    of softplus(pre) - bit * pre, pre = clip(x . W[node] + b[node], -40, 40). Like the
+    reference kernel, padded path slots (shorter paths of the default tree) contribute
+    softplus(0) = log 2 each; custom trees pass ``path_table``/``path_code`` ([N, L], -1
+    terminated). One batched gather + contraction, no per-sample loop."""
+    x = _t(input)
+    lab = _t(label).long().reshape(-1)
+    W = _t(weight)
+    if path_table is not None:
+        node = _t(path_table).long()
+        bit = _t(path_code).long()
+        valid = torch.cumprod((node >= 0).long(), -1).bool()
+    else:
+        node, bit, valid = _hs_default_paths(lab, num_classes)
+    safe = node.clamp_min(0)
+    pre = torch.einsum('nd,nld->nl', x, W[safe])
+    if bias is not None:
+        pre = pre + _t(bias).reshape(-1)[safe]
+    pre = torch.where(valid, pre, torch.zeros_like(pre)).clamp(-40.0, 40.0)
+    out = TF.softplus(pre).sum(-1) - (pre * (bit * valid).to(pre.dtype)).sum(-1)
+    return _w(out.unsqueeze(-1))
 
 
 def margin_cross_entropy(logits, label, margin1=1.0, margin2=0.5, margin3=0.0, scale=64.0,

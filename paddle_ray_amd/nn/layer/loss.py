@@ -74,10 +74,33 @@ class NLLLoss(Layer):
 
 
 class RNNTLoss(Layer):
-    def forward(self, *a):
-        return F.rnnt_loss(*a)
+    """parity: python/paddle/nn/layer/loss.py RNNTLoss."""
+
+    def __init__(self, blank=0, fastemit_lambda=0.001, reduction='mean', name=None):
+        super().__init__()
+        self.blank, self.fastemit_lambda, self.reduction = blank, fastemit_lambda, reduction
+
+    def forward(self, input, label, input_lengths, label_lengths):
+        return F.rnnt_loss(input, label, input_lengths, label_lengths, blank=self.blank,
+                           fastemit_lambda=self.fastemit_lambda, reduction=self.reduction)
 
 
 class HSigmoidLoss(Layer):
-    def forward(self, *a):
-        return F.hsigmoid_loss(*a)
+    """parity: python/paddle/nn/layer/loss.py HSigmoidLoss — weight [C, feature_size],
+    bias [C, 1] with C = num_classes - 1 (default tree) or num_classes (custom tree)."""
+
+    def __init__(self, feature_size, num_classes, weight_attr=None, bias_attr=None,
+                 is_custom=False, is_sparse=False, name=None):
+        super().__init__()
+        if num_classes < 2 and not is_custom:
+            raise ValueError("num_classes must not be less than 2 with default tree")
+        self._num_classes, self._is_custom, self._is_sparse = num_classes, is_custom, is_sparse
+        C = num_classes if is_custom else num_classes - 1
+        self.weight = self.create_parameter([C, feature_size], attr=weight_attr)
+        self.bias = None if bias_attr is False else \
+            self.create_parameter([C, 1], attr=bias_attr, is_bias=True)
+
+    def forward(self, input, label, path_table=None, path_code=None):
+        return F.hsigmoid_loss(input, label, self._num_classes, self.weight, self.bias,
+                               path_table=path_table, path_code=path_code,
+                               is_sparse=self._is_sparse)

@@ -41,4 +41,6 @@ def run_check():
 
 
 from . import unique_name  # noqa
+from .layers_utils import (flatten, pack_sequence_as, map_structure,  # noqa
+                           assert_same_structure, is_sequence)
 from .dlpack import to_dlpack, from_dlpack  # noqa
