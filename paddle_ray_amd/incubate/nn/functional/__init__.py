@@ -63,9 +63,19 @@ def fused_dropout_add(x, y, p=0.5, training=True, mode='upscale_in_train', name=
 def fused_bias_dropout_residual_layer_norm(x, residual, bias=None, ln_scale=None, ln_bias=None,
                                            dropout_rate=0.5, ln_epsilon=1e-5, training=True,
                                            mode='upscale_in_train', name=None):
-    h = _u(x) if bias is None else _u(x) + _u(bias)
-    h = _u(residual) + _drop(h, dropout_rate, training, mode)
-    return Tensor(_ln(h, ln_scale, ln_bias, ln_epsilon))
+    """LayerNorm(residual + dropout(x + bias)) as ONE add_dropout_layer_norm kernel pass
+    (upscale_in_train; the downscale_in_infer variant composes)."""
+    t, r = _u(x), _u(residual)
+    if mode != 'upscale_in_train':
+        h = t if bias is None else t + _u(bias)
+        return Tensor(_ln(r + _drop(h, dropout_rate, training, mode), ln_scale, ln_bias,
+                          ln_epsilon))
+    E = t.shape[-1]
+    b = _u(bias) if bias is not None else torch.zeros(E, dtype=t.dtype, device=t.device)
+    w = _u(ln_scale) if ln_scale is not None else torch.ones(E, dtype=t.dtype, device=t.device)
+    lb = _u(ln_bias) if ln_bias is not None else torch.zeros(E, dtype=t.dtype, device=t.device)
+    _, y = K.add_dropout_layer_norm(r, t, b, w, lb, dropout_rate, ln_epsilon, training)
+    return Tensor(y)
 
 
 def fused_multi_head_attention(x, qkv_weight, linear_weight, pre_layer_norm=False,
@@ -100,6 +110,12 @@ def fused_multi_head_attention(x, qkv_weight, linear_weight, pre_layer_norm=Fals
     if attn_mask is None and (attn_dropout_rate == 0 or not training) and t.is_cuda and \
             t.dtype in (torch.bfloat16, torch.float16):
         o = K.flash_attention(q, k, v, causal=False)
+    elif mode == 'upscale_in_train':
+        # masked / dropout attention: fused SDPA (no [B, H, S, S] fp32 score tensor)
+        am = None if attn_mask is None else _u(attn_mask).to(q.dtype)
+        o = torch.nn.functional.scaled_dot_product_attention(
+            q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2), am,
+            attn_dropout_rate if training else 0.0).transpose(1, 2)
     else:
         s = torch.einsum('bqnd,bknd->bnqk', q, k) / math.sqrt(hd)
         if attn_mask is not None:
@@ -147,26 +163,155 @@ def fused_feedforward(x, linear1_weight, linear2_weight, linear1_bias=None, line
     return Tensor(h)
 
 
+def _rotary(x, cos, sin, dims):
+    """Half-split rotation inside each of ``dims`` chunks of the head dim (reference
+    RotrayKernel / mmha rotary): x [B, S, H, D], cos/sin [B, S, D]."""
+    B, S, H, D = x.shape
+    last = D // dims
+    half = last // 2
+    xv = x.float().view(B, S, H, dims, last)
+    c = cos.float().view(B, S, 1, dims, last)
+    sn = sin.float().view(B, S, 1, dims, last)
+    left, right = xv[..., :half], xv[..., half:]
+    out = torch.cat([left * c[..., :half] - right * sn[..., :half],
+                     right * c[..., half:] + left * sn[..., half:]], -1)
+    return out.view(B, S, H, D).to(x.dtype)
+
+
+def _qkv(y, w, b, trans_qkvw):
+    B, S, E = y.shape
+    if trans_qkvw:                       # [3, H, D, E]
+        _, H, D, _ = w.shape
+        out = K.linear_nt(y.reshape(B * S, E), w.reshape(3 * H * D, E))
+    else:                                # [E, 3, H, D]
+        _, _, H, D = w.shape
+        out = K.linear(y.reshape(B * S, E), w.reshape(E, 3 * H * D))
+    if b is not None:
+        out = out + b.reshape(-1).to(out.dtype)
+    return out.view(B, S, 3, H, D)
+
+
+def _ones_zeros(t, n, like):
+    return t if t is not None else (torch.ones(n, dtype=like.dtype, device=like.device) if n
+                                     else None)
+
+
 def fused_multi_transformer(x, ln_scales, ln_biases, qkv_weights, qkv_biases, linear_weights,
                             linear_biases, ffn_ln_scales, ffn_ln_biases, ffn1_weights, ffn1_biases,
                             ffn2_weights, ffn2_biases, pre_layer_norm=True, epsilon=1e-05,
-                            cache_kvs=None, time_step=None, attn_mask=None, dropout_rate=0.0,
+                            cache_kvs=None, pre_caches=None, seq_lens=None, rotary_embs=None,
+                            time_step=None, attn_mask=None, dropout_rate=0.0, rotary_emb_dims=0,
                             activation="gelu", training=False, mode='upscale_in_train',
                             trans_qkvw=True, ring_id=-1, name=None):
-    h = x
-    for i in range(len(qkv_weights)):
-        h = fused_multi_head_attention(h, qkv_weights[i], linear_weights[i], pre_layer_norm,
-                                       ln_scales[i], ln_biases[i], None, None, epsilon,
-                                       qkv_biases[i] if qkv_biases else None,
-                                       linear_biases[i] if linear_biases else None, None,
-                                       attn_mask, dropout_rate, dropout_rate, epsilon, training,
-                                       mode)
-        h = fused_feedforward(h, ffn1_weights[i], ffn2_weights[i],
-                              ffn1_biases[i] if ffn1_biases else None,
-                              ffn2_biases[i] if ffn2_biases else None, ffn_ln_scales[i],
-                              ffn_ln_biases[i], None, None, dropout_rate, dropout_rate,
-                              activation, epsilon, epsilon, pre_layer_norm, training, mode)
-    return h
+    """N transformer layers for inference / generation (parity: reference
+    incubate/nn/functional/fused_transformer.py:872 and fused_multi_transformer_op.cu.h).
+
+    * context phase (``time_step`` None): QKV GEMM, optional rotary, attention over
+      [pre_cache ; prompt] (flash kernel when unmasked, else masked SDPA), and with
+      ``cache_kvs`` ([2, B, H, max_len, D] per layer) the prompt's K/V written in place.
+    * decode phase (``time_step`` = t, x [B, 1, E]): the HIP decode-attention kernel streams
+      cache positions [0, t) split-K across the chip and appends the token's K/V at t.
+    * every residual add + dropout + following LayerNorm is ONE add_dropout_layer_norm
+      kernel; FFN1 runs with its bias+activation in the GEMM epilogue.
+    Returns ``out`` or ``(out, cache_kvs)`` when caches are given (updated in place)."""
+    if mode not in ('downscale_in_infer', 'upscale_in_train'):
+        raise ValueError("mode argument should be 'downscale_in_infer' or 'upscale_in_train'")
+    h = _u(x)
+    B, S, E = h.shape
+    n = len(qkv_weights)
+    p = dropout_rate if training else 0.0
+    decode = time_step is not None
+    t = int(_u(time_step).reshape(-1)[0]) if decode and not isinstance(time_step, int) else \
+        (int(time_step) if decode else None)
+    if decode and S != 1:
+        raise ValueError("fused_multi_transformer: decode phase (time_step given) takes one token")
+    rot = None
+    if rotary_embs is not None and rotary_emb_dims:
+        re = _u(rotary_embs)                          # [2, B, 1, S, D]
+        rot = (re[0].reshape(B, S, -1), re[1].reshape(B, S, -1))
+    mask = _t(attn_mask)
+    sl = _t(seq_lens)
+    zero_b = torch.zeros(E, dtype=h.dtype, device=h.device)
+    one_w = torch.ones(E, dtype=h.dtype, device=h.device)
+
+    def lnp(lst, i, default):
+        return _u(lst[i]) if lst is not None and lst[i] is not None else default
+
+    r = h
+    y = K.layer_norm(h, lnp(ln_scales, 0, one_w), lnp(ln_biases, 0, zero_b), epsilon) \
+        if pre_layer_norm else h
+    for i in range(n):
+        qkv = _qkv(y, _u(qkv_weights[i]), _t(qkv_biases[i]) if qkv_biases else None, trans_qkvw)
+        H, D = qkv.shape[3], qkv.shape[4]
+        if rot is not None:
+            q = _rotary(qkv[:, :, 0], rot[0], rot[1], rotary_emb_dims)
+            k = _rotary(qkv[:, :, 1], rot[0], rot[1], rotary_emb_dims)
+            qkv = torch.stack([q, k, qkv[:, :, 2]], 2)
+        cache = _u(cache_kvs[i]) if cache_kvs is not None else None
+        if decode:
+            if cache is None:
+                raise ValueError("fused_multi_transformer: time_step needs cache_kvs")
+            o = K.mmha_decode(qkv[:, 0].contiguous(), cache, t, mask).reshape(B, 1, H * D)
+        else:
+            q, k, v = qkv.unbind(2)                  # [B, S, H, D]
+            P = 0
+            if pre_caches is not None and pre_caches[i] is not None:
+                pc = _u(pre_caches[i])               # [2, B, H, P, D]
+                P = pc.shape[3]
+                k = torch.cat([pc[0].transpose(1, 2).to(k.dtype), k], 1)
+                v = torch.cat([pc[1].transpose(1, 2).to(v.dtype), v], 1)
+            if cache is not None:
+                cache[0, :, :, :P + S] = k.transpose(1, 2)
+                cache[1, :, :, :P + S] = v.transpose(1, 2)
+            if mask is None and sl is None and h.is_cuda and h.dtype in (torch.bfloat16,
+                                                                         torch.float16):
+                o = K.flash_attention(q.contiguous(), k.contiguous(), v.contiguous(), causal=False)
+            else:
+                am = None if mask is None else mask.to(torch.float32)
+                if sl is not None:
+                    pad = torch.arange(P + S, device=h.device)[None, :] >= \
+                        (sl.reshape(-1, 1).to(h.device) + P)
+                    pm = torch.zeros(B, 1, 1, P + S, device=h.device).masked_fill(
+                        pad[:, None, None, :], float('-inf'))
+                    am = pm if am is None else am + pm
+                o = torch.nn.functional.scaled_dot_product_attention(
+                    q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2),
+                    None if am is None else am.to(q.dtype), p)
+                o = o.transpose(1, 2)
+            o = o.reshape(B, S, H * D)
+        a = K.linear(o, _u(linear_weights[i]))
+        lb = _t(linear_biases[i]) if linear_biases else None
+        lb = zero_b if lb is None else lb
+        if pre_layer_norm:
+            r, y = K.add_dropout_layer_norm(r, a, lb, lnp(ffn_ln_scales, i, one_w),
+                                            lnp(ffn_ln_biases, i, zero_b), p, epsilon, training)
+        else:
+            _, r = K.add_dropout_layer_norm(r, a, lb, lnp(ln_scales, i, one_w),
+                                            lnp(ln_biases, i, zero_b), p, epsilon, training)
+            y = r
+        b1 = _t(ffn1_biases[i]) if ffn1_biases else None
+        f = K.gemm_bias_act(y, _u(ffn1_weights[i]), b1, 'gelu' if activation == 'gelu' else
+                            activation)
+        if p:
+            f = torch.nn.functional.dropout(f, p, True)
+        f = K.linear(f, _u(ffn2_weights[i]))
+        b2 = _t(ffn2_biases[i]) if ffn2_biases else None
+        b2 = zero_b if b2 is None else b2
+        if pre_layer_norm:
+            if i + 1 < n:
+                r, y = K.add_dropout_layer_norm(r, f, b2, lnp(ln_scales, i + 1, one_w),
+                                                lnp(ln_biases, i + 1, zero_b), p, epsilon,
+                                                training)
+            else:
+                r = r + _drop(f + b2, p, training, mode)
+        else:
+            _, r = K.add_dropout_layer_norm(r, f, b2, lnp(ffn_ln_scales, i, one_w),
+                                            lnp(ffn_ln_biases, i, zero_b), p, epsilon, training)
+            y = r
+    out = Tensor(r)
+    if cache_kvs is not None:
+        return out, cache_kvs
+    return out
 
 
 def fused_ec_moe(x, gate, bmm0_weight, bmm0_bias, bmm1_weight, bmm1_bias, act_type):

@@ -130,20 +130,68 @@ class FusedTransformerEncoderLayer(Layer):
 
 
 class FusedMultiTransformer(Layer):
-    def __init__(self, embed_dim, num_heads, dim_feedforward, dropout_rate=0.0, activation="gelu",
-                 normalize_before=True, num_layers=1, epsilon=1e-5, **kw):
-        super().__init__()
-        self.layers = [FusedTransformerEncoderLayer(embed_dim, num_heads, dim_feedforward,
-                                                    dropout_rate, activation,
-                                                    normalize_before=normalize_before)
-                       for _ in range(num_layers)]
-        for i, l in enumerate(self.layers):
-            self.add_sublayer(str(i), l)
+    """Stack of pre/post-LN transformer layers for inference and generation, parameters in
+    the reference layout (parity: python/paddle/incubate/nn/layer/fused_transformer.py
+    FusedMultiTransformer): qkv [3, H, D, E], linear [E, E], ffn1 [E, F], ffn2 [F, E].
+    ``forward(src, attn_mask, caches, ..., time_step)`` runs the context phase (caches
+    filled in place) or, with ``time_step``, one decode step on the HIP cache kernel."""
 
-    def forward(self, src, attn_mask=None, caches=None, time_step=None):
-        for l in self.layers:
-            src = l(src, attn_mask)
-        return src
+    def __init__(self, embed_dim, num_heads, dim_feedforward, dropout_rate=0.0, activation="gelu",
+                 normalize_before=True, ln_scale_attrs=None, ln_bias_attrs=None,
+                 qkv_weight_attrs=None, qkv_bias_attrs=None, linear_weight_attrs=None,
+                 linear_bias_attrs=None, ffn_ln_scale_attrs=None, ffn_ln_bias_attrs=None,
+                 ffn1_weight_attrs=None, ffn1_bias_attrs=None, ffn2_weight_attrs=None,
+                 ffn2_bias_attrs=None, epsilon=1e-5, num_layers=-1, nranks=1,
+                 trans_qkvw=True, ring_id=-1, name=None):
+        super().__init__()
+        if num_layers < 0:
+            num_layers = len(qkv_weight_attrs) if isinstance(qkv_weight_attrs, (list, tuple)) else 1
+        assert embed_dim % num_heads == 0
+        self.embed_dim, self.num_heads = embed_dim, num_heads
+        self.head_dim = embed_dim // num_heads
+        self.normalize_before, self._epsilon = normalize_before, epsilon
+        self.dropout_rate, self.activation, self._trans_qkvw = dropout_rate, activation, trans_qkvw
+        one = I.Constant(1.0)
+
+        def attr(a, i):
+            return a[i] if isinstance(a, (list, tuple)) else a
+        names = ('ln_scales', 'ln_biases', 'qkv_weights', 'qkv_biases', 'linear_weights',
+                 'linear_biases', 'ffn_ln_scales', 'ffn_ln_biases', 'ffn1_weights', 'ffn1_biases',
+                 'ffn2_weights', 'ffn2_biases')
+        for n in names:
+            setattr(self, n, [])
+        E, H, D, F = embed_dim, num_heads, self.head_dim, dim_feedforward
+        qkv_shape = [3, H, D, E] if trans_qkvw else [E, 3, H, D]
+        for i in range(num_layers):
+            specs = (
+                ('ln_scales', [E], ln_scale_attrs, False, one),
+                ('ln_biases', [E], ln_bias_attrs, True, None),
+                ('qkv_weights', qkv_shape, qkv_weight_attrs, False, None),
+                ('qkv_biases', [3, H, D], qkv_bias_attrs, True, None),
+                ('linear_weights', [E, E], linear_weight_attrs, False, None),
+                ('linear_biases', [E], linear_bias_attrs, True, None),
+                ('ffn_ln_scales', [E], ffn_ln_scale_attrs, False, one),
+                ('ffn_ln_biases', [E], ffn_ln_bias_attrs, True, None),
+                ('ffn1_weights', [E, F], ffn1_weight_attrs, False, None),
+                ('ffn1_biases', [F], ffn1_bias_attrs, True, None),
+                ('ffn2_weights', [F, E], ffn2_weight_attrs, False, None),
+                ('ffn2_biases', [E], ffn2_bias_attrs, True, None))
+            for n, shp, a, is_bias, init in specs:
+                p = self.create_parameter(shp, attr(a, i), is_bias=is_bias, default_initializer=init)
+                self.add_parameter(f'{n}_{i}', p)
+                getattr(self, n).append(p)
+
+    def forward(self, src, attn_mask=None, caches=None, pre_caches=None, rotary_embs=None,
+                rotary_emb_dims=0, seq_lens=None, time_step=None):
+        return FF.fused_multi_transformer(
+            src, self.ln_scales, self.ln_biases, self.qkv_weights, self.qkv_biases,
+            self.linear_weights, self.linear_biases, self.ffn_ln_scales, self.ffn_ln_biases,
+            self.ffn1_weights, self.ffn1_biases, self.ffn2_weights, self.ffn2_biases,
+            pre_layer_norm=self.normalize_before, epsilon=self._epsilon, cache_kvs=caches,
+            pre_caches=pre_caches, seq_lens=seq_lens, rotary_embs=rotary_embs,
+            time_step=time_step, attn_mask=attn_mask, dropout_rate=self.dropout_rate,
+            rotary_emb_dims=rotary_emb_dims, activation=self.activation, training=self.training,
+            trans_qkvw=self._trans_qkvw)
 
 
 class FusedEcMoe(Layer):

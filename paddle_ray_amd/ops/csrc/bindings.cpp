@@ -30,6 +30,9 @@ void pra_vp_ce_part_fwd(const void*, const int64_t*, float*, int, int, int64_t, 
 void pra_vp_ce_final(const float*, const int64_t*, float*, float*, int, int, int64_t, int, hipStream_t);
 void pra_vp_ce_bwd(const void*, const int64_t*, const float*, const float*, void*, int, int, int64_t, int64_t, int,
                    int, hipStream_t);
+int pra_mmha_splits(int, int, int);
+int pra_mmha_decode(const void*, void*, const float*, float*, void*, int, int, int, int, int, int, int, float, int,
+                    hipStream_t);
 void pra_bias_gelu_fwd(const void*, const void*, void*, int64_t, int, int, int, hipStream_t);
 void pra_bias_gelu_bwd(const void*, const void*, const void*, void*, int64_t, int, int, int, hipStream_t);
 void pra_adamw_mt(const int64_t*, const float*, const int64_t*, int, float, float, float, float, float, float, float,
@@ -150,6 +153,14 @@ PYBIND11_MODULE(_pra_hip, m) {
                         int ign, int dt, P s) {
     pra_vp_ce_bwd(CV(logits), I64(labels), CF(lse), CF(dloss), V(dl), rows, V_, start, vtot, ign, dt, S(s));
     check_launch("vp_ce_bwd");
+  });
+  m.def("mmha_splits", [](int B, int H, int t) { return pra_mmha_splits(B, H, t); });
+  m.def("mmha_decode", [](P qkv, P cache, P mask, P ws, P out, int B, int H, int L, int D, int t, int splits,
+                          int mask_len, float scale, int dt, P s) {
+    if (pra_mmha_decode(CV(qkv), V(cache), CF(mask), F(ws), V(out), B, H, L, D, t, splits, mask_len, scale, dt,
+                        S(s)) != 0)
+      throw std::invalid_argument("mmha_decode: unsupported head_dim/dtype or time_step out of range");
+    check_launch("mmha_decode");
   });
   m.def("bias_gelu_fwd", [](P x, P b, P y, int64_t rows, int cols, int dt, int approx, P s) {
     pra_bias_gelu_fwd(CV(x), CV(b), V(y), rows, cols, dt, approx, S(s));

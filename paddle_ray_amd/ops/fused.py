@@ -606,6 +606,55 @@ def vocab_parallel_cross_entropy(logits, labels, pg=None, world=1, rank=0, ignor
 
 
 # =============================================================================
+# Decode-phase attention over a KV cache (decode_attn.hip; parity: the reference's masked
+# multihead attention kernel of fused_multi_transformer). qkv [B, 3, H, D] is the current
+# token's projection, cache [2, B, H, L, D]; positions [0, t) are read from the cache, the
+# token's own K/V are written into it at position t. Inference only (no autograd).
+# =============================================================================
+@R.register_kernel('mmha_decode', 'ref')
+def _mmha_ref(qkv, cache, t, mask):
+    q, k, v = qkv.unbind(1)                                   # [B, H, D]
+    cache[0, :, :, t] = k
+    cache[1, :, :, t] = v
+    K_, V_ = cache[0, :, :, :t + 1].float(), cache[1, :, :, :t + 1].float()
+    s = torch.einsum('bhd,bhld->bhl', q.float(), K_) / math.sqrt(q.shape[-1])
+    if mask is not None:
+        s = s + mask.reshape(mask.shape[0], -1)[:, None, :t + 1].float()
+    p = torch.softmax(s, -1)
+    return torch.einsum('bhl,bhld->bhd', p, V_).to(qkv.dtype)
+
+
+@R.register_kernel('mmha_decode', 'hip')
+def _mmha_hip(qkv, cache, t, mask):
+    B, _, H, D = qkv.shape
+    L = cache.shape[3]
+    if not (qkv.is_contiguous() and cache.is_contiguous() and cache.dtype == qkv.dtype and
+            tuple(cache.shape) == (2, B, H, L, D) and D in (64, 128, 256) and 0 <= t < L):
+        raise ValueError(f"mmha_decode: qkv {tuple(qkv.shape)} / cache {tuple(cache.shape)} / "
+                         f"t={t} not supported by the HIP kernel")
+    splits = _native.lib().mmha_splits(B, H, t)
+    ws = torch.empty(B * H * splits * (2 + D) + 4 if splits > 1 else 4, device=qkv.device,
+                     dtype=torch.float32)
+    out = torch.empty(B, H, D, device=qkv.device, dtype=qkv.dtype)
+    mlen = 0
+    if mask is not None:
+        mask = mask.reshape(B, -1).float().contiguous()
+        mlen = mask.shape[1]
+        if mlen < t + 1:
+            raise ValueError(f"mmha_decode: mask covers {mlen} positions, need {t + 1}")
+    _native.lib().mmha_decode(_ptr(qkv), _ptr(cache), _ptr(mask) if mask is not None else 0,
+                              _ptr(ws), _ptr(out), B, H, L, D, int(t), splits, mlen,
+                              1.0 / math.sqrt(D), _dt(qkv), _stream())
+    return out
+
+
+def mmha_decode(qkv, cache, time_step, mask=None):
+    """One decode step of multi-head attention; returns [B, H, D] and appends K/V to
+    ``cache`` at ``time_step`` in place."""
+    return R.dispatch('mmha_decode', qkv, qkv.contiguous(), cache, int(time_step), mask)
+
+
+# =============================================================================
 # bias + GELU
 # =============================================================================
 def _gelu_ref(x, approximate):
