@@ -69,7 +69,15 @@ def test_context_phase_matches_pseudo_code(pre_ln):
                                atol=2e-4)
 
 
-def _generate_vs_full(m, B, S0, steps, device='cpu', dtype=torch.float32, tol=2e-4):
+def _close(a, b, tol):
+    """max error relative to the tensor's scale (bf16 rounds ~2^-8 of each value's magnitude;
+    element-wise rtol is meaningless for entries near zero)."""
+    a, b = a.float(), b.float()
+    err = float((a - b).abs().max()) / max(float(b.abs().max()), 1e-6)
+    assert err < tol, err
+
+
+def _generate_vs_full(m, B, S0, steps, device='cpu', dtype=torch.float32, tol=2e-5):
     E, H = m.embed_dim, m.num_heads
     D = E // H
     L = len(m.qkv_weights)
@@ -79,12 +87,12 @@ def _generate_vs_full(m, B, S0, steps, device='cpu', dtype=torch.float32, tol=2e
               for _ in range(L)]
     out, caches = m(paddle.Tensor(x[:, :S0]), attn_mask=paddle.Tensor(_causal(S0, B).to(device, dtype)),
                     caches=caches)
-    torch.testing.assert_close(out._t.float(), full[:, :S0].float(), rtol=tol, atol=tol)
+    _close(out._t, full[:, :S0], tol)
     for t in range(S0, S0 + steps):
         mask = torch.zeros(B, 1, 1, t + 1, device=device)
         out, caches = m(paddle.Tensor(x[:, t:t + 1]), attn_mask=paddle.Tensor(mask), caches=caches,
                         time_step=paddle.to_tensor(np.array([t], 'int32')))
-        torch.testing.assert_close(out._t[:, 0].float(), full[:, t].float(), rtol=tol, atol=tol)
+        _close(out._t[:, 0], full[:, t], tol)
     return caches
 
 
@@ -166,4 +174,4 @@ def test_generation_on_gpu_bf16():
     paddle.set_device('gpu')
     m = _model(True, E=256, H=2, F=512, L=2)       # head_dim 128
     m.to(dtype='bfloat16')
-    _generate_vs_full(m, 2, 9, 6, device='cuda', dtype=torch.bfloat16, tol=6e-2)
+    _generate_vs_full(m, 2, 9, 6, device='cuda', dtype=torch.bfloat16, tol=2e-2)
