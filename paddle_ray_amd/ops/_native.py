@@ -21,10 +21,32 @@ def _load():
         spec = importlib.util.spec_from_file_location('paddle_ray_amd.ops._pra_hip', cands[0])
         mod = importlib.util.module_from_spec(spec)
         spec.loader.exec_module(mod)
+        _check_provenance(mod)
         _lib = mod
     except Exception as e:  # pragma: no cover - depends on runtime libs
         _err = e
     return _lib
+
+
+def build_info():
+    import json
+    return json.loads(lib().build_info())
+
+
+def _check_provenance(mod):
+    """Refuse a library that was not built from the sources beside it (a stale build or a
+    foreign binary): the hash compiled into the .so must match csrc/ as it is now. Set
+    PRA_SKIP_PROVENANCE=1 to bypass (e.g. an installed wheel without sources)."""
+    import json
+    if os.environ.get('PRA_SKIP_PROVENANCE') == '1' or not os.path.isdir(os.path.join(_HERE, 'csrc')):
+        return
+    from .build import sources_hash
+    info = json.loads(mod.build_info())
+    want = sources_hash()
+    if info.get('sources_sha256') != want:
+        raise ImportError(f"_pra_hip was built from different sources (library "
+                          f"{info.get('sources_sha256', '?')[:12]}, csrc/ {want[:12]}); rebuild "
+                          f"with `python -m paddle_ray_amd.ops.build`")
 
 
 def available():

@@ -6,8 +6,16 @@ Each ``csrc/*.hip`` is compiled with ``hipcc --offload-arch=gfx950 -O3``; the
 pybind11 binding is compiled by hipcc as host code; everything is linked into
 ``paddle_ray_amd/ops/_pra_hip<EXT_SUFFIX>`` which travels with the repo
 snapshot to the GPU box (built .so files are git-ignored).
+
+Provenance: objects are rebuilt when the SHA-256 of their source (+ common.h + the exact
+compile command) changes — content, not mtimes — and the linked library embeds
+``pra_build_info()`` = {sources hash, arch, hipcc version}. ``_native`` compares that hash
+with the sources next to it at load time, so a stale or foreign binary is refused instead
+of silently running.
 """
 import concurrent.futures as cf
+import hashlib
+import json
 import os
 import subprocess
 import sys
@@ -24,11 +32,29 @@ def _out_path():
     return os.path.join(HERE, '_pra_hip' + sysconfig.get_config_var('EXT_SUFFIX'))
 
 
-def _needs(obj, srcs):
-    if not os.path.exists(obj):
-        return True
-    t = os.path.getmtime(obj)
-    return any(os.path.getmtime(s) > t for s in srcs)
+def _digest(paths, cmd=()):
+    h = hashlib.sha256()
+    for p in paths:
+        h.update(os.path.basename(p).encode())
+        with open(p, 'rb') as f:
+            h.update(f.read())
+    h.update('\0'.join(cmd).encode())
+    return h.hexdigest()
+
+
+def sources_hash():
+    """Hash of every source that goes into the library (what build_info() must match)."""
+    files = sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC)
+                   if f.endswith(('.hip', '.h', '.cpp')))
+    return _digest(files, (ARCH,))
+
+
+def _manifest_path():
+    return os.path.join(BUILD, 'manifest.json')
+
+
+def _needs(obj, key, manifest):
+    return not os.path.exists(obj) or manifest.get(os.path.basename(obj)) != key
 
 
 def _run(cmd):
@@ -38,34 +64,69 @@ def _run(cmd):
     return r
 
 
+def _hipcc_version():
+    try:
+        r = subprocess.run([HIPCC, '--version'], capture_output=True, text=True)
+        for line in r.stdout.splitlines():
+            if 'HIP version' in line:
+                return line.split(':', 1)[1].strip()
+    except OSError:
+        pass
+    return 'unknown'
+
+
 def build(force=False, verbose=True):
     import pybind11
     os.makedirs(BUILD, exist_ok=True)
+    try:
+        with open(_manifest_path()) as f:
+            manifest = json.load(f)
+    except (OSError, ValueError):
+        manifest = {}
     common = os.path.join(CSRC, 'common.h')
     hip_srcs = sorted(f for f in os.listdir(CSRC) if f.endswith('.hip'))
-    jobs = []
-    objs = []
+    jobs, keys, objs = [], {}, []
     for f in hip_srcs:
         src = os.path.join(CSRC, f)
         obj = os.path.join(BUILD, f.replace('.hip', '.o'))
         objs.append(obj)
-        if force or _needs(obj, [src, common]):
-            jobs.append([HIPCC, f'--offload-arch={ARCH}', '-O3', '-fPIC', '-std=c++17', '-c', src, '-o', obj,
-                         '-I', CSRC, '-munsafe-fp-atomics'])
+        cmd = [HIPCC, f'--offload-arch={ARCH}', '-O3', '-fPIC', '-std=c++17', '-c', src, '-o', obj,
+               '-I', CSRC, '-munsafe-fp-atomics']
+        keys[os.path.basename(obj)] = _digest([src, common], cmd)
+        if force or _needs(obj, keys[os.path.basename(obj)], manifest):
+            jobs.append(cmd)
     bsrc = os.path.join(CSRC, 'bindings.cpp')
     bobj = os.path.join(BUILD, 'bindings.o')
     objs.append(bobj)
-    if force or _needs(bobj, [bsrc]):
-        jobs.append([HIPCC, '-O2', '-fPIC', '-std=c++17', '-c', bsrc, '-o', bobj,
-                     '-I', pybind11.get_include(), '-I', sysconfig.get_paths()['include']])
+    bcmd = [HIPCC, '-O2', '-fPIC', '-std=c++17', '-c', bsrc, '-o', bobj,
+            '-I', pybind11.get_include(), '-I', sysconfig.get_paths()['include']]
+    keys['bindings.o'] = _digest([bsrc], bcmd)
+    if force or _needs(bobj, keys['bindings.o'], manifest):
+        jobs.append(bcmd)
     with cf.ThreadPoolExecutor(max_workers=min(8, max(1, len(jobs)))) as ex:
         for j in ex.map(_run, jobs):
             pass
+    # provenance record compiled into the library itself
+    info = {'sources_sha256': sources_hash(), 'arch': ARCH, 'hipcc': _hipcc_version()}
+    isrc = os.path.join(BUILD, 'build_info.cpp')
+    iobj = os.path.join(BUILD, 'build_info.o')
+    text = ('extern "C" const char* pra_build_info() { return R"PRA(' + json.dumps(info) +
+            ')PRA"; }\n')
+    old = open(isrc).read() if os.path.exists(isrc) else None
+    if old != text or not os.path.exists(iobj):
+        with open(isrc, 'w') as f:
+            f.write(text)
+        _run([HIPCC, '-O2', '-fPIC', '-c', isrc, '-o', iobj])
+        jobs.append('build_info')
+    objs.append(iobj)
     out = _out_path()
     if force or jobs or not os.path.exists(out):
         _run([HIPCC, '-shared', '-fPIC', f'--offload-arch={ARCH}', '-o', out] + objs)
+    manifest.update(keys)
+    with open(_manifest_path(), 'w') as f:
+        json.dump(manifest, f, indent=1)
     if verbose:
-        print(f"built {out} ({len(jobs)} objects recompiled)")
+        print(f"built {out} ({len(jobs)} objects recompiled, sources {info['sources_sha256'][:12]})")
     return out
 
 

@@ -30,6 +30,7 @@ void pra_vp_ce_part_fwd(const void*, const int64_t*, float*, int, int, int64_t, 
 void pra_vp_ce_final(const float*, const int64_t*, float*, float*, int, int, int64_t, int, hipStream_t);
 void pra_vp_ce_bwd(const void*, const int64_t*, const float*, const float*, void*, int, int, int64_t, int64_t, int,
                    int, hipStream_t);
+const char* pra_build_info();
 int pra_mmha_splits(int, int, int);
 int pra_mmha_decode(const void*, void*, const float*, float*, void*, int, int, int, int, int, int, int, float, int,
                     hipStream_t);
@@ -154,6 +155,7 @@ PYBIND11_MODULE(_pra_hip, m) {
     pra_vp_ce_bwd(CV(logits), I64(labels), CF(lse), CF(dloss), V(dl), rows, V_, start, vtot, ign, dt, S(s));
     check_launch("vp_ce_bwd");
   });
+  m.def("build_info", []() { return std::string(pra_build_info()); });
   m.def("mmha_splits", [](int B, int H, int t) { return pra_mmha_splits(B, H, t); });
   m.def("mmha_decode", [](P qkv, P cache, P mask, P ws, P out, int B, int H, int L, int D, int t, int splits,
                           int mask_len, float scale, int dt, P s) {
