@@ -55,6 +55,11 @@ def _check_dtypes(op, *pairs):
 
 # =============================================================================
 # LayerNorm (last-dim normalisation over `cols`)
+# kernel keys: the dtypes each HIP kernel is compiled for (registry dispatch falls back to the
+# ref kernel for any other dtype instead of handing the HIP kernel a buffer it misreads)
+_FLOATS = (torch.float32, torch.float16, torch.bfloat16)
+_HALF = (torch.float16, torch.bfloat16)
+
 # =============================================================================
 @R.register_kernel('layer_norm_fwd', 'ref')
 def _ln_fwd_ref(x2, w, b, eps):
@@ -95,7 +100,7 @@ def _adl_nblk(rows):
     return max(1, min(512, (rows + 7) // 8))
 
 
-@R.register_kernel('layer_norm_fwd', 'hip')
+@R.register_kernel('layer_norm_fwd', 'hip', dtypes=_FLOATS)
 def _ln_fwd_hip(x2, w, b, eps):
     _check_dtypes('layer_norm', (w, b))
     L = _native.lib()
@@ -113,7 +118,7 @@ def _ln_fwd_hip(x2, w, b, eps):
     return y, mean, rstd
 
 
-@R.register_kernel('layer_norm_bwd', 'hip')
+@R.register_kernel('layer_norm_bwd', 'hip', dtypes=_FLOATS)
 def _ln_bwd_hip(dy, x2, w, mean, rstd, need_dw, need_db):
     L = _native.lib()
     rows, cols = x2.shape
@@ -224,7 +229,7 @@ def _adl_bwd_ref(dy, dr_out, r, w, mean, rstd, p, seed, need_dw, need_db, need_d
     return dri.to(r.dtype), dh.to(r.dtype), dw, db, dhb
 
 
-@R.register_kernel('add_dropout_ln_fwd', 'hip')
+@R.register_kernel('add_dropout_ln_fwd', 'hip', dtypes=_FLOATS)
 def _adl_fwd_hip(x2, h2, hb, w, b, p, eps, seed):
     _check_dtypes('add_dropout_layer_norm', (x2, h2), (x2, hb), (w, b))
     rows, cols = x2.shape
@@ -240,7 +245,7 @@ def _adl_fwd_hip(x2, h2, hb, w, b, p, eps, seed):
     return r, y, mean, rstd
 
 
-@R.register_kernel('add_dropout_ln_bwd', 'hip')
+@R.register_kernel('add_dropout_ln_bwd', 'hip', dtypes=_FLOATS)
 def _adl_bwd_hip(dy, dr_out, r, w, mean, rstd, p, seed, need_dw, need_db, need_dhb):
     _check_dtypes('add_dropout_layer_norm_grad', (r, dy), (r, dr_out))
     rows, cols = r.shape
@@ -328,7 +333,7 @@ def _rms_bwd_ref(dy, x2, w, rstd, need_dw):
     return dx.to(x2.dtype), dw
 
 
-@R.register_kernel('rms_norm_fwd', 'hip')
+@R.register_kernel('rms_norm_fwd', 'hip', dtypes=_FLOATS)
 def _rms_fwd_hip(x2, w, eps):
     L = _native.lib()
     rows, cols = x2.shape
@@ -339,7 +344,7 @@ def _rms_fwd_hip(x2, w, eps):
     return y, rstd
 
 
-@R.register_kernel('rms_norm_bwd', 'hip')
+@R.register_kernel('rms_norm_bwd', 'hip', dtypes=_FLOATS)
 def _rms_bwd_hip(dy, x2, w, rstd, need_dw):
     L = _native.lib()
     rows, cols = x2.shape
@@ -391,14 +396,14 @@ def _sm_bwd_ref(y2, dy2):
     return (yf * (dyf - (yf * dyf).sum(-1, keepdim=True))).to(y2.dtype)
 
 
-@R.register_kernel('softmax_fwd', 'hip')
+@R.register_kernel('softmax_fwd', 'hip', dtypes=_FLOATS)
 def _sm_fwd_hip(x2):
     y = torch.empty_like(x2)
     _native.lib().softmax_fwd(_ptr(x2), _ptr(y), x2.shape[0], x2.shape[1], _dt(x2), _stream())
     return y
 
 
-@R.register_kernel('softmax_bwd', 'hip')
+@R.register_kernel('softmax_bwd', 'hip', dtypes=_FLOATS)
 def _sm_bwd_hip(y2, dy2):
     dx = torch.empty_like(y2)
     _native.lib().softmax_bwd(_ptr(y2), _ptr(dy2), _ptr(dx), y2.shape[0], y2.shape[1], _dt(y2),
@@ -451,7 +456,7 @@ def _ce_bwd_ref(logits, labels, lse, dloss, ignore_index):
     return g.to(logits.dtype)
 
 
-@R.register_kernel('softmax_ce_fwd', 'hip')
+@R.register_kernel('softmax_ce_fwd', 'hip', dtypes=_FLOATS)
 def _ce_fwd_hip(logits, labels, ignore_index):
     rows, V = logits.shape
     loss = torch.empty(rows, device=logits.device, dtype=torch.float32)
@@ -461,7 +466,7 @@ def _ce_fwd_hip(logits, labels, ignore_index):
     return loss, lse
 
 
-@R.register_kernel('softmax_ce_bwd', 'hip')
+@R.register_kernel('softmax_ce_bwd', 'hip', dtypes=_FLOATS)
 def _ce_bwd_hip(logits, labels, lse, dloss, ignore_index):
     rows, V = logits.shape
     dl = torch.empty_like(logits)
@@ -517,7 +522,7 @@ def _vp_part_ref(logits, labels, start):
     return torch.stack([m, s, picked], -1).contiguous()
 
 
-@R.register_kernel('vp_ce_part_fwd', 'hip')
+@R.register_kernel('vp_ce_part_fwd', 'hip', dtypes=_FLOATS)
 def _vp_part_hip(logits, labels, start):
     rows, V = logits.shape
     st = torch.empty(rows, 3, device=logits.device, dtype=torch.float32)
@@ -556,7 +561,7 @@ def _vp_bwd_ref(logits, labels, lse, dloss, start, vtot, ignore_index):
     return (g * (dloss.float() * valid.float())[:, None]).to(logits.dtype)
 
 
-@R.register_kernel('vp_ce_bwd', 'hip')
+@R.register_kernel('vp_ce_bwd', 'hip', dtypes=_FLOATS)
 def _vp_bwd_hip(logits, labels, lse, dloss, start, vtot, ignore_index):
     rows, V = logits.shape
     dl = torch.empty_like(logits)
@@ -624,7 +629,7 @@ def _mmha_ref(qkv, cache, t, mask):
     return torch.einsum('bhl,bhld->bhd', p, V_).to(qkv.dtype)
 
 
-@R.register_kernel('mmha_decode', 'hip')
+@R.register_kernel('mmha_decode', 'hip', dtypes=_FLOATS)
 def _mmha_hip(qkv, cache, t, mask):
     B, _, H, D = qkv.shape
     L = cache.shape[3]
@@ -676,7 +681,7 @@ def _bg_bwd_ref(dy2, x2, b, approximate):
     return g.to(x2.dtype)
 
 
-@R.register_kernel('bias_gelu_fwd', 'hip')
+@R.register_kernel('bias_gelu_fwd', 'hip', dtypes=_FLOATS)
 def _bg_fwd_hip(x2, b, approximate):
     y = torch.empty_like(x2)
     _native.lib().bias_gelu_fwd(_ptr(x2), _ptr(b), _ptr(y), x2.shape[0], x2.shape[1], _dt(x2),
@@ -687,7 +692,7 @@ def _bg_fwd_hip(x2, b, approximate):
 R.register_kernel('bias_gelu_bwd_db', 'hip')(lambda *a: None)  # dispatch-stats marker
 
 
-@R.register_kernel('bias_gelu_bwd', 'hip')
+@R.register_kernel('bias_gelu_bwd', 'hip', dtypes=_FLOATS)
 def _bg_bwd_hip(dy2, x2, b, approximate):
     dx = torch.empty_like(x2)
     _native.lib().bias_gelu_bwd(_ptr(dy2), _ptr(x2), _ptr(b), _ptr(dx), x2.shape[0], x2.shape[1],
@@ -779,7 +784,7 @@ def _fa_supported(q, k, v):
             k.shape == v.shape and q.shape[0] == k.shape[0] and q.shape[2] == k.shape[2])
 
 
-@R.register_kernel('flash_attn_fwd', 'hip')
+@R.register_kernel('flash_attn_fwd', 'hip', dtypes=_HALF)
 def _fa_fwd_hip(q, k, v, causal, scale):
     _check_dtypes('flash_attention', (q, k), (q, v))
     if not _fa_supported(q, k, v):
@@ -796,7 +801,7 @@ def _fa_fwd_hip(q, k, v, causal, scale):
     return o, lse
 
 
-@R.register_kernel('flash_attn_bwd', 'hip')
+@R.register_kernel('flash_attn_bwd', 'hip', dtypes=_HALF)
 def _fa_bwd_hip(do, q, k, v, o, lse, causal, scale, dq=None, dk=None, dv=None):
     do = _like(do, q.dtype)
     _check_dtypes('flash_attention_grad', (q, k), (q, v), (q, o))
@@ -920,7 +925,7 @@ def _gemm_ref(layout, a, b, out=None, bias=None, z=None, epi=None, beta=0, want_
     return (yo, cs) if want_colsum else yo
 
 
-@R.register_kernel('gemm', 'hip')
+@R.register_kernel('gemm', 'hip', dtypes=_HALF)
 def _gemm_hip(layout, a, b, out=None, bias=None, z=None, epi=None, beta=0, want_colsum=False):
     """One MFMA GEMM launch (+ split-K reduce when the tile grid would leave CUs idle).
     Returns None when the shape/layout is outside what the kernel assumes (caller falls back)."""
@@ -1212,6 +1217,24 @@ def _mt_table(cols, n_list, extra_f, device, chunk=65536):
     return dev_tab, dev_f, dev_ch, len(chunks)
 
 
+@R.register_kernel('adamw_mt', 'hip')
+def _adamw_mt_hip(tab, ftab, ch, nch, lr, b1, b2, eps, bc1, bc2, grad_scale, scale_t, outs):
+    """Multi-tensor AdamW over a device pointer table (one launch for every parameter);
+    returns ``outs`` (the updated fp32 masters / params) so the NaN/Inf checker sees them."""
+    _native.lib().adamw_mt(_ptr(tab), _ptr(ftab), _ptr(ch), nch, float(lr), float(b1), float(b2),
+                           float(eps), float(bc1), float(bc2), float(grad_scale), _stream(),
+                           0 if scale_t is None else _ptr(scale_t))
+    return outs
+
+
+@R.register_kernel('momentum_mt', 'hip')
+def _momentum_mt_hip(tab, ftab, ch, nch, lr, mu, nesterov, grad_scale, scale_t, outs):
+    _native.lib().momentum_mt(_ptr(tab), _ptr(ftab), _ptr(ch), nch, float(lr), float(mu),
+                              int(nesterov), float(grad_scale), _stream(),
+                              0 if scale_t is None else _ptr(scale_t))
+    return outs
+
+
 class MultiTensorAdamW:
     """Cached multi-tensor launch plan for a fixed parameter list (built once, replayed)."""
 
@@ -1247,9 +1270,9 @@ class MultiTensorAdamW:
         tab, ftab, ch, nch = self._plan
         bc1 = 1 - b1 ** step
         bc2 = 1 - b2 ** step
-        _native.lib().adamw_mt(_ptr(tab), _ptr(ftab), _ptr(ch), nch, float(lr), float(b1),
-                               float(b2), float(eps), float(bc1), float(bc2), float(grad_scale),
-                               _stream(), _ptr(scale_tensor))
+        outs = [m if m is not None else p for m, p in zip(self.masters, self.params)]
+        R.dispatch('adamw_mt', tab, tab, ftab, ch, nch, lr, b1, b2, eps, bc1, bc2, grad_scale,
+                   scale_tensor, outs)
 
 
 def momentum_ref(params, grads, vels, masters, lr, mu, wds, use_nesterov, grad_scale=1.0):
@@ -1264,17 +1287,25 @@ def momentum_ref(params, grads, vels, masters, lr, mu, wds, use_nesterov, grad_s
             p.copy_(master)
 
 
+@R.register_kernel('sumsq', 'ref')
+def _sumsq_ref(tensors):
+    return sum((t.float() ** 2).sum() for t in tensors)
+
+
+@R.register_kernel('sumsq', 'hip', dtypes=_FLOATS)
+def _sumsq_hip(tensors):
+    out = torch.zeros(1, device=tensors[0].device, dtype=torch.float32)
+    L = _native.lib()
+    for t in tensors:
+        L.sumsq_accum(_ptr(t), _ptr(out), t.numel(), _dt(t), _stream())
+    return out[0]
+
+
 def global_l2_norm_sq(tensors):
     """Sum of squares over a list of tensors (fp32 accumulate)."""
     if not tensors:
         return None
-    if tensors[0].is_cuda and _native.available():
-        out = torch.zeros(1, device=tensors[0].device, dtype=torch.float32)
-        L = _native.lib()
-        for t in tensors:
-            L.sumsq_accum(_ptr(t), _ptr(out), t.numel(), _dt(t), _stream())
-        return out[0]
-    return sum((t.float() ** 2).sum() for t in tensors)
+    return R.dispatch('sumsq', tensors[0], tensors)
 
 
 # =============================================================================
@@ -1328,7 +1359,7 @@ def _bn_hip_ok(x2):
     return x2.shape[1] % 8 == 0 and x2.numel() // 8 < 2 ** 32 and x2.is_contiguous()
 
 
-@R.register_kernel('batch_norm_fwd', 'hip')
+@R.register_kernel('batch_norm_fwd', 'hip', dtypes=_FLOATS)
 def _bn_fwd_hip(x2, z2, w, b, rmean, rvar, training, momentum, eps, relu):
     _check_dtypes('batch_norm', (x2, z2), (w, b))
     """Returns (y, mean, invstd, relu keep-mask bytes or None)."""
@@ -1356,7 +1387,7 @@ def _bn_fwd_hip(x2, z2, w, b, rmean, rvar, training, momentum, eps, relu):
     return y, mean, torch.rsqrt(rvar.float() + eps), None
 
 
-@R.register_kernel('batch_norm_bwd', 'hip')
+@R.register_kernel('batch_norm_bwd', 'hip', dtypes=_FLOATS)
 def _bn_bwd_hip(dy, y, mask, x2, w, mean, invstd, relu, need_dz):
     if not _bn_hip_ok(x2):
         return _bn_bwd_ref(dy, y, mask, x2, w, mean, invstd, relu, need_dz)
@@ -1455,7 +1486,7 @@ def _emb_bwd_ref(ids, dy, w_shape, w_dtype, pad, into=None):
     return g.to(w_dtype)
 
 
-@R.register_kernel('embedding_fwd', 'hip')
+@R.register_kernel('embedding_fwd', 'hip', dtypes=_FLOATS)
 def _emb_fwd_hip(ids, w, pad):
     D = w.shape[1]
     if D % 8 != 0 or not w.is_contiguous():
@@ -1467,7 +1498,7 @@ def _emb_fwd_hip(ids, w, pad):
     return out.view(*ids.shape, D)
 
 
-@R.register_kernel('embedding_bwd', 'hip')
+@R.register_kernel('embedding_bwd', 'hip', dtypes=_FLOATS)
 def _emb_bwd_hip(ids, dy, w_shape, w_dtype, pad, into=None):
     V, D = w_shape
     tgt_dt = into.dtype if into is not None else w_dtype
@@ -1543,7 +1574,7 @@ def _gba_ref(x2, w, b, act, want_z):
     return y, (z.to(x2.dtype) if want_z and act else None)
 
 
-@R.register_kernel('gemm_bias_act', 'hip')
+@R.register_kernel('gemm_bias_act', 'hip', dtypes=_HALF)
 def _gba_hip(x2, w, b, act, want_z):
     M, K = x2.shape
     N = w.shape[1]

@@ -268,9 +268,9 @@ class Momentum(Optimizer):
                     [K._DT[p._t.dtype] for p in ps]]
             self._fused_plan = (key, K._mt_table(cols, n, [wds, lrm], ps[0]._t.device))
         tab, ftab, ch, nch = self._fused_plan[1]
-        _native.lib().momentum_mt(tab.data_ptr(), ftab.data_ptr(), ch.data_ptr(), nch, float(lr),
-                                  float(self._momentum), int(self._use_nesterov), float(gs),
-                                  K._stream(), 0 if scale_t is None else scale_t.data_ptr())
+        from ..ops import registry as R
+        R.dispatch('momentum_mt', tab, tab, ftab, ch, nch, lr, self._momentum, self._use_nesterov,
+                   gs, scale_t, [m if m is not None else p._t for p, m in zip(ps, masters)])
 
 
 class Adam(Optimizer):

@@ -30,6 +30,7 @@ from ..framework.core import Tensor, Parameter, _u
 from ..nn.layer.layers import Layer
 from ..ops import fused as K
 from ..ops import _native
+from ..ops import registry as R
 from .data_parallel import GradBucketReducer, _avg_supported
 from .flat import FlatGroup, group_params_into_buckets
 from ..distributed import watchdog as _watchdog
@@ -560,6 +561,11 @@ class ShardedOptimizer:
                                [None if lowp is None else master], lr * lrm, mu, [self._wd(p)],
                                getattr(o, '_use_nesterov', False))
 
+    def _updated_shards(self):
+        """The tensors the multi-tensor kernel writes (fp32 masters, else the param shards)."""
+        return [m if m is not None else g.param_shard
+                for m, g in zip(self._masters, self.state.groups)]
+
     def _step_hip(self, lr, scale_t=None):
         o = self._inner
         if self._plan is None:
@@ -590,15 +596,13 @@ class ShardedOptimizer:
                         master, grad, m, v, lowp = self._piece_views(gi, lo, hi)
                         grad.add_(master.to(grad.dtype), alpha=w)
             b1, b2 = o._beta1, o._beta2
-            _native.lib().adamw_mt(tab.data_ptr(), ftab.data_ptr(), ch.data_ptr(), nch, float(lr),
-                                   float(b1), float(b2), float(o._epsilon),
-                                   float(1 - b1 ** self._step), float(1 - b2 ** self._step), 1.0,
-                                   K._stream(), 0 if scale_t is None else scale_t.data_ptr())
+            R.dispatch('adamw_mt', tab, tab, ftab, ch, nch, lr, b1, b2, o._epsilon,
+                       1 - b1 ** self._step, 1 - b2 ** self._step, 1.0, scale_t,
+                       self._updated_shards())
         else:
-            _native.lib().momentum_mt(tab.data_ptr(), ftab.data_ptr(), ch.data_ptr(), nch, float(lr),
-                                      float(getattr(o, '_momentum', 0.0)),
-                                      int(getattr(o, '_use_nesterov', False)), 1.0, K._stream(),
-                                      0 if scale_t is None else scale_t.data_ptr())
+            R.dispatch('momentum_mt', tab, tab, ftab, ch, nch, lr, getattr(o, '_momentum', 0.0),
+                       getattr(o, '_use_nesterov', False), 1.0, scale_t,
+                       self._updated_shards())
 
     def minimize(self, loss, *a, **k):
         loss.backward()
