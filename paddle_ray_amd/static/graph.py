@@ -29,6 +29,7 @@ resolves names through the static op table and refuses anything else.
 import collections
 import contextlib
 import itertools
+import weakref
 import json
 import os
 import time
@@ -41,6 +42,7 @@ from . import _STATIC
 
 _PROBES = (3, 5)  # sizes substituted for unknown (-1) dims during meta shape inference
 _var_ids = itertools.count()
+_ALL_VARS = weakref.WeakValueDictionary()  # vid -> Variable, across programs / sub-blocks
 
 
 # =============================================================================
@@ -63,6 +65,7 @@ class Variable(Tensor):
         self.__dict__['is_data'] = is_data
         self.__dict__['_sg'] = stop_gradient
         self.__dict__['op'] = None
+        _ALL_VARS[self.vid] = self
 
     @property
     def shape(self):
@@ -328,9 +331,18 @@ def _materialize(obj, env):
     return obj
 
 
-def _meta_env(block, probe):
+def _scope_vars(block, extra=()):
+    """The block's variables plus outer-block variables an op inside a sub-block reads."""
+    vs = dict(block.vars)
+    for vid in extra:
+        if vid not in vs and vid in _ALL_VARS:
+            vs[vid] = _ALL_VARS[vid]
+    return vs
+
+
+def _meta_env(block, probe, extra=()):
     env = {}
-    for vid, v in block.vars.items():
+    for vid, v in _scope_vars(block, extra).items():
         shp = [probe if s < 0 else s for s in v._vshape]
         env[vid] = Tensor(torch.empty(shp, dtype=v.dtype, device='meta'))
     return env
@@ -372,7 +384,9 @@ def _param_to_meta(obj):
     return obj
 
 
-def record_op(op_type, fn, args, kwargs):
+def record_op(op_type, fn, args, kwargs, out_specs=None):
+    """Append an op to the current program. ``out_specs`` = (template, [(shape, dtype)])
+    skips shape inference (control-flow ops whose output shapes are their loop vars')."""
     prog = default_main_program()
     blk = prog.global_block()
     in_vids, params = [], []
@@ -381,6 +395,21 @@ def record_op(op_type, fn, args, kwargs):
     for p in params:
         if isinstance(p, Parameter):
             prog._register_param(p)
+    if out_specs is not None:
+        tmpl, specs = out_specs
+        out_vars = []
+        for shp, dt in specs:
+            v = Variable(blk, list(shp), dt, stop_gradient=False)
+            blk.vars[v.vid] = v
+            out_vars.append(v)
+        op = OpDesc(op_type, fn, targs, tkw, in_vids, [v.vid for v in out_vars], tmpl)
+        op.attrs['params'] = [p for p in params if isinstance(p, Parameter)]
+        _record_amp(op)
+        for v in out_vars:
+            v.__dict__['op'] = op
+        blk.ops.append(op)
+        prog._bump()
+        return _rebuild(tmpl, iter(out_vars))
     # shape inference: run the op on meta tensors with two probe sizes for unknown dims
     outs = []
     for probe in _PROBES:
@@ -389,12 +418,12 @@ def record_op(op_type, fn, args, kwargs):
         try:
             with torch.no_grad():
                 try:
-                    env = _meta_env(blk, probe)
+                    env = _meta_env(blk, probe, in_vids)
                     r = fn(*_param_to_meta(_materialize(targs, env)),
                            **_param_to_meta(_materialize(tkw, env)))
                 except Exception:
                     # data-dependent op (needs values): infer on zero tensors instead
-                    env = _real_probe_env(blk, probe)
+                    env = _real_probe_env(blk, probe, in_vids)
                     r = fn(*_materialize(targs, env), **_materialize(tkw, env))
         finally:
             _STATIC[0] = prev
@@ -1283,10 +1312,10 @@ def _all_vars(out):
     return bool(flat) and all(isinstance(t, Variable) for t in flat)
 
 
-def _real_probe_env(block, probe):
+def _real_probe_env(block, probe, extra=()):
     env = {}
     dev = _default_device()
-    for vid, v in block.vars.items():
+    for vid, v in _scope_vars(block, extra).items():
         shp = [probe if s < 0 else s for s in v._vshape]
         env[vid] = Tensor(torch.zeros(shp, dtype=v.dtype, device=dev))
     return env
