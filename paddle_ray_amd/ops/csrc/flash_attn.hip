@@ -102,35 +102,33 @@ __device__ __forceinline__ int swz(int row, int ch) {
   return (row >> 3) * (8 * D) + (ch >> 2) * 256 + (row & 7) * 32 + 8 * ((ch & 3) ^ ((row >> 2) & 3));
 }
 
-// Block-cooperative staged load of a 64-row x D tile by NT threads, pair mapping:
-// pair-chunk pc = t + NT*p -> rows 2*(pc%32), 2*(pc%32)+1, 16-B column chunk pc/32.
+// Block-cooperative staged load of a 64-row x D tile by NT threads, row-coalesced mapping:
+// chunk c = t + NT*p -> row c / NCH, 16-B column chunk c % NCH, so consecutive lanes read
+// consecutive 16 B of the same row and one wave instruction touches 64*16/NCH... whole
+// 128-B lines (D=128: 4 rows x 256 B) instead of 16-B pieces of 64 different rows (which
+// left the texture-address unit stalled on 64 partial lines per instruction).
 template <typename T, int D, int NT>
 struct TileRegs {
   static constexpr int NCH = D / 8;                          // 16-B chunks per row
-  static constexpr int NPASS = (32 * NCH + NT - 1) / NT;
-  uint4 r0[NPASS], r1[NPASS];
+  static constexpr int NPASS = (kTile * NCH + NT - 1) / NT;
+  uint4 r[NPASS];
 
   __device__ __forceinline__ void load(const T* base, int64_t row_stride, int row0, int nrows) {
 #pragma unroll
     for (int p = 0; p < NPASS; ++p) {
-      const int pc = threadIdx.x + NT * p, kp = pc & 31, dc = pc >> 5;
-      const int ra = row0 + 2 * kp, rb = ra + 1;
-      const bool ok = dc < NCH;
-      r0[p] = (ok && ra < nrows) ? *reinterpret_cast<const uint4*>(base + (int64_t)ra * row_stride + dc * 8)
-                                 : make_uint4(0, 0, 0, 0);
-      r1[p] = (ok && rb < nrows) ? *reinterpret_cast<const uint4*>(base + (int64_t)rb * row_stride + dc * 8)
-                                 : make_uint4(0, 0, 0, 0);
+      const int c = threadIdx.x + NT * p, row = c / NCH, dc = c % NCH;
+      const int rr = row0 + row;
+      r[p] = (row < kTile && rr < nrows)
+                 ? *reinterpret_cast<const uint4*>(base + (int64_t)rr * row_stride + dc * 8)
+                 : make_uint4(0, 0, 0, 0);
     }
   }
   // swizzled row image [64][D] (see swz)
   __device__ __forceinline__ void store_swz(T* img) const {
 #pragma unroll
     for (int p = 0; p < NPASS; ++p) {
-      const int pc = threadIdx.x + NT * p, kp = pc & 31, dc = pc >> 5;
-      if (dc < NCH) {
-        *reinterpret_cast<uint4*>(img + swz<D>(2 * kp, dc)) = r0[p];
-        *reinterpret_cast<uint4*>(img + swz<D>(2 * kp + 1, dc)) = r1[p];
-      }
+      const int c = threadIdx.x + NT * p, row = c / NCH, dc = c % NCH;
+      if (row < kTile) *reinterpret_cast<uint4*>(img + swz<D>(row, dc)) = r[p];
     }
   }
 };
@@ -148,26 +146,44 @@ __device__ __forceinline__ typename V8<T>::type frag_global(const T* rowp, int d
 
 __device__ __forceinline__ int acc_row(int reg, int h) { return (reg & 3) + 8 * (reg >> 2) + 4 * h; }
 
-// Row fragment from a swizzled image: a tile is staged once (no transposed copy built from
-// scattered 4-B writes) and read both ways.
-template <typename T, int D>
-__device__ __forceinline__ typename V8<T>::type frag_rows_swz(const T* img, int row, int s, int h) {
-  return *reinterpret_cast<const typename V8<T>::type*>(img + swz<D>(row, 2 * s + h));
-}
 typedef short v4i16 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
+// Per-lane element offsets into a swizzled [64][D] image, computed ONCE per kernel: every
+// row / transposed fragment is then (image base + lane offset + compile-time immediate), so
+// the tile loops carry no per-fragment address arithmetic (swz() with runtime lane terms
+// cost ~100 VALU per tile). Derivation: for row = 32*mt + r and chunk 2s+h, swz() splits into
+// mt*32D + (s>>1)*256 + [lane part depending on s&1]; for the transposed read of k-step S,
+// d-tile dt it is S*16D + dt*256 + [lane part], with a second lane part for rows +8.
+template <int D>
+struct LaneOffs {
+  int row[2];
+  int tra, trb;
+  __device__ __forceinline__ explicit LaneOffs(int lane) {
+    const int r = lane & 31, h = lane >> 5, x = (r >> 2) & 3;
+    row[0] = (r >> 3) * 8 * D + (r & 7) * 32 + 8 * (h ^ x);
+    row[1] = (r >> 3) * 8 * D + (r & 7) * 32 + 8 * ((2 + h) ^ x);
+    const int g = (lane >> 4) & 1, q = (lane >> 2) & 3, p = lane & 3;
+    const int cc = 2 * g + (p >> 1);
+    tra = (4 * h + q) * 32 + 8 * (cc ^ h) + 4 * (p & 1);
+    trb = 8 * D + (4 * h + q) * 32 + 8 * (cc ^ (h + 2)) + 4 * (p & 1);
+  }
+};
+
+// row fragment of image rows 32*mt + (lane&31), k-step s: 16 B of row at chunk 2s+h
+template <typename T, int D>
+__device__ __forceinline__ typename V8<T>::type frag_rows(const T* img, const LaneOffs<D>& lo, int mt, int s) {
+  return *reinterpret_cast<const typename V8<T>::type*>(img + lo.row[s & 1] + mt * 32 * D + (s >> 1) * 256);
+}
+
 // Transposed A fragment (row = column 32*dt + (lane&31) of the image) over the k-step S of
 // the image's rows, in the permuted k order of an accumulator-derived B operand:
 // elem j <-> image row 16S + 8(j>>2) + 4h + (j&3). Two ds_read_b64_tr_b16: lane 4q+p of each
 // 16-lane group addresses row (base+q), columns 4p..4p+3 of the group's 16 columns and
 // receives its own column of the 4 rows. EXEC must be full (every lane takes part).
 template <typename T, int D>
-__device__ __forceinline__ typename V8<T>::type frag_trr(const T* img, int dt, int S, int h, int lane) {
-  const int g = (lane >> 4) & 1, q = (lane >> 2) & 3, p = lane & 3;
-  const int c = 4 * dt + 2 * g + (p >> 1);
-  const int ra = 16 * S + 4 * h + q;
-  const T* pa = img + swz<D>(ra, c) + 4 * (p & 1);
-  const T* pb = img + swz<D>(ra + 8, c) + 4 * (p & 1);
+__device__ __forceinline__ typename V8<T>::type frag_tr(const T* img, const LaneOffs<D>& lo, int dt, int S) {
+  const T* pa = img + lo.tra + S * 16 * D + dt * 256;
+  const T* pb = img + lo.trb + S * 16 * D + dt * 256;
   const v4i16 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)pa);
   const v4i16 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)pb);
   const u32x2 ua = __builtin_bit_cast(u32x2, a), ub = __builtin_bit_cast(u32x2, b);
@@ -189,9 +205,12 @@ fwd_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restrict
   T* img0 = reinterpret_cast<T*>(smem);  // [2][2][64*D]
   constexpr int NS = D / 16, ND = D / 32, BM = NW * 32;
 
-  const int nqb = gridDim.x;
-  const int qb = CAUSAL ? (nqb - 1 - blockIdx.x) : blockIdx.x;  // heaviest causal blocks first
-  const int bh = blockIdx.y, b = bh / H, hh = bh % H;
+  const int nqb = gridDim.y;
+  // grid (B*H, q-blocks): every (b, h) of one q-block row launches before the next row, so
+  // the heaviest causal blocks of ALL heads go first (LPT order, no late 16-tile straggler),
+  // and the q-blocks of one head share an XCD's L2 for K/V when B*H % 8 == 0
+  const int qb = CAUSAL ? (nqb - 1 - blockIdx.y) : blockIdx.y;
+  const int bh = blockIdx.x, b = bh / H, hh = bh % H;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
   const int q0 = qb * BM;
   const int myq = q0 + wave * 32 + r;
@@ -228,7 +247,10 @@ fwd_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restrict
   }
   __syncthreads();
 
-  for (int kt = 0; kt < ntiles; ++kt) {
+  const LaneOffs<D> lo(lane);
+  // one tile: the masked variant only for tiles that straddle Sk or the causal diagonal
+  auto tile = [&](int kt, auto mask_c) {
+    constexpr bool MASK = decltype(mask_c)::value;
     const int k0 = kt * kTile;
     const T* Ks = img0 + (2 * (kt & 1)) * kTile * D;
     const T* Vs = Ks + kTile * D;
@@ -245,7 +267,7 @@ fwd_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restrict
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
-        for (int s = 0; s < NS; ++s) kfr[mt][s] = frag_rows_swz<T, D>(Ks, 32 * mt + r, s, h);
+        for (int s = 0; s < NS; ++s) kfr[mt][s] = frag_rows<T, D>(Ks, lo, mt, s);
       // nothing crosses this point: every read is issued before the first MFMA, and the
       // waitcnt pass then counts them down (lgkmcnt(N)) one MFMA at a time
       __builtin_amdgcn_sched_barrier(0);
@@ -263,10 +285,9 @@ fwd_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restrict
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-      for (int dt = 0; dt < ND; ++dt) vfr[ks][dt] = frag_trr<T, D>(Vs, dt, ks, h, lane);
+      for (int dt = 0; dt < ND; ++dt) vfr[ks][dt] = frag_tr<T, D>(Vs, lo, dt, ks);
     __builtin_amdgcn_sched_barrier(0);
-    const bool need_mask = (k0 + kTile > Sk) || (CAUSAL && (k0 + kTile - 1 > q0 + off));
-    if (need_mask) {
+    if constexpr (MASK) {
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
@@ -308,7 +329,7 @@ fwd_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restrict
       const typename V8<T>::type pf = pack_frag<T>(s_acc[ks >> 1], 8 * (ks & 1));
 #pragma unroll
       for (int dt = 0; dt < ND; ++dt)
-        acc_o[dt] = mfma<T>(ks < 2 ? vfr[ks & 1][dt] : frag_trr<T, D>(Vs, dt, ks, h, lane), pf, acc_o[dt]);
+        acc_o[dt] = mfma<T>(ks < 2 ? vfr[ks & 1][dt] : frag_tr<T, D>(Vs, lo, dt, ks), pf, acc_o[dt]);
     }
     if (kt + 1 < ntiles) {  // idle buffer: last read before the previous barrier
       T* nb = img0 + (2 * ((kt + 1) & 1)) * kTile * D;
@@ -316,7 +337,13 @@ fwd_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restrict
       vr.store_swz(nb + kTile * D);
     }
     __syncthreads();
-  }
+  };
+  // tiles [0, nfull) need no mask: every key < Sk and (causal) <= the block's first query
+  int nfull = min(ntiles, Sk / kTile);
+  if (CAUSAL) nfull = min(nfull, (q0 + off + 1) / kTile);
+  if (nfull < 0) nfull = 0;
+  for (int kt = 0; kt < nfull; ++kt) tile(kt, std::false_type{});
+  for (int kt = nfull; kt < ntiles; ++kt) tile(kt, std::true_type{});
 
   if (myq < Sq) {
     const float inv = l_run > 0.f ? 1.f / l_run : 0.f;
@@ -353,9 +380,9 @@ bwd_dq_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restr
   constexpr int NS = D / 16, ND = D / 32, BM = NW * 32;
   const float LOG2E = 1.4426950408889634f;
 
-  const int nqb = gridDim.x;
-  const int qb = CAUSAL ? (nqb - 1 - blockIdx.x) : blockIdx.x;
-  const int bh = blockIdx.y, b = bh / H, hh = bh % H;
+  const int nqb = gridDim.y;
+  const int qb = CAUSAL ? (nqb - 1 - blockIdx.y) : blockIdx.y;  // heaviest first (see fwd)
+  const int bh = blockIdx.x, b = bh / H, hh = bh % H;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
   const int q0 = qb * BM;
   const int myq = q0 + wave * 32 + r;
@@ -389,6 +416,7 @@ bwd_dq_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restr
   if (CAUSAL) n_end = min(Sk, q0 + BM + off);
   const int ntiles = n_end > 0 ? (n_end + kTile - 1) / kTile : 0;
 
+  const LaneOffs<D> lo(lane);
   TileRegs<T, D, NW * 64> kr, vr;
   if (ntiles > 0) {
     kr.load(kb_, kss, 0, Sk);
@@ -421,8 +449,7 @@ bwd_dq_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restr
 #pragma unroll
           for (int j = 0; j < G; ++j) {
             const int f = g * G + j;
-            fr[g & 1][j] = f < NS ? frag_rows_swz<T, D>(Ks, 32 * mt + r, f, h)
-                                  : frag_rows_swz<T, D>(Vs, 32 * mt + r, f - NS, h);
+            fr[g & 1][j] = f < NS ? frag_rows<T, D>(Ks, lo, mt, f) : frag_rows<T, D>(Vs, lo, mt, f - NS);
           }
         }
         if (g > 0) {
@@ -453,7 +480,7 @@ bwd_dq_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restr
     for (int ks = 0; ks < 4; ++ks) {
       const typename V8<T>::type sf = pack_frag<T>(s_acc[ks >> 1], 8 * (ks & 1));
 #pragma unroll
-      for (int dt = 0; dt < ND; ++dt) acc_q[dt] = mfma<T>(frag_trr<T, D>(Ks, dt, ks, h, lane), sf, acc_q[dt]);
+      for (int dt = 0; dt < ND; ++dt) acc_q[dt] = mfma<T>(frag_tr<T, D>(Ks, lo, dt, ks), sf, acc_q[dt]);
     }
     if (kt + 1 < ntiles) {  // idle buffer: last read before the previous barrier
       T* nb = img0 + (2 * ((kt + 1) & 1)) * kTile * D;
@@ -501,8 +528,8 @@ bwd_dkdv_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __res
   constexpr int NS = D / 16, ND = D / 32;
   const float LOG2E = 1.4426950408889634f;
 
-  const int kb = blockIdx.x;
-  const int bh = blockIdx.y, b = bh / H, hh = bh % H;
+  const int kb = blockIdx.y;  // causal: key block 0 sweeps the most query tiles, launched first
+  const int bh = blockIdx.x, b = bh / H, hh = bh % H;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
   const int kblk0 = kb * 128;
   const int mykey = kblk0 + wave * 32 + r;
@@ -555,7 +582,9 @@ bwd_dkdv_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __res
   if (ntiles > 0) { load_tile(q_begin); store_tile(0); }
   __syncthreads();
 
-  for (int it = 0; it < ntiles; ++it) {
+  const LaneOffs<D> lo(lane);
+  auto tile = [&](int it, auto mask_c) {
+    constexpr bool MASK = decltype(mask_c)::value;
     const int buf = it & 1;
     const T* Qs = img0 + (2 * buf) * kTile * D;
     const T* Ds = Qs + kTile * D;
@@ -563,18 +592,24 @@ bwd_dkdv_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __res
     const float* Dl = Dlb + buf * kTile;
     const int qs0 = q_begin + it * kTile;
     if (it + 1 < ntiles) load_tile(qs0 + kTile);
-    const bool need_mask = (qs0 + kTile > Sq) || (CAUSAL && (kblk0 + 127 > qs0 + off));
 #pragma unroll
     for (int nt = 0; nt < 2; ++nt) {  // two 32-query halves of the tile
-      f32x16 s_acc = f32x16{}, dp_acc = f32x16{};
+      // rows (queries) in registers: q = 32nt + acc_row(i,h); the dP chain starts at -delta
+      f32x16 s_acc = f32x16{}, dp_acc;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const float4 d4 = *reinterpret_cast<const float4*>(Dl + 32 * nt + 8 * g + 4 * h);
+        dp_acc[4 * g + 0] = -d4.x; dp_acc[4 * g + 1] = -d4.y;
+        dp_acc[4 * g + 2] = -d4.z; dp_acc[4 * g + 3] = -d4.w;
+      }
       {
         // all 2*NS row fragments in flight before the MFMAs (one wave per SIMD here: an LDS
         // round trip per MFMA would be fully exposed)
         typename V8<T>::type qfr[NS], dfr[NS];
 #pragma unroll
         for (int s = 0; s < NS; ++s) {
-          qfr[s] = frag_rows_swz<T, D>(Qs, 32 * nt + r, s, h);
-          dfr[s] = frag_rows_swz<T, D>(Ds, 32 * nt + r, s, h);
+          qfr[s] = frag_rows<T, D>(Qs, lo, nt, s);
+          dfr[s] = frag_rows<T, D>(Ds, lo, nt, s);
         }
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -583,24 +618,20 @@ bwd_dkdv_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __res
           dp_acc = mfma<T>(dfr[s], vf[s], dp_acc);
         }
       }
-      // rows (queries) in registers: q = 32nt + acc_row(i,h)
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        const int qr0 = 32 * nt + 8 * g + 4 * h;
-        const float4 l4 = *reinterpret_cast<const float4*>(Ls + qr0);
-        const float4 d4 = *reinterpret_cast<const float4*>(Dl + qr0);
+        const float4 l4 = *reinterpret_cast<const float4*>(Ls + 32 * nt + 8 * g + 4 * h);
         const float la[4] = {l4.x, l4.y, l4.z, l4.w};
-        const float da[4] = {d4.x, d4.y, d4.z, d4.w};
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
           const int i = 4 * g + c;
           float p = fexp2(fmaf(s_acc[i], scale_log2, -la[c]));
-          if (need_mask) {
-            const int qq = qs0 + qr0 + c;
+          if constexpr (MASK) {
+            const int qq = qs0 + 32 * nt + 8 * g + 4 * h + c;
             if (qq >= Sq || (CAUSAL && mykey > qq + off)) p = 0.f;
           }
           s_acc[i] = p;
-          dp_acc[i] = p * (dp_acc[i] - da[c]);
+          dp_acc[i] = p * dp_acc[i];
         }
       }
       // dV^T += dO^T P ; dK^T += Q^T dS   (k = queries of this 32-half, 2 steps of 16);
@@ -610,8 +641,8 @@ bwd_dkdv_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __res
         typename V8<T>::type dtr[ND], qtr[ND];
 #pragma unroll
         for (int dt = 0; dt < ND; ++dt) {
-          dtr[dt] = frag_trr<T, D>(Ds, dt, 2 * nt + ks, h, lane);
-          qtr[dt] = frag_trr<T, D>(Qs, dt, 2 * nt + ks, h, lane);
+          dtr[dt] = frag_tr<T, D>(Ds, lo, dt, 2 * nt + ks);
+          qtr[dt] = frag_tr<T, D>(Qs, lo, dt, 2 * nt + ks);
         }
         const typename V8<T>::type pf = pack_frag<T>(s_acc, 8 * ks);
         const typename V8<T>::type sf = pack_frag<T>(dp_acc, 8 * ks);
@@ -626,7 +657,18 @@ bwd_dkdv_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __res
     // the idle buffer was last read before the previous barrier: fill it now
     if (it + 1 < ntiles) store_tile(buf ^ 1);
     __syncthreads();
+  };
+  // query tiles that straddle the causal diagonal of this 128-key block (the first ones) or
+  // Sq (the last one) need the mask; separate loops keep one body copy live at a time
+  int it0 = 0;
+  if (CAUSAL) {
+    while (it0 < ntiles && kblk0 + 127 > q_begin + it0 * kTile + off) ++it0;
   }
+  int it1 = ntiles;
+  while (it1 > it0 && q_begin + (it1 - 1) * kTile + kTile > Sq) --it1;
+  for (int it = 0; it < it0; ++it) tile(it, std::true_type{});
+  for (int it = it0; it < it1; ++it) tile(it, std::false_type{});
+  for (int it = it1; it < ntiles; ++it) tile(it, std::true_type{});
 
   if (kvalid) {
     T* krow = dk + (int64_t)b * dksb + (int64_t)mykey * dkss + (int64_t)hh * dksh;
@@ -653,7 +695,7 @@ static void launch_fwd_nw(const void* q, const void* k, const void* v, void* o, 
   const size_t lds = 4 * kTile * D * sizeof(T);
   auto kern = fwd_kernel<T, D, C, NW>;
   hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  dim3 grid((Sq + NW * 32 - 1) / (NW * 32), B * H);
+  dim3 grid(B * H, (Sq + NW * 32 - 1) / (NW * 32));
   hipLaunchKernelGGL(kern, grid, dim3(NW * 64), lds, s, (const T*)q, (const T*)k, (const T*)v, (T*)o, lse, H, Sq, Sk,
                      st[0], st[1], st[2], st[3], st[4], st[5], st[6], st[7], st[8], scale * 1.4426950408889634f);
 }
@@ -676,7 +718,7 @@ static void launch_bwd(const void* q, const void* k, const void* v, const void* 
       constexpr int NW = decltype(nwc)::value;
       auto kern = bwd_dq_kernel<T, D, C, NW>;
       hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      hipLaunchKernelGGL(kern, dim3((Sq + NW * 32 - 1) / (NW * 32), B * H), dim3(NW * 64), lds, s, (const T*)q,
+      hipLaunchKernelGGL(kern, dim3(B * H, (Sq + NW * 32 - 1) / (NW * 32)), dim3(NW * 64), lds, s, (const T*)q,
                          (const T*)k, (const T*)v, (const T*)dO, lse, delta, (T*)dq, H, Sq, Sk, st[0], st[1], st[2],
                          st[3], st[4], st[5], st[6], st[7], st[8], st[9], st[10], st[11], scale, sl2);
     };
@@ -686,7 +728,7 @@ static void launch_bwd(const void* q, const void* k, const void* v, const void* 
     const size_t lds = 4 * kTile * D * sizeof(T) + 4 * kTile * sizeof(float);
     auto kern = bwd_dkdv_kernel<T, D, C>;
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(kern, dim3((Sk + 127) / 128, B * H), dim3(256), lds, s, (const T*)q, (const T*)k,
+    hipLaunchKernelGGL(kern, dim3(B * H, (Sk + 127) / 128), dim3(256), lds, s, (const T*)q, (const T*)k,
                        (const T*)v, (const T*)dO, lse, delta, (T*)dk, (T*)dv, H, Sq, Sk, st[0], st[1], st[2],
                        st[3], st[4], st[5], st[6], st[7], st[8], st[12], st[13], st[14], st[15], st[16], st[17],
                        scale, sl2);

@@ -143,6 +143,37 @@ def test_flash_attention(dt, D, causal, S):
         assert err < tol * 4 * max(1.0, gr.abs().max().item()), err
 
 
+@pytest.mark.parametrize('causal', [True, False])
+@pytest.mark.parametrize('Sq,Sk', [(130, 300), (300, 130), (64, 1024), (520, 520)])
+def test_flash_attention_cross_lengths(causal, Sq, Sk):
+    """Sq != Sk (bottom-right aligned causal mask) and lengths around the 64-row tiles: the
+    masked/unmasked tile split of every kernel must agree with the reference."""
+    torch.manual_seed(2)
+    B, H, D = 2, 2, 128
+    q = torch.randn(B, Sq, H, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    k = torch.randn(B, Sk, H, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    v = torch.randn(B, Sk, H, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    scale = 1.0 / math.sqrt(D)
+    o = F.flash_attention(q, k, v, causal=causal, scale=scale)
+    do = torch.randn_like(o)
+    o.backward(do)
+    qr, kr, vr = (t.detach().float().requires_grad_() for t in (q, k, v))
+    # reference with rows that see no key (causal, Sq > Sk) defined as zero output / zero grad
+    qf, kf, vf = (t.permute(0, 2, 1, 3) for t in (qr, kr, vr))
+    sc = qf @ kf.transpose(-1, -2) * scale
+    if causal:
+        m = torch.ones(Sq, Sk, dtype=torch.bool, device=DEV).triu(Sk - Sq + 1)
+        sc = sc.masked_fill(m, float('-inf'))
+    dead = torch.isinf(sc).all(-1, keepdim=True)
+    pr = torch.softmax(sc.masked_fill(dead, 0.0), -1) * (~dead)
+    orf = (pr @ vf).permute(0, 2, 1, 3)
+    orf.backward(do.float())
+    assert (o.float() - orf).abs().max().item() < 4e-2
+    for g, gr in ((q.grad, qr.grad), (k.grad, kr.grad), (v.grad, vr.grad)):
+        err = (g.float() - gr).abs().max().item()
+        assert err < 8e-2 * max(1.0, gr.abs().max().item()), err
+
+
 def test_flash_attention_spike_rows():
     """A spiked key forces the online-softmax rescale path (CDNA guide rule 26)."""
     B, S, H, D = 1, 256, 2, 128
