@@ -258,6 +258,16 @@ fwd_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restrict
       kr.load(kb_, kss, k0 + kTile, Sk);
       vr.load(vb_, vss, k0 + kTile, Sk);
     }
+    // masked tiles: 32-key halves beyond every query of THIS wave (causal) or past Sk are
+    // skipped by the wave (a wave-uniform branch); all waves still stage and sync
+    int nlive = 2;
+    if constexpr (MASK) {
+      int kmax = Sk - 1;
+      if (CAUSAL) kmax = min(kmax, q0 + wave * 32 + 31 + off);
+      nlive = k0 > kmax ? 0 : (k0 + 32 > kmax ? 1 : 2);
+      nlive = __builtin_amdgcn_readfirstlane(nlive);
+    }
+    if (nlive > 0) {
     // S^T = K Q^T : two 32-key tiles (raw scores). All 2*NS K fragments are read from LDS
     // before the first MFMA so the reads overlap each other instead of one LDS round trip
     // per MFMA (hipcc otherwise reuses one fragment register: read, wait, mfma, read, ...).
@@ -267,15 +277,21 @@ fwd_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restrict
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
-        for (int s = 0; s < NS; ++s) kfr[mt][s] = frag_rows<T, D>(Ks, lo, mt, s);
+        for (int s = 0; s < NS; ++s)
+          if (mt < nlive) kfr[mt][s] = frag_rows<T, D>(Ks, lo, mt, s);
       // nothing crosses this point: every read is issued before the first MFMA, and the
       // waitcnt pass then counts them down (lgkmcnt(N)) one MFMA at a time
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt) {
-        s_acc[mt] = f32x16{};
+        if (mt < nlive) {
+          s_acc[mt] = f32x16{};
 #pragma unroll
-        for (int s = 0; s < NS; ++s) s_acc[mt] = mfma<T>(kfr[mt][s], qf[s], s_acc[mt]);
+          for (int s = 0; s < NS; ++s) s_acc[mt] = mfma<T>(kfr[mt][s], qf[s], s_acc[mt]);
+        } else {
+#pragma unroll
+          for (int i = 0; i < 16; ++i) s_acc[mt][i] = -INFINITY;
+        }
       }
     }
     // V^T fragments of the PV product, issued right behind the S MFMAs (the K fragment
@@ -323,14 +339,17 @@ fwd_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restrict
       }
     ps += __shfl_xor(ps, 32, 64);
     l_run += ps;
-    // O^T += V^T P^T
+    // O^T += V^T P^T (k-steps of a dead half contribute nothing)
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
-      const typename V8<T>::type pf = pack_frag<T>(s_acc[ks >> 1], 8 * (ks & 1));
+      if (ks < 2 * nlive) {
+        const typename V8<T>::type pf = pack_frag<T>(s_acc[ks >> 1], 8 * (ks & 1));
 #pragma unroll
-      for (int dt = 0; dt < ND; ++dt)
-        acc_o[dt] = mfma<T>(ks < 2 ? vfr[ks & 1][dt] : frag_tr<T, D>(Vs, lo, dt, ks), pf, acc_o[dt]);
+        for (int dt = 0; dt < ND; ++dt)
+          acc_o[dt] = mfma<T>(ks < 2 ? vfr[ks & 1][dt] : frag_tr<T, D>(Vs, lo, dt, ks), pf, acc_o[dt]);
+      }
     }
+    }  // nlive > 0
     if (kt + 1 < ntiles) {  // idle buffer: last read before the previous barrier
       T* nb = img0 + (2 * ((kt + 1) & 1)) * kTile * D;
       kr.store_swz(nb);
@@ -426,7 +445,8 @@ bwd_dq_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restr
   }
   __syncthreads();
 
-  for (int kt = 0; kt < ntiles; ++kt) {
+  auto tile = [&](int kt, auto mask_c) {
+    constexpr bool MASK = decltype(mask_c)::value;
     const int k0 = kt * kTile;
     const T* Ks = img0 + (2 * (kt & 1)) * kTile * D;
     const T* Vs = Ks + kTile * D;
@@ -434,13 +454,23 @@ bwd_dq_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restr
       kr.load(kb_, kss, k0 + kTile, Sk);
       vr.load(vb_, vss, k0 + kTile, Sk);
     }
+    // masked tiles: 32-key halves past every query of THIS wave / past Sk are skipped
+    int nlive = 2;
+    if constexpr (MASK) {
+      int kmax = Sk - 1;
+      if (CAUSAL) kmax = min(kmax, q0 + wave * 32 + 31 + off);
+      nlive = k0 > kmax ? 0 : (k0 + 32 > kmax ? 1 : 2);
+      nlive = __builtin_amdgcn_readfirstlane(nlive);
+    }
+    if (nlive > 0) {
     f32x16 s_acc[2], dp_acc[2];
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt) {
       s_acc[mt] = f32x16{};
       dp_acc[mt] = f32x16{};
-      // fragments read in groups of 4, one group ahead of the MFMAs that consume them
-      // (8 fragments live at most: this kernel is at the 256-VGPR occupancy-2 limit)
+      if (mt >= nlive) continue;
+      // fragments read in groups of 2, one group ahead of the MFMAs that consume them
+      // (this kernel is at the 256-VGPR occupancy-2 limit)
       constexpr int G = 2, NG = 2 * NS / G;  // groups over the K (first NS) then V fragments
       typename V8<T>::type fr[2][G];
 #pragma unroll
@@ -463,32 +493,39 @@ bwd_dq_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restr
         __builtin_amdgcn_sched_barrier(0);
       }
     }
-    const bool need_mask = (k0 + kTile > Sk) || (CAUSAL && (k0 + kTile - 1 > q0 + off));
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         float p = fexp2(fmaf(s_acc[mt][i], scale_log2, -lse2));
-        if (need_mask) {
+        if constexpr (MASK) {
           const int key = k0 + 32 * mt + acc_row(i, h);
-          if (key >= Sk || (CAUSAL && key > myq + off)) p = 0.f;
+          if (mt >= nlive || key >= Sk || (CAUSAL && key > myq + off)) p = 0.f;
         }
         s_acc[mt][i] = p * (dp_acc[mt][i] - dlt);  // dS^T (unscaled)
       }
     // dQ^T += K^T dS^T
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
-      const typename V8<T>::type sf = pack_frag<T>(s_acc[ks >> 1], 8 * (ks & 1));
+      if (ks < 2 * nlive) {
+        const typename V8<T>::type sf = pack_frag<T>(s_acc[ks >> 1], 8 * (ks & 1));
 #pragma unroll
-      for (int dt = 0; dt < ND; ++dt) acc_q[dt] = mfma<T>(frag_tr<T, D>(Ks, lo, dt, ks), sf, acc_q[dt]);
+        for (int dt = 0; dt < ND; ++dt) acc_q[dt] = mfma<T>(frag_tr<T, D>(Ks, lo, dt, ks), sf, acc_q[dt]);
+      }
     }
+    }  // nlive > 0
     if (kt + 1 < ntiles) {  // idle buffer: last read before the previous barrier
       T* nb = img0 + (2 * ((kt + 1) & 1)) * kTile * D;
       kr.store_swz(nb);
       vr.store_swz(nb + kTile * D);
     }
     __syncthreads();
-  }
+  };
+  int nfull = min(ntiles, Sk / kTile);
+  if (CAUSAL) nfull = min(nfull, (q0 + off + 1) / kTile);
+  if (nfull < 0) nfull = 0;
+  for (int kt = 0; kt < nfull; ++kt) tile(kt, std::false_type{});
+  for (int kt = nfull; kt < ntiles; ++kt) tile(kt, std::true_type{});
 
   if (qvalid) {
     T* row = dq + (int64_t)b * dqsb + (int64_t)myq * dqss + (int64_t)hh * dqsh;
@@ -592,8 +629,21 @@ bwd_dkdv_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __res
     const float* Dl = Dlb + buf * kTile;
     const int qs0 = q_begin + it * kTile;
     if (it + 1 < ntiles) load_tile(qs0 + kTile);
+    // masked tiles: a 32-query half whose every query precedes this wave's first key (causal)
+    // or lies past Sq contributes nothing for the wave — skipped (wave-uniform branch)
+    int nt_lo = 0, nt_hi = 2;
+    if constexpr (MASK) {
+      const int kw0 = kblk0 + wave * 32;
+      if (CAUSAL) {
+        while (nt_lo < 2 && kw0 > qs0 + 32 * nt_lo + 31 + off) ++nt_lo;
+      }
+      while (nt_hi > nt_lo && qs0 + 32 * (nt_hi - 1) >= Sq) --nt_hi;
+      nt_lo = __builtin_amdgcn_readfirstlane(nt_lo);
+      nt_hi = __builtin_amdgcn_readfirstlane(nt_hi);
+    }
 #pragma unroll
     for (int nt = 0; nt < 2; ++nt) {  // two 32-query halves of the tile
+      if (nt < nt_lo || nt >= nt_hi) continue;
       // rows (queries) in registers: q = 32nt + acc_row(i,h); the dP chain starts at -delta
       f32x16 s_acc = f32x16{}, dp_acc;
 #pragma unroll
@@ -704,7 +754,8 @@ static void launch_fwd_nw(const void* q, const void* k, const void* v, void* o, 
 template <typename T, int D, bool C>
 static void launch_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B, int H, int Sq,
                        int Sk, const int64_t* st, float scale, hipStream_t s) {
-  launch_fwd_nw<T, D, C, 8>(q, k, v, o, lse, B, H, Sq, Sk, st, scale, s);
+  if (C) launch_fwd_nw<T, D, C, 4>(q, k, v, o, lse, B, H, Sq, Sk, st, scale, s);
+  else launch_fwd_nw<T, D, C, 8>(q, k, v, o, lse, B, H, Sq, Sk, st, scale, s);
 }
 
 template <typename T, int D, bool C>
