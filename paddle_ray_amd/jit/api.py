@@ -9,6 +9,11 @@ reference's dy2static is used for:
   input signature captures the whole forward into a ``torch.cuda.CUDAGraph`` (= hipGraph
   on ROCm) with static input buffers; later calls copy inputs in and replay the graph —
   one launch instead of hundreds (launch-bound serving / small-batch inference).
+* **Training capture** (``build_strategy.use_hip_graph = True`` on a call that needs
+  gradients): the forward AND its backward are captured as two graphs sharing one memory
+  pool; the call becomes one autograd node whose forward replays the first graph and whose
+  backward replays the second, returning input and parameter gradients (accumulated into
+  ``.grad`` as usual). Parameters must keep their storage (optimizers update in place).
 * **Program export**: ``concrete_program`` / ``jit.save`` record the layer into a static
   ``Program`` (static/graph.py) from ``InputSpec``s and write ``.pdmodel`` (JSON op list)
   + ``.pdiparams``; ``jit.load`` returns a ``TranslatedLayer`` that replays the program
@@ -108,6 +113,105 @@ class _GraphEntry:
         return self.out
 
 
+class _TrainGraph:
+    """Forward + backward of ``fn`` captured as two HIP graphs (parity in spirit with the
+    reference's to_static training programs run by the standalone executor)."""
+
+    def __init__(self, fn, params, args, kwargs):
+        ins = _flat_tensors((args, kwargs), [])
+        self.params = [p for p in params if not p.stop_gradient]
+        self.static_in = [t._t.detach().clone().requires_grad_(t._t.requires_grad) for t in ins]
+        it = iter(self.static_in)
+
+        def swap(o):
+            if isinstance(o, Tensor):
+                return Tensor(next(it))
+            if isinstance(o, list):
+                return [swap(x) for x in o]
+            if isinstance(o, tuple):
+                return tuple(swap(x) for x in o)
+            if isinstance(o, dict):
+                return {k: swap(v) for k, v in o.items()}
+            return o
+        sargs, skw = swap(args), swap(kwargs)
+        ptens = [p._t for p in self.params]
+        diff_in = [t for t in self.static_in if t.requires_grad]
+        wrt = diff_in + ptens
+        saved_grads = [p.grad for p in ptens]
+        for p in ptens:   # fused kernels add into an existing .grad in place: keep them pure
+            p.grad = None
+        try:
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                for _ in range(2):  # warm up allocator / lazy inits / autotuning
+                    outs = [o._t for o in _flat_tensors(fn(*sargs, **skw), [])]
+                    torch.autograd.grad(outs, wrt, [torch.ones_like(o) for o in outs],
+                                        allow_unused=True)
+            torch.cuda.current_stream().wait_stream(s)
+            pool = torch.cuda.graph_pool_handle()
+            self.fwd_graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.fwd_graph, pool=pool):
+                out = fn(*sargs, **skw)
+            self.out_struct = out
+            self.static_out = [o._t for o in _flat_tensors(out, [])]
+            self.static_gout = [torch.empty_like(o) for o in self.static_out]
+            self.bwd_graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.bwd_graph, pool=pool):
+                grads = torch.autograd.grad(self.static_out, wrt, self.static_gout,
+                                            allow_unused=True)
+            self.static_grads = [g if g is not None else None for g in grads]
+        finally:
+            for p, g in zip(ptens, saved_grads):
+                p.grad = g
+        self.diff_mask = [t.requires_grad for t in self.static_in]
+        entry = self
+
+        class _Graphed(torch.autograd.Function):
+            @staticmethod
+            def forward(ctx, *tensors):
+                n_in = len(entry.static_in)
+                for buf, t in zip(entry.static_in, tensors[:n_in]):
+                    buf.detach().copy_(t, non_blocking=True)
+                entry.fwd_graph.replay()
+                return tuple(o.detach() for o in entry.static_out)
+
+            @staticmethod
+            def backward(ctx, *gouts):
+                for buf, g in zip(entry.static_gout, gouts):
+                    if g is None:
+                        buf.zero_()
+                    else:
+                        buf.copy_(g, non_blocking=True)
+                entry.bwd_graph.replay()
+                gi = iter(entry.static_grads)
+                res = []
+                for m in entry.diff_mask:
+                    res.append(next(gi).clone() if m else None)
+                for _ in entry.params:
+                    g = next(gi)
+                    res.append(None if g is None else g.clone())
+                return tuple(res)
+        self._fn = _Graphed
+
+    def __call__(self, args, kwargs):
+        ins = [t._t for t in _flat_tensors((args, kwargs), [])]
+        outs = self._fn.apply(*ins, *[p._t for p in self.params])
+        it = iter(outs)
+
+        def rebuild(o):
+            if isinstance(o, Tensor):
+                return Tensor(next(it))
+            if isinstance(o, list):
+                return [rebuild(x) for x in o]
+            if isinstance(o, tuple):
+                return tuple(rebuild(x) for x in o)
+            if isinstance(o, dict):
+                return {k: rebuild(v) for k, v in o.items()}
+            return o
+        return rebuild(self.out_struct)
+
+
 class StaticFunction:
     """Callable returned by ``to_static``."""
 
@@ -153,10 +257,26 @@ class StaticFunction:
             return any(not p.stop_gradient for p in self._layer.parameters())
         return True
 
+    def _use_train_graph(self, args, kwargs):
+        bs = self._build_strategy
+        if not (bs is not None and getattr(bs, 'use_hip_graph', False)):
+            return False  # training capture is opt-in: parameters must keep their storage
+        if not torch.cuda.is_available() or not torch.is_grad_enabled():
+            return False
+        ins = _flat_tensors((args, kwargs), [])
+        return bool(ins) and all(t._t.is_cuda for t in ins) and self._needs_grad(args, kwargs)
+
     def __call__(self, *args, **kwargs):
         from ..static import _STATIC
         if not _enabled[0] or _STATIC[0]:
             return self._fn(*args, **kwargs)
+        if self._use_train_graph(args, kwargs):
+            key = ('train',) + _signature(args, kwargs)
+            g = self._graphs.get(key)
+            if g is None:
+                params = self._layer.parameters() if self._layer is not None else []
+                g = self._graphs[key] = _TrainGraph(self._fn, params, args, kwargs)
+            return g(args, kwargs)
         if self._use_graph(args, kwargs):
             key = _signature(args, kwargs)
             g = self._graphs.get(key)

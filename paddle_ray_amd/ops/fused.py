@@ -306,7 +306,15 @@ class AddDropoutLNFn(torch.autograd.Function):
 
 def add_dropout_layer_norm(x, h, hbias, w, b, p=0.0, eps=1e-5, training=True):
     """(r, y) with r = x + dropout(h + hbias), y = LayerNorm(r)·w + b."""
-    return AddDropoutLNFn.apply(x, h, hbias, w, b, p if training else 0.0, eps)
+    p = p if training else 0.0
+    if p > 0 and x.is_cuda and torch.cuda.is_current_stream_capturing():
+        # the kernel's dropout seed is a host value: a captured HIP graph would replay ONE
+        # mask forever. Under capture use torch's graph-aware RNG (seed/offset advanced per
+        # replay) and the LayerNorm kernel.
+        hh = h if hbias is None else h + hbias.to(h.dtype)
+        r = x + torch.nn.functional.dropout(hh.to(x.dtype), p, True)
+        return r, layer_norm(r, w, b, eps)
+    return AddDropoutLNFn.apply(x, h, hbias, w, b, p, eps)
 
 
 # =============================================================================
