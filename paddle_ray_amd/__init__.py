@@ -8,6 +8,9 @@ __version__ = '0.1.0'
 
 import torch as _torch
 
+from .native import allocator as _allocator  # noqa: E402
+_allocator.maybe_enable_from_env()  # PRA_ALLOCATOR=auto_growth: before any device allocation
+
 from .framework.core import (Tensor, Parameter, EagerParamBase, Place, CPUPlace, CUDAPlace,  # noqa
                              CUDAPinnedPlace, XPUPlace, NPUPlace, to_tensor, is_tensor, no_grad,
                              enable_grad, set_grad_enabled, is_grad_enabled, set_device, get_device,

@@ -24,27 +24,56 @@ def synchronize(device=None):
     torch.cuda.synchronize(_dev(device))
 
 
+def _native():
+    from ...native import allocator
+    return allocator if allocator.enabled() else None
+
+
+def _idx(device):
+    d = _dev(device)
+    return d.index if isinstance(d, torch.device) and d.index is not None else \
+        (d if isinstance(d, int) else torch.cuda.current_device())
+
+
+def _nstat(device, key):
+    return _native().stats(_idx(device))[key]
+
+
 def empty_cache():
+    if _native():
+        _native().empty_cache(torch.cuda.current_device())
+        return
     torch.cuda.empty_cache()
 
 
 def max_memory_allocated(device=None):
+    if _native():
+        return _nstat(device, 'peak_allocated')
     return torch.cuda.max_memory_allocated(_dev(device))
 
 
 def max_memory_reserved(device=None):
+    if _native():
+        return _nstat(device, 'peak_reserved')
     return torch.cuda.max_memory_reserved(_dev(device))
 
 
 def memory_allocated(device=None):
+    if _native():
+        return _nstat(device, 'allocated')
     return torch.cuda.memory_allocated(_dev(device))
 
 
 def memory_reserved(device=None):
+    if _native():
+        return _nstat(device, 'reserved')
     return torch.cuda.memory_reserved(_dev(device))
 
 
 def reset_max_memory_allocated(device=None):
+    if _native():
+        _native().reset_peak(_idx(device))
+        return
     torch.cuda.reset_peak_memory_stats(_dev(device))
 
 

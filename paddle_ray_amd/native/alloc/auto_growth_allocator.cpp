@@ -1,0 +1,319 @@
+// Auto-growth best-fit device allocator with per-stream free lists.
+//
+// Parity: paddle/fluid/memory/allocation/auto_growth_best_fit_allocator.cc (chunks grown on
+// demand, best-fit block search, block splitting and neighbour coalescing, free chunks
+// released on demand) and stream_safe_cuda_allocator.cc (a block freed on stream S is reused
+// by stream S without synchronisation; another stream only takes it after the event
+// recorded at free time completed). Plugged into PyTorch-ROCm through
+// torch.cuda.memory.CUDAPluggableAllocator (pra_alloc / pra_free) so every framework tensor
+// comes from it when enabled; statistics feed paddle.device.cuda.memory_* .
+//
+// Built twice: with hipcc against the HIP runtime (the real allocator), and with
+// -DPRA_ALLOC_HOST against malloc so the block bookkeeping is unit-tested on the CPU.
+#include <algorithm>
+#include <cstdint>
+#include <cstdlib>
+#include <map>
+#include <mutex>
+#include <set>
+#include <unordered_map>
+#include <vector>
+
+#ifdef PRA_ALLOC_HOST
+typedef void* stream_t;
+typedef void* event_t;
+static int backend_malloc(void** p, size_t n) {
+  *p = std::aligned_alloc(256, n);
+  return *p ? 0 : 1;
+}
+static void backend_free(void* p) { std::free(p); }
+static void backend_set_device(int) {}
+static event_t event_record(stream_t) { return nullptr; }
+static bool event_done(event_t) { return true; }
+static void event_destroy(event_t) {}
+static void device_sync() {}
+#else
+#include <hip/hip_runtime.h>
+typedef hipStream_t stream_t;
+typedef hipEvent_t event_t;
+static int backend_malloc(void** p, size_t n) { return hipMalloc(p, n) == hipSuccess ? 0 : 1; }
+static void backend_free(void* p) { (void)hipFree(p); }
+static void backend_set_device(int d) { (void)hipSetDevice(d); }
+static event_t event_record(stream_t s) {
+  event_t e = nullptr;
+  if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
+  (void)hipEventRecord(e, s);
+  return e;
+}
+static bool event_done(event_t e) { return e == nullptr || hipEventQuery(e) == hipSuccess; }
+static void event_destroy(event_t e) {
+  if (e) (void)hipEventDestroy(e);
+}
+static void device_sync() { (void)hipDeviceSynchronize(); }
+#endif
+
+namespace {
+
+constexpr size_t kAlign = 256;
+constexpr size_t kMinSplit = 512;  // remainders smaller than this stay with the block
+
+struct Chunk;
+struct Block {
+  char* ptr;
+  size_t size;
+  bool free;
+  Chunk* chunk;
+  Block* prev;  // address-ordered neighbours inside the chunk
+  Block* next;
+  stream_t stream;  // stream of the last user
+  event_t event;    // recorded on `stream` when freed (cross-stream reuse gate)
+};
+
+struct Chunk {
+  char* base;
+  size_t size;
+  Block* head;
+};
+
+struct Stats {
+  int64_t allocated = 0, reserved = 0, peak_allocated = 0, peak_reserved = 0;
+  int64_t n_alloc = 0, n_free = 0, n_chunks = 0, n_backend_alloc = 0, n_backend_free = 0;
+};
+
+struct DeviceAllocator {
+  std::mutex mu;
+  size_t growth = size_t(64) << 20;  // minimum chunk size
+  // free blocks per stream, ordered by (size, address) -> best fit = lower_bound
+  std::map<stream_t, std::set<std::pair<size_t, Block*>>> free_sets;
+  std::unordered_map<void*, Block*> live;
+  std::vector<Chunk*> chunks;
+  Stats st;
+
+  static size_t round(size_t n) { return ((n ? n : 1) + kAlign - 1) / kAlign * kAlign; }
+
+  void insert_free(Block* b) { free_sets[b->stream].insert({b->size, b}); }
+  void erase_free(Block* b) {
+    auto it = free_sets.find(b->stream);
+    if (it != free_sets.end()) it->second.erase({b->size, b});
+  }
+
+  Block* take(Block* b, size_t n, stream_t s) {
+    erase_free(b);
+    if (b->event) {
+      event_destroy(b->event);
+      b->event = nullptr;
+    }
+    if (b->size - n >= kMinSplit) {  // split: remainder stays free on the block's stream
+      Block* r = new Block{b->ptr + n, b->size - n, true, b->chunk, b, b->next, b->stream, nullptr};
+      if (b->next) b->next->prev = r;
+      b->next = r;
+      b->size = n;
+      insert_free(r);
+    }
+    b->free = false;
+    b->stream = s;
+    live[b->ptr] = b;
+    st.allocated += (int64_t)b->size;
+    st.peak_allocated = std::max(st.peak_allocated, st.allocated);
+    st.n_alloc++;
+    return b;
+  }
+
+  Block* find(size_t n, stream_t s) {
+    auto it = free_sets.find(s);
+    if (it != free_sets.end()) {
+      auto f = it->second.lower_bound({n, nullptr});
+      if (f != it->second.end()) return f->second;
+    }
+    // another stream's block, once the work queued before its free has completed
+    Block* best = nullptr;
+    for (auto& kv : free_sets) {
+      if (kv.first == s) continue;
+      for (auto f = kv.second.lower_bound({n, nullptr}); f != kv.second.end(); ++f) {
+        if (event_done(f->second->event)) {
+          if (!best || f->second->size < best->size) best = f->second;
+          break;
+        }
+      }
+    }
+    return best;
+  }
+
+  bool grow(size_t n) {
+    size_t csz = std::max(n, growth);
+    csz = (csz + (size_t(2) << 20) - 1) / (size_t(2) << 20) * (size_t(2) << 20);
+    void* p = nullptr;
+    if (backend_malloc(&p, csz) != 0) return false;
+    Chunk* c = new Chunk{(char*)p, csz, nullptr};
+    Block* b = new Block{(char*)p, csz, true, c, nullptr, nullptr, nullptr, nullptr};
+    c->head = b;
+    chunks.push_back(c);
+    insert_free(b);
+    st.reserved += (int64_t)csz;
+    st.peak_reserved = std::max(st.peak_reserved, st.reserved);
+    st.n_chunks++;
+    st.n_backend_alloc++;
+    return true;
+  }
+
+  // release chunks that are one free block; returns bytes released
+  size_t release_free_chunks() {
+    size_t freed = 0;
+    std::vector<Chunk*> keep;
+    for (Chunk* c : chunks) {
+      Block* b = c->head;
+      if (b->free && b->next == nullptr && b->size == c->size && event_done(b->event)) {
+        erase_free(b);
+        event_destroy(b->event);
+        backend_free(c->base);
+        st.reserved -= (int64_t)c->size;
+        st.n_chunks--;
+        st.n_backend_free++;
+        freed += c->size;
+        delete b;
+        delete c;
+      } else {
+        keep.push_back(c);
+      }
+    }
+    chunks.swap(keep);
+    return freed;
+  }
+
+  void* alloc(size_t size, stream_t s) {
+    std::lock_guard<std::mutex> g(mu);
+    const size_t n = round(size);
+    Block* b = find(n, s);
+    if (!b) {
+      if (!grow(n)) {  // out of memory: wait for pending frees, drop free chunks, retry
+        device_sync();
+        release_free_chunks();
+        if (!grow(n)) return nullptr;
+      }
+      b = find(n, s);
+      if (!b) return nullptr;
+    }
+    return take(b, n, s)->ptr;
+  }
+
+  void free_(void* p, stream_t s) {
+    std::lock_guard<std::mutex> g(mu);
+    auto it = live.find(p);
+    if (it == live.end()) return;
+    Block* b = it->second;
+    live.erase(it);
+    st.allocated -= (int64_t)b->size;
+    st.n_free++;
+    b->free = true;
+    b->stream = s;
+    b->event = event_record(s);
+    // coalesce with free neighbours freed on the same stream, or whose pending work is done
+    // (their event completed: any stream may take them, so the merged block can be s's)
+    auto mergeable = [&](Block* o) {
+      return o && o->free && (o->stream == s || event_done(o->event));
+    };
+    if (mergeable(b->next)) {
+      Block* n = b->next;
+      erase_free(n);
+      event_destroy(n->event);
+      b->size += n->size;
+      b->next = n->next;
+      if (n->next) n->next->prev = b;
+      delete n;
+    }
+    if (mergeable(b->prev)) {
+      Block* pr = b->prev;
+      erase_free(pr);
+      event_destroy(pr->event);
+      pr->size += b->size;
+      pr->next = b->next;
+      if (b->next) b->next->prev = pr;
+      pr->event = b->event;  // the merged block is gated by this free's event
+      pr->stream = s;
+      b->event = nullptr;
+      delete b;
+      b = pr;
+    }
+    insert_free(b);
+  }
+
+  // bookkeeping invariant check (tests): blocks tile every chunk exactly, free sets agree
+  bool check() {
+    std::lock_guard<std::mutex> g(mu);
+    size_t nfree = 0;
+    for (auto& kv : free_sets) nfree += kv.second.size();
+    size_t seen_free = 0;
+    int64_t used = 0, reserved = 0;
+    for (Chunk* c : chunks) {
+      char* expect = c->base;
+      for (Block* b = c->head; b; b = b->next) {
+        if (b->ptr != expect || b->chunk != c) return false;
+        if (b->next && b->next->prev != b) return false;
+        expect += b->size;
+        if (b->free) {
+          seen_free++;
+          if (!free_sets[b->stream].count({b->size, b})) return false;
+        } else {
+          used += (int64_t)b->size;
+        }
+      }
+      if (expect != c->base + c->size) return false;
+      reserved += (int64_t)c->size;
+    }
+    return seen_free == nfree && used == st.allocated && reserved == st.reserved;
+  }
+};
+
+std::mutex g_mu;
+std::map<int, DeviceAllocator*> g_dev;
+
+DeviceAllocator* dev(int d) {
+  std::lock_guard<std::mutex> g(g_mu);
+  auto it = g_dev.find(d);
+  if (it != g_dev.end()) return it->second;
+  DeviceAllocator* a = new DeviceAllocator();
+  if (const char* e = std::getenv("PRA_ALLOC_CHUNK_MB")) a->growth = size_t(std::atoll(e)) << 20;
+  g_dev[d] = a;
+  return a;
+}
+
+}  // namespace
+
+extern "C" {
+// CUDAPluggableAllocator entry points
+void* pra_alloc(size_t size, int device, stream_t stream) {
+  backend_set_device(device);
+  return dev(device)->alloc(size, stream);
+}
+void pra_free(void* ptr, size_t size, int device, stream_t stream) {
+  (void)size;
+  dev(device)->free_(ptr, stream);
+}
+// stats: allocated, reserved, peak_allocated, peak_reserved, n_alloc, n_free, n_chunks,
+// n_backend_alloc, n_backend_free
+void pra_alloc_stats(int device, int64_t* out) {
+  DeviceAllocator* a = dev(device);
+  std::lock_guard<std::mutex> g(a->mu);
+  const Stats& s = a->st;
+  int64_t v[9] = {s.allocated, s.reserved, s.peak_allocated, s.peak_reserved, s.n_alloc,
+                  s.n_free, s.n_chunks, s.n_backend_alloc, s.n_backend_free};
+  for (int i = 0; i < 9; ++i) out[i] = v[i];
+}
+void pra_alloc_reset_peak(int device) {
+  DeviceAllocator* a = dev(device);
+  std::lock_guard<std::mutex> g(a->mu);
+  a->st.peak_allocated = a->st.allocated;
+  a->st.peak_reserved = a->st.reserved;
+}
+int64_t pra_alloc_empty_cache(int device) {
+  DeviceAllocator* a = dev(device);
+  std::lock_guard<std::mutex> g(a->mu);
+  return (int64_t)a->release_free_chunks();
+}
+void pra_alloc_set_growth(int device, int64_t bytes) {
+  DeviceAllocator* a = dev(device);
+  std::lock_guard<std::mutex> g(a->mu);
+  a->growth = (size_t)bytes;
+}
+int pra_alloc_check(int device) { return dev(device)->check() ? 1 : 0; }
+}

@@ -6,7 +6,30 @@ import sysconfig
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
+def build_allocator(force=False, verbose=True):
+    """The auto-growth allocator twice: against the HIP runtime (hipcc, host code) and against
+    malloc (-DPRA_ALLOC_HOST) for CPU unit tests of its bookkeeping."""
+    src = os.path.join(HERE, 'alloc', 'auto_growth_allocator.cpp')
+    outs = []
+    for name, cmd in (
+            ('_pra_alloc_host.so', ['g++', '-O2', '-std=c++17', '-shared', '-fPIC', '-pthread',
+                                    '-DPRA_ALLOC_HOST', src]),
+            ('_pra_alloc_hip.so', [os.environ.get('HIPCC', '/opt/rocm/bin/hipcc'), '-O2',
+                                   '-std=c++17', '-shared', '-fPIC', src])):
+        out = os.path.join(HERE, name)
+        outs.append(out)
+        if not force and os.path.exists(out) and os.path.getmtime(out) > os.path.getmtime(src):
+            continue
+        r = subprocess.run(cmd + ['-o', out], capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(r.stderr)
+        if verbose:
+            print(f'built {out}')
+    return outs
+
+
 def build(force=False, verbose=True):
+    build_allocator(force, verbose)
     import pybind11
     import glob
     srcs = sorted(glob.glob(os.path.join(HERE, 'src', '*.cpp')))

@@ -1,0 +1,116 @@
+"""Native auto-growth best-fit allocator (parity: auto_growth_best_fit_allocator.cc +
+stream_safe_cuda_allocator.cc). CPU: the block bookkeeping, built against malloc, under
+random alloc/free traffic on several streams. GPU: a training step with every tensor coming
+from the HIP build through torch's pluggable-allocator hook."""
+import ctypes
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from paddle_ray_amd.native import allocator as A
+
+MB = 1 << 20
+
+
+@pytest.fixture
+def lib():
+    path = A.library_path(host=True)
+    if not os.path.exists(path):
+        from paddle_ray_amd.native.build import build_allocator
+        build_allocator()
+    return A.load(host=True)
+
+
+def _alloc(lib, dev, n, stream=0):
+    p = lib.pra_alloc(n, dev, ctypes.c_void_p(stream))
+    assert p, n
+    return p
+
+
+def test_random_traffic_keeps_invariants(lib):
+    dev = 11
+    lib.pra_alloc_set_growth(dev, 8 * MB)
+    rs = np.random.RandomState(0)
+    live = {}
+    for step in range(3000):
+        if live and (rs.rand() < 0.45 or len(live) > 200):
+            p = list(live)[rs.randint(len(live))]
+            n, s = live.pop(p)
+            lib.pra_free(p, n, dev, ctypes.c_void_p(s))
+        else:
+            n = int(rs.choice([rs.randint(1, 4096), rs.randint(4096, 2 * MB), rs.randint(MB, 12 * MB)]))
+            s = int(rs.randint(0, 3))
+            p = _alloc(lib, dev, n, s)
+            live[p] = (n, s)
+        if step % 97 == 0:
+            assert lib.pra_alloc_check(dev) == 1, step
+            spans = sorted((p, p + ((n + 255) // 256) * 256) for p, (n, _) in live.items())
+            assert all(a[1] <= b[0] for a, b in zip(spans, spans[1:])), "live blocks overlap"
+            st = A.stats(dev, lib)
+            want = sum(((n + 255) // 256) * 256 for n, _ in live.values())
+            # a block keeps a remainder smaller than the split threshold (<= 256 B extra)
+            assert 0 <= st['allocated'] - want <= 256 * len(live)
+    for p, (n, s) in list(live.items()):
+        lib.pra_free(p, n, dev, ctypes.c_void_p(s))
+    assert lib.pra_alloc_check(dev) == 1
+    st = A.stats(dev, lib)
+    assert st['allocated'] == 0 and st['num_allocs'] == st['num_frees']
+    released = A.empty_cache(dev, lib)
+    assert released > 0 and A.stats(dev, lib)['reserved'] == 0   # every chunk coalesced back
+
+
+def test_best_fit_split_and_coalesce(lib):
+    dev = 12
+    lib.pra_alloc_set_growth(dev, 16 * MB)
+    a = _alloc(lib, dev, 1 * MB)
+    b = _alloc(lib, dev, 3 * MB)
+    c = _alloc(lib, dev, 1 * MB)
+    d = _alloc(lib, dev, 2 * MB)
+    assert b == a + MB and c == b + 3 * MB            # split from one chunk, address order
+    lib.pra_free(b, 3 * MB, dev, None)
+    lib.pra_free(d, 2 * MB, dev, None)                 # d merges with the chunk's tail
+    e = _alloc(lib, dev, 2 * MB + 17)                  # best fit: b's 3 MB hole, not the tail
+    assert e == b
+    lib.pra_free(e, 0, dev, None)
+    lib.pra_free(a, MB, dev, None)
+    lib.pra_free(c, MB, dev, None)                     # a|b|c|tail coalesce into one block
+    st = A.stats(dev, lib)
+    assert st['num_chunks'] == 1 and st['allocated'] == 0
+    f = _alloc(lib, dev, 16 * MB)                      # whole chunk again: no new backend alloc
+    assert f == a and A.stats(dev, lib)['num_backend_allocs'] == 1
+    lib.pra_free(f, 0, dev, None)
+    assert lib.pra_alloc_check(dev) == 1
+
+
+_GPU_SCRIPT = r'''
+import paddle_ray_amd as paddle
+from paddle_ray_amd.native import allocator as A
+from paddle_ray_amd.models import gpt_config, GPTForPretraining
+assert A.enabled()
+paddle.set_device('gpu:0')
+m = GPTForPretraining(gpt_config('gpt3-tiny'))
+opt = paddle.optimizer.AdamW(1e-3, parameters=m.parameters())
+ids = paddle.randint(0, 1024, [4, 65])
+losses = []
+for _ in range(4):
+    loss = m(ids[:, :-1], ids[:, 1:])
+    loss.backward(); opt.step(); opt.clear_grad()
+    losses.append(float(loss))
+st = A.stats(0)
+print('STATS', st['num_allocs'], st['allocated'], st['reserved'], paddle.device.cuda.memory_allocated())
+assert st['num_allocs'] > 50 and st['reserved'] >= st['allocated'] > 0
+assert paddle.device.cuda.memory_allocated() == st['allocated']
+assert losses[-1] < losses[0], losses
+print('OK', losses)
+'''
+
+
+@pytest.mark.gpu
+def test_training_on_native_allocator_gpu():
+    env = dict(os.environ, PRA_ALLOCATOR='auto_growth')
+    r = subprocess.run([sys.executable, '-c', _GPU_SCRIPT], env=env, capture_output=True, text=True,
+                       timeout=300, cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    assert r.returncode == 0 and 'OK' in r.stdout, r.stdout[-2000:] + r.stderr[-3000:]
