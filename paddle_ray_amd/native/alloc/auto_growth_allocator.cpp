@@ -83,6 +83,12 @@ struct Stats {
 struct DeviceAllocator {
   std::mutex mu;
   size_t growth = size_t(64) << 20;  // minimum chunk size
+  // Events only matter once a second stream allocates: until then every block is reused in
+  // stream order and frees record nothing. When a second stream first shows up the device
+  // is synchronised once (all earlier, event-less frees are then complete).
+  stream_t first_stream = nullptr;
+  bool seen_stream = false, multi_stream = false;
+  std::vector<event_t> event_pool;
   // free blocks per stream, ordered by (size, address) -> best fit = lower_bound
   std::map<stream_t, std::set<std::pair<size_t, Block*>>> free_sets;
   std::unordered_map<void*, Block*> live;
@@ -97,12 +103,37 @@ struct DeviceAllocator {
     if (it != free_sets.end()) it->second.erase({b->size, b});
   }
 
-  Block* take(Block* b, size_t n, stream_t s) {
-    erase_free(b);
+  void note_stream(stream_t s) {
+    if (!seen_stream) {
+      seen_stream = true;
+      first_stream = s;
+    } else if (!multi_stream && s != first_stream) {
+      device_sync();
+      multi_stream = true;
+    }
+  }
+  event_t new_event(stream_t s) {
+    if (!multi_stream) return nullptr;
+#ifdef PRA_ALLOC_HOST
+    return event_record(s);
+#else
+    if (event_pool.empty()) return event_record(s);
+    event_t e = event_pool.back();
+    event_pool.pop_back();
+    (void)hipEventRecord(e, s);
+    return e;
+#endif
+  }
+  void drop_event(Block* b) {
     if (b->event) {
-      event_destroy(b->event);
+      event_pool.push_back(b->event);
       b->event = nullptr;
     }
+  }
+
+  Block* take(Block* b, size_t n, stream_t s) {
+    erase_free(b);
+    drop_event(b);
     if (b->size - n >= kMinSplit) {  // split: remainder stays free on the block's stream
       Block* r = new Block{b->ptr + n, b->size - n, true, b->chunk, b, b->next, b->stream, nullptr};
       if (b->next) b->next->prev = r;
@@ -164,7 +195,7 @@ struct DeviceAllocator {
       Block* b = c->head;
       if (b->free && b->next == nullptr && b->size == c->size && event_done(b->event)) {
         erase_free(b);
-        event_destroy(b->event);
+        drop_event(b);
         backend_free(c->base);
         st.reserved -= (int64_t)c->size;
         st.n_chunks--;
@@ -182,6 +213,7 @@ struct DeviceAllocator {
 
   void* alloc(size_t size, stream_t s) {
     std::lock_guard<std::mutex> g(mu);
+    note_stream(s);
     const size_t n = round(size);
     Block* b = find(n, s);
     if (!b) {
@@ -206,7 +238,7 @@ struct DeviceAllocator {
     st.n_free++;
     b->free = true;
     b->stream = s;
-    b->event = event_record(s);
+    b->event = new_event(s);
     // coalesce with free neighbours freed on the same stream, or whose pending work is done
     // (their event completed: any stream may take them, so the merged block can be s's)
     auto mergeable = [&](Block* o) {
@@ -215,7 +247,7 @@ struct DeviceAllocator {
     if (mergeable(b->next)) {
       Block* n = b->next;
       erase_free(n);
-      event_destroy(n->event);
+      drop_event(n);
       b->size += n->size;
       b->next = n->next;
       if (n->next) n->next->prev = b;
@@ -224,7 +256,7 @@ struct DeviceAllocator {
     if (mergeable(b->prev)) {
       Block* pr = b->prev;
       erase_free(pr);
-      event_destroy(pr->event);
+      drop_event(pr);
       pr->size += b->size;
       pr->next = b->next;
       if (b->next) b->next->prev = pr;
