@@ -897,6 +897,7 @@ EPI = {None: 0, 'gelu': 1, 'gelu_tanh': 2, 'relu': 3, 'dgelu': 4, 'dgelu_tanh': 
 # beta=1 accumulation), hipBLASLt for the dgrad dy·Wᵀ layout where it is still faster
 # (profiles/r2_gemm/summary.md); 'mfma' = in-tree kernel everywhere; 'blas' = hipBLASLt everywhere.
 _GEMM_MODE = __import__('os').environ.get('PRA_GEMM', 'auto')
+_GEMM_SHAPE_POLICY = __import__('os').environ.get('PRA_GEMM_POLICY', '1') == '1'
 
 
 def _gemm_operand_ok(t):
@@ -950,6 +951,15 @@ def _gemm_hip(layout, a, b, out=None, bias=None, z=None, epi=None, beta=0, want_
     else:
         K, M = a.shape
         N = b.shape[1]
+    if _GEMM_MODE == 'auto' and _GEMM_SHAPE_POLICY and epi is None and not want_colsum:
+        # per-shape policy from the measured table (profiles/r2_gemm/summary.md): hipBLASLt wins
+        # the long-K plain forward (fc2 x·W K=8192: 0.95x, LM-head dgrad K=50304: 0.94x) and
+        # the mid-size split-K wgrad (qkv 2048x6144: 0.91x, 192 tiles -> 4-way split)
+        tiles = ((M + 255) // 256) * ((N + 255) // 256)
+        if layout == GEMM_FWD and K >= 4096:
+            return None
+        if layout == GEMM_TN and 128 <= tiles < 224:
+            return None
     if out is None:
         out = torch.empty((M, N), device=a.device, dtype=a.dtype)
     elif not _gemm_operand_ok(out) or out.dtype != a.dtype or tuple(out.shape) != (M, N):
