@@ -94,6 +94,8 @@ def main():
 
     if a.model.startswith('gpt'):
         result = bench_gpt(a, paddle, torch, dist, C, world, rank, dev)
+    elif a.model.startswith('bert'):
+        result = bench_bert(a, paddle, torch, dist, C, world, rank, dev)
     else:
         result = bench_resnet(a, paddle, torch, dist, C, world, rank, dev)
     result['backend'] = dist.get_backend() if world > 1 else 'none'
@@ -208,6 +210,61 @@ def bench_resnet(a, paddle, torch, dist, C, world, rank, dev):
             "config": {"model": "ResNet50", "global_batch": bs * world, "seq_len": None,
                        "parallelism": f"dp{world}"},
             "samples_per_sec_per_gpu": round(ips / world, 2)}
+
+
+def bench_bert(a, paddle, torch, dist, C, world, rank, dev):
+    """BASELINE config 3: BERT-base pretraining through the STATIC-graph Executor with AMP
+    (static.amp.decorate, bf16): per-op grad ops, fwd+bwd replayed as one HIP graph, AdamW."""
+    import numpy as np
+    from paddle_ray_amd import static
+    from paddle_ray_amd.models import bert_config, BertForPretraining
+    name = 'bert-base-uncased' if a.model in ('bert', 'bert-base') else a.model
+    cfg = bert_config(name)
+    bs = a.micro_batch if a.micro_batch != 16 else 32
+    S = a.seq if a.seq != 1024 else 512
+    paddle.seed(1234)
+    model = BertForPretraining(cfg)
+    paddle.enable_static()
+    main_p, startup = static.Program(), static.Program()
+    with static.program_guard(main_p, startup):
+        ids_v = static.data('ids', [bs, S], 'int64')
+        lab_v = static.data('lab', [bs, S], 'int64')
+        nsp_v = static.data('nsp', [bs], 'int64')
+        loss_v = model(ids_v, labels=lab_v, next_sentence_label=nsp_v)
+        opt = static.amp.decorate(paddle.optimizer.AdamW(1e-4, parameters=model.parameters()),
+                                  use_bf16=True)
+        opt.minimize(loss_v)
+    exe = static.Executor()
+    exe.run(startup)
+    prog = main_p
+    if dev.type == 'cuda':
+        prog = static.CompiledProgram(main_p)
+        prog._build_strategy.use_hip_graph = True
+    rs = np.random.RandomState(rank)
+    ids = rs.randint(5, cfg.vocab_size, (bs, S))
+    lab = np.full((bs, S), -1)
+    pos = rs.rand(bs, S) < 0.15
+    lab[pos] = ids[pos]
+    ids[pos] = 103
+    feed = {'ids': torch.from_numpy(ids.astype('int64')).to(dev),
+            'lab': torch.from_numpy(lab.astype('int64')).to(dev),
+            'nsp': torch.from_numpy(rs.randint(0, 2, (bs,)).astype('int64')).to(dev)}
+    feed = {k: paddle.Tensor(v) for k, v in feed.items()}
+    last = [None]
+
+    def step():
+        last[0] = exe.run(prog, feed=feed, fetch_list=[loss_v], return_numpy=False)[0]
+
+    dt = _timed(step, a, torch, dist, world, dev)
+    paddle.disable_static()
+    sps = bs * world * a.steps / dt
+    return {"metric": "samples/sec BERT-base static+AMP", "value": round(sps, 2),
+            "unit": "sequences/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+            "ms_per_step": round(dt / a.steps * 1000, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
+            "config": {"model": name, "global_batch": bs * world, "seq_len": S,
+                       "parallelism": f"dp{world}", "executor": "static Program, HIP graph"},
+            "tokens_per_sec": round(sps * S, 1), "final_loss": float(last[0])}
 
 
 if __name__ == '__main__':

@@ -225,8 +225,9 @@ class BertModel(nn.Layer):
         if attention_mask is None:
             ids = _u(input_ids)
             pad = ids == self.pad_token_id
-            if not bool(pad.any()):
-                return None  # no padding: the flash kernel path
+            capturing = ids.is_cuda and torch.cuda.is_current_stream_capturing()
+            if not capturing and not bool(pad.any()):
+                return None  # no padding: the flash kernel path (a HIP graph keeps the mask)
             return Tensor((pad.to(dtype) * -1e4)[:, None, None, :])
         m = _u(attention_mask)
         if m.dim() == 2:
