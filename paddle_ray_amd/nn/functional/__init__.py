@@ -435,9 +435,11 @@ def _conv_padding(padding, n, t=None, ksize=None, stride=None, dilation=None):
     return _ntuple(padding, n), None
 
 
-# opt-in: measured slower on MI355X for ResNet50 (hipBLASLt has no split-K for the huge-K
-# wgrad GEMMs: 710 us vs MIOpen's 96 us), kept for A/B
-_CONV1X1_GEMM = os.environ.get('PRA_CONV1X1_GEMM', '0') == '1'
+# 1x1 channels-last convs: 'mfma' = GEMMs with the in-tree split-K MFMA kernel for dgrad /
+# wgrad (ops/fused.py Conv1x1Fn), 'blas' = one hipBLASLt GEMM per direction (round-1 A/B:
+# no split-K for the huge-K wgrad), 'miopen' = MIOpen's implicit-GEMM kernels
+_CONV1X1 = os.environ.get('PRA_CONV1X1', 'miopen')
+_CONV1X1_GEMM = _CONV1X1 == 'blas' or os.environ.get('PRA_CONV1X1_GEMM', '0') == '1'
 
 
 def _conv1x1_gemm(t, w, bias, st):
@@ -458,9 +460,12 @@ def _conv(fn, n, x, weight, bias, stride, padding, dilation, groups, data_format
     t = _t(x)
     cl = data_format in ('NHWC', 'NLC', 'NDHWC')
     pad_, extra = _conv_padding(padding, n)
-    if (_CONV1X1_GEMM and n == 2 and cl and t.is_cuda and groups == 1 and extra is None
-            and _t(weight).shape[2:] == (1, 1) and _ntuple(dilation, 2) == (1, 1)
+    if ((_CONV1X1_GEMM or _CONV1X1 == 'mfma') and n == 2 and cl and t.is_cuda and groups == 1
+            and extra is None and _t(weight).shape[2:] == (1, 1) and _ntuple(dilation, 2) == (1, 1)
             and pad_ in (0, (0, 0), [0, 0]) and t.dtype == _t(weight).dtype):
+        if _CONV1X1 == 'mfma' and t.dtype in (torch.bfloat16, torch.float16):
+            return _w(K.conv1x1_nhwc(t, _t(weight), None if bias is None else _t(bias),
+                                     _ntuple(stride, 2)))
         return _w(_conv1x1_gemm(t, _t(weight), None if bias is None else _t(bias),
                                 _ntuple(stride, 2)))
     if cl:

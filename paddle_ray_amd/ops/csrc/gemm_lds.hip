@@ -580,6 +580,14 @@ extern "C" int pra_gemm_lds_splits(int M, int N, int K) {
     const double eff = w / __builtin_ceil(w) * (1.0 - 0.03 * (sp - 1));
     if (eff > best_eff + 1e-9) { best_eff = eff; best = sp; }
   }
+  // few output tiles over a very long K (conv weight gradients: K = N*H*W up to ~800K):
+  // split further until the chip is covered, each split still >= 64 K-steps
+  if (tiles * best < 256 && nk / best >= 128) {
+    int sp = (256 + tiles - 1) / tiles;
+    if (sp > nk / 64) sp = nk / 64;
+    if (sp > 256) sp = 256;
+    if (sp > best) best = sp;
+  }
   return best;
 }
 

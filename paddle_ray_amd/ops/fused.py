@@ -1019,6 +1019,52 @@ def _gemm_ref_fast(layout, a, b, out, bias, z, epi, beta, want_colsum):
 
 
 # =============================================================================
+# 1x1 convolution (channels-last) as GEMMs: y = x·Wᵀ (hipBLASLt NT), dx = dy·W (in-tree MFMA
+# GEMM), dW = dyᵀ·x (in-tree MFMA GEMM, split-K over K = N·H·W). Parity: the reference's
+# conv2d with 1x1 filters (phi conv kernels); stride-2 1x1 (ResNet downsample) reads the
+# strided positions and scatters dx back.
+# =============================================================================
+class Conv1x1Fn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, bias, sh, sw):
+        xs = x if (sh, sw) == (1, 1) else x[:, ::sh, ::sw, :]
+        xs = xs.contiguous()
+        n, h, wd, cin = xs.shape
+        cout = w.shape[0]
+        x2, w2 = xs.view(-1, cin), w.reshape(cout, cin)
+        y = gemm(GEMM_NT, x2, w2, bias=None if bias is None else bias.to(x.dtype))
+        ctx.save_for_backward(x2, w2)
+        ctx.meta = (tuple(x.shape), tuple(xs.shape), tuple(w.shape), sh, sw, bias is not None)
+        return y.view(n, h, wd, cout)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w2 = ctx.saved_tensors
+        xshape, xsshape, wshape, sh, sw, hb = ctx.meta
+        dy2 = dy.reshape(-1, w2.shape[0])
+        if not dy2.is_contiguous() or dy2.data_ptr() % 16:
+            dy2 = dy2.contiguous()
+        dy2 = _like(dy2, x2.dtype)
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx2 = gemm(GEMM_FWD, dy2, w2)
+            if (sh, sw) == (1, 1):
+                dx = dx2.view(xshape)
+            else:
+                dx = torch.zeros(xshape, dtype=dx2.dtype, device=dx2.device)
+                dx[:, ::sh, ::sw, :] = dx2.view(xsshape)
+        if ctx.needs_input_grad[1]:
+            dw = gemm(GEMM_TN, dy2, x2).view(wshape)
+        if hb and ctx.needs_input_grad[2]:
+            db = dy2.sum(0, dtype=torch.float32).to(dy2.dtype)
+        return dx, dw, db, None, None
+
+
+def conv1x1_nhwc(x, w, bias=None, stride=(1, 1)):
+    return Conv1x1Fn.apply(x, w, bias, int(stride[0]), int(stride[1]))
+
+
+# =============================================================================
 # Linear with fused weight-gradient accumulation
 # =============================================================================
 def _acc_grad_ok(g, w, dt):
