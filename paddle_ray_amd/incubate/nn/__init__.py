@@ -1,7 +1,7 @@
 """paddle.incubate.nn fused layers (parity: python/paddle/incubate/nn/layer/fused_transformer.py)."""
 from . import functional  # noqa
 from .layer import (FusedMultiHeadAttention, FusedFeedForward, FusedTransformerEncoderLayer,  # noqa
-                    FusedMultiTransformer, FusedLinear, FusedBiasDropoutResidualLayerNorm,
+                    FusedMultiTransformer, FusedMultiTransformerDecoder, FusedLinear, FusedBiasDropoutResidualLayerNorm,
                     FusedEcMoe, FusedDropoutAdd)
 from . import attn_bias  # noqa: E402,F401
 from .memory_efficient_attention import memory_efficient_attention  # noqa: E402,F401

@@ -221,8 +221,12 @@ def fused_multi_transformer(x, ln_scales, ln_biases, qkv_weights, qkv_biases, li
     n = len(qkv_weights)
     p = dropout_rate if training else 0.0
     decode = time_step is not None
-    t = int(_u(time_step).reshape(-1)[0]) if decode and not isinstance(time_step, int) else \
-        (int(time_step) if decode else None)
+    if decode and not isinstance(time_step, int):
+        ts = _u(time_step)
+        # a device int32 step stays on the device (graph-capturable decode); host -> int
+        t = ts.reshape(-1)[:1] if (ts.is_cuda and ts.dtype == torch.int32) else int(ts.reshape(-1)[0])
+    else:
+        t = int(time_step) if decode else None
     if decode and S != 1:
         raise ValueError("fused_multi_transformer: decode phase (time_step given) takes one token")
     rot = None

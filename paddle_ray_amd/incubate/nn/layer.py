@@ -194,6 +194,89 @@ class FusedMultiTransformer(Layer):
             trans_qkvw=self._trans_qkvw)
 
 
+class FusedMultiTransformerDecoder:
+    """Serving loop for a ``FusedMultiTransformer``: persistent KV caches, a prefill call, and
+    per-token decode steps replayed from ONE captured HIP graph (the decode-attention kernel
+    reads the position from a device int32 counter that the graph itself advances), so a
+    step costs one graph launch instead of ~10 kernel launches per layer.
+
+        dec = FusedMultiTransformerDecoder(model, batch_size=8, max_seq_len=2048)
+        h = dec.prefill(prompt_hidden)          # [B, S0, E], fills the caches
+        for _ in range(n): h_t = dec.step(x_t)  # [B, 1, E] -> [B, 1, E]
+    ``attn_mask`` (additive, [B, max_seq_len]) masks padded positions across all steps.
+    """
+
+    def __init__(self, model, batch_size, max_seq_len, use_graph=True):
+        import torch
+        self.model = model
+        self.B, self.L = int(batch_size), int(max_seq_len)
+        p0 = model.qkv_weights[0]._t
+        self.dev, self.dtype = p0.device, p0.dtype
+        H, D, E = model.num_heads, model.head_dim, model.embed_dim
+        n = len(model.qkv_weights)
+        self.caches = [torch.zeros(2, self.B, H, self.L, D, device=self.dev, dtype=self.dtype)
+                       for _ in range(n)]
+        self.t = torch.zeros(1, dtype=torch.int32, device=self.dev)
+        self.mask = torch.zeros(self.B, 1, 1, self.L, dtype=torch.float32, device=self.dev)
+        self.x_buf = torch.zeros(self.B, 1, E, device=self.dev, dtype=self.dtype)
+        self.use_graph = use_graph and self.dev.type == 'cuda'
+        self._graph = None
+        self._out = None
+
+    def _caches(self):
+        from ...framework.core import Tensor
+        return [Tensor(c) for c in self.caches]
+
+    def set_mask(self, attn_mask):
+        import torch
+        m = attn_mask._t if hasattr(attn_mask, '_t') else torch.as_tensor(attn_mask)
+        self.mask.copy_(m.reshape(self.B, 1, 1, self.L).to(self.mask.dtype))
+
+    def prefill(self, x, attn_mask=None):
+        """Context phase over the prompt (caches filled in place); decode continues at S0."""
+        from ...framework.core import Tensor
+        import torch
+        xt = x._t if hasattr(x, '_t') else x
+        S0 = xt.shape[1]
+        if attn_mask is None:
+            m = torch.triu(torch.full((S0, S0), float('-inf'), device=self.dev), 1)
+            attn_mask = Tensor(m.expand(self.B, 1, S0, S0).to(self.dtype))
+        with torch.no_grad():
+            out, _ = self.model(Tensor(xt), attn_mask=attn_mask, caches=self._caches())
+        self.t.fill_(S0)
+        return out
+
+    def _step_eager(self):
+        from ...framework.core import Tensor
+        out, _ = self.model(Tensor(self.x_buf), attn_mask=Tensor(self.mask), caches=self._caches(),
+                            time_step=Tensor(self.t))
+        return out._t
+
+    def step(self, x_tok):
+        """One token for every sequence: returns [B, 1, E]; the position advances by one."""
+        import torch
+        from ...framework.core import Tensor
+        xt = x_tok._t if hasattr(x_tok, '_t') else x_tok
+        self.x_buf.copy_(xt.reshape(self.x_buf.shape))
+        with torch.no_grad():
+            if not self.use_graph:
+                out = self._step_eager()
+                self.t.add_(1)
+                return Tensor(out)
+            if self._graph is None:
+                s = torch.cuda.Stream()
+                s.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(s):  # warm-up (rewrites the same cache slot, t unchanged)
+                    self._step_eager()
+                torch.cuda.current_stream().wait_stream(s)
+                self._graph = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(self._graph):
+                    self._out = self._step_eager()
+                    self.t.add_(1)
+            self._graph.replay()
+        return Tensor(self._out.clone())
+
+
 class FusedEcMoe(Layer):
     def __init__(self, hidden_size, inter_size, num_experts, act_type, weight_attr=None,
                  bias_attr=None):

@@ -32,8 +32,8 @@ void pra_vp_ce_bwd(const void*, const int64_t*, const float*, const float*, void
                    int, hipStream_t);
 const char* pra_build_info();
 int pra_mmha_splits(int, int, int);
-int pra_mmha_decode(const void*, void*, const float*, float*, void*, int, int, int, int, int, int, int, float, int,
-                    hipStream_t);
+int pra_mmha_decode(const void*, void*, const float*, float*, void*, int, int, int, int, int, const int*, int, int,
+                    float, int, hipStream_t);
 void pra_bias_gelu_fwd(const void*, const void*, void*, int64_t, int, int, int, hipStream_t);
 void pra_bias_gelu_bwd(const void*, const void*, const void*, void*, int64_t, int, int, int, hipStream_t);
 void pra_adamw_mt(const int64_t*, const float*, const int64_t*, int, float, float, float, float, float, float, float,
@@ -157,10 +157,10 @@ PYBIND11_MODULE(_pra_hip, m) {
   });
   m.def("build_info", []() { return std::string(pra_build_info()); });
   m.def("mmha_splits", [](int B, int H, int t) { return pra_mmha_splits(B, H, t); });
-  m.def("mmha_decode", [](P qkv, P cache, P mask, P ws, P out, int B, int H, int L, int D, int t, int splits,
-                          int mask_len, float scale, int dt, P s) {
-    if (pra_mmha_decode(CV(qkv), V(cache), CF(mask), F(ws), V(out), B, H, L, D, t, splits, mask_len, scale, dt,
-                        S(s)) != 0)
+  m.def("mmha_decode", [](P qkv, P cache, P mask, P ws, P out, int B, int H, int L, int D, int t, P t_dev,
+                          int splits, int mask_len, float scale, int dt, P s) {
+    if (pra_mmha_decode(CV(qkv), V(cache), CF(mask), F(ws), V(out), B, H, L, D, t,
+                        reinterpret_cast<const int*>(t_dev), splits, mask_len, scale, dt, S(s)) != 0)
       throw std::invalid_argument("mmha_decode: unsupported head_dim/dtype or time_step out of range");
     check_launch("mmha_decode");
   });

@@ -53,15 +53,20 @@ __global__ void __launch_bounds__(kWaves * 64) mmha_split_k(
     float* __restrict__ ws_ml,      // [B, H, S, 2]
     float* __restrict__ ws_acc,     // [B, H, S, D]
     T* __restrict__ out,            // [B, H, D] (used when splits == 1)
-    int B, int H, int L, int t, int keys_per_split, int mask_len, float scale) {
+    int B, int H, int L, int t_host, const int* __restrict__ t_dev, int keys_per_split, int mask_len,
+    float scale) {
+  // t_dev (HIP-graph decode loops): the position comes from device memory, so one captured
+  // graph serves every step; an out-of-range position writes nothing and outputs zeros
+  const int t = t_dev ? t_dev[0] : t_host;
   constexpr int G = D / 8;            // lanes per key
   constexpr int KPW = 64 / G;         // keys per wave per sub-step
   const int split = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
   const int splits = gridDim.x;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int gl = lane % G, grp = lane / G;
+  const bool t_ok = t >= 0 && t < L && !(mask && mask_len < t + 1);
   const int lo = split * keys_per_split;
-  const int hi = min(t + 1, lo + keys_per_split);
+  const int hi = t_ok ? min(t + 1, lo + keys_per_split) : lo;
 
   const size_t BH = (size_t)B * H;
   const T* qrow = qkv + ((size_t)b * 3 * H + h) * D;
@@ -70,7 +75,7 @@ __global__ void __launch_bounds__(kWaves * 64) mmha_split_k(
   T* kc = cache + ((size_t)b * H + h) * (size_t)L * D;
   T* vc = cache + (BH + (size_t)b * H + h) * (size_t)L * D;
 
-  if (t >= lo && t < hi && wave == 0 && grp == 0) {  // append the new token to the cache
+  if (t_ok && t >= lo && t < hi && wave == 0 && grp == 0) {  // append the new token to the cache
     float kv[8];
     load8<T>(knew + gl * 8, kv);
     store8<T>(kc + (size_t)t * D + gl * 8, kv);
@@ -176,13 +181,13 @@ __global__ void __launch_bounds__(D) mmha_combine_k(const float* __restrict__ ws
 
 template <typename T, int D>
 int launch(const void* qkv, void* cache, const float* mask, float* ws, void* out, int B, int H, int L, int t,
-           int splits, int mask_len, float scale, hipStream_t s) {
-  const int keys = t + 1;
+           const int* t_dev, int splits, int mask_len, float scale, hipStream_t s) {
+  const int keys = t_dev ? L : t + 1;  // device position: splits cover the whole cache
   const int per = (keys + splits - 1) / splits;
   float* ws_ml = ws;
   float* ws_acc = ws + (((size_t)B * H * splits * 2 + 3) / 4) * 4;  // 16-B aligned
   hipLaunchKernelGGL((mmha_split_k<T, D>), dim3(splits, H, B), dim3(kWaves * 64), 0, s, (const T*)qkv, (T*)cache,
-                     mask, ws_ml, ws_acc, (T*)out, B, H, L, t, per, mask_len, scale);
+                     mask, ws_ml, ws_acc, (T*)out, B, H, L, t, t_dev, per, mask_len, scale);
   if (splits > 1)
     hipLaunchKernelGGL((mmha_combine_k<T, D>), dim3(H, B), dim3(D), 0, s, ws_ml, ws_acc, (T*)out, splits);
   return 0;
@@ -207,13 +212,14 @@ int pra_mmha_splits(int B, int H, int t) {
 
 // ws: fp32 workspace of B*H*splits*(2 + D) + 4 floats (unused when splits == 1)
 int pra_mmha_decode(const void* qkv, void* cache, const float* mask, float* ws, void* out, int B, int H, int L,
-                    int D, int t, int splits, int mask_len, float scale, int dt, hipStream_t s) {
-  if (t < 0 || t >= L || splits < 1 || (mask && mask_len < t + 1)) return -1;
+                    int D, int t, const int* t_dev, int splits, int mask_len, float scale, int dt, hipStream_t s) {
+  if (splits < 1) return -1;
+  if (!t_dev && (t < 0 || t >= L || (mask && mask_len < t + 1))) return -1;
 #define PRA_MMHA(TT)                                                                                          \
   switch (D) {                                                                                                \
-    case 64: return launch<TT, 64>(qkv, cache, mask, ws, out, B, H, L, t, splits, mask_len, scale, s);        \
-    case 128: return launch<TT, 128>(qkv, cache, mask, ws, out, B, H, L, t, splits, mask_len, scale, s);      \
-    case 256: return launch<TT, 256>(qkv, cache, mask, ws, out, B, H, L, t, splits, mask_len, scale, s);      \
+    case 64: return launch<TT, 64>(qkv, cache, mask, ws, out, B, H, L, t, t_dev, splits, mask_len, scale, s);        \
+    case 128: return launch<TT, 128>(qkv, cache, mask, ws, out, B, H, L, t, t_dev, splits, mask_len, scale, s);      \
+    case 256: return launch<TT, 256>(qkv, cache, mask, ws, out, B, H, L, t, t_dev, splits, mask_len, scale, s);      \
     default: return -1;                                                                                       \
   }
   if (dt == kBF16) { PRA_MMHA(bf16) }

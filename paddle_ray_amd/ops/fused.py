@@ -626,6 +626,8 @@ def vocab_parallel_cross_entropy(logits, labels, pg=None, world=1, rank=0, ignor
 # =============================================================================
 @R.register_kernel('mmha_decode', 'ref')
 def _mmha_ref(qkv, cache, t, mask):
+    if isinstance(t, torch.Tensor):
+        t = int(t.reshape(-1)[0])
     q, k, v = qkv.unbind(1)                                   # [B, H, D]
     cache[0, :, :, t] = k
     cache[1, :, :, t] = v
@@ -641,11 +643,17 @@ def _mmha_ref(qkv, cache, t, mask):
 def _mmha_hip(qkv, cache, t, mask):
     B, _, H, D = qkv.shape
     L = cache.shape[3]
+    t_dev = None
+    if isinstance(t, torch.Tensor):  # device position (HIP-graph decode loops): read in-kernel
+        if not (t.is_cuda and t.dtype == torch.int32 and t.is_contiguous()):
+            raise ValueError("mmha_decode: a tensor time_step must be a CUDA int32 tensor")
+        t_dev, t = t, 0
     if not (qkv.is_contiguous() and cache.is_contiguous() and cache.dtype == qkv.dtype and
-            tuple(cache.shape) == (2, B, H, L, D) and D in (64, 128, 256) and 0 <= t < L):
+            tuple(cache.shape) == (2, B, H, L, D) and D in (64, 128, 256) and
+            (t_dev is not None or 0 <= t < L)):
         raise ValueError(f"mmha_decode: qkv {tuple(qkv.shape)} / cache {tuple(cache.shape)} / "
                          f"t={t} not supported by the HIP kernel")
-    splits = _native.lib().mmha_splits(B, H, t)
+    splits = _native.lib().mmha_splits(B, H, L - 1 if t_dev is not None else t)
     ws = torch.empty(B * H * splits * (2 + D) + 4 if splits > 1 else 4, device=qkv.device,
                      dtype=torch.float32)
     out = torch.empty(B, H, D, device=qkv.device, dtype=qkv.dtype)
@@ -653,18 +661,22 @@ def _mmha_hip(qkv, cache, t, mask):
     if mask is not None:
         mask = mask.reshape(B, -1).float().contiguous()
         mlen = mask.shape[1]
-        if mlen < t + 1:
+        if t_dev is None and mlen < t + 1:
             raise ValueError(f"mmha_decode: mask covers {mlen} positions, need {t + 1}")
     _native.lib().mmha_decode(_ptr(qkv), _ptr(cache), _ptr(mask) if mask is not None else 0,
-                              _ptr(ws), _ptr(out), B, H, L, D, int(t), splits, mlen,
+                              _ptr(ws), _ptr(out), B, H, L, D, int(t),
+                              _ptr(t_dev) if t_dev is not None else 0, splits, mlen,
                               1.0 / math.sqrt(D), _dt(qkv), _stream())
     return out
 
 
 def mmha_decode(qkv, cache, time_step, mask=None):
     """One decode step of multi-head attention; returns [B, H, D] and appends K/V to
-    ``cache`` at ``time_step`` in place."""
-    return R.dispatch('mmha_decode', qkv, qkv.contiguous(), cache, int(time_step), mask)
+    ``cache`` at ``time_step`` in place. ``time_step`` may be a CUDA int32 tensor: the kernel
+    reads it on the device (no host sync), so the step can live in a captured HIP graph."""
+    if not isinstance(time_step, torch.Tensor):
+        time_step = int(time_step)
+    return R.dispatch('mmha_decode', qkv, qkv.contiguous(), cache, time_step, mask)
 
 
 # =============================================================================
@@ -956,8 +968,8 @@ def _gemm_hip(layout, a, b, out=None, bias=None, z=None, epi=None, beta=0, want_
         # the long-K plain forward (fc2 x·W K=8192: 0.95x, LM-head dgrad K=50304: 0.94x) and
         # the mid-size split-K wgrad (qkv 2048x6144: 0.91x, 192 tiles -> 4-way split)
         tiles = ((M + 255) // 256) * ((N + 255) // 256)
-        if layout == GEMM_FWD and K >= 4096:
-            return None
+        if layout == GEMM_FWD and (K >= 4096 or M < 128):
+            return None  # long-K forward, and skinny decode-time GEMMs (256-row tiles idle)
         if layout == GEMM_TN and 128 <= tiles < 224:
             return None
     if out is None:
@@ -1702,7 +1714,10 @@ def gemm_bias_act(x, w, b=None, act=None):
     MFMA kernel launch (gemm.hip); unsupported layouts fall back to matmul + epilogue."""
     a = _ACT[act] if not isinstance(act, int) else act
     x2 = x.reshape(-1, x.shape[-1])
-    if x.is_cuda and not gemm_supported(x2 if x2.is_contiguous() else x2.contiguous(), w):
+    if x.is_cuda and (x2.shape[0] < 128 or
+                      not gemm_supported(x2 if x2.is_contiguous() else x2.contiguous(), w)):
+        # skinny (decode-time) rows: hipBLASLt + the activation (3.0 vs 3.6 ms per 24-layer
+        # graph decode step at batch 8); the MFMA tile would idle
         z = torch.matmul(x, w)
         return _act_ref(z if b is None else z + b, a)
     return GemmBiasActFn.apply(x, w, b, a)

@@ -68,6 +68,19 @@ def main():
     print(json.dumps(dict(model=f'{L}x{E} FusedMultiTransformer decode', batch=B, ctx=ctx,
                           ms_per_token_step=round(dt * 1e3, 3),
                           tokens_per_s=round(B / dt, 1))), flush=True)
+    # the same step replayed from one captured HIP graph (device-side position counter)
+    from paddle_ray_amd.incubate.nn import FusedMultiTransformerDecoder
+    dec = FusedMultiTransformerDecoder(m, B, ctx + 256)
+    dec.t.fill_(ctx)
+    xt = torch.randn(B, 1, E, device='cuda', dtype=torch.bfloat16)
+
+    def gstep():
+        dec.step(xt)
+        dec.t.fill_(ctx)  # keep the context length fixed for the measurement
+    dg = bench(gstep, iters=50, warmup=3)
+    print(json.dumps(dict(model=f'{L}x{E} FusedMultiTransformerDecoder (HIP graph)', batch=B,
+                          ctx=ctx, ms_per_token_step=round(dg * 1e3, 3),
+                          tokens_per_s=round(B / dg, 1))), flush=True)
 
 
 if __name__ == '__main__':

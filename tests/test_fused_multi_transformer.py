@@ -175,3 +175,33 @@ def test_generation_on_gpu_bf16():
     m = _model(True, E=256, H=2, F=512, L=2)       # head_dim 128
     m.to(dtype='bfloat16')
     _generate_vs_full(m, 2, 9, 6, device='cuda', dtype=torch.bfloat16, tol=2e-2)
+
+
+def _decoder_vs_full(dev, dtype, tol, E=32, H=4, L=2):
+    from paddle_ray_amd.incubate.nn import FusedMultiTransformerDecoder
+    m = _model(True, E=E, H=H, F=2 * E, L=L)
+    if dtype != torch.float32:
+        m.to(dtype='bfloat16')
+    B, S0, steps = 2, 5, 4
+    x = torch.randn(B, S0 + steps, E).to(device=dev, dtype=dtype)
+    full = m(paddle.Tensor(x), attn_mask=paddle.Tensor(_causal(S0 + steps, B).to(dev, dtype)))._t
+    dec = FusedMultiTransformerDecoder(m, B, 16)
+    out = dec.prefill(paddle.Tensor(x[:, :S0]))
+    _close(out._t, full[:, :S0], tol)
+    for t in range(S0, S0 + steps):
+        o = dec.step(paddle.Tensor(x[:, t:t + 1]))
+        _close(o._t[:, 0], full[:, t], tol)
+    assert int(dec.t.item()) == S0 + steps
+    return dec
+
+
+def test_decoder_runner_cpu():
+    dec = _decoder_vs_full('cpu', torch.float32, 2e-5)
+    assert dec._graph is None
+
+
+@pytest.mark.gpu
+def test_decoder_runner_hip_graph_gpu():
+    paddle.set_device('gpu')
+    dec = _decoder_vs_full('cuda', torch.bfloat16, 2e-2, E=256, H=2)
+    assert dec._graph is not None   # steps after the first replayed the captured graph
