@@ -436,9 +436,10 @@ def _conv_padding(padding, n, t=None, ksize=None, stride=None, dilation=None):
 
 
 # 1x1 channels-last convs: 'mfma' = GEMMs with the in-tree split-K MFMA kernel for dgrad /
-# wgrad (ops/fused.py Conv1x1Fn), 'blas' = one hipBLASLt GEMM per direction (round-1 A/B:
+# wgrad (ops/fused.py Conv1x1Fn; default: ResNet50 7596 vs 7485 img/s with MIOpen, A/B on one
+# box), 'blas' = one hipBLASLt GEMM per direction (round-1 A/B:
 # no split-K for the huge-K wgrad), 'miopen' = MIOpen's implicit-GEMM kernels
-_CONV1X1 = os.environ.get('PRA_CONV1X1', 'miopen')
+_CONV1X1 = os.environ.get('PRA_CONV1X1', 'mfma')
 _CONV1X1_GEMM = _CONV1X1 == 'blas' or os.environ.get('PRA_CONV1X1_GEMM', '0') == '1'
 
 
