@@ -641,6 +641,65 @@ bwd_dkdv_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __res
       nt_lo = __builtin_amdgcn_readfirstlane(nt_lo);
       nt_hi = __builtin_amdgcn_readfirstlane(nt_hi);
     }
+    if constexpr (!MASK) {
+      // software-pipelined unmasked tile: S/dP of BOTH 32-query halves first, then each
+      // half's softmax VALU sits behind the other half's MFMAs in program order (nothing
+      // pins the order there), so the matrix pipe keeps running while the exps issue
+      f32x16 sa[2], da[2];
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) {
+        sa[nt] = f32x16{};
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const float4 d4 = *reinterpret_cast<const float4*>(Dl + 32 * nt + 8 * g + 4 * h);
+          da[nt][4 * g + 0] = -d4.x; da[nt][4 * g + 1] = -d4.y;
+          da[nt][4 * g + 2] = -d4.z; da[nt][4 * g + 3] = -d4.w;
+        }
+        typename V8<T>::type qfr[NS], dfr[NS];
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+          qfr[s] = frag_rows<T, D>(Qs, lo, nt, s);
+          dfr[s] = frag_rows<T, D>(Ds, lo, nt, s);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+          sa[nt] = mfma<T>(qfr[s], kf[s], sa[nt]);
+          da[nt] = mfma<T>(dfr[s], vf[s], da[nt]);
+        }
+      }
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const float4 l4 = *reinterpret_cast<const float4*>(Ls + 32 * nt + 8 * g + 4 * h);
+          const float la[4] = {l4.x, l4.y, l4.z, l4.w};
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            const int i = 4 * g + c;
+            const float p = fexp2(fmaf(sa[nt][i], scale_log2, -la[c]));
+            sa[nt][i] = p;
+            da[nt][i] = p * da[nt][i];
+          }
+        }
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          typename V8<T>::type dtr[ND], qtr[ND];
+#pragma unroll
+          for (int dt = 0; dt < ND; ++dt) {
+            dtr[dt] = frag_tr<T, D>(Ds, lo, dt, 2 * nt + ks);
+            qtr[dt] = frag_tr<T, D>(Qs, lo, dt, 2 * nt + ks);
+          }
+          const typename V8<T>::type pf = pack_frag<T>(sa[nt], 8 * ks);
+          const typename V8<T>::type sf = pack_frag<T>(da[nt], 8 * ks);
+#pragma unroll
+          for (int dt = 0; dt < ND; ++dt) {
+            acc_v[dt] = mfma<T>(dtr[dt], pf, acc_v[dt]);
+            acc_k[dt] = mfma<T>(qtr[dt], sf, acc_k[dt]);
+          }
+        }
+      }
+    } else
 #pragma unroll
     for (int nt = 0; nt < 2; ++nt) {  // two 32-query halves of the tile
       if (nt < nt_lo || nt >= nt_hi) continue;
