@@ -35,6 +35,7 @@
 // `beta=1` accumulates into C (dW += xᵀ·dy straight into the flat gradient buffer).
 #include "common.h"
 #include <stdlib.h>
+#include <type_traits>
 
 namespace pra {
 namespace {
@@ -149,6 +150,7 @@ struct Dma {
     base = (uint64_t)b;
     step = KC ? (uint64_t)BKT * 2 : (uint64_t)BKT * ld * 2;
   }
+  __device__ __forceinline__ void advance(int ksteps) { base += (uint64_t)ksteps * step; }
   __device__ __forceinline__ void issue1(uint32_t lds_img, int wave, int kt, int n) {
     const uint64_t g = base + (uint64_t)kt * step;
     // readfirstlane returns int: go through uint32_t so the low word is ZERO-extended
@@ -159,6 +161,47 @@ struct Dma {
     // vmcnt(0) ahead of the fragment reads: the explicit vmcnt in the K loop is the only wait.
     const uint32_t dst = __builtin_amdgcn_readfirstlane(lds_img + (n * NT + wave * 64) * 16);
     asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff[n]), "s"(gs), "s"(dst)
+                 : "memory");
+  }
+};
+
+// Implicit-GEMM convolution operand A = im2col(x) for a channels-last input that is already
+// zero-padded spatially (x_pad [N][Hp][Wp][C]): row m = output pixel (n, ho, wo), column
+// k = (kh, kw, c). With C % 64 == 0 a K-step (64 k) lies inside one filter tap, so every staged
+// row segment is 128 contiguous bytes of one input pixel: the LDS-DMA gathers rows straight
+// from x_pad (per-lane source addresses), nothing is materialised.
+struct ConvGeom {
+  int Ho, Wo, Hp, Wp, C, KW, S;
+};
+
+template <int NT, int NDMA>
+struct ConvDmaA {
+  uint32_t pix[NDMA];  // element offset of x_pad[n][ho*S][wo*S][8c] for the staged row / chunk
+  uint64_t base;
+  int kt0;
+  ConvGeom g;
+  __device__ __forceinline__ void init(const uint16_t* x, const ConvGeom& cg, int m0, int M, int tid) {
+    g = cg;
+#pragma unroll
+    for (int n = 0; n < NDMA; ++n) {
+      const int P = n * NT + tid;
+      const int row = P >> 3, c = (P & 7) ^ kc_swz(row);
+      const int m = min(m0 + row, M - 1);
+      const int wo = m % g.Wo, t = m / g.Wo, ho = t % g.Ho, img = t / g.Ho;
+      pix[n] = (uint32_t)(((img * g.Hp + ho * g.S) * g.Wp + wo * g.S) * g.C + 8 * c);
+    }
+    base = (uint64_t)x;
+    kt0 = 0;
+  }
+  __device__ __forceinline__ void advance(int ksteps) { kt0 += ksteps; }
+  __device__ __forceinline__ void issue1(uint32_t lds_img, int wave, int kt, int n) {
+    const int k0 = (kt + kt0) * BKT;                 // wave-uniform: scalar math
+    const int tap = k0 / g.C, cin0 = k0 - tap * g.C, kh = tap / g.KW, kw = tap - kh * g.KW;
+    const uint32_t voff = (pix[n] + (uint32_t)((kh * g.Wp + kw) * g.C + cin0)) * 2u;
+    const uint64_t gs = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(base >> 32)) << 32) |
+                        (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)base);
+    const uint32_t dst = __builtin_amdgcn_readfirstlane(lds_img + (n * NT + wave * 64) * 16);
+    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(gs), "s"(dst)
                  : "memory");
   }
 };
@@ -185,12 +228,12 @@ __device__ __forceinline__ typename V8<T>::type frag(const char* img, int r0, in
   }
 }
 
-template <typename T, typename CF, bool AK, bool BK, int E, bool BETA, bool SPLIT>
+template <typename T, typename CF, bool AK, bool BK, int E, bool BETA, bool SPLIT, bool CONV = false>
 __global__ __launch_bounds__(CF::NT, 1) void gemm_lds_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
                                                           const uint16_t* __restrict__ bias, uint16_t* __restrict__ C,
                                                           uint16_t* __restrict__ Z, float* __restrict__ colsum,
                                                           int M, int N, int K, int lda, int ldb, int ldc, int ldz,
-                                                          int splits, float* __restrict__ ws) {
+                                                          int splits, float* __restrict__ ws, ConvGeom cg = {}) {
   constexpr int NT = CF::NT, TI = CF::TI, TJ = CF::TJ, NDMA = CF::NDMA, WC = CF::WC;
   constexpr int RW = TI * 16, CW = TJ * 16;  // rows / columns per wave
   __shared__ __attribute__((aligned(1024))) char lds[LDS_BYTES];
@@ -215,16 +258,18 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_lds_kernel(const uint16_t* __r
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wr = wave / WC, wc = wave % WC;
 
-  Dma<AK, NT, NDMA> da;
+  typename std::conditional<CONV, ConvDmaA<NT, NDMA>, Dma<AK, NT, NDMA>>::type da;
   Dma<BK, NT, NDMA> db;
-  if (AK) da.init(A, lda, m0, M - 1, tid); else da.init(A, lda, m0, M - 8, tid);
+  if constexpr (CONV) da.init(A, cg, m0, M, tid);
+  else if (AK) da.init(A, lda, m0, M - 1, tid);
+  else da.init(A, lda, m0, M - 8, tid);
   if (BK) db.init(B, ldb, n0, N - 1, tid); else db.init(B, ldb, n0, N - 8, tid);
   int nk = K / BKT;
   if (SPLIT) {
     const int per = (nk + splits - 1) / splits, kb = split * per;
     nk = max(0, min(nk, kb + per) - kb);
-    da.base += (uint64_t)kb * da.step;
-    db.base += (uint64_t)kb * db.step;
+    da.advance(kb);
+    db.advance(kb);
   }
 
   f32x4 acc[TI][TJ];
@@ -558,8 +603,39 @@ int launch_t(int layout, const void* A, const void* B, const void* bias, void* C
   }
 }
 
+template <typename T, int E>
+int launch_conv(const void* xpad, const void* W, const void* bias, void* Y, int M, int N, int K, const ConvGeom& cg,
+                hipStream_t s) {
+  const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  gemm_lds_kernel<T, W8, true, false, E, false, false, true><<<tiles, W8::NT, 0, s>>>(
+      static_cast<const uint16_t*>(xpad), static_cast<const uint16_t*>(W), static_cast<const uint16_t*>(bias),
+      static_cast<uint16_t*>(Y), nullptr, nullptr, M, N, K, 0, N, N, N, 1, nullptr, cg);
+  return 0;
+}
+
 }  // namespace
 }  // namespace pra
+
+// Implicit-GEMM convolution, channels-last, on the LDS-DMA MFMA kernel:
+//   Y[N*Ho*Wo][Cout] = im2col(x_pad) · Wk[KH*KW*C][Cout] (+ bias, optional ReLU)
+// x_pad is the zero-padded input [N][Hp][Wp][C]; Wk the HWIO filter as a [K][Cout] matrix.
+// Requires C % 64 == 0, Cout % 8 == 0, x_pad smaller than 4 GB (32-bit DMA offsets).
+extern "C" int pra_conv_lds(const void* xpad, const void* W, const void* bias, void* Y, int Nimg, int Hp, int Wp,
+                            int C, int Ho, int Wo, int Cout, int KH, int KW, int S, int relu, int dtype,
+                            hipStream_t s) {
+  if (C % 64 || Cout % 8 || KH <= 0 || KW <= 0 || S <= 0) return -1;
+  if ((long long)Nimg * Hp * Wp * C * 2 >= (1ll << 32)) return -1;
+  if ((Ho - 1) * S + KH > Hp || (Wo - 1) * S + KW > Wp) return -1;
+  const long long Mll = (long long)Nimg * Ho * Wo;
+  if (Mll >= (1ll << 31)) return -1;
+  const int M = (int)Mll, K = KH * KW * C;
+  pra::ConvGeom cg{Ho, Wo, Hp, Wp, C, KW, S};
+  if (dtype == pra::kBF16) return relu ? pra::launch_conv<pra::bf16, pra::kRelu>(xpad, W, bias, Y, M, Cout, K, cg, s)
+                                  : pra::launch_conv<pra::bf16, pra::kNone>(xpad, W, bias, Y, M, Cout, K, cg, s);
+  if (dtype == pra::kF16) return relu ? pra::launch_conv<pra::f16, pra::kRelu>(xpad, W, bias, Y, M, Cout, K, cg, s)
+                                 : pra::launch_conv<pra::f16, pra::kNone>(xpad, W, bias, Y, M, Cout, K, cg, s);
+  return -1;
+}
 
 // layout: 0 = A[M][K]·B[K][N] (forward), 1 = A[M][K]·B[N][K]ᵀ (dgrad / NT), 2 = A[K][M]ᵀ·B[K][N] (wgrad).
 // epi: 0 none, 1 gelu(erf), 2 gelu(tanh), 3 relu (Z receives the pre-activation if given),

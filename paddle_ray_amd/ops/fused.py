@@ -1077,6 +1077,81 @@ def conv1x1_nhwc(x, w, bias=None, stride=(1, 1)):
 
 
 # =============================================================================
+# KxK convolution (channels-last, groups 1, dilation 1) as an implicit GEMM on the LDS-DMA MFMA
+# kernel (gemm_lds.hip ConvDmaA): the im2col rows are gathered from the zero-padded NHWC input
+# by the DMA, never materialised. Forward for any stride; the stride-1 input gradient is the
+# same kernel on the padded output gradient with the flipped, in/out-transposed filter; the
+# weight gradient (and strided input gradients) use MIOpen's convolution_backward.
+# Parity: the reference's conv2d (phi gpudnn conv kernels) for ResNet's 3x3 layers.
+# =============================================================================
+def conv_kxk_supported(x, w, stride, padding):
+    """Host-side shape check before any launch (the kernel assumes these)."""
+    if not (x.is_cuda and x.dim() == 4 and w.dim() == 4 and x.dtype in _HALF and w.dtype == x.dtype):
+        return False
+    cin, cout = x.shape[3], w.shape[0]
+    return (w.shape[1] == cin and cin % 64 == 0 and cout % 8 == 0 and stride >= 1 and padding >= 0
+            and x.shape[1] + 2 * padding >= w.shape[2] and x.shape[2] + 2 * padding >= w.shape[3])
+
+
+def _conv_lds(x, wk, bias, kh, kw, stride, pad, relu=False):
+    """y[N,Ho,Wo,Cout] = conv(x NHWC, wk [kh*kw*C, Cout]) via the implicit-GEMM kernel."""
+    n, h, wd, c = x.shape
+    cout = wk.shape[1]
+    xp = torch.nn.functional.pad(x, (0, 0, pad, pad, pad, pad)) if pad else x.contiguous()
+    hp, wp = h + 2 * pad, wd + 2 * pad
+    ho, wo = (hp - kh) // stride + 1, (wp - kw) // stride + 1
+    y = torch.empty((n, ho, wo, cout), device=x.device, dtype=x.dtype)
+    if bias is not None and (bias.dtype != x.dtype or not bias.is_contiguous()):
+        bias = bias.to(x.dtype).contiguous()
+    _native.lib().conv_lds(xp.data_ptr(), wk.data_ptr(), _ptr(bias), y.data_ptr(), n, hp, wp, c, ho, wo,
+                           cout, kh, kw, stride, int(relu), _dt(x), _stream())
+    return y
+
+
+class ConvKxKFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, bias, stride, pad):
+        cout, cin, kh, kw = w.shape
+        x = x.contiguous()
+        wk = w.permute(2, 3, 1, 0).reshape(kh * kw * cin, cout).contiguous()
+        y = _conv_lds(x, wk, bias, kh, kw, stride, pad)
+        ctx.save_for_backward(x, w)
+        ctx.meta = (stride, pad, bias is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        stride, pad, hb = ctx.meta
+        cout, cin, kh, kw = w.shape
+        dy = _like(dy.contiguous(), x.dtype)
+        ours_dx = (ctx.needs_input_grad[0] and stride == 1 and cout % 64 == 0 and cin % 8 == 0
+                   and kh - 1 - pad >= 0 and kw - 1 - pad >= 0 and kh == kw)
+        dx = dw = db = None
+        if ours_dx:
+            wf = w.flip(2, 3).permute(2, 3, 0, 1).reshape(kh * kw * cout, cin).contiguous()
+            dx = _conv_lds(dy, wf, None, kh, kw, 1, kh - 1 - pad)
+        need_lib_dx = ctx.needs_input_grad[0] and not ours_dx
+        if need_lib_dx or ctx.needs_input_grad[1]:
+            # NCHW-shaped views of the channels-last tensors: MIOpen runs its NHWC kernels
+            gx, gw, _ = torch.ops.aten.convolution_backward(
+                dy.permute(0, 3, 1, 2), x.permute(0, 3, 1, 2), w, None, [stride, stride], [pad, pad],
+                [1, 1], False, [0, 0], 1, [need_lib_dx, bool(ctx.needs_input_grad[1]), False])
+            if need_lib_dx:
+                dx = gx.permute(0, 2, 3, 1).contiguous()
+            if ctx.needs_input_grad[1]:
+                dw = gw
+        if hb and ctx.needs_input_grad[2]:
+            db = dy.reshape(-1, cout).sum(0, dtype=torch.float32).to(dy.dtype)
+        return dx, dw, db, None, None
+
+
+def conv_kxk_nhwc(x, w, bias=None, stride=1, padding=0):
+    """Channels-last KxK conv x[N,H,W,Cin] * w[Cout,Cin,KH,KW] -> [N,Ho,Wo,Cout]."""
+    return ConvKxKFn.apply(x, w, bias, int(stride), int(padding))
+
+
+# =============================================================================
 # Linear with fused weight-gradient accumulation
 # =============================================================================
 def _acc_grad_ok(g, w, dt):
@@ -1714,10 +1789,7 @@ def gemm_bias_act(x, w, b=None, act=None):
     MFMA kernel launch (gemm.hip); unsupported layouts fall back to matmul + epilogue."""
     a = _ACT[act] if not isinstance(act, int) else act
     x2 = x.reshape(-1, x.shape[-1])
-    if x.is_cuda and (x2.shape[0] < 128 or
-                      not gemm_supported(x2 if x2.is_contiguous() else x2.contiguous(), w)):
-        # skinny (decode-time) rows: hipBLASLt + the activation (3.0 vs 3.6 ms per 24-layer
-        # graph decode step at batch 8); the MFMA tile would idle
+    if x.is_cuda and not gemm_supported(x2 if x2.is_contiguous() else x2.contiguous(), w):
         z = torch.matmul(x, w)
         return _act_ref(z if b is None else z + b, a)
     return GemmBiasActFn.apply(x, w, b, a)

@@ -1,0 +1,47 @@
+"""Implicit-GEMM KxK convolution (ops/fused.py ConvKxKFn over gemm_lds.hip ConvDmaA) against
+a plain PyTorch fp32 conv2d of the same op."""
+import pytest
+import torch
+
+from paddle_ray_amd.ops import fused as K
+
+CASES = [
+    # n, h, w, cin, cout, k, stride, pad
+    (2, 14, 14, 64, 64, 3, 1, 1),
+    (2, 15, 13, 64, 128, 3, 2, 1),
+    (3, 9, 11, 128, 96, 3, 1, 1),
+    (1, 12, 12, 64, 64, 5, 1, 2),
+    (2, 10, 10, 128, 64, 3, 1, 0),
+    (4, 7, 7, 512, 512, 3, 1, 1),
+]
+
+
+def test_conv_kxk_supported_cpu():
+    x = torch.zeros(1, 8, 8, 64, dtype=torch.bfloat16)
+    w = torch.zeros(64, 64, 3, 3, dtype=torch.bfloat16)
+    assert not K.conv_kxk_supported(x, w, 1, 1)  # host tensors never reach the kernel
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", CASES)
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_conv_kxk_fwd_bwd(case, dtype):
+    n, h, w_, cin, cout, k, s, p = case
+    torch.manual_seed(0)
+    x = torch.randn(n, h, w_, cin, device='cuda', dtype=dtype)
+    w = (torch.randn(cout, cin, k, k, device='cuda') / (cin * k * k) ** 0.5).to(dtype)
+    b = torch.randn(cout, device='cuda', dtype=dtype)
+    assert K.conv_kxk_supported(x, w, s, p)
+    xr, wr, br = (t.float().requires_grad_() for t in (x, w, b))
+    xh, wh, bh = (t.clone().requires_grad_() for t in (x, w, b))
+    y = K.conv_kxk_nhwc(xh, wh, bh, s, p)
+    yr = torch.nn.functional.conv2d(xr.permute(0, 3, 1, 2), wr, br, s, p).permute(0, 2, 3, 1)
+    assert y.shape == yr.shape
+    torch.testing.assert_close(y.float(), yr, atol=3e-2, rtol=3e-2)
+    dy = torch.randn_like(yr)
+    yr.backward(dy)
+    y.backward(dy.to(dtype))
+    for got, ref in ((xh.grad, xr.grad), (wh.grad, wr.grad), (bh.grad, br.grad)):
+        err = (got.float() - ref).abs().max().item()
+        scale = ref.abs().max().item() + 1e-6
+        assert err <= 2e-2 * scale + 2e-2, (err, scale)
