@@ -533,6 +533,41 @@ class Tensor:
     def get_tensor(self):
         return self
 
+    # --- LoD (level-of-detail) sequence info, as on the reference's LoDTensor
+    # (paddle/fluid/framework/lod_tensor.h): offset lists per level, host-side metadata -----
+    def set_lod(self, lod):
+        lod = [[int(v) for v in level] for level in lod]
+        for level in lod:
+            if not level or level[0] != 0 or any(b < a for a, b in zip(level, level[1:])):
+                raise ValueError(f"invalid LoD level {level}: offsets must start at 0 and not decrease")
+        if lod and lod[-1][-1] != (self._t.shape[0] if self._t.dim() else 1):
+            raise ValueError(f"LoD {lod} does not cover the tensor's first dimension {tuple(self._t.shape)}")
+        self.__dict__['_lod'] = lod
+
+    def lod(self):
+        return [list(level) for level in self.__dict__.get('_lod', [])]
+
+    def set_recursive_sequence_lengths(self, lengths):
+        lod = []
+        for level in lengths:
+            off = [0]
+            for n in level:
+                off.append(off[-1] + int(n))
+            lod.append(off)
+        self.set_lod(lod)
+
+    def recursive_sequence_lengths(self):
+        return [[b - a for a, b in zip(level, level[1:])] for level in self.lod()]
+
+    def has_valid_recursive_sequence_lengths(self):
+        lod = self.__dict__.get('_lod')
+        if not lod:
+            return True
+        for upper, lower in zip(lod, lod[1:]):
+            if upper[-1] != len(lower) - 1:
+                return False
+        return lod[-1][-1] == self._t.shape[0]
+
     def set_value(self, value):
         v = value._t if isinstance(value, Tensor) else torch.as_tensor(np.asarray(value))
         with torch.no_grad():

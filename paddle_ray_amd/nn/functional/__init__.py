@@ -441,6 +441,9 @@ def _conv_padding(padding, n, t=None, ksize=None, stride=None, dilation=None):
 # no split-K for the huge-K wgrad), 'miopen' = MIOpen's implicit-GEMM kernels
 _CONV1X1 = os.environ.get('PRA_CONV1X1', 'mfma')
 _CONV1X1_GEMM = _CONV1X1 == 'blas' or os.environ.get('PRA_CONV1X1_GEMM', '0') == '1'
+# KxK channels-last convs (groups 1, Cin % 64 == 0): 'mfma' = implicit GEMM on the in-tree
+# LDS-DMA kernel (ops/fused.py ConvKxKFn), 'miopen' = MIOpen
+_CONVKXK = os.environ.get('PRA_CONVKXK', 'miopen')
 
 
 def _conv1x1_gemm(t, w, bias, st):
@@ -469,6 +472,13 @@ def _conv(fn, n, x, weight, bias, stride, padding, dilation, groups, data_format
                                      _ntuple(stride, 2)))
         return _w(_conv1x1_gemm(t, _t(weight), None if bias is None else _t(bias),
                                 _ntuple(stride, 2)))
+    if (_CONVKXK == 'mfma' and n == 2 and cl and t.is_cuda and groups == 1 and extra is None
+            and _ntuple(dilation, 2) == (1, 1)):
+        st, pd = _ntuple(stride, 2), _ntuple(pad_, 2) if not isinstance(pad_, str) else None
+        w = _t(weight)
+        if (pd is not None and st[0] == st[1] and pd[0] == pd[1] and w.shape[2] == w.shape[3] > 1
+                and K.conv_kxk_supported(t, w, st[0], pd[0])):
+            return _w(K.conv_kxk_nhwc(t, w, None if bias is None else _t(bias), st[0], pd[0]))
     if cl:
         t = t.movedim(-1, 1)
     if extra is not None:
@@ -1088,8 +1098,34 @@ def flash_attention(query, key, value, dropout=0.0, causal=False, return_softmax
     return out, None
 
 
-def sparse_attention(*a, **k):
-    raise NotImplementedError("sparse_attention is not available in the MI355X build yet")
+def sparse_attention(query, key, value, sparse_csr_offset, sparse_csr_columns,
+                     key_padding_mask=None, attn_mask=None, name=None):
+    """softmax(Q·Kᵀ/√d restricted to a CSR layout) · V (parity:
+    python/paddle/nn/functional/sparse_attention.py). The per-(batch, head) CSR pattern
+    [S+1 offsets, nnz columns] is scattered into a boolean layout once; key_padding_mask
+    [B, S] and attn_mask [S, S] (0 = masked) narrow it further. Rows with no admitted key
+    return zeros."""
+    q, k, v = _t(query), _t(key), _t(value)
+    b, h, s, d = q.shape
+    off = _t(sparse_csr_offset).long().reshape(b * h, s + 1)
+    cols = _t(sparse_csr_columns).long().reshape(b * h, -1)
+    nnz = cols.shape[1]
+    row = torch.searchsorted(off[:, 1:].contiguous(),
+                             torch.arange(nnz, device=q.device).expand(b * h, nnz).contiguous(),
+                             right=True)
+    valid = torch.arange(nnz, device=q.device)[None] < off[:, -1:]
+    layout = torch.zeros(b * h, s, s, dtype=torch.bool, device=q.device)
+    bh = torch.arange(b * h, device=q.device)[:, None].expand_as(row)
+    layout[bh[valid], row.clamp(max=s - 1)[valid], cols[valid]] = True
+    layout = layout.view(b, h, s, s)
+    if key_padding_mask is not None:
+        layout = layout & (_t(key_padding_mask) != 0).view(b, 1, 1, s)
+    if attn_mask is not None:
+        layout = layout & (_t(attn_mask) != 0).view(1, 1, s, s)
+    sc = torch.matmul(q.float(), k.float().transpose(-1, -2)) / math.sqrt(d)
+    sc = sc.masked_fill(~layout, float('-inf'))
+    p = torch.softmax(sc, -1).nan_to_num(0.0)
+    return _w(torch.matmul(p, v.float()).to(q.dtype))
 
 
 def class_center_sample(label, num_classes, num_samples, group=None):

@@ -93,23 +93,35 @@ __device__ __forceinline__ float act(float x) {
   return x;
 }
 
-constexpr int BM = 256, BN = 256, BKT = 64;
-constexpr int IMG = BM * BKT * 2;       // 32 KB per operand image
-constexpr int SLOT = 2 * IMG;           // A image + B image
-constexpr int LDS_BYTES = 2 * SLOT + 128 * 4 * 4;  // double-buffered 128 KB (+2 KB: epilogue image pitch)
+constexpr int BM = 256, BN = 256, BKT = 64;  // the GEMM tile (conv configs below narrow BN)
 
-// Wave layouts of the 256x256 tile: WR x WC waves, each (256/WR) x (256/WC) outputs.
-//   W8: 2 x 4 waves (128x64 each, 2 waves/SIMD, 32 accumulators)
-//   W4: 2 x 2 waves (128x128 each, 1 wave/SIMD, 64 accumulators in AGPRs): half the LDS
-//       fragment traffic per MFMA and half the waves meeting at each barrier.
-template <int WR_, int WC_>
+// Wave layouts of a BM_ x BN_ tile: WR x WC waves, each (BM_/WR) x (BN_/WC) outputs.
+//   W8: 256x256, 2 x 4 waves (128x64 each, 2 waves/SIMD, 32 accumulators)
+//   W4: 256x256, 2 x 2 waves (128x128 each, 1 wave/SIMD, 64 accumulators in AGPRs)
+//   C128 / C64: narrow-N tiles for convolutions with 128 / 64 output channels (256x128 and
+//       512x64, 64x64 per wave): a 256-wide tile would leave half / three quarters of its
+//       MFMAs on padding columns. Their B operand must be K-contiguous (BK = true).
+// Each K-step stages A [BM][64] and B [BN][64] (or [64][BN]) images, double-buffered.
+template <int WR_, int WC_, int BM_ = 256, int BN_ = 256>
 struct WCfg {
-  static constexpr int WR = WR_, WC = WC_, NT = 64 * WR_ * WC_;
-  static constexpr int TI = BM / WR_ / 16, TJ = BN / WC_ / 16;  // 16x16 MFMA tiles per wave
-  static constexpr int NDMA = IMG / (NT * 16);                   // glds per thread per operand per K-step
+  static constexpr int WR = WR_, WC = WC_, NT = 64 * WR_ * WC_, BM = BM_, BN = BN_;
+  static constexpr int TI = BM_ / WR_ / 16, TJ = BN_ / WC_ / 16;  // 16x16 MFMA tiles per wave
+  static constexpr int IMGA = BM_ * BKT * 2, IMGB = BN_ * BKT * 2, SLOT = IMGA + IMGB;
+  static constexpr int NDA = IMGA / (NT * 16), NDB = IMGB / (NT * 16);  // glds per thread per K-step
+  static constexpr int EPI = 128 * (BN_ + 4) * 4;  // epilogue image: 128 rows of fp32, padded pitch
+  static constexpr int LDS = 2 * SLOT > EPI ? 2 * SLOT : EPI;
 };
 using W8 = WCfg<2, 4>;
 using W4 = WCfg<2, 2>;
+using C128 = WCfg<4, 2, 256, 128>;
+using C64 = WCfg<8, 1, 512, 64>;
+
+// s_waitcnt vmcnt(N) (expcnt / lgkmcnt left unconstrained)
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | 0x70 | 0xF00);
+}
 
 typedef short v4i16 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
@@ -234,9 +246,12 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_lds_kernel(const uint16_t* __r
                                                           uint16_t* __restrict__ Z, float* __restrict__ colsum,
                                                           int M, int N, int K, int lda, int ldb, int ldc, int ldz,
                                                           int splits, float* __restrict__ ws, ConvGeom cg = {}) {
-  constexpr int NT = CF::NT, TI = CF::TI, TJ = CF::TJ, NDMA = CF::NDMA, WC = CF::WC;
+  constexpr int NT = CF::NT, TI = CF::TI, TJ = CF::TJ, NDA = CF::NDA, NDB = CF::NDB, WC = CF::WC;
+  constexpr int BM = CF::BM, BN = CF::BN, IMGA = CF::IMGA, SLOT = CF::SLOT;
   constexpr int RW = TI * 16, CW = TJ * 16;  // rows / columns per wave
-  __shared__ __attribute__((aligned(1024))) char lds[LDS_BYTES];
+  static_assert(BK || BN == 256, "the M/N-contiguous B image is 256 columns wide");
+  static_assert(TJ <= TI && 128 % RW == 0 && NDA >= 1 && NDB >= 1, "wave layout");
+  __shared__ __attribute__((aligned(1024))) char lds[CF::LDS];
   typedef typename V8<T>::type v8;
   const uint32_t lds_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)lds;
 
@@ -258,8 +273,8 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_lds_kernel(const uint16_t* __r
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wr = wave / WC, wc = wave % WC;
 
-  typename std::conditional<CONV, ConvDmaA<NT, NDMA>, Dma<AK, NT, NDMA>>::type da;
-  Dma<BK, NT, NDMA> db;
+  typename std::conditional<CONV, ConvDmaA<NT, NDA>, Dma<AK, NT, NDA>>::type da;
+  Dma<BK, NT, NDB> db;
   if constexpr (CONV) da.init(A, cg, m0, M, tid);
   else if (AK) da.init(A, lda, m0, M - 1, tid);
   else da.init(A, lda, m0, M - 8, tid);
@@ -281,7 +296,7 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_lds_kernel(const uint16_t* __r
   v8 fa0[TI], fb0[TJ], fa1[TI], fb1[TJ];
   auto read_frags = [&](v8 (&fa)[TI], v8 (&fb)[TJ], int kt, int s) {
     const char* ai = lds + (kt & 1) * SLOT;
-    const char* bi = ai + IMG;
+    const char* bi = ai + IMGA;
 #pragma unroll
     for (int j = 0; j < TJ; ++j) fb[j] = frag<T, BK>(bi, wc * CW + j * 16, s, lane);
 #pragma unroll
@@ -294,15 +309,15 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_lds_kernel(const uint16_t* __r
                   int dkt) {
     const uint32_t so = lds_base + (dkt & 1) * SLOT;
     const char* ai = lds + (rkt & 1) * SLOT;
-    const char* bi = ai + IMG;
-    constexpr int DPS = (2 * NDMA + TI - 1) / TI;  // DMA instructions per segment
+    const char* bi = ai + IMGA;
+    constexpr int DPS = (NDA + NDB + TI - 1) / TI;  // DMA instructions per segment
 #pragma unroll
     for (int i = 0; i < TI; ++i) {
       if (dma) {
 #pragma unroll
-        for (int d = i * DPS; d < (i + 1) * DPS && d < 2 * NDMA; ++d) {
-          if (d < NDMA) da.issue1(so, wave, dkt, d);
-          else db.issue1(so + IMG, wave, dkt, d - NDMA);
+        for (int d = i * DPS; d < (i + 1) * DPS && d < NDA + NDB; ++d) {
+          if (d < NDA) da.issue1(so, wave, dkt, d);
+          else db.issue1(so + IMGA, wave, dkt, d - NDA);
         }
       }
       if (rd) {
@@ -323,14 +338,13 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_lds_kernel(const uint16_t* __r
   for (int t = 0; t < 2; ++t) {
     if (t < nk) {
 #pragma unroll
-      for (int n = 0; n < NDMA; ++n) da.issue1(lds_base + t * SLOT, wave, t, n);
+      for (int n = 0; n < NDA; ++n) da.issue1(lds_base + t * SLOT, wave, t, n);
 #pragma unroll
-      for (int n = 0; n < NDMA; ++n) db.issue1(lds_base + t * SLOT + IMG, wave, t, n);
+      for (int n = 0; n < NDB; ++n) db.issue1(lds_base + t * SLOT + IMGA, wave, t, n);
     }
   }
   if (nk >= 2) {
-    if (NDMA == 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    wait_vmcnt<NDA + NDB>();  // step 0 landed, step 1 still in flight
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
@@ -379,12 +393,12 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_lds_kernel(const uint16_t* __r
   // then all 8 waves stream it out row-major: 8 columns per lane, whole 512-B row segments per 32
   // lanes, so the bias/activation/pre-activation/beta/dGELU traffic is 16-B coalesced loads and
   // stores instead of 8-B scatters across 16 rows.
-  // acc[i][j][r] = C[m0 + wr*128 + i*16 + (lane&15)][n0 + wc*64 + j*16 + 4*(lane>>4) + r]
+  // acc[i][j][r] = C[m0 + wr*RW + i*16 + (lane&15)][n0 + wc*CW + j*16 + 4*(lane>>4) + r]
   float* img = reinterpret_cast<float*>(lds);
   constexpr int PITCH = BN + 4;  // floats
-  // this thread's output units: row tid>>5 (+RSTEP per q), 8 columns at (tid&31)*8 (fixed per thread)
-  constexpr int RSTEP = NT / 32, NQ = 128 / RSTEP;
-  const int ucol = (tid & 31) * 8, urow = tid >> 5;
+  // this thread's output units: row tid/TPR (+RSTEP per q), 8 columns at (tid%TPR)*8 (fixed per thread)
+  constexpr int TPR = BN / 8, RSTEP = NT / TPR, NQ = 128 / RSTEP, QB = NQ < 4 ? NQ : 4;
+  const int ucol = (tid % TPR) * 8, urow = tid / TPR;
   const int n = n0 + ucol;
   const bool ncol_ok = n < N;  // N % 8 == 0: a unit is all-in or all-out
   float bv[8];
@@ -400,15 +414,15 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_lds_kernel(const uint16_t* __r
 #pragma unroll
   for (int e = 0; e < 8; ++e) cs[e] = 0.f;
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
+  for (int h = 0; h < BM / 128; ++h) {
     __builtin_amdgcn_s_waitcnt(0xC07F);
-    __syncthreads();  // (h=0) every wave is done reading K-loop tiles; (h=1) half 0 streamed out
-    if (wr == h) {
+    __syncthreads();  // (h=0) every wave is done reading K-loop tiles; (h>0) chunk h-1 streamed out
+    if ((wr * RW) / 128 == h) {
 #pragma unroll
       for (int i = 0; i < TI; ++i)
 #pragma unroll
         for (int j = 0; j < TJ; ++j) {
-          const int r = i * 16 + (lane & 15), c = wc * CW + j * 16 + 4 * (lane >> 4);
+          const int r = wr * RW - h * 128 + i * 16 + (lane & 15), c = wc * CW + j * 16 + 4 * (lane >> 4);
           *reinterpret_cast<f32x4*>(img + r * PITCH + c) = acc[i][j];
         }
     }
@@ -416,13 +430,13 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_lds_kernel(const uint16_t* __r
     // NQ units per thread in batches of 4: every load of a batch (LDS image, Z / C) is issued
     // before any of its math so the global-load latency is paid once per batch, not per unit
 #pragma unroll
-    for (int bq = 0; bq < NQ; bq += 4) {
-      f32x4 lo[4], hi[4];
-      uint4 gz[4];
-      bool ok[4];
-      int64_t moff[4];
+    for (int bq = 0; bq < NQ; bq += QB) {
+      f32x4 lo[QB], hi[QB];
+      uint4 gz[QB];
+      bool ok[QB];
+      int64_t moff[QB];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < QB; ++u) {
         const int rr = urow + RSTEP * (bq + u), m = m0 + h * 128 + rr;
         ok[u] = m < M && ncol_ok;
         moff[u] = (int64_t)(ok[u] ? m : 0);
@@ -435,7 +449,7 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_lds_kernel(const uint16_t* __r
         }
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < QB; ++u) {
         if (!ok[u]) continue;
         const int64_t m = moff[u];
         float v[8] = {lo[u][0], lo[u][1], lo[u][2], lo[u][3], hi[u][0], hi[u][1], hi[u][2], hi[u][3]};
@@ -477,7 +491,7 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_lds_kernel(const uint16_t* __r
       }
     }
   }
-  if (colsum) {
+  if constexpr (TPR == 32 && NT == 512) if (colsum) {
     // threads sharing (tid & 31) own the same 8 columns: lanes l, l^32 then the 8 waves via LDS
 #pragma unroll
     for (int e = 0; e < 8; ++e) cs[e] += __shfl_xor(cs[e], 32, 64);
@@ -603,13 +617,22 @@ int launch_t(int layout, const void* A, const void* B, const void* bias, void* C
   }
 }
 
+template <typename T, typename CF, int E>
+void launch_conv_cfg(const void* xpad, const void* W, const void* bias, void* Y, int M, int N, int K,
+                     const ConvGeom& cg, hipStream_t s) {
+  const int tiles = ((M + CF::BM - 1) / CF::BM) * ((N + CF::BN - 1) / CF::BN);
+  gemm_lds_kernel<T, CF, true, true, E, false, false, true><<<tiles, CF::NT, 0, s>>>(
+      static_cast<const uint16_t*>(xpad), static_cast<const uint16_t*>(W), static_cast<const uint16_t*>(bias),
+      static_cast<uint16_t*>(Y), nullptr, nullptr, M, N, K, 0, K, N, N, 1, nullptr, cg);
+}
+
+// tile by output channels: 512x64 for N <= 64, 256x128 for N <= 128, else 256x256
 template <typename T, int E>
 int launch_conv(const void* xpad, const void* W, const void* bias, void* Y, int M, int N, int K, const ConvGeom& cg,
                 hipStream_t s) {
-  const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
-  gemm_lds_kernel<T, W8, true, false, E, false, false, true><<<tiles, W8::NT, 0, s>>>(
-      static_cast<const uint16_t*>(xpad), static_cast<const uint16_t*>(W), static_cast<const uint16_t*>(bias),
-      static_cast<uint16_t*>(Y), nullptr, nullptr, M, N, K, 0, N, N, N, 1, nullptr, cg);
+  if (N <= 64) launch_conv_cfg<T, C64, E>(xpad, W, bias, Y, M, N, K, cg, s);
+  else if (N <= 128) launch_conv_cfg<T, C128, E>(xpad, W, bias, Y, M, N, K, cg, s);
+  else launch_conv_cfg<T, W8, E>(xpad, W, bias, Y, M, N, K, cg, s);
   return 0;
 }
 
@@ -617,8 +640,8 @@ int launch_conv(const void* xpad, const void* W, const void* bias, void* Y, int 
 }  // namespace pra
 
 // Implicit-GEMM convolution, channels-last, on the LDS-DMA MFMA kernel:
-//   Y[N*Ho*Wo][Cout] = im2col(x_pad) · Wk[KH*KW*C][Cout] (+ bias, optional ReLU)
-// x_pad is the zero-padded input [N][Hp][Wp][C]; Wk the HWIO filter as a [K][Cout] matrix.
+//   Y[N*Ho*Wo][Cout] = im2col(x_pad) · Wkᵀ (+ bias, optional ReLU)
+// x_pad is the zero-padded input [N][Hp][Wp][C]; Wk the OHWI filter as a [Cout][KH*KW*C] matrix.
 // Requires C % 64 == 0, Cout % 8 == 0, x_pad smaller than 4 GB (32-bit DMA offsets).
 extern "C" int pra_conv_lds(const void* xpad, const void* W, const void* bias, void* Y, int Nimg, int Hp, int Wp,
                             int C, int Ho, int Wo, int Cout, int KH, int KW, int S, int relu, int dtype,

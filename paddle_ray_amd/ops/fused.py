@@ -1094,9 +1094,9 @@ def conv_kxk_supported(x, w, stride, padding):
 
 
 def _conv_lds(x, wk, bias, kh, kw, stride, pad, relu=False):
-    """y[N,Ho,Wo,Cout] = conv(x NHWC, wk [kh*kw*C, Cout]) via the implicit-GEMM kernel."""
+    """y[N,Ho,Wo,Cout] = conv(x NHWC, wk [Cout, kh*kw*C] (OHWI)) via the implicit-GEMM kernel."""
     n, h, wd, c = x.shape
-    cout = wk.shape[1]
+    cout = wk.shape[0]
     xp = torch.nn.functional.pad(x, (0, 0, pad, pad, pad, pad)) if pad else x.contiguous()
     hp, wp = h + 2 * pad, wd + 2 * pad
     ho, wo = (hp - kh) // stride + 1, (wp - kw) // stride + 1
@@ -1113,7 +1113,7 @@ class ConvKxKFn(torch.autograd.Function):
     def forward(ctx, x, w, bias, stride, pad):
         cout, cin, kh, kw = w.shape
         x = x.contiguous()
-        wk = w.permute(2, 3, 1, 0).reshape(kh * kw * cin, cout).contiguous()
+        wk = w.permute(0, 2, 3, 1).reshape(cout, kh * kw * cin).contiguous()  # a view for channels-last w
         y = _conv_lds(x, wk, bias, kh, kw, stride, pad)
         ctx.save_for_backward(x, w)
         ctx.meta = (stride, pad, bias is not None)
@@ -1129,7 +1129,7 @@ class ConvKxKFn(torch.autograd.Function):
                    and kh - 1 - pad >= 0 and kw - 1 - pad >= 0 and kh == kw)
         dx = dw = db = None
         if ours_dx:
-            wf = w.flip(2, 3).permute(2, 3, 0, 1).reshape(kh * kw * cout, cin).contiguous()
+            wf = w.flip(2, 3).permute(1, 2, 3, 0).reshape(cin, kh * kw * cout).contiguous()
             dx = _conv_lds(dy, wf, None, kh, kw, 1, kh - 1 - pad)
         need_lib_dx = ctx.needs_input_grad[0] and not ours_dx
         if need_lib_dx or ctx.needs_input_grad[1]:

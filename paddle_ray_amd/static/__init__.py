@@ -36,4 +36,5 @@ from .graph import (Program, Block, Variable, Executor, global_scope, scope_guar
                     IpuCompiledProgram, exponential_decay, ctr_metric_bundle, _static_minimize,
                     Scope)
 from . import nn  # noqa: E402
+from .sequence_lod import create_lod_tensor  # noqa: E402,F401
 from . import amp  # noqa: E402

@@ -1226,8 +1226,71 @@ def accuracy(input, label, k=1, correct=None, total=None):
     return static_op('accuracy', acc)(input, label, k)
 
 
-def auc(input, label, curve='ROC', num_thresholds=4095, topk=1, slide_steps=1):
-    raise NotImplementedError("static auc: use paddle.metric.Auc on fetched outputs")
+def _stateful_metric(name, fn, args, specs):
+    """Run ``fn`` now (eager) or record it as one op whose persistable state lives in ``fn``'s
+    closure and is updated every time the program executes (``out_specs`` given, so shape
+    inference never runs the update on probe data)."""
+    if _STATIC[0] and _has_var(args):
+        flat = [(list(s), d) for s, d in specs]
+        tmpl = ('tuple', ['T'] * len(flat))
+        return record_op(name, fn, list(args), {}, out_specs=(tmpl, flat))
+    return fn(*args)
+
+
+def auc(input, label, curve='ROC', num_thresholds=4095, topk=1, slide_steps=1,
+        ins_tag_weight=None):
+    """Streaming AUC over bucketed positive-class scores (parity: python/paddle/static/nn/
+    metric.py auc). Returns (auc, batch_auc, [batch_stat_pos, batch_stat_neg, stat_pos,
+    stat_neg]); the global stats accumulate over every run, the batch stats over the last
+    ``slide_steps`` runs (0 = all)."""
+    nb = num_thresholds + 1
+    st = {'pos': torch.zeros(nb, dtype=torch.float64), 'neg': torch.zeros(nb, dtype=torch.float64),
+          'win': []}
+
+    def _area(pos, neg):
+        # thresholds from high to low: trapezoids of (FP, TP) (ROC) or (recall, precision) (PR)
+        tp = torch.cumsum(pos.flip(0), 0)
+        fp = torch.cumsum(neg.flip(0), 0)
+        P, N = tp[-1], fp[-1]
+        if curve.upper() == 'PR':
+            prec = tp / (tp + fp).clamp(min=1)
+            rec = tp / P.clamp(min=1)
+            r0 = torch.cat([rec.new_zeros(1), rec[:-1]])
+            p0 = torch.cat([prec.new_ones(1), prec[:-1]])
+            return float(((rec - r0) * (prec + p0) / 2).sum())
+        if P == 0 or N == 0:
+            return 0.0
+        tp0 = torch.cat([tp.new_zeros(1), tp[:-1]])
+        fp0 = torch.cat([fp.new_zeros(1), fp[:-1]])
+        return float(((fp - fp0) * (tp + tp0) / 2).sum() / (P * N))
+
+    def run(pred, lab, *tw):
+        p = _u(pred).detach().double().cpu()
+        score = p[:, -1] if p.dim() == 2 and p.shape[1] > 1 else p.reshape(-1)
+        y = _u(lab).reshape(-1).cpu() != 0
+        if tw and float(_u(tw[0]).reshape(-1)[0]) == 0:
+            y = y[:0]
+            score = score[:0]
+        bucket = (score * num_thresholds).long().clamp(0, num_thresholds)
+        bp = torch.bincount(bucket[y], minlength=nb).double()
+        bn = torch.bincount(bucket[~y], minlength=nb).double()
+        st['pos'] += bp
+        st['neg'] += bn
+        st['win'].append((bp, bn))
+        if slide_steps > 0:
+            st['win'] = st['win'][-slide_steps:]
+        wp = sum(w[0] for w in st['win'])
+        wn = sum(w[1] for w in st['win'])
+        dev = _u(pred).device
+        f = lambda v: Tensor(torch.tensor([v], dtype=torch.float64, device=dev))  # noqa: E731
+        g = lambda v: Tensor(v.to(dev).reshape(1, -1).to(torch.int64))  # noqa: E731
+        return (f(_area(st['pos'], st['neg'])), f(_area(wp, wn)), g(wp), g(wn), g(st['pos']),
+                g(st['neg']))
+
+    args = [input, label] + ([ins_tag_weight] if ins_tag_weight is not None else [])
+    specs = [([1], torch.float64)] * 2 + [([1, nb], torch.int64)] * 4
+    out = _stateful_metric('auc', run, args, specs)
+    return out[0], out[1], list(out[2:])
 
 
 class WeightNormParamAttr:
@@ -1282,11 +1345,28 @@ def exponential_decay(learning_rate, decay_steps, decay_rate, staircase=False):
     return ExponentialDecay(learning_rate, decay_rate ** (1.0 / decay_steps))
 
 
-def ctc_metric_bundle(*a, **k):
-    raise NotImplementedError
+def ctr_metric_bundle(input, label, ins_tag_weight=None):
+    """Running CTR sums (parity: python/paddle/fluid/contrib/layers/metric_op.py
+    ctr_metric_bundle): squared error, absolute error, predicted-ctr sum, q (sum of
+    sigmoid(input)), positives and instance count, accumulated over every run; a batch whose
+    ins_tag_weight is 0 (fake data) adds nothing to q and the instance count."""
+    st = torch.zeros(6, dtype=torch.float32)
+
+    def run(pred, lab, *tw):
+        p = _u(pred).detach().float().cpu().reshape(-1)
+        y = _u(lab).detach().float().cpu().reshape(-1)
+        w = float(_u(tw[0]).reshape(-1)[0]) if tw else 1.0
+        d = p - y
+        st.add_(torch.stack([(d * d).sum(), d.abs().sum(), p.sum(), torch.sigmoid(p).sum() * w,
+                                 y.sum(), torch.tensor(float(p.numel())) * w]))
+        dev = _u(pred).device
+        return tuple(Tensor(st[i:i + 1].clone().to(dev)) for i in range(6))
+
+    args = [input, label] + ([ins_tag_weight] if ins_tag_weight is not None else [])
+    return _stateful_metric('ctr_metric_bundle', run, args, [([1], torch.float32)] * 6)
 
 
-ctr_metric_bundle = ctc_metric_bundle
+ctc_metric_bundle = ctr_metric_bundle
 
 
 # =============================================================================

@@ -300,10 +300,7 @@ def py_func(func, x, out, backward_func=None, skip_vars_in_backward_input=None):
     return pf(func, x, out, backward_func, skip_vars_in_backward_input)
 
 
-def _seq(*a, **k):
-    raise NotImplementedError("LoD sequence ops are not part of the MI355X build")
-
-
-sequence_conv = sequence_softmax = sequence_pool = sequence_concat = sequence_first_step = _seq
-sequence_last_step = sequence_slice = sequence_expand = sequence_expand_as = sequence_pad = _seq
-sequence_unpad = sequence_reshape = sequence_scatter = sequence_enumerate = sequence_reverse = _seq
+from .sequence_lod import (  # noqa: E402,F401
+    sequence_conv, sequence_softmax, sequence_pool, sequence_concat, sequence_first_step,
+    sequence_last_step, sequence_slice, sequence_expand, sequence_expand_as, sequence_pad,
+    sequence_unpad, sequence_reshape, sequence_scatter, sequence_enumerate, sequence_reverse)

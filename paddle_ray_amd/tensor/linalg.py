@@ -203,5 +203,17 @@ def matrix_exp(x, name=None):
     return Tensor(torch.linalg.matrix_exp(_t(x)))
 
 
-def histogramdd(*a, **k):
-    raise NotImplementedError
+def histogramdd(x, bins=10, ranges=None, density=False, weights=None, name=None):
+    """D-dimensional histogram of the points x[..., D] -> (hist, [edges per dim])."""
+    t = _t(x)
+    pts = t.reshape(-1, t.shape[-1]).double().cpu()
+    w = None if weights is None else _t(weights).reshape(-1).double().cpu()
+    if isinstance(bins, (list, tuple)) and bins and not isinstance(bins[0], int):
+        b = [_t(e).double().cpu() if isinstance(e, Tensor) else torch.as_tensor(e, dtype=torch.float64)
+             for e in bins]
+        hist, edges = torch.histogramdd(pts, bins=b, weight=w, density=density)
+    else:
+        rg = None if ranges is None else [float(r) for r in ranges]
+        hist, edges = torch.histogramdd(pts, bins=bins, range=rg, weight=w, density=density)
+    return Tensor(hist.to(t.dtype if t.is_floating_point() else torch.float32).to(t.device)), \
+        [Tensor(e.to(t.dtype if t.is_floating_point() else torch.float32).to(t.device)) for e in edges]

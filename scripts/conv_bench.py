@@ -26,7 +26,7 @@ tot = {'ours_f': 0, 'mi_f': 0, 'ours_d': 0, 'mi_d': 0}
 for hw, cin, cout, s in shapes:
     x = torch.randn(B, hw, hw, cin, device='cuda', dtype=torch.bfloat16)
     w = (torch.randn(cout, cin, 3, 3, device='cuda') * 0.05).to(torch.bfloat16)
-    wk = w.permute(2, 3, 1, 0).reshape(9 * cin, cout).contiguous()
+    wk = w.permute(0, 2, 3, 1).reshape(cout, 9 * cin).contiguous()
     xc = x.permute(0, 3, 1, 2)
     wc = w.contiguous(memory_format=torch.channels_last)
     y = K._conv_lds(x, wk, None, 3, 3, s, 1)
@@ -40,7 +40,7 @@ for hw, cin, cout, s in shapes:
     tot['mi_f'] += f_m
     if s == 1:
         dy = torch.randn_like(y)
-        wf = w.flip(2, 3).permute(2, 3, 0, 1).reshape(9 * cout, cin).contiguous()
+        wf = w.flip(2, 3).permute(1, 2, 3, 0).reshape(cin, 9 * cout).contiguous()
         dyc = dy.permute(0, 3, 1, 2)
         d_o = t(lambda: K._conv_lds(dy, wf, None, 3, 3, 1, 1))
         d_m = t(lambda: torch.ops.aten.convolution_backward(dyc, xc, wc, None, [1, 1], [1, 1], [1, 1], False,
