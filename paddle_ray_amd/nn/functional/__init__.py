@@ -442,8 +442,9 @@ def _conv_padding(padding, n, t=None, ksize=None, stride=None, dilation=None):
 _CONV1X1 = os.environ.get('PRA_CONV1X1', 'mfma')
 _CONV1X1_GEMM = _CONV1X1 == 'blas' or os.environ.get('PRA_CONV1X1_GEMM', '0') == '1'
 # KxK channels-last convs (groups 1, Cin % 64 == 0): 'mfma' = implicit GEMM on the in-tree
-# LDS-DMA kernel (ops/fused.py ConvKxKFn), 'miopen' = MIOpen
-_CONVKXK = os.environ.get('PRA_CONVKXK', 'miopen')
+# LDS-DMA kernel for forward and stride-1 dgrad (ops/fused.py ConvKxKFn; default: ResNet50
+# 7983 vs 7793 img/s, profiles/r2_conv), 'miopen' = MIOpen for every direction
+_CONVKXK = os.environ.get('PRA_CONVKXK', 'mfma')
 
 
 def _conv1x1_gemm(t, w, bias, st):

@@ -64,7 +64,8 @@ int pra_gemm_lds(int, const void*, const void*, const void*, void*, void*, float
                  int, int, int, int, float*, hipStream_t);
 int pra_gemm_lds_splits(int, int, int);
 int pra_conv_lds(const void*, const void*, const void*, void*, int, int, int, int, int, int, int, int, int, int, int,
-                 int, hipStream_t);
+                 int, float*, hipStream_t);
+int pra_conv_lds_splits(int, int, int);
 int pra_colsum_partials(const float*, void*, int, int, int, hipStream_t);
 void pra_bn_fwd_train(const void*, const void*, const void*, const void*, float*, float*, void*, uint8_t*, float*,
                       float*, float*, float*, int, int, int, float, float, int, int, int, hipStream_t);
@@ -94,12 +95,14 @@ PYBIND11_MODULE(_pra_hip, m) {
       throw std::invalid_argument("gemm_bias_act: unsupported shape/stride/dtype");
     check_launch("gemm_bias_act");
   });
-  m.def("conv_lds", [](P x, P w, P bias, P y, int n, int hp, int wp, int c, int ho, int wo, int cout, int kh,
-                       int kw, int st, int relu, int dt, P s) {
-    if (pra_conv_lds(CV(x), CV(w), CV(bias), V(y), n, hp, wp, c, ho, wo, cout, kh, kw, st, relu, dt, S(s)) != 0)
+  m.def("conv_lds", [](P x, P w, P bias, P y, int n, int h, int wd, int c, int cout, int kh, int kw, int st,
+                       int pad, int relu, int dt, int splits, P ws, P s) {
+    if (pra_conv_lds(CV(x), CV(w), CV(bias), V(y), n, h, wd, c, cout, kh, kw, st, pad, relu, dt, splits,
+                     reinterpret_cast<float*>(ws), S(s)) != 0)
       throw std::invalid_argument("conv_lds: unsupported shape/dtype");
     check_launch("conv_lds");
   });
+  m.def("conv_lds_splits", [](int m, int n, int k) { return pra_conv_lds_splits(m, n, k); });
   m.def("gemm_lds_splits", [](int M, int N, int K) { return pra_gemm_lds_splits(M, N, K); });
   m.def("gemm_lds", [](int layout, P a, P b, P bias, P c, P z, P colsum, int M, int N, int K, int lda, int ldb,
                        int ldc, int ldz, int dt, int epi, int beta, int splits, P ws, P s) {

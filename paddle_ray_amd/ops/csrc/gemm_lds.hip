@@ -177,19 +177,23 @@ struct Dma {
   }
 };
 
-// Implicit-GEMM convolution operand A = im2col(x) for a channels-last input that is already
-// zero-padded spatially (x_pad [N][Hp][Wp][C]): row m = output pixel (n, ho, wo), column
-// k = (kh, kw, c). With C % 64 == 0 a K-step (64 k) lies inside one filter tap, so every staged
-// row segment is 128 contiguous bytes of one input pixel: the LDS-DMA gathers rows straight
-// from x_pad (per-lane source addresses), nothing is materialised.
+// Implicit-GEMM convolution operand A = im2col(x) for a channels-last input x [N][H][W][C]:
+// row m = output pixel (n, ho, wo), column k = (kh, kw, c). With C % 64 == 0 a K-step (64 k)
+// lies inside one filter tap, so every staged row segment is 128 contiguous bytes of one input
+// pixel: the LDS-DMA gathers rows straight from x (per-lane source offsets), nothing is
+// materialised. The zero padding is the buffer descriptor's range check: a tap that falls
+// outside the image gets an offset past num_records and the DMA writes zeros to LDS.
 struct ConvGeom {
-  int Ho, Wo, Hp, Wp, C, KW, S;
+  int Ho, Wo, H, W, C, KW, S, P;
 };
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 template <int NT, int NDMA>
 struct ConvDmaA {
-  uint32_t pix[NDMA];  // element offset of x_pad[n][ho*S][wo*S][8c] for the staged row / chunk
-  uint64_t base;
+  int pix[NDMA];       // element offset of x[n][ho*S-P][wo*S-P][8c] (may be negative) per staged chunk
+  uint32_t hw[NDMA];   // (ho*S-P) << 16 | (wo*S-P) & 0xffff
+  u32x4 rs;            // buffer descriptor of x (wave-uniform, SGPRs)
   int kt0;
   ConvGeom g;
   __device__ __forceinline__ void init(const uint16_t* x, const ConvGeom& cg, int m0, int M, int tid) {
@@ -200,20 +204,27 @@ struct ConvDmaA {
       const int row = P >> 3, c = (P & 7) ^ kc_swz(row);
       const int m = min(m0 + row, M - 1);
       const int wo = m % g.Wo, t = m / g.Wo, ho = t % g.Ho, img = t / g.Ho;
-      pix[n] = (uint32_t)(((img * g.Hp + ho * g.S) * g.Wp + wo * g.S) * g.C + 8 * c);
+      const int hi = ho * g.S - g.P, wi = wo * g.S - g.P;
+      pix[n] = ((img * g.H + hi) * g.W + wi) * g.C + 8 * c;
+      hw[n] = ((uint32_t)hi << 16) | ((uint32_t)wi & 0xffffu);
     }
-    base = (uint64_t)x;
+    const uint64_t b = (uint64_t)x;
+    rs[0] = __builtin_amdgcn_readfirstlane((uint32_t)b);
+    rs[1] = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32)) & 0xffffu;  // stride 0
+    rs[2] = __builtin_amdgcn_readfirstlane((uint32_t)((int64_t)M / (g.Ho * g.Wo) * g.H * g.W * g.C * 2));
+    rs[3] = 0x00020000u;
     kt0 = 0;
   }
   __device__ __forceinline__ void advance(int ksteps) { kt0 += ksteps; }
   __device__ __forceinline__ void issue1(uint32_t lds_img, int wave, int kt, int n) {
-    const int k0 = (kt + kt0) * BKT;                 // wave-uniform: scalar math
+    const int k0 = (kt + kt0) * BKT;  // wave-uniform: scalar math
     const int tap = k0 / g.C, cin0 = k0 - tap * g.C, kh = tap / g.KW, kw = tap - kh * g.KW;
-    const uint32_t voff = (pix[n] + (uint32_t)((kh * g.Wp + kw) * g.C + cin0)) * 2u;
-    const uint64_t gs = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(base >> 32)) << 32) |
-                        (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)base);
+    const int hi = ((int)hw[n] >> 16) + kh, wi = (int)(int16_t)(hw[n] & 0xffffu) + kw;
+    const bool ok = (unsigned)hi < (unsigned)g.H && (unsigned)wi < (unsigned)g.W;
+    const uint32_t voff = ok ? (uint32_t)(pix[n] + (kh * g.W + kw) * g.C + cin0) * 2u : 0x80000000u;
     const uint32_t dst = __builtin_amdgcn_readfirstlane(lds_img + (n * NT + wave * 64) * 16);
-    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(gs), "s"(dst)
+    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(rs),
+                 "s"(dst)
                  : "memory");
   }
 };
@@ -619,20 +630,31 @@ int launch_t(int layout, const void* A, const void* B, const void* bias, void* C
 
 template <typename T, typename CF, int E>
 void launch_conv_cfg(const void* xpad, const void* W, const void* bias, void* Y, int M, int N, int K,
-                     const ConvGeom& cg, hipStream_t s) {
+                     const ConvGeom& cg, int splits, float* ws, hipStream_t s) {
   const int tiles = ((M + CF::BM - 1) / CF::BM) * ((N + CF::BN - 1) / CF::BN);
+  auto px = static_cast<const uint16_t*>(xpad);
+  auto pw = static_cast<const uint16_t*>(W);
+  auto pb = static_cast<const uint16_t*>(bias);
+  auto py = static_cast<uint16_t*>(Y);
+  if (splits > 1) {  // few output tiles (late ResNet stages): split the K = KH*KW*C loop
+    gemm_lds_kernel<T, CF, true, true, kNone, false, true, true><<<tiles * splits, CF::NT, 0, s>>>(
+        px, pw, nullptr, nullptr, nullptr, nullptr, M, N, K, 0, K, N, N, splits, ws, cg);
+    const int64_t quads = (int64_t)M * N / 4;
+    splitk_reduce_k<T, E, false><<<(int)((quads + 255) / 256), 256, 0, s>>>(ws, splits, pb, py, nullptr, M, N, N, N);
+    return;
+  }
   gemm_lds_kernel<T, CF, true, true, E, false, false, true><<<tiles, CF::NT, 0, s>>>(
-      static_cast<const uint16_t*>(xpad), static_cast<const uint16_t*>(W), static_cast<const uint16_t*>(bias),
-      static_cast<uint16_t*>(Y), nullptr, nullptr, M, N, K, 0, K, N, N, 1, nullptr, cg);
+      px, pw, pb, py, nullptr, nullptr, M, N, K, 0, K, N, N, 1, nullptr, cg);
 }
 
-// tile by output channels: 512x64 for N <= 64, 256x128 for N <= 128, else 256x256
+// tile by output channels: 512x64 for N <= 64, 256x128 for N <= 128, else 256x256 (split-K
+// only there: the narrow tiles serve the large-M early layers)
 template <typename T, int E>
 int launch_conv(const void* xpad, const void* W, const void* bias, void* Y, int M, int N, int K, const ConvGeom& cg,
-                hipStream_t s) {
-  if (N <= 64) launch_conv_cfg<T, C64, E>(xpad, W, bias, Y, M, N, K, cg, s);
-  else if (N <= 128) launch_conv_cfg<T, C128, E>(xpad, W, bias, Y, M, N, K, cg, s);
-  else launch_conv_cfg<T, W8, E>(xpad, W, bias, Y, M, N, K, cg, s);
+                int splits, float* ws, hipStream_t s) {
+  if (N <= 64) launch_conv_cfg<T, C64, E>(xpad, W, bias, Y, M, N, K, cg, 1, nullptr, s);
+  else if (N <= 128) launch_conv_cfg<T, C128, E>(xpad, W, bias, Y, M, N, K, cg, 1, nullptr, s);
+  else launch_conv_cfg<T, W8, E>(xpad, W, bias, Y, M, N, K, cg, splits, ws, s);
   return 0;
 }
 
@@ -640,32 +662,35 @@ int launch_conv(const void* xpad, const void* W, const void* bias, void* Y, int 
 }  // namespace pra
 
 // Implicit-GEMM convolution, channels-last, on the LDS-DMA MFMA kernel:
-//   Y[N*Ho*Wo][Cout] = im2col(x_pad) · Wkᵀ (+ bias, optional ReLU)
-// x_pad is the zero-padded input [N][Hp][Wp][C]; Wk the OHWI filter as a [Cout][KH*KW*C] matrix.
-// Requires C % 64 == 0, Cout % 8 == 0, x_pad smaller than 4 GB (32-bit DMA offsets).
-extern "C" int pra_conv_lds(const void* xpad, const void* W, const void* bias, void* Y, int Nimg, int Hp, int Wp,
-                            int C, int Ho, int Wo, int Cout, int KH, int KW, int S, int relu, int dtype,
+//   Y[N*Ho*Wo][Cout] = im2col(x) · Wkᵀ (+ bias, optional ReLU), zero padding P on H and W
+// x is the input [N][H][W][C]; Wk the OHWI filter as a [Cout][KH*KW*C] matrix.
+// Requires C % 64 == 0, Cout % 8 == 0 and x smaller than 2 GB (32-bit DMA offsets with the
+// out-of-image sentinel above every valid one).
+// splits > 1 (Cout > 128 only): split-K through the fp32 workspace ws [splits][M][Cout]
+// (pra_conv_lds_splits gives the factor).
+extern "C" int pra_conv_lds(const void* x, const void* W, const void* bias, void* Y, int Nimg, int H, int Wd,
+                            int C, int Cout, int KH, int KW, int S, int P, int relu, int dtype, int splits, float* ws,
                             hipStream_t s) {
-  if (C % 64 || Cout % 8 || KH <= 0 || KW <= 0 || S <= 0) return -1;
-  if ((long long)Nimg * Hp * Wp * C * 2 >= (1ll << 32)) return -1;
-  if ((Ho - 1) * S + KH > Hp || (Wo - 1) * S + KW > Wp) return -1;
+  if (C % 64 || Cout % 8 || KH <= 0 || KW <= 0 || S <= 0 || P < 0 || H <= 0 || Wd <= 0) return -1;
+  if (H >= 32768 || Wd >= 32768 || (long long)Nimg * H * Wd * C * 2 >= (1ll << 31)) return -1;
+  const int Ho = (H + 2 * P - KH) / S + 1, Wo = (Wd + 2 * P - KW) / S + 1;
+  if (Ho <= 0 || Wo <= 0) return -1;
   const long long Mll = (long long)Nimg * Ho * Wo;
   if (Mll >= (1ll << 31)) return -1;
   const int M = (int)Mll, K = KH * KW * C;
-  pra::ConvGeom cg{Ho, Wo, Hp, Wp, C, KW, S};
-  if (dtype == pra::kBF16) return relu ? pra::launch_conv<pra::bf16, pra::kRelu>(xpad, W, bias, Y, M, Cout, K, cg, s)
-                                  : pra::launch_conv<pra::bf16, pra::kNone>(xpad, W, bias, Y, M, Cout, K, cg, s);
-  if (dtype == pra::kF16) return relu ? pra::launch_conv<pra::f16, pra::kRelu>(xpad, W, bias, Y, M, Cout, K, cg, s)
-                                 : pra::launch_conv<pra::f16, pra::kNone>(xpad, W, bias, Y, M, Cout, K, cg, s);
+  if (splits > 1 && (Cout <= 128 || !ws)) return -1;
+  pra::ConvGeom cg{Ho, Wo, H, Wd, C, KW, S, P};
+  if (dtype == pra::kBF16) return relu ? pra::launch_conv<pra::bf16, pra::kRelu>(x, W, bias, Y, M, Cout, K, cg, splits, ws, s)
+                                  : pra::launch_conv<pra::bf16, pra::kNone>(x, W, bias, Y, M, Cout, K, cg, splits, ws, s);
+  if (dtype == pra::kF16) return relu ? pra::launch_conv<pra::f16, pra::kRelu>(x, W, bias, Y, M, Cout, K, cg, splits, ws, s)
+                                 : pra::launch_conv<pra::f16, pra::kNone>(x, W, bias, Y, M, Cout, K, cg, splits, ws, s);
   return -1;
 }
 
-// layout: 0 = A[M][K]·B[K][N] (forward), 1 = A[M][K]·B[N][K]ᵀ (dgrad / NT), 2 = A[K][M]ᵀ·B[K][N] (wgrad).
-// epi: 0 none, 1 gelu(erf), 2 gelu(tanh), 3 relu (Z receives the pre-activation if given),
-//      4/5 dgelu(erf/tanh): C = acc * gelu'(Z) (Z required). colsum (optional, fp32
-//      [ceil(M/256)][N]) receives per-tile column partial sums of the stored C.
-// Returns -1 (nothing launched) for shapes outside what the kernel assumes: K % 64, N % 8 and every
-// leading dimension % 8 (16-B rows), M-contiguous operands need their MN extent >= 8.
+// Split-K factor for an implicit-GEMM conv (1 for the narrow-tile configs, Cout <= 128)
+extern "C" int pra_gemm_lds_splits(int M, int N, int K);
+extern "C" int pra_conv_lds_splits(int M, int Cout, int K) { return Cout <= 128 ? 1 : pra_gemm_lds_splits(M, Cout, K); }
+
 // Split-K factor for a problem: 1 unless the tile grid leaves CUs idle (fewer than ~256 tiles on
 // a long K loop); then the factor that best fills whole rounds of 256 workgroups.
 extern "C" int pra_gemm_lds_splits(int M, int N, int K) {

@@ -1078,8 +1078,8 @@ def conv1x1_nhwc(x, w, bias=None, stride=(1, 1)):
 
 # =============================================================================
 # KxK convolution (channels-last, groups 1, dilation 1) as an implicit GEMM on the LDS-DMA MFMA
-# kernel (gemm_lds.hip ConvDmaA): the im2col rows are gathered from the zero-padded NHWC input
-# by the DMA, never materialised. Forward for any stride; the stride-1 input gradient is the
+# kernel (gemm_lds.hip ConvDmaA): the im2col rows are gathered from the NHWC input by the
+# buffer LDS-DMA (padding = its range check), never materialised. Forward for any stride; the stride-1 input gradient is the
 # same kernel on the padded output gradient with the flipped, in/out-transposed filter; the
 # weight gradient (and strided input gradients) use MIOpen's convolution_backward.
 # Parity: the reference's conv2d (phi gpudnn conv kernels) for ResNet's 3x3 layers.
@@ -1090,21 +1090,26 @@ def conv_kxk_supported(x, w, stride, padding):
         return False
     cin, cout = x.shape[3], w.shape[0]
     return (w.shape[1] == cin and cin % 64 == 0 and cout % 8 == 0 and stride >= 1 and padding >= 0
-            and x.shape[1] + 2 * padding >= w.shape[2] and x.shape[2] + 2 * padding >= w.shape[3])
+            and x.shape[1] + 2 * padding >= w.shape[2] and x.shape[2] + 2 * padding >= w.shape[3]
+            and x.numel() * 2 < 2 ** 31 and max(x.shape[1], x.shape[2]) < 32768)
 
 
 def _conv_lds(x, wk, bias, kh, kw, stride, pad, relu=False):
-    """y[N,Ho,Wo,Cout] = conv(x NHWC, wk [Cout, kh*kw*C] (OHWI)) via the implicit-GEMM kernel."""
+    """y[N,Ho,Wo,Cout] = conv(x NHWC, wk [Cout, kh*kw*C] (OHWI)) via the implicit-GEMM kernel
+    (zero padding applied by the kernel's DMA range check, the input is read in place)."""
     n, h, wd, c = x.shape
     cout = wk.shape[0]
-    xp = torch.nn.functional.pad(x, (0, 0, pad, pad, pad, pad)) if pad else x.contiguous()
-    hp, wp = h + 2 * pad, wd + 2 * pad
-    ho, wo = (hp - kh) // stride + 1, (wp - kw) // stride + 1
+    x = x.contiguous()
+    ho, wo = (h + 2 * pad - kh) // stride + 1, (wd + 2 * pad - kw) // stride + 1
     y = torch.empty((n, ho, wo, cout), device=x.device, dtype=x.dtype)
     if bias is not None and (bias.dtype != x.dtype or not bias.is_contiguous()):
         bias = bias.to(x.dtype).contiguous()
-    _native.lib().conv_lds(xp.data_ptr(), wk.data_ptr(), _ptr(bias), y.data_ptr(), n, hp, wp, c, ho, wo,
-                           cout, kh, kw, stride, int(relu), _dt(x), _stream())
+    L = _native.lib()
+    m = n * ho * wo
+    splits = L.conv_lds_splits(m, cout, kh * kw * c)
+    ws = torch.empty((splits, m, cout), device=x.device, dtype=torch.float32) if splits > 1 else None
+    L.conv_lds(x.data_ptr(), wk.data_ptr(), _ptr(bias), y.data_ptr(), n, h, wd, c, cout, kh, kw,
+               stride, pad, int(relu), _dt(x), splits, _ptr(ws), _stream())
     return y
 
 
