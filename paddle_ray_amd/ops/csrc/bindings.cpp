@@ -72,7 +72,7 @@ void pra_bn_fwd_train(const void*, const void*, const void*, const void*, float*
 void pra_bn_fwd_infer(const void*, const void*, const void*, const void*, const float*, const float*, void*, float*,
                       int, int, float, int, int, int, hipStream_t);
 void pra_bn_bwd(const void*, const void*, const uint8_t*, const void*, const void*, const float*, const float*, void*,
-                void*, void*, void*, float*, float*, int, int, int, int, int, int, hipStream_t);
+                void*, void*, void*, float*, float*, int, int, int, int, int, int, int, hipStream_t);
 }
 
 #define V(x) reinterpret_cast<void*>(x)
@@ -247,9 +247,9 @@ PYBIND11_MODULE(_pra_hip, m) {
     check_launch("bn_fwd_infer");
   });
   m.def("bn_bwd", [](P dy, P y, P mask, P x, P w, P mean, P invstd, P dx, P dz, P dw, P db, P part, P coef, int M,
-                     int C, int nrb, int relu, int dt, int dtw, P s) {
+                     int C, int nrb, int relu, int dt, int dtw, int acc, P s) {
     pra_bn_bwd(CV(dy), CV(y), reinterpret_cast<const uint8_t*>(mask), CV(x), CV(w), CF(mean), CF(invstd), V(dx), V(dz),
-               V(dw), V(db), F(part), F(coef), M, C, nrb, relu, dt, dtw, S(s));
+               V(dw), V(db), F(part), F(coef), M, C, nrb, relu, dt, dtw, acc, S(s));
     check_launch("bn_bwd");
   });
   m.def("embedding_fwd", [](P ids, P w, P out, int64_t n, int D, int64_t V, int64_t pad, int dt, P s) {

@@ -219,15 +219,16 @@ __global__ void __launch_bounds__(1024) bn_fin_bwd_k(const float* __restrict__ p
                                                      int dtw, const float* __restrict__ mean,
                                                      const float* __restrict__ invstd, void* __restrict__ dw,
                                                      void* __restrict__ db, float* __restrict__ coef, int nrb, int M,
-                                                     int C) {
+                                                     int C, int acc) {
   __shared__ double red[2048];
   const int c = blockIdx.x * 64 + (threadIdx.x & 63), rl = threadIdx.x >> 6;
   double S1, S2;
   merge_parts(part, nrb, C, c, rl, S1, S2, red);
   if (rl != 0 || c >= C) return;
   const float is = invstd[c];
-  if (dw) stw(dw, c, dtw, (float)(S2 * is));
-  if (db) stw(db, c, dtw, (float)S1);
+  // acc: add into the existing parameter gradients (no separate AccumulateGrad add)
+  if (dw) stw(dw, c, dtw, (float)(S2 * is) + (acc ? ldw(dw, c, dtw) : 0.f));
+  if (db) stw(db, c, dtw, (float)S1 + (acc ? ldw(db, c, dtw) : 0.f));
   const float a = (w ? ldw(w, c, dtw) : 1.f) * is;
   const float c1 = (float)(-(double)a * is * is * S2 / M);
   coef[c] = a;
@@ -411,7 +412,7 @@ void pra_bn_fwd_infer(const void* x, const void* z, const void* w, const void* b
 // dz (residual grad) may be null. coef: [3, C] fp32 scratch.
 void pra_bn_bwd(const void* dy, const void* y, const uint8_t* mask, const void* x, const void* w, const float* mean,
                 const float* invstd, void* dx, void* dz, void* dw, void* db, float* part, float* coef, int M, int C,
-                int nrb, int relu, int dt, int dtw, hipStream_t s) {
+                int nrb, int relu, int dt, int dtw, int acc, hipStream_t s) {
   const int rpb = bn_rpb(M, C, nrb);
   const dim3 rg(bn_grid_x(C), nrb);
   const uint32_t nvec = (uint32_t)((size_t)M * C / 8);
@@ -424,7 +425,7 @@ void pra_bn_bwd(const void* dy, const void* y, const uint8_t* mask, const void* 
       hipLaunchKernelGGL((bn_reduce_k<T, 1, false>), rg, dim3(kRedThreads), 0, s, (const T*)x, (const T*)dy, nullptr,
                          nullptr, mean, part, M, C, rpb);
     hipLaunchKernelGGL(bn_fin_bwd_k, dim3((C + 63) / 64), dim3(1024), 0, s, part, w, dtw, mean, invstd, dw, db, coef,
-                       nrb, M, C);
+                       nrb, M, C, acc);
     if (relu)
       hipLaunchKernelGGL((bn_bwd_apply_k<T, true>), dim3(g), dim3(kBnThreads), 0, s, (const T*)dy, (const T*)y, mask,
                          (const T*)x, coef, (T*)dx, (T*)dz, nvec, C);

@@ -1046,6 +1046,7 @@ class Conv1x1Fn(torch.autograd.Function):
         x2, w2 = xs.view(-1, cin), w.reshape(cout, cin)
         y = gemm(GEMM_NT, x2, w2, bias=None if bias is None else bias.to(x.dtype))
         ctx.save_for_backward(x2, w2)
+        ctx.w = w
         ctx.meta = (tuple(x.shape), tuple(xs.shape), tuple(w.shape), sh, sw, bias is not None)
         return y.view(n, h, wd, cout)
 
@@ -1066,7 +1067,13 @@ class Conv1x1Fn(torch.autograd.Function):
                 dx = torch.zeros(xshape, dtype=dx2.dtype, device=dx2.device)
                 dx[:, ::sh, ::sw, :] = dx2.view(xsshape)
         if ctx.needs_input_grad[1]:
-            dw = gemm(GEMM_TN, dy2, x2).view(wshape)
+            g = ctx.w.grad
+            if _acc_grad_ok(g, ctx.w, dy2.dtype):
+                # dW accumulated into the existing gradient by the beta=1 epilogue (the weight's
+                # AccumulateGrad node still runs and fires its post-accumulate hooks)
+                gemm(GEMM_TN, dy2, x2, out=g.view(w2.shape), beta=1)
+            else:
+                dw = gemm(GEMM_TN, dy2, x2).view(wshape)
         if hb and ctx.needs_input_grad[2]:
             db = dy2.sum(0, dtype=torch.float32).to(dy2.dtype)
         return dx, dw, db, None, None
@@ -1544,7 +1551,9 @@ def _bn_fwd_hip(x2, z2, w, b, rmean, rvar, training, momentum, eps, relu):
 
 
 @R.register_kernel('batch_norm_bwd', 'hip', dtypes=_FLOATS)
-def _bn_bwd_hip(dy, y, mask, x2, w, mean, invstd, relu, need_dz):
+def _bn_bwd_hip(dy, y, mask, x2, w, mean, invstd, relu, need_dz, acc=None):
+    """acc = (w.grad, b.grad): the scale / shift gradients are added into these in the
+    finalize kernel and (None, None) is returned for them."""
     if not _bn_hip_ok(x2):
         return _bn_bwd_ref(dy, y, mask, x2, w, mean, invstd, relu, need_dz)
     L = _native.lib()
@@ -1556,14 +1565,20 @@ def _bn_bwd_hip(dy, y, mask, x2, w, mean, invstd, relu, need_dz):
     if need_dz:
         dz = torch.empty_like(x2) if relu else dy
     pdt = w.dtype if w is not None else torch.float32
-    dwb = torch.empty((2, C), device=dev, dtype=pdt)
+    if acc is not None:
+        gw, gb = acc
+    else:
+        dwb = torch.empty((2, C), device=dev, dtype=pdt)
+        gw, gb = dwb[0], dwb[1]
     nrb = L.bn_nrb(M, C)
     part = torch.empty((2, nrb, C), device=dev, dtype=torch.float32)
     coef = torch.empty((3, C), device=dev, dtype=torch.float32)
     L.bn_bwd(_ptr(dy), _ptr(y) if relu else 0, _ptr(mask) if relu else 0, _ptr(x2), _ptr(w), _ptr(mean), _ptr(invstd),
-             _ptr(dx), _ptr(dz) if (need_dz and relu) else 0, _ptr(dwb[0]), _ptr(dwb[1]),
-             _ptr(part), _ptr(coef), M, C, nrb, int(relu), _dt(x2), _DT[pdt], _stream())
-    return dx, dz, dwb[0], dwb[1]
+             _ptr(dx), _ptr(dz) if (need_dz and relu) else 0, _ptr(gw), _ptr(gb),
+             _ptr(part), _ptr(coef), M, C, nrb, int(relu), _dt(x2), _DT[pdt], int(acc is not None), _stream())
+    if acc is not None:
+        return dx, dz, None, None
+    return dx, dz, gw, gb
 
 
 class BatchNormActFn(torch.autograd.Function):
@@ -1582,7 +1597,7 @@ class BatchNormActFn(torch.autograd.Function):
         # ReLU backward needs only the keep-bits (1 B per 8 channels) when the kernel wrote them
         ctx.save_for_backward(x2, y if (relu and mask is None) else None, mask, w, mean, invstd)
         ctx.relu, ctx.shp, ctx.has_z = relu, shp, z is not None
-        ctx.has_b, ctx.training = b is not None, training
+        ctx.has_b, ctx.training, ctx.b = b is not None, training, b
         return y.view(shp)
 
     @staticmethod
@@ -1599,8 +1614,18 @@ class BatchNormActFn(torch.autograd.Function):
             dz = g.to(x2.dtype).view(ctx.shp) if ctx.has_z else None
             return ((g * a).to(x2.dtype).view(ctx.shp), dz, dw if w is not None else None,
                     g.sum(0).to(pdt) if ctx.has_b else None, None, None, None, None, None, None)
-        dx, dz, dw, db = R.dispatch('batch_norm_bwd', x2, dy2, y, mask, x2, w, mean, invstd, ctx.relu,
-                                    ctx.has_z and ctx.needs_input_grad[1])
+        acc = None
+        b = ctx.b
+        if (x2.is_cuda and w is not None and b is not None and ctx.needs_input_grad[2]
+                and ctx.needs_input_grad[3] and _acc_grad_ok(w.grad, w, w.dtype)
+                and _acc_grad_ok(b.grad, b, w.dtype) and R.select_backend(x2, 'batch_norm_bwd') == 'hip'):
+            acc = (w.grad, b.grad)  # scale/shift grads accumulated in the finalize kernel
+        if acc is not None:
+            dx, dz, dw, db = _bn_bwd_hip(dy2, y, mask, x2, w, mean, invstd, ctx.relu,
+                                         ctx.has_z and ctx.needs_input_grad[1], acc=acc)
+        else:
+            dx, dz, dw, db = R.dispatch('batch_norm_bwd', x2, dy2, y, mask, x2, w, mean, invstd, ctx.relu,
+                                        ctx.has_z and ctx.needs_input_grad[1])
         return (dx.view(ctx.shp), dz.view(ctx.shp) if dz is not None else None,
                 dw if (w is not None and ctx.needs_input_grad[2]) else None,
                 db if (ctx.has_b and ctx.needs_input_grad[3]) else None,

@@ -155,12 +155,13 @@ class Optimizer:
         return None, None
 
     def clear_grad(self, set_to_zero=True):
+        if set_to_zero:
+            gs = [p._t.grad for p in self._parameter_list if p._t.grad is not None]
+            if gs:
+                torch._foreach_zero_(gs)  # multi-tensor launches, not one fill per parameter
+            return
         for p in self._parameter_list:
-            if p._t.grad is not None:
-                if set_to_zero:
-                    p._t.grad.zero_()
-                else:
-                    p._t.grad = None
+            p._t.grad = None
 
     clear_gradients = clear_grad
 

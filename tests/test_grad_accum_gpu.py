@@ -1,0 +1,46 @@
+"""Parameter gradients accumulated inside the kernels (BN finalize, conv1x1 wgrad beta=1
+epilogue) match autograd's own accumulation over two backward passes, and the
+post-accumulate hooks still fire."""
+import pytest
+import torch
+
+from paddle_ray_amd.ops import fused as K
+
+
+@pytest.mark.gpu
+def test_bn_grad_accumulates_in_kernel():
+    torch.manual_seed(0)
+    M, C = 4096, 64
+    x = torch.randn(M, C, device='cuda', dtype=torch.bfloat16)
+    w = torch.randn(C, device='cuda', requires_grad=True)
+    b = torch.randn(C, device='cuda', requires_grad=True)
+    fired = []
+    w.register_post_accumulate_grad_hook(lambda t: fired.append('w'))
+    rm, rv = torch.zeros(C, device='cuda'), torch.ones(C, device='cuda')
+    dys = [torch.randn(M, C, device='cuda', dtype=torch.bfloat16) for _ in range(2)]
+    for dy in dys:
+        K.batch_norm_act(x, None, w, b, rm, rv, True, relu=True).backward(dy)
+    assert fired == ['w', 'w']
+    wr, br = w.detach().clone().requires_grad_(), b.detach().clone().requires_grad_()
+    for dy in dys:
+        xf = x.float()
+        y = torch.relu((xf - xf.mean(0)) / torch.sqrt(xf.var(0, unbiased=False) + 1e-5) * wr + br)
+        y.backward(dy.float())
+    torch.testing.assert_close(w.grad, wr.grad, rtol=2e-2, atol=2e-1)
+    torch.testing.assert_close(b.grad, br.grad, rtol=2e-2, atol=2e-1)
+
+
+@pytest.mark.gpu
+def test_conv1x1_wgrad_accumulates_in_kernel():
+    torch.manual_seed(0)
+    x = torch.randn(4, 16, 16, 64, device='cuda', dtype=torch.bfloat16)
+    w = (torch.randn(128, 64, 1, 1, device='cuda') * 0.1).to(torch.bfloat16).requires_grad_()
+    fired = []
+    w.register_post_accumulate_grad_hook(lambda t: fired.append(1))
+    dys = [torch.randn(4, 16, 16, 128, device='cuda', dtype=torch.bfloat16) for _ in range(2)]
+    for dy in dys:
+        K.conv1x1_nhwc(x, w).backward(dy)
+    assert len(fired) == 2
+    ref = sum(torch.einsum('nhwo,nhwi->oi', dy.float(), x.float()) for dy in dys)
+    err = (w.grad.float().view(128, 64) - ref).abs().max().item()
+    assert err <= 2e-2 * ref.abs().max().item() + 0.5, err
