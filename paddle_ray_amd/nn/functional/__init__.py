@@ -570,6 +570,12 @@ def _pool(kind, n, x, kernel_size, stride, padding, ceil_mode, data_format, excl
           return_mask=False, divisor_override=None):
     t = _t(x)
     cl = data_format in ('NHWC', 'NLC', 'NDHWC')
+    if kind == 'max' and n == 2 and cl and not ceil_mode and not return_mask and t.is_cuda:
+        ks = _ntuple(kernel_size, 2)
+        st = ks if stride is None else _ntuple(stride, 2)
+        pd, extra = _pool_pad(padding, 2)
+        if extra is None and not isinstance(pd, str) and K.max_pool_nhwc_supported(t, ks, st, pd):
+            return _w(K.max_pool2d_nhwc(t, ks, st, pd))
     if cl:
         t = t.movedim(-1, 1)
     ks = _ntuple(kernel_size, n)

@@ -58,6 +58,10 @@ int pra_embedding_bwd(const int64_t*, const int64_t*, const void*, void*, int64_
 void pra_bias_gelu_bwd_db(const void*, const void*, const void*, void*, float*, int, int, int, int, int,
                           hipStream_t);
 int pra_bn_nrb(int, int);
+int pra_max_pool_fwd(const void*, void*, uint8_t*, int, int, int, int, int, int, int, int, int, int, int, int, int,
+                     hipStream_t);
+int pra_max_pool_bwd(const void*, const uint8_t*, void*, int, int, int, int, int, int, int, int, int, int, int, int,
+                     int, hipStream_t);
 int pra_gemm_bias_act(const void*, const void*, const void*, void*, void*, int, int, int, int, int, int, int, int,
                       hipStream_t);
 int pra_gemm_lds(int, const void*, const void*, const void*, void*, void*, float*, int, int, int, int, int, int, int,
@@ -251,6 +255,20 @@ PYBIND11_MODULE(_pra_hip, m) {
     pra_bn_bwd(CV(dy), CV(y), reinterpret_cast<const uint8_t*>(mask), CV(x), CV(w), CF(mean), CF(invstd), V(dx), V(dz),
                V(dw), V(db), F(part), F(coef), M, C, nrb, relu, dt, dtw, acc, S(s));
     check_launch("bn_bwd");
+  });
+  m.def("max_pool_fwd", [](P x, P y, P idx, int n, int h, int w, int c, int ho, int wo, int kh, int kw, int sh,
+                           int sw, int ph, int pw, int dt, P s) {
+    if (pra_max_pool_fwd(CV(x), V(y), reinterpret_cast<uint8_t*>(idx), n, h, w, c, ho, wo, kh, kw, sh, sw, ph, pw, dt,
+                         S(s)) != 0)
+      throw std::invalid_argument("max_pool_fwd: unsupported geometry");
+    check_launch("max_pool_fwd");
+  });
+  m.def("max_pool_bwd", [](P dy, P idx, P dx, int n, int h, int w, int c, int ho, int wo, int kh, int kw, int sh,
+                           int sw, int ph, int pw, int dt, P s) {
+    if (pra_max_pool_bwd(CV(dy), reinterpret_cast<const uint8_t*>(idx), V(dx), n, h, w, c, ho, wo, kh, kw, sh, sw, ph,
+                         pw, dt, S(s)) != 0)
+      throw std::invalid_argument("max_pool_bwd: unsupported geometry");
+    check_launch("max_pool_bwd");
   });
   m.def("embedding_fwd", [](P ids, P w, P out, int64_t n, int D, int64_t V, int64_t pad, int dt, P s) {
     if (pra_embedding_fwd(I64(ids), CV(w), V(out), n, D, V, pad, dt, S(s)) != 0)

@@ -1639,6 +1639,45 @@ def batch_norm_act(x, z, w, b, rmean, rvar, training, momentum=0.9, eps=1e-5, re
 
 
 # =============================================================================
+# Max pooling, channels-last (parity: paddle/phi/kernels/funcs/pooling.cu): the forward keeps
+# the winning tap per output element as one byte; the backward gathers (no atomics, no
+# zero-fill, no int64 index tensor)
+# =============================================================================
+def max_pool_nhwc_supported(x, k, s, p):
+    return (x.is_cuda and x.dim() == 4 and x.dtype in _FLOATS and x.shape[3] % 8 == 0
+            and k[0] * k[1] <= 255 and p[0] < k[0] and p[1] < k[1] and min(s) >= 1 and min(p) >= 0)
+
+
+class MaxPoolNHWCFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, kh, kw, sh, sw, ph, pw):
+        x = x.contiguous()
+        n, h, w, c = x.shape
+        ho, wo = (h + 2 * ph - kh) // sh + 1, (w + 2 * pw - kw) // sw + 1
+        y = torch.empty((n, ho, wo, c), device=x.device, dtype=x.dtype)
+        idx = torch.empty((n, ho, wo, c), device=x.device, dtype=torch.uint8)
+        _native.lib().max_pool_fwd(x.data_ptr(), y.data_ptr(), idx.data_ptr(), n, h, w, c, ho, wo, kh, kw, sh,
+                                   sw, ph, pw, _dt(x), _stream())
+        ctx.save_for_backward(idx)
+        ctx.geo = (n, h, w, c, ho, wo, kh, kw, sh, sw, ph, pw)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        idx, = ctx.saved_tensors
+        n, h, w, c = ctx.geo[:4]
+        dy = dy.contiguous()
+        dx = torch.empty((n, h, w, c), device=dy.device, dtype=dy.dtype)
+        _native.lib().max_pool_bwd(dy.data_ptr(), idx.data_ptr(), dx.data_ptr(), *ctx.geo, _dt(dy), _stream())
+        return dx, None, None, None, None, None, None
+
+
+def max_pool2d_nhwc(x, kernel, stride, padding):
+    return MaxPoolNHWCFn.apply(x, int(kernel[0]), int(kernel[1]), int(stride[0]), int(stride[1]),
+                               int(padding[0]), int(padding[1]))
+
+
+# =============================================================================
 # Embedding lookup (parity: paddle/phi/kernels/gpu/embedding_kernel.cu,
 # embedding_grad_kernel.cu); ids outside [0, V) or == padding_idx read as zero rows
 # =============================================================================
