@@ -1036,9 +1036,87 @@ def _gemm_ref_fast(layout, a, b, out, bias, z, epi, beta, want_colsum):
 # conv2d with 1x1 filters (phi conv kernels); stride-2 1x1 (ResNet downsample) reads the
 # strided positions and scatters dx back.
 # =============================================================================
+class GradJoin:
+    """Gradient join for a tensor consumed by several fused ops (a residual block's input: the
+    first 1x1 conv, the downsample conv and the residual input of the last BN+add+ReLU).
+    Instead of each op returning its own full-size gradient and autograd summing them with
+    separate add kernels, every contributor adds into one pending buffer (1x1 dgrad through
+    the GEMM's beta=1 epilogue, a strided conv into its sampled positions, BN's dz as the
+    initial buffer) and only the LAST contributor to run backward returns the total; the
+    others return None. Contributors register in forward, so the count is exact."""
+
+    __slots__ = ('x', 'n', 'left', 'pending')
+
+    def __init__(self, x):
+        self.x, self.n, self.left, self.pending = x, 0, None, None
+
+    def _finish(self):
+        if self.left is None:
+            self.left = self.n
+        self.left -= 1
+        if self.left == 0:
+            out, self.pending = self.pending, None
+            self.left = None
+            return out
+        return None
+
+    def add_gemm(self, dy2, w2, xshape):
+        if self.pending is None:
+            self.pending = gemm(GEMM_FWD, dy2, w2).view(xshape)
+        else:
+            gemm(GEMM_FWD, dy2, w2, out=self.pending.view(-1, w2.shape[1]), beta=1)
+        return self._finish()
+
+    def add_strided(self, dx2, xshape, sh, sw):
+        if self.pending is None:
+            self.pending = torch.zeros(xshape, dtype=dx2.dtype, device=dx2.device)
+            self.pending[:, ::sh, ::sw, :] = dx2
+        else:
+            self.pending[:, ::sh, ::sw, :] += dx2
+        return self._finish()
+
+    def add_tensor(self, g, owned):
+        if self.pending is None:
+            self.pending = g if owned else g.clone()
+        else:
+            self.pending += g
+        return self._finish()
+
+
+_JOIN = [None]
+
+
+class grad_join:
+    """``with grad_join(x):`` — fused ops inside that consume ``x`` (the same tensor object)
+    join their input gradients (see GradJoin). No-op without autograd."""
+
+    def __init__(self, x):
+        self.x = x
+
+    def __enter__(self):
+        self.prev = _JOIN[0]
+        x = self.x
+        ok = isinstance(x, torch.Tensor) and x.requires_grad and torch.is_grad_enabled() and x.is_cuda
+        _JOIN[0] = GradJoin(x) if ok else None
+        return _JOIN[0]
+
+    def __exit__(self, *exc):
+        _JOIN[0] = self.prev
+        return False
+
+
+def _join_for(t):
+    j = _JOIN[0]
+    if j is not None and t is j.x:
+        j.n += 1
+        return j
+    return None
+
+
 class Conv1x1Fn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, bias, sh, sw):
+    def forward(ctx, x, w, bias, sh, sw, join=None):
+        ctx.join = join
         xs = x if (sh, sw) == (1, 1) else x[:, ::sh, ::sw, :]
         xs = xs.contiguous()
         n, h, wd, cin = xs.shape
@@ -1060,12 +1138,18 @@ class Conv1x1Fn(torch.autograd.Function):
         dy2 = _like(dy2, x2.dtype)
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            dx2 = gemm(GEMM_FWD, dy2, w2)
-            if (sh, sw) == (1, 1):
-                dx = dx2.view(xshape)
+            j = ctx.join
+            if j is not None and (sh, sw) == (1, 1):
+                dx = j.add_gemm(dy2, w2, xshape)
+            elif j is not None:
+                dx = j.add_strided(gemm(GEMM_FWD, dy2, w2).view(xsshape), xshape, sh, sw)
             else:
-                dx = torch.zeros(xshape, dtype=dx2.dtype, device=dx2.device)
-                dx[:, ::sh, ::sw, :] = dx2.view(xsshape)
+                dx2 = gemm(GEMM_FWD, dy2, w2)
+                if (sh, sw) == (1, 1):
+                    dx = dx2.view(xshape)
+                else:
+                    dx = torch.zeros(xshape, dtype=dx2.dtype, device=dx2.device)
+                    dx[:, ::sh, ::sw, :] = dx2.view(xsshape)
         if ctx.needs_input_grad[1]:
             g = ctx.w.grad
             if _acc_grad_ok(g, ctx.w, dy2.dtype):
@@ -1076,11 +1160,11 @@ class Conv1x1Fn(torch.autograd.Function):
                 dw = gemm(GEMM_TN, dy2, x2).view(wshape)
         if hb and ctx.needs_input_grad[2]:
             db = dy2.sum(0, dtype=torch.float32).to(dy2.dtype)
-        return dx, dw, db, None, None
+        return dx, dw, db, None, None, None
 
 
 def conv1x1_nhwc(x, w, bias=None, stride=(1, 1)):
-    return Conv1x1Fn.apply(x, w, bias, int(stride[0]), int(stride[1]))
+    return Conv1x1Fn.apply(x, w, bias, int(stride[0]), int(stride[1]), _join_for(x))
 
 
 # =============================================================================
@@ -1585,7 +1669,8 @@ class BatchNormActFn(torch.autograd.Function):
     """y = act(BN(x) + z) over channels-last x[..., C]; running stats updated in place."""
 
     @staticmethod
-    def forward(ctx, x, z, w, b, rmean, rvar, training, momentum, eps, relu):
+    def forward(ctx, x, z, w, b, rmean, rvar, training, momentum, eps, relu, join=None):
+        ctx.join = join
         shp = x.shape
         C = shp[-1]
         x2 = x.contiguous().view(-1, C)
@@ -1612,8 +1697,10 @@ class BatchNormActFn(torch.autograd.Function):
             pdt = w.dtype if w is not None else torch.float32
             dw = (g * (x2.float() - mean) * invstd).sum(0).to(pdt)
             dz = g.to(x2.dtype).view(ctx.shp) if ctx.has_z else None
+            if dz is not None and ctx.join is not None:
+                dz = ctx.join.add_tensor(dz, owned=True)
             return ((g * a).to(x2.dtype).view(ctx.shp), dz, dw if w is not None else None,
-                    g.sum(0).to(pdt) if ctx.has_b else None, None, None, None, None, None, None)
+                    g.sum(0).to(pdt) if ctx.has_b else None, None, None, None, None, None, None, None)
         acc = None
         b = ctx.b
         if (x2.is_cuda and w is not None and b is not None and ctx.needs_input_grad[2]
@@ -1626,16 +1713,21 @@ class BatchNormActFn(torch.autograd.Function):
         else:
             dx, dz, dw, db = R.dispatch('batch_norm_bwd', x2, dy2, y, mask, x2, w, mean, invstd, ctx.relu,
                                         ctx.has_z and ctx.needs_input_grad[1])
-        return (dx.view(ctx.shp), dz.view(ctx.shp) if dz is not None else None,
+        if dz is not None:
+            dz = dz.view(ctx.shp)
+            if ctx.join is not None:
+                dz = ctx.join.add_tensor(dz, owned=dz.data_ptr() != dy2.data_ptr())
+        return (dx.view(ctx.shp), dz,
                 dw if (w is not None and ctx.needs_input_grad[2]) else None,
                 db if (ctx.has_b and ctx.needs_input_grad[3]) else None,
-                None, None, None, None, None, None)
+                None, None, None, None, None, None, None)
 
 
 def batch_norm_act(x, z, w, b, rmean, rvar, training, momentum=0.9, eps=1e-5, relu=False):
     """Channels-last BatchNorm with optional fused residual add and ReLU (paddle momentum
     convention: running = momentum * running + (1 - momentum) * batch)."""
-    return BatchNormActFn.apply(x, z, w, b, rmean, rvar, training, momentum, eps, relu)
+    return BatchNormActFn.apply(x, z, w, b, rmean, rvar, training, momentum, eps, relu,
+                                _join_for(z) if z is not None else None)
 
 
 # =============================================================================

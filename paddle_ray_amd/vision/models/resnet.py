@@ -5,6 +5,7 @@ MIOpen's fast bf16 conv kernels want on MI355X (no NCHW<->NHWC transposes).
 """
 from ... import nn
 from ...nn import functional as F
+from ...ops.fused import grad_join as _grad_join
 
 
 def _bn_act(bn, x, z=None, act='relu'):
@@ -66,12 +67,15 @@ class BottleneckBlock(nn.Layer):
         self.stride = stride
 
     def forward(self, x):
-        identity = x
-        out = _bn_act(self.bn1, self.conv1(x))
-        out = _bn_act(self.bn2, self.conv2(out))
-        if self.downsample is not None:
-            identity = self.downsample(x)
-        return _bn_act(self.bn3, self.conv3(out), identity)
+        # the block input's gradient is joined in-kernel across its consumers (conv1, the
+        # downsample conv or the residual add) instead of summed by separate add kernels
+        with _grad_join(x._t):
+            identity = x
+            out = _bn_act(self.bn1, self.conv1(x))
+            out = _bn_act(self.bn2, self.conv2(out))
+            if self.downsample is not None:
+                identity = self.downsample(x)
+            return _bn_act(self.bn3, self.conv3(out), identity)
 
 
 class ResNet(nn.Layer):

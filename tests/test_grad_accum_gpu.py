@@ -44,3 +44,37 @@ def test_conv1x1_wgrad_accumulates_in_kernel():
     ref = sum(torch.einsum('nhwo,nhwi->oi', dy.float(), x.float()) for dy in dys)
     err = (w.grad.float().view(128, 64) - ref).abs().max().item()
     assert err <= 2e-2 * ref.abs().max().item() + 0.5, err
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("stride,down", [(1, False), (2, True), (1, True)])
+def test_bottleneck_grad_join_matches_autograd_sum(stride, down, monkeypatch):
+    """Block-input gradient joined in-kernel (GradJoin) == autograd's own sum of branches."""
+    import contextlib
+    import paddle_ray_amd as paddle
+    from paddle_ray_amd.vision.models import resnet as R
+    paddle.seed(0)
+    inpl, planes = (64, 16) if not down else (64, 32)
+    ds = None
+    if down:
+        ds = paddle.nn.Sequential(
+            paddle.nn.Conv2D(inpl, planes * 4, 1, stride=stride, bias_attr=False, data_format='NHWC'),
+            paddle.nn.BatchNorm2D(planes * 4, data_format='NHWC'))
+    blk = R.BottleneckBlock(inpl, planes, stride=stride, downsample=ds, data_format='NHWC')
+    blk = paddle.amp.decorate(blk, level='O2', dtype='bfloat16')
+    x0 = torch.randn(4, 16, 16, inpl, device='cuda', dtype=torch.bfloat16)
+    outs = []
+    for joined in (True, False):
+        if not joined:
+            monkeypatch.setattr(R, '_grad_join', lambda t: contextlib.nullcontext())
+        for p in blk.parameters():
+            p._t.grad = None
+        x = paddle.Tensor(x0.clone().requires_grad_())
+        y = blk(x)
+        g = torch.randn(y.shape, device='cuda', generator=torch.Generator('cuda').manual_seed(1)).to(y._t.dtype)
+        y._t.backward(g)
+        outs.append((x._t.grad.float().clone(), [p._t.grad.float().clone() for p in blk.parameters()]))
+    (gx1, gp1), (gx2, gp2) = outs
+    torch.testing.assert_close(gx1, gx2, rtol=2e-2, atol=2e-2)
+    for a, b in zip(gp1, gp2):
+        torch.testing.assert_close(a, b, rtol=5e-2, atol=5e-2)
