@@ -47,7 +47,7 @@ void pra_adl_fwd(const void*, const void*, const void*, const void*, const void*
                  int, float, float, uint64_t, uint64_t, int, int, hipStream_t);
 void pra_adl_bwd(const void*, const void*, const void*, const void*, const float*, const float*, void*, void*, float*,
                  float*, float*, int, int, int, float, uint64_t, uint64_t, int, int, hipStream_t);
-void pra_colsum16(const float*, void*, int, int, int, hipStream_t);
+void pra_colsum16(const float*, void*, int, int, int, int, hipStream_t);
 int pra_flash_fwd(const void*, const void*, const void*, void*, float*, int, int, int, int, int, const int64_t*, float,
                   int, int, hipStream_t);
 int pra_flash_bwd(const void*, const void*, const void*, const void*, const float*, const float*, void*, void*, void*,
@@ -215,8 +215,12 @@ PYBIND11_MODULE(_pra_hip, m) {
     check_launch("adl_bwd");
   });
   m.def("colsum16", [](P part, P out, int nblk, int cols, int dt, P s) {
-    pra_colsum16(CF(part), V(out), nblk, cols, dt, S(s));
+    pra_colsum16(CF(part), V(out), nblk, cols, dt, 0, S(s));
     check_launch("colsum16");
+  });
+  m.def("colsum16_acc", [](P part, P out, int nblk, int cols, int dt, P s) {
+    pra_colsum16(CF(part), V(out), nblk, cols, dt, 1, S(s));
+    check_launch("colsum16_acc");
   });
   m.def("flash_bwd_pre", [](P o, P dO, P delta, int B, int H, int Sq, int D, int dt, P s) {
     pra_flash_bwd_pre(CV(o), CV(dO), F(delta), B, H, Sq, D, dt, S(s));

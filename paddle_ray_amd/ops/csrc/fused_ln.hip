@@ -214,7 +214,7 @@ __global__ void __launch_bounds__(256) adl_bwd_k(const T* __restrict__ dy, const
 // out[c] = sum_b part[b][c]; workgroup = 16 columns x 16 row slices
 template <typename O>
 __global__ void __launch_bounds__(256) colsum16_k(const float* __restrict__ part, O* __restrict__ out, int nblk,
-                                                  int cols) {
+                                                  int cols, int acc) {
   __shared__ float red[16][17];
   const int cl = threadIdx.x & 15, rg = threadIdx.x >> 4;
   const int c = blockIdx.x * 16 + cl;
@@ -227,6 +227,7 @@ __global__ void __launch_bounds__(256) colsum16_k(const float* __restrict__ part
     float t = 0.f;
 #pragma unroll
     for (int i = 0; i < 16; ++i) t += red[i][cl];
+    if (acc) t += Cvt<O>::to(out[c]);  // accumulate into an existing gradient
     out[c] = Cvt<O>::from(t);
   }
 }
@@ -283,8 +284,8 @@ void pra_adl_bwd(const void* dy, const void* dr_out, const void* r, const void* 
 #undef K_BWD
 }
 
-void pra_colsum16(const float* part, void* out, int nblk, int cols, int dto, hipStream_t s) {
+void pra_colsum16(const float* part, void* out, int nblk, int cols, int dto, int acc, hipStream_t s) {
   PRA_DISPATCH_FLOAT(dto, TO, hipLaunchKernelGGL((colsum16_k<TO>), dim3((cols + 15) / 16), dim3(256), 0, s,
-                                                 part, (TO*)out, nblk, cols));
+                                                 part, (TO*)out, nblk, cols, acc));
 }
 }

@@ -246,7 +246,10 @@ def _adl_fwd_hip(x2, h2, hb, w, b, p, eps, seed):
 
 
 @R.register_kernel('add_dropout_ln_bwd', 'hip', dtypes=_FLOATS)
-def _adl_bwd_hip(dy, dr_out, r, w, mean, rstd, p, seed, need_dw, need_db, need_dhb):
+def _adl_bwd_hip(dy, dr_out, r, w, mean, rstd, p, seed, need_dw, need_db, need_dhb, into=None):
+    """into: (w.grad, b.grad, hb.grad) or None per slot — those column sums are ADDED into the
+    existing gradient by the reduction kernel and None is returned in their place (no
+    AccumulateGrad add kernels for the LayerNorm / bias parameters)."""
     _check_dtypes('add_dropout_layer_norm_grad', (r, dy), (r, dr_out))
     rows, cols = r.shape
     if not _adl_ok(cols):
@@ -262,14 +265,25 @@ def _adl_bwd_hip(dy, dr_out, r, w, mean, rstd, p, seed, need_dw, need_db, need_d
               _ptr(part[2]) if need_dhb else 0, rows, cols, nblk, float(p), seed, 0, _dt(r),
               _dt(w) if w is not None else _dt(r), _stream())
     outs = []
+    into = into or (None, None, None)
     for need, i, dt in ((need_dw, 0, pdt), (need_db, 1, pdt), (need_dhb, 2, r.dtype)):
-        if need:
+        if need and into[i] is not None:
+            L.colsum16_acc(_ptr(part[i]), _ptr(into[i]), nblk, cols, _DT[into[i].dtype], _stream())
+            outs.append(None)
+        elif need:
             o = torch.empty(cols, device=r.device, dtype=dt)
             L.colsum16(_ptr(part[i]), _ptr(o), nblk, cols, _DT[dt], _stream())
             outs.append(o)
         else:
             outs.append(None)
     return (dri, dh) + tuple(outs)
+
+
+def _acc_target(p):
+    """p's existing gradient when a kernel may add into it in place (see LinearFn)."""
+    if p is None or not p.is_cuda or not p.requires_grad or p.grad_fn is not None:
+        return None
+    return p.grad if _acc_grad_ok(p.grad, p, p.dtype) else None
 
 
 class AddDropoutLNFn(torch.autograd.Function):
@@ -285,6 +299,7 @@ class AddDropoutLNFn(torch.autograd.Function):
         seed = _dropout_seed() if p > 0 else 0
         r, y, mean, rstd = R.dispatch('add_dropout_ln_fwd', x2, x2, h2, hb, w, b, p, eps, seed)
         ctx.save_for_backward(r, w, mean, rstd)
+        ctx.params = (w, b, hb)
         ctx.p, ctx.seed, ctx.shp = p, seed, shp
         ctx.has_b, ctx.has_hb = b is not None, hb is not None
         return r.view(shp), y.view(shp)
@@ -296,11 +311,15 @@ class AddDropoutLNFn(torch.autograd.Function):
         if g_y is None:
             g_y = torch.zeros_like(r)
         dr_out = None if g_r is None else _like(g_r, r.dtype).contiguous().view(-1, cols)
-        dri, dh, dw, db, dhb = R.dispatch(
-            'add_dropout_ln_bwd', r, _like(g_y, r.dtype).contiguous().view(-1, cols), dr_out, r, w,
-            mean, rstd,
-            ctx.p, ctx.seed, w is not None and ctx.needs_input_grad[3],
-            ctx.has_b and ctx.needs_input_grad[4], ctx.has_hb and ctx.needs_input_grad[2])
+        args = (r, _like(g_y, r.dtype).contiguous().view(-1, cols), dr_out, r, w, mean, rstd,
+                ctx.p, ctx.seed, w is not None and ctx.needs_input_grad[3],
+                ctx.has_b and ctx.needs_input_grad[4], ctx.has_hb and ctx.needs_input_grad[2])
+        if r.is_cuda and R.select_backend(r, 'add_dropout_ln_bwd') == 'hip':
+            pw, pb, phb = ctx.params
+            into = (_acc_target(pw), _acc_target(pb), _acc_target(phb))
+            dri, dh, dw, db, dhb = _adl_bwd_hip(*args[1:], into=into)
+        else:
+            dri, dh, dw, db, dhb = R.dispatch('add_dropout_ln_bwd', *args)
         return dri.view(ctx.shp), dh.view(ctx.shp), dhb, dw, db, None, None
 
 

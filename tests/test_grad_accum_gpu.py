@@ -78,3 +78,30 @@ def test_bottleneck_grad_join_matches_autograd_sum(stride, down, monkeypatch):
     torch.testing.assert_close(gx1, gx2, rtol=2e-2, atol=2e-2)
     for a, b in zip(gp1, gp2):
         torch.testing.assert_close(a, b, rtol=5e-2, atol=5e-2)
+
+
+@pytest.mark.gpu
+def test_add_dropout_ln_param_grads_accumulate_in_kernel():
+    torch.manual_seed(0)
+    R_, C = 512, 1024
+    x = torch.randn(R_, C, device='cuda', dtype=torch.bfloat16)
+    h = torch.randn(R_, C, device='cuda', dtype=torch.bfloat16)
+    hb = torch.randn(C, device='cuda', dtype=torch.bfloat16, requires_grad=True)
+    w = torch.randn(C, device='cuda', dtype=torch.bfloat16, requires_grad=True)
+    b = torch.randn(C, device='cuda', dtype=torch.bfloat16, requires_grad=True)
+    fired = []
+    for t in (hb, w, b):
+        t.register_post_accumulate_grad_hook(lambda t: fired.append(1))
+    gs = [torch.randn(R_, C, device='cuda', dtype=torch.bfloat16) for _ in range(2)]
+    for g in gs:
+        r, y = K.add_dropout_layer_norm(x, h, hb, w, b, p=0.0)
+        y.backward(g)
+    assert len(fired) == 6
+    refs = [t.detach().float().clone().requires_grad_() for t in (hb, w, b)]
+    for g in gs:
+        rr = x.float() + h.float() + refs[0]
+        yr = torch.nn.functional.layer_norm(rr, (C,), refs[1], refs[2], 1e-5)
+        yr.backward(g.float())
+    for got, ref in zip((hb, w, b), refs):
+        err = (got.grad.float() - ref.grad).abs().max().item()
+        assert err <= 2e-2 * ref.grad.abs().max().item() + 0.5, err
