@@ -96,6 +96,8 @@ def main():
         result = bench_gpt(a, paddle, torch, dist, C, world, rank, dev)
     elif a.model.startswith('bert'):
         result = bench_bert(a, paddle, torch, dist, C, world, rank, dev)
+    elif a.model.startswith('ernie'):
+        result = bench_ernie(a, paddle, torch, dist, C, world, rank, dev)
     else:
         result = bench_resnet(a, paddle, torch, dist, C, world, rank, dev)
     result['backend'] = dist.get_backend() if world > 1 else 'none'
@@ -210,6 +212,64 @@ def bench_resnet(a, paddle, torch, dist, C, world, rank, dev):
             "config": {"model": "ResNet50", "global_batch": bs * world, "seq_len": None,
                        "parallelism": f"dp{world}"},
             "samples_per_sec_per_gpu": round(ips / world, 2)}
+
+
+def bench_ernie(a, paddle, torch, dist, C, world, rank, dev):
+    """BASELINE config 5: ERNIE-3.0 10B MLM pretraining, Fleet hybrid TP=2 x PP=world/2 (TP=2 x
+    PP=4 on 8 GPUs: Megatron column/row-parallel layers with RCCL all-reduce inside each stage,
+    1F1B micro-batch schedule over RCCL send/recv between stages); one GPU trains the whole
+    10B model (bf16 params, fp32 AdamW master/moments: ~160 GB of 288). Tokens/s of the job."""
+    import numpy as np
+    from paddle_ray_amd.distributed import fleet
+    from paddle_ray_amd.models import ernie_config, ernie_pipe
+    mp = 2 if world % 2 == 0 else 1
+    pp = world // mp
+    S = a.seq if a.seq != 1024 else 512
+    micro = a.micro_batch if a.micro_batch != 16 else 2
+    acc = max(8, 2 * pp)
+    name = 'ernie-3.0-10b' if a.model in ('ernie', 'ernie-10b', 'ernie-3.0-10b') else a.model
+    cfg = ernie_config(name, mp_degree=mp, hidden_dropout_prob=a.dropout,
+                       attention_probs_dropout_prob=0.0, max_position_embeddings=max(S, 512))
+    if world > 1:
+        st = fleet.DistributedStrategy()
+        st.hybrid_configs = {'dp_degree': 1, 'mp_degree': mp, 'pp_degree': pp}
+        st.pipeline_configs = {'micro_batch_size': micro, 'accumulate_steps': acc}
+        fleet.init(is_collective=True, strategy=st)
+    paddle.seed(1234)
+    pl = ernie_pipe(cfg)
+    pl = paddle.amp.decorate(pl, level='O2', dtype='bfloat16')
+    opt = paddle.optimizer.AdamW(1e-4, parameters=pl.parameters(), multi_precision=True)
+    rs = np.random.RandomState(rank)
+    B = micro * acc
+    ids = paddle.to_tensor(rs.randint(5, cfg.vocab_size, (B, S)))
+    labels = paddle.to_tensor(rs.randint(5, cfg.vocab_size, (B, S)))
+    if world > 1:
+        model = fleet.distributed_model(pl)
+        opt = fleet.distributed_optimizer(opt)
+
+        def step():
+            model.train_batch([ids, labels], opt)
+    else:
+        idc, lbc = ids.split(acc, 0), labels.split(acc, 0)
+
+        def step():
+            for i in range(acc):
+                loss = pl._loss_fn(pl(idc[i]), lbc[i]) / acc
+                loss.backward()
+            opt.step()
+            opt.clear_grad()
+
+    dt = _timed(step, a, torch, dist, world, dev)
+    tps = B * S * a.steps / dt
+    n_params = sum(int(np.prod(p.shape)) for p in pl.parameters()) * mp
+    return {"metric": "tokens/sec ERNIE-3.0-10B Fleet TP x PP", "value": round(tps, 2),
+            "unit": "tokens/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+            "ms_per_step": round(dt / a.steps * 1000, 3), "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": "bf16",
+            "data": "synthetic (random tokens, random-init weights)",
+            "config": {"model": "ERNIE-3.0-10B" if name == "ernie-3.0-10b" else name, "global_batch": B, "seq_len": S,
+                       "parallelism": f"tp{mp}_pp{pp}", "micro_batch": micro,
+                       "accumulate_steps": acc, "params_per_stage_x_tp": n_params}}
 
 
 def bench_bert(a, paddle, torch, dist, C, world, rank, dev):

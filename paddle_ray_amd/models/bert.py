@@ -59,6 +59,11 @@ BERT_CONFIGS = {
     'ernie-3.0-medium-zh': dict(vocab_size=40000, num_hidden_layers=6,
                                 max_position_embeddings=2048, type_vocab_size=4,
                                 use_task_id=True, layer_norm_eps=1e-5),
+    # BASELINE config 5: ERNIE-3.0 10B class dense encoder (48 x 4096, 64 heads, 16384 FFN:
+    # 9.7B encoder + 0.16B embedding parameters) for the TP=2 x PP=4 Fleet hybrid run
+    'ernie-3.0-10b': dict(vocab_size=40000, hidden_size=4096, num_hidden_layers=48,
+                          num_attention_heads=64, intermediate_size=16384,
+                          max_position_embeddings=2048, type_vocab_size=4, layer_norm_eps=1e-5),
 }
 
 
