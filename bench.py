@@ -225,7 +225,7 @@ def bench_ernie(a, paddle, torch, dist, C, world, rank, dev):
     mp = 2 if world % 2 == 0 else 1
     pp = world // mp
     S = a.seq if a.seq != 1024 else 512
-    micro = a.micro_batch if a.micro_batch != 16 else 2
+    micro = a.micro_batch if a.micro_batch != 16 else 8
     acc = max(8, 2 * pp)
     name = 'ernie-3.0-10b' if a.model in ('ernie', 'ernie-10b', 'ernie-3.0-10b') else a.model
     cfg = ernie_config(name, mp_degree=mp, hidden_dropout_prob=a.dropout,
