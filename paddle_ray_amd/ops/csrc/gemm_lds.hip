@@ -251,7 +251,8 @@ __device__ __forceinline__ typename V8<T>::type frag(const char* img, int r0, in
   }
 }
 
-template <typename T, typename CF, bool AK, bool BK, int E, bool BETA, bool SPLIT, bool CONV = false>
+template <typename T, typename CF, bool AK, bool BK, int E, bool BETA, bool SPLIT, bool CONV = false,
+          int DPSX = 0>
 __global__ __launch_bounds__(CF::NT, 1) void gemm_lds_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
                                                           const uint16_t* __restrict__ bias, uint16_t* __restrict__ C,
                                                           uint16_t* __restrict__ Z, float* __restrict__ colsum,
@@ -316,19 +317,24 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_lds_kernel(const uint16_t* __r
   // 32 MFMAs of one k-half, interleaved segment by segment with (optionally) the fragment reads
   // of the next k-half and one LDS-DMA instruction of the next K-step every other segment, so
   // DMA issue and LDS reads hide under the wave's own matrix work.
-  auto half = [&](v8 (&ca)[TI], v8 (&cb)[TJ], v8 (&na)[TI], v8 (&nb)[TJ], bool rd, int rkt, int rs, bool dma,
-                  int dkt) {
-    const uint32_t so = lds_base + (dkt & 1) * SLOT;
+  // dA / dB: issue this half's share of operand A's (step kA) / B's (step kB) DMA
+  auto half = [&](v8 (&ca)[TI], v8 (&cb)[TJ], v8 (&na)[TI], v8 (&nb)[TJ], bool rd, int rkt, int rs, bool dA,
+                  int kA, bool dB, int kB) {
+    const uint32_t soA = lds_base + (kA & 1) * SLOT, soB = lds_base + (kB & 1) * SLOT + IMGA;
     const char* ai = lds + (rkt & 1) * SLOT;
     const char* bi = ai + IMGA;
-    constexpr int DPS = (NDA + NDB + TI - 1) / TI;  // DMA instructions per segment
+    // DMA instructions per segment (DPSX > 0: front-load them into the first segments)
+    constexpr int DPS = DPSX > 0 ? DPSX : (NDA + NDB + TI - 1) / TI;
 #pragma unroll
     for (int i = 0; i < TI; ++i) {
-      if (dma) {
+      if (dA || dB) {
 #pragma unroll
         for (int d = i * DPS; d < (i + 1) * DPS && d < NDA + NDB; ++d) {
-          if (d < NDA) da.issue1(so, wave, dkt, d);
-          else db.issue1(so + IMGA, wave, dkt, d - NDA);
+          if (d < NDA) {
+            if (dA) da.issue1(soA, wave, kA, d);
+          } else if (dB) {
+            db.issue1(soB, wave, kB, d - NDA);
+          }
         }
       }
       if (rd) {
@@ -366,15 +372,18 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_lds_kernel(const uint16_t* __r
   // K-step kt (slot kt&1): half 0 computes (kt,0) from F0 while reading (kt,1) into F1; then the
   // barrier that retires step kt+1's DMA and every wave's reads of slot kt; half 1 refills slot kt
   // with step kt+2 (DMA) and computes (kt,1) from F1 while reading (kt+1,0) into F0.
+  // (measured: issuing B of step kt+1 under half 0 of step kt instead, so both halves carry DMA,
+  // was 8-15 % slower on every GPT shape: half a K-step does not cover the DMA latency)
+  const bool dmaon = SPLIT || splits != 0;
   for (int kt = 0; kt < nk; ++kt) {
-    half(fa0, fb0, fa1, fb1, true, kt, 1, false, 0);
+    half(fa0, fb0, fa1, fb1, true, kt, 1, false, 0, false, 0);
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): (kt,1) fragments landed; slot kt reads done
     if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // step kt+1 landed (this wave)
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
     // (non-split launches pass splits = 0 only for the PRA_GEMM_ABLATE=nodma timing ablation)
-    half(fa1, fb1, fa0, fb0, kt + 1 < nk, kt + 1, 0, kt + 2 < nk && (SPLIT || splits != 0), kt + 2);
+    half(fa1, fb1, fa0, fb0, kt + 1 < nk, kt + 1, 0, kt + 2 < nk && dmaon, kt + 2, kt + 2 < nk && dmaon, kt + 2);
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_waitcnt(0xC07F);  // (kt+1,0) fragments landed
   }
@@ -594,6 +603,8 @@ void launch_e(const void* A, const void* B, const void* bias, void* C, void* Z, 
     else splitk_reduce_k<T, E, false><<<blocks, 256, 0, s>>>(ws, splits, pbias, pc, pz, M, N, ldc, ldz);
     return;
   }
+  // (measured: front-loading the step's DMA into the first 2 / 4 segments of the half instead of
+  // one per segment was 1-10 % slower on every GPT shape)
 #define PRA_GEMM_LAUNCH(CFG, BETA_)                                                                         \
   gemm_lds_kernel<T, CFG, AK, BK, E, BETA_, false><<<tiles, CFG::NT, 0, s>>>(pa, pb, pbias, pc, pz, colsum, M, N, K, \
                                                                            lda, ldb, ldc, ldz, ablate, nullptr)
