@@ -126,6 +126,10 @@ def init_parallel_env(backend=None, timeout_s=None):
         os.environ['MASTER_PORT'] = ep.split(':')[1] if ':' in ep else '29500'
     use_gpu = torch.cuda.is_available() and _default_device().type == 'cuda'
     if backend is None or backend == 'auto':
+        # PRA_DIST_BACKEND=gloo rehearses a multi-rank GPU job on ONE device (RCCL refuses two
+        # ranks on one GPU): same code paths, host-staged collectives
+        backend = os.environ.get('PRA_DIST_BACKEND', 'auto')
+    if backend == 'auto':
         backend = 'nccl' if use_gpu else 'gloo'
     if backend in ('rccl', 'xccl', 'bkcl'):
         backend = 'nccl'
