@@ -70,6 +70,8 @@ int pra_gemm_lds_splits(int, int, int);
 int pra_conv_lds(const void*, const void*, const void*, void*, int, int, int, int, int, int, int, int, int, int, int,
                  int, float*, hipStream_t);
 int pra_conv_lds_splits(int, int, int);
+int pra_conv_wgrad_lds(const void*, const void*, void*, int, int, int, int, int, int, int, int, int, int, int, float*,
+                       hipStream_t);
 int pra_colsum_partials(const float*, void*, int, int, int, hipStream_t);
 void pra_bn_fwd_train(const void*, const void*, const void*, const void*, float*, float*, void*, uint8_t*, float*,
                       float*, float*, float*, int, int, int, float, float, int, int, int, hipStream_t);
@@ -105,6 +107,13 @@ PYBIND11_MODULE(_pra_hip, m) {
                      reinterpret_cast<float*>(ws), S(s)) != 0)
       throw std::invalid_argument("conv_lds: unsupported shape/dtype");
     check_launch("conv_lds");
+  });
+  m.def("conv_wgrad_lds", [](P dy, P x, P dw, int n, int h, int wd, int c, int cout, int kh, int kw, int st, int pad,
+                             int dt, int splits, P ws, P s) {
+    if (pra_conv_wgrad_lds(CV(dy), CV(x), V(dw), n, h, wd, c, cout, kh, kw, st, pad, dt, splits,
+                           reinterpret_cast<float*>(ws), S(s)) != 0)
+      throw std::invalid_argument("conv_wgrad_lds: unsupported shape/dtype");
+    check_launch("conv_wgrad_lds");
   });
   m.def("conv_lds_splits", [](int m, int n, int k) { return pra_conv_lds_splits(m, n, k); });
   m.def("gemm_lds_splits", [](int M, int N, int K) { return pra_gemm_lds_splits(M, N, K); });

@@ -229,6 +229,69 @@ struct ConvDmaA {
   }
 };
 
+// Weight-gradient operand B = im2col(x) for dW = dyᵀ · im2col(x): GEMM K = output pixel
+// (n, ho, wo), N = (kh, kw, c), staged as the M/N-contiguous image [64 pixels][256 columns]
+// (chunk ^= mc_swz(k)). A thread's NDMA chunks share one image column (rows k, k+16, k+32,
+// k+48 have equal mc_swz), hence one (kh, kw, c) for the whole kernel; each chunk walks its
+// pixel forward by 64 per staged K-step (carry arithmetic, no divisions in the loop).
+// Out-of-image taps read zeros through the buffer range check, as in ConvDmaA.
+template <int NT, int NDMA>
+struct ConvDmaBW {
+  int base[NDMA];       // element offset of x[img][ho*S][wo*S][0] of the chunk's current pixel
+  uint32_t hw[NDMA];    // ho << 16 | wo of that pixel
+  int colterm;          // ((kh-P)*W + (kw-P))*C + c of the thread's column
+  uint32_t kp;          // (kh-P) << 16 | (kw-P) & 0xffff
+  u32x4 rs;
+  ConvGeom g;
+  int dH, dW;           // 64 pixels = dH output rows + dW output columns
+  __device__ __forceinline__ void seek(int n, int pix) {
+    const int wo = pix % g.Wo, t = pix / g.Wo, ho = t % g.Ho, im = t / g.Ho;
+    base[n] = ((im * g.H + ho * g.S) * g.W + wo * g.S) * g.C;
+    hw[n] = ((uint32_t)ho << 16) | (uint32_t)wo;
+  }
+  __device__ __forceinline__ void init(const uint16_t* x, const ConvGeom& cg, int n0, int K, int tid) {
+    g = cg;
+    const int k = tid >> 5, c = (tid & 31) ^ mc_swz(k);  // same column for every chunk
+    const int col = n0 + 8 * c;
+    const int tap = col / g.C, cin = col - tap * g.C, kh = tap / g.KW, kw = tap - kh * g.KW;
+    colterm = ((kh - g.P) * g.W + (kw - g.P)) * g.C + cin;
+    kp = ((uint32_t)(kh - g.P) << 16) | ((uint32_t)(kw - g.P) & 0xffffu);
+    dH = 64 / g.Wo;
+    dW = 64 - dH * g.Wo;
+#pragma unroll
+    for (int n = 0; n < NDMA; ++n) seek(n, (n * NT + tid) >> 5);
+    const uint64_t b = (uint64_t)x;
+    rs[0] = __builtin_amdgcn_readfirstlane((uint32_t)b);
+    rs[1] = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32)) & 0xffffu;
+    rs[2] = __builtin_amdgcn_readfirstlane((uint32_t)((int64_t)K / (g.Ho * g.Wo) * g.H * g.W * g.C * 2));
+    rs[3] = 0x00020000u;
+  }
+  __device__ __forceinline__ void advance(int ksteps) {
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int n = 0; n < NDMA; ++n) seek(n, ksteps * 64 + ((n * NT + tid) >> 5));
+  }
+  __device__ __forceinline__ void issue1(uint32_t lds_img, int wave, int /*kt*/, int n) {
+    int ho = (int)(hw[n] >> 16), wo = (int)(hw[n] & 0xffffu);
+    const int hi = ho * g.S + ((int)kp >> 16), wi = wo * g.S + (int)(int16_t)(kp & 0xffffu);
+    const bool ok = (unsigned)hi < (unsigned)g.H && (unsigned)wi < (unsigned)g.W;
+    const uint32_t voff = ok ? (uint32_t)(base[n] + colterm) * 2u : 0x80000000u;
+    const uint32_t dst = __builtin_amdgcn_readfirstlane(lds_img + (n * NT + wave * 64) * 16);
+    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(rs),
+                 "s"(dst)
+                 : "memory");
+    // this chunk's next staged K-step is 64 pixels further (carries, no divisions)
+    const int SC = g.S * g.C, SWC = g.S * g.W * g.C;
+    wo += dW;
+    ho += dH;
+    int b = base[n] + dW * SC + dH * SWC;
+    if (wo >= g.Wo) { wo -= g.Wo; ho += 1; b += SWC - g.Wo * SC; }
+    while (ho >= g.Ho) { ho -= g.Ho; b += g.H * g.W * g.C - g.Ho * SWC; }
+    base[n] = b;
+    hw[n] = ((uint32_t)ho << 16) | (uint32_t)wo;
+  }
+};
+
 // Fragment for rows [r0, r0+16) (row = lane&15), k = 32*s + 8*(lane>>4) + j of a K-step.
 template <typename T, bool KC>
 __device__ __forceinline__ typename V8<T>::type frag(const char* img, int r0, int s, int lane) {
@@ -252,7 +315,7 @@ __device__ __forceinline__ typename V8<T>::type frag(const char* img, int r0, in
 }
 
 template <typename T, typename CF, bool AK, bool BK, int E, bool BETA, bool SPLIT, bool CONV = false,
-          int DPSX = 0>
+          int DPSX = 0, bool CONVW = false>
 __global__ __launch_bounds__(CF::NT, 1) void gemm_lds_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
                                                           const uint16_t* __restrict__ bias, uint16_t* __restrict__ C,
                                                           uint16_t* __restrict__ Z, float* __restrict__ colsum,
@@ -262,6 +325,7 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_lds_kernel(const uint16_t* __r
   constexpr int BM = CF::BM, BN = CF::BN, IMGA = CF::IMGA, SLOT = CF::SLOT;
   constexpr int RW = TI * 16, CW = TJ * 16;  // rows / columns per wave
   static_assert(BK || BN == 256, "the M/N-contiguous B image is 256 columns wide");
+  static_assert(!CONVW || (!BK && NDB == 4), "conv wgrad gathers the 256-wide B image");
   static_assert(TJ <= TI && 128 % RW == 0 && NDA >= 1 && NDB >= 1, "wave layout");
   __shared__ __attribute__((aligned(1024))) char lds[CF::LDS];
   typedef typename V8<T>::type v8;
@@ -286,11 +350,13 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_lds_kernel(const uint16_t* __r
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wr = wave / WC, wc = wave % WC;
 
   typename std::conditional<CONV, ConvDmaA<NT, NDA>, Dma<AK, NT, NDA>>::type da;
-  Dma<BK, NT, NDB> db;
+  typename std::conditional<CONVW, ConvDmaBW<NT, NDB>, Dma<BK, NT, NDB>>::type db;
   if constexpr (CONV) da.init(A, cg, m0, M, tid);
   else if (AK) da.init(A, lda, m0, M - 1, tid);
   else da.init(A, lda, m0, M - 8, tid);
-  if (BK) db.init(B, ldb, n0, N - 1, tid); else db.init(B, ldb, n0, N - 8, tid);
+  if constexpr (CONVW) db.init(B, cg, n0, K, tid);
+  else if (BK) db.init(B, ldb, n0, N - 1, tid);
+  else db.init(B, ldb, n0, N - 8, tid);
   int nk = K / BKT;
   if (SPLIT) {
     const int per = (nk + splits - 1) / splits, kb = split * per;
@@ -658,6 +724,26 @@ void launch_conv_cfg(const void* xpad, const void* W, const void* bias, void* Y,
       px, pw, pb, py, nullptr, nullptr, M, N, K, 0, K, N, N, 1, nullptr, cg);
 }
 
+// dW [Cout][KH*KW*C] = dy[pix][Cout]ᵀ · im2col(x)[pix][KH*KW*C] (TN, gathered B), split-K over pixels
+template <typename T>
+void launch_conv_wgrad(const void* dy, const void* x, void* dW, int Mpix, int Cout, int Nk, const ConvGeom& cg,
+                       int splits, float* ws, hipStream_t s) {
+  const int tiles = ((Cout + BM - 1) / BM) * ((Nk + BN - 1) / BN);
+  auto pdy = static_cast<const uint16_t*>(dy);
+  auto px = static_cast<const uint16_t*>(x);
+  auto pw = static_cast<uint16_t*>(dW);
+  if (splits > 1) {
+    gemm_lds_kernel<T, W8, false, false, kNone, false, true, false, 0, true><<<tiles * splits, W8::NT, 0, s>>>(
+        pdy, px, nullptr, nullptr, nullptr, nullptr, Cout, Nk, Mpix, Cout, 0, Nk, Nk, splits, ws, cg);
+    const int64_t quads = (int64_t)Cout * Nk / 4;
+    splitk_reduce_k<T, kNone, false><<<(int)((quads + 255) / 256), 256, 0, s>>>(ws, splits, nullptr, pw, nullptr, Cout,
+                                                                               Nk, Nk, Nk);
+    return;
+  }
+  gemm_lds_kernel<T, W8, false, false, kNone, false, false, false, 0, true><<<tiles, W8::NT, 0, s>>>(
+      pdy, px, nullptr, pw, nullptr, nullptr, Cout, Nk, Mpix, Cout, 0, Nk, Nk, 1, nullptr, cg);
+}
+
 // tile by output channels: 512x64 for N <= 64, 256x128 for N <= 128, else 256x256 (split-K
 // only there: the narrow tiles serve the large-M early layers)
 template <typename T, int E>
@@ -696,6 +782,26 @@ extern "C" int pra_conv_lds(const void* x, const void* W, const void* bias, void
   if (dtype == pra::kF16) return relu ? pra::launch_conv<pra::f16, pra::kRelu>(x, W, bias, Y, M, Cout, K, cg, splits, ws, s)
                                  : pra::launch_conv<pra::f16, pra::kNone>(x, W, bias, Y, M, Cout, K, cg, splits, ws, s);
   return -1;
+}
+
+// Convolution weight gradient on the same kernel: dW (OHWI, [Cout][KH*KW*C]) from dy
+// [N*Ho*Wo][Cout] and x [N][H][W][C]. Requires C % 64 == 0, Cout % 8 == 0, Cout >= 8, N*Ho*Wo
+// % 64 == 0, x < 2 GB. splits > 1: fp32 workspace ws [splits][Cout][KH*KW*C].
+extern "C" int pra_conv_wgrad_lds(const void* dy, const void* x, void* dW, int Nimg, int H, int Wd, int C, int Cout,
+                                  int KH, int KW, int S, int P, int dtype, int splits, float* ws, hipStream_t s) {
+  if (C % 64 || Cout % 8 || Cout < 8 || KH <= 0 || KW <= 0 || S <= 0 || P < 0 || H <= 0 || Wd <= 0) return -1;
+  if (H >= 32768 || Wd >= 32768 || (long long)Nimg * H * Wd * C * 2 >= (1ll << 31)) return -1;
+  const int Ho = (H + 2 * P - KH) / S + 1, Wo = (Wd + 2 * P - KW) / S + 1;
+  if (Ho <= 0 || Wo <= 0) return -1;
+  const long long Mll = (long long)Nimg * Ho * Wo;
+  if (Mll >= (1ll << 31) || Mll % 64 || (long long)Mll * Cout * 2 >= (1ll << 32)) return -1;
+  if (splits > 1 && !ws) return -1;
+  const int Nk = KH * KW * C;
+  pra::ConvGeom cg{Ho, Wo, H, Wd, C, KW, S, P};
+  if (dtype == pra::kBF16) pra::launch_conv_wgrad<pra::bf16>(dy, x, dW, (int)Mll, Cout, Nk, cg, splits, ws, s);
+  else if (dtype == pra::kF16) pra::launch_conv_wgrad<pra::f16>(dy, x, dW, (int)Mll, Cout, Nk, cg, splits, ws, s);
+  else return -1;
+  return 0;
 }
 
 // Split-K factor for an implicit-GEMM conv (1 for the narrow-tile configs, Cout <= 128)

@@ -1223,6 +1223,38 @@ def _conv_lds(x, wk, bias, kh, kw, stride, pad, relu=False):
     return y
 
 
+def _conv_wgrad_ok(x, dy, cout):
+    n, h, wd, c = x.shape
+    # Cout >= 256 only: the 256-row tile idles 3/4 (1/2) of its MFMA rows at Cout 64 (128), where
+    # MIOpen's wgrad is faster (profiles/r2_conv/conv3x3_wgrad.log)
+    return (_CONV_WGRAD == 'mfma' and c % 64 == 0 and cout >= 256 and cout % 8 == 0
+            and x.numel() * 2 < 2 ** 31
+            and (dy.shape[0] * dy.shape[1] * dy.shape[2]) % 64 == 0 and max(h, wd) < 32768)
+
+
+def _conv_wgrad_lds(dy, x, kh, kw, stride, pad):
+    """dW [Cout, kh, kw, C] (OHWI) = dyᵀ · im2col(x) on the implicit-GEMM kernel (split-K over
+    the output pixels, im2col rows gathered by the DMA)."""
+    n, h, wd, c = x.shape
+    cout = dy.shape[3]
+    L = _native.lib()
+    mpix = dy.shape[0] * dy.shape[1] * dy.shape[2]
+    nk = kh * kw * c
+    # fill ONE wave of <= 256 workgroups (a 257th starts a second round), each split >= 16
+    # K-steps of 64 pixels (profiles/r2_conv/conv3x3_wgrad.log)
+    tiles = ((cout + 255) // 256) * ((nk + 255) // 256)
+    splits = max(1, min(256 // tiles, mpix // (64 * 16), 256)) if tiles < 224 else 1
+    ws = torch.empty((splits, cout, nk), device=x.device, dtype=torch.float32) if splits > 1 else None
+    dw = torch.empty((cout, kh, kw, c), device=x.device, dtype=x.dtype)
+    L.conv_wgrad_lds(dy.data_ptr(), x.data_ptr(), dw.data_ptr(), n, h, wd, c, cout, kh, kw, stride, pad,
+                     _dt(x), splits, _ptr(ws), _stream())
+    return dw
+
+
+# weight gradient of KxK convs: 'mfma' = implicit GEMM on the in-tree kernel, 'miopen' = MIOpen
+_CONV_WGRAD = __import__('os').environ.get('PRA_CONV_WGRAD', 'mfma')
+
+
 class ConvKxKFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, bias, stride, pad):
@@ -1247,14 +1279,18 @@ class ConvKxKFn(torch.autograd.Function):
             wf = w.flip(2, 3).permute(1, 2, 3, 0).reshape(cin, kh * kw * cout).contiguous()
             dx = _conv_lds(dy, wf, None, kh, kw, 1, kh - 1 - pad)
         need_lib_dx = ctx.needs_input_grad[0] and not ours_dx
-        if need_lib_dx or ctx.needs_input_grad[1]:
+        ours_dw = ctx.needs_input_grad[1] and _conv_wgrad_ok(x, dy, cout)
+        if ours_dw:
+            dw = _conv_wgrad_lds(dy, x, kh, kw, stride, pad).permute(0, 3, 1, 2).contiguous()
+        need_lib_dw = ctx.needs_input_grad[1] and not ours_dw
+        if need_lib_dx or need_lib_dw:
             # NCHW-shaped views of the channels-last tensors: MIOpen runs its NHWC kernels
             gx, gw, _ = torch.ops.aten.convolution_backward(
                 dy.permute(0, 3, 1, 2), x.permute(0, 3, 1, 2), w, None, [stride, stride], [pad, pad],
-                [1, 1], False, [0, 0], 1, [need_lib_dx, bool(ctx.needs_input_grad[1]), False])
+                [1, 1], False, [0, 0], 1, [need_lib_dx, need_lib_dw, False])
             if need_lib_dx:
                 dx = gx.permute(0, 2, 3, 1).contiguous()
-            if ctx.needs_input_grad[1]:
+            if need_lib_dw:
                 dw = gw
         if hb and ctx.needs_input_grad[2]:
             db = dy.reshape(-1, cout).sum(0, dtype=torch.float32).to(dy.dtype)

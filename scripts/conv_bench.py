@@ -54,3 +54,24 @@ for hw, cin, cout, s in shapes:
         tot['mi_d'] += d_m
     print(line, flush=True)
 print({k: round(v, 3) for k, v in tot.items()}, flush=True)
+
+# weight gradient: in-tree implicit GEMM vs MIOpen
+tw = {'ours': 0.0, 'miopen': 0.0}
+for hw, cin, cout, s in shapes:
+    x = torch.randn(B, hw, hw, cin, device='cuda', dtype=torch.bfloat16)
+    w = (torch.randn(cout, cin, 3, 3, device='cuda') * 0.05).to(torch.bfloat16)
+    ho = (hw + 2 - 3) // s + 1
+    dy = torch.randn(B, ho, ho, cout, device='cuda', dtype=torch.bfloat16)
+    xc, dyc = x.permute(0, 3, 1, 2), dy.permute(0, 3, 1, 2)
+    wc = w.contiguous(memory_format=torch.channels_last)
+    mi = lambda: torch.ops.aten.convolution_backward(dyc, xc, wc, None, [s, s], [1, 1], [1, 1], False,  # noqa
+                                                     [0, 0], 1, [False, True, False])
+    ou = lambda: K._conv_wgrad_lds(dy, x, 3, 3, s, 1)  # noqa
+    ref = mi()[1].float()
+    got = ou().permute(0, 3, 1, 2).float()
+    err = (got - ref).abs().max().item() / (ref.abs().max().item() + 1e-6)
+    t_o, t_m = t(ou), t(mi)
+    tw['ours'] += t_o
+    tw['miopen'] += t_m
+    print(f"wgrad hw{hw} {cin}->{cout} s{s}: ours {t_o:.3f} ms miopen {t_m:.3f} ms rel err {err:.4f}", flush=True)
+print({k: round(v, 3) for k, v in tw.items()}, flush=True)

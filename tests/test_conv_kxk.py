@@ -45,3 +45,23 @@ def test_conv_kxk_fwd_bwd(case, dtype):
         err = (got.float() - ref).abs().max().item()
         scale = ref.abs().max().item() + 1e-6
         assert err <= 2e-2 * scale + 2e-2, (err, scale)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", [(2, 8, 8, 64, 64, 3, 1, 1), (4, 16, 16, 64, 128, 3, 2, 1),
+                                  (2, 16, 16, 128, 256, 3, 1, 1), (16, 4, 4, 256, 64, 3, 1, 0),
+                                  (1, 16, 8, 64, 72, 5, 1, 2)])
+def test_conv_wgrad_lds(case):
+    n, h, w_, cin, cout, k, s, p = case
+    torch.manual_seed(0)
+    x = torch.randn(n, h, w_, cin, device='cuda', dtype=torch.bfloat16)
+    ho, wo = (h + 2 * p - k) // s + 1, (w_ + 2 * p - k) // s + 1
+    dy = torch.randn(n, ho, wo, cout, device='cuda', dtype=torch.bfloat16)
+    if (n * ho * wo) % 64:
+        pytest.skip("pixel count not a multiple of 64 (MIOpen path)")
+    got = K._conv_wgrad_lds(dy, x, k, k, s, p).permute(0, 3, 1, 2).float()
+    wr = torch.zeros(cout, cin, k, k, device='cuda', requires_grad=True)
+    torch.nn.functional.conv2d(x.float().permute(0, 3, 1, 2), wr, None, s, p).backward(
+        dy.float().permute(0, 3, 1, 2))
+    err = (got - wr.grad).abs().max().item()
+    assert err <= 1e-2 * wr.grad.abs().max().item() + 1e-2, err
