@@ -258,7 +258,19 @@ __global__ void __launch_bounds__(256) sumsq_vec_k(const T* __restrict__ x, floa
   __shared__ float red[16];
   float s = 0.f;
   const size_t nv = n / 8;
-  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < nv; i += (size_t)gridDim.x * blockDim.x) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  // four independent 16-B loads in flight per lane (one at a time left HBM half idle)
+  for (; i + 3 * stride < nv; i += 4 * stride) {
+    float v[4][8];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) load8<T>(x + (i + u * stride) * 8, v[u]);
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += v[u][j] * v[u][j];
+  }
+  for (; i < nv; i += stride) {
     float v[8];
     load8<T>(x + i * 8, v);
 #pragma unroll
@@ -300,9 +312,9 @@ __global__ void __launch_bounds__(256) attn_delta_k(const T* __restrict__ o, con
     for (int i = 0; i < 8; ++i) s += a[i] * g[i];
   }
   for (int off = lpr / 2; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
-  if (valid && sub == 0) {
-    const int64_t h = r % H, bs = r / H, sq = bs % S, b = bs / S;
-    delta[(b * H + h) * S + sq] = s;
+  if (valid && sub == 0) {  // rows < 2^31 (host-checked): 32-bit index math, not 64-bit emulated division
+    const int ri = (int)r, h = ri % H, bs = ri / H, sq = bs % S, b = bs / S;
+    delta[((int64_t)b * H + h) * S + sq] = s;
   }
 }
 
@@ -369,7 +381,7 @@ void pra_sumsq_accum(const void* x, float* out, int64_t n, int dt, hipStream_t s
 void pra_flash_bwd_pre(const void* o, const void* dO, float* delta, int B, int H, int S, int D, int dt,
                        hipStream_t s) {
   int64_t rows = (int64_t)B * S * H;
-  if (!rows) return;
+  if (!rows || rows >= (1ll << 31)) return;
   const int64_t threads = rows * (D / 8);
   PRA_DISPATCH_FLOAT(dt, T, hipLaunchKernelGGL((attn_delta_k<T>), dim3((threads + 255) / 256), dim3(256), 0, s,
                                                (const T*)o, (const T*)dO, delta, B, H, S, D));
