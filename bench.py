@@ -131,6 +131,22 @@ def _timed(step_fn, a, torch, dist, world, dev):
     return dt
 
 
+def _op_profile(step_fn, a, torch, rank):
+    """One extra (untimed) step under torch.profiler with Python stacks: per-op tables grouped
+    by call site (which layer issues each fill / copy / reduce kernel)."""
+    os.makedirs(a.profile_dir, exist_ok=True)
+    acts = [torch.profiler.ProfilerActivity.CPU, torch.profiler.ProfilerActivity.CUDA]
+    with torch.profiler.profile(activities=acts, with_stack=True, record_shapes=True) as prof:
+        step_fn()
+        torch.cuda.synchronize()
+    ka = prof.key_averages(group_by_stack_n=6)
+    with open(os.path.join(a.profile_dir, f'ops_by_stack_rank{rank}.txt'), 'w') as f:
+        f.write(ka.table(sort_by='self_cuda_time_total', row_limit=120, max_name_column_width=60))
+    with open(os.path.join(a.profile_dir, f'ops_rank{rank}.txt'), 'w') as f:
+        f.write(prof.key_averages(group_by_input_shape=True).table(
+            sort_by='self_cuda_time_total', row_limit=150, max_name_column_width=60))
+
+
 def bench_gpt(a, paddle, torch, dist, C, world, rank, dev):
     from paddle_ray_amd.models import gpt_config, GPTForPretraining, gpt_flops_per_token
     from paddle_ray_amd.distributed.sharding import group_sharded_parallel
@@ -159,11 +175,9 @@ def bench_gpt(a, paddle, torch, dist, C, world, rank, dev):
         sched.step()
         losses.append(loss.detach())
 
-    prof = None
-    if a.profile_dir:
-        prof = torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CPU,
-                                                  torch.profiler.ProfilerActivity.CUDA])
     dt = _timed(step, a, torch, dist, world, dev)
+    if a.profile_dir:
+        _op_profile(step, a, torch, rank)
     last_loss = float(losses[-1].item())
     tok = a.micro_batch * a.seq * world * a.steps
     tps = tok / dt

@@ -390,7 +390,7 @@ fwd_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restrict
 template <typename T, int D, bool CAUSAL, int NW>
 __global__ void __launch_bounds__(NW * 64, 2)
 bwd_dq_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restrict__ v, const T* __restrict__ dO,
-              const float* __restrict__ lse, const float* __restrict__ delta, T* __restrict__ dq, int H, int Sq,
+              const T* __restrict__ o, const float* __restrict__ lse, float* __restrict__ delta, T* __restrict__ dq, int H, int Sq,
               int Sk, int64_t qsb, int64_t qss, int64_t qsh, int64_t ksb, int64_t kss, int64_t ksh, int64_t vsb,
               int64_t vss, int64_t vsh, int64_t dqsb, int64_t dqss, int64_t dqsh, float scale, float scale_log2) {
   // double-buffered {K, V} swizzled row images; K^T fragments by transposed reads of K
@@ -424,7 +424,26 @@ bwd_dq_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restr
     }
   }
   const float lse2 = qvalid ? lse[(int64_t)bh * Sq + myq] * LOG2E : INFINITY;
-  const float dlt = qvalid ? delta[(int64_t)bh * Sq + myq] : 0.f;
+  float dlt;
+  if (o) {
+    // delta = rowsum(dO * O) of this lane's query, computed here (the lane already holds its dO
+    // row) and stored for the dK/dV kernel that runs next: no separate preprocess pass
+    const T* ob_ = o + (int64_t)b * Sq * HD + (int64_t)hh * D;
+    const int qq = qvalid ? myq : 0;
+    float part = 0.f;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const typename V8<T>::type of = frag_global<T>(ob_ + (int64_t)qq * HD, 16 * s + 8 * h, qvalid);
+      const u32x4 uo = __builtin_bit_cast(u32x4, of), ud = __builtin_bit_cast(u32x4, df[s]);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        part += lo16<T>(uo[j]) * lo16<T>(ud[j]) + hi16<T>(uo[j]) * hi16<T>(ud[j]);
+    }
+    dlt = part + __shfl_xor(part, 32, 64);
+    if (qvalid && h == 0) delta[(int64_t)bh * Sq + myq] = dlt;
+  } else {
+    dlt = qvalid ? delta[(int64_t)bh * Sq + myq] : 0.f;
+  }
   wait_vmem_all();
 
   f32x16 acc_q[ND];
@@ -818,8 +837,8 @@ static void launch_fwd(const void* q, const void* k, const void* v, void* o, flo
 }
 
 template <typename T, int D, bool C>
-static void launch_bwd(const void* q, const void* k, const void* v, const void* dO, const float* lse,
-                       const float* delta, void* dq, void* dk, void* dv, int B, int H, int Sq, int Sk,
+static void launch_bwd(const void* q, const void* k, const void* v, const void* dO, const void* o, const float* lse,
+                       float* delta, void* dq, void* dk, void* dv, int B, int H, int Sq, int Sk,
                        const int64_t* st, float scale, hipStream_t s) {
   const float sl2 = scale * 1.4426950408889634f;
   {
@@ -829,7 +848,7 @@ static void launch_bwd(const void* q, const void* k, const void* v, const void* 
       auto kern = bwd_dq_kernel<T, D, C, NW>;
       hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       hipLaunchKernelGGL(kern, dim3(B * H, (Sq + NW * 32 - 1) / (NW * 32)), dim3(NW * 64), lds, s, (const T*)q,
-                         (const T*)k, (const T*)v, (const T*)dO, lse, delta, (T*)dq, H, Sq, Sk, st[0], st[1], st[2],
+                         (const T*)k, (const T*)v, (const T*)dO, (const T*)o, lse, delta, (T*)dq, H, Sq, Sk, st[0], st[1], st[2],
                          st[3], st[4], st[5], st[6], st[7], st[8], st[9], st[10], st[11], scale, sl2);
     };
     go(std::integral_constant<int, 8>{});
@@ -869,12 +888,14 @@ int pra_flash_fwd(const void* q, const void* k, const void* v, void* o, float* l
   PRA_FA_DISPATCH(launch_fwd, q, k, v, o, lse, B, H, Sq, Sk, strides, scale, s);
   return 0;
 }
-int pra_flash_bwd(const void* q, const void* k, const void* v, const void* dO, const float* lse, const float* delta,
-                  void* dq, void* dk, void* dv, int B, int H, int Sq, int Sk, int D, const int64_t* strides,
-                  float scale, int causal, int dt, hipStream_t s) {
+// o != nullptr: delta = rowsum(dO * O) is computed inside the dQ kernel (o and dO [B, Sq, H, D]
+// contiguous) and written to `delta` for the dK/dV kernel; o == nullptr: `delta` is an input.
+int pra_flash_bwd(const void* q, const void* k, const void* v, const void* dO, const void* o, const float* lse,
+                  float* delta, void* dq, void* dk, void* dv, int B, int H, int Sq, int Sk, int D,
+                  const int64_t* strides, float scale, int causal, int dt, hipStream_t s) {
   if (!(D == 64 || D == 128) || !(dt == kBF16 || dt == kF16)) return -1;
   if (B * H == 0 || Sq == 0) return 0;
-  PRA_FA_DISPATCH(launch_bwd, q, k, v, dO, lse, delta, dq, dk, dv, B, H, Sq, Sk, strides, scale, s);
+  PRA_FA_DISPATCH(launch_bwd, q, k, v, dO, o, lse, delta, dq, dk, dv, B, H, Sq, Sk, strides, scale, s);
   return 0;
 }
 }

@@ -850,8 +850,9 @@ def _fa_bwd_hip(do, q, k, v, o, lse, causal, scale, dq=None, dk=None, dv=None):
     B, Sq, H, D = q.shape
     Sk = k.shape[1]
     do = do.contiguous()
+    o = o.contiguous()
+    # delta = rowsum(dO * O) is computed by the dQ kernel itself (written for the dK/dV kernel)
     delta = torch.empty((B, H, Sq), device=q.device, dtype=torch.float32)
-    L.flash_bwd_pre(_ptr(o), _ptr(do), _ptr(delta), B, H, Sq, D, _dt(q), _stream())
     if dq is None:
         dq = torch.empty((B, Sq, H, D), device=q.device, dtype=q.dtype)
         dk = torch.empty((B, Sk, H, D), device=q.device, dtype=q.dtype)
@@ -859,7 +860,7 @@ def _fa_bwd_hip(do, q, k, v, o, lse, causal, scale, dq=None, dk=None, dv=None):
     st = [q.stride(0), q.stride(1), q.stride(2), k.stride(0), k.stride(1), k.stride(2),
           v.stride(0), v.stride(1), v.stride(2), dq.stride(0), dq.stride(1), dq.stride(2),
           dk.stride(0), dk.stride(1), dk.stride(2), dv.stride(0), dv.stride(1), dv.stride(2)]
-    L.flash_bwd(_ptr(q), _ptr(k), _ptr(v), _ptr(do), _ptr(lse), _ptr(delta), _ptr(dq), _ptr(dk),
+    L.flash_bwd(_ptr(q), _ptr(k), _ptr(v), _ptr(do), _ptr(o), _ptr(lse), _ptr(delta), _ptr(dq), _ptr(dk),
                 _ptr(dv), B, H, Sq, Sk, D, st, float(scale), int(causal), _dt(q), _stream())
     return dq, dk, dv
 
@@ -1323,7 +1324,7 @@ class LinearFn(torch.autograd.Function):
         x2 = x.reshape(-1, x.shape[-1])
         y = gemm(GEMM_FWD, x2, w, bias=b)
         ctx.save_for_backward(x)
-        ctx.w = w
+        ctx.w, ctx.b = w, b
         ctx.has_b = b is not None
         return y.view(*x.shape[:-1], w.shape[-1])
 
@@ -1345,8 +1346,27 @@ class LinearFn(torch.autograd.Function):
                 gemm(GEMM_TN, x2, dy2, out=g, beta=1)
             else:
                 dw = gemm(GEMM_TN, x2, dy2)
-        db = dy2.sum(0) if ctx.has_b and ctx.needs_input_grad[2] else None
+        db = bias_grad(dy2, ctx.b) if ctx.has_b and ctx.needs_input_grad[2] else None
         return dx, dw, db
+
+
+def bias_grad(dy2, b):
+    """colsum(dy2) for a Linear bias: HIP row-block partial sums + column reduction; added
+    straight into ``b.grad`` when it already exists (returns None then, like the dW path)."""
+    rows, cols = dy2.shape
+    if not (dy2.is_cuda and cols % 8 == 0 and dy2.dtype in _DT and _native.available()):
+        return dy2.sum(0)
+    L = _native.lib()
+    nrb = max(1, min(256, rows // 32))
+    part = torch.empty((nrb, cols), device=dy2.device, dtype=torch.float32)
+    L.colsum_rows(_ptr(dy2), _ptr(part), rows, cols, nrb, _dt(dy2), _stream())
+    g = b.grad if b.is_leaf else None
+    if _acc_grad_ok(g, b, dy2.dtype):
+        L.colsum16_acc(_ptr(part), _ptr(g), nrb, cols, _dt(g), _stream())
+        return None
+    db = torch.empty(cols, device=dy2.device, dtype=dy2.dtype)
+    L.colsum16(_ptr(part), _ptr(db), nrb, cols, _dt(db), _stream())
+    return db
 
 
 def linear(x, w, b=None):

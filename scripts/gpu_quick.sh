@@ -10,6 +10,7 @@ step() { local name=$1 t=$2; shift 2; timeout -k 10 "$t" "$@" > $OUT/$name.log 2
 if [ "${2:-none}" != none ]; then
   step tests 300 python -u -m pytest $2 -m gpu -x -q --timeout 120 --timeout-method thread
 fi
+step fa 120 python -m scripts.fa_one 16 16 1024 128 1 50
 step bench 300 python bench.py --steps 20 --warmup 5 --profile-dir $OUT/ops
 if [ "${3:-1}" = 1 ]; then
   step prof 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o gpt --output-format csv -- python3 bench.py --steps 5 --warmup 2

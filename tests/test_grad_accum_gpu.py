@@ -105,3 +105,28 @@ def test_add_dropout_ln_param_grads_accumulate_in_kernel():
     for got, ref in zip((hb, w, b), refs):
         err = (got.grad.float() - ref.grad).abs().max().item()
         assert err <= 2e-2 * ref.grad.abs().max().item() + 0.5, err
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rows,cols", [(16384, 6144), (1000, 264), (7, 8)])
+def test_linear_bias_grad_colsum_kernel(rows, cols):
+    """Linear bias gradient = colsum(dy) on the HIP row-block kernel, fresh and accumulated
+    into an existing .grad, vs an fp32 reference."""
+    g = torch.Generator(device='cuda').manual_seed(3)
+    dy = torch.randn(rows, cols, device='cuda', dtype=torch.bfloat16, generator=g)
+    b = torch.zeros(cols, device='cuda', dtype=torch.bfloat16, requires_grad=True)
+    ref = dy.float().sum(0)
+    with torch.no_grad():
+        db = K.bias_grad(dy, b)
+    tol = 2e-2 * max(1.0, rows ** 0.5 / 16)
+    torch.testing.assert_close(db.float(), ref, atol=tol, rtol=1e-2)
+    b.grad = torch.ones(cols, device='cuda', dtype=torch.bfloat16)
+    with torch.no_grad():
+        assert K.bias_grad(dy, b) is None
+    torch.testing.assert_close(b.grad.float(), ref + 1, atol=tol, rtol=1e-2)
+    # through autograd: LinearFn's bias gradient
+    x = torch.randn(rows, 16, device='cuda', dtype=torch.bfloat16, generator=g, requires_grad=True)
+    w = torch.randn(16, cols, device='cuda', dtype=torch.bfloat16, generator=g, requires_grad=True)
+    b2 = torch.zeros(cols, device='cuda', dtype=torch.bfloat16, requires_grad=True)
+    K.linear(x, w, b2).backward(dy)
+    torch.testing.assert_close(b2.grad.float(), ref, atol=tol, rtol=1e-2)
