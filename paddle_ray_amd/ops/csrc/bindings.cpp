@@ -51,7 +51,7 @@ void pra_colsum16(const float*, void*, int, int, int, int, hipStream_t);
 int pra_flash_fwd(const void*, const void*, const void*, void*, float*, int, int, int, int, int, const int64_t*, float,
                   int, int, hipStream_t);
 int pra_flash_bwd(const void*, const void*, const void*, const void*, const void*, const float*, float*, void*, void*,
-                  void*, int, int, int, int, int, const int64_t*, float, int, int, hipStream_t);
+                  void*, void*, int, int, int, int, int, const int64_t*, float, int, int, hipStream_t);
 int pra_embedding_fwd(const int64_t*, const void*, void*, int64_t, int, int64_t, int64_t, int, hipStream_t);
 int pra_embedding_bwd(const int64_t*, const int64_t*, const void*, void*, int64_t, int, int64_t, int64_t, int, int,
                       int, hipStream_t);
@@ -244,10 +244,10 @@ PYBIND11_MODULE(_pra_hip, m) {
       throw std::invalid_argument("flash_fwd: unsupported head_dim/dtype");
     check_launch("flash_fwd");
   });
-  m.def("flash_bwd", [](P q, P k, P v, P dO, P o, P lse, P delta, P dq, P dk, P dv, int B, int H, int Sq, int Sk,
-                        int D, std::vector<int64_t> st, float scale, int causal, int dt, P s) {
+  m.def("flash_bwd", [](P q, P k, P v, P dO, P o, P lse, P delta, P dq, P dk, P dv, P dsT, int B, int H, int Sq,
+                        int Sk, int D, std::vector<int64_t> st, float scale, int causal, int dt, P s) {
     if (st.size() != 18) throw std::invalid_argument("flash_bwd: need 18 strides");
-    if (pra_flash_bwd(CV(q), CV(k), CV(v), CV(dO), CV(o), CF(lse), F(delta), V(dq), V(dk), V(dv), B, H, Sq, Sk, D, st.data(),
+    if (pra_flash_bwd(CV(q), CV(k), CV(v), CV(dO), CV(o), CF(lse), F(delta), V(dq), V(dk), V(dv), V(dsT), B, H, Sq, Sk, D, st.data(),
                       scale, causal, dt, S(s)) != 0)
       throw std::invalid_argument("flash_bwd: unsupported head_dim/dtype");
     check_launch("flash_bwd");

@@ -567,13 +567,16 @@ bwd_dq_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restr
 //   A = Q (row-major LDS image), B = K^T (K fragments in registers)
 // dV^T += dO^T P,  dK^T += Q^T dS  (A from transposed images, B = accumulators)
 // ============================================================================
-template <typename T, int D, bool CAUSAL>
+// WDS: also store dS^T (bf16/f16, unscaled) to dsT[bh][key][query] (row pitch Sqp, Skp rows) for
+// bwd_dq_ds_kernel, which then forms dQ = dS K without recomputing S and dP.
+template <typename T, int D, bool CAUSAL, bool WDS>
 __global__ void __launch_bounds__(256, 1)
 bwd_dkdv_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restrict__ v, const T* __restrict__ dO,
                 const float* __restrict__ lse, const float* __restrict__ delta, T* __restrict__ dk,
                 T* __restrict__ dv, int H, int Sq, int Sk, int64_t qsb, int64_t qss, int64_t qsh, int64_t ksb,
                 int64_t kss, int64_t ksh, int64_t vsb, int64_t vss, int64_t vsh, int64_t dksb, int64_t dkss,
-                int64_t dksh, int64_t dvsb, int64_t dvss, int64_t dvsh, float scale, float scale_log2) {
+                int64_t dksh, int64_t dvsb, int64_t dvss, int64_t dvsh, float scale, float scale_log2,
+                T* __restrict__ dsT, int Sqp, int64_t dsbh) {
   // Double-buffered LDS: buffer b = {Q image, dO image} (swizzled rows, read both row-wise and
   // transposed) + lse/delta of the tile's 64 queries. The next tile is written into the idle
   // buffer right after the current tile's MFMAs are issued: one barrier per tile.
@@ -639,6 +642,16 @@ bwd_dkdv_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __res
   __syncthreads();
 
   const LaneOffs<D> lo(lane);
+  // this lane's dS^T row (its key); rows up to the 128-rounded Sk are allocated
+  T* dsrow = WDS ? dsT + (int64_t)bh * dsbh + (int64_t)mykey * Sqp : nullptr;
+  // packed dS fragment of k-step ks (keys on lanes, queries 16ks + 4h + {0..3, 8..11} of the half
+  // starting at query qh): two 8-byte stores into the lane's dS^T row
+  auto store_ds = [&](const typename V8<T>::type& sf, int qh, int ks) {
+    const u32x4 u = __builtin_bit_cast(u32x4, sf);
+    T* p = dsrow + qh + 16 * ks + 4 * h;
+    *reinterpret_cast<u32x2*>(p) = u32x2{u[0], u[1]};
+    *reinterpret_cast<u32x2*>(p + 8) = u32x2{u[2], u[3]};
+  };
   auto tile = [&](int it, auto mask_c) {
     constexpr bool MASK = decltype(mask_c)::value;
     const int buf = it & 1;
@@ -711,6 +724,7 @@ bwd_dkdv_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __res
           }
           const typename V8<T>::type pf = pack_frag<T>(sa[nt], 8 * ks);
           const typename V8<T>::type sf = pack_frag<T>(da[nt], 8 * ks);
+          if constexpr (WDS) store_ds(sf, qs0 + 32 * nt, ks);
 #pragma unroll
           for (int dt = 0; dt < ND; ++dt) {
             acc_v[dt] = mfma<T>(dtr[dt], pf, acc_v[dt]);
@@ -774,6 +788,7 @@ bwd_dkdv_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __res
         }
         const typename V8<T>::type pf = pack_frag<T>(s_acc, 8 * ks);
         const typename V8<T>::type sf = pack_frag<T>(dp_acc, 8 * ks);
+        if constexpr (WDS) store_ds(sf, qs0 + 32 * nt, ks);
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int dt = 0; dt < ND; ++dt) {
@@ -817,6 +832,115 @@ bwd_dkdv_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __res
   }
 }
 
+// ============================================================================
+// backward: dQ = dS K from the dS^T the dK/dV kernel stored (queries on lanes, sweep key tiles).
+// dQ^T += K^T dS^T: A = K^T and B = dS^T both by transposed reads of swizzled row images (K
+// [64 keys][D], dS^T [64 keys][128 queries]) in the same permuted k order, so the operands
+// agree key for key. dS^T entries above the causal diagonal were never written: masked here.
+// ============================================================================
+template <typename T, int D, bool CAUSAL>
+__global__ void __launch_bounds__(256, 2)
+bwd_dq_ds_kernel(const T* __restrict__ k, const T* __restrict__ dsT, T* __restrict__ dq, int H, int Sq, int Sk,
+                 int Sqp, int64_t dsbh, int64_t ksb, int64_t kss, int64_t ksh, int64_t dqsb, int64_t dqss,
+                 int64_t dqsh, float scale) {
+  constexpr int NW = 4, BM = NW * 32, ND = D / 32, BUF = kTile * D + kTile * BM;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  T* img0 = reinterpret_cast<T*>(smem);  // [2][K image 64*D | dS^T image 64*BM]
+
+  const int nqb = gridDim.y;
+  const int qb = CAUSAL ? (nqb - 1 - blockIdx.y) : blockIdx.y;  // heaviest first
+  const int bh = blockIdx.x, b = bh / H, hh = bh % H;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+  const int q0 = qb * BM;
+  const int myq = q0 + wave * 32 + r;
+  const int off = Sk - Sq;
+  const T* kb_ = k + b * ksb + hh * ksh;
+  const T* sb_ = dsT + (int64_t)bh * dsbh + q0;
+
+  f32x16 acc_q[ND];
+#pragma unroll
+  for (int i = 0; i < ND; ++i) acc_q[i] = f32x16{};
+
+  int n_end = Sk;
+  if (CAUSAL) n_end = min(Sk, q0 + BM + off);
+  const int ntiles = n_end > 0 ? (n_end + kTile - 1) / kTile : 0;
+
+  const LaneOffs<D> lo(lane);
+  const LaneOffs<BM> ls(lane);
+  TileRegs<T, D, NW * 64> kr;
+  TileRegs<T, BM, NW * 64> sr;
+  if (ntiles > 0) {
+    kr.load(kb_, kss, 0, Sk);
+    sr.load(sb_, Sqp, 0, Sk);
+    kr.store_swz(img0);
+    sr.store_swz(img0 + kTile * D);
+  }
+  __syncthreads();
+
+  auto tile = [&](int kt, auto mask_c) {
+    constexpr bool MASK = decltype(mask_c)::value;
+    const int k0 = kt * kTile;
+    const T* Ks = img0 + (kt & 1) * BUF;
+    const T* Ss = Ks + kTile * D;
+    if (kt + 1 < ntiles) {
+      kr.load(kb_, kss, k0 + kTile, Sk);
+      sr.load(sb_, Sqp, k0 + kTile, Sk);
+    }
+    int nlive = 2;
+    if constexpr (MASK) {
+      int kmax = Sk - 1;
+      if (CAUSAL) kmax = min(kmax, q0 + wave * 32 + 31 + off);
+      nlive = k0 > kmax ? 0 : (k0 + 32 > kmax ? 1 : 2);
+      nlive = __builtin_amdgcn_readfirstlane(nlive);
+    }
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      if (ks < 2 * nlive) {
+        typename V8<T>::type bf = frag_tr<T, BM>(Ss, ls, wave, ks);
+        if constexpr (MASK && CAUSAL) {
+          // element j <-> key k0 + 16ks + 8(j>>2) + 4h + (j&3); keys past this query are zero
+          u32x4 u = __builtin_bit_cast(u32x4, bf);
+          const int kb0 = k0 + 16 * ks + 4 * h - off;
+#pragma unroll
+          for (int w = 0; w < 4; ++w) {
+            const int key_lo = kb0 + 8 * (w >> 1) + 2 * (w & 1);
+            const uint32_t mlo = key_lo > myq ? 0u : 0xffffu, mhi = key_lo + 1 > myq ? 0u : 0xffff0000u;
+            u[w] &= (mlo | mhi);
+          }
+          bf = as_v8<T>(u);
+        }
+#pragma unroll
+        for (int dt = 0; dt < ND; ++dt) acc_q[dt] = mfma<T>(frag_tr<T, D>(Ks, lo, dt, ks), bf, acc_q[dt]);
+      }
+    }
+    if (kt + 1 < ntiles) {  // idle buffer: last read before the previous barrier
+      T* nb = img0 + ((kt + 1) & 1) * BUF;
+      kr.store_swz(nb);
+      sr.store_swz(nb + kTile * D);
+    }
+    __syncthreads();
+  };
+  int nfull = min(ntiles, Sk / kTile);
+  if (CAUSAL) nfull = min(nfull, (q0 + off + 1) / kTile);
+  if (nfull < 0) nfull = 0;
+  for (int kt = 0; kt < nfull; ++kt) tile(kt, std::false_type{});
+  for (int kt = nfull; kt < ntiles; ++kt) tile(kt, std::true_type{});
+
+  if (myq < Sq) {
+    T* row = dq + (int64_t)b * dqsb + (int64_t)myq * dqss + (int64_t)hh * dqsh;
+#pragma unroll
+    for (int dt = 0; dt < ND; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int d = 32 * dt + 8 * g + 4 * h;
+        uint2 w;
+        w.x = pack2<T>(acc_q[dt][4 * g + 0] * scale, acc_q[dt][4 * g + 1] * scale);
+        w.y = pack2<T>(acc_q[dt][4 * g + 2] * scale, acc_q[dt][4 * g + 3] * scale);
+        *reinterpret_cast<uint2*>(row + d) = w;
+      }
+  }
+}
+
 template <typename T, int D, bool C, int NW>
 static void launch_fwd_nw(const void* q, const void* k, const void* v, void* o, float* lse, int B, int H, int Sq,
                           int Sk, const int64_t* st, float scale, hipStream_t s) {
@@ -838,9 +962,31 @@ static void launch_fwd(const void* q, const void* k, const void* v, void* o, flo
 
 template <typename T, int D, bool C>
 static void launch_bwd(const void* q, const void* k, const void* v, const void* dO, const void* o, const float* lse,
-                       float* delta, void* dq, void* dk, void* dv, int B, int H, int Sq, int Sk,
+                       float* delta, void* dq, void* dk, void* dv, void* dsT, int B, int H, int Sq, int Sk,
                        const int64_t* st, float scale, hipStream_t s) {
   const float sl2 = scale * 1.4426950408889634f;
+  if (dsT) {
+    // dK/dV first (stores dS^T), then dQ = dS K; `delta` is an input here
+    const int Sqp = (Sq + 127) / 128 * 128;
+    const int64_t dsbh = (int64_t)((Sk + 127) / 128 * 128) * Sqp;
+    {
+      const size_t lds = 4 * kTile * D * sizeof(T) + 4 * kTile * sizeof(float);
+      auto kern = bwd_dkdv_kernel<T, D, C, true>;
+      hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      hipLaunchKernelGGL(kern, dim3(B * H, (Sk + 127) / 128), dim3(256), lds, s, (const T*)q, (const T*)k,
+                         (const T*)v, (const T*)dO, lse, delta, (T*)dk, (T*)dv, H, Sq, Sk, st[0], st[1], st[2],
+                         st[3], st[4], st[5], st[6], st[7], st[8], st[12], st[13], st[14], st[15], st[16], st[17],
+                         scale, sl2, (T*)dsT, Sqp, dsbh);
+    }
+    {
+      const size_t lds = 2 * (kTile * D + kTile * 128) * sizeof(T);
+      auto kern = bwd_dq_ds_kernel<T, D, C>;
+      hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      hipLaunchKernelGGL(kern, dim3(B * H, (Sq + 127) / 128), dim3(256), lds, s, (const T*)k, (const T*)dsT,
+                         (T*)dq, H, Sq, Sk, Sqp, dsbh, st[3], st[4], st[5], st[9], st[10], st[11], scale);
+    }
+    return;
+  }
   {
     const size_t lds = 4 * kTile * D * sizeof(T);
     auto go = [&](auto nwc) {
@@ -855,12 +1001,12 @@ static void launch_bwd(const void* q, const void* k, const void* v, const void* 
   }
   {
     const size_t lds = 4 * kTile * D * sizeof(T) + 4 * kTile * sizeof(float);
-    auto kern = bwd_dkdv_kernel<T, D, C>;
+    auto kern = bwd_dkdv_kernel<T, D, C, false>;
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(kern, dim3(B * H, (Sk + 127) / 128), dim3(256), lds, s, (const T*)q, (const T*)k,
                        (const T*)v, (const T*)dO, lse, delta, (T*)dk, (T*)dv, H, Sq, Sk, st[0], st[1], st[2],
                        st[3], st[4], st[5], st[6], st[7], st[8], st[12], st[13], st[14], st[15], st[16], st[17],
-                       scale, sl2);
+                       scale, sl2, (T*)nullptr, 0, (int64_t)0);
   }
 }
 
@@ -890,12 +1036,15 @@ int pra_flash_fwd(const void* q, const void* k, const void* v, void* o, float* l
 }
 // o != nullptr: delta = rowsum(dO * O) is computed inside the dQ kernel (o and dO [B, Sq, H, D]
 // contiguous) and written to `delta` for the dK/dV kernel; o == nullptr: `delta` is an input.
+// dsT != nullptr (requires o == nullptr): dS^T scratch of B*H*roundup(Sk,128)*roundup(Sq,128)
+// elements; dQ = dS K is formed from it instead of recomputing S and dP in a dQ sweep.
 int pra_flash_bwd(const void* q, const void* k, const void* v, const void* dO, const void* o, const float* lse,
-                  float* delta, void* dq, void* dk, void* dv, int B, int H, int Sq, int Sk, int D,
+                  float* delta, void* dq, void* dk, void* dv, void* dsT, int B, int H, int Sq, int Sk, int D,
                   const int64_t* strides, float scale, int causal, int dt, hipStream_t s) {
   if (!(D == 64 || D == 128) || !(dt == kBF16 || dt == kF16)) return -1;
+  if (dsT && o) return -2;
   if (B * H == 0 || Sq == 0) return 0;
-  PRA_FA_DISPATCH(launch_bwd, q, k, v, dO, o, lse, delta, dq, dk, dv, B, H, Sq, Sk, strides, scale, s);
+  PRA_FA_DISPATCH(launch_bwd, q, k, v, dO, o, lse, delta, dq, dk, dv, dsT, B, H, Sq, Sk, strides, scale, s);
   return 0;
 }
 }

@@ -11,6 +11,7 @@ Each op has a ``hip`` kernel (gfx950, ``ops/csrc/*.hip``) and a ``ref`` kernel
   adamw       -> paddle/phi/kernels/gpu/adamw_kernel.cu, fused_adam_kernel.cu
 """
 import math
+import os
 
 import torch
 
@@ -840,6 +841,12 @@ def _fa_fwd_hip(q, k, v, causal, scale):
     return o, lse
 
 
+# dQ path of the flash-attention backward: 'ds' = dQ = dS K from a dS^T scratch written by the
+# dK/dV kernel (up to PRA_FA_DS_MAX_MB of scratch), 'sweep' = a dQ kernel recomputing S and dP
+_FA_DQ = os.environ.get('PRA_FA_DQ', 'ds')
+_FA_DS_MAX_BYTES = int(os.environ.get('PRA_FA_DS_MAX_MB', '4096')) << 20
+
+
 @R.register_kernel('flash_attn_bwd', 'hip', dtypes=_HALF)
 def _fa_bwd_hip(do, q, k, v, o, lse, causal, scale, dq=None, dk=None, dv=None):
     do = _like(do, q.dtype)
@@ -851,8 +858,17 @@ def _fa_bwd_hip(do, q, k, v, o, lse, causal, scale, dq=None, dk=None, dv=None):
     Sk = k.shape[1]
     do = do.contiguous()
     o = o.contiguous()
-    # delta = rowsum(dO * O) is computed by the dQ kernel itself (written for the dK/dV kernel)
     delta = torch.empty((B, H, Sq), device=q.device, dtype=torch.float32)
+    ds_elems = B * H * (-(-Sk // 128) * 128) * (-(-Sq // 128) * 128)
+    if _FA_DQ == 'ds' and ds_elems * 2 <= _FA_DS_MAX_BYTES:
+        # dK/dV kernel stores dS^T (bf16 scratch), dQ = dS K from it: S and dP are not recomputed
+        # for dQ. delta = rowsum(dO * O) comes from the preprocess kernel.
+        L.flash_bwd_pre(_ptr(o), _ptr(do), _ptr(delta), B, H, Sq, D, _dt(q), _stream())
+        ds = torch.empty(ds_elems, device=q.device, dtype=q.dtype)
+        o_arg, ds_arg = 0, _ptr(ds)
+    else:
+        # delta is computed by the dQ sweep kernel itself (written for the dK/dV kernel)
+        o_arg, ds_arg = _ptr(o), 0
     if dq is None:
         dq = torch.empty((B, Sq, H, D), device=q.device, dtype=q.dtype)
         dk = torch.empty((B, Sk, H, D), device=q.device, dtype=q.dtype)
@@ -860,8 +876,8 @@ def _fa_bwd_hip(do, q, k, v, o, lse, causal, scale, dq=None, dk=None, dv=None):
     st = [q.stride(0), q.stride(1), q.stride(2), k.stride(0), k.stride(1), k.stride(2),
           v.stride(0), v.stride(1), v.stride(2), dq.stride(0), dq.stride(1), dq.stride(2),
           dk.stride(0), dk.stride(1), dk.stride(2), dv.stride(0), dv.stride(1), dv.stride(2)]
-    L.flash_bwd(_ptr(q), _ptr(k), _ptr(v), _ptr(do), _ptr(o), _ptr(lse), _ptr(delta), _ptr(dq), _ptr(dk),
-                _ptr(dv), B, H, Sq, Sk, D, st, float(scale), int(causal), _dt(q), _stream())
+    L.flash_bwd(_ptr(q), _ptr(k), _ptr(v), _ptr(do), o_arg, _ptr(lse), _ptr(delta), _ptr(dq), _ptr(dk),
+                _ptr(dv), ds_arg, B, H, Sq, Sk, D, st, float(scale), int(causal), _dt(q), _stream())
     return dq, dk, dv
 
 

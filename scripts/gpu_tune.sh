@@ -8,6 +8,6 @@ step() { local name=$1 t=$2; shift 2; timeout -k 10 "$t" "$@" > $OUT/$name.log 2
          echo "[$name rc=$rc]"; tail -n 3 $OUT/$name.log; if fatal $rc; then exit $rc; fi; }
 step tune 1000 python -u scripts/tune_gemms.py --out $OUT/gemm_gfx950.csv --steps 2
 export PRA_GEMM_TUNING_FILE=$OUT/gemm_gfx950.csv
-step tuned 300 python bench.py --steps 10 --warmup 3
-step untuned 300 python bench.py --steps 10 --warmup 3 --no-tuned-gemms
+step tuned 300 python bench.py --steps 20 --warmup 5
+step untuned 300 python bench.py --steps 20 --warmup 5 --no-tuned-gemms
 exit 0

@@ -428,3 +428,41 @@ def test_memory_efficient_attention_block_diagonal_gpu():
         s = torch.einsum('bmhk,bnhk->bhmn', q.float(), k.float()) / math.sqrt(128) + dense
         ref = torch.einsum('bhmn,bnhk->bmhk', torch.softmax(s, -1), v.float())
         assert (out.float() - ref).abs().max().item() < 2e-2
+
+
+@pytest.mark.parametrize('causal', [True, False])
+@pytest.mark.parametrize('Sq,Sk,D', [(1024, 1024, 128), (300, 130, 128), (130, 300, 64), (520, 520, 64)])
+def test_flash_attention_dq_paths_agree(causal, Sq, Sk, D, monkeypatch):
+    """dQ from the stored dS^T (default) vs the recomputing dQ sweep: both against an fp32
+    reference and against each other. dV must be identical between the paths (dK differs by
+    the delta = rowsum(dO*O) summation order: preprocess kernel vs inside the dQ sweep)."""
+    from paddle_ray_amd.ops import fused as K
+    torch.manual_seed(5)
+    B, H = 2, 4
+    q = torch.randn(B, Sq, H, D, device=DEV, dtype=torch.bfloat16)
+    k = torch.randn(B, Sk, H, D, device=DEV, dtype=torch.bfloat16)
+    v = torch.randn(B, Sk, H, D, device=DEV, dtype=torch.bfloat16)
+    scale = 1.0 / math.sqrt(D)
+    o, lse = K._fa_fwd_hip(q, k, v, causal, scale)
+    do = torch.randn_like(o)
+    grads = {}
+    for path in ('ds', 'sweep'):
+        monkeypatch.setattr(K, '_FA_DQ', path)
+        grads[path] = K._fa_bwd_hip(do, q, k, v, o, lse, causal, scale)
+    qr, kr, vr = (t.detach().float().requires_grad_() for t in (q, k, v))
+    qf, kf, vf = (t.permute(0, 2, 1, 3) for t in (qr, kr, vr))
+    sc = qf @ kf.transpose(-1, -2) * scale
+    if causal:
+        m = torch.ones(Sq, Sk, dtype=torch.bool, device=DEV).triu(Sk - Sq + 1)
+        sc = sc.masked_fill(m, float('-inf'))
+    dead = torch.isinf(sc).all(-1, keepdim=True)
+    pr = torch.softmax(sc.masked_fill(dead, 0.0), -1) * (~dead)
+    (pr @ vf).permute(0, 2, 1, 3).backward(do.float())
+    for path, (dq, dk, dv) in grads.items():
+        for name, g, gr in (('dq', dq, qr.grad), ('dk', dk, kr.grad), ('dv', dv, vr.grad)):
+            err = (g.float() - gr).abs().max().item()
+            assert err < 8e-2 * max(1.0, gr.abs().max().item()), (path, name, err)
+    a, b = grads['ds'], grads['sweep']
+    torch.testing.assert_close(a[2], b[2], atol=0, rtol=0)
+    torch.testing.assert_close(a[1].float(), b[1].float(), atol=2e-2, rtol=2e-2)
+    torch.testing.assert_close(a[0].float(), b[0].float(), atol=2e-2, rtol=2e-2)
