@@ -192,6 +192,43 @@ __device__ __forceinline__ typename V8<T>::type frag_tr(const T* img, const Lane
   return as_v8<T>(u);
 }
 
+// LDS-DMA plan for one swizzled [64][W] image (W = row length in elements): DMA instruction n of
+// a wave writes image elements [512 (n*NWV + wave), +512), lane l the 8 at +8l. Per lane the
+// (row, chunk) that lands there, as a byte offset from the tile's first row.
+template <int W, int NT>
+struct SwzDma {
+  static constexpr int NI = kTile * W * 2 / 1024;  // 1-KB DMA instructions per tile
+  static constexpr int PER = NI / (NT / 64);       // per wave
+  static_assert(NI % (NT / 64) == 0, "DMA split");
+  uint32_t voff[PER];
+  u32x4 rs;
+  __device__ __forceinline__ void init(const void* base, int64_t pitch_el, int nrows, int wave, int lane) {
+#pragma unroll
+    for (int n = 0; n < PER; ++n) {
+      const int E = 512 * (n * (NT / 64) + wave) + 8 * lane;  // image element offset
+      const int rg = E / (8 * W), rem = E % (8 * W), cg = rem / 256, r2 = rem % 256;
+      const int row = rg * 8 + r2 / 32, x = (r2 % 32) / 8;
+      const int ch = cg * 4 + (x ^ ((row >> 2) & 3));
+      voff[n] = (uint32_t)((row * pitch_el + ch * 8) * 2);
+    }
+    const uint64_t bb = (uint64_t)base;
+    rs[0] = __builtin_amdgcn_readfirstlane((uint32_t)bb);
+    rs[1] = __builtin_amdgcn_readfirstlane((uint32_t)(bb >> 32)) & 0xffffu;  // stride 0
+    rs[2] = __builtin_amdgcn_readfirstlane((uint32_t)((int64_t)nrows * pitch_el * 2));  // rows >= nrows read 0
+    rs[3] = 0x00020000u;
+  }
+  // stage the tile whose first row is at byte offset row_bytes into the image at LDS byte address img
+  __device__ __forceinline__ void issue(uint32_t img, uint32_t row_bytes, int wave) {
+#pragma unroll
+    for (int n = 0; n < PER; ++n) {
+      const uint32_t dst = __builtin_amdgcn_readfirstlane(img + 1024u * (n * (NT / 64) + wave));
+      asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff[n] + row_bytes),
+                   "s"(rs), "s"(dst)
+                   : "memory", "m0");
+    }
+  }
+};
+
 // ============================================================================
 // forward
 // ============================================================================
@@ -238,13 +275,19 @@ fwd_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restrict
   if (CAUSAL) n_end = min(Sk, q0 + BM + off);
   const int ntiles = n_end > 0 ? (n_end + kTile - 1) / kTile : 0;
 
-  TileRegs<T, D, NW * 64> kr, vr;
-  if (ntiles > 0) {
-    kr.load(kb_, kss, 0, Sk);
-    vr.load(vb_, vss, 0, Sk);
-    kr.store_swz(img0);
-    vr.store_swz(img0 + kTile * D);
-  }
+  // K/V tiles are staged by LDS-DMA straight into the swizzled images (no VGPR staging and no
+  // ds_write; the buffer range check zero-fills key rows >= Sk)
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
+  SwzDma<D, NW * 64> kd, vd;
+  kd.init(kb_, kss, Sk, wave, lane);
+  vd.init(vb_, vss, Sk, wave, lane);
+  auto stage = [&](int kt) {
+    const uint32_t img = lds0 + (uint32_t)((2 * (kt & 1)) * kTile * D * sizeof(T));
+    kd.issue(img, (uint32_t)((int64_t)kt * kTile * kss * 2), wave);
+    vd.issue(img + kTile * D * sizeof(T), (uint32_t)((int64_t)kt * kTile * vss * 2), wave);
+  };
+  if (ntiles > 0) stage(0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
   const LaneOffs<D> lo(lane);
@@ -254,10 +297,7 @@ fwd_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restrict
     const int k0 = kt * kTile;
     const T* Ks = img0 + (2 * (kt & 1)) * kTile * D;
     const T* Vs = Ks + kTile * D;
-    if (kt + 1 < ntiles) {  // issue next tile's global loads; written after the compute
-      kr.load(kb_, kss, k0 + kTile, Sk);
-      vr.load(vb_, vss, k0 + kTile, Sk);
-    }
+    if (kt + 1 < ntiles) stage(kt + 1);  // idle buffer: last read before the previous barrier
     // masked tiles: 32-key halves beyond every query of THIS wave (causal) or past Sk are
     // skipped by the wave (a wave-uniform branch); all waves still stage and sync
     int nlive = 2;
@@ -350,11 +390,7 @@ fwd_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restrict
       }
     }
     }  // nlive > 0
-    if (kt + 1 < ntiles) {  // idle buffer: last read before the previous barrier
-      T* nb = img0 + (2 * ((kt + 1) & 1)) * kTile * D;
-      kr.store_swz(nb);
-      vr.store_swz(nb + kTile * D);
-    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of tile kt+1 landed
     __syncthreads();
   };
   // tiles [0, nfull) need no mask: every key < Sk and (causal) <= the block's first query
@@ -619,11 +655,17 @@ bwd_dkdv_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __res
   if (CAUSAL) q_begin = max(0, kblk0 - off) / kTile * kTile;
   const int ntiles = q_begin < Sq ? (Sq - q_begin + kTile - 1) / kTile : 0;
 
-  TileRegs<T, D, 256> qr, dr;
+  // Q / dO tiles by LDS-DMA straight into the swizzled images (rows >= Sq read as zero);
+  // the tile's 64 lse / delta values go through registers
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
+  SwzDma<D, 256> qd, dd;
+  qd.init(qb_, qss, Sq, wave, lane);
+  dd.init(dob_, HD, Sq, wave, lane);
   float lreg = 0.f, dreg = 0.f;
   auto load_tile = [&](int qs0) {
-    qr.load(qb_, qss, qs0, Sq);
-    dr.load(dob_, HD, qs0, Sq);
+    const uint32_t img = lds0 + (uint32_t)((2 * (((qs0 - q_begin) / kTile) & 1)) * kTile * D * sizeof(T));
+    qd.issue(img, (uint32_t)((int64_t)qs0 * qss * 2), wave);
+    dd.issue(img + kTile * D * sizeof(T), (uint32_t)((int64_t)qs0 * HD * 2), wave);
     if (threadIdx.x < kTile) {
       const int qq = qs0 + threadIdx.x;
       lreg = qq < Sq ? lse[(int64_t)bh * Sq + qq] : INFINITY;  // scaled at store (no wait here)
@@ -631,26 +673,38 @@ bwd_dkdv_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __res
     }
   };
   auto store_tile = [&](int buf) {
-    qr.store_swz(img0 + (2 * buf) * kTile * D);
-    dr.store_swz(img0 + (2 * buf + 1) * kTile * D);
     if (threadIdx.x < kTile) {
       Lsb[buf * kTile + threadIdx.x] = lreg * LOG2E;
       Dlb[buf * kTile + threadIdx.x] = dreg;
     }
   };
   if (ntiles > 0) { load_tile(q_begin); store_tile(0); }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
   const LaneOffs<D> lo(lane);
-  // this lane's dS^T row (its key); rows up to the 128-rounded Sk are allocated
-  T* dsrow = WDS ? dsT + (int64_t)bh * dsbh + (int64_t)mykey * Sqp : nullptr;
-  // packed dS fragment of k-step ks (keys on lanes, queries 16ks + 4h + {0..3, 8..11} of the half
-  // starting at query qh): two 8-byte stores into the lane's dS^T row
-  auto store_ds = [&](const typename V8<T>::type& sf, int qh, int ks) {
+  // dS^T of one 32-query half goes out through a wave-private [32 keys][32 queries] LDS stage
+  // (80-B row pitch: conflict-free 8-B writes): lanes write their key row's packed fragments,
+  // then read back 16 B each in row order, so the global stores are 64-B row segments (4 lanes
+  // per key row) instead of 32 scattered 16-B pieces per store instruction.
+  // Rows up to the 128-rounded Sk are allocated.
+  constexpr int SP = 80;  // stage row pitch, bytes
+  char* stage = reinterpret_cast<char*>(Dlb + 2 * kTile) + wave * 32 * SP;
+  T* dsw = WDS ? dsT + (int64_t)bh * dsbh + (int64_t)(kblk0 + wave * 32 + (lane >> 2)) * Sqp + 8 * (lane & 3)
+               : nullptr;
+  // packed dS fragment of k-step ks (keys on lanes, queries 16ks + 4h + {0..3, 8..11} of the half)
+  auto store_ds = [&](const typename V8<T>::type& sf, int ks) {
     const u32x4 u = __builtin_bit_cast(u32x4, sf);
-    T* p = dsrow + qh + 16 * ks + 4 * h;
+    char* p = stage + r * SP + (16 * ks + 4 * h) * 2;
     *reinterpret_cast<u32x2*>(p) = u32x2{u[0], u[1]};
-    *reinterpret_cast<u32x2*>(p + 8) = u32x2{u[2], u[3]};
+    *reinterpret_cast<u32x2*>(p + 16) = u32x2{u[2], u[3]};
+  };
+  // the half starting at query qh is complete in the stage: 2 x 16 rows x 64 B to dS^T
+  auto flush_ds = [&](int qh) {
+    const u32x4 a = *reinterpret_cast<const u32x4*>(stage + (lane >> 2) * SP + 16 * (lane & 3));
+    const u32x4 c = *reinterpret_cast<const u32x4*>(stage + (16 + (lane >> 2)) * SP + 16 * (lane & 3));
+    *reinterpret_cast<u32x4*>(dsw + qh) = a;
+    *reinterpret_cast<u32x4*>(dsw + 16 * (int64_t)Sqp + qh) = c;
   };
   auto tile = [&](int it, auto mask_c) {
     constexpr bool MASK = decltype(mask_c)::value;
@@ -724,13 +778,14 @@ bwd_dkdv_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __res
           }
           const typename V8<T>::type pf = pack_frag<T>(sa[nt], 8 * ks);
           const typename V8<T>::type sf = pack_frag<T>(da[nt], 8 * ks);
-          if constexpr (WDS) store_ds(sf, qs0 + 32 * nt, ks);
+          if constexpr (WDS) store_ds(sf, ks);
 #pragma unroll
           for (int dt = 0; dt < ND; ++dt) {
             acc_v[dt] = mfma<T>(dtr[dt], pf, acc_v[dt]);
             acc_k[dt] = mfma<T>(qtr[dt], sf, acc_k[dt]);
           }
         }
+        if constexpr (WDS) flush_ds(qs0 + 32 * nt);
       }
     } else
 #pragma unroll
@@ -788,7 +843,7 @@ bwd_dkdv_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __res
         }
         const typename V8<T>::type pf = pack_frag<T>(s_acc, 8 * ks);
         const typename V8<T>::type sf = pack_frag<T>(dp_acc, 8 * ks);
-        if constexpr (WDS) store_ds(sf, qs0 + 32 * nt, ks);
+        if constexpr (WDS) store_ds(sf, ks);
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int dt = 0; dt < ND; ++dt) {
@@ -796,9 +851,12 @@ bwd_dkdv_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __res
           acc_k[dt] = mfma<T>(qtr[dt], sf, acc_k[dt]);
         }
       }
+      if constexpr (WDS) flush_ds(qs0 + 32 * nt);
     }
-    // the idle buffer was last read before the previous barrier: fill it now
+    // the idle buffer was last read before the previous barrier: its Q/dO DMA was issued at the
+    // top of this tile, lse/delta are written now
     if (it + 1 < ntiles) store_tile(buf ^ 1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   };
   // query tiles that straddle the causal diagonal of this 128-key block (the first ones) or
@@ -835,17 +893,24 @@ bwd_dkdv_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __res
 // ============================================================================
 // backward: dQ = dS K from the dS^T the dK/dV kernel stored (queries on lanes, sweep key tiles).
 // dQ^T += K^T dS^T: A = K^T and B = dS^T both by transposed reads of swizzled row images (K
-// [64 keys][D], dS^T [64 keys][128 queries]) in the same permuted k order, so the operands
+// [64 keys][D], dS^T [64 keys][256 queries]) in the same permuted k order, so the operands
 // agree key for key. dS^T entries above the causal diagonal were never written: masked here.
+// 8 waves x 32 queries share one K tile; both images are filled by LDS-DMA
+// (buffer_load ... lds: no VGPR staging, no ds_write) with per-lane source offsets that
+// realise the swizzle, and the buffer range check zero-fills key rows >= Sk.
 // ============================================================================
 template <typename T, int D, bool CAUSAL>
-__global__ void __launch_bounds__(256, 2)
+__global__ void __launch_bounds__(512, 1)
 bwd_dq_ds_kernel(const T* __restrict__ k, const T* __restrict__ dsT, T* __restrict__ dq, int H, int Sq, int Sk,
                  int Sqp, int64_t dsbh, int64_t ksb, int64_t kss, int64_t ksh, int64_t dqsb, int64_t dqss,
                  int64_t dqsh, float scale) {
-  constexpr int NW = 4, BM = NW * 32, ND = D / 32, BUF = kTile * D + kTile * BM;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  T* img0 = reinterpret_cast<T*>(smem);  // [2][K image 64*D | dS^T image 64*BM]
+  constexpr int NW = 8, NT = NW * 64, BM = NW * 32, ND = D / 32, BUF = kTile * D + kTile * BM;
+  // 3-slot ring, tiles staged two ahead: the per-tile MFMA work (16 per wave) is far shorter
+  // than a DMA round trip, so one tile in flight per CU left the kernel latency-bound
+  constexpr int NBUF = 3;
+  extern __shared__ __attribute__((aligned(1024))) char smem[];
+  T* img0 = reinterpret_cast<T*>(smem);  // [NBUF][K image 64*D | dS^T image 64*BM]
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
 
   const int nqb = gridDim.y;
   const int qb = CAUSAL ? (nqb - 1 - blockIdx.y) : blockIdx.y;  // heaviest first
@@ -854,8 +919,6 @@ bwd_dq_ds_kernel(const T* __restrict__ k, const T* __restrict__ dsT, T* __restri
   const int q0 = qb * BM;
   const int myq = q0 + wave * 32 + r;
   const int off = Sk - Sq;
-  const T* kb_ = k + b * ksb + hh * ksh;
-  const T* sb_ = dsT + (int64_t)bh * dsbh + q0;
 
   f32x16 acc_q[ND];
 #pragma unroll
@@ -867,25 +930,34 @@ bwd_dq_ds_kernel(const T* __restrict__ k, const T* __restrict__ dsT, T* __restri
 
   const LaneOffs<D> lo(lane);
   const LaneOffs<BM> ls(lane);
-  TileRegs<T, D, NW * 64> kr;
-  TileRegs<T, BM, NW * 64> sr;
-  if (ntiles > 0) {
-    kr.load(kb_, kss, 0, Sk);
-    sr.load(sb_, Sqp, 0, Sk);
-    kr.store_swz(img0);
-    sr.store_swz(img0 + kTile * D);
+  SwzDma<D, NT> kd;
+  SwzDma<BM, NT> sd;
+  kd.init(k + b * ksb + hh * ksh, kss, Sk, wave, lane);
+  sd.init(dsT + (int64_t)bh * dsbh + q0, Sqp, Sk, wave, lane);
+  auto stage = [&](int kt) {
+    const uint32_t img = lds0 + (uint32_t)((kt % NBUF) * BUF * sizeof(T));
+    kd.issue(img, (uint32_t)((int64_t)kt * kTile * kss * 2), wave);
+    sd.issue(img + kTile * D * sizeof(T), (uint32_t)((int64_t)kt * kTile * Sqp * 2), wave);
+  };
+  // DMA instructions per wave and stage: vmcnt(PER) leaves the newest stage in flight
+  constexpr int PER = SwzDma<D, NT>::PER + SwzDma<BM, NT>::PER;
+  static_assert(PER < 16, "vmcnt field");
+  if (ntiles > 0) stage(0);
+  if (ntiles > 1) {
+    stage(1);
+    __builtin_amdgcn_s_waitcnt(0x0F70 | PER);  // tile 0 landed, tile 1 in flight
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
 
   auto tile = [&](int kt, auto mask_c) {
     constexpr bool MASK = decltype(mask_c)::value;
     const int k0 = kt * kTile;
-    const T* Ks = img0 + (kt & 1) * BUF;
+    const T* Ks = img0 + (kt % NBUF) * BUF;
     const T* Ss = Ks + kTile * D;
-    if (kt + 1 < ntiles) {
-      kr.load(kb_, kss, k0 + kTile, Sk);
-      sr.load(sb_, Sqp, k0 + kTile, Sk);
-    }
+    const bool ahead = kt + 2 < ntiles;
+    if (ahead) stage(kt + 2);  // slot (kt+2)%3 was last read in tile kt-1, before the last barrier
     int nlive = 2;
     if constexpr (MASK) {
       int kmax = Sk - 1;
@@ -909,15 +981,16 @@ bwd_dq_ds_kernel(const T* __restrict__ k, const T* __restrict__ dsT, T* __restri
           }
           bf = as_v8<T>(u);
         }
+        typename V8<T>::type af[ND];
 #pragma unroll
-        for (int dt = 0; dt < ND; ++dt) acc_q[dt] = mfma<T>(frag_tr<T, D>(Ks, lo, dt, ks), bf, acc_q[dt]);
+        for (int dt = 0; dt < ND; ++dt) af[dt] = frag_tr<T, D>(Ks, lo, dt, ks);
+#pragma unroll
+        for (int dt = 0; dt < ND; ++dt) acc_q[dt] = mfma<T>(af[dt], bf, acc_q[dt]);
       }
     }
-    if (kt + 1 < ntiles) {  // idle buffer: last read before the previous barrier
-      T* nb = img0 + ((kt + 1) & 1) * BUF;
-      kr.store_swz(nb);
-      sr.store_swz(nb + kTile * D);
-    }
+    // this wave's DMA of tile kt+1 landed (tile kt+2's may stay in flight)
+    if (ahead) __builtin_amdgcn_s_waitcnt(0x0F70 | PER);
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   };
   int nfull = min(ntiles, Sk / kTile);
@@ -967,10 +1040,10 @@ static void launch_bwd(const void* q, const void* k, const void* v, const void* 
   const float sl2 = scale * 1.4426950408889634f;
   if (dsT) {
     // dK/dV first (stores dS^T), then dQ = dS K; `delta` is an input here
-    const int Sqp = (Sq + 127) / 128 * 128;
+    const int Sqp = (Sq + 255) / 256 * 256;
     const int64_t dsbh = (int64_t)((Sk + 127) / 128 * 128) * Sqp;
     {
-      const size_t lds = 4 * kTile * D * sizeof(T) + 4 * kTile * sizeof(float);
+      const size_t lds = 4 * kTile * D * sizeof(T) + 4 * kTile * sizeof(float) + 4 * 32 * 80;  // + dS^T stage
       auto kern = bwd_dkdv_kernel<T, D, C, true>;
       hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       hipLaunchKernelGGL(kern, dim3(B * H, (Sk + 127) / 128), dim3(256), lds, s, (const T*)q, (const T*)k,
@@ -979,10 +1052,10 @@ static void launch_bwd(const void* q, const void* k, const void* v, const void* 
                          scale, sl2, (T*)dsT, Sqp, dsbh);
     }
     {
-      const size_t lds = 2 * (kTile * D + kTile * 128) * sizeof(T);
+      const size_t lds = 3 * (kTile * D + kTile * 256) * sizeof(T);
       auto kern = bwd_dq_ds_kernel<T, D, C>;
       hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      hipLaunchKernelGGL(kern, dim3(B * H, (Sq + 127) / 128), dim3(256), lds, s, (const T*)k, (const T*)dsT,
+      hipLaunchKernelGGL(kern, dim3(B * H, (Sq + 255) / 256), dim3(512), lds, s, (const T*)k, (const T*)dsT,
                          (T*)dq, H, Sq, Sk, Sqp, dsbh, st[3], st[4], st[5], st[9], st[10], st[11], scale);
     }
     return;
@@ -1036,7 +1109,7 @@ int pra_flash_fwd(const void* q, const void* k, const void* v, void* o, float* l
 }
 // o != nullptr: delta = rowsum(dO * O) is computed inside the dQ kernel (o and dO [B, Sq, H, D]
 // contiguous) and written to `delta` for the dK/dV kernel; o == nullptr: `delta` is an input.
-// dsT != nullptr (requires o == nullptr): dS^T scratch of B*H*roundup(Sk,128)*roundup(Sq,128)
+// dsT != nullptr (requires o == nullptr): dS^T scratch of B*H*roundup(Sk,128)*roundup(Sq,256)
 // elements; dQ = dS K is formed from it instead of recomputing S and dP in a dQ sweep.
 int pra_flash_bwd(const void* q, const void* k, const void* v, const void* dO, const void* o, const float* lse,
                   float* delta, void* dq, void* dk, void* dv, void* dsT, int B, int H, int Sq, int Sk, int D,

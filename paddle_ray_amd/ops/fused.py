@@ -859,7 +859,7 @@ def _fa_bwd_hip(do, q, k, v, o, lse, causal, scale, dq=None, dk=None, dv=None):
     do = do.contiguous()
     o = o.contiguous()
     delta = torch.empty((B, H, Sq), device=q.device, dtype=torch.float32)
-    ds_elems = B * H * (-(-Sk // 128) * 128) * (-(-Sq // 128) * 128)
+    ds_elems = B * H * (-(-Sk // 128) * 128) * (-(-Sq // 256) * 256)
     if _FA_DQ == 'ds' and ds_elems * 2 <= _FA_DS_MAX_BYTES:
         # dK/dV kernel stores dS^T (bf16 scratch), dQ = dS K from it: S and dP are not recomputed
         # for dQ. delta = rowsum(dO * O) comes from the preprocess kernel.
