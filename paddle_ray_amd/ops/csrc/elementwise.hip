@@ -298,13 +298,15 @@ __global__ void __launch_bounds__(256) sumsq_vec_k(const T* __restrict__ x, floa
   const size_t nv = n / 8;
   const size_t stride = (size_t)gridDim.x * blockDim.x;
   size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-  // four independent 16-B loads in flight per lane (one at a time left HBM half idle)
-  for (; i + 3 * stride < nv; i += 4 * stride) {
-    float v[4][8];
+  // eight independent 16-B loads in flight per lane (one at a time left HBM half idle); the
+  // grid is capped at one workgroup per CU so the closing same-address atomics stay few
+  // (thousands of them serialise at the memory-side atomic unit)
+  for (; i + 7 * stride < nv; i += 8 * stride) {
+    float v[8][8];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) load8<T>(x + (i + u * stride) * 8, v[u]);
+    for (int u = 0; u < 8; ++u) load8<T>(x + (i + u * stride) * 8, v[u]);
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
+    for (int u = 0; u < 8; ++u)
 #pragma unroll
       for (int j = 0; j < 8; ++j) s += v[u][j] * v[u][j];
   }
@@ -408,7 +410,7 @@ void pra_sumsq_accum(const void* x, float* out, int64_t n, int dt, hipStream_t s
   if (!n) return;
   if (((uintptr_t)x & 15) == 0) {
     int g = grid_for((size_t)n / 8);
-    if (g > 2048) g = 2048;
+    if (g > 256) g = 256;
     PRA_DISPATCH_FLOAT(dt, T, hipLaunchKernelGGL((sumsq_vec_k<T>), dim3(g), dim3(256), 0, s, (const T*)x, out,
                                                  (size_t)n));
   } else {

@@ -129,30 +129,42 @@ __global__ void __launch_bounds__(256) adl_bwd_k(const T* __restrict__ dy, const
                                                  float scale, uint64_t seed, uint64_t offset) {
   extern __shared__ __attribute__((aligned(16))) float red_lds[];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  float aw[C][8], ab[C][8], ah[C][8], wv[C][8];
+  float aw[C][8], ab[C][8], ah[C][8];
 #pragma unroll
-  for (int c = 0; c < C; ++c) {
-    const int idx = (c * 64 + lane) * 8;
+  for (int c = 0; c < C; ++c)
 #pragma unroll
-    for (int i = 0; i < 8; ++i) { aw[c][i] = 0.f; ab[c][i] = 0.f; ah[c][i] = 0.f; wv[c][i] = 1.f; }
-    if (idx < cols && w) load8<W>(w + idx, wv[c]);
-  }
+    for (int i = 0; i < 8; ++i) { aw[c][i] = 0.f; ab[c][i] = 0.f; ah[c][i] = 0.f; }
   for (int row = blockIdx.x * 4 + wid; row < rows; row += gridDim.x * 4) {
     const size_t base = (size_t)row * cols;
     const float mu = mean[row], rs = rstd[row];
-    float xh[C][8], g[C][8];
+    float xh[C][8], g[C][8], e[C][8];
+    // the residual's incoming grad is loaded with r / dy (not after the row reductions): one
+    // memory round trip per row instead of two. The LN weight is re-read per row (L1/L2-resident)
+    // instead of pinned in registers, which pays for e[][] at the same occupancy.
+    if (dr_out) {
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        const int idx = (c * 64 + lane) * 8;
+        if (idx < cols) load8<T>(dr_out + base + idx, e[c]);
+      }
+    }
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int c = 0; c < C; ++c) {
       const int idx = (c * 64 + lane) * 8;
       if (idx < cols) {
-        float rv[8], dv[8];
+        float rv[8], dv[8], wv[8];
         load8<T>(r + base + idx, rv);
         load8<T>(dy + base + idx, dv);
+        if (w) load8<W>(w + idx, wv);
+        else {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) wv[i] = 1.f;
+        }
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
           xh[c][i] = (rv[i] - mu) * rs;
-          g[c][i] = dv[i] * wv[c][i];
+          g[c][i] = dv[i] * wv[i];
           s1 += g[c][i] * xh[c][i];
           s2 += g[c][i];
           aw[c][i] += dv[i] * xh[c][i];
@@ -169,10 +181,8 @@ __global__ void __launch_bounds__(256) adl_bwd_k(const T* __restrict__ dy, const
 #pragma unroll
         for (int i = 0; i < 8; ++i) o[i] = (g[c][i] - c2 - xh[c][i] * c1) * rs;
         if (dr_out) {
-          float e[8];
-          load8<T>(dr_out + base + idx, e);
 #pragma unroll
-          for (int i = 0; i < 8; ++i) o[i] += e[i];
+          for (int i = 0; i < 8; ++i) o[i] += e[c][i];
         }
         store8<T>(dr_in + base + idx, o);
         if (dh) {

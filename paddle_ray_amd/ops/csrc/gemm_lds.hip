@@ -440,19 +440,34 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_lds_kernel(const uint16_t* __r
   // with step kt+2 (DMA) and computes (kt,1) from F1 while reading (kt+1,0) into F0.
   // (measured: issuing B of step kt+1 under half 0 of step kt instead, so both halves carry DMA,
   // was 8-15 % slower on every GPT shape: half a K-step does not cover the DMA latency)
+  // (non-split launches pass splits = 0 only for the PRA_GEMM_ABLATE=nodma timing ablation)
   const bool dmaon = SPLIT || splits != 0;
-  for (int kt = 0; kt < nk; ++kt) {
+  // STEADY: kt + 2 < nk and DMA on, known at compile time -> the K-step body has no branches
+  // (the generic body tests "read next half" / "stage step kt+2" around every MFMA segment: ~16
+  // wave-uniform branches per K-step in the steady state). The last two steps run the generic body.
+  auto kstep = [&](int kt, auto steady_c) {
+    constexpr bool STEADY = decltype(steady_c)::value;
     half(fa0, fb0, fa1, fb1, true, kt, 1, false, 0, false, 0);
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): (kt,1) fragments landed; slot kt reads done
-    if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // step kt+1 landed (this wave)
+    if (STEADY || kt + 1 < nk) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // step kt+1 landed (this wave)
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    // (non-split launches pass splits = 0 only for the PRA_GEMM_ABLATE=nodma timing ablation)
-    half(fa1, fb1, fa0, fb0, kt + 1 < nk, kt + 1, 0, kt + 2 < nk && dmaon, kt + 2, kt + 2 < nk && dmaon, kt + 2);
+    if constexpr (STEADY) {
+      half(fa1, fb1, fa0, fb0, true, kt + 1, 0, true, kt + 2, true, kt + 2);
+    } else {
+      half(fa1, fb1, fa0, fb0, kt + 1 < nk, kt + 1, 0, kt + 2 < nk && dmaon, kt + 2, kt + 2 < nk && dmaon, kt + 2);
+    }
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_waitcnt(0xC07F);  // (kt+1,0) fragments landed
-  }
+  };
+  int kt = 0;
+  // (the implicit-GEMM convolutions keep the generic body: their gather state already sits at
+  // the register limit and a second body copy made them spill)
+  if constexpr (!CONV && !CONVW)
+    if (dmaon)
+      for (; kt + 2 < nk; ++kt) kstep(kt, std::true_type{});
+  for (; kt < nk; ++kt) kstep(kt, std::false_type{});
   }  // nk > 0
 
   if (SPLIT) {
