@@ -347,7 +347,10 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_lds_kernel(const uint16_t* __r
   const int tm = first_m + (pid % group) % gm, tn = (pid % group) / gm;
   const int m0 = tm * BM, n0 = tn * BN;
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wr = wave / WC, wc = wave % WC;
+  // wave index as an SGPR value: the per-wave DMA destinations (M0) and fragment bases are then
+  // scalar arithmetic (no v_readfirstlane + s_nop per LDS-DMA issue)
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6),
+            wr = wave / WC, wc = wave % WC;
 
   typename std::conditional<CONV, ConvDmaA<NT, NDA>, Dma<AK, NT, NDA>>::type da;
   typename std::conditional<CONVW, ConvDmaBW<NT, NDB>, Dma<BK, NT, NDB>>::type db;
@@ -686,6 +689,8 @@ void launch_e(const void* A, const void* B, const void* bias, void* C, void* Z, 
   }
   // (measured: front-loading the step's DMA into the first 2 / 4 segments of the half instead of
   // one per segment was 1-10 % slower on every GPT shape)
+  // (measured: one static s_setprio 1 for waves 4-7 instead of the per-segment flips is neutral,
+  // 11.65 vs 11.60 ms over the 15 GPT shapes, 131.2 vs 131.1-131.3 ms per GPT step)
 #define PRA_GEMM_LAUNCH(CFG, BETA_)                                                                         \
   gemm_lds_kernel<T, CFG, AK, BK, E, BETA_, false><<<tiles, CFG::NT, 0, s>>>(pa, pb, pbias, pc, pz, colsum, M, N, K, \
                                                                            lda, ldb, ldc, ldz, ablate, nullptr)
