@@ -47,6 +47,7 @@ def ref_mm(layout, a, b):
 
 def ours(layout, a, b, c, M, N, K, bias=None, z=None, colsum=None, epi=0, beta=0):
     from paddle_ray_amd.ops import fused as F
+    F._GEMM_MODE = 'mfma'  # the in-tree kernel on every layout (auto routes dy·Wᵀ to hipBLASLt)
     r = F._gemm_hip(layout, a, b, out=c)  # includes the split-K choice for small grids
     assert r is not None
 
