@@ -715,32 +715,22 @@ bwd_dkdv_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __res
     const float* Dl = Dlb + buf * kTile;
     const int qs0 = q_begin + it * kTile;
     if (it + 1 < ntiles) load_tile(qs0 + kTile);
-    // masked tiles: a 32-query half whose every query precedes this wave's first key (causal)
-    // or lies past Sq contributes nothing for the wave — skipped (wave-uniform branch)
-    int nt_lo = 0, nt_hi = 2;
-    if constexpr (MASK) {
-      const int kw0 = kblk0 + wave * 32;
-      if (CAUSAL) {
-        while (nt_lo < 2 && kw0 > qs0 + 32 * nt_lo + 31 + off) ++nt_lo;
-      }
-      while (nt_hi > nt_lo && qs0 + 32 * (nt_hi - 1) >= Sq) --nt_hi;
-      nt_lo = __builtin_amdgcn_readfirstlane(nt_lo);
-      nt_hi = __builtin_amdgcn_readfirstlane(nt_hi);
-    }
-    if constexpr (!MASK) {
-      // software-pipelined unmasked tile: S/dP of BOTH 32-query halves first, then each
-      // half's softmax VALU sits behind the other half's MFMAs in program order (nothing
-      // pins the order there), so the matrix pipe keeps running while the exps issue
+    {
+      // software-pipelined tile: S/dP of BOTH 32-query halves first, then each half's softmax
+      // VALU sits behind the other half's MFMAs in program order (nothing pins the order there),
+      // so the matrix pipe keeps running while the exps issue. Masked tiles (causal diagonal,
+      // Sq tail) run the same body with a per-element mask: a wave whose half is entirely
+      // masked still computes it (P = dS = 0), which costs nothing on the tile's critical path
+      // -- the barrier waits for the wave that has both halves live -- while the former
+      // unpipelined masked body ran ~2.5x the VALU per tile on 20-25 % of the causal tiles.
+      // dP starts from zero (MFMA with a zero C operand) and delta is subtracted in the softmax
+      // VALU: seeding the accumulator with -delta cost a v_xor + a v_accvgpr_write per element
+      // (the S/dP accumulators live in AGPRs at this register pressure)
       f32x16 sa[2], da[2];
 #pragma unroll
       for (int nt = 0; nt < 2; ++nt) {
         sa[nt] = f32x16{};
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const float4 d4 = *reinterpret_cast<const float4*>(Dl + 32 * nt + 8 * g + 4 * h);
-          da[nt][4 * g + 0] = -d4.x; da[nt][4 * g + 1] = -d4.y;
-          da[nt][4 * g + 2] = -d4.z; da[nt][4 * g + 3] = -d4.w;
-        }
+        da[nt] = f32x16{};
         typename V8<T>::type qfr[NS], dfr[NS];
 #pragma unroll
         for (int s = 0; s < NS; ++s) {
@@ -759,13 +749,18 @@ bwd_dkdv_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __res
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const float4 l4 = *reinterpret_cast<const float4*>(Ls + 32 * nt + 8 * g + 4 * h);
-          const float la[4] = {l4.x, l4.y, l4.z, l4.w};
+          const float4 d4 = *reinterpret_cast<const float4*>(Dl + 32 * nt + 8 * g + 4 * h);
+          const float la[4] = {l4.x, l4.y, l4.z, l4.w}, dl[4] = {d4.x, d4.y, d4.z, d4.w};
 #pragma unroll
           for (int c = 0; c < 4; ++c) {
             const int i = 4 * g + c;
-            const float p = fexp2(fmaf(sa[nt][i], scale_log2, -la[c]));
+            float p = fexp2(fmaf(sa[nt][i], scale_log2, -la[c]));
+            if constexpr (MASK) {
+              const int qq = qs0 + 32 * nt + 8 * g + 4 * h + c;
+              if (qq >= Sq || (CAUSAL && mykey > qq + off)) p = 0.f;
+            }
             sa[nt][i] = p;
-            da[nt][i] = p * da[nt][i];
+            da[nt][i] = p * (da[nt][i] - dl[c]);
           }
         }
 #pragma unroll
@@ -787,71 +782,6 @@ bwd_dkdv_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __res
         }
         if constexpr (WDS) flush_ds(qs0 + 32 * nt);
       }
-    } else
-#pragma unroll
-    for (int nt = 0; nt < 2; ++nt) {  // two 32-query halves of the tile
-      if (nt < nt_lo || nt >= nt_hi) continue;
-      // rows (queries) in registers: q = 32nt + acc_row(i,h); the dP chain starts at -delta
-      f32x16 s_acc = f32x16{}, dp_acc;
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const float4 d4 = *reinterpret_cast<const float4*>(Dl + 32 * nt + 8 * g + 4 * h);
-        dp_acc[4 * g + 0] = -d4.x; dp_acc[4 * g + 1] = -d4.y;
-        dp_acc[4 * g + 2] = -d4.z; dp_acc[4 * g + 3] = -d4.w;
-      }
-      {
-        // all 2*NS row fragments in flight before the MFMAs (one wave per SIMD here: an LDS
-        // round trip per MFMA would be fully exposed)
-        typename V8<T>::type qfr[NS], dfr[NS];
-#pragma unroll
-        for (int s = 0; s < NS; ++s) {
-          qfr[s] = frag_rows<T, D>(Qs, lo, nt, s);
-          dfr[s] = frag_rows<T, D>(Ds, lo, nt, s);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int s = 0; s < NS; ++s) {
-          s_acc = mfma<T>(qfr[s], kf[s], s_acc);
-          dp_acc = mfma<T>(dfr[s], vf[s], dp_acc);
-        }
-      }
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const float4 l4 = *reinterpret_cast<const float4*>(Ls + 32 * nt + 8 * g + 4 * h);
-        const float la[4] = {l4.x, l4.y, l4.z, l4.w};
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          const int i = 4 * g + c;
-          float p = fexp2(fmaf(s_acc[i], scale_log2, -la[c]));
-          if constexpr (MASK) {
-            const int qq = qs0 + 32 * nt + 8 * g + 4 * h + c;
-            if (qq >= Sq || (CAUSAL && mykey > qq + off)) p = 0.f;
-          }
-          s_acc[i] = p;
-          dp_acc[i] = p * dp_acc[i];
-        }
-      }
-      // dV^T += dO^T P ; dK^T += Q^T dS   (k = queries of this 32-half, 2 steps of 16);
-      // the transposed operands come straight from the row images (ds_read_b64_tr_b16)
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        typename V8<T>::type dtr[ND], qtr[ND];
-#pragma unroll
-        for (int dt = 0; dt < ND; ++dt) {
-          dtr[dt] = frag_tr<T, D>(Ds, lo, dt, 2 * nt + ks);
-          qtr[dt] = frag_tr<T, D>(Qs, lo, dt, 2 * nt + ks);
-        }
-        const typename V8<T>::type pf = pack_frag<T>(s_acc, 8 * ks);
-        const typename V8<T>::type sf = pack_frag<T>(dp_acc, 8 * ks);
-        if constexpr (WDS) store_ds(sf, ks);
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int dt = 0; dt < ND; ++dt) {
-          acc_v[dt] = mfma<T>(dtr[dt], pf, acc_v[dt]);
-          acc_k[dt] = mfma<T>(qtr[dt], sf, acc_k[dt]);
-        }
-      }
-      if constexpr (WDS) flush_ds(qs0 + 32 * nt);
     }
     // the idle buffer was last read before the previous barrier: its Q/dO DMA was issued at the
     // top of this tile, lse/delta are written now
