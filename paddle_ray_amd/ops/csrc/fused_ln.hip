@@ -15,6 +15,7 @@
 // Parity: paddle/fluid/operators/fused/fused_dropout_helper.h,
 // fused_layernorm_residual_dropout_bias.h (FusedBiasDropoutResidualLayerNorm).
 #include "common.h"
+#include <stdlib.h>
 
 namespace pra {
 
@@ -119,14 +120,19 @@ __global__ void __launch_bounds__(256) adl_fwd_k(const T* __restrict__ x, const 
 
 // dy: grad of y; dr_out: extra grad arriving at r from its other consumer (may be null)
 // outputs: dr_in (= total grad of r = grad of x), dh (= dr_in * keep * scale) if h path
-template <typename T, typename W, int C>
-__global__ void __launch_bounds__(256) adl_bwd_k(const T* __restrict__ dy, const T* __restrict__ dr_out,
-                                                 const T* __restrict__ r, const W* __restrict__ w,
-                                                 const float* __restrict__ mean, const float* __restrict__ rstd,
-                                                 T* __restrict__ dr_in, T* __restrict__ dh,
-                                                 float* __restrict__ pw, float* __restrict__ pb,
-                                                 float* __restrict__ pbias, int rows, int cols, uint32_t thr,
-                                                 float scale, uint64_t seed, uint64_t offset) {
+// TWO = false: one pass per row, xh / dy*w / dr_out held in registers across the row reductions
+// (248 VGPRs: 2 waves per SIMD). TWO = true: the row is read twice -- pass 1 only accumulates
+// the row sums and the dW / dB partials, pass 2 re-reads r and dy (L2-resident: the wave just
+// read them) with dr_out and writes the outputs -- so nothing row-sized stays live across the
+// reductions and the kernel fits 3 waves per SIMD (more HBM reads in flight per CU).
+template <typename T, typename W, int C, bool TWO>
+__device__ __forceinline__ void adl_bwd_body(const T* __restrict__ dy, const T* __restrict__ dr_out,
+                                             const T* __restrict__ r, const W* __restrict__ w,
+                                             const float* __restrict__ mean, const float* __restrict__ rstd,
+                                             T* __restrict__ dr_in, T* __restrict__ dh,
+                                             float* __restrict__ pw, float* __restrict__ pb,
+                                             float* __restrict__ pbias, int rows, int cols, uint32_t thr,
+                                             float scale, uint64_t seed, uint64_t offset) {
   extern __shared__ __attribute__((aligned(16))) float red_lds[];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   float aw[C][8], ab[C][8], ah[C][8];
@@ -137,11 +143,11 @@ __global__ void __launch_bounds__(256) adl_bwd_k(const T* __restrict__ dy, const
   for (int row = blockIdx.x * 4 + wid; row < rows; row += gridDim.x * 4) {
     const size_t base = (size_t)row * cols;
     const float mu = mean[row], rs = rstd[row];
-    float xh[C][8], g[C][8], e[C][8];
-    // the residual's incoming grad is loaded with r / dy (not after the row reductions): one
-    // memory round trip per row instead of two. The LN weight is re-read per row (L1/L2-resident)
-    // instead of pinned in registers, which pays for e[][] at the same occupancy.
-    if (dr_out) {
+    float xh[TWO ? 1 : C][8], g[TWO ? 1 : C][8], e[TWO ? 1 : C][8];
+    // (one pass) the residual's incoming grad is loaded with r / dy (not after the row
+    // reductions): one memory round trip per row instead of two. The LN weight is re-read per
+    // row (L1/L2-resident) instead of pinned in registers, which pays for e[][].
+    if (!TWO && dr_out) {
 #pragma unroll
       for (int c = 0; c < C; ++c) {
         const int idx = (c * 64 + lane) * 8;
@@ -163,11 +169,11 @@ __global__ void __launch_bounds__(256) adl_bwd_k(const T* __restrict__ dy, const
         }
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-          xh[c][i] = (rv[i] - mu) * rs;
-          g[c][i] = dv[i] * wv[i];
-          s1 += g[c][i] * xh[c][i];
-          s2 += g[c][i];
-          aw[c][i] += dv[i] * xh[c][i];
+          const float x_ = (rv[i] - mu) * rs, g_ = dv[i] * wv[i];
+          if constexpr (!TWO) { xh[c][i] = x_; g[c][i] = g_; }
+          s1 += g_ * x_;
+          s2 += g_;
+          aw[c][i] += dv[i] * x_;
           ab[c][i] += dv[i];
         }
       }
@@ -178,11 +184,28 @@ __global__ void __launch_bounds__(256) adl_bwd_k(const T* __restrict__ dy, const
       const int idx = (c * 64 + lane) * 8;
       if (idx < cols) {
         float o[8];
+        if constexpr (TWO) {
+          float rv[8], dv[8], wv[8], ev[8];
+          load8<T>(r + base + idx, rv);
+          load8<T>(dy + base + idx, dv);
+          if (dr_out) load8<T>(dr_out + base + idx, ev);
+          if (w) load8<W>(w + idx, wv);
+          else {
 #pragma unroll
-        for (int i = 0; i < 8; ++i) o[i] = (g[c][i] - c2 - xh[c][i] * c1) * rs;
-        if (dr_out) {
+            for (int i = 0; i < 8; ++i) wv[i] = 1.f;
+          }
 #pragma unroll
-          for (int i = 0; i < 8; ++i) o[i] += e[c][i];
+          for (int i = 0; i < 8; ++i) {
+            o[i] = (dv[i] * wv[i] - c2 - (rv[i] - mu) * rs * c1) * rs;
+            if (dr_out) o[i] += ev[i];
+          }
+        } else {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) o[i] = (g[c][i] - c2 - xh[c][i] * c1) * rs;
+          if (dr_out) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) o[i] += e[c][i];
+          }
         }
         store8<T>(dr_in + base + idx, o);
         if (dh) {
@@ -220,6 +243,23 @@ __global__ void __launch_bounds__(256) adl_bwd_k(const T* __restrict__ dy, const
     }
   }
 }
+
+#define ADL_BWD_ARGS                                                                                         \
+  const T* __restrict__ dy, const T* __restrict__ dr_out, const T* __restrict__ r, const W* __restrict__ w,  \
+      const float* __restrict__ mean, const float* __restrict__ rstd, T* __restrict__ dr_in, T* __restrict__ dh, \
+      float* __restrict__ pw, float* __restrict__ pb, float* __restrict__ pbias, int rows, int cols, uint32_t thr, \
+      float scale, uint64_t seed, uint64_t offset
+template <typename T, typename W, int C>
+__global__ void __launch_bounds__(256) adl_bwd_k(ADL_BWD_ARGS) {
+  adl_bwd_body<T, W, C, false>(dy, dr_out, r, w, mean, rstd, dr_in, dh, pw, pb, pbias, rows, cols, thr, scale, seed,
+                               offset);
+}
+template <typename T, typename W, int C>
+__global__ void __launch_bounds__(256, 3) adl_bwd2_k(ADL_BWD_ARGS) {
+  adl_bwd_body<T, W, C, true>(dy, dr_out, r, w, mean, rstd, dr_in, dh, pw, pb, pbias, rows, cols, thr, scale, seed,
+                              offset);
+}
+#undef ADL_BWD_ARGS
 
 // out[c] = sum_b part[b][c]; workgroup = 16 columns x 16 row slices
 template <typename O>
@@ -323,10 +363,16 @@ void pra_adl_bwd(const void* dy, const void* dr_out, const void* r, const void* 
   uint32_t thr = (dh && p > 0.f) ? (uint32_t)(p * 65536.f + 0.5f) : 0u;
   float scale = thr ? 1.f / (1.f - p) : 1.f;
   size_t lds = (size_t)4 * cols * sizeof(float);
+  static const bool two = !(getenv("PRA_ADL_BWD") && atoi(getenv("PRA_ADL_BWD")) == 1);
 #define K_BWD(CC, TX, TW)                                                                                  \
-  hipLaunchKernelGGL((adl_bwd_k<TX, TW, CC>), dim3(nblk), dim3(256), lds, s, (const TX*)dy, (const TX*)dr_out, \
-                     (const TX*)r, (const TW*)w, mean, rstd, (TX*)dr_in, (TX*)dh, pw, pb, pbias, rows, cols, thr, \
-                     scale, seed, offset)
+  if (two)                                                                                                 \
+    hipLaunchKernelGGL((adl_bwd2_k<TX, TW, CC>), dim3(nblk), dim3(256), lds, s, (const TX*)dy, (const TX*)dr_out, \
+                       (const TX*)r, (const TW*)w, mean, rstd, (TX*)dr_in, (TX*)dh, pw, pb, pbias, rows, cols, thr, \
+                       scale, seed, offset);                                                               \
+  else                                                                                                     \
+    hipLaunchKernelGGL((adl_bwd_k<TX, TW, CC>), dim3(nblk), dim3(256), lds, s, (const TX*)dy, (const TX*)dr_out, \
+                       (const TX*)r, (const TW*)w, mean, rstd, (TX*)dr_in, (TX*)dh, pw, pb, pbias, rows, cols, thr, \
+                       scale, seed, offset)
   PRA_DISPATCH_FLOAT(dt, TX, {
     if (dtw == dt) { ADL_DISPATCH_C(cols, K_BWD, TX, TX); }
     else { ADL_DISPATCH_C(cols, K_BWD, TX, float); }

@@ -98,7 +98,8 @@ def _adl_ok(cols):
 
 
 def _adl_nblk(rows):
-    return max(1, min(512, (rows + 7) // 8))
+    # 768 workgroups of 4 waves = 3 waves per SIMD on 256 CUs (the two-pass backward's occupancy)
+    return max(1, min(768, (rows + 7) // 8))
 
 
 @R.register_kernel('layer_norm_fwd', 'hip', dtypes=_FLOATS)
