@@ -58,6 +58,7 @@ int pra_embedding_bwd(const int64_t*, const int64_t*, const void*, void*, int64_
 void pra_bias_gelu_bwd_db(const void*, const void*, const void*, void*, float*, int, int, int, int, int,
                           hipStream_t);
 void pra_colsum_rows(const void*, float*, int, int, int, int, hipStream_t);
+int pra_colsum_multi(const float* const*, void* const*, const int*, int, int, int, int, hipStream_t);
 int pra_bn_nrb(int, int);
 int pra_max_pool_fwd(const void*, void*, uint8_t*, int, int, int, int, int, int, int, int, int, int, int, int, int,
                      hipStream_t);
@@ -299,6 +300,18 @@ PYBIND11_MODULE(_pra_hip, m) {
                                P s) {
     pra_bias_gelu_bwd_db(CV(dy), CV(x), CV(b), V(dx), F(part), rows, cols, nrb, dt, approx, S(s));
     check_launch("bias_gelu_bwd_db");
+  });
+  m.def("colsum_multi", [](std::vector<P> parts, std::vector<P> outs, std::vector<int> accs, int nblk, int cols,
+                           int dt, P s) {
+    const int n = (int)parts.size();
+    if (n != (int)outs.size() || n != (int)accs.size() || n < 1 || n > 3)
+      throw std::invalid_argument("colsum_multi: 1-3 jobs with matching lists");
+    const float* pp[3];
+    void* po[3];
+    for (int j = 0; j < n; ++j) { pp[j] = CF(parts[j]); po[j] = V(outs[j]); }
+    if (pra_colsum_multi(pp, po, accs.data(), n, nblk, cols, dt, S(s)) != 0)
+      throw std::invalid_argument("colsum_multi: unsupported shape/alignment");
+    check_launch("colsum_multi");
   });
   m.def("colsum_rows", [](P x, P part, int rows, int cols, int nrb, int dt, P s) {
     if (cols % 8) throw std::invalid_argument("colsum_rows: cols % 8 != 0");

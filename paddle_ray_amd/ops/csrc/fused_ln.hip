@@ -286,8 +286,8 @@ __global__ void __launch_bounds__(256) colsum16_k(const float* __restrict__ part
 // row slices; each lane keeps four 16-B loads in flight (the 16-column form issued one 4-B load
 // at a time per lane and ran latency-bound at ~0.35 TB/s)
 template <typename O>
-__global__ void __launch_bounds__(256) colsum4_k(const float* __restrict__ part, O* __restrict__ out, int nblk,
-                                                 int cols, int acc) {
+__device__ __forceinline__ void colsum4_body(const float* __restrict__ part, O* __restrict__ out, int nblk, int cols,
+                                             int acc) {
   __shared__ float4 red[16][17];
   const int cq = threadIdx.x & 15, rs = threadIdx.x >> 4;
   const int c = (blockIdx.x * 16 + cq) * 4;
@@ -320,6 +320,23 @@ __global__ void __launch_bounds__(256) colsum4_k(const float* __restrict__ part,
 #pragma unroll
     for (int e = 0; e < 4; ++e) out[c + e] = Cvt<O>::from(r[e] + (acc ? Cvt<O>::to(out[c + e]) : 0.f));
   }
+}
+template <typename O>
+__global__ void __launch_bounds__(256) colsum4_k(const float* __restrict__ part, O* __restrict__ out, int nblk,
+                                                 int cols, int acc) {
+  colsum4_body<O>(part, out, nblk, cols, acc);
+}
+// up to 3 independent column reductions of one shape in ONE launch (grid.y = job): the LayerNorm
+// weight / bias and the residual-branch bias gradients of one add+dropout+LN backward
+struct ColsumJobs {
+  const float* part[3];
+  void* out[3];
+  int acc[3];
+};
+template <typename O>
+__global__ void __launch_bounds__(256) colsum4_multi_k(ColsumJobs jobs, int nblk, int cols) {
+  const int j = blockIdx.y;
+  colsum4_body<O>(jobs.part[j], static_cast<O*>(jobs.out[j]), nblk, cols, jobs.acc[j]);
 }
 
 }  // namespace pra
@@ -380,6 +397,21 @@ void pra_adl_bwd(const void* dy, const void* dr_out, const void* r, const void* 
 #undef K_BWD
 }
 
+// njobs <= 3 reductions part[j] [nblk][cols] -> out[j] (+= when acc[j]), one dtype; cols % 4 == 0
+int pra_colsum_multi(const float* const* part, void* const* out, const int* acc, int njobs, int nblk, int cols,
+                     int dto, hipStream_t s) {
+  if (njobs < 1 || njobs > 3 || cols % 4) return -1;
+  ColsumJobs jb{};
+  for (int j = 0; j < njobs; ++j) {
+    if (((uintptr_t)part[j] & 15) != 0) return -1;
+    jb.part[j] = part[j];
+    jb.out[j] = out[j];
+    jb.acc[j] = acc[j];
+  }
+  PRA_DISPATCH_FLOAT(dto, TO, hipLaunchKernelGGL((colsum4_multi_k<TO>), dim3((cols + 63) / 64, njobs), dim3(256), 0,
+                                                 s, jb, nblk, cols));
+  return 0;
+}
 void pra_colsum16(const float* part, void* out, int nblk, int cols, int dto, int acc, hipStream_t s) {
   if (cols % 4 == 0 && ((uintptr_t)part & 15) == 0) {
     PRA_DISPATCH_FLOAT(dto, TO, hipLaunchKernelGGL((colsum4_k<TO>), dim3((cols + 63) / 64), dim3(256), 0, s,

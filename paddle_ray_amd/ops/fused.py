@@ -266,18 +266,25 @@ def _adl_bwd_hip(dy, dr_out, r, w, mean, rstd, p, seed, need_dw, need_db, need_d
               _ptr(dh), _ptr(part[0]) if need_dw else 0, _ptr(part[1]) if need_db else 0,
               _ptr(part[2]) if need_dhb else 0, rows, cols, nblk, float(p), seed, 0, _dt(r),
               _dt(w) if w is not None else _dt(r), _stream())
-    outs = []
+    outs, jobs = [], []
     into = into or (None, None, None)
     for need, i, dt in ((need_dw, 0, pdt), (need_db, 1, pdt), (need_dhb, 2, r.dtype)):
         if need and into[i] is not None:
-            L.colsum16_acc(_ptr(part[i]), _ptr(into[i]), nblk, cols, _DT[into[i].dtype], _stream())
+            jobs.append((i, into[i], 1))
             outs.append(None)
         elif need:
             o = torch.empty(cols, device=r.device, dtype=dt)
-            L.colsum16(_ptr(part[i]), _ptr(o), nblk, cols, _DT[dt], _stream())
+            jobs.append((i, o, 0))
             outs.append(o)
         else:
             outs.append(None)
+    if jobs and cols % 4 == 0 and len({o.dtype for _, o, _ in jobs}) == 1:
+        # every parameter-gradient reduction of this backward in one launch
+        L.colsum_multi([_ptr(part[i]) for i, _, _ in jobs], [_ptr(o) for _, o, _ in jobs],
+                       [a for _, _, a in jobs], nblk, cols, _DT[jobs[0][1].dtype], _stream())
+    else:
+        for i, o, a in jobs:
+            (L.colsum16_acc if a else L.colsum16)(_ptr(part[i]), _ptr(o), nblk, cols, _DT[o.dtype], _stream())
     return (dri, dh) + tuple(outs)
 
 
