@@ -1459,7 +1459,7 @@ class MlpGeluFn(torch.autograd.Function):
         h = gemm(GEMM_FWD, x2, w1, bias=b1, z=z, epi='gelu_tanh' if approximate else 'gelu')
         y = gemm(GEMM_FWD, h, w2)
         ctx.save_for_backward(x, z, h)
-        ctx.w1, ctx.w2 = w1, w2
+        ctx.w1, ctx.w2, ctx.b1 = w1, w2, b1
         ctx.approximate = approximate
         return y.view(*x.shape[:-1], w2.shape[1])
 
@@ -1474,10 +1474,11 @@ class MlpGeluFn(torch.autograd.Function):
         if _GEMM_MODE == 'auto':
             # dgrad on hipBLASLt, then ONE fused pass for gelu'(z) and the bias gradient
             dh = torch.mm(dy2, w2.t())
-            dz, db1 = _dgelu_db(dh, z, ctx.approximate)
+            dz, db1 = _dgelu_db(dh, z, ctx.approximate, ctx.b1)
         else:
             dz, db1 = gemm(GEMM_NT, dy2, w2, z=z, epi='dgelu_tanh' if ctx.approximate else 'dgelu',
                            want_colsum=True)
+            db1 = db1.to(dz.dtype)
         dw1 = dw2 = None
         g2 = w2.grad
         if _acc_grad_ok(g2, w2, dy2.dtype):
@@ -1490,21 +1491,26 @@ class MlpGeluFn(torch.autograd.Function):
             gemm(GEMM_TN, x2, dz, out=g1, beta=1)
         else:
             dw1 = gemm(GEMM_TN, x2, dz)
-        return dx, dw1, db1.to(dz.dtype), dw2, None
+        return dx, dw1, db1, dw2, None
 
 
-def _dgelu_db(dh, z, approximate):
-    """dz = dh * gelu'(z) and db = colsum(dz) in one pass (bias_gelu_bwd_db kernel, zero bias)."""
+def _dgelu_db(dh, z, approximate, b=None):
+    """dz = dh * gelu'(z) and db = colsum(dz) in one pass (bias_gelu_bwd_db kernel; z is the
+    pre-activation, bias already in it). db is added straight into ``b.grad`` when it exists
+    (returned as None then), else returned in z's dtype."""
     rows, cols = z.shape
     L = _native.lib()
     nrb = max(1, min(256, rows // 16))
     part = torch.empty((nrb, cols), device=z.device, dtype=torch.float32)
     dz = torch.empty_like(z)
-    zero_b = torch.zeros(cols, device=z.device, dtype=z.dtype)
-    L.bias_gelu_bwd_db(_ptr(dh), _ptr(z), _ptr(zero_b), _ptr(dz), _ptr(part), rows, cols, nrb, _dt(z),
+    L.bias_gelu_bwd_db(_ptr(dh), _ptr(z), 0, _ptr(dz), _ptr(part), rows, cols, nrb, _dt(z),
                        int(approximate), _stream())
-    db = torch.empty(cols, device=z.device, dtype=torch.float32)
-    L.colsum16(_ptr(part), _ptr(db), nrb, cols, 0, _stream())
+    g = b.grad if (b is not None and b.is_leaf) else None
+    if b is not None and _acc_grad_ok(g, b, z.dtype):
+        L.colsum16_acc(_ptr(part), _ptr(g), nrb, cols, _dt(g), _stream())
+        return dz, None
+    db = torch.empty(cols, device=z.device, dtype=z.dtype)
+    L.colsum16(_ptr(part), _ptr(db), nrb, cols, _dt(db), _stream())
     return dz, db
 
 

@@ -158,3 +158,7 @@ def test_mlp_gelu_fused(approx, mode):
     _close(y, yf)
     for got, ref in ((x.grad, xf.grad), (w1.grad, w1f.grad), (b1.grad, b1f.grad), (w2.grad, w2f.grad)):
         _close(got, ref, tol=3e-2)
+    # second backward: every parameter gradient (fc1 bias included) accumulates in place
+    K.mlp_gelu(x, w1, b1, w2, approx).backward(gy)
+    for got, ref in ((w1.grad, w1f.grad), (b1.grad, b1f.grad), (w2.grad, w2f.grad)):
+        _close(got, 2 * ref, tol=3e-2)
