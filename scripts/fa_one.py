@@ -35,6 +35,20 @@ def main():
         dt = (time.perf_counter() - t0) / iters
         print(f"{name}: {dt * 1e6:.1f} us  {fl / dt / 1e12:.1f} TF/s (B{B} H{H} S{S} D{D} causal={causal})",
               flush=True)
+        # the same calls replayed from one captured HIP graph: GPU time without host launch gaps
+        graph = torch.cuda.CUDAGraph()
+        fn()
+        torch.cuda.synchronize()
+        with torch.cuda.graph(graph):
+            for _ in range(iters):
+                fn()
+        graph.replay()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        graph.replay()
+        torch.cuda.synchronize()
+        dg = (time.perf_counter() - t0) / iters
+        print(f"{name} (graph replay): {dg * 1e6:.1f} us  {fl / dg / 1e12:.1f} TF/s", flush=True)
 
 
 if __name__ == '__main__':
