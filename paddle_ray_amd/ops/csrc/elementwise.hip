@@ -76,6 +76,25 @@ __global__ void __launch_bounds__(256) bias_gelu_bwd_db_k(const T* __restrict__ 
   for (int i = 0; i < 8; ++i) { db[i] = 0.f; if (!b) bb[i] = 0.f; }
   const int r0 = blockIdx.y * rpb, r1 = min(rows, r0 + rpb);
   int r = r0;
+  // four rows (8 independent 16-B loads) in flight per lane
+  for (; r + 3 < r1; r += 4) {
+    float a[4][8], g[4][8];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const size_t o = (size_t)(r + u) * cols + c;
+      load8<T>(x + o, a[u]);
+      load8<T>(dy + o, g[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) a[u][i] = g[u][i] * gelu_df(a[u][i] + bb[i], approx);
+      store8<T>(dx + (size_t)(r + u) * cols + c, a[u]);
+      // d bias from the ROUNDED dx values (what a separate colsum(dx) would read)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) db[i] += Cvt<T>::to(Cvt<T>::from(a[u][i]));
+    }
+  }
   for (; r + 1 < r1; r += 2) {
     float a0[8], g0[8], a1[8], g1[8];
     const size_t o0 = (size_t)r * cols + c, o1 = o0 + cols;
@@ -90,7 +109,6 @@ __global__ void __launch_bounds__(256) bias_gelu_bwd_db_k(const T* __restrict__ 
     }
     store8<T>(dx + o0, a0);
     store8<T>(dx + o1, a1);
-    // d bias from the ROUNDED dx values (what a separate colsum(dx) would read)
 #pragma unroll
     for (int i = 0; i < 8; ++i)
       db[i] += Cvt<T>::to(Cvt<T>::from(a0[i])) + Cvt<T>::to(Cvt<T>::from(a1[i]));
