@@ -462,7 +462,10 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_lds_kernel(const uint16_t* __r
       half(fa1, fb1, fa0, fb0, kt + 1 < nk, kt + 1, 0, kt + 2 < nk && dmaon, kt + 2, kt + 2 < nk && dmaon, kt + 2);
     }
     __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_waitcnt(0xC07F);  // (kt+1,0) fragments landed
+    // (kt+1,0) fragments landed. The steady body leaves this to the compiler's per-register
+    // lgkmcnt(N) before each consuming MFMA (no LDS-safety role: slot kt+1 is refilled only after
+    // the next half-0 drain + barrier), so the next half starts on its first fragments.
+    if constexpr (!STEADY) __builtin_amdgcn_s_waitcnt(0xC07F);
   };
   int kt = 0;
   // (the implicit-GEMM convolutions keep the generic body: their gather state already sits at
