@@ -46,11 +46,48 @@ def _free_port():
         return s.getsockname()[1]
 
 
+def _supervise(procs, limit_s, poll_s=0.2, grace_s=10.0):
+    """Wait for every rank; the FIRST non-zero exit (or the wall-clock limit) terminates the
+    siblings (SIGTERM, then SIGKILL after ``grace_s``) so one dead rank cannot leave the others
+    blocked inside a collective. Returns the first failing status (124 on the time limit)."""
+    import signal
+    t_end = time.monotonic() + limit_s
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            c = p.poll()
+            if c is None:
+                continue
+            live.remove(p)
+            if c != 0 and rc == 0:
+                rc = c
+                print(f"bench.py: rank pid {p.pid} exited with {c}; stopping {len(live)} sibling(s)",
+                      file=sys.stderr, flush=True)
+        if live and (rc != 0 or time.monotonic() > t_end):
+            if rc == 0:
+                rc = 124
+                print(f"bench.py: wall-clock limit {limit_s:.0f}s reached; stopping the ranks",
+                      file=sys.stderr, flush=True)
+            for p in live:
+                p.send_signal(signal.SIGTERM)
+            t_kill = time.monotonic() + grace_s
+            while live and time.monotonic() < t_kill:
+                live = [p for p in live if p.poll() is None]
+                time.sleep(poll_s)
+            for p in live:
+                p.kill()
+                p.wait()
+            live = []
+        time.sleep(poll_s)
+    return rc
+
+
 def _spawn_ranks(n):
     """``--gpus N`` without a launcher: start N fresh rank processes (one per GPU) and
-    exit with the worst child status. Runs before this process imports torch or touches
-    the GPU, so every rank initialises HIP in a clean process (no fork after HIP init,
-    no exec from a GPU process)."""
+    exit with the first failing child status (siblings are stopped, see ``_supervise``).
+    Runs before this process imports torch or touches the GPU, so every rank initialises
+    HIP in a clean process (no fork after HIP init, no exec from a GPU process)."""
     import subprocess
     port = str(_free_port())
     procs = []
@@ -60,11 +97,7 @@ def _spawn_ranks(n):
                    HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get('HSA_ENABLE_IPC_MODE_LEGACY', '0'))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
                                       env=env))
-    rc = 0
-    for p in procs:
-        c = p.wait()
-        rc = rc or c
-    return rc
+    return _supervise(procs, float(os.environ.get('PRA_BENCH_TIMEOUT', 570)))
 
 
 def main():
@@ -81,6 +114,9 @@ def main():
         raise SystemExit(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world}; launch one rank per GPU "
                          f"(torchrun --nproc-per-node {a.gpus}) or drop WORLD_SIZE to self-spawn")
     if world > 1:
+        # a rank stuck in a collective fails within 5 minutes (the default watchdog budget is
+        # 30), well inside the driver's bench limit, so a broken run still reports
+        os.environ.setdefault('PRA_COMM_TIMEOUT', '300')
         C.init_parallel_env()
     rank = C.get_rank()
     dev = torch.device('cuda', torch.cuda.current_device()) if torch.cuda.is_available() \

@@ -67,7 +67,8 @@ class ParallelEnv:
         self._world_size = int(os.environ.get('PADDLE_TRAINERS_NUM',
                                               os.environ.get('WORLD_SIZE', 1)))
         self._local_rank = int(os.environ.get('LOCAL_RANK', self._rank))
-        self._device_id = int(os.environ.get('FLAGS_selected_gpus', self._local_rank))
+        sel = os.environ.get('FLAGS_selected_gpus', '').split(',')[0].strip()
+        self._device_id = int(sel) if sel.lstrip('-').isdigit() else self._local_rank
         eps = os.environ.get('PADDLE_TRAINER_ENDPOINTS', '')
         self._trainer_endpoints = eps.split(',') if eps else []
         self._current_endpoint = os.environ.get('PADDLE_CURRENT_ENDPOINT', '')
@@ -113,6 +114,18 @@ def is_initialized():
     return dist.is_initialized()
 
 
+def _bound_device(env=None):
+    """The HIP device this rank drives: ``FLAGS_selected_gpus`` (set per rank by
+    ``distributed.launch --gpus 4,5``) when present, else ``LOCAL_RANK`` — both modulo the
+    visible device count (a rehearsal with more ranks than GPUs shares devices)."""
+    env = env or ParallelEnv()
+    n = max(torch.cuda.device_count(), 1)
+    sel = os.environ.get('FLAGS_selected_gpus', '').split(',')[0].strip()
+    if sel.lstrip('-').isdigit():
+        return int(sel) % n
+    return env.local_rank % n
+
+
 def init_parallel_env(backend=None, timeout_s=None):
     """Create the default process group from torchrun / paddle launch env vars."""
     if dist.is_initialized():
@@ -134,9 +147,10 @@ def init_parallel_env(backend=None, timeout_s=None):
     if backend in ('rccl', 'xccl', 'bkcl'):
         backend = 'nccl'
     if use_gpu:
-        torch.cuda.set_device(env.local_rank % max(torch.cuda.device_count(), 1))
+        dev_id = _bound_device(env)
+        torch.cuda.set_device(dev_id)
         from ..framework.core import set_device
-        set_device(f'gpu:{env.local_rank % max(torch.cuda.device_count(), 1)}')
+        set_device(f'gpu:{dev_id}')
     to = datetime.timedelta(seconds=timeout_s or int(os.environ.get('PRA_COMM_TIMEOUT', 1800)))
     kw = {}
     if backend == 'nccl' and use_gpu:
@@ -174,6 +188,26 @@ def new_group(ranks=None, backend=None, timeout=None):
     g = Group(ranks, pg, gid)
     _groups[gid] = g
     return g
+
+
+def twin_group(group=None):
+    """A second communicator over exactly the ranks of ``group`` (its own RCCL stream), so two
+    streams of collectives on one rank set (ZeRO-3 parameter all-gathers and gradient
+    reduce-scatters) do not serialise behind each other. Collective over the WHOLE job: every
+    rank calls it at the same point, each passing its own group; the member lists are
+    exchanged and every distinct list is created in one global order (``new_group`` contract)."""
+    ws = dist.get_world_size() if dist.is_initialized() else 1
+    mine = tuple(range(ws)) if group is None else tuple(sorted(group.ranks))
+    if ws == 1:
+        return new_group(list(mine))
+    lists = [None] * ws
+    dist.all_gather_object(lists, mine)
+    out = None
+    for ranks in sorted(set(tuple(r) for r in lists)):
+        g = new_group(list(ranks))
+        if ranks == mine:
+            out = g
+    return out
 
 
 def destroy_process_group(group=None):

@@ -191,6 +191,11 @@ class Fleet:
         return {1: 'os', 2: 'os_g', 3: 'p_g_os'}[stage]
 
     def distributed_model(self, model):
+        out = self._distributed_model(model)
+        self._wrapped_model = out
+        return out
+
+    def _distributed_model(self, model):
         """Wrap ``model`` for the active hybrid mode (parity: fleet/model.py:30-140).
 
         * sharding_degree > 1 (alone, with dp, or with mp): ``ShardedModel`` over the sharding
@@ -211,9 +216,20 @@ class Fleet:
         mode = hcg.get_parallel_mode()
         sh = hcg.get_sharding_parallel_world_size()
         if mode == ParallelMode.PIPELINE_PARALLEL:
+            state = None
             if sh > 1:
-                raise NotImplementedError("pipeline x sharding: use sharding_degree=1 with pp>1")
-            return _wrap_amp(_pp.PipelineParallel(model, hcg, st), st)
+                # pipeline x sharding (parity: pipeline_parallel.py:40-89 with the
+                # DygraphShardingOptimizer of hybrid_parallel_optimizer.py:243-313): optimizer
+                # state sharded over the sharding group inside each stage (stage 1)
+                if self._sharding_level() != 'os':
+                    raise NotImplementedError("pipeline x sharding supports sharding stage 1")
+                from ...parallel.sharding import ShardedState
+                dpg = hcg.get_data_parallel_group()
+                state = ShardedState(model, 'os', hcg.get_sharding_parallel_group(),
+                                     dp_group=dpg if dpg.nranks > 1 else None,
+                                     segment_bytes=int(st.fuse_grad_size_in_MB) << 20)
+                self._sharded_state = state
+            return _wrap_amp(_pp.PipelineParallel(model, hcg, st, sharded_state=state), st)
         if sh > 1:
             from ...parallel.sharding import ShardedState, ShardedModel
             if hcg.get_model_parallel_world_size() > 1:
@@ -251,8 +267,26 @@ class Fleet:
             opt = HybridParallelOptimizer(optimizer, hcg, st)
         if st.gradient_merge and int(st.gradient_merge_configs.get('k_steps', 1)) > 1:
             opt = GradientMergeOptimizer(opt, int(st.gradient_merge_configs['k_steps']),
-                                         bool(st.gradient_merge_configs.get('avg', True)))
+                                         bool(st.gradient_merge_configs.get('avg', True)),
+                                         reducer=self._grad_reducer())
+        self._wrapped_optimizer = opt
         return opt
+
+    def _grad_reducer(self):
+        """The bucket reducer whose collectives gradient merge may skip on non-final
+        micro-steps: DataParallel's all-reduce and sharding stage 1/2's all-reduce /
+        reduce-scatter (their full gradient buffers accumulate locally). Stage 3 frees its
+        full gradients after every backward and accumulates into the owned shard instead."""
+        m = getattr(self, '_wrapped_model', None)
+        while m is not None and not hasattr(m, '_reducer') and not hasattr(m, '_state') \
+                and hasattr(m, '_layers') and isinstance(getattr(m, '_layers'), Layer):
+            m = m._layers
+        if m is None:
+            return None
+        state = m.__dict__.get('_state')
+        if state is not None:
+            return state.reducer if state.stage in (1, 2) else None
+        return getattr(m, '_reducer', None)
 
     def distributed_scaler(self, scaler):
         """HybridParallelGradScaler: found_inf is MAX-reduced over every hybrid group."""
@@ -272,7 +306,26 @@ class Fleet:
         save_persistables(executor, dirname, main_program)
 
     def state_dict(self):
-        return {}
+        """Checkpoint of the job as this rank sees it: the wrapped model's FULL parameters (a
+        sharded model gathers them) and, once ``distributed_optimizer`` ran, the optimizer state
+        in the reference's per-parameter layout (a sharded optimizer gathers every shard, so the
+        file resumes at any sharding degree). Every rank of the hybrid groups must call it."""
+        sd = {}
+        m = getattr(self, '_wrapped_model', None)
+        if m is not None:
+            sd['model'] = m.state_dict()
+        o = getattr(self, '_wrapped_optimizer', None)
+        if o is not None:
+            sd['optimizer'] = o.state_dict()
+        return sd
+
+    def set_state_dict(self, sd):
+        m = getattr(self, '_wrapped_model', None)
+        if m is not None and 'model' in sd:
+            m.set_state_dict(sd['model'])
+        o = getattr(self, '_wrapped_optimizer', None)
+        if o is not None and 'optimizer' in sd:
+            o.set_state_dict(sd['optimizer'])
 
 
 from ...nn.layer.layers import Layer  # noqa: E402
@@ -356,11 +409,20 @@ class GradientMergeOptimizer:
     accumulate over ``k_steps`` backward passes; the inner step runs on every k-th call
     (grads averaged when ``avg``) and only then are grads cleared."""
 
-    def __init__(self, inner, k_steps, avg=True):
+    def __init__(self, inner, k_steps, avg=True, reducer=None):
         self._inner_opt = inner
         self.k_steps = k_steps
         self.avg = avg
         self._calls = 0
+        # no_sync for the k-1 non-final backward passes: the gradient collectives run once per
+        # k micro-steps, on the locally accumulated buffers (parity: the reference merges
+        # gradients before its allreduce ops)
+        self._reducer = reducer
+        self._arm()
+
+    def _arm(self):
+        if self._reducer is not None:
+            self._reducer.enabled = (self._calls + 1) % self.k_steps == 0
 
     def _grads(self):
         g = getattr(self._inner_opt, '_scaler_grads', None)
@@ -370,6 +432,7 @@ class GradientMergeOptimizer:
 
     def step(self):
         self._calls += 1
+        self._arm()  # the NEXT backward reduces only if it completes a merge window
         if self._calls % self.k_steps:
             return
         if self.avg:
@@ -437,10 +500,10 @@ class HybridParallelOptimizer:
 
             def hook(sq_local, params=params):
                 # recompute split: distributed params are summed over mp ranks, replicated once
-                d = [p._t.grad for p in params if p._t.grad is not None and
-                     getattr(p, 'is_distributed', False)]
-                r = [p._t.grad for p in params if p._t.grad is not None and
-                     not getattr(p, 'is_distributed', False)]
+                ps = [p for p in params if p._t.grad is not None and
+                      getattr(p, 'is_firstly_shared', True)]  # tied weights counted once
+                d = [p._t.grad for p in ps if getattr(p, 'is_distributed', False)]
+                r = [p._t.grad for p in ps if not getattr(p, 'is_distributed', False)]
                 from ...ops.fused import global_l2_norm_sq
                 sd = global_l2_norm_sq(d) if d else torch.zeros((), device=sq_local.device)
                 sr = global_l2_norm_sq(r) if r else torch.zeros((), device=sq_local.device)
@@ -471,6 +534,8 @@ init = fleet.init
 distributed_model = fleet.distributed_model
 distributed_optimizer = fleet.distributed_optimizer
 get_hybrid_communicate_group = fleet.get_hybrid_communicate_group
+state_dict = fleet.state_dict
+set_state_dict = fleet.set_state_dict
 distributed_scaler = fleet.distributed_scaler
 is_first_worker = fleet.is_first_worker
 worker_index = fleet.worker_index

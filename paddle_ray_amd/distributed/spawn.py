@@ -29,10 +29,30 @@ class MultiprocessContext:
         self.processes = procs
 
     def join(self, timeout=None):
-        ok = True
-        for p in self.processes:
-            p.join(timeout)
-            ok = ok and p.exitcode == 0
+        """Poll every worker; the first failure terminates the others (a dead rank would
+        otherwise leave its peers blocked in a collective until the comm timeout)."""
+        import time
+        t_end = None if timeout is None else time.monotonic() + timeout
+        live = list(self.processes)
+        failed = False
+        while live:
+            for p in list(live):
+                if p.exitcode is not None:
+                    live.remove(p)
+                    failed = failed or p.exitcode != 0
+            if live and (failed or (t_end is not None and time.monotonic() > t_end)):
+                for p in live:
+                    p.terminate()
+                for p in live:
+                    p.join(10)
+                    if p.exitcode is None:
+                        p.kill()
+                        p.join()
+                if not failed:
+                    return False
+                break
+            time.sleep(0.1)
+        ok = all(p.exitcode == 0 for p in self.processes)
         if not ok:
             codes = [p.exitcode for p in self.processes]
             raise RuntimeError(f"spawned workers failed with exit codes {codes}")

@@ -20,18 +20,31 @@
 #include <vector>
 
 #ifdef PRA_ALLOC_HOST
+// Host build: an "event" is a flag that is pending until the test completes it
+// (pra_alloc_host_complete_events), or done at once unless pending mode is on.
+struct HostEvent {
+  bool done;
+};
 typedef void* stream_t;
-typedef void* event_t;
+typedef HostEvent* event_t;
+static bool g_host_pending = false;
+static std::vector<HostEvent*> g_host_events;
 static int backend_malloc(void** p, size_t n) {
   *p = std::aligned_alloc(256, n);
   return *p ? 0 : 1;
 }
 static void backend_free(void* p) { std::free(p); }
 static void backend_set_device(int) {}
-static event_t event_record(stream_t) { return nullptr; }
-static bool event_done(event_t) { return true; }
+static event_t event_record(stream_t) {
+  HostEvent* e = new HostEvent{!g_host_pending};
+  g_host_events.push_back(e);
+  return e;
+}
+static bool event_done(event_t e) { return e == nullptr || e->done; }
 static void event_destroy(event_t) {}
-static void device_sync() {}
+static void device_sync() {
+  for (HostEvent* e : g_host_events) e->done = true;
+}
 #else
 #include <hip/hip_runtime.h>
 typedef hipStream_t stream_t;
@@ -133,9 +146,15 @@ struct DeviceAllocator {
 
   Block* take(Block* b, size_t n, stream_t s) {
     erase_free(b);
+    // a block taken from its own stream's list may still be in use by work queued on that
+    // stream before its free: the split remainder keeps a gate of its own, recorded on that
+    // stream now (it completes after that work), so another stream cannot take it early
+    const bool pending = !event_done(b->event);
+    const stream_t old_stream = b->stream;
     drop_event(b);
     if (b->size - n >= kMinSplit) {  // split: remainder stays free on the block's stream
-      Block* r = new Block{b->ptr + n, b->size - n, true, b->chunk, b, b->next, b->stream, nullptr};
+      Block* r = new Block{b->ptr + n, b->size - n, true, b->chunk, b, b->next, b->stream,
+                           pending ? new_event(old_stream) : nullptr};
       if (b->next) b->next->prev = r;
       b->next = r;
       b->size = n;
@@ -348,4 +367,11 @@ void pra_alloc_set_growth(int device, int64_t bytes) {
   a->growth = (size_t)bytes;
 }
 int pra_alloc_check(int device) { return dev(device)->check() ? 1 : 0; }
+#ifdef PRA_ALLOC_HOST
+// host-build test hooks: events recorded from now on stay pending until completed
+void pra_alloc_host_set_pending(int on) { g_host_pending = on != 0; }
+void pra_alloc_host_complete_events() {
+  for (HostEvent* e : g_host_events) e->done = true;
+}
+#endif
 }

@@ -309,9 +309,6 @@ class Adam(Optimizer):
         b1 = float(b1.item()) if isinstance(b1, Tensor) else b1
         b2 = float(b2.item()) if isinstance(b2, Tensor) else b2
         step = self._step_count
-        for p in ps:  # keep reference-compatible pow accumulators
-            self._acc('beta1_pow_acc', p, 1.0, shape=[1]).fill_(b1 ** step)
-            self._acc('beta2_pow_acc', p, 1.0, shape=[1]).fill_(b2 ** step)
         coupled = not self._decoupled and any(wds)
         if coupled:
             # Adam + L2: clip first, then the coupled decay folded into the gradient
@@ -341,6 +338,41 @@ class Adam(Optimizer):
             grads = [p._t.grad if coef is None else p._t.grad * coef for p in ps]
             K.adamw_ref([p._t for p in ps], grads, ms, vs, masters, lr, b1, b2, self._epsilon, wds,
                         lrm, step)
+
+
+    def _betas(self):
+        b1, b2 = self._beta1, self._beta2
+        return (float(b1.item()) if isinstance(b1, Tensor) else b1,
+                float(b2.item()) if isinstance(b2, Tensor) else b2)
+
+    def state_dict(self):
+        """Adds the reference's ``{param}_beta{1,2}_pow_acc_0``: the accumulator starts at beta
+        and is multiplied after every update (adamw.py:343-348), so after t steps it holds
+        beta**(t+1). They are derived from the step count here, not kept per parameter (no
+        per-step fill launches)."""
+        sd = super().state_dict()
+        b1, b2 = self._betas()
+        t = self._step_count
+        for pn in self._accumulators.get('moment1', {}):
+            sd[f'{pn}_beta1_pow_acc_0'] = Tensor(torch.tensor([b1 ** (t + 1)], dtype=torch.float32))
+            sd[f'{pn}_beta2_pow_acc_0'] = Tensor(torch.tensor([b2 ** (t + 1)], dtype=torch.float32))
+        return sd
+
+    def set_state_dict(self, state_dict):
+        super().set_state_dict(state_dict)
+        for acc in ('beta1_pow_acc', 'beta2_pow_acc'):
+            self._accumulators.pop(acc, None)
+        if '@step' not in state_dict:  # a reference file: recover t from beta1**(t+1)
+            pw = [v for k, v in state_dict.items() if k.endswith('_beta1_pow_acc_0')]
+            if pw:
+                self._step_count = beta_pow_to_step(pw[0], self._betas()[0])
+
+
+def beta_pow_to_step(pw, beta):
+    """Steps taken, from a reference ``beta_pow_acc`` (= beta**(t+1) after t updates)."""
+    import math
+    v = float(_u(pw).reshape(-1)[0]) if isinstance(pw, Tensor) else float(np.asarray(pw).reshape(-1)[0])
+    return max(0, int(round(math.log(v) / math.log(beta))) - 1)
 
 
 class AdamW(Adam):

@@ -34,13 +34,22 @@ class GradBucketReducer:
     """Shared by DataParallel (all-reduce) and sharding stage 1 (all-reduce) / 2,3 (reduce-scatter).
 
     ``dp_pg``: in hybrid dp x sharding, the owned (already sharding-reduced) gradient shard
-    is then averaged over the data-parallel group. ``on_launch(gi)`` / ``on_finalize()`` let
-    ZeRO-3 free a bucket's gathered parameters as soon as its gradients are complete.
+    is then averaged over the data-parallel group. On RCCL that all-reduce is issued per bucket
+    as soon as the bucket's reduce-scatter is launched, from a side HIP stream that waits on the
+    reduce-scatter's completion event, so the dp traffic overlaps the rest of the backward (the
+    compute stream never waits for it until ``finalize``). ``on_launch(gi)`` / ``on_finalize()``
+    let ZeRO-3 free a bucket's gathered parameters as soon as its gradients are complete.
+    ``accumulate``: several backward passes before one optimizer step ADD into the shard
+    gradients (ZeRO-3 frees and re-zeroes the full gradient buffer after every backward, so the
+    reduce-scatter of pass k > 1 lands in a scratch shard that is then added; parity:
+    group_sharded_stage3.py:675-694 adding into ``param.bw_storage``). ``reset_accumulation``
+    (called from ``clear_grad``) makes the next pass write the shard directly again.
     Every RCCL work is registered with the collective watchdog until it is waited on.
     """
 
     def __init__(self, groups, pg, world, mode='allreduce', shard_grads=None, dp_pg=None,
-                 dp_world=1, on_launch=None, on_finalize=None, name='dp_bucket'):
+                 dp_world=1, on_launch=None, on_finalize=None, name='dp_bucket',
+                 accumulate=False):
         self.groups = groups
         self.pg = pg
         self.world = world
@@ -51,10 +60,16 @@ class GradBucketReducer:
         self.dp_avg = _avg_supported(dp_pg) if dp_pg is not None else False
         self.on_launch, self.on_finalize = on_launch, on_finalize
         self.name = name
+        self.accumulate = accumulate and mode != 'allreduce'
+        self.fresh = [True] * len(groups)   # shard_grads[gi] holds nothing of this step yet
+        self._scratch = [None] * len(groups)
         self.counts = [0] * len(groups)
         self.launched = [False] * len(groups)
         self.works = []
+        self.dp_works = []
+        self._side = None
         self.enabled = True
+        self.auto_finalize = True  # finalize at the end of the backward that first fires a hook
         self._cb_queued = False
         self.finalize_count = 0
         self._hooks = []
@@ -68,7 +83,7 @@ class GradBucketReducer:
         def hook(t):
             if not self.enabled:
                 return
-            if not self._cb_queued:
+            if not self._cb_queued and self.auto_finalize:
                 self._cb_queued = True
                 from .recompute import queue_outer_callback
                 queue_outer_callback(self.finalize)
@@ -76,6 +91,22 @@ class GradBucketReducer:
             if self.counts[gi] == self.n_req[gi]:
                 self._launch(gi)
         return hook
+
+    def reset_accumulation(self):
+        self.fresh = [True] * len(self.groups)
+
+    def _rs_target(self, gi):
+        """Where this pass's reduce-scatter of bucket gi lands: the shard itself on the first
+        pass of a step, else a scratch shard added at finalize."""
+        if not self.accumulate or self.fresh[gi]:
+            return self.shard_grads[gi]
+        if self._scratch[gi] is None:
+            self._scratch[gi] = torch.empty_like(self.shard_grads[gi])
+        return self._scratch[gi]
+
+    def _dp_overlap(self):
+        return (self.dp_pg is not None and self.dp_world > 1 and self.world > 1 and
+                torch.cuda.is_available() and _avg_supported(self.dp_pg) and self.avg)
 
     def _launch(self, gi):
         if self.launched[gi]:
@@ -85,17 +116,31 @@ class GradBucketReducer:
             g = self.groups[gi]
             op = dist.ReduceOp.AVG if self.avg else dist.ReduceOp.SUM
             if self.mode == 'allreduce':
-                w = dist.all_reduce(g.grad_buf, op=op, group=self.pg, async_op=True)
+                out = g.grad_buf
+                w = dist.all_reduce(out, op=op, group=self.pg, async_op=True)
             else:
-                w = dist.reduce_scatter_tensor(self.shard_grads[gi], g.grad_buf, op=op,
-                                               group=self.pg, async_op=True)
-            self.works.append((gi, _watchdog.track(f'{self.name}.{self.mode}[{gi}]', w,
-                                                   self.world)))
+                out = self._rs_target(gi)
+                w = dist.reduce_scatter_tensor(out, g.grad_buf, op=op, group=self.pg,
+                                               async_op=True)
+            w = _watchdog.track(f'{self.name}.{self.mode}[{gi}]', w, self.world)
+            self.works.append((gi, w))
+            if self._dp_overlap():
+                # the side stream waits for this bucket's reduce-scatter, then the dp all-reduce
+                # of the shard runs on the dp communicator's stream: the compute stream is free
+                if self._side is None:
+                    self._side = torch.cuda.Stream()
+                self._side.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(self._side):
+                    w.wait()
+                    w2 = dist.all_reduce(out, op=dist.ReduceOp.AVG, group=self.dp_pg,
+                                         async_op=True)
+                self.dp_works.append((gi, _watchdog.track(
+                    f'{self.name}.dp_allreduce[{gi}]', w2, self.dp_world)))
         if self.on_launch is not None:
             self.on_launch(gi)
 
     def _shard_out(self, gi):
-        return self.groups[gi].grad_buf if self.mode == 'allreduce' else self.shard_grads[gi]
+        return self.groups[gi].grad_buf if self.mode == 'allreduce' else self._rs_target(gi)
 
     def finalize(self):
         for gi in range(len(self.groups)):
@@ -107,21 +152,32 @@ class GradBucketReducer:
                 self._shard_out(gi).div_(self.world)
         if self.world == 1 and self.mode != 'allreduce':
             for gi, g in enumerate(self.groups):
-                if self.shard_grads[gi].data_ptr() != g.grad_buf.data_ptr():
-                    self.shard_grads[gi].copy_(g.shard(g.grad_buf))
+                dst = self._rs_target(gi)
+                if dst.data_ptr() != g.grad_buf.data_ptr():
+                    dst.copy_(g.shard(g.grad_buf))
         if self.dp_pg is not None and self.dp_world > 1:
-            # hybrid dp x sharding: average the owned shard over the replicas
-            op = dist.ReduceOp.AVG if self.dp_avg else dist.ReduceOp.SUM
-            dws = []
-            for gi, g in enumerate(self.groups):
-                out = self.shard_grads[gi] if self.shard_grads is not None else g.grad_buf
-                dws.append((out, _watchdog.track(f'{self.name}.dp_allreduce[{gi}]', dist.all_reduce(
-                    out, op=op, group=self.dp_pg, async_op=True), self.dp_world)))
-            for out, w in dws:
-                w.wait()
-                if not self.dp_avg:
-                    out.div_(self.dp_world)
+            if self.dp_works:  # issued during the backward (RCCL): only wait here
+                for gi, w in self.dp_works:
+                    w.wait()
+            else:
+                # hybrid dp x sharding: average the owned shard over the replicas
+                op = dist.ReduceOp.AVG if self.dp_avg else dist.ReduceOp.SUM
+                dws = []
+                for gi, g in enumerate(self.groups):
+                    out = self._shard_out(gi) if self.shard_grads is not None else g.grad_buf
+                    dws.append((out, _watchdog.track(f'{self.name}.dp_allreduce[{gi}]', dist.all_reduce(
+                        out, op=op, group=self.dp_pg, async_op=True), self.dp_world)))
+                for out, w in dws:
+                    w.wait()
+                    if not self.dp_avg:
+                        out.div_(self.dp_world)
+        if self.accumulate:
+            for gi in range(len(self.groups)):
+                if not self.fresh[gi]:
+                    self.shard_grads[gi].add_(self._scratch[gi])
+                self.fresh[gi] = False
         self.works.clear()
+        self.dp_works.clear()
         self.counts = [0] * len(self.groups)
         self.launched = [False] * len(self.groups)
         self._cb_queued = False

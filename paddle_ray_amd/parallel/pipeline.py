@@ -169,9 +169,15 @@ class PipelineLayer(Layer):
         return out
 
     def _synchronize_shared_weights(self):
+        from ..distributed import collective as C
+        me = C.get_rank()
         for key, (g, ranks, _) in self._shared_comm.items():
             for p in self._shared_params(key):
                 dist.broadcast(p._t.data, ranks[0], group=g.process_group)
+            # the global-norm clip counts a tied weight once: on its first owner only
+            # (parity: pp_layers.py:485-496 is_firstly_shared)
+            for p in self.shared_layers[key].parameters():
+                p.is_firstly_shared = me == ranks[0]
 
     def allreduce_shared_weight_gradients(self):
         for key, (g, ranks, _) in self._shared_comm.items():
@@ -215,11 +221,23 @@ _META_LEN = 64
 
 
 class _P2P:
-    """Point-to-point activation / gradient exchange on the pipe group's ring (the wrap
-    from the last stage to the first is used by the interleaved schedule). Activations may
-    be tuples; only floating tensors carry gradients back."""
+    """Point-to-point activation / gradient exchange between pipeline stages.
 
-    def __init__(self, hcg):
+    Every DIRECTED channel has its own 2-rank communicator: activations s -> s+1, gradients
+    s+1 -> s, and (interleaved schedule only) the ring wrap: activations from the last stage
+    to the first and gradients back (parity: the send_next / recv_prev groups of
+    pp_utils/p2p_communication.py). On RCCL a communicator is one stream per rank and
+    transfers on it are matched in issue order, so a channel with exactly one sender and one
+    receiver, both walking the same schedule, can never pair a send with the wrong receive,
+    and an activation send never queues behind (or waits for) a gradient transfer travelling
+    the other way — the cycle a shared per-pair communicator forms once a message is larger
+    than the RCCL staging buffer. Sends are asynchronous (the host never blocks on them);
+    receives make the compute stream wait for the transfer. A sent tensor is released as
+    soon as its send has completed (checked at every new send), not at batch end.
+    Activations may be tuples; only floating tensors carry gradients back."""
+
+    def __init__(self, hcg, virtual=1):
+        from ..distributed import collective as C
         self.hcg = hcg
         self.stage = hcg.get_stage_id()
         self.nstages = hcg.get_pipe_parallel_world_size()
@@ -231,56 +249,91 @@ class _P2P:
         self.dev = torch.device('cuda', torch.cuda.current_device()) \
             if torch.cuda.is_available() and dist.get_backend(self.pg) == 'nccl' else \
             torch.device('cpu')
-        self.meta_from = {}   # peer -> [(shape, dtype)] of what that peer sends us
+        # channels: (kind, src_stage, dst_stage) -> process group; created by every rank for
+        # every pipe group in one global order (new_group is collective)
+        n = self.nstages
+        edges = [('act', s, s + 1) for s in range(n - 1)] + [('grad', s + 1, s) for s in range(n - 1)]
+        if virtual > 1:
+            edges += [('act', n - 1, 0), ('grad', 0, n - 1)]
+        self.chan = {}
+        me = C.get_rank()
+        for pipe_ranks in hcg.topology().get_comm_list('pipe'):
+            for kind, a, b in edges:
+                grp = C.new_group([pipe_ranks[a], pipe_ranks[b]])
+                if me in (pipe_ranks[a], pipe_ranks[b]):
+                    self.chan[(kind, a, b)] = grp.process_group
+        self.meta_from = {}   # channel -> [(shape, dtype)] of what arrives on it
         self.meta_sent = set()
-        self.pending = []     # (work, tensor) isends to wait for before the batch ends
+        self.pending = []     # (work, tensor) isends not yet known to be complete
+        self.peak_pending = 0
 
-    def _isend(self, t, peer, what):
+    def _ch(self, kind, a, b):
+        return self.chan[(kind, a % self.nstages, b % self.nstages)]
+
+    def _prune(self):
+        self.pending = [(w, t) for w, t in self.pending if not w.is_completed()]
+
+    def _isend(self, t, peer, pg, what):
         t = t.detach().contiguous()
-        w = _watchdog.track(f'pp.{what}', dist.isend(t, peer, group=self.pg), 2)
+        self._prune()
+        w = _watchdog.track(f'pp.{what}', dist.isend(t, peer, group=pg), 2)
         self.pending.append((w, t))
+        self.peak_pending = max(self.peak_pending, len(self.pending))
 
-    def _recv(self, t, peer, what):
-        _watchdog.track(f'pp.{what}', dist.irecv(t, peer, group=self.pg), 2).wait()
+    def _recv(self, t, peer, pg, what):
+        _watchdog.track(f'pp.{what}', dist.irecv(t, peer, group=pg), 2).wait()
         return t
 
-    def send_acts(self, acts, peer):
+    def send_acts(self, acts, dst_stage):
+        pg = self._ch('act', self.stage, dst_stage)
+        peer = self.ranks[dst_stage % self.nstages]
         ts = [t for t in acts if isinstance(t, torch.Tensor)]
-        if peer not in self.meta_sent:
-            m = torch.zeros(_META_LEN, dtype=torch.int64, device=self.dev)
+        if pg not in self.meta_sent:
+            m = torch.zeros(_META_LEN, dtype=torch.int64)
             m[0] = len(ts)
             k = 1
             for t in ts:
                 m[k], m[k + 1] = t.dim(), _DT_CODES.index(t.dtype)
                 m[k + 2:k + 2 + t.dim()] = torch.tensor(list(t.shape))
                 k += 2 + t.dim()
-            self._isend(m, peer, 'meta')
-            self.meta_sent.add(peer)
+            self._isend(m.to(self.dev), peer, pg, 'meta')
+            self.meta_sent.add(pg)
         for t in ts:
-            self._isend(t, peer, 'send_fwd')
+            self._isend(t, peer, pg, 'send_fwd')
 
-    def recv_acts(self, peer):
-        if peer not in self.meta_from:
-            m = self._recv(torch.zeros(_META_LEN, dtype=torch.int64, device=self.dev), peer, 'meta')
+    def recv_acts(self, src_stage):
+        pg = self._ch('act', src_stage, self.stage)
+        peer = self.ranks[src_stage % self.nstages]
+        if pg not in self.meta_from:
+            m = self._recv(torch.zeros(_META_LEN, dtype=torch.int64, device=self.dev), peer, pg,
+                           'meta').cpu()
             n, k, meta = int(m[0]), 1, []
             for _ in range(n):
                 nd, dt = int(m[k]), _DT_CODES[int(m[k + 1])]
                 meta.append((tuple(int(v) for v in m[k + 2:k + 2 + nd]), dt))
                 k += 2 + nd
-            self.meta_from[peer] = meta
+            self.meta_from[pg] = meta
         out = []
-        for shp, dt in self.meta_from[peer]:
-            t = self._recv(torch.empty(shp, dtype=dt, device=self.dev), peer, 'recv_fwd')
+        for shp, dt in self.meta_from[pg]:
+            t = self._recv(torch.empty(shp, dtype=dt, device=self.dev), peer, pg, 'recv_fwd')
             out.append(t.requires_grad_(t.is_floating_point()))
         return out
 
-    def send_grads(self, grads, peer):
+    def send_grads(self, grads, dst_stage):
+        pg = self._ch('grad', self.stage, dst_stage)
+        peer = self.ranks[dst_stage % self.nstages]
         for g in grads:
-            self._isend(g, peer, 'send_bwd')
+            self._isend(g, peer, pg, 'send_bwd')
 
-    def recv_grads(self, like, peer):
-        return [self._recv(torch.empty_like(t), peer, 'recv_bwd') for t in like
+    def recv_grads(self, like, src_stage):
+        pg = self._ch('grad', src_stage, self.stage)
+        peer = self.ranks[src_stage % self.nstages]
+        return [self._recv(torch.empty_like(t), peer, pg, 'recv_bwd') for t in like
                 if t.is_floating_point()]
+
+    def new_batch(self):
+        self.meta_from.clear()
+        self.meta_sent.clear()  # both sides re-exchange activation meta every batch
 
     def flush(self):
         for w, _ in self.pending:
@@ -288,8 +341,27 @@ class _P2P:
         self.pending.clear()
 
 
+def interleaved_order(M, nstages, V, stage):
+    """The interleaved 1F1B schedule of one stage (parity: pipeline_parallel.py:535-760,
+    PipelineParallelWithInterleave): forward unit k runs chunk ``(k // nstages) % V`` on
+    micro-batch ``(k // (nstages * V)) * nstages + k % nstages``; backward unit k runs the
+    mirrored chunk ``V - 1 - (k // nstages) % V`` on the same micro-batch formula. Returns
+    (warmup, [('F'|'B', k), ...]): ``warmup`` forward units first (startup), then one
+    forward + one backward per step (steady), then the remaining backwards (cooldown)."""
+    total = M * V
+    if M == nstages:
+        warmup = total
+    else:
+        warmup = min((nstages - stage - 1) * 2 + (V - 1) * nstages, total)
+    seq = [('F', k) for k in range(warmup)]
+    for i in range(total - warmup):
+        seq += [('F', warmup + i), ('B', i)]
+    seq += [('B', k) for k in range(total - warmup, total)]
+    return warmup, seq
+
+
 class PipelineParallel(Layer):
-    def __init__(self, layers, hcg, strategy):
+    def __init__(self, layers, hcg, strategy, sharded_state=None):
         super().__init__()
         self._layers = layers
         self._hcg = hcg
@@ -298,12 +370,23 @@ class PipelineParallel(Layer):
         self.accumulate_steps = cfg.get('accumulate_steps', 1)
         self.is_first = hcg.is_first_stage()
         self.is_last = hcg.is_last_stage()
-        self._p2p = _P2P(hcg) if hcg.get_pipe_parallel_world_size() > 1 else None
+        V = layers._num_virtual if isinstance(layers, PipelineLayer) else 1
+        self._p2p = _P2P(hcg, V) if hcg.get_pipe_parallel_world_size() > 1 else None
         self.total_loss = None
+        self.peak_live_units = 0
         self._dp_group = hcg.get_data_parallel_group()
         self._dp_reducer = None
-        if self._dp_group is not None and self._dp_group.nranks > 1:
+        self._state = sharded_state
+        if sharded_state is not None:
+            # pipeline x sharding (stage 1): the sharding state's bucket reducer all-reduces
+            # this stage's gradients over the sharding group (+ dp), the sharded optimizer
+            # updates the owned shards and all-gathers the new parameters
+            self._dp_reducer = sharded_state.reducer
+        elif self._dp_group is not None and self._dp_group.nranks > 1:
             self._build_dp_buckets(strategy)
+        if self._dp_reducer is not None:
+            self._dp_reducer.enabled = False
+            self._dp_reducer.auto_finalize = False  # the schedule decides when to finalize
 
     def _build_dp_buckets(self, strategy):
         """Flat gradient buckets over this stage's parameters, all-reduced over the dp group
@@ -318,7 +401,6 @@ class PipelineParallel(Layer):
         self._dp_groups = [FlatGroup(b) for b in group_params_into_buckets(params, int(mb) << 20)]
         self._dp_reducer = GradBucketReducer(self._dp_groups, g.process_group, g.nranks,
                                              'allreduce', name='pp.dp_bucket')
-        self._dp_reducer.enabled = False
 
     def forward(self, *a, **k):
         return self._layers(*a, **k)
@@ -374,10 +456,10 @@ class PipelineParallel(Layer):
                     y = _u(scaler.scale(Tensor(y)))
                 y.backward()
                 losses.append(y.detach())
+            self.peak_live_units = 1
             self.total_loss = torch.stack(losses).sum()
             return self.total_loss
-        p2p.meta_from.clear()
-        p2p.meta_sent.clear()  # both sides re-exchange activation meta every batch
+        p2p.new_batch()
         if self._layers._num_virtual > 1:
             losses = self._interleaved(inputs, labels, M, scaler)
         else:
@@ -398,27 +480,29 @@ class PipelineParallel(Layer):
         warmup = min(nst - st - 1, M)
         pending, losses = [], []
         nb = [0]
+        self.peak_live_units = 0
 
         def fwd(i):
-            xs = self._first_inputs(inputs, i) if self.is_first else p2p.recv_acts(p2p.prev)
+            xs = self._first_inputs(inputs, i) if self.is_first else p2p.recv_acts(st - 1)
             ys = self._run_chunk(xs, self._micro(labels, i), 0, True)
             if self.is_last:
                 if scaler is not None:
                     ys = [_u(scaler.scale(Tensor(ys[0])))]
                 losses.append(ys[0].detach())
             else:
-                p2p.send_acts(ys, p2p.next)
+                p2p.send_acts(ys, st + 1)
             pending.append((xs, ys))
+            self.peak_live_units = max(self.peak_live_units, len(pending))
 
         def bwd():
             xs, ys = pending.pop(0)
-            gys = [None] if self.is_last else p2p.recv_grads(ys, p2p.next)
+            gys = [None] if self.is_last else p2p.recv_grads(ys, st + 1)
             nb[0] += 1
             if self._dp_reducer is not None:
                 self._dp_reducer.enabled = nb[0] == M  # last micro-batch: launch bucket reduces
             dxs = self._backward(xs, ys, gys)
             if not self.is_first:
-                p2p.send_grads(dxs, p2p.prev)
+                p2p.send_grads(dxs, st - 1)
 
         for i in range(warmup):
             fwd(i)
@@ -429,38 +513,60 @@ class PipelineParallel(Layer):
             bwd()
         return losses
 
-    # -- interleaved (virtual stages) ----------------------------------------------------------
+    # -- interleaved 1F1B (virtual stages) -----------------------------------------------------
     def _interleaved(self, inputs, labels, M, scaler):
-        """Depth-first over virtual chunks: every stage runs chunk v for all micro-batches,
-        handing activations around the ring (last stage -> first stage between chunks), then
-        the backward in exactly the reverse order. Sends are asynchronous, receives block, and
-        every peer pair sees one consistent order, so no cycle of waits can form."""
+        """Interleaved 1F1B over V virtual chunks per stage (``interleaved_order``): startup
+        forwards, then alternating one forward / one backward, then the cooldown backwards.
+        Chunk v of the last stage feeds chunk v+1 of the first stage over the ring-wrap
+        channel (and gradients travel back the same way). At most ``warmup + 1`` units keep
+        their activations alive at once, independent of the number of micro-batches."""
         p2p = self._p2p
         V = self._layers._num_virtual
         nst, st = p2p.nstages, p2p.stage
+        if M % nst:
+            raise ValueError(f"interleaved pipeline needs accumulate_steps ({M}) to be a "
+                             f"multiple of the pipeline degree ({nst})")
         bufs, losses = {}, []
-        for v in range(V):
-            first_chunk = st == 0 and v == 0
-            last_chunk = st == nst - 1 and v == V - 1
-            for m in range(M):
-                xs = self._first_inputs(inputs, m) if first_chunk else p2p.recv_acts(p2p.prev)
-                ys = self._run_chunk(xs, self._micro(labels, m), v, v == V - 1)
-                if last_chunk:
-                    if scaler is not None:
-                        ys = [_u(scaler.scale(Tensor(ys[0])))]
-                    losses.append(ys[0].detach())
-                else:
-                    p2p.send_acts(ys, p2p.next)
-                bufs[(v, m)] = (xs, ys)
-        for v in reversed(range(V)):
-            first_chunk = st == 0 and v == 0
-            last_chunk = st == nst - 1 and v == V - 1
-            for m in range(M):
-                xs, ys = bufs.pop((v, m))
-                gys = [None] if last_chunk else p2p.recv_grads(ys, p2p.next)
-                dxs = self._backward(xs, ys, gys)
-                if not first_chunk:
-                    p2p.send_grads(dxs, p2p.prev)
+        self.peak_live_units = 0
+
+        def chunk(k, fwd):
+            v = (k // nst) % V
+            return v if fwd else V - 1 - v
+
+        def micro(k):
+            return (k // (nst * V)) * nst + k % nst
+
+        def fwd(k):
+            v, m = chunk(k, True), micro(k)
+            if st == 0 and v == 0:
+                xs = self._first_inputs(inputs, m)
+            else:
+                xs = p2p.recv_acts(st - 1)   # stage 0 (v > 0): from the last stage, ring wrap
+            ys = self._run_chunk(xs, self._micro(labels, m), v, v == V - 1)
+            if st == nst - 1 and v == V - 1:
+                if scaler is not None:
+                    ys = [_u(scaler.scale(Tensor(ys[0])))]
+                losses.append(ys[0].detach())
+            else:
+                p2p.send_acts(ys, st + 1)
+            bufs[(v, m)] = (xs, ys)
+            self.peak_live_units = max(self.peak_live_units, len(bufs))
+
+        def bwd(k):
+            v, m = chunk(k, False), micro(k)
+            xs, ys = bufs.pop((v, m))
+            last = st == nst - 1 and v == V - 1
+            gys = [None] if last else p2p.recv_grads(ys, st + 1)
+            if self._dp_reducer is not None:
+                # the last micro-batch of each chunk completes that chunk's gradients
+                self._dp_reducer.enabled = m == M - 1
+            dxs = self._backward(xs, ys, gys)
+            if not (st == 0 and v == 0):
+                p2p.send_grads(dxs, st - 1)
+
+        _, seq = interleaved_order(M, nst, V, st)
+        for op, k in seq:
+            fwd(k) if op == 'F' else bwd(k)
         return losses
 
     # -- gradient reduction + step --------------------------------------------------------------
@@ -469,21 +575,19 @@ class PipelineParallel(Layer):
         if r is None:
             return
         r.enabled = True
-        for gi in range(len(r.groups)):
-            r._launch(gi)
         r.finalize()
 
     def train_batch(self, data, optimizer, lr_scheduler=None, scaler=None):
         self._layers.train()
-        if self._dp_reducer is not None:
+        if self._state is not None:
+            self._state.before_forward()
+        elif self._dp_reducer is not None:
             for g in self._dp_groups:
                 if g.grads_missing():
                     g.grad_buf.zero_()
                     g.reattach_grads()
-        before = self._dp_reducer.finalize_count if self._dp_reducer is not None else 0
         loss = self.forward_backward_pipeline(data, scaler)
-        if self._dp_reducer is not None and self._dp_reducer.finalize_count == before:
-            self._reduce_dp()  # interleaved schedule (or no hook fired): reduce all buckets now
+        self._reduce_dp()  # launches what the hooks did not and waits for every bucket
         self._layers.allreduce_shared_weight_gradients()
         if self._dp_reducer is not None:
             self._dp_reducer.enabled = False

@@ -107,7 +107,7 @@ class ShardedState:
 
     def __init__(self, layer, level, group=None, segment_bytes=128 << 20, grad_fp32=False,
                  dp_group=None, segment_size=2 ** 20, exclude_layer=None,
-                 release_after_forward=True):
+                 release_after_forward='auto'):
         from ..distributed import collective as C
         self.layer = layer
         self.stage = LEVELS[level] if isinstance(level, str) else int(level)
@@ -120,10 +120,11 @@ class ShardedState:
         self.dp_world = 1 if dp_group is None else dp_group.nranks
         params = [p for p in layer.parameters() if not p.stop_gradient]
         if self.world > 1 or self.dp_world > 1:
-            for grp, pg in ((group, self.pg), (dp_group, self.dp_pg)):
-                if grp is not None and grp.nranks == 1:
-                    continue
-                if grp is None and self.world == 1:
+            # the sharding group (None = the whole job) and, in hybrid dp x sharding, the dp
+            # group (None = no dp replicas: nothing to broadcast there)
+            for i, (grp, pg, n) in enumerate(((group, self.pg, self.world),
+                                              (dp_group, self.dp_pg, self.dp_world))):
+                if n == 1 or (i == 1 and dp_group is None):
                     continue
                 src = grp.ranks[0] if grp is not None else 0
                 for t in [p._t for p in layer.parameters()] + [b._t for b in layer.buffers()]:
@@ -160,7 +161,14 @@ class ShardedState:
         self.unit_meta = [u for u in self.unit_meta if u.gids]
         for i, u in enumerate(self.unit_meta):
             u.index = i
-        self.release_after_forward = release_after_forward
+        self.release_after_forward = self._resolve_release(release_after_forward)
+        # ZeRO-3 all-gathers run on their own communicator (own RCCL stream), so the backward
+        # prefetch of unit i-1 is not queued behind unit i's gradient reduce-scatter
+        self.ag_pg = self.pg
+        if self.zero3:
+            from ..distributed import collective as C
+            self.ag_group = C.twin_group(group)
+            self.ag_pg = self.ag_group.process_group
         self.shard_grads = [g.shard(g.grad_buf) if self.world == 1 else
                             torch.zeros(g.shard_numel, dtype=g.grad_dtype, device=g.device)
                             for g in self.groups]
@@ -172,7 +180,7 @@ class ShardedState:
             self.groups, self.pg, self.world, mode, self.shard_grads, dp_pg=self.dp_pg,
             dp_world=self.dp_world, on_launch=self._on_grads_launched if self.zero3 else None,
             on_finalize=self._on_backward_done if self.zero3 else None,
-            name=f'sharding{self.stage}') \
+            name=f'sharding{self.stage}', accumulate=self.zero3) \
             if self.stage > 1 or self.world > 1 or self.dp_world > 1 else None
         self.gather_works = {}
         self.params_stale = False
@@ -196,6 +204,26 @@ class ShardedState:
                     self.groups[gi].release_params()
                     self.groups[gi].release_grads()
 
+    def _resolve_release(self, mode):
+        """``release_after_forward``: True frees every unit after its forward and re-gathers
+        it in backward (minimum memory); False keeps the gathered units resident from their
+        forward to their gradient reduce-scatter (no backward re-gather traffic); 'auto' keeps
+        them when the full unit parameters fit in ``PRA_ZERO3_RESIDENT_FRAC`` (default 0.25) of
+        the device memory — SURVEY §3: with 288 GB per MI355X a 1.3B model's gathered bf16
+        weights (2.6 GB) are about 1 % of HBM."""
+        if mode != 'auto':
+            return bool(mode)
+        env = __import__('os').environ.get('PRA_ZERO3_RESIDENT')
+        if env is not None:
+            return env in ('0', 'false', 'False')
+        if not self.zero3 or not self.groups or self.groups[0].device.type != 'cuda':
+            return True
+        unit_bytes = sum(self.groups[gi].numel * self.groups[gi].param_buf.element_size()
+                         for u in self.unit_meta for gi in u.gids)
+        total = torch.cuda.get_device_properties(self.groups[0].device).total_memory
+        frac = float(__import__('os').environ.get('PRA_ZERO3_RESIDENT_FRAC', '0.25'))
+        return unit_bytes > frac * total
+
     # -- memory accounting ----------------------------------------------------------------
     def resident_bytes(self):
         return sum(g.resident_bytes() for g in self.groups)
@@ -216,7 +244,7 @@ class ShardedState:
             return
         g.materialize_params()
         self.gather_works[gi] = _watchdog.track(f'sharding3.all_gather[{gi}]', dist.all_gather_into_tensor(
-            g.param_buf, g.param_shard, group=self.pg, async_op=True), self.world)
+            g.param_buf, g.param_shard, group=self.ag_pg, async_op=True), self.world)
         self._note_peak()
 
     def _gather_unit(self, u, wait):
@@ -355,6 +383,8 @@ class ShardedState:
         if self.stage > 1 and self.world > 1:
             for s in self.shard_grads:
                 s.zero_()
+        if self.reducer is not None:
+            self.reducer.reset_accumulation()
 
     def params_loaded(self):
         """Full parameter values were written into the gathered buffers (set_state_dict):
@@ -457,17 +487,27 @@ class ShardedOptimizer:
         def nsq(ts):
             return K.global_l2_norm_sq(ts).reshape(1).float() if ts else \
                 torch.zeros(1, device=dev)
-        # owned shards partition the gradients: local sum of squares + one all-reduce
-        if self._mp_pg is None:
+        # owned shards partition the gradients: local sum of squares + one all-reduce. A
+        # pipeline-tied weight (is_firstly_shared False on all but its first owner stage) is
+        # counted once, so its pieces are left out on the other stages.
+        tied = [pc for pc in self._pieces if not getattr(pc[1], 'is_firstly_shared', True)]
+        if self._mp_pg is None and tied:
+            gs = st.shard_grads
+            sq = nsq([gs[gi][lo:hi] for gi, p, lo, hi, _ in self._pieces
+                      if getattr(p, 'is_firstly_shared', True)])
+            if st.world > 1:
+                dist.all_reduce(sq, group=st.pg)
+        elif self._mp_pg is None:
             sq = nsq(st.shard_grads)
             if st.world > 1:
                 dist.all_reduce(sq, group=st.pg)
         else:
             # TP-split parameters are summed over the mp group, replicated ones counted once
             gs = st.shard_grads
-            d = [gs[gi][lo:hi] for gi, p, lo, hi, _ in self._pieces if getattr(p, 'is_distributed', False)]
+            d = [gs[gi][lo:hi] for gi, p, lo, hi, _ in self._pieces
+                 if getattr(p, 'is_distributed', False) and getattr(p, 'is_firstly_shared', True)]
             r = [gs[gi][lo:hi] for gi, p, lo, hi, _ in self._pieces
-                 if not getattr(p, 'is_distributed', False)]
+                 if not getattr(p, 'is_distributed', False) and getattr(p, 'is_firstly_shared', True)]
             both = torch.cat([nsq(d), nsq(r)])
             if st.world > 1:
                 dist.all_reduce(both, group=st.pg)
@@ -659,10 +699,11 @@ class ShardedOptimizer:
                 if self._kind in ('Adam', 'AdamW'):
                     o = self._inner
                     for p in g.params:
+                        # reference convention: beta**(t+1) after t updates (adamw.py:343-348)
                         sd[f'{p.name}_beta1_pow_acc_0'] = Tensor(
-                            torch.tensor([o._beta1 ** self._step], dtype=torch.float32))
+                            torch.tensor([o._beta1 ** (self._step + 1)], dtype=torch.float32))
                         sd[f'{p.name}_beta2_pow_acc_0'] = Tensor(
-                            torch.tensor([o._beta2 ** self._step], dtype=torch.float32))
+                            torch.tensor([o._beta2 ** (self._step + 1)], dtype=torch.float32))
             if masters:
                 sd['master_weights'] = masters
         sd['@step'] = self._step
@@ -701,8 +742,8 @@ class ShardedOptimizer:
         if step is None and self._kind in ('Adam', 'AdamW'):
             b1 = [v for k, v in sd.items() if isinstance(k, str) and k.endswith('_beta1_pow_acc_0')]
             if b1:
-                step = int(round(math.log(float(_u(b1[0]).reshape(-1)[0])) /
-                                 math.log(self._inner._beta1)))
+                from ..optimizer.optimizer import beta_pow_to_step
+                step = beta_pow_to_step(b1[0], self._inner._beta1)
         if step is not None:
             self._step = int(step)
         if 'LR_Scheduler' in sd:
@@ -774,14 +815,15 @@ class ShardedModel(Layer):
 def group_sharded_parallel(model, optimizer, level, scaler=None, group=None, offload=False,
                            sync_buffers=False, buffer_max_size=2 ** 23, segment_size=2 ** 20,
                            sync_comm=False, dp_group=None, exclude_layer=None,
-                           bucket_mb=128):
+                           bucket_mb=128, release_after_forward='auto'):
     """paddle.distributed.sharding.group_sharded_parallel (parity:
     python/paddle/distributed/sharding/group_sharded.py). ``offload=True`` keeps the fp32
     master weights and optimizer moments in host memory (the update runs on the CPU)."""
     if level not in LEVELS:
         raise ValueError(f"level must be one of {list(LEVELS)}")
     st = ShardedState(model, level, group, segment_bytes=bucket_mb << 20, dp_group=dp_group,
-                      segment_size=segment_size, exclude_layer=exclude_layer)
+                      segment_size=segment_size, exclude_layer=exclude_layer,
+                      release_after_forward=release_after_forward)
     # the (bucketed, flat) params were re-pointed in place: the inner optimizer's list stays valid
     sopt = ShardedOptimizer(optimizer, st, offload=offload)
     if scaler is not None:

@@ -142,3 +142,24 @@ def test_sharded_checkpoint_resumes_at_world_size_1(tmp_path):
     _train(r, ro, xs, ys, 4)
     for a, b in zip(m.parameters(), r.parameters()):
         np.testing.assert_allclose(a.numpy(), b.numpy(), rtol=2e-4, atol=2e-5)
+
+
+def test_adam_beta_pow_reference_convention():
+    """beta{1,2}_pow_acc follow the reference (adamw.py:343-348): beta**(t+1) after t updates,
+    and a file without '@step' resumes at step t."""
+    import paddle_ray_amd as paddle
+    lin = paddle.nn.Linear(3, 2)
+    opt = paddle.optimizer.AdamW(0.1, beta1=0.8, beta2=0.9, parameters=lin.parameters())
+    for _ in range(3):
+        lin(paddle.ones([2, 3])).sum().backward()
+        opt.step()
+        opt.clear_grad()
+    sd = opt.state_dict()
+    key = [k for k in sd if k.endswith('_beta1_pow_acc_0')][0]
+    np.testing.assert_allclose(float(sd[key]), 0.8 ** 4, rtol=1e-6)
+    k2 = key.replace('beta1', 'beta2')
+    np.testing.assert_allclose(float(sd[k2]), 0.9 ** 4, rtol=1e-6)
+    sd.pop('@step')
+    opt2 = paddle.optimizer.AdamW(0.1, beta1=0.8, beta2=0.9, parameters=lin.parameters())
+    opt2.set_state_dict(sd)
+    assert opt2._step_count == 3

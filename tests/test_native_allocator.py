@@ -114,3 +114,31 @@ def test_training_on_native_allocator_gpu():
     r = subprocess.run([sys.executable, '-c', _GPU_SCRIPT], env=env, capture_output=True, text=True,
                        timeout=300, cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     assert r.returncode == 0 and 'OK' in r.stdout, r.stdout[-2000:] + r.stderr[-3000:]
+
+
+def test_split_remainder_keeps_pending_gate(lib):
+    """A block reused by its own stream while its free-time event is still pending is split:
+    the remainder must stay gated (another stream may not take it until that work is done)."""
+    dev = 41
+    lib.pra_alloc_set_growth(dev, 2 * MB)
+    s1, s2 = 0x1000, 0x2000
+    a = _alloc(lib, dev, 2 * MB, s1)           # chunk 1 is exactly a
+    warm = _alloc(lib, dev, 1 * MB, s2)        # second stream (chunk 2): events recorded from now on
+    lib.pra_alloc_host_set_pending(1)
+    try:
+        lib.pra_free(a, 2 * MB, dev, ctypes.c_void_p(s1))   # pending: s1 work may still use it
+        b = _alloc(lib, dev, 256 << 10, s1)                # same stream: reuses a, splits it
+        assert b == a
+        # 1.5 MB fits only in a's 1.75 MB remainder among existing free blocks
+        c = _alloc(lib, dev, 3 * MB // 2, s2)
+        assert not (a <= c < a + 2 * MB), "remainder handed to another stream before its event"
+        lib.pra_alloc_host_complete_events()
+        d = _alloc(lib, dev, 3 * MB // 2, s2)                # gate passed: now it may
+        assert a <= d < a + 2 * MB
+        assert lib.pra_alloc_check(dev) == 1
+        for p, n, s in ((b, 256 << 10, s1), (c, 3 * MB // 2, s2), (d, 3 * MB // 2, s2),
+                        (warm, MB, s2)):
+            lib.pra_free(p, n, dev, ctypes.c_void_p(s))
+    finally:
+        lib.pra_alloc_host_set_pending(0)
+        lib.pra_alloc_host_complete_events()

@@ -140,7 +140,8 @@ def _pp_worker(rank, world, pp, dp, virtual, steps=3, n_micro=4, mbs=2):
         losses.append(float(model.train_batch(
             [paddle.to_tensor(xs[d * n:(d + 1) * n]), paddle.to_tensor(ys[d * n:(d + 1) * n])], opt)))
     embw = pl.shared_layers['embed'].weight.numpy() if 'embed' in pl.shared_layers else None
-    return {'losses': losses, 'emb': embw, 'stage': hcg.get_stage_id(), 'dp': d, 'nst': nst}
+    return {'losses': losses, 'emb': embw, 'stage': hcg.get_stage_id(), 'dp': d, 'nst': nst,
+            'peak': model.peak_live_units}
 
 
 def test_pp2_tied_embedding_and_tuple_acts(tmp_path):
@@ -195,3 +196,118 @@ def test_ernie_pipe_tied_embeddings(tmp_path):
     res = run_ranks(_ernie_tied_worker, 2, tmp_path)
     np.testing.assert_allclose(res[0]['emb'], res[1]['emb'], rtol=1e-6, atol=1e-7)
     assert res[0]['losses'][-1] < res[0]['losses'][0]
+
+
+# -- interleaved 1F1B schedule, bounded activations, pp x sharding ----------------------------
+def test_interleaved_order_is_a_valid_1f1b():
+    from paddle_ray_amd.parallel.pipeline import interleaved_order
+    for nst, V, M in [(2, 2, 4), (2, 2, 8), (4, 2, 8), (4, 3, 12), (2, 3, 2)]:
+        for st in range(nst):
+            warmup, seq = interleaved_order(M, nst, V, st)
+            fw = [k for op, k in seq if op == 'F']
+            bw = [k for op, k in seq if op == 'B']
+            assert fw == list(range(M * V)) and bw == list(range(M * V))
+            live, peak = 0, 0
+            for op, _ in seq:
+                live += 1 if op == 'F' else -1
+                peak = max(peak, live)
+            # live activations are bounded by the startup depth, not by M
+            assert peak == min(warmup + 1, M * V) if M != nst else peak == M * V
+            if M > nst:
+                assert peak <= (nst - st - 1) * 2 + (V - 1) * nst + 1
+
+
+def _pp_peak_worker(rank, world, n_micro):
+    r = _pp_worker(rank, world, 2, 1, 2, steps=1, n_micro=n_micro)
+    return r
+
+
+def test_interleaved_peak_live_units_independent_of_microbatches(tmp_path):
+    import paddle_ray_amd  # noqa: F401
+    peaks = {}
+    for n_micro in (4, 8):
+        (tmp_path / str(n_micro)).mkdir()
+        res = run_ranks(_pp_peak_worker, 2, tmp_path / str(n_micro), (n_micro,))
+        peaks[n_micro] = [r['peak'] for r in sorted(res, key=lambda r: r['stage'])]
+        ref, _ = _single(1, n_micro, 2)
+        for r in res:
+            np.testing.assert_allclose(r['losses'], ref, rtol=1e-4, atol=1e-6)
+    # stage 0 (deepest startup): (2-0-1)*2 + (2-1)*2 + 1 = 5 live units; stage 1: 3
+    assert peaks[4] == peaks[8] == [5, 3], peaks
+    assert all(p <= 2 * 2 + 2 for p in peaks[8])  # far below V * M = 16
+
+
+def _pp_sharding_worker(rank, world, steps=3, n_micro=4, mbs=2):
+    import paddle_ray_amd as paddle
+    from paddle_ray_amd.distributed import fleet
+    from paddle_ray_amd.parallel.pipeline import PipelineLayer
+    st = fleet.DistributedStrategy()
+    st.hybrid_configs = {'dp_degree': 1, 'mp_degree': 1, 'pp_degree': 2, 'sharding_degree': 2}
+    st.sharding_configs = {'stage': 1}
+    st.pipeline_configs = {'micro_batch_size': mbs, 'accumulate_steps': n_micro}
+    fleet.init(is_collective=True, strategy=st)
+    hcg = fleet.get_hybrid_communicate_group()
+    paddle.seed(100 + rank)
+    pl = PipelineLayer(_descs(), loss_fn=_loss)
+    emb, body, head = _build_full()
+    full = [emb] + body + [emb]
+    part = hcg.get_stage_id()
+    lo, hi = pl.segment_parts[part], pl.segment_parts[part + 1]
+    for i in range(lo, hi):
+        if not hasattr(pl._layers_desc[i], 'layer_name'):
+            pl._chunks[0][i - lo].set_state_dict(full[i].state_dict())
+    if hcg.get_stage_id() == 0:
+        pl.shared_layers['embed'].set_state_dict(emb.state_dict())
+    pl._synchronize_shared_weights()
+    opt = paddle.optimizer.AdamW(0.05, parameters=pl.parameters(), weight_decay=0.01,
+                                 grad_clip=paddle.nn.ClipGradByGlobalNorm(1.0))
+    model = fleet.distributed_model(pl)
+    opt = fleet.distributed_optimizer(opt)
+    xs, ys = _data(n_micro * mbs * 2)
+    d = hcg.get_sharding_parallel_rank()
+    n = n_micro * mbs
+    for _ in range(steps):
+        model.train_batch([paddle.to_tensor(xs[d * n:(d + 1) * n]),
+                           paddle.to_tensor(ys[d * n:(d + 1) * n])], opt)
+    params = {}
+    for v, fns in enumerate(pl._chunks):
+        for i, f in enumerate(fns):
+            idx = pl.segment_parts[part] + i
+            if hasattr(f, 'parameters') and not hasattr(pl._layers_desc[idx], 'layer_name'):
+                params[idx] = [p.numpy() for p in f.parameters()]
+    return {'stage': hcg.get_stage_id(), 'sh': hcg.get_sharding_parallel_world_size(),
+            'emb': pl.shared_layers['embed'].weight.numpy(), 'params': params,
+            'sharded': type(opt).__name__}
+
+
+def _single_adamw(steps=3, n_micro=4, mbs=2, slices=2):
+    import paddle_ray_amd as paddle
+    emb, body, head = _build_full()
+    params = emb.parameters() + [p for l in body for p in l.parameters()]
+    opt = paddle.optimizer.AdamW(0.05, parameters=params, weight_decay=0.01,
+                                 grad_clip=paddle.nn.ClipGradByGlobalNorm(1.0))
+    xs, ys = _data(n_micro * mbs * slices)
+    nm = n_micro * slices
+    for _ in range(steps):
+        for i in range(nm):
+            x = emb(paddle.to_tensor(xs[i * mbs:(i + 1) * mbs]))
+            for l in body:
+                x = l(x)
+            (_loss(head(emb, x), paddle.to_tensor(ys[i * mbs:(i + 1) * mbs])) / nm).backward()
+        opt.step()
+        opt.clear_grad()
+    full = [emb] + body + [emb]
+    return emb.weight.numpy(), {i: [p.numpy() for p in full[i].parameters()] for i in range(1, 6)}
+
+
+def test_pp2_sharding2_matches_single(tmp_path):
+    """pipeline x sharding stage 1 on 4 ranks: AdamW + global-norm clip with optimizer state
+    sharded inside each stage reproduces the single-process parameters."""
+    ref_emb, ref = _single_adamw()
+    res = run_ranks(_pp_sharding_worker, 4, tmp_path)
+    for r in res:
+        assert r['sh'] == 2 and r['sharded'] == 'ShardedOptimizer'
+        np.testing.assert_allclose(r['emb'], ref_emb, rtol=2e-4, atol=2e-5)
+        for idx, ps in r['params'].items():
+            for a, b in zip(ps, ref[idx]):
+                np.testing.assert_allclose(a, b, rtol=2e-4, atol=2e-5, err_msg=str(idx))
