@@ -17,7 +17,11 @@ reference's dy2static is used for:
 * **Program export**: ``concrete_program`` / ``jit.save`` record the layer into a static
   ``Program`` (static/graph.py) from ``InputSpec``s and write ``.pdmodel`` (JSON op list)
   + ``.pdiparams``; ``jit.load`` returns a ``TranslatedLayer`` that replays the program
-  eagerly, so it can run inference or be fine-tuned.
+  eagerly, so it can run inference or be fine-tuned. Before recording, the function's
+  tensor-valued ``if`` / ``while`` statements are converted (``dy2static.py``) into
+  ``static.nn.cond`` / ``while_loop`` sub-blocks, which serialize as nested op lists.
+* Graph replay hands out fresh output tensors on every call, and a function that cannot be
+  captured (host read of device data, data-dependent shapes) runs eagerly instead.
 """
 import functools
 import os
@@ -110,7 +114,31 @@ class _GraphEntry:
         for buf, t in zip(self.static_in, _flat_tensors((args, kwargs), [])):
             buf.copy_(t._t, non_blocking=True)
         self.graph.replay()
-        return self.out
+        # the captured outputs are the graph's static buffers, rewritten by the next replay:
+        # every call hands out its own copies (y1 = f(x1); y2 = f(x2) keeps y1)
+        return _clone_struct(self.out)
+
+
+def _clone_struct(o):
+    if isinstance(o, Tensor):
+        c = Tensor(o._t.clone())
+        c.stop_gradient = o.stop_gradient
+        return c
+    if isinstance(o, torch.Tensor):
+        return o.clone()
+    if isinstance(o, list):
+        return [_clone_struct(x) for x in o]
+    if isinstance(o, tuple):
+        return tuple(_clone_struct(x) for x in o)
+    if isinstance(o, dict):
+        return {k: _clone_struct(v) for k, v in o.items()}
+    return o
+
+
+class _Eager:
+    """Marks a signature whose capture failed (a host read of device data, a data-dependent
+    shape, a synchronising op): it runs eagerly from then on."""
+    reason = None
 
 
 class _TrainGraph:
@@ -275,15 +303,35 @@ class StaticFunction:
             g = self._graphs.get(key)
             if g is None:
                 params = self._layer.parameters() if self._layer is not None else []
-                g = self._graphs[key] = _TrainGraph(self._fn, params, args, kwargs)
-            return g(args, kwargs)
-        if self._use_graph(args, kwargs):
+                g = self._capture(key, lambda: _TrainGraph(self._fn, params, args, kwargs))
+            if not isinstance(g, _Eager):
+                return g(args, kwargs)
+        elif self._use_graph(args, kwargs):
             key = _signature(args, kwargs)
             g = self._graphs.get(key)
             if g is None:
-                g = self._graphs[key] = _GraphEntry(self._fn, args, kwargs)
-            return g(args, kwargs)
+                g = self._capture(key, lambda: _GraphEntry(self._fn, args, kwargs))
+            if not isinstance(g, _Eager):
+                return g(args, kwargs)
         return self._fn(*args, **kwargs)
+
+    def _capture(self, key, build):
+        """Capture a graph for ``key``; if the function cannot be captured the error is
+        swallowed, the half-built graph discarded, and the signature runs eagerly in this
+        process from then on (no restart, no retry per call)."""
+        try:
+            g = build()
+        except Exception as e:  # noqa: BLE001 - any capture failure means: not capturable
+            torch.cuda.synchronize()
+            g = _Eager()
+            g.reason = f'{type(e).__name__}: {e}'
+        self._graphs[key] = g
+        return g
+
+    def graph_status(self):
+        """{signature: 'graph' | 'eager (<why the capture failed>)'} for the calls seen so far."""
+        return {k: ('eager (' + v.reason + ')') if isinstance(v, _Eager) else 'graph'
+                for k, v in self._graphs.items()}
 
     # -- program export --------------------------------------------------------------
     def get_concrete_program(self, *input_spec, **kwargs):
@@ -316,9 +364,13 @@ def _to_spec(s, i):
 
 
 def _record_program(fn, specs, layer=None):
-    """Trace ``fn`` on symbolic inputs -> (Program, feed Variables, fetch Variables)."""
+    """Trace ``fn`` on symbolic inputs -> (Program, feed Variables, fetch Variables).
+    ``fn`` is first control-flow converted (dy2static.convert_function): an ``if`` / ``while``
+    on a tensor value records both branches / the loop as sub-blocks decided at run time."""
     from .. import static
     from ..static import graph as G
+    from .dy2static import convert_function
+    fn = convert_function(fn)
     specs = [_to_spec(s, i) for i, s in enumerate(specs)]
     was_static = static._STATIC[0]
     was_training = layer.training if layer is not None else None

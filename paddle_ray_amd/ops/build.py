@@ -83,7 +83,7 @@ def build(force=False, verbose=True):
             manifest = json.load(f)
     except (OSError, ValueError):
         manifest = {}
-    common = os.path.join(CSRC, 'common.h')
+    headers = sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith('.h'))
     hip_srcs = sorted(f for f in os.listdir(CSRC) if f.endswith('.hip'))
     jobs, keys, objs = [], {}, []
     for f in hip_srcs:
@@ -92,7 +92,7 @@ def build(force=False, verbose=True):
         objs.append(obj)
         cmd = [HIPCC, f'--offload-arch={ARCH}', '-O3', '-fPIC', '-std=c++17', '-c', src, '-o', obj,
                '-I', CSRC, '-munsafe-fp-atomics']
-        keys[os.path.basename(obj)] = _digest([src, common], cmd)
+        keys[os.path.basename(obj)] = _digest([src] + headers, cmd)
         if force or _needs(obj, keys[os.path.basename(obj)], manifest):
             jobs.append(cmd)
     bsrc = os.path.join(CSRC, 'bindings.cpp')

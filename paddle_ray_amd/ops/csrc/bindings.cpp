@@ -69,6 +69,8 @@ int pra_gemm_bias_act(const void*, const void*, const void*, void*, void*, int, 
 int pra_gemm_lds(int, const void*, const void*, const void*, void*, void*, float*, int, int, int, int, int, int, int,
                  int, int, int, int, float*, hipStream_t);
 int pra_gemm_lds_splits(int, int, int);
+void pra_gemm_set_w4(int);
+int pra_gemm_get_w4();
 int pra_conv_lds(const void*, const void*, const void*, void*, int, int, int, int, int, int, int, int, int, int, int,
                  int, float*, hipStream_t);
 int pra_conv_lds_splits(int, int, int);
@@ -119,6 +121,8 @@ PYBIND11_MODULE(_pra_hip, m) {
   });
   m.def("conv_lds_splits", [](int m, int n, int k) { return pra_conv_lds_splits(m, n, k); });
   m.def("gemm_lds_splits", [](int M, int N, int K) { return pra_gemm_lds_splits(M, N, K); });
+  m.def("gemm_set_w4", [](int mask) { pra_gemm_set_w4(mask); });
+  m.def("gemm_get_w4", []() { return pra_gemm_get_w4(); });
   m.def("gemm_lds", [](int layout, P a, P b, P bias, P c, P z, P colsum, int M, int N, int K, int lda, int ldb,
                        int ldc, int ldz, int dt, int epi, int beta, int splits, P ws, P s) {
     if (pra_gemm_lds(layout, CV(a), CV(b), CV(bias), V(c), V(z), F(colsum), M, N, K, lda, ldb, ldc, ldz, dt, epi, beta,

@@ -33,639 +33,24 @@
 // with the pre-activation optionally stored to Z, or dGELU: C = acc * gelu'(Z) with per-tile
 // column partial sums written to `colsum` (the bias gradient, reduced by pra_colsum_partials);
 // `beta=1` accumulates into C (dW += xᵀ·dy straight into the flat gradient buffer).
-#include "common.h"
-#include <stdlib.h>
-#include <type_traits>
+#include "gemm_core.h"
+
+extern "C" int pra_gemm_w4(int layout, const void* A, const void* B, const void* bias, void* C, void* Z,
+                           float* colsum, int M, int N, int K, int lda, int ldb, int ldc, int ldz, int dtype,
+                           int epi, int beta, int splits, float* ws, hipStream_t s);
 
 namespace pra {
 namespace {
 
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-template <typename T> struct V8;
-template <> struct V8<bf16> { typedef __bf16 type __attribute__((ext_vector_type(8))); };
-template <> struct V8<f16> { typedef _Float16 type __attribute__((ext_vector_type(8))); };
-
-template <typename T>
-__device__ __forceinline__ f32x4 mma(typename V8<T>::type a, typename V8<T>::type b, f32x4 c);
-template <>
-__device__ __forceinline__ f32x4 mma<bf16>(V8<bf16>::type a, V8<bf16>::type b, f32x4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
-}
-template <>
-__device__ __forceinline__ f32x4 mma<f16>(V8<f16>::type a, V8<f16>::type b, f32x4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
-}
-
-template <typename T> __device__ __forceinline__ float to_f(uint16_t u);
-template <> __device__ __forceinline__ float to_f<bf16>(uint16_t u) { return bf2f(u); }
-template <> __device__ __forceinline__ float to_f<f16>(uint16_t u) { return (float)__builtin_bit_cast(_Float16, u); }
-template <typename T> __device__ __forceinline__ uint32_t pack2(float a, float b);
-template <> __device__ __forceinline__ uint32_t pack2<bf16>(float a, float b) { return pack_bf2(a, b); }
-template <> __device__ __forceinline__ uint32_t pack2<f16>(float a, float b) {
-  return (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)a) | ((uint32_t)__builtin_bit_cast(uint16_t, (_Float16)b) << 16);
-}
-
-enum Epi : int { kNone = 0, kGeluErf = 1, kGeluTanh = 2, kRelu = 3, kDGeluErf = 4, kDGeluTanh = 5 };
-
-// tanh(u) = 1 - 2 / (exp(2u) + 1): one v_exp + one v_rcp (saturates cleanly at +-1)
-__device__ __forceinline__ float fast_tanh(float u) {
-  return 1.f - 2.f * __builtin_amdgcn_rcpf(__expf(2.f * u) + 1.f);
-}
-__device__ __forceinline__ float gelu_tanh(float x) {
-  const float u = 0.79788456080286536f * (x + 0.044715f * x * x * x);
-  return 0.5f * x * (1.f + fast_tanh(u));
-}
-__device__ __forceinline__ float dgelu_tanh(float x) {
-  const float u = 0.79788456080286536f * (x + 0.044715f * x * x * x);
-  const float t = fast_tanh(u);
-  return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * 0.79788456080286536f * (1.f + 0.134145f * x * x);
-}
-__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
-__device__ __forceinline__ float dgelu_erf(float x) {
-  return 0.5f * (1.f + erff(x * 0.70710678118654752f)) + x * 0.3989422804014327f * __expf(-0.5f * x * x);
-}
-
-template <int E>
-__device__ __forceinline__ float act(float x) {
-  if (E == kGeluErf) return gelu_erf(x);
-  if (E == kGeluTanh) return gelu_tanh(x);
-  if (E == kRelu) return fmaxf(x, 0.f);
-  return x;
-}
-
-constexpr int BM = 256, BN = 256, BKT = 64;  // the GEMM tile (conv configs below narrow BN)
-
-// Wave layouts of a BM_ x BN_ tile: WR x WC waves, each (BM_/WR) x (BN_/WC) outputs.
-//   W8: 256x256, 2 x 4 waves (128x64 each, 2 waves/SIMD, 32 accumulators)
-//   W4: 256x256, 2 x 2 waves (128x128 each, 1 wave/SIMD, 64 accumulators in AGPRs)
-//   C128 / C64: narrow-N tiles for convolutions with 128 / 64 output channels (256x128 and
-//       512x64, 64x64 per wave): a 256-wide tile would leave half / three quarters of its
-//       MFMAs on padding columns. Their B operand must be K-contiguous (BK = true).
-// Each K-step stages A [BM][64] and B [BN][64] (or [64][BN]) images, double-buffered.
-template <int WR_, int WC_, int BM_ = 256, int BN_ = 256>
-struct WCfg {
-  static constexpr int WR = WR_, WC = WC_, NT = 64 * WR_ * WC_, BM = BM_, BN = BN_;
-  static constexpr int TI = BM_ / WR_ / 16, TJ = BN_ / WC_ / 16;  // 16x16 MFMA tiles per wave
-  static constexpr int IMGA = BM_ * BKT * 2, IMGB = BN_ * BKT * 2, SLOT = IMGA + IMGB;
-  static constexpr int NDA = IMGA / (NT * 16), NDB = IMGB / (NT * 16);  // glds per thread per K-step
-  static constexpr int EPI = 128 * (BN_ + 4) * 4;  // epilogue image: 128 rows of fp32, padded pitch
-  static constexpr int LDS = 2 * SLOT > EPI ? 2 * SLOT : EPI;
-};
-using W8 = WCfg<2, 4>;
-using W4 = WCfg<2, 2>;
-using C128 = WCfg<4, 2, 256, 128>;
-using C64 = WCfg<8, 1, 512, 64>;
-
-// s_waitcnt vmcnt(N) (expcnt / lgkmcnt left unconstrained)
-template <int N>
-__device__ __forceinline__ void wait_vmcnt() {
-  static_assert(N >= 0 && N < 64, "vmcnt range");
-  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | 0x70 | 0xF00);
-}
-
-typedef short v4i16 __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-
-// MC image [64 k][256] (512-B rows): 16-B chunk ^= mc_swz(k) makes the two ds_read_b64_tr_b16
-// of a 32-lane half (k rows 8g+q, g = 0,1, q = 0..3) hit 16 distinct slots of the bank row.
-__device__ __forceinline__ int mc_swz(int k) { return 2 * ((k & 3) | ((k >> 1) & 4)); }
-// KC image [256 rows][64 k] (128-B rows): 16-B chunk ^= (row>>1)&7. ds_read_b128 serves lanes in
-// the groups {0-3,12-15,20-27}, {4-11,16-19,28-31} (+32); with this XOR each group's 16 lanes hit
-// 16 distinct 16-B slots (conflict-free).
-__device__ __forceinline__ int kc_swz(int row) { return (row >> 1) & 7; }
-
-// Per-thread DMA plan for one operand image (NDMA glds per thread per K-step). A K-step moves
-// whole 128-B lines of every row (BK = 64 bf16), so each L2 line is requested once.
-// KC image: position P (16-B chunk 0..2047) = row P>>3, slot P&7 holds global chunk (P&7)^kc_swz(row).
-// MC image: position P = k-row P>>5, slot P&31 holds global chunk (P&31)^mc_swz(k).
-template <bool KC, int NT, int NDMA>
-struct Dma {
-  uint32_t voff[NDMA];  // per-lane byte offsets of the chunks this thread stages
-  uint64_t base;        // wave-uniform operand base (SGPRs); advanced per K-step
-  uint64_t step;        // bytes per K-step
-  __device__ __forceinline__ void init(const uint16_t* b, int ld, int r0, int rmax, int tid) {
-#pragma unroll
-    for (int n = 0; n < NDMA; ++n) {
-      const int P = n * NT + tid;
-      if (KC) {
-        const int row = P >> 3, c = (P & 7) ^ kc_swz(row);
-        const int r = min(r0 + row, rmax);
-        voff[n] = (uint32_t)(((int64_t)r * ld + 8 * c) * 2);
-      } else {
-        const int k = P >> 5, c = (P & 31) ^ mc_swz(k);
-        const int col = min(r0 + 8 * c, rmax);  // rmax = last valid 8-aligned chunk start
-        voff[n] = (uint32_t)(((int64_t)k * ld + col) * 2);
-      }
-    }
-    base = (uint64_t)b;
-    step = KC ? (uint64_t)BKT * 2 : (uint64_t)BKT * ld * 2;
+// Which layouts run the 4-wave configuration (bit = 1 << layout): PRA_GEMM_W4 at first use,
+// pra_gemm_set_w4 afterwards (A/B timing in one process).
+int g_w4_mask = -1;
+int w4_mask() {
+  if (g_w4_mask < 0) {
+    const char* e = getenv("PRA_GEMM_W4");
+    g_w4_mask = e ? atoi(e) : 0;
   }
-  __device__ __forceinline__ void advance(int ksteps) { base += (uint64_t)ksteps * step; }
-  __device__ __forceinline__ void issue1(uint32_t lds_img, int wave, int kt, int n) {
-    const uint64_t g = base + (uint64_t)kt * step;
-    // readfirstlane returns int: go through uint32_t so the low word is ZERO-extended
-    const uint64_t gs = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(g >> 32)) << 32) |
-                        (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)g);
-    // wave-uniform LDS base in M0; the hardware adds lane*16. Issued from inline asm so the
-    // compiler's waitcnt model does not see an LDS write in flight and never drains it with
-    // vmcnt(0) ahead of the fragment reads: the explicit vmcnt in the K loop is the only wait.
-    const uint32_t dst = __builtin_amdgcn_readfirstlane(lds_img + (n * NT + wave * 64) * 16);
-    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff[n]), "s"(gs), "s"(dst)
-                 : "memory");
-  }
-};
-
-// Implicit-GEMM convolution operand A = im2col(x) for a channels-last input x [N][H][W][C]:
-// row m = output pixel (n, ho, wo), column k = (kh, kw, c). With C % 64 == 0 a K-step (64 k)
-// lies inside one filter tap, so every staged row segment is 128 contiguous bytes of one input
-// pixel: the LDS-DMA gathers rows straight from x (per-lane source offsets), nothing is
-// materialised. The zero padding is the buffer descriptor's range check: a tap that falls
-// outside the image gets an offset past num_records and the DMA writes zeros to LDS.
-struct ConvGeom {
-  int Ho, Wo, H, W, C, KW, S, P;
-};
-
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-
-template <int NT, int NDMA>
-struct ConvDmaA {
-  int pix[NDMA];       // element offset of x[n][ho*S-P][wo*S-P][8c] (may be negative) per staged chunk
-  uint32_t hw[NDMA];   // (ho*S-P) << 16 | (wo*S-P) & 0xffff
-  u32x4 rs;            // buffer descriptor of x (wave-uniform, SGPRs)
-  int kt0;
-  ConvGeom g;
-  __device__ __forceinline__ void init(const uint16_t* x, const ConvGeom& cg, int m0, int M, int tid) {
-    g = cg;
-#pragma unroll
-    for (int n = 0; n < NDMA; ++n) {
-      const int P = n * NT + tid;
-      const int row = P >> 3, c = (P & 7) ^ kc_swz(row);
-      const int m = min(m0 + row, M - 1);
-      const int wo = m % g.Wo, t = m / g.Wo, ho = t % g.Ho, img = t / g.Ho;
-      const int hi = ho * g.S - g.P, wi = wo * g.S - g.P;
-      pix[n] = ((img * g.H + hi) * g.W + wi) * g.C + 8 * c;
-      hw[n] = ((uint32_t)hi << 16) | ((uint32_t)wi & 0xffffu);
-    }
-    const uint64_t b = (uint64_t)x;
-    rs[0] = __builtin_amdgcn_readfirstlane((uint32_t)b);
-    rs[1] = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32)) & 0xffffu;  // stride 0
-    rs[2] = __builtin_amdgcn_readfirstlane((uint32_t)((int64_t)M / (g.Ho * g.Wo) * g.H * g.W * g.C * 2));
-    rs[3] = 0x00020000u;
-    kt0 = 0;
-  }
-  __device__ __forceinline__ void advance(int ksteps) { kt0 += ksteps; }
-  __device__ __forceinline__ void issue1(uint32_t lds_img, int wave, int kt, int n) {
-    const int k0 = (kt + kt0) * BKT;  // wave-uniform: scalar math
-    const int tap = k0 / g.C, cin0 = k0 - tap * g.C, kh = tap / g.KW, kw = tap - kh * g.KW;
-    const int hi = ((int)hw[n] >> 16) + kh, wi = (int)(int16_t)(hw[n] & 0xffffu) + kw;
-    const bool ok = (unsigned)hi < (unsigned)g.H && (unsigned)wi < (unsigned)g.W;
-    const uint32_t voff = ok ? (uint32_t)(pix[n] + (kh * g.W + kw) * g.C + cin0) * 2u : 0x80000000u;
-    const uint32_t dst = __builtin_amdgcn_readfirstlane(lds_img + (n * NT + wave * 64) * 16);
-    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(rs),
-                 "s"(dst)
-                 : "memory");
-  }
-};
-
-// Weight-gradient operand B = im2col(x) for dW = dyᵀ · im2col(x): GEMM K = output pixel
-// (n, ho, wo), N = (kh, kw, c), staged as the M/N-contiguous image [64 pixels][256 columns]
-// (chunk ^= mc_swz(k)). A thread's NDMA chunks share one image column (rows k, k+16, k+32,
-// k+48 have equal mc_swz), hence one (kh, kw, c) for the whole kernel; each chunk walks its
-// pixel forward by 64 per staged K-step (carry arithmetic, no divisions in the loop).
-// Out-of-image taps read zeros through the buffer range check, as in ConvDmaA.
-template <int NT, int NDMA>
-struct ConvDmaBW {
-  int base[NDMA];       // element offset of x[img][ho*S][wo*S][0] of the chunk's current pixel
-  uint32_t hw[NDMA];    // ho << 16 | wo of that pixel
-  int colterm;          // ((kh-P)*W + (kw-P))*C + c of the thread's column
-  uint32_t kp;          // (kh-P) << 16 | (kw-P) & 0xffff
-  u32x4 rs;
-  ConvGeom g;
-  int dH, dW;           // 64 pixels = dH output rows + dW output columns
-  __device__ __forceinline__ void seek(int n, int pix) {
-    const int wo = pix % g.Wo, t = pix / g.Wo, ho = t % g.Ho, im = t / g.Ho;
-    base[n] = ((im * g.H + ho * g.S) * g.W + wo * g.S) * g.C;
-    hw[n] = ((uint32_t)ho << 16) | (uint32_t)wo;
-  }
-  __device__ __forceinline__ void init(const uint16_t* x, const ConvGeom& cg, int n0, int K, int tid) {
-    g = cg;
-    const int k = tid >> 5, c = (tid & 31) ^ mc_swz(k);  // same column for every chunk
-    const int col = n0 + 8 * c;
-    const int tap = col / g.C, cin = col - tap * g.C, kh = tap / g.KW, kw = tap - kh * g.KW;
-    colterm = ((kh - g.P) * g.W + (kw - g.P)) * g.C + cin;
-    kp = ((uint32_t)(kh - g.P) << 16) | ((uint32_t)(kw - g.P) & 0xffffu);
-    dH = 64 / g.Wo;
-    dW = 64 - dH * g.Wo;
-#pragma unroll
-    for (int n = 0; n < NDMA; ++n) seek(n, (n * NT + tid) >> 5);
-    const uint64_t b = (uint64_t)x;
-    rs[0] = __builtin_amdgcn_readfirstlane((uint32_t)b);
-    rs[1] = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32)) & 0xffffu;
-    rs[2] = __builtin_amdgcn_readfirstlane((uint32_t)((int64_t)K / (g.Ho * g.Wo) * g.H * g.W * g.C * 2));
-    rs[3] = 0x00020000u;
-  }
-  __device__ __forceinline__ void advance(int ksteps) {
-    const int tid = threadIdx.x;
-#pragma unroll
-    for (int n = 0; n < NDMA; ++n) seek(n, ksteps * 64 + ((n * NT + tid) >> 5));
-  }
-  __device__ __forceinline__ void issue1(uint32_t lds_img, int wave, int /*kt*/, int n) {
-    int ho = (int)(hw[n] >> 16), wo = (int)(hw[n] & 0xffffu);
-    const int hi = ho * g.S + ((int)kp >> 16), wi = wo * g.S + (int)(int16_t)(kp & 0xffffu);
-    const bool ok = (unsigned)hi < (unsigned)g.H && (unsigned)wi < (unsigned)g.W;
-    const uint32_t voff = ok ? (uint32_t)(base[n] + colterm) * 2u : 0x80000000u;
-    const uint32_t dst = __builtin_amdgcn_readfirstlane(lds_img + (n * NT + wave * 64) * 16);
-    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(rs),
-                 "s"(dst)
-                 : "memory");
-    // this chunk's next staged K-step is 64 pixels further (carries, no divisions)
-    const int SC = g.S * g.C, SWC = g.S * g.W * g.C;
-    wo += dW;
-    ho += dH;
-    int b = base[n] + dW * SC + dH * SWC;
-    if (wo >= g.Wo) { wo -= g.Wo; ho += 1; b += SWC - g.Wo * SC; }
-    while (ho >= g.Ho) { ho -= g.Ho; b += g.H * g.W * g.C - g.Ho * SWC; }
-    base[n] = b;
-    hw[n] = ((uint32_t)ho << 16) | (uint32_t)wo;
-  }
-};
-
-// Fragment for rows [r0, r0+16) (row = lane&15), k = 32*s + 8*(lane>>4) + j of a K-step.
-template <typename T, bool KC>
-__device__ __forceinline__ typename V8<T>::type frag(const char* img, int r0, int s, int lane) {
-  typedef typename V8<T>::type v8;
-  if (KC) {
-    const int row = r0 + (lane & 15), c = (4 * s + (lane >> 4)) ^ kc_swz(row);
-    return *reinterpret_cast<const v8*>(img + row * 128 + c * 16);
-  } else {
-    // ds_read_b64_tr_b16: lane 4q+p of each 16-lane group g addresses k-row 32s+8g+q (+4),
-    // columns r0+4p..+3, and receives its own column's 4 k-values.
-    const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
-    const int k = 32 * s + 8 * g + q, x = mc_swz(k);  // mc_swz(k) == mc_swz(k + 4)
-    const int c = ((r0 >> 3) + (p >> 1)) ^ x;
-    const char* a0 = img + k * 512 + c * 16 + 8 * (p & 1);
-    const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)a0);
-    const v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(a0 + 4 * 512));
-    const u32x2 ul = __builtin_bit_cast(u32x2, lo), uh = __builtin_bit_cast(u32x2, hi);
-    const u32x4 u = {ul[0], ul[1], uh[0], uh[1]};
-    return __builtin_bit_cast(v8, u);
-  }
-}
-
-template <typename T, typename CF, bool AK, bool BK, int E, bool BETA, bool SPLIT, bool CONV = false,
-          int DPSX = 0, bool CONVW = false>
-__global__ __launch_bounds__(CF::NT, 1) void gemm_lds_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
-                                                          const uint16_t* __restrict__ bias, uint16_t* __restrict__ C,
-                                                          uint16_t* __restrict__ Z, float* __restrict__ colsum,
-                                                          int M, int N, int K, int lda, int ldb, int ldc, int ldz,
-                                                          int splits, float* __restrict__ ws, ConvGeom cg = {}) {
-  constexpr int NT = CF::NT, TI = CF::TI, TJ = CF::TJ, NDA = CF::NDA, NDB = CF::NDB, WC = CF::WC;
-  constexpr int BM = CF::BM, BN = CF::BN, IMGA = CF::IMGA, SLOT = CF::SLOT;
-  constexpr int RW = TI * 16, CW = TJ * 16;  // rows / columns per wave
-  static_assert(BK || BN == 256, "the M/N-contiguous B image is 256 columns wide");
-  static_assert(!CONVW || (!BK && NDB == 4), "conv wgrad gathers the 256-wide B image");
-  static_assert(TJ <= TI && 128 % RW == 0 && NDA >= 1 && NDB >= 1, "wave layout");
-  __shared__ __attribute__((aligned(1024))) char lds[CF::LDS];
-  typedef typename V8<T>::type v8;
-  const uint32_t lds_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)lds;
-
-  const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;
-  const int nb = gridDim.x;
-  int pid = blockIdx.x;
-  {  // contiguous tile run per XCD (bijective for any grid size)
-    const int q = nb >> 3, r = nb & 7, xcd = pid & 7;
-    pid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (pid >> 3);
-  }
-  // split-K: the splits of one tile are adjacent ids (same XCD); each covers a K range and
-  // writes an fp32 partial tile that splitk_reduce_k combines
-  const int split = SPLIT ? pid % splits : 0;
-  if (SPLIT) pid /= splits;
-  const int group = 8 * tiles_n, gi = pid / group, first_m = gi * 8;
-  const int gm = min(tiles_m - first_m, 8);
-  const int tm = first_m + (pid % group) % gm, tn = (pid % group) / gm;
-  const int m0 = tm * BM, n0 = tn * BN;
-
-  // wave index as an SGPR value: the per-wave DMA destinations (M0) and fragment bases are then
-  // scalar arithmetic (no v_readfirstlane + s_nop per LDS-DMA issue)
-  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6),
-            wr = wave / WC, wc = wave % WC;
-
-  typename std::conditional<CONV, ConvDmaA<NT, NDA>, Dma<AK, NT, NDA>>::type da;
-  typename std::conditional<CONVW, ConvDmaBW<NT, NDB>, Dma<BK, NT, NDB>>::type db;
-  if constexpr (CONV) da.init(A, cg, m0, M, tid);
-  else if (AK) da.init(A, lda, m0, M - 1, tid);
-  else da.init(A, lda, m0, M - 8, tid);
-  if constexpr (CONVW) db.init(B, cg, n0, K, tid);
-  else if (BK) db.init(B, ldb, n0, N - 1, tid);
-  else db.init(B, ldb, n0, N - 8, tid);
-  int nk = K / BKT;
-  if (SPLIT) {
-    const int per = (nk + splits - 1) / splits, kb = split * per;
-    nk = max(0, min(nk, kb + per) - kb);
-    da.advance(kb);
-    db.advance(kb);
-  }
-
-  f32x4 acc[TI][TJ];
-#pragma unroll
-  for (int i = 0; i < TI; ++i)
-#pragma unroll
-    for (int j = 0; j < TJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  v8 fa0[TI], fb0[TJ], fa1[TI], fb1[TJ];
-  auto read_frags = [&](v8 (&fa)[TI], v8 (&fb)[TJ], int kt, int s) {
-    const char* ai = lds + (kt & 1) * SLOT;
-    const char* bi = ai + IMGA;
-#pragma unroll
-    for (int j = 0; j < TJ; ++j) fb[j] = frag<T, BK>(bi, wc * CW + j * 16, s, lane);
-#pragma unroll
-    for (int i = 0; i < TI; ++i) fa[i] = frag<T, AK>(ai, wr * RW + i * 16, s, lane);
-  };
-  // 32 MFMAs of one k-half, interleaved segment by segment with (optionally) the fragment reads
-  // of the next k-half and one LDS-DMA instruction of the next K-step every other segment, so
-  // DMA issue and LDS reads hide under the wave's own matrix work.
-  // dA / dB: issue this half's share of operand A's (step kA) / B's (step kB) DMA
-  auto half = [&](v8 (&ca)[TI], v8 (&cb)[TJ], v8 (&na)[TI], v8 (&nb)[TJ], bool rd, int rkt, int rs, bool dA,
-                  int kA, bool dB, int kB) {
-    const uint32_t soA = lds_base + (kA & 1) * SLOT, soB = lds_base + (kB & 1) * SLOT + IMGA;
-    const char* ai = lds + (rkt & 1) * SLOT;
-    const char* bi = ai + IMGA;
-    // DMA instructions per segment (DPSX > 0: front-load them into the first segments)
-    constexpr int DPS = DPSX > 0 ? DPSX : (NDA + NDB + TI - 1) / TI;
-#pragma unroll
-    for (int i = 0; i < TI; ++i) {
-      if (dA || dB) {
-#pragma unroll
-        for (int d = i * DPS; d < (i + 1) * DPS && d < NDA + NDB; ++d) {
-          if (d < NDA) {
-            if (dA) da.issue1(soA, wave, kA, d);
-          } else if (dB) {
-            db.issue1(soB, wave, kB, d - NDA);
-          }
-        }
-      }
-      if (rd) {
-        if (i < TJ) nb[i] = frag<T, BK>(bi, wc * CW + i * 16, rs, lane);
-        na[i] = frag<T, AK>(ai, wr * RW + i * 16, rs, lane);
-      }
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int j = 0; j < TJ; ++j) acc[i][j] = mma<T>(cb[j], ca[i], acc[i][j]);
-      __builtin_amdgcn_s_setprio(0);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  };
-
-  // prologue: K-steps 0 and 1 in flight, k-half 0 of step 0 in registers
-  if (nk > 0) {
-#pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    if (t < nk) {
-#pragma unroll
-      for (int n = 0; n < NDA; ++n) da.issue1(lds_base + t * SLOT, wave, t, n);
-#pragma unroll
-      for (int n = 0; n < NDB; ++n) db.issue1(lds_base + t * SLOT + IMGA, wave, t, n);
-    }
-  }
-  if (nk >= 2) {
-    wait_vmcnt<NDA + NDB>();  // step 0 landed, step 1 still in flight
-  } else {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_sched_barrier(0);
-  read_frags(fa0, fb0, 0, 0);
-
-  // K-step kt (slot kt&1): half 0 computes (kt,0) from F0 while reading (kt,1) into F1; then the
-  // barrier that retires step kt+1's DMA and every wave's reads of slot kt; half 1 refills slot kt
-  // with step kt+2 (DMA) and computes (kt,1) from F1 while reading (kt+1,0) into F0.
-  // (measured: issuing B of step kt+1 under half 0 of step kt instead, so both halves carry DMA,
-  // was 8-15 % slower on every GPT shape: half a K-step does not cover the DMA latency)
-  // (non-split launches pass splits = 0 only for the PRA_GEMM_ABLATE=nodma timing ablation)
-  const bool dmaon = SPLIT || splits != 0;
-  // STEADY: kt + 2 < nk and DMA on, known at compile time -> the K-step body has no branches
-  // (the generic body tests "read next half" / "stage step kt+2" around every MFMA segment: ~16
-  // wave-uniform branches per K-step in the steady state). The last two steps run the generic body.
-  auto kstep = [&](int kt, auto steady_c) {
-    constexpr bool STEADY = decltype(steady_c)::value;
-    half(fa0, fb0, fa1, fb1, true, kt, 1, false, 0, false, 0);
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): (kt,1) fragments landed; slot kt reads done
-    if (STEADY || kt + 1 < nk) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // step kt+1 landed (this wave)
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    if constexpr (STEADY) {
-      half(fa1, fb1, fa0, fb0, true, kt + 1, 0, true, kt + 2, true, kt + 2);
-    } else {
-      half(fa1, fb1, fa0, fb0, kt + 1 < nk, kt + 1, 0, kt + 2 < nk && dmaon, kt + 2, kt + 2 < nk && dmaon, kt + 2);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    // (kt+1,0) fragments landed. The steady body leaves this to the compiler's per-register
-    // lgkmcnt(N) before each consuming MFMA (no LDS-safety role: slot kt+1 is refilled only after
-    // the next half-0 drain + barrier), so the next half starts on its first fragments.
-    if constexpr (!STEADY) __builtin_amdgcn_s_waitcnt(0xC07F);
-  };
-  int kt = 0;
-  // (the implicit-GEMM convolutions keep the generic body: their gather state already sits at
-  // the register limit and a second body copy made them spill)
-  if constexpr (!CONV && !CONVW)
-    if (dmaon)
-      for (; kt + 2 < nk; ++kt) kstep(kt, std::true_type{});
-  for (; kt < nk; ++kt) kstep(kt, std::false_type{});
-  }  // nk > 0
-
-  if (SPLIT) {
-    float* wsp = ws + (int64_t)split * M * N;
-    const int mrow = m0 + wr * RW + (lane & 15);
-    const int ncol = n0 + wc * CW + 4 * (lane >> 4);
-#pragma unroll
-    for (int i = 0; i < TI; ++i) {
-      const int m = mrow + i * 16;
-      if (m >= M) continue;
-#pragma unroll
-      for (int j = 0; j < TJ; ++j) {
-        const int n = ncol + j * 16;
-        if (n < N)
-          *reinterpret_cast<float4*>(wsp + (int64_t)m * N + n) =
-              make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
-      }
-    }
-    return;
-  }
-
-  // Epilogue through LDS (the K loop is done with it): for each 128-row half the waves that own
-  // it park their fp32 accumulators in an [128][256+4] image (ds_write_b128, conflict-free pitch),
-  // then all 8 waves stream it out row-major: 8 columns per lane, whole 512-B row segments per 32
-  // lanes, so the bias/activation/pre-activation/beta/dGELU traffic is 16-B coalesced loads and
-  // stores instead of 8-B scatters across 16 rows.
-  // acc[i][j][r] = C[m0 + wr*RW + i*16 + (lane&15)][n0 + wc*CW + j*16 + 4*(lane>>4) + r]
-  float* img = reinterpret_cast<float*>(lds);
-  constexpr int PITCH = BN + 4;  // floats
-  // this thread's output units: row tid/TPR (+RSTEP per q), 8 columns at (tid%TPR)*8 (fixed per thread)
-  constexpr int TPR = BN / 8, RSTEP = NT / TPR, NQ = 128 / RSTEP, QB = NQ < 4 ? NQ : 4;
-  const int ucol = (tid % TPR) * 8, urow = tid / TPR;
-  const int n = n0 + ucol;
-  const bool ncol_ok = n < N;  // N % 8 == 0: a unit is all-in or all-out
-  float bv[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) bv[e] = 0.f;
-  if (bias && ncol_ok) {
-    const uint4 bb = *reinterpret_cast<const uint4*>(bias + n);
-    const uint32_t w4[4] = {bb.x, bb.y, bb.z, bb.w};
-#pragma unroll
-    for (int e = 0; e < 4; ++e) { bv[2 * e] = to_f<T>(w4[e] & 0xffff); bv[2 * e + 1] = to_f<T>(w4[e] >> 16); }
-  }
-  float cs[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) cs[e] = 0.f;
-#pragma unroll
-  for (int h = 0; h < BM / 128; ++h) {
-    __builtin_amdgcn_s_waitcnt(0xC07F);
-    __syncthreads();  // (h=0) every wave is done reading K-loop tiles; (h>0) chunk h-1 streamed out
-    if ((wr * RW) / 128 == h) {
-#pragma unroll
-      for (int i = 0; i < TI; ++i)
-#pragma unroll
-        for (int j = 0; j < TJ; ++j) {
-          const int r = wr * RW - h * 128 + i * 16 + (lane & 15), c = wc * CW + j * 16 + 4 * (lane >> 4);
-          *reinterpret_cast<f32x4*>(img + r * PITCH + c) = acc[i][j];
-        }
-    }
-    __syncthreads();
-    // NQ units per thread in batches of 4: every load of a batch (LDS image, Z / C) is issued
-    // before any of its math so the global-load latency is paid once per batch, not per unit
-#pragma unroll
-    for (int bq = 0; bq < NQ; bq += QB) {
-      f32x4 lo[QB], hi[QB];
-      uint4 gz[QB];
-      bool ok[QB];
-      int64_t moff[QB];
-#pragma unroll
-      for (int u = 0; u < QB; ++u) {
-        const int rr = urow + RSTEP * (bq + u), m = m0 + h * 128 + rr;
-        ok[u] = m < M && ncol_ok;
-        moff[u] = (int64_t)(ok[u] ? m : 0);
-        lo[u] = *reinterpret_cast<const f32x4*>(img + rr * PITCH + ucol);
-        hi[u] = *reinterpret_cast<const f32x4*>(img + rr * PITCH + ucol + 4);
-        if (E == kDGeluErf || E == kDGeluTanh) {
-          if (ok[u]) gz[u] = *reinterpret_cast<const uint4*>(Z + moff[u] * ldz + n);
-        } else if (BETA) {
-          if (ok[u]) gz[u] = *reinterpret_cast<const uint4*>(C + moff[u] * ldc + n);
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < QB; ++u) {
-        if (!ok[u]) continue;
-        const int64_t m = moff[u];
-        float v[8] = {lo[u][0], lo[u][1], lo[u][2], lo[u][3], hi[u][0], hi[u][1], hi[u][2], hi[u][3]};
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] += bv[e];
-        if (E == kDGeluErf || E == kDGeluTanh) {
-          const uint32_t w4[4] = {gz[u].x, gz[u].y, gz[u].z, gz[u].w};
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const float z0 = to_f<T>(w4[e] & 0xffff), z1 = to_f<T>(w4[e] >> 16);
-            v[2 * e] *= (E == kDGeluErf) ? dgelu_erf(z0) : dgelu_tanh(z0);
-            v[2 * e + 1] *= (E == kDGeluErf) ? dgelu_erf(z1) : dgelu_tanh(z1);
-          }
-        } else if (E != kNone) {
-          if (Z) {
-            uint4 o;
-            o.x = pack2<T>(v[0], v[1]); o.y = pack2<T>(v[2], v[3]);
-            o.z = pack2<T>(v[4], v[5]); o.w = pack2<T>(v[6], v[7]);
-            *reinterpret_cast<uint4*>(Z + m * ldz + n) = o;
-          }
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] = act<E>(v[e]);
-        }
-        if (BETA && !(E == kDGeluErf || E == kDGeluTanh)) {
-          const uint32_t w4[4] = {gz[u].x, gz[u].y, gz[u].z, gz[u].w};
-#pragma unroll
-          for (int e = 0; e < 4; ++e) { v[2 * e] += to_f<T>(w4[e] & 0xffff); v[2 * e + 1] += to_f<T>(w4[e] >> 16); }
-        }
-        uint4 o;
-        o.x = pack2<T>(v[0], v[1]); o.y = pack2<T>(v[2], v[3]);
-        o.z = pack2<T>(v[4], v[5]); o.w = pack2<T>(v[6], v[7]);
-        *reinterpret_cast<uint4*>(C + m * ldc + n) = o;
-        if (colsum) {
-          // the bias gradient sums the ROUNDED output (what a separate reduction would read)
-          const uint32_t w4[4] = {o.x, o.y, o.z, o.w};
-#pragma unroll
-          for (int e = 0; e < 4; ++e) { cs[2 * e] += to_f<T>(w4[e] & 0xffff); cs[2 * e + 1] += to_f<T>(w4[e] >> 16); }
-        }
-      }
-    }
-  }
-  if constexpr (TPR == 32 && NT == 512) if (colsum) {
-    // threads sharing (tid & 31) own the same 8 columns: lanes l, l^32 then the 8 waves via LDS
-#pragma unroll
-    for (int e = 0; e < 8; ++e) cs[e] += __shfl_xor(cs[e], 32, 64);
-    __syncthreads();
-    if (lane < 32) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) img[wave * 256 + lane * 8 + e] = cs[e];
-    }
-    __syncthreads();
-    if (tid < 256) {
-      float t = 0.f;
-#pragma unroll
-      for (int w = 0; w < NT / 64; ++w) t += img[w * 256 + tid];
-      const int nn = n0 + tid;
-      if (nn < N) colsum[(int64_t)tm * N + nn] = t;
-    }
-  }
-}
-
-// split-K combine: C[m][n..n+3] = epi(sum_s ws[s][m][n..n+3] + bias) (+ C if BETA)
-template <typename T, int E, bool BETA>
-__global__ void splitk_reduce_k(const float* __restrict__ ws, int splits, const uint16_t* __restrict__ bias,
-                                uint16_t* __restrict__ C, uint16_t* __restrict__ Z, int M, int N, int ldc, int ldz) {
-  const int64_t idx = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
-  if (idx >= (int64_t)M * N) return;
-  const int m = (int)(idx / N), n = (int)(idx % N);
-  float4 a = *reinterpret_cast<const float4*>(ws + idx);
-  for (int s = 1; s < splits; ++s) {
-    const float4 b = *reinterpret_cast<const float4*>(ws + (int64_t)s * M * N + idx);
-    a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
-  }
-  float v[4] = {a.x, a.y, a.z, a.w};
-  if (bias) {
-    const uint2 bb = *reinterpret_cast<const uint2*>(bias + n);
-    v[0] += to_f<T>(bb.x & 0xffff); v[1] += to_f<T>(bb.x >> 16);
-    v[2] += to_f<T>(bb.y & 0xffff); v[3] += to_f<T>(bb.y >> 16);
-  }
-  if (E != kNone) {
-    if (Z) {
-      uint2 o;
-      o.x = pack2<T>(v[0], v[1]);
-      o.y = pack2<T>(v[2], v[3]);
-      *reinterpret_cast<uint2*>(Z + (int64_t)m * ldz + n) = o;
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) v[r] = act<E>(v[r]);
-  }
-  uint16_t* c = C + (int64_t)m * ldc + n;
-  if (BETA) {
-    const uint2 cc = *reinterpret_cast<const uint2*>(c);
-    v[0] += to_f<T>(cc.x & 0xffff); v[1] += to_f<T>(cc.x >> 16);
-    v[2] += to_f<T>(cc.y & 0xffff); v[3] += to_f<T>(cc.y >> 16);
-  }
-  uint2 o;
-  o.x = pack2<T>(v[0], v[1]);
-  o.y = pack2<T>(v[2], v[3]);
-  *reinterpret_cast<uint2*>(c) = o;
-}
-
-// sum of P partial rows [P][N] fp32 -> out[N] (dtype T)
-template <typename T>
-__global__ void colsum_partials_k(const float* __restrict__ part, T* __restrict__ out, int P, int N) {
-  const int n = blockIdx.x * blockDim.x + threadIdx.x;
-  if (n >= N) return;
-  float s = 0.f;
-  for (int p = 0; p < P; ++p) s += part[(int64_t)p * N + n];
-  out[n] = Cvt<T>::from(s);
+  return g_w4_mask;
 }
 
 template <typename T, bool AK, bool BK, int E>
@@ -677,12 +62,18 @@ void launch_e(const void* A, const void* B, const void* bias, void* C, void* Z, 
   auto pbias = static_cast<const uint16_t*>(bias);
   auto pc = static_cast<uint16_t*>(C);
   auto pz = static_cast<uint16_t*>(Z);
-  // W4 (1 wave/SIMD, 128x128 per wave) measured 12-45 % slower than W8 on every GPT-1.3B shape
-  // (profiles/r2_gemm/summary.md); it stays a compile-time option, not instantiated.
+  // W4 (1 wave/SIMD, 128x128 per wave, gemm_w4.hip) per layout mask; its round-2 measurement
+  // (12-45 % slower) was taken with the accumulators spilled to scratch by the compiler.
   constexpr bool four = false;
   static const int ablate = getenv("PRA_GEMM_ABLATE") ? 0 : 1;  // 0: no DMA after the prologue (timing only)
+  constexpr int layout = AK ? (BK ? 1 : 0) : 2;
+  const bool w4 = std::is_same<T, bf16>::value && E != kRelu && (w4_mask() >> layout & 1);
   if (splits > 1) {
-    gemm_lds_kernel<T, W8, AK, BK, kNone, false, true><<<tiles * splits, W8::NT, 0, s>>>(
+    if (w4)
+      pra_gemm_w4(layout, A, B, nullptr, nullptr, nullptr, nullptr, M, N, K, lda, ldb, ldc, ldz, kBF16, 0, 0,
+                  splits, ws, s);
+    else
+      gemm_lds_kernel<T, W8, AK, BK, kNone, false, true><<<tiles * splits, W8::NT, 0, s>>>(
           pa, pb, nullptr, nullptr, nullptr, nullptr, M, N, K, lda, ldb, ldc, ldz, splits, ws);
     const int64_t quads = (int64_t)M * N / 4;
     const int blocks = (int)((quads + 255) / 256);
@@ -698,6 +89,9 @@ void launch_e(const void* A, const void* B, const void* bias, void* C, void* Z, 
   gemm_lds_kernel<T, CFG, AK, BK, E, BETA_, false><<<tiles, CFG::NT, 0, s>>>(pa, pb, pbias, pc, pz, colsum, M, N, K, \
                                                                            lda, ldb, ldc, ldz, ablate, nullptr)
   (void)four;
+  if (w4 && pra_gemm_w4(layout, A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, kBF16, E, beta, 1, nullptr,
+                        s) == 0)
+    return;
   if (beta) PRA_GEMM_LAUNCH(W8, true); else PRA_GEMM_LAUNCH(W8, false);
 #undef PRA_GEMM_LAUNCH
 }
@@ -889,3 +283,6 @@ extern "C" int pra_colsum_partials(const float* part, void* out, int P, int N, i
   else return -1;
   return 0;
 }
+
+extern "C" void pra_gemm_set_w4(int mask) { pra::g_w4_mask = mask; }
+extern "C" int pra_gemm_get_w4() { return pra::w4_mask(); }

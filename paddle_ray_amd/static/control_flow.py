@@ -38,7 +38,10 @@ def _flat(out):
 
 
 class _SubBlock:
-    """A traced sub-program: placeholders -> outputs, plus captured outer Variables."""
+    """A traced sub-program: placeholders -> outputs, plus captured outer Variables. It is
+    an argument of the control-flow op that runs it and serializes as a nested op list
+    (graph._encode ``__block__``; the ProgramDesc sub-block of the reference)."""
+    _pra_block = True
 
     def __init__(self, outer_prog):
         self.prog = G.Program()
@@ -80,18 +83,23 @@ class _SubBlock:
         self.outputs = outputs
         return self
 
+    @property
+    def ph_vids(self):
+        return [v.vid for v in self.placeholders]
+
+    @property
+    def cap_vids(self):
+        return [v.vid for v in self.captured]
+
+    def block_ops(self):
+        return self.prog.global_block().ops
+
     def run(self, feed_vals, captured_vals, out_obj=None):
         """Execute the sub-block eagerly; returns the values of ``out_obj`` (default: the
         traced outputs)."""
         env = {v.vid: t for v, t in zip(self.placeholders, feed_vals)}
         env.update({v.vid: t for v, t in zip(self.captured, captured_vals)})
-        for op in self.prog.global_block().ops:
-            res = op.fn(*G._materialize(op.args, env), **G._materialize(op.kwargs, env))
-            if op.out_vids:
-                flat, _ = G._flatten_out(res)
-                for vid, t in zip(op.out_vids, flat):
-                    env[vid] = t
-        return _resolve(self.outputs if out_obj is None else out_obj, env)
+        return G.run_block_ops(self.block_ops(), env, self.outputs if out_obj is None else out_obj)
 
 
 def _resolve(obj, env):
@@ -137,20 +145,40 @@ def while_loop(cond, body, loop_vars, is_test=False, name=None):
     cb.finish(c)
     bb.finish(out)
     nl, ncc = len(loop_vars), len(cb.captured)
-
-    def run_while(*vals):
-        vs = list(vals[:nl])
-        c_cap = vals[nl:nl + ncc]
-        b_cap = vals[nl + ncc:]
-        while bool(_u(cb.run(vs, c_cap)).reshape(-1)[0]):
-            vs = list(bb.run(vs, b_cap))
-        return tuple(vs)
-    run_while.__name__ = 'while'
-    args = loop_vars + cb.captured + bb.captured + [cb.params + bb.params]
+    args = [cb, bb, nl, ncc] + loop_vars + cb.captured + bb.captured + [cb.params + bb.params]
     specs = [_spec(v) for v in loop_vars]
     tmpl = ('tuple', ['T'] * nl)
-    outs = G.record_op('while', lambda *a: run_while(*a[:-1]), args, {}, out_specs=(tmpl, specs))
+    outs = G.record_op('while', while_op, args, {}, out_specs=(tmpl, specs))
     return list(outs)
+
+
+def while_op(cb, bb, nl, ncc, *vals):
+    """The ``while`` op (parity: controlflow/while_op.cc): re-run the body sub-block while the
+    condition sub-block yields true. ``vals`` = loop vars, captured inputs of the condition,
+    of the body, then the parameter list (an input for the planner only)."""
+    vals = vals[:-1]
+    vs = list(vals[:nl])
+    c_cap = vals[nl:nl + ncc]
+    b_cap = vals[nl + ncc:]
+    while bool(_u(cb.run(vs, c_cap)).reshape(-1)[0]):
+        vs = list(bb.run(vs, b_cap))
+    return tuple(vs)
+
+
+def conditional_block_op(pred, tb, fb, nt, *caps):
+    """The ``conditional_block`` op (parity: controlflow/conditional_block_op.cc + select_input):
+    run the sub-block of the branch ``pred`` selects. ``caps`` = captured inputs of the true
+    block, of the false block, then the parameter list."""
+    caps = caps[:-1]
+    take = bool(_u(pred).reshape(-1)[0])
+    out = tb.run([], caps[:nt]) if take else fb.run([], caps[nt:])
+    flat = _flat(out)
+    # an output that is a plain outer value/constant keeps its own tensor
+    return tuple(o if isinstance(o, Tensor) else Tensor(torch.as_tensor(o)) for o in flat)
+
+
+for _f in (while_op, conditional_block_op):
+    G.register_static_op(f'{_f.__module__}:{_f.__qualname__}', _f)
 
 
 # -- cond --------------------------------------------------------------------------------------
@@ -179,16 +207,9 @@ def cond(pred, true_fn=None, false_fn=None, name=None, return_names=None):
     tb.finish(t_out)
     fb.finish(f_out)
     nt = len(tb.captured)
-
-    def run_cond(p, *caps):
-        take = bool(_u(p).reshape(-1)[0])
-        out = tb.run([], caps[:nt]) if take else fb.run([], caps[nt:])
-        flat = _flat(out)
-        # an output that is a plain outer value/constant keeps its own tensor
-        return tuple(o if isinstance(o, Tensor) else Tensor(torch.as_tensor(o)) for o in flat)
-    args = [pred] + tb.captured + fb.captured + [tb.params + fb.params]
+    args = [pred, tb, fb, nt] + tb.captured + fb.captured + [tb.params + fb.params]
     specs = [_spec(v) for v in tf]
-    outs = G.record_op('conditional_block', lambda *a: run_cond(*a[:-1]), args, {},
+    outs = G.record_op('conditional_block', conditional_block_op, args, {},
                        out_specs=(('tuple', ['T'] * len(tf)), specs))
     it = iter(outs)
     return G._rebuild(G._flatten_out(t_out)[1], it) if isinstance(t_out, (list, tuple)) \

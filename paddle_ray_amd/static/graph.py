@@ -992,7 +992,72 @@ def _resolve(op_type):
     return fn
 
 
+class _LoadedBlock:
+    """A control-flow sub-block read back from a ``.pdmodel`` (the serialized twin of
+    control_flow._SubBlock): its ops, the vids of its placeholders / captured outer variables,
+    and its output structure. ``run`` interprets it like the traced original."""
+    _pra_block = True
+
+    def __init__(self, ops, ph_vids, cap_vids, outputs):
+        self.ops, self.ph_vids, self.cap_vids, self.outputs = ops, ph_vids, cap_vids, outputs
+
+    def block_ops(self):
+        return self.ops
+
+    def run(self, feed_vals, captured_vals, out_obj=None):
+        env = dict(zip(self.ph_vids, feed_vals))
+        env.update(zip(self.cap_vids, captured_vals))
+        return run_block_ops(self.ops, env, self.outputs if out_obj is None else out_obj)
+
+
+def run_block_ops(ops, env, outputs):
+    """Interpret ``ops`` over ``env`` (vid -> tensor) and resolve ``outputs`` from it."""
+    for op in ops:
+        res = op.fn(*_materialize(op.args, env), **_materialize(op.kwargs, env))
+        if op.out_vids:
+            flat, _ = _flatten_out(res)
+            for vid, t in zip(op.out_vids, flat):
+                env[vid] = t
+    return _resolve_refs(outputs, env)
+
+
+def _resolve_refs(obj, env):
+    if isinstance(obj, (Variable, _VarRef)):
+        return env[obj.vid]
+    if isinstance(obj, (list, tuple)):
+        return type(obj)(_resolve_refs(o, env) for o in obj)
+    return obj
+
+
+def _as_refs(obj):
+    if isinstance(obj, Variable):
+        return _VarRef(obj.vid)
+    if isinstance(obj, (list, tuple)):
+        return type(obj)(_as_refs(o) for o in obj)
+    return obj
+
+
+def _encode_ops(ops, params):
+    enc = []
+    for op in ops:
+        qn = _qualname(op.fn, op.type)
+        if qn not in _OP_TABLE:
+            raise TypeError(f"op {op.type!r} is not a registered static op; cannot serialize")
+        enc.append({'type': qn, 'args': _encode(op.args, params),
+                    'kwargs': _encode(op.kwargs, params), 'in': op.in_vids, 'out': op.out_vids})
+    return enc
+
+
+def _decode_ops(enc, params):
+    return [OpDesc(o['type'], _resolve(o['type']), _decode(o['args'], params),
+                   _decode(o['kwargs'], params), o['in'], o['out'], None) for o in enc]
+
+
 def _encode(obj, params):
+    if getattr(obj, '_pra_block', False):  # a control-flow sub-block: nested op list
+        return {'__block__': {'ops': _encode_ops(obj.block_ops(), params),
+                              'ph': list(obj.ph_vids), 'cap': list(obj.cap_vids),
+                              'out': _encode(_as_refs(obj.outputs), params)}}
     if isinstance(obj, _VarRef):
         return {'__var__': obj.vid}
     if isinstance(obj, Tensor):
@@ -1027,6 +1092,10 @@ def _decode(obj, params):
     if isinstance(obj, dict):
         if '__var__' in obj:
             return _VarRef(obj['__var__'])
+        if '__block__' in obj:
+            b = obj['__block__']
+            return _LoadedBlock(_decode_ops(b['ops'], params), b['ph'], b['cap'],
+                                _decode(b['out'], params))
         if '__param__' in obj:
             return params[obj['__param__']]
         if '__const__' in obj:

@@ -72,6 +72,46 @@ def timeit(fn, iters):
     return s.elapsed_time(e) / iters
 
 
+def main_w4():
+    """8-wave vs 4-wave configuration vs hipBLASLt, interleaved in one process."""
+    dev = torch.device('cuda')
+    print("| GEMM | layout | M | N | K | err W8 | err W4 | W8 us | W4 us | hipBLASLt us | W4 PF/s | W4/W8 | W4 vs hipBLASLt |")
+    print("|---|---|---|---|---|---|---|---|---|---|---|---|---|", flush=True)
+    tot = [0.0, 0.0, 0.0]
+    for name, layout, M, N, K in SHAPES:
+        L.gemm_set_w4(0)
+        e8 = check(name, layout, M, N, K, dev)
+        L.gemm_set_w4(7)
+        e4 = check(name, layout, M, N, K, dev)
+        a, b = operands(layout, M, N, K, dev)
+        c = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+
+        def f8():
+            L.gemm_set_w4(0)
+            ours(layout, a, b, c, M, N, K)
+
+        def f4():
+            L.gemm_set_w4(7)
+            ours(layout, a, b, c, M, N, K)
+        fh = lambda: ref_mm(layout, a, b)  # noqa: E731
+        for f in (f8, f4, fh):
+            f()
+        torch.cuda.synchronize()
+        it = 5 if M * N * K > 1e12 else 20
+        ts = [[], [], []]
+        for _ in range(5):
+            for i, f in enumerate((f8, f4, fh)):
+                ts[i].append(timeit(f, it))
+        m = [statistics.median(t) for t in ts]
+        for i in range(3):
+            tot[i] += m[i]
+        fl = 2.0 * M * N * K
+        print(f"| {name} | {layout} | {M} | {N} | {K} | {e8:.1e} | {e4:.1e} | {m[0] * 1e3:.1f} | {m[1] * 1e3:.1f} | "
+              f"{m[2] * 1e3:.1f} | {fl / m[1] / 1e12:.3f} | {m[0] / m[1]:.3f} | {m[2] / m[1]:.3f} |", flush=True)
+    print(f"\ntotal W8 {tot[0]:.3f} ms, W4 {tot[1]:.3f} ms, hipBLASLt {tot[2]:.3f} ms")
+    L.gemm_set_w4(0)
+
+
 def main():
     dev = torch.device('cuda')
     quick = '--quick' in sys.argv
@@ -102,7 +142,9 @@ def main():
     print(f"\ntotal ours {tot_o:.3f} ms, hipBLASLt {tot_h:.3f} ms")
 
 
-if __name__ == '__main__' and '--fused' not in sys.argv:
+if __name__ == '__main__' and '--w4' in sys.argv:
+    main_w4()
+elif __name__ == '__main__' and '--fused' not in sys.argv:
     main()
 
 
@@ -132,6 +174,8 @@ def fused_main():
         F.BiasGeluFn.backward(type('C', (), {'saved_tensors': (zz, b1), 'needs_input_grad': (True, True, False),
                                              'approximate': True, 'shp': zz.shape})(), dh)
 
+    if '--w4' in sys.argv:
+        _native.lib().gemm_set_w4(7)
     print("\n| fused op | ours us | hipBLASLt + separate kernel us | ratio |\n|---|---|---|---|")
     for name, fo, fh in (('fc1 fwd +bias+GELU+Z', ours_fwd, blas_fwd), ('fc2 dgrad +dGELU+db', ours_bwd, blas_bwd)):
         fo(); fh()

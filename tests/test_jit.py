@@ -109,3 +109,107 @@ def test_inference_predictor(tmp_path):
     pred.run()
     out = pred.get_output_handle(pred.get_output_names()[0]).copy_to_cpu()
     np.testing.assert_allclose(out, net(paddle.to_tensor(x)).numpy(), rtol=1e-5, atol=1e-6)
+
+
+# -- graph replay semantics, capture fallback, dy2static control flow ---------------------------
+@pytest.mark.gpu
+def test_hip_graph_replay_outputs_are_fresh():
+    """y1 = f(x1); y2 = f(x2) must keep y1 (replay rewrites the graph's static buffers)."""
+    paddle.set_device('gpu')
+    lin = paddle.nn.Linear(8, 8)
+    lin.eval()
+    f = paddle.jit.to_static(lin)
+    with paddle.no_grad():
+        x1, x2 = paddle.randn([4, 8]), paddle.randn([4, 8])
+        y1 = f(x1)
+        y1_ref = y1.numpy().copy()
+        y2 = f(x2)
+        y3 = f(x1)
+    assert list(f.forward.graph_status().values()) == ['graph']
+    np.testing.assert_allclose(y1.numpy(), y1_ref)
+    np.testing.assert_allclose(y2.numpy(), lin(x2).numpy(), rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(y3.numpy(), y1_ref, rtol=1e-6)
+    assert y1._t.data_ptr() != y2._t.data_ptr()
+
+
+@pytest.mark.gpu
+def test_hip_graph_capture_failure_falls_back_to_eager():
+    """A data-dependent host read cannot be captured: the call runs eagerly, correctly."""
+    paddle.set_device('gpu')
+
+    @paddle.jit.to_static
+    def f(x):
+        if x.mean() > 0:   # host read of a device value
+            return x * 2
+        return x - 1
+
+    with paddle.no_grad():
+        p, n = paddle.ones([4]), -paddle.ones([4])
+        np.testing.assert_allclose(f(p).numpy(), 2 * np.ones(4))
+        np.testing.assert_allclose(f(n).numpy(), -2 * np.ones(4))
+        np.testing.assert_allclose(f(p).numpy(), 2 * np.ones(4))
+    st = list(f.graph_status().values())
+    assert len(st) == 1 and st[0].startswith('eager'), st
+
+
+class _Branchy(paddle.nn.Layer):
+    def __init__(self):
+        super().__init__()
+        self.l = paddle.nn.Linear(4, 4)
+
+    def forward(self, x):
+        y = self.l(x)
+        if y.mean() > 0 and y.max() > 1:
+            z = y * 2.0
+        else:
+            z = y - 10.0
+        i = paddle.zeros([1])
+        while i < y.abs().max():   # trip count depends on the input
+            z = z + 1.0
+            i = i + 1
+        if z.sum() > 1e9:
+            return z * 0
+        return z
+
+
+def test_dy2static_if_while_both_branches_after_save_load(tmp_path):
+    """`if` / `while` on tensor values: eager and jit.save/load agree for BOTH branches (the
+    saved program holds conditional_block / while sub-blocks decided by the fed values)."""
+    paddle.seed(0)
+    net = _Branchy()
+    net.l.weight.set_value(np.eye(4, dtype='float32'))
+    net.l.bias.set_value(np.zeros(4, 'float32'))
+    pos = paddle.to_tensor(np.full((2, 4), 5.0, 'float32'))
+    neg = paddle.to_tensor(np.full((2, 4), -5.0, 'float32'))
+    e_pos, e_neg = net(pos).numpy(), net(neg).numpy()
+    np.testing.assert_allclose(e_pos, np.full((2, 4), 15.0))
+    np.testing.assert_allclose(e_neg, np.full((2, 4), -10.0))
+    path = str(tmp_path / 'branchy')
+    paddle.jit.save(net, path, input_spec=[InputSpec([None, 4], 'float32')])
+    ops = open(path + '.pdmodel').read()
+    assert 'conditional_block_op' in ops and 'while_op' in ops
+    ld = paddle.jit.load(path)
+    np.testing.assert_allclose(ld(pos).numpy(), e_pos, rtol=1e-6)
+    np.testing.assert_allclose(ld(neg).numpy(), e_neg, rtol=1e-6)
+    two = paddle.to_tensor(np.full((2, 4), 2.0, 'float32'))  # 2 trips instead of 5
+    np.testing.assert_allclose(ld(two).numpy(), net(two).numpy(), rtol=1e-6)
+
+
+def test_dy2static_converter_units():
+    from paddle_ray_amd.jit.dy2static import convert_function
+
+    def g(x, n):
+        acc = 0
+        k = 0
+        while k < n:
+            acc = acc + x
+            k = k + 1
+        if acc > 10 or n == 0:
+            out = acc
+        else:
+            out = -acc
+        return out
+    cg = convert_function(g)
+    assert getattr(cg, '_pra_converted', False)
+    for x, n in ((3, 5), (1, 2), (4, 0)):
+        assert cg(x, n) == g(x, n)
