@@ -44,13 +44,16 @@ def memory_efficient_attention(query, key, value, attn_bias=None, p=0.0, scale=N
         bias = _u(attn_bias.materialize([q.shape[1], k.shape[1]])).to(q.device) if causal \
             else None
         return Tensor(_dense(q, k, v, bias, p, scale, training))
-    if isinstance(attn_bias, AB.BlockDiagonalMask) and flash:
-        outs = []
-        for (qa, qb), (ka, kb) in zip(attn_bias.q_seqinfo.intervals(),
-                                      attn_bias.k_seqinfo.intervals()):
-            outs.append(K.flash_attention(q[:, qa:qb], k[:, ka:kb], v[:, ka:kb],
-                                          causal=attn_bias.causal, scale=scale))
-        return Tensor(torch.cat(outs, 1))
+    if isinstance(attn_bias, AB.BlockDiagonalMask) and flash and q.shape[0] == 1:
+        # the packed blocks are independent sequences: ONE varlen flash launch over all of them
+        qi, ki = attn_bias.q_seqinfo.intervals(), attn_bias.k_seqinfo.intervals()
+        cu_q = torch.tensor([0] + [b for _, b in qi], dtype=torch.int32, device=q.device)
+        cu_k = torch.tensor([0] + [b for _, b in ki], dtype=torch.int32, device=q.device)
+        mq = max(b - a for a, b in qi)
+        mk = max(b - a for a, b in ki)
+        o = K.flash_attn_varlen(q[0], k[0], v[0], cu_q, cu_k, mq, mk, causal=attn_bias.causal,
+                                scale=scale)
+        return Tensor(o[None])
     if isinstance(attn_bias, AB.AttentionBias):
         bias = _u(attn_bias.materialize([q.shape[0], q.shape[2], q.shape[1], k.shape[1]],
                                         dtype='float32')).to(q.device)

@@ -146,10 +146,10 @@ class BertSelfAttention(nn.Layer):
         if attn_mask is None and drop == 0.0:
             o = K.flash_attention_qkvpacked(qkv, causal=False)
         else:
-            q, k, v = (t.transpose(1, 2) for t in qkv.unbind(2))
-            m = None if attn_mask is None else _u(attn_mask).to(q.dtype)
-            o = torch.nn.functional.scaled_dot_product_attention(q, k, v, m, drop)
-            o = o.transpose(1, 2)
+            # padded batches (additive mask) / attention dropout: the flash kernel's extended path
+            q, k, v = qkv.unbind(2)
+            m = None if attn_mask is None else _u(attn_mask)
+            o = K.flash_attention_ext(q, k, v, causal=False, attn_mask=m, dropout=drop)
         return o.reshape(B, S, self.num_heads * self.head_dim)
 
     def forward(self, x, attn_mask=None):

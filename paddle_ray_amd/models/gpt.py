@@ -117,9 +117,9 @@ class GPTAttention(nn.Layer):
         B, S = qkv.shape[0], qkv.shape[1]
         qkv = qkv.view(B, S, 3, self.num_heads, self.head_dim)
         if self.attn_dropout > 0 and self.training:
+            # in-kernel dropout on the attention probabilities (flash kernel, same bits in bwd)
             q, k, v = qkv.unbind(2)
-            o = F.scaled_dot_product_attention(Tensor(q), Tensor(k), Tensor(v), None,
-                                               self.attn_dropout, True, True)._t
+            o = K.flash_attention_ext(q, k, v, causal=True, dropout=self.attn_dropout)
         else:
             o = K.flash_attention_qkvpacked(qkv, causal=True)
         return o.reshape(B, S, self.num_heads * self.head_dim)
@@ -138,8 +138,7 @@ class GPTAttention(nn.Layer):
         qkv = qkv.view(B, S, 3, self.num_heads, self.head_dim)
         q, k, v = qkv.unbind(2)
         if self.attn_dropout > 0 and self.training:
-            o = F.scaled_dot_product_attention(Tensor(q), Tensor(k), Tensor(v), None,
-                                               self.attn_dropout, True, True)._t
+            o = K.flash_attention_ext(q, k, v, causal=True, dropout=self.attn_dropout)
         else:
             o = K.flash_attention(q, k, v, causal=True)
         return self.out_proj(Tensor(o.reshape(B, S, self.num_heads * self.head_dim)))

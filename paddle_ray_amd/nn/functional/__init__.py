@@ -1086,23 +1086,60 @@ def scaled_dot_product_attention(query, key, value, attn_mask=None, dropout_p=0.
                                  training=True, name=None):
     """Inputs [batch, seq, heads, head_dim] (paddle layout)."""
     q, k, v = _t(query), _t(key), _t(value)
-    if attn_mask is None and (dropout_p == 0.0 or not training) and q.is_cuda:
+    drop = dropout_p if training else 0.0
+    if attn_mask is None and drop == 0.0 and q.is_cuda:
         return _w(K.flash_attention(q, k, v, causal=is_causal))
-    qt, kt, vt = (t.transpose(1, 2) for t in (q, k, v))
-    o = TF.scaled_dot_product_attention(qt, kt, vt, _opt(attn_mask),
-                                        dropout_p if training else 0.0, is_causal)
-    return _w(o.transpose(1, 2))
+    # additive / boolean mask and dropout: the flash kernel's extended path on the device (fp32
+    # reference of the same math, same dropout bits, on the host)
+    return _w(K.flash_attention_ext(q, k, v, causal=is_causal, attn_mask=_opt(attn_mask),
+                                    dropout=drop))
+
+
+def _seed_of(fixed_seed_offset):
+    if fixed_seed_offset is None:
+        return None
+    so = _t(fixed_seed_offset).reshape(-1).tolist()
+    return int(so[0])
 
 
 def flash_attention(query, key, value, dropout=0.0, causal=False, return_softmax=False,
                     fixed_seed_offset=None, rng_name="", training=True, name=None):
-    """paddle.nn.functional.flash_attention.flash_attention -> (out, softmax|None)."""
+    """paddle.nn.functional.flash_attention.flash_attention -> (out, softmax|None) (parity:
+    python/paddle/nn/functional/flash_attention.py:20). Dropout runs inside the flash kernel.
+    ``return_softmax`` (a debugging output of the reference) returns the dropped probabilities
+    from the fp32 reference of the same kernel math."""
     q, k, v = _t(query), _t(key), _t(value)
-    if dropout > 0 and training:
-        out = scaled_dot_product_attention(query, key, value, None, dropout, causal, training)
+    drop = dropout if training else 0.0
+    if drop > 0:
+        out = _w(K.flash_attention_ext(q, k, v, causal=causal, dropout=drop,
+                                       seed=_seed_of(fixed_seed_offset)))
     else:
         out = _w(K.flash_attention(q, k, v, causal=causal))
-    return out, None
+    sm = None
+    if return_softmax:
+        with torch.no_grad():
+            B, Sq, H, D = q.shape
+            qf, kf = q.float().permute(0, 2, 1, 3), k.float().permute(0, 2, 1, 3)
+            s_ = torch.matmul(qf, kf.transpose(-1, -2)) / math.sqrt(D)
+            if causal:
+                Sk = kf.shape[2]
+                s_ = s_.masked_fill(torch.ones(Sq, Sk, dtype=torch.bool, device=q.device).triu(Sk - Sq + 1),
+                                    float('-inf'))
+            sm = _w(torch.softmax(s_, -1).to(q.dtype))
+    return out, sm
+
+
+def flash_attn_unpadded(query, key, value, cu_seqlens_q, cu_seqlens_k, max_seqlen_q, max_seqlen_k,
+                        scale, dropout=0.0, causal=False, return_softmax=False,
+                        fixed_seed_offset=None, rng_name="", training=True, name=None):
+    """Variable-length (packed) flash attention (parity: python/paddle/nn/functional/
+    flash_attention.py:121 flash_attn_unpadded): query [total_q, H, D], key/value
+    [total_k, H, D], cu_seqlens_* int32 [B+1]; one HIP launch covers every sequence."""
+    q, k, v = _t(query), _t(key), _t(value)
+    out = K.flash_attn_varlen(q, k, v, _t(cu_seqlens_q), _t(cu_seqlens_k), int(max_seqlen_q),
+                              int(max_seqlen_k), causal=causal, scale=float(scale),
+                              dropout=dropout if training else 0.0, seed=_seed_of(fixed_seed_offset))
+    return _w(out), None
 
 
 def sparse_attention(query, key, value, sparse_csr_offset, sparse_csr_columns,

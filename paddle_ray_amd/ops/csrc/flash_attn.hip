@@ -93,6 +93,50 @@ __device__ __forceinline__ typename V8<T>::type pack_frag(const f32x16& acc, int
 
 constexpr int kTile = 64;        // rows per staged tile (keys in fwd/dQ, queries in dK/dV)
 
+// Extended attention (the EXT kernel variants; parity: flash_attn_kernel.cu:183 / :250 and
+// python/paddle/nn/functional/flash_attention.py:20,121):
+//   * varlen (flash_attn_unpadded): q/k/v/o rows packed [total, H, D]; sequence b is rows
+//     [cu_q[b], cu_q[b+1]) of q/o and [cu_k[b], cu_k[b+1]) of k/v. lse / delta stay
+//     [B, H, SqMax] (padded), the dS^T scratch [B*H][SkMax][SqMax] (rounded).
+//   * additive mask [B|1, H|1, Sq, Sk] (element strides msb/msh/msq, 0 = broadcast; keys
+//     contiguous), in q's dtype or fp32, added to the scaled scores.
+//   * dropout on the probabilities: keep iff a counter hash of (seed, offset, b*H+h, query, key)
+//     clears the threshold; kept values scaled by 1/(1-p). The backward regenerates the same
+//     bits (FA2: dV = (P∘Z)ᵀdO, dS = P∘(Z∘dP − delta), delta = rowsum(dO∘O)).
+struct FaExt {
+  const int* cu_q;
+  const int* cu_k;
+  const void* mask;
+  int64_t msb, msh, msq;
+  int mask_f32;
+  float mask_mul;  // 1 / scale: the kernels add mask/scale to the raw q·k scores
+  uint32_t thr;    // dropout threshold on 24-bit uniforms (0 = no dropout)
+  float inv_keep;
+  uint64_t seed, offset;
+};
+
+__device__ __forceinline__ uint32_t fa_mix32(uint32_t x) {
+  x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
+  return x;
+}
+// dropout multiplier of element (query q, key kk) of head row bh: 0 or 1/(1-p)
+__device__ __forceinline__ float fa_drop(const FaExt& e, int bh, int q, int kk) {
+  const uint64_t c = ((uint64_t)(uint32_t)bh << 40) ^ ((uint64_t)(uint32_t)q << 20) ^ (uint64_t)(uint32_t)kk;
+  const uint32_t a = fa_mix32((uint32_t)c ^ (uint32_t)e.seed ^ ((uint32_t)e.offset * 0x85ebca6bU));
+  const uint32_t r = fa_mix32(a ^ (uint32_t)(c >> 32) ^ (uint32_t)(e.seed >> 32) ^ (uint32_t)(e.offset >> 32) ^
+                              0x9e3779b9U);
+  return (r >> 8) >= e.thr ? e.inv_keep : 0.f;
+}
+// additive mask value (already divided by the softmax scale) of (b, h, query q, key kk)
+template <typename T>
+__device__ __forceinline__ float fa_mask(const FaExt& e, int b, int hh, int q, int kk) {
+  const int64_t i = (int64_t)b * e.msb + (int64_t)hh * e.msh + (int64_t)q * e.msq + kk;
+  float m;
+  if (e.mask_f32) m = static_cast<const float*>(e.mask)[i];
+  else m = Cvt<T>::to(static_cast<const T*>(e.mask)[i]);
+  return m * e.mask_mul;
+}
+
 // Swizzled tile image [64][D] (no padding), element offset of 16-B chunk ch of row `row`:
 // 8-row x 32-column subtiles of 512 B, chunk (ch&3) XOR-ed with (row>>2)&3. One image serves
 // row fragments (ds_read_b128) and transposed fragments (ds_read_b64_tr_b16) bank-conflict
@@ -232,11 +276,11 @@ struct SwzDma {
 // ============================================================================
 // forward
 // ============================================================================
-template <typename T, int D, bool CAUSAL, int NW>
+template <typename T, int D, bool CAUSAL, int NW, bool EXT = false>
 __global__ void __launch_bounds__(NW * 64, 2)
 fwd_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restrict__ v, T* __restrict__ o,
-           float* __restrict__ lse, int H, int Sq, int Sk, int64_t qsb, int64_t qss, int64_t qsh, int64_t ksb,
-           int64_t kss, int64_t ksh, int64_t vsb, int64_t vss, int64_t vsh, float scale_log2) {
+           float* __restrict__ lse, int H, int SqM, int SkM, int64_t qsb, int64_t qss, int64_t qsh, int64_t ksb,
+           int64_t kss, int64_t ksh, int64_t vsb, int64_t vss, int64_t vsh, float scale_log2, FaExt ext = {}) {
   // double-buffered {K, V} swizzled images; V^T fragments by transposed reads of V
   extern __shared__ __attribute__((aligned(16))) char smem[];
   T* img0 = reinterpret_cast<T*>(smem);  // [2][2][64*D]
@@ -251,11 +295,22 @@ fwd_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restrict
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
   const int q0 = qb * BM;
   const int myq = q0 + wave * 32 + r;
+  int Sq = SqM, Sk = SkM;
+  int64_t qrow0 = (int64_t)b * SqM, krow0 = 0;  // first packed row of this sequence (o rows / k,v rows)
+  if constexpr (EXT) {
+    if (ext.cu_q) {
+      qrow0 = ext.cu_q[b];
+      krow0 = ext.cu_k[b];
+      Sq = ext.cu_q[b + 1] - (int)qrow0;
+      Sk = ext.cu_k[b + 1] - (int)krow0;
+      if (q0 >= Sq) return;  // the whole block is past this sequence (uniform: before any barrier)
+    }
+  }
   const int off = Sk - Sq;
 
-  const T* qb_ = q + b * qsb + hh * qsh;
-  const T* kb_ = k + b * ksb + hh * ksh;
-  const T* vb_ = v + b * vsb + hh * vsh;
+  const T* qb_ = EXT && ext.cu_q ? q + qrow0 * qss + hh * qsh : q + b * qsb + hh * qsh;
+  const T* kb_ = EXT && ext.cu_q ? k + krow0 * kss + hh * ksh : k + b * ksb + hh * ksh;
+  const T* vb_ = EXT && ext.cu_q ? v + krow0 * vss + hh * vsh : v + b * vsb + hh * vsh;
 
   typename V8<T>::type qf[NS];
   {
@@ -353,6 +408,17 @@ fwd_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restrict
           s_acc[mt][i] = bad ? -INFINITY : s_acc[mt][i];
         }
     }
+    if constexpr (EXT) {
+      if (ext.mask && myq < Sq) {
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const int key = k0 + 32 * mt + acc_row(i, h);
+            if (mt < nlive && key < Sk) s_acc[mt][i] += fa_mask<T>(ext, b, hh, myq, key);
+          }
+      }
+    }
     float mx = -INFINITY;
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt)
@@ -374,8 +440,10 @@ fwd_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restrict
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         float p = fexp2(fmaf(s_acc[mt][i], scale_log2, -m_use));
+        ps += p;  // the softmax denominator sums the undropped probabilities
+        if constexpr (EXT)
+          if (ext.thr) p *= fa_drop(ext, bh, myq, k0 + 32 * mt + acc_row(i, h));
         s_acc[mt][i] = p;
-        ps += p;
       }
     ps += __shfl_xor(ps, 32, 64);
     l_run += ps;
@@ -402,7 +470,7 @@ fwd_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restrict
 
   if (myq < Sq) {
     const float inv = l_run > 0.f ? 1.f / l_run : 0.f;
-    T* orow = o + ((int64_t)b * Sq + myq) * ((int64_t)H * D) + (int64_t)hh * D;
+    T* orow = o + (qrow0 + myq) * ((int64_t)H * D) + (int64_t)hh * D;
 #pragma unroll
     for (int dt = 0; dt < ND; ++dt)
 #pragma unroll
@@ -415,7 +483,7 @@ fwd_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restrict
       }
     if (h == 0) {
       const float l2 = l_run > 0.f ? (m_run + log2f(l_run)) : INFINITY;
-      lse[(int64_t)bh * Sq + myq] = l2 * 0.6931471805599453f;
+      lse[(int64_t)bh * SqM + myq] = l2 * 0.6931471805599453f;
     }
   }
 }
@@ -605,14 +673,14 @@ bwd_dq_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restr
 // ============================================================================
 // WDS: also store dS^T (bf16/f16, unscaled) to dsT[bh][key][query] (row pitch Sqp, Skp rows) for
 // bwd_dq_ds_kernel, which then forms dQ = dS K without recomputing S and dP.
-template <typename T, int D, bool CAUSAL, bool WDS>
+template <typename T, int D, bool CAUSAL, bool WDS, bool EXT = false>
 __global__ void __launch_bounds__(256, 1)
 bwd_dkdv_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restrict__ v, const T* __restrict__ dO,
                 const float* __restrict__ lse, const float* __restrict__ delta, T* __restrict__ dk,
-                T* __restrict__ dv, int H, int Sq, int Sk, int64_t qsb, int64_t qss, int64_t qsh, int64_t ksb,
+                T* __restrict__ dv, int H, int SqM, int SkM, int64_t qsb, int64_t qss, int64_t qsh, int64_t ksb,
                 int64_t kss, int64_t ksh, int64_t vsb, int64_t vss, int64_t vsh, int64_t dksb, int64_t dkss,
                 int64_t dksh, int64_t dvsb, int64_t dvss, int64_t dvsh, float scale, float scale_log2,
-                T* __restrict__ dsT, int Sqp, int64_t dsbh) {
+                T* __restrict__ dsT, int Sqp, int64_t dsbh, FaExt ext = {}) {
   // Double-buffered LDS: buffer b = {Q image, dO image} (swizzled rows, read both row-wise and
   // transposed) + lse/delta of the tile's 64 queries. The next tile is written into the idle
   // buffer right after the current tile's MFMAs are issued: one barrier per tile.
@@ -628,14 +696,26 @@ bwd_dkdv_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __res
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
   const int kblk0 = kb * 128;
   const int mykey = kblk0 + wave * 32 + r;
+  int Sq = SqM, Sk = SkM;
+  int64_t qrow0 = (int64_t)b * SqM, krow0 = 0;
+  if constexpr (EXT) {
+    if (ext.cu_q) {
+      qrow0 = ext.cu_q[b];
+      krow0 = ext.cu_k[b];
+      Sq = ext.cu_q[b + 1] - (int)qrow0;
+      Sk = ext.cu_k[b + 1] - (int)krow0;
+      if (kblk0 >= Sk) return;  // uniform, before any barrier
+    }
+  }
   const int off = Sk - Sq;
   const bool kvalid = mykey < Sk;
+  const bool vl = EXT && ext.cu_q;
 
-  const T* qb_ = q + b * qsb + hh * qsh;
-  const T* kb_ = k + b * ksb + hh * ksh;
-  const T* vb_ = v + b * vsb + hh * vsh;
+  const T* qb_ = vl ? q + qrow0 * qss + hh * qsh : q + b * qsb + hh * qsh;
+  const T* kb_ = vl ? k + krow0 * kss + hh * ksh : k + b * ksb + hh * ksh;
+  const T* vb_ = vl ? v + krow0 * vss + hh * vsh : v + b * vsb + hh * vsh;
   const int64_t HD = (int64_t)H * D;
-  const T* dob_ = dO + (int64_t)b * Sq * HD + (int64_t)hh * D;
+  const T* dob_ = dO + qrow0 * HD + (int64_t)hh * D;
 
   typename V8<T>::type kf[NS], vf[NS];
   {
@@ -668,8 +748,8 @@ bwd_dkdv_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __res
     dd.issue(img + kTile * D * sizeof(T), (uint32_t)((int64_t)qs0 * HD * 2), wave);
     if (threadIdx.x < kTile) {
       const int qq = qs0 + threadIdx.x;
-      lreg = qq < Sq ? lse[(int64_t)bh * Sq + qq] : INFINITY;  // scaled at store (no wait here)
-      dreg = qq < Sq ? delta[(int64_t)bh * Sq + qq] : 0.f;
+      lreg = qq < Sq ? lse[(int64_t)bh * SqM + qq] : INFINITY;  // scaled at store (no wait here)
+      dreg = qq < Sq ? delta[(int64_t)bh * SqM + qq] : 0.f;
     }
   };
   auto store_tile = [&](int buf) {
@@ -754,10 +834,21 @@ bwd_dkdv_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __res
 #pragma unroll
           for (int c = 0; c < 4; ++c) {
             const int i = 4 * g + c;
-            float p = fexp2(fmaf(sa[nt][i], scale_log2, -la[c]));
+            const int qq = qs0 + 32 * nt + 8 * g + 4 * h + c;
+            float sv = sa[nt][i];
+            if constexpr (EXT)
+              if (ext.mask && qq < Sq && kvalid) sv += fa_mask<T>(ext, b, hh, qq, mykey);
+            float p = fexp2(fmaf(sv, scale_log2, -la[c]));
             if constexpr (MASK) {
-              const int qq = qs0 + 32 * nt + 8 * g + 4 * h + c;
               if (qq >= Sq || (CAUSAL && mykey > qq + off)) p = 0.f;
+            }
+            if constexpr (EXT) {
+              if (ext.thr) {
+                const float z = fa_drop(ext, bh, qq, mykey);  // same bits as the forward
+                sa[nt][i] = p * z;
+                da[nt][i] = p * (da[nt][i] * z - dl[c]);
+                continue;
+              }
             }
             sa[nt][i] = p;
             da[nt][i] = p * (da[nt][i] - dl[c]);
@@ -802,8 +893,8 @@ bwd_dkdv_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __res
   for (int it = it1; it < ntiles; ++it) tile(it, std::true_type{});
 
   if (kvalid) {
-    T* krow = dk + (int64_t)b * dksb + (int64_t)mykey * dkss + (int64_t)hh * dksh;
-    T* vrow = dv + (int64_t)b * dvsb + (int64_t)mykey * dvss + (int64_t)hh * dvsh;
+    T* krow = (vl ? dk + krow0 * dkss : dk + (int64_t)b * dksb) + (int64_t)mykey * dkss + (int64_t)hh * dksh;
+    T* vrow = (vl ? dv + krow0 * dvss : dv + (int64_t)b * dvsb) + (int64_t)mykey * dvss + (int64_t)hh * dvsh;
 #pragma unroll
     for (int dt = 0; dt < ND; ++dt)
 #pragma unroll
@@ -829,11 +920,11 @@ bwd_dkdv_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __res
 // (buffer_load ... lds: no VGPR staging, no ds_write) with per-lane source offsets that
 // realise the swizzle, and the buffer range check zero-fills key rows >= Sk.
 // ============================================================================
-template <typename T, int D, bool CAUSAL>
+template <typename T, int D, bool CAUSAL, bool EXT = false>
 __global__ void __launch_bounds__(512, 1)
-bwd_dq_ds_kernel(const T* __restrict__ k, const T* __restrict__ dsT, T* __restrict__ dq, int H, int Sq, int Sk,
+bwd_dq_ds_kernel(const T* __restrict__ k, const T* __restrict__ dsT, T* __restrict__ dq, int H, int SqM, int SkM,
                  int Sqp, int64_t dsbh, int64_t ksb, int64_t kss, int64_t ksh, int64_t dqsb, int64_t dqss,
-                 int64_t dqsh, float scale) {
+                 int64_t dqsh, float scale, FaExt ext = {}) {
   constexpr int NW = 8, NT = NW * 64, BM = NW * 32, ND = D / 32, BUF = kTile * D + kTile * BM;
   // 3-slot ring, tiles staged two ahead: the per-tile MFMA work (16 per wave) is far shorter
   // than a DMA round trip, so one tile in flight per CU left the kernel latency-bound
@@ -848,6 +939,18 @@ bwd_dq_ds_kernel(const T* __restrict__ k, const T* __restrict__ dsT, T* __restri
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
   const int q0 = qb * BM;
   const int myq = q0 + wave * 32 + r;
+  int Sq = SqM, Sk = SkM;
+  int64_t qrow0 = 0, krow0 = 0;
+  const bool vl = EXT && ext.cu_q;
+  if constexpr (EXT) {
+    if (ext.cu_q) {
+      qrow0 = ext.cu_q[b];
+      krow0 = ext.cu_k[b];
+      Sq = ext.cu_q[b + 1] - (int)qrow0;
+      Sk = ext.cu_k[b + 1] - (int)krow0;
+      if (q0 >= Sq) return;  // uniform, before any barrier
+    }
+  }
   const int off = Sk - Sq;
 
   f32x16 acc_q[ND];
@@ -862,7 +965,7 @@ bwd_dq_ds_kernel(const T* __restrict__ k, const T* __restrict__ dsT, T* __restri
   const LaneOffs<BM> ls(lane);
   SwzDma<D, NT> kd;
   SwzDma<BM, NT> sd;
-  kd.init(k + b * ksb + hh * ksh, kss, Sk, wave, lane);
+  kd.init(vl ? k + krow0 * kss + hh * ksh : k + b * ksb + hh * ksh, kss, Sk, wave, lane);
   sd.init(dsT + (int64_t)bh * dsbh + q0, Sqp, Sk, wave, lane);
   auto stage = [&](int kt) {
     const uint32_t img = lds0 + (uint32_t)((kt % NBUF) * BUF * sizeof(T));
@@ -930,7 +1033,7 @@ bwd_dq_ds_kernel(const T* __restrict__ k, const T* __restrict__ dsT, T* __restri
   for (int kt = nfull; kt < ntiles; ++kt) tile(kt, std::true_type{});
 
   if (myq < Sq) {
-    T* row = dq + (int64_t)b * dqsb + (int64_t)myq * dqss + (int64_t)hh * dqsh;
+    T* row = (vl ? dq + qrow0 * dqss : dq + (int64_t)b * dqsb) + (int64_t)myq * dqss + (int64_t)hh * dqsh;
 #pragma unroll
     for (int dt = 0; dt < ND; ++dt)
 #pragma unroll
@@ -952,7 +1055,8 @@ static void launch_fwd_nw(const void* q, const void* k, const void* v, void* o, 
   hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   dim3 grid(B * H, (Sq + NW * 32 - 1) / (NW * 32));
   hipLaunchKernelGGL(kern, grid, dim3(NW * 64), lds, s, (const T*)q, (const T*)k, (const T*)v, (T*)o, lse, H, Sq, Sk,
-                     st[0], st[1], st[2], st[3], st[4], st[5], st[6], st[7], st[8], scale * 1.4426950408889634f);
+                     st[0], st[1], st[2], st[3], st[4], st[5], st[6], st[7], st[8], scale * 1.4426950408889634f,
+                     FaExt{});
 }
 
 // 8 waves = one 256-query block per CU (4-wave blocks, two per CU, measured the same)
@@ -979,14 +1083,14 @@ static void launch_bwd(const void* q, const void* k, const void* v, const void* 
       hipLaunchKernelGGL(kern, dim3(B * H, (Sk + 127) / 128), dim3(256), lds, s, (const T*)q, (const T*)k,
                          (const T*)v, (const T*)dO, lse, delta, (T*)dk, (T*)dv, H, Sq, Sk, st[0], st[1], st[2],
                          st[3], st[4], st[5], st[6], st[7], st[8], st[12], st[13], st[14], st[15], st[16], st[17],
-                         scale, sl2, (T*)dsT, Sqp, dsbh);
+                         scale, sl2, (T*)dsT, Sqp, dsbh, FaExt{});
     }
     {
       const size_t lds = 3 * (kTile * D + kTile * 256) * sizeof(T);
       auto kern = bwd_dq_ds_kernel<T, D, C>;
       hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       hipLaunchKernelGGL(kern, dim3(B * H, (Sq + 255) / 256), dim3(512), lds, s, (const T*)k, (const T*)dsT,
-                         (T*)dq, H, Sq, Sk, Sqp, dsbh, st[3], st[4], st[5], st[9], st[10], st[11], scale);
+                         (T*)dq, H, Sq, Sk, Sqp, dsbh, st[3], st[4], st[5], st[9], st[10], st[11], scale, FaExt{});
     }
     return;
   }
@@ -1009,7 +1113,45 @@ static void launch_bwd(const void* q, const void* k, const void* v, const void* 
     hipLaunchKernelGGL(kern, dim3(B * H, (Sk + 127) / 128), dim3(256), lds, s, (const T*)q, (const T*)k,
                        (const T*)v, (const T*)dO, lse, delta, (T*)dk, (T*)dv, H, Sq, Sk, st[0], st[1], st[2],
                        st[3], st[4], st[5], st[6], st[7], st[8], st[12], st[13], st[14], st[15], st[16], st[17],
-                       scale, sl2, (T*)nullptr, 0, (int64_t)0);
+                       scale, sl2, (T*)nullptr, 0, (int64_t)0, FaExt{});
+  }
+}
+
+// extended variants (varlen / additive mask / dropout): forward + the dS^T backward
+template <typename T, int D, bool C>
+static void launch_fwd_ext(const void* q, const void* k, const void* v, void* o, float* lse, int B, int H, int Sq,
+                           int Sk, const int64_t* st, float scale, const FaExt& ext, hipStream_t s) {
+  constexpr int NW = C ? 4 : 8;
+  const size_t lds = 4 * kTile * D * sizeof(T);
+  auto kern = fwd_kernel<T, D, C, NW, true>;
+  hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  dim3 grid(B * H, (Sq + NW * 32 - 1) / (NW * 32));
+  hipLaunchKernelGGL(kern, grid, dim3(NW * 64), lds, s, (const T*)q, (const T*)k, (const T*)v, (T*)o, lse, H, Sq, Sk,
+                     st[0], st[1], st[2], st[3], st[4], st[5], st[6], st[7], st[8], scale * 1.4426950408889634f, ext);
+}
+
+template <typename T, int D, bool C>
+static void launch_bwd_ext(const void* q, const void* k, const void* v, const void* dO, const float* lse,
+                           const float* delta, void* dq, void* dk, void* dv, void* dsT, int B, int H, int Sq, int Sk,
+                           const int64_t* st, float scale, const FaExt& ext, hipStream_t s) {
+  const float sl2 = scale * 1.4426950408889634f;
+  const int Sqp = (Sq + 255) / 256 * 256;
+  const int64_t dsbh = (int64_t)((Sk + 127) / 128 * 128) * Sqp;
+  {
+    const size_t lds = 4 * kTile * D * sizeof(T) + 4 * kTile * sizeof(float) + 4 * 32 * 80;
+    auto kern = bwd_dkdv_kernel<T, D, C, true, true>;
+    hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(kern, dim3(B * H, (Sk + 127) / 128), dim3(256), lds, s, (const T*)q, (const T*)k,
+                       (const T*)v, (const T*)dO, lse, delta, (T*)dk, (T*)dv, H, Sq, Sk, st[0], st[1], st[2],
+                       st[3], st[4], st[5], st[6], st[7], st[8], st[12], st[13], st[14], st[15], st[16], st[17],
+                       scale, sl2, (T*)dsT, Sqp, dsbh, ext);
+  }
+  {
+    const size_t lds = 3 * (kTile * D + kTile * 256) * sizeof(T);
+    auto kern = bwd_dq_ds_kernel<T, D, C, true>;
+    hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(kern, dim3(B * H, (Sq + 255) / 256), dim3(512), lds, s, (const T*)k, (const T*)dsT,
+                       (T*)dq, H, Sq, Sk, Sqp, dsbh, st[3], st[4], st[5], st[9], st[10], st[11], scale, ext);
   }
 }
 
@@ -1041,6 +1183,36 @@ int pra_flash_fwd(const void* q, const void* k, const void* v, void* o, float* l
 // contiguous) and written to `delta` for the dK/dV kernel; o == nullptr: `delta` is an input.
 // dsT != nullptr (requires o == nullptr): dS^T scratch of B*H*roundup(Sk,128)*roundup(Sq,256)
 // elements; dQ = dS K is formed from it instead of recomputing S and dP in a dQ sweep.
+// Extended forward: varlen (cu_q / cu_k [B+1] row prefix sums of packed [total, H, D] q/k/v/o;
+// Sq, Sk = the longest sequences; lse [B, H, Sq]), additive mask (element strides msb / msh /
+// msq, keys contiguous; mask_f32: fp32 else q's dtype), dropout p_drop with (seed, offset).
+int pra_flash_fwd_ext(const void* q, const void* k, const void* v, void* o, float* lse, int B, int H, int Sq, int Sk,
+                      int D, const int64_t* strides, float scale, int causal, int dt, const int* cu_q,
+                      const int* cu_k, const void* mask, int64_t msb, int64_t msh, int64_t msq, int mask_f32,
+                      float p_drop, uint64_t seed, uint64_t offset, hipStream_t s) {
+  if (!(D == 64 || D == 128) || !(dt == kBF16 || dt == kF16)) return -1;
+  if (!(p_drop >= 0.f && p_drop < 1.f) || (!cu_q) != (!cu_k)) return -1;
+  if (B * H == 0 || Sq == 0) return 0;
+  fa::FaExt e{cu_q, cu_k, mask, msb, msh, msq, mask_f32, 1.f / scale,
+              (uint32_t)(p_drop * 16777216.f), p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f, seed, offset};
+  PRA_FA_DISPATCH(launch_fwd_ext, q, k, v, o, lse, B, H, Sq, Sk, strides, scale, e, s);
+  return 0;
+}
+// Extended backward (same extras as the forward; `delta` = rowsum(dO*O) [B, H, Sq] is an input,
+// dsT the dS^T scratch of B*H*roundup(Sk,128)*roundup(Sq,256) elements)
+int pra_flash_bwd_ext(const void* q, const void* k, const void* v, const void* dO, const float* lse,
+                      const float* delta, void* dq, void* dk, void* dv, void* dsT, int B, int H, int Sq, int Sk, int D,
+                      const int64_t* strides, float scale, int causal, int dt, const int* cu_q, const int* cu_k,
+                      const void* mask, int64_t msb, int64_t msh, int64_t msq, int mask_f32, float p_drop,
+                      uint64_t seed, uint64_t offset, hipStream_t s) {
+  if (!(D == 64 || D == 128) || !(dt == kBF16 || dt == kF16) || !dsT) return -1;
+  if (!(p_drop >= 0.f && p_drop < 1.f) || (!cu_q) != (!cu_k)) return -1;
+  if (B * H == 0 || Sq == 0) return 0;
+  fa::FaExt e{cu_q, cu_k, mask, msb, msh, msq, mask_f32, 1.f / scale,
+              (uint32_t)(p_drop * 16777216.f), p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f, seed, offset};
+  PRA_FA_DISPATCH(launch_bwd_ext, q, k, v, dO, lse, delta, dq, dk, dv, dsT, B, H, Sq, Sk, strides, scale, e, s);
+  return 0;
+}
 int pra_flash_bwd(const void* q, const void* k, const void* v, const void* dO, const void* o, const float* lse,
                   float* delta, void* dq, void* dk, void* dv, void* dsT, int B, int H, int Sq, int Sk, int D,
                   const int64_t* strides, float scale, int causal, int dt, hipStream_t s) {

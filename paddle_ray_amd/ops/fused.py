@@ -13,6 +13,7 @@ Each op has a ``hip`` kernel (gfx950, ``ops/csrc/*.hip``) and a ``ref`` kernel
 import math
 import os
 
+import numpy as np
 import torch
 
 from . import registry as R
@@ -941,6 +942,206 @@ def flash_attention(q, k, v, causal=False, scale=None):
     if scale is None:
         scale = 1.0 / math.sqrt(q.shape[-1])
     return FlashAttnFn.apply(q, k, v, causal, scale)
+
+
+# -- extended flash attention: additive mask, in-kernel dropout, varlen (packed) ----------------
+_M32 = 0xffffffff
+
+
+def _mix32_t(x):
+    x = x ^ (x >> 16)
+    x = (x * 0x7feb352d) & _M32
+    x = x ^ (x >> 15)
+    x = (x * 0x846ca68b) & _M32
+    return x ^ (x >> 16)
+
+
+def fa_dropout_mask_ref(seed, offset, bh, q, kk, p_drop):
+    """The keep multiplier (0 or 1/(1-p)) the flash kernels use for (head row bh, query q, key
+    kk) — a torch port of flash_attn.hip fa_drop for references and tests. bh/q/kk: int64
+    tensors (broadcastable)."""
+    thr = int(float(np.float32(p_drop)) * 16777216.0)
+    inv_keep = float(np.float32(1.0) / (np.float32(1.0) - np.float32(p_drop)))
+    c = (bh << 40) ^ (q << 20) ^ kk
+    k0 = (seed & _M32) ^ (((offset & _M32) * 0x85ebca6b) & _M32)
+    a = _mix32_t((c & _M32) ^ k0)
+    r = _mix32_t(a ^ ((c >> 32) & _M32) ^ ((seed >> 32) & _M32) ^ ((offset >> 32) & _M32) ^ 0x9e3779b9)
+    return torch.where((r >> 8) >= thr, inv_keep, 0.0)
+
+
+def _fa_ext_ref_dense(q, k, v, causal, scale, mask=None, p_drop=0.0, seed=0, offset=0, bh0=None):
+    """fp32 reference of the extended kernels for one dense batch [B, S, H, D] (autograd-able)."""
+    qf, kf, vf = (t.float().permute(0, 2, 1, 3) for t in (q, k, v))
+    B, H, Sq, Sk = qf.shape[0], qf.shape[1], qf.shape[2], kf.shape[2]
+    s = torch.matmul(qf, kf.transpose(-1, -2)) * scale
+    if mask is not None:
+        s = s + mask.float()
+    if causal:
+        m = torch.ones(Sq, Sk, dtype=torch.bool, device=s.device).triu(Sk - Sq + 1)
+        s = s.masked_fill(m, float('-inf'))
+    lse = torch.logsumexp(s, -1)
+    p = torch.exp(s - lse[..., None]).nan_to_num(0.0)
+    if p_drop > 0:
+        dev = q.device
+        bh = (torch.arange(B * H, device=dev) if bh0 is None else bh0).view(B, H, 1, 1)
+        qi = torch.arange(Sq, device=dev).view(1, 1, Sq, 1)
+        ki = torch.arange(Sk, device=dev).view(1, 1, 1, Sk)
+        p = p * fa_dropout_mask_ref(seed, offset, bh, qi, ki, p_drop).to(p.dtype)
+    o = torch.matmul(p, vf).permute(0, 2, 1, 3)
+    return o, lse
+
+
+def _mask_strides(mask, B, H, Sq, Sk):
+    """[B|1, H|1, Sq, Sk] additive mask (any broadcastable rank <= 4, keys contiguous) ->
+    (tensor, msb, msh, msq, is_fp32) with 0 strides on broadcast dims."""
+    m = mask
+    while m.dim() < 4:
+        m = m.unsqueeze(0)
+    m = m.expand(B, H, Sq, Sk)
+    if m.stride(3) != 1:
+        m = m.contiguous()
+    return m, m.stride(0), m.stride(1), m.stride(2), m.dtype == torch.float32
+
+
+_FA_RNG_OFFSET = [0]
+
+
+def _fa_next_rng(seed=None, numel=1):
+    """(seed, offset) for one dropout call: the generator's seed, and an offset advanced per call
+    (the Philox-offset discipline of the reference's flash_attn kernels)."""
+    if seed is None:
+        seed = int(torch.initial_seed()) & ((1 << 63) - 1)
+    off = _FA_RNG_OFFSET[0]
+    _FA_RNG_OFFSET[0] += 1
+    return seed, off
+
+
+class FlashAttnExtFn(torch.autograd.Function):
+    """Flash attention with an additive mask and/or in-kernel dropout, dense [B, S, H, D] or
+    varlen packed [total, H, D] (cu_q / cu_k int32 [B+1]): one HIP forward, the dS^T backward."""
+
+    @staticmethod
+    def forward(ctx, q, k, v, mask, cu_q, cu_k, max_sq, max_sk, causal, scale, p_drop, seed, offset):
+        L = _native.lib()
+        varlen = cu_q is not None
+        if varlen:
+            B = cu_q.numel() - 1
+            H, D = q.shape[1], q.shape[2]
+            Sq, Sk = int(max_sq), int(max_sk)
+            st = [0, q.stride(0), q.stride(1), 0, k.stride(0), k.stride(1), 0, v.stride(0), v.stride(1)]
+            o = torch.empty((q.shape[0], H, D), device=q.device, dtype=q.dtype)
+        else:
+            B, Sq, H, D = q.shape
+            Sk = k.shape[1]
+            st = [q.stride(0), q.stride(1), q.stride(2), k.stride(0), k.stride(1), k.stride(2),
+                  v.stride(0), v.stride(1), v.stride(2)]
+            o = torch.empty((B, Sq, H, D), device=q.device, dtype=q.dtype)
+        lse = torch.empty((B, H, Sq), device=q.device, dtype=torch.float32)
+        mk, msb, msh, msq, m32 = (None, 0, 0, 0, False) if mask is None else \
+            _mask_strides(mask, B, H, Sq, Sk)
+        L.flash_fwd_ext(_ptr(q), _ptr(k), _ptr(v), _ptr(o), _ptr(lse), B, H, Sq, Sk, D, st, float(scale),
+                        int(causal), _dt(q), _ptr(cu_q) if varlen else 0, _ptr(cu_k) if varlen else 0,
+                        _ptr(mk) if mk is not None else 0, msb, msh, msq, int(m32), float(p_drop),
+                        int(seed), int(offset), _stream())
+        ctx.save_for_backward(q, k, v, o, lse, mk if mk is not None else torch.empty(0), cu_q if varlen else
+                              torch.empty(0), cu_k if varlen else torch.empty(0))
+        ctx.meta = (varlen, B, H, D, Sq, Sk, st, causal, scale, p_drop, seed, offset,
+                    (msb, msh, msq, m32) if mk is not None else None)
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        q, k, v, o, lse, mk, cu_q, cu_k = ctx.saved_tensors
+        varlen, B, H, D, Sq, Sk, st, causal, scale, p_drop, seed, offset, mmeta = ctx.meta
+        L = _native.lib()
+        do = _like(do, q.dtype).contiguous()
+        delta = torch.empty((B, H, Sq), device=q.device, dtype=torch.float32)
+        if varlen:
+            dd = (do.float() * o.float()).sum(-1)                     # [total, H]
+            lens = (cu_q[1:] - cu_q[:-1]).long()
+            bidx = torch.repeat_interleave(torch.arange(B, device=q.device), lens)
+            qidx = torch.arange(q.shape[0], device=q.device) - cu_q.long()[bidx]
+            delta.view(B, H, Sq).permute(0, 2, 1)[bidx, qidx] = dd
+            dq = torch.empty_like(q)
+            dk = torch.empty_like(k)
+            dv = torch.empty_like(v)
+            gst = st + [0, dq.stride(0), dq.stride(1), 0, dk.stride(0), dk.stride(1), 0, dv.stride(0),
+                        dv.stride(1)]
+        else:
+            L.flash_bwd_pre(_ptr(o), _ptr(do), _ptr(delta), B, H, Sq, D, _dt(q), _stream())
+            dq = torch.empty((B, Sq, H, D), device=q.device, dtype=q.dtype)
+            dk = torch.empty((B, Sk, H, D), device=q.device, dtype=q.dtype)
+            dv = torch.empty((B, Sk, H, D), device=q.device, dtype=q.dtype)
+            gst = st + [dq.stride(0), dq.stride(1), dq.stride(2), dk.stride(0), dk.stride(1), dk.stride(2),
+                        dv.stride(0), dv.stride(1), dv.stride(2)]
+        ds = torch.empty(B * H * (-(-Sk // 128) * 128) * (-(-Sq // 256) * 256), device=q.device,
+                         dtype=q.dtype)
+        msb, msh, msq, m32 = mmeta if mmeta is not None else (0, 0, 0, False)
+        L.flash_bwd_ext(_ptr(q), _ptr(k), _ptr(v), _ptr(do), _ptr(lse), _ptr(delta), _ptr(dq), _ptr(dk),
+                        _ptr(dv), _ptr(ds), B, H, Sq, Sk, D, gst, float(scale), int(causal), _dt(q),
+                        _ptr(cu_q) if varlen else 0, _ptr(cu_k) if varlen else 0,
+                        _ptr(mk) if mmeta is not None else 0, msb, msh, msq, int(m32), float(p_drop),
+                        int(seed), int(offset), _stream())
+        return dq, dk, dv, None, None, None, None, None, None, None, None, None, None
+
+
+def _fa_ext_ok(q, k, v):
+    return (q.is_cuda and _native.available() and q.dtype in (torch.bfloat16, torch.float16) and
+            q.shape[-1] in (64, 128) and q.stride(-1) == 1 and k.stride(-1) == 1 and
+            v.stride(-1) == 1 and k.dtype == q.dtype and v.dtype == q.dtype)
+
+
+def flash_attention_ext(q, k, v, causal=False, scale=None, attn_mask=None, dropout=0.0, seed=None):
+    """[B, S, H, D] flash attention with an optional additive ``attn_mask`` (broadcastable to
+    [B, H, Sq, Sk]; a bool mask means keep=True) and in-kernel dropout on the probabilities."""
+    if scale is None:
+        scale = 1.0 / math.sqrt(q.shape[-1])
+    B, Sq, H, _ = q.shape
+    Sk = k.shape[1]
+    if attn_mask is not None and attn_mask.dtype == torch.bool:
+        attn_mask = torch.zeros(attn_mask.shape, dtype=q.dtype, device=q.device).masked_fill(
+            ~attn_mask, float('-inf'))
+    if attn_mask is not None and attn_mask.dtype not in (q.dtype, torch.float32):
+        attn_mask = attn_mask.to(q.dtype)
+    sd, off = _fa_next_rng(seed) if dropout > 0 else (0, 0)
+    if _fa_ext_ok(q, k, v):
+        R._STATS[('flash_attn_ext', 'hip')] += 1
+        return FlashAttnExtFn.apply(q, k, v, attn_mask, None, None, Sq, Sk, causal, scale,
+                                    float(dropout), sd, off)
+    R._STATS[('flash_attn_ext', 'ref')] += 1
+    o, _ = _fa_ext_ref_dense(q, k, v, causal, scale, attn_mask, dropout, sd, off)
+    return o.to(q.dtype)
+
+
+def flash_attn_varlen(q, k, v, cu_q, cu_k, max_sq, max_sk, causal=False, scale=None, dropout=0.0,
+                      seed=None):
+    """Packed variable-length attention (paddle flash_attn_unpadded): q [total_q, H, D],
+    k/v [total_k, H, D], cu_q/cu_k [B+1] row prefix sums; sequence b attends only inside itself."""
+    if scale is None:
+        scale = 1.0 / math.sqrt(q.shape[-1])
+    cu_q = cu_q.to(device=q.device, dtype=torch.int32).contiguous()
+    cu_k = cu_k.to(device=q.device, dtype=torch.int32).contiguous()
+    sd, off = _fa_next_rng(seed) if dropout > 0 else (0, 0)
+    if _fa_ext_ok(q, k, v):
+        R._STATS[('flash_attn_varlen', 'hip')] += 1
+        return FlashAttnExtFn.apply(q, k, v, None, cu_q, cu_k, int(max_sq), int(max_sk), causal, scale,
+                                    float(dropout), sd, off)
+    R._STATS[('flash_attn_varlen', 'ref')] += 1
+    return flash_attn_varlen_ref(q, k, v, cu_q, cu_k, causal, scale, dropout, sd, off)
+
+
+def flash_attn_varlen_ref(q, k, v, cu_q, cu_k, causal, scale, dropout=0.0, seed=0, offset=0):
+    """Per-sequence dense fp32 reference of the varlen kernel (same dropout bits)."""
+    outs = []
+    H = q.shape[1]
+    cq, ck = cu_q.tolist(), cu_k.tolist()
+    for b in range(len(cq) - 1):
+        qs, ks, vs = q[cq[b]:cq[b + 1]], k[ck[b]:ck[b + 1]], v[ck[b]:ck[b + 1]]
+        bh0 = torch.arange(b * H, (b + 1) * H, device=q.device)
+        o, _ = _fa_ext_ref_dense(qs[None], ks[None], vs[None], causal, scale, None, dropout, seed, offset,
+                                 bh0=bh0)
+        outs.append(o[0])
+    return torch.cat(outs, 0).to(q.dtype)
 
 
 # =============================================================================

@@ -1,0 +1,156 @@
+"""Flash attention extensions: additive mask, in-kernel dropout, varlen (flash_attn_unpadded).
+GPU tests compare the HIP kernels with an fp32 PyTorch reference that applies the SAME dropout
+bits (ops.fused.fa_dropout_mask_ref, a port of the kernel's counter hash); varlen against
+per-sequence dense attention. Parity: python/paddle/nn/functional/flash_attention.py:20,121,
+paddle/phi/kernels/gpu/flash_attn_kernel.cu:183,250."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+import paddle_ray_amd as paddle
+from paddle_ray_amd.ops import fused as K
+
+
+def test_dropout_hash_statistics_cpu():
+    bh = torch.arange(4).view(4, 1, 1)
+    q = torch.arange(64).view(1, 64, 1)
+    k = torch.arange(64).view(1, 1, 64)
+    z = K.fa_dropout_mask_ref(1234, 7, bh, q, k, 0.25)
+    keep = (z > 0).float().mean().item()
+    assert abs(keep - 0.75) < 0.02
+    np.testing.assert_allclose(z[z > 0].unique().numpy(), [1 / 0.75], rtol=1e-6)
+    z2 = K.fa_dropout_mask_ref(1234, 8, bh, q, k, 0.25)
+    assert (z != z2).float().mean() > 0.2  # a new offset draws new bits
+
+
+def test_varlen_ref_matches_dense_per_sequence_cpu():
+    torch.manual_seed(0)
+    lens = [5, 9, 3]
+    H, D = 2, 16
+    cu = torch.tensor([0] + list(np.cumsum(lens)), dtype=torch.int32)
+    q, k, v = (torch.randn(sum(lens), H, D) for _ in range(3))
+    o = K.flash_attn_varlen(q, k, v, cu, cu, max(lens), max(lens), causal=True)
+    for b, L in enumerate(lens):
+        a, e = int(cu[b]), int(cu[b + 1])
+        ref, _ = K._fa_ext_ref_dense(q[a:e][None], k[a:e][None], v[a:e][None], True, 1 / math.sqrt(D))
+        np.testing.assert_allclose(o[a:e].numpy(), ref[0].numpy(), rtol=1e-5, atol=1e-6)
+
+
+def test_sdpa_mask_and_dropout_api_cpu():
+    import paddle_ray_amd.nn.functional as F
+    q = paddle.randn([2, 8, 2, 16])
+    m = paddle.zeros([2, 1, 1, 8])
+    m[:, :, :, 6:] = float('-inf')
+    o = F.scaled_dot_product_attention(q, q, q, attn_mask=m, training=False)
+    ref, _ = K._fa_ext_ref_dense(q._t, q._t, q._t, False, 1 / 4.0, m._t)
+    np.testing.assert_allclose(o.numpy(), ref.numpy(), rtol=1e-5, atol=1e-6)
+    out, _ = F.flash_attention(q, q, q, dropout=0.5, causal=True)
+    assert out.shape == [2, 8, 2, 16]
+
+
+def _fp32_grads(fn, tensors, g):
+    ts = [t.detach().float().requires_grad_(True) for t in tensors]
+    out = fn(*ts)
+    out.backward(g.float())
+    return out.detach(), [t.grad for t in ts]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('causal', [False, True])
+@pytest.mark.parametrize('D', [64, 128])
+def test_flash_dropout_matches_reference_with_same_mask(causal, D):
+    torch.manual_seed(1)
+    dev = torch.device('cuda')
+    B, S, H = 2, 320, 3
+    p = 0.2
+    q, k, v = (torch.randn(B, S, H, D, device=dev, dtype=torch.bfloat16, requires_grad=True)
+               for _ in range(3))
+    seed, off = 4321, 17
+    sc = 1 / math.sqrt(D)
+    o = K.FlashAttnExtFn.apply(q, k, v, None, None, None, S, S, causal, sc, p, seed, off)
+    g = torch.randn_like(o)
+    o.backward(g)
+    ro, rg = _fp32_grads(lambda a, b, c: K._fa_ext_ref_dense(a, b, c, causal, sc, None, p, seed, off)[0],
+                         (q, k, v), g)
+    err = (o.float() - ro).abs().max().item() / ro.abs().max().item()
+    assert err < 2e-2, err
+    for got, ref, n in zip((q.grad, k.grad, v.grad), rg, 'qkv'):
+        e = (got.float() - ref).abs().max().item() / ref.abs().max().item()
+        assert e < 3e-2, (n, e)
+
+
+@pytest.mark.gpu
+def test_flash_additive_mask_fwd_bwd():
+    torch.manual_seed(2)
+    dev = torch.device('cuda')
+    B, S, H, D = 2, 200, 2, 64
+    q, k, v = (torch.randn(B, S, H, D, device=dev, dtype=torch.bfloat16, requires_grad=True)
+               for _ in range(3))
+    # padding mask [B, 1, 1, S] (-inf past each batch's length) + a random bias [1, H, S, S]
+    m = torch.zeros(B, 1, 1, S, device=dev)
+    m[0, ..., 150:] = float('-inf')
+    bias = (torch.randn(1, H, S, S, device=dev) * 0.5)
+    mask = (m + bias).to(torch.bfloat16)
+    o = K.flash_attention_ext(q, k, v, attn_mask=mask)
+    g = torch.randn_like(o)
+    o.backward(g)
+    sc = 1 / math.sqrt(D)
+    ro, rg = _fp32_grads(lambda a, b, c: K._fa_ext_ref_dense(a, b, c, False, sc, mask.float())[0], (q, k, v), g)
+    assert (o.float() - ro).abs().max().item() / ro.abs().max().item() < 2e-2
+    for got, ref in zip((q.grad, k.grad, v.grad), rg):
+        assert (got.float() - ref).abs().max().item() / ref.abs().max().item() < 3e-2
+    # fp32 mask path and bool mask path
+    o32 = K.flash_attention_ext(q.detach(), k.detach(), v.detach(), attn_mask=(m + bias).float())
+    assert (o32.float() - ro).abs().max().item() / ro.abs().max().item() < 2e-2
+    keep = torch.ones(B, 1, S, S, dtype=torch.bool, device=dev).tril()
+    ob = K.flash_attention_ext(q.detach(), k.detach(), v.detach(), attn_mask=keep)
+    oc = K.flash_attention(q.detach(), k.detach(), v.detach(), causal=True)
+    assert (ob.float() - oc.float()).abs().max().item() < 2e-2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('causal', [False, True])
+def test_flash_varlen_matches_per_sequence_dense(causal):
+    torch.manual_seed(3)
+    dev = torch.device('cuda')
+    lens = [37, 300, 1, 129, 256]
+    H, D = 4, 128
+    cu = torch.tensor([0] + list(np.cumsum(lens)), dtype=torch.int32, device=dev)
+    tot = sum(lens)
+    q, k, v = (torch.randn(tot, H, D, device=dev, dtype=torch.bfloat16, requires_grad=True) for _ in range(3))
+    o = K.flash_attn_varlen(q, k, v, cu, cu, max(lens), max(lens), causal=causal)
+    g = torch.randn_like(o)
+    o.backward(g)
+    sc = 1 / math.sqrt(D)
+    for b, L in enumerate(lens):
+        a, e = int(cu[b]), int(cu[b + 1])
+        qs, ks, vs = (t.detach()[a:e][None] for t in (q, k, v))
+        ro, rg = _fp32_grads(lambda x, y, z: K._fa_ext_ref_dense(x, y, z, causal, sc)[0], (qs, ks, vs), g[a:e][None])
+        assert (o[a:e].float() - ro[0]).abs().max().item() < 3e-2 * max(1.0, ro.abs().max().item())
+        for got, ref in zip((q.grad[a:e], k.grad[a:e], v.grad[a:e]), rg):
+            assert (got.float() - ref[0]).abs().max().item() < 4e-2 * max(1.0, ref.abs().max().item())
+    # the paddle API + dropout through varlen
+    import paddle_ray_amd.nn.functional as F
+    out, _ = F.flash_attn_unpadded(paddle.Tensor(q.detach()), paddle.Tensor(k.detach()),
+                                   paddle.Tensor(v.detach()), paddle.Tensor(cu), paddle.Tensor(cu),
+                                   max(lens), max(lens), sc, dropout=0.1, causal=causal)
+    assert out.shape == [tot, H, D] and torch.isfinite(out._t.float()).all()
+
+
+@pytest.mark.gpu
+def test_gpt_attention_dropout_uses_flash_kernel():
+    from paddle_ray_amd.models import gpt_config, GPTForPretraining
+    from paddle_ray_amd.ops import registry as R
+    paddle.set_device('gpu')
+    paddle.set_default_dtype('bfloat16')
+    m = GPTForPretraining(gpt_config('gpt3-tiny', attention_dropout=0.1))
+    paddle.set_default_dtype('float32')
+    ids = paddle.randint(0, 1000, [2, 65])
+    R.reset_stats()
+    loss = m(ids[:, :-1], ids[:, 1:])
+    loss.backward()
+    st = R.stats()
+    assert st.get(('flash_attn_ext', 'hip'), 0) > 0, st
+    assert np.isfinite(float(loss))
