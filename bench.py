@@ -324,7 +324,9 @@ def bench_ernie(a, paddle, torch, dist, C, world, rank, dev):
 
 def bench_bert(a, paddle, torch, dist, C, world, rank, dev):
     """BASELINE config 3: BERT-base pretraining through the STATIC-graph Executor with AMP
-    (static.amp.decorate, bf16): per-op grad ops, fwd+bwd replayed as one HIP graph, AdamW."""
+    (static.amp.decorate, bf16): per-op grad ops, fwd+bwd replayed as one HIP graph, AdamW.
+    MLM as in the reference's BERT pretraining data (max_predictions_per_seq = 80 at seq 512,
+    20 at 128): the prediction head and its softmax-CE run on the masked positions only."""
     import numpy as np
     from paddle_ray_amd import static
     from paddle_ray_amd.models import bert_config, BertForPretraining
@@ -336,11 +338,13 @@ def bench_bert(a, paddle, torch, dist, C, world, rank, dev):
     model = BertForPretraining(cfg)
     paddle.enable_static()
     main_p, startup = static.Program(), static.Program()
+    P = max(1, int(round(S * 0.15625)))  # masked positions per sequence (80 at 512)
     with static.program_guard(main_p, startup):
         ids_v = static.data('ids', [bs, S], 'int64')
-        lab_v = static.data('lab', [bs, S], 'int64')
+        pos_v = static.data('pos', [bs * P], 'int64')
+        lab_v = static.data('lab', [bs * P], 'int64')
         nsp_v = static.data('nsp', [bs], 'int64')
-        loss_v = model(ids_v, labels=lab_v, next_sentence_label=nsp_v)
+        loss_v = model(ids_v, masked_positions=pos_v, labels=lab_v, next_sentence_label=nsp_v)
         opt = static.amp.decorate(paddle.optimizer.AdamW(1e-4, parameters=model.parameters()),
                                   use_bf16=True)
         opt.minimize(loss_v)
@@ -352,11 +356,11 @@ def bench_bert(a, paddle, torch, dist, C, world, rank, dev):
         prog._build_strategy.use_hip_graph = True
     rs = np.random.RandomState(rank)
     ids = rs.randint(5, cfg.vocab_size, (bs, S))
-    lab = np.full((bs, S), -1)
-    pos = rs.rand(bs, S) < 0.15
-    lab[pos] = ids[pos]
-    ids[pos] = 103
+    pos = np.stack([np.sort(rs.choice(S, P, replace=False)) + i * S for i in range(bs)]).reshape(-1)
+    lab = ids.reshape(-1)[pos].copy()
+    ids.reshape(-1)[pos] = 103  # [MASK]
     feed = {'ids': torch.from_numpy(ids.astype('int64')).to(dev),
+            'pos': torch.from_numpy(pos.astype('int64')).to(dev),
             'lab': torch.from_numpy(lab.astype('int64')).to(dev),
             'nsp': torch.from_numpy(rs.randint(0, 2, (bs,)).astype('int64')).to(dev)}
     feed = {k: paddle.Tensor(v) for k, v in feed.items()}
@@ -373,7 +377,8 @@ def bench_bert(a, paddle, torch, dist, C, world, rank, dev):
             "ms_per_step": round(dt / a.steps * 1000, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
             "config": {"model": name, "global_batch": bs * world, "seq_len": S,
-                       "parallelism": f"dp{world}", "executor": "static Program, HIP graph"},
+                       "parallelism": f"dp{world}", "executor": "static Program, HIP graph",
+                       "masked_positions_per_seq": P},
             "tokens_per_sec": round(sps * S, 1), "final_loss": float(last[0])}
 
 

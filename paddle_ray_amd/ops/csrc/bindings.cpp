@@ -60,7 +60,7 @@ int pra_flash_bwd(const void*, const void*, const void*, const void*, const void
                   void*, void*, int, int, int, int, int, const int64_t*, float, int, int, hipStream_t);
 int pra_embedding_fwd(const int64_t*, const void*, void*, int64_t, int, int64_t, int64_t, int, hipStream_t);
 int pra_embedding_bwd(const int64_t*, const int64_t*, const void*, void*, int64_t, int, int64_t, int64_t, int, int,
-                      int, hipStream_t);
+                      int, float*, hipStream_t);
 void pra_bias_gelu_bwd_db(const void*, const void*, const void*, void*, float*, int, int, int, int, int,
                           hipStream_t);
 void pra_colsum_rows(const void*, float*, int, int, int, int, hipStream_t);
@@ -323,8 +323,8 @@ PYBIND11_MODULE(_pra_hip, m) {
     check_launch("embedding_fwd");
   });
   m.def("embedding_bwd", [](P sids, P perm, P dy, P dw, int64_t n, int D, int64_t V, int64_t pad, int dtg, int dtw,
-                            int acc, P s) {
-    if (pra_embedding_bwd(I64(sids), I64(perm), CV(dy), V(dw), n, D, V, pad, dtg, dtw, acc, S(s)) != 0)
+                            int acc, P ws, P s) {
+    if (pra_embedding_bwd(I64(sids), I64(perm), CV(dy), V(dw), n, D, V, pad, dtg, dtw, acc, F(ws), S(s)) != 0)
       throw std::invalid_argument("embedding_bwd: unsupported D/dtype");
     check_launch("embedding_bwd");
   });

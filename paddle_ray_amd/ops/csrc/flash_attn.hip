@@ -110,7 +110,7 @@ struct FaExt {
   int64_t msb, msh, msq;
   int mask_f32;
   float mask_mul;  // 1 / scale: the kernels add mask/scale to the raw q·k scores
-  uint32_t thr;    // dropout threshold on 24-bit uniforms (0 = no dropout)
+  uint32_t thr;    // dropout threshold on 32-bit uniforms (0 = no dropout)
   float inv_keep;
   uint64_t seed, offset;
 };
@@ -119,13 +119,17 @@ __device__ __forceinline__ uint32_t fa_mix32(uint32_t x) {
   x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
   return x;
 }
-// dropout multiplier of element (query q, key kk) of head row bh: 0 or 1/(1-p)
-__device__ __forceinline__ float fa_drop(const FaExt& e, int bh, int q, int kk) {
-  const uint64_t c = ((uint64_t)(uint32_t)bh << 40) ^ ((uint64_t)(uint32_t)q << 20) ^ (uint64_t)(uint32_t)kk;
-  const uint32_t a = fa_mix32((uint32_t)c ^ (uint32_t)e.seed ^ ((uint32_t)e.offset * 0x85ebca6bU));
-  const uint32_t r = fa_mix32(a ^ (uint32_t)(c >> 32) ^ (uint32_t)(e.seed >> 32) ^ (uint32_t)(e.offset >> 32) ^
-                              0x9e3779b9U);
-  return (r >> 8) >= e.thr ? e.inv_keep : 0.f;
+// dropout multiplier of element (query q, key kk) of head row bh: 0 or 1/(1-p). One lowbias32
+// round over a multiply-xor fold of (seed, offset, bh, q, kk): ~8 VALU per element (the two-round
+// counter hash cost more than the attention math at head_dim 64); fwd and bwd call the same
+// function, so the backward regenerates the forward's bits exactly.
+__device__ __forceinline__ uint32_t fa_key(const FaExt& e, int bh) {
+  return fa_mix32((uint32_t)e.seed ^ (uint32_t)(e.seed >> 32) * 0x27d4eb2fU ^
+                  (uint32_t)e.offset * 0x165667b1U ^ (uint32_t)bh * 0xc2b2ae3dU);
+}
+__device__ __forceinline__ float fa_drop(const FaExt& e, uint32_t key, int q, int kk) {
+  const uint32_t r = fa_mix32(key ^ (uint32_t)q * 0x9e3779b1U ^ (uint32_t)kk * 0x85ebca77U);
+  return r >= e.thr ? e.inv_keep : 0.f;
 }
 // additive mask value (already divided by the softmax scale) of (b, h, query q, key kk)
 template <typename T>
@@ -307,6 +311,7 @@ fwd_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restrict
     }
   }
   const int off = Sk - Sq;
+  const uint32_t dkey = EXT ? fa_key(ext, bh) : 0u;  // per-(head row) dropout hash key
 
   const T* qb_ = EXT && ext.cu_q ? q + qrow0 * qss + hh * qsh : q + b * qsb + hh * qsh;
   const T* kb_ = EXT && ext.cu_q ? k + krow0 * kss + hh * ksh : k + b * ksb + hh * ksh;
@@ -442,7 +447,7 @@ fwd_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restrict
         float p = fexp2(fmaf(s_acc[mt][i], scale_log2, -m_use));
         ps += p;  // the softmax denominator sums the undropped probabilities
         if constexpr (EXT)
-          if (ext.thr) p *= fa_drop(ext, bh, myq, k0 + 32 * mt + acc_row(i, h));
+          if (ext.thr) p *= fa_drop(ext, dkey, myq, k0 + 32 * mt + acc_row(i, h));
         s_acc[mt][i] = p;
       }
     ps += __shfl_xor(ps, 32, 64);
@@ -710,6 +715,7 @@ bwd_dkdv_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __res
   const int off = Sk - Sq;
   const bool kvalid = mykey < Sk;
   const bool vl = EXT && ext.cu_q;
+  const uint32_t dkey = EXT ? fa_key(ext, bh) : 0u;  // per-(head row) dropout hash key
 
   const T* qb_ = vl ? q + qrow0 * qss + hh * qsh : q + b * qsb + hh * qsh;
   const T* kb_ = vl ? k + krow0 * kss + hh * ksh : k + b * ksb + hh * ksh;
@@ -844,7 +850,7 @@ bwd_dkdv_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __res
             }
             if constexpr (EXT) {
               if (ext.thr) {
-                const float z = fa_drop(ext, bh, qq, mykey);  // same bits as the forward
+                const float z = fa_drop(ext, dkey, qq, mykey);  // same bits as the forward
                 sa[nt][i] = p * z;
                 da[nt][i] = p * (da[nt][i] * z - dl[c]);
                 continue;
@@ -1194,7 +1200,7 @@ int pra_flash_fwd_ext(const void* q, const void* k, const void* v, void* o, floa
   if (!(p_drop >= 0.f && p_drop < 1.f) || (!cu_q) != (!cu_k)) return -1;
   if (B * H == 0 || Sq == 0) return 0;
   fa::FaExt e{cu_q, cu_k, mask, msb, msh, msq, mask_f32, 1.f / scale,
-              (uint32_t)(p_drop * 16777216.f), p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f, seed, offset};
+              (uint32_t)((double)p_drop * 4294967296.0), p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f, seed, offset};
   PRA_FA_DISPATCH(launch_fwd_ext, q, k, v, o, lse, B, H, Sq, Sk, strides, scale, e, s);
   return 0;
 }
@@ -1209,7 +1215,7 @@ int pra_flash_bwd_ext(const void* q, const void* k, const void* v, const void* d
   if (!(p_drop >= 0.f && p_drop < 1.f) || (!cu_q) != (!cu_k)) return -1;
   if (B * H == 0 || Sq == 0) return 0;
   fa::FaExt e{cu_q, cu_k, mask, msb, msh, msq, mask_f32, 1.f / scale,
-              (uint32_t)(p_drop * 16777216.f), p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f, seed, offset};
+              (uint32_t)((double)p_drop * 4294967296.0), p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f, seed, offset};
   PRA_FA_DISPATCH(launch_bwd_ext, q, k, v, dO, lse, delta, dq, dk, dv, dsT, B, H, Sq, Sk, strides, scale, e, s);
   return 0;
 }

@@ -958,15 +958,15 @@ def _mix32_t(x):
 
 def fa_dropout_mask_ref(seed, offset, bh, q, kk, p_drop):
     """The keep multiplier (0 or 1/(1-p)) the flash kernels use for (head row bh, query q, key
-    kk) — a torch port of flash_attn.hip fa_drop for references and tests. bh/q/kk: int64
-    tensors (broadcastable)."""
-    thr = int(float(np.float32(p_drop)) * 16777216.0)
+    kk) — a torch port of flash_attn.hip fa_key / fa_drop for references and tests. bh/q/kk:
+    int64 tensors (broadcastable)."""
+    thr = int(float(np.float32(p_drop)) * 4294967296.0)  # the kernel receives a float32 p
     inv_keep = float(np.float32(1.0) / (np.float32(1.0) - np.float32(p_drop)))
-    c = (bh << 40) ^ (q << 20) ^ kk
-    k0 = (seed & _M32) ^ (((offset & _M32) * 0x85ebca6b) & _M32)
-    a = _mix32_t((c & _M32) ^ k0)
-    r = _mix32_t(a ^ ((c >> 32) & _M32) ^ ((seed >> 32) & _M32) ^ ((offset >> 32) & _M32) ^ 0x9e3779b9)
-    return torch.where((r >> 8) >= thr, inv_keep, 0.0)
+    s0 = (seed & _M32) ^ ((((seed >> 32) & _M32) * 0x27d4eb2f) & _M32) ^ \
+        (((offset & _M32) * 0x165667b1) & _M32)
+    key = _mix32_t(((bh & _M32) * 0xc2b2ae3d & _M32) ^ s0)
+    r = _mix32_t(key ^ (((q & _M32) * 0x9e3779b1) & _M32) ^ (((kk & _M32) * 0x85ebca77) & _M32))
+    return torch.where(r >= thr, inv_keep, 0.0)
 
 
 def _fa_ext_ref_dense(q, k, v, causal, scale, mask=None, p_drop=0.0, seed=0, offset=0, bh0=None):
@@ -2129,9 +2129,11 @@ def _emb_bwd_hip(ids, dy, w_shape, w_dtype, pad, into=None):
     sids, perm = torch.sort(flat, stable=True)
     dy2 = dy.reshape(-1, D).contiguous()
     out = into if into is not None else torch.zeros(w_shape, dtype=w_dtype, device=dy.device)
+    # segmented two-pass form: repeated ids (positions, token types) spread over many waves
+    ws = torch.empty(2 * (-(-flat.numel() // 32)) * D, dtype=torch.float32, device=dy.device)
     _native.lib().embedding_bwd(_ptr(sids), _ptr(perm), _ptr(dy2), _ptr(out), flat.numel(), D, V,
                                 -1 if pad is None else int(pad), _dt(dy2), _DT[out.dtype],
-                                1, _stream())
+                                1, _ptr(ws), _stream())
     return out
 
 

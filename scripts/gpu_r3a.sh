@@ -11,4 +11,7 @@ step newtests 400 python -u -m pytest tests/test_flash_ext.py tests/test_jit.py 
 step w4 300 python scripts/gemm_lds_bench.py --w4
 step fused8 120 python scripts/gemm_lds_bench.py --fused
 step fused4 120 python scripts/gemm_lds_bench.py --fused --w4
+step bert 300 python bench.py --model bert-base --steps 20 --warmup 5
+step bertprof 300 rocprofv3 --kernel-trace --stats -d $OUT/bprof -o bert --output-format csv -- python3 bench.py --model bert-base --steps 5 --warmup 2
+step gpt 300 python bench.py --steps 20 --warmup 5
 exit 0

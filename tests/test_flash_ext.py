@@ -145,7 +145,7 @@ def test_gpt_attention_dropout_uses_flash_kernel():
     from paddle_ray_amd.ops import registry as R
     paddle.set_device('gpu')
     paddle.set_default_dtype('bfloat16')
-    m = GPTForPretraining(gpt_config('gpt3-tiny', attention_dropout=0.1))
+    m = GPTForPretraining(gpt_config('gpt3-tiny', num_heads=2, attention_dropout=0.1))  # head_dim 64
     paddle.set_default_dtype('float32')
     ids = paddle.randint(0, 1000, [2, 65])
     R.reset_stats()

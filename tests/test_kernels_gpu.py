@@ -402,6 +402,27 @@ def test_embedding_fwd_bwd(dt, D):
     assert torch.allclose(w.grad.float(), g0.float() + gref, atol=2 * tol, rtol=tol)
 
 
+@pytest.mark.parametrize('dt', [torch.float32, torch.bfloat16])
+def test_embedding_bwd_long_runs_segmented(dt):
+    """Runs much longer than a 32-row segment (token types, positions: one id over the whole
+    batch) are split over many waves and recombined; runs crossing block boundaries, runs that
+    start mid-block and the padding id all meet the index_add reference."""
+    torch.manual_seed(1)
+    V, D = 40, 768
+    ids = torch.cat([torch.zeros(5000, dtype=torch.long), torch.full((33,), 3), torch.full((1,), 4),
+                     torch.randint(0, V, (700,)), torch.full((64,), 9), torch.full((95,), 5)]).to(DEV)
+    ids = ids[torch.randperm(ids.numel(), device=DEV)].view(-1, 7)
+    w = torch.randn(V, D, device=DEV, dtype=dt, requires_grad=True)
+    out = F.embedding(ids, w, 5)
+    dy = torch.randn_like(out)
+    out.backward(dy)
+    keep = (ids != 5).unsqueeze(-1)
+    gref = torch.zeros(V, D, device=DEV)
+    gref.index_add_(0, ids.reshape(-1), (dy.float() * keep).reshape(-1, D))
+    tol = _tol(dt) * 10
+    assert torch.allclose(w.grad.float(), gref, atol=tol * 8, rtol=tol)
+
+
 def test_embedding_out_of_range_reads_zero():
     w = torch.randn(10, 16, device=DEV)
     ids = torch.tensor([[0, 9, 10, -1, 1000]], device=DEV)
