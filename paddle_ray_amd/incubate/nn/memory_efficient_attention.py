@@ -46,7 +46,7 @@ def memory_efficient_attention(query, key, value, attn_bias=None, p=0.0, scale=N
         return Tensor(_dense(q, k, v, bias, p, scale, training))
     if isinstance(attn_bias, AB.BlockDiagonalMask) and flash and q.shape[0] == 1:
         # the packed blocks are independent sequences: ONE varlen flash launch over all of them
-        qi, ki = attn_bias.q_seqinfo.intervals(), attn_bias.k_seqinfo.intervals()
+        qi, ki = list(attn_bias.q_seqinfo.intervals()), list(attn_bias.k_seqinfo.intervals())
         cu_q = torch.tensor([0] + [b for _, b in qi], dtype=torch.int32, device=q.device)
         cu_k = torch.tensor([0] + [b for _, b in ki], dtype=torch.int32, device=q.device)
         mq = max(b - a for a, b in qi)

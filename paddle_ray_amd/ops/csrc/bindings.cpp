@@ -52,10 +52,10 @@ int pra_flash_fwd(const void*, const void*, const void*, void*, float*, int, int
                   int, int, hipStream_t);
 int pra_flash_fwd_ext(const void*, const void*, const void*, void*, float*, int, int, int, int, int, const int64_t*,
                       float, int, int, const int*, const int*, const void*, int64_t, int64_t, int64_t, int, float,
-                      uint64_t, uint64_t, hipStream_t);
+                      uint64_t, uint64_t, uint32_t*, hipStream_t);
 int pra_flash_bwd_ext(const void*, const void*, const void*, const void*, const float*, const float*, void*, void*,
                       void*, void*, int, int, int, int, int, const int64_t*, float, int, int, const int*, const int*,
-                      const void*, int64_t, int64_t, int64_t, int, float, uint64_t, uint64_t, hipStream_t);
+                      const void*, int64_t, int64_t, int64_t, int, float, uint64_t, uint64_t, uint32_t*, hipStream_t);
 int pra_flash_bwd(const void*, const void*, const void*, const void*, const void*, const float*, float*, void*, void*,
                   void*, void*, int, int, int, int, int, const int64_t*, float, int, int, hipStream_t);
 int pra_embedding_fwd(const int64_t*, const void*, void*, int64_t, int, int64_t, int64_t, int, hipStream_t);
@@ -257,23 +257,23 @@ PYBIND11_MODULE(_pra_hip, m) {
   });
   m.def("flash_fwd_ext", [](P q, P k, P v, P o, P lse, int B, int H, int Sq, int Sk, int D, std::vector<int64_t> st,
                             float scale, int causal, int dt, P cu_q, P cu_k, P mask, int64_t msb, int64_t msh,
-                            int64_t msq, int mask_f32, float p_drop, uint64_t seed, uint64_t offset, P s) {
+                            int64_t msq, int mask_f32, float p_drop, uint64_t seed, uint64_t offset, P dbits, P s) {
     if (st.size() != 9) throw std::invalid_argument("flash_fwd_ext: need 9 strides");
     if (pra_flash_fwd_ext(CV(q), CV(k), CV(v), V(o), F(lse), B, H, Sq, Sk, D, st.data(), scale, causal, dt,
                           reinterpret_cast<const int*>(cu_q), reinterpret_cast<const int*>(cu_k), CV(mask), msb, msh,
-                          msq, mask_f32, p_drop, seed, offset, S(s)) != 0)
+                          msq, mask_f32, p_drop, seed, offset, reinterpret_cast<uint32_t*>(dbits), S(s)) != 0)
       throw std::invalid_argument("flash_fwd_ext: unsupported arguments");
     check_launch("flash_fwd_ext");
   });
   m.def("flash_bwd_ext", [](P q, P k, P v, P dO, P lse, P delta, P dq, P dk, P dv, P dsT, int B, int H, int Sq, int Sk,
                             int D, std::vector<int64_t> st, float scale, int causal, int dt, P cu_q, P cu_k, P mask,
                             int64_t msb, int64_t msh, int64_t msq, int mask_f32, float p_drop, uint64_t seed,
-                            uint64_t offset, P s) {
+                            uint64_t offset, P dbits, P s) {
     if (st.size() != 18) throw std::invalid_argument("flash_bwd_ext: need 18 strides");
     if (pra_flash_bwd_ext(CV(q), CV(k), CV(v), CV(dO), CF(lse), CF(delta), V(dq), V(dk), V(dv), V(dsT), B, H, Sq, Sk,
                           D, st.data(), scale, causal, dt, reinterpret_cast<const int*>(cu_q),
                           reinterpret_cast<const int*>(cu_k), CV(mask), msb, msh, msq, mask_f32, p_drop, seed,
-                          offset, S(s)) != 0)
+                          offset, reinterpret_cast<uint32_t*>(dbits), S(s)) != 0)
       throw std::invalid_argument("flash_bwd_ext: unsupported arguments");
     check_launch("flash_bwd_ext");
   });

@@ -113,6 +113,10 @@ struct FaExt {
   uint32_t thr;    // dropout threshold on 32-bit uniforms (0 = no dropout)
   float inv_keep;
   uint64_t seed, offset;
+  // dropout keep bits the forward stores for the backward: [B*H][SqMax][dbits_ld] words, bit
+  // (key & 31) of word (query, key >> 5); the dK/dV kernel reads them instead of re-hashing
+  uint32_t* dbits;
+  int dbits_ld;
 };
 
 __device__ __forceinline__ uint32_t fa_mix32(uint32_t x) {
@@ -440,16 +444,32 @@ fwd_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restrict
     }
     m_run = m_new;
     float ps = 0.f;
+    uint32_t kbits[2] = {0u, 0u};  // this lane's keep bits of the two 32-key halves
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         float p = fexp2(fmaf(s_acc[mt][i], scale_log2, -m_use));
         ps += p;  // the softmax denominator sums the undropped probabilities
-        if constexpr (EXT)
-          if (ext.thr) p *= fa_drop(ext, dkey, myq, k0 + 32 * mt + acc_row(i, h));
+        if constexpr (EXT) {
+          if (ext.thr) {
+            const float z = fa_drop(ext, dkey, myq, k0 + 32 * mt + acc_row(i, h));
+            kbits[mt] |= (z != 0.f ? 1u : 0u) << acc_row(i, h);
+            p *= z;
+          }
+        }
         s_acc[mt][i] = p;
       }
+    if constexpr (EXT) {
+      if (ext.thr && ext.dbits) {  // both lane halves' 16 bits -> one word per (query, 32 keys)
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) {
+          const uint32_t w = kbits[mt] | __shfl_xor(kbits[mt], 32, 64);
+          if (h == 0 && myq < Sq && mt < nlive)
+            ext.dbits[((int64_t)bh * SqM + myq) * ext.dbits_ld + (k0 >> 5) + mt] = w;
+        }
+      }
+    }
     ps += __shfl_xor(ps, 32, 64);
     l_run += ps;
     // O^T += V^T P^T (k-steps of a dead half contribute nothing)
@@ -748,6 +768,11 @@ bwd_dkdv_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __res
   qd.init(qb_, qss, Sq, wave, lane);
   dd.init(dob_, HD, Sq, wave, lane);
   float lreg = 0.f, dreg = 0.f;
+  uint32_t mreg = 0u;
+  // EXT + dropout: the forward's keep-bit words of the tile's 64 queries x this block's 4 key
+  // words ([2][4 waves][64] after the dS^T stage), loaded with lse / delta
+  const bool dbits = EXT && ext.thr && ext.dbits;
+  uint32_t* Mb = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(Dlb + 2 * kTile) + 4 * 32 * 80);
   auto load_tile = [&](int qs0) {
     const uint32_t img = lds0 + (uint32_t)((2 * (((qs0 - q_begin) / kTile) & 1)) * kTile * D * sizeof(T));
     qd.issue(img, (uint32_t)((int64_t)qs0 * qss * 2), wave);
@@ -757,12 +782,17 @@ bwd_dkdv_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __res
       lreg = qq < Sq ? lse[(int64_t)bh * SqM + qq] : INFINITY;  // scaled at store (no wait here)
       dreg = qq < Sq ? delta[(int64_t)bh * SqM + qq] : 0.f;
     }
+    if (dbits) {
+      const int qq = qs0 + (threadIdx.x & 63), kw = (kblk0 >> 5) + (threadIdx.x >> 6);
+      mreg = qq < Sq && kw < ext.dbits_ld ? ext.dbits[((int64_t)bh * SqM + qq) * ext.dbits_ld + kw] : 0u;
+    }
   };
   auto store_tile = [&](int buf) {
     if (threadIdx.x < kTile) {
       Lsb[buf * kTile + threadIdx.x] = lreg * LOG2E;
       Dlb[buf * kTile + threadIdx.x] = dreg;
     }
+    if (dbits) Mb[buf * 256 + threadIdx.x] = mreg;
   };
   if (ntiles > 0) { load_tile(q_begin); store_tile(0); }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -837,6 +867,10 @@ bwd_dkdv_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __res
           const float4 l4 = *reinterpret_cast<const float4*>(Ls + 32 * nt + 8 * g + 4 * h);
           const float4 d4 = *reinterpret_cast<const float4*>(Dl + 32 * nt + 8 * g + 4 * h);
           const float la[4] = {l4.x, l4.y, l4.z, l4.w}, dl[4] = {d4.x, d4.y, d4.z, d4.w};
+          uint4 mw = make_uint4(0u, 0u, 0u, 0u);
+          if constexpr (EXT)
+            if (dbits) mw = *reinterpret_cast<const uint4*>(Mb + buf * 256 + wave * 64 + 32 * nt + 8 * g + 4 * h);
+          const uint32_t mwa[4] = {mw.x, mw.y, mw.z, mw.w};
 #pragma unroll
           for (int c = 0; c < 4; ++c) {
             const int i = 4 * g + c;
@@ -850,7 +884,9 @@ bwd_dkdv_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __res
             }
             if constexpr (EXT) {
               if (ext.thr) {
-                const float z = fa_drop(ext, dkey, qq, mykey);  // same bits as the forward
+                // the forward's keep bit (stored) or the same hash (no bit store)
+                const float z = dbits ? ((mwa[c] >> (mykey & 31)) & 1u ? ext.inv_keep : 0.f)
+                                      : fa_drop(ext, dkey, qq, mykey);
                 sa[nt][i] = p * z;
                 da[nt][i] = p * (da[nt][i] * z - dl[c]);
                 continue;
@@ -1144,7 +1180,7 @@ static void launch_bwd_ext(const void* q, const void* k, const void* v, const vo
   const int Sqp = (Sq + 255) / 256 * 256;
   const int64_t dsbh = (int64_t)((Sk + 127) / 128 * 128) * Sqp;
   {
-    const size_t lds = 4 * kTile * D * sizeof(T) + 4 * kTile * sizeof(float) + 4 * 32 * 80;
+    const size_t lds = 4 * kTile * D * sizeof(T) + 4 * kTile * sizeof(float) + 4 * 32 * 80 + 2 * 256 * 4;
     auto kern = bwd_dkdv_kernel<T, D, C, true, true>;
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(kern, dim3(B * H, (Sk + 127) / 128), dim3(256), lds, s, (const T*)q, (const T*)k,
@@ -1191,16 +1227,18 @@ int pra_flash_fwd(const void* q, const void* k, const void* v, void* o, float* l
 // elements; dQ = dS K is formed from it instead of recomputing S and dP in a dQ sweep.
 // Extended forward: varlen (cu_q / cu_k [B+1] row prefix sums of packed [total, H, D] q/k/v/o;
 // Sq, Sk = the longest sequences; lse [B, H, Sq]), additive mask (element strides msb / msh /
-// msq, keys contiguous; mask_f32: fp32 else q's dtype), dropout p_drop with (seed, offset).
+// msq, keys contiguous; mask_f32: fp32 else q's dtype), dropout p_drop with (seed, offset);
+// dbits (optional, B*H*Sq*ceil(Sk/32) words) receives the keep bits for the backward.
 int pra_flash_fwd_ext(const void* q, const void* k, const void* v, void* o, float* lse, int B, int H, int Sq, int Sk,
                       int D, const int64_t* strides, float scale, int causal, int dt, const int* cu_q,
                       const int* cu_k, const void* mask, int64_t msb, int64_t msh, int64_t msq, int mask_f32,
-                      float p_drop, uint64_t seed, uint64_t offset, hipStream_t s) {
+                      float p_drop, uint64_t seed, uint64_t offset, uint32_t* dbits, hipStream_t s) {
   if (!(D == 64 || D == 128) || !(dt == kBF16 || dt == kF16)) return -1;
   if (!(p_drop >= 0.f && p_drop < 1.f) || (!cu_q) != (!cu_k)) return -1;
   if (B * H == 0 || Sq == 0) return 0;
   fa::FaExt e{cu_q, cu_k, mask, msb, msh, msq, mask_f32, 1.f / scale,
-              (uint32_t)((double)p_drop * 4294967296.0), p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f, seed, offset};
+              (uint32_t)((double)p_drop * 4294967296.0), p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f, seed, offset,
+              dbits, (Sk + 31) / 32};
   PRA_FA_DISPATCH(launch_fwd_ext, q, k, v, o, lse, B, H, Sq, Sk, strides, scale, e, s);
   return 0;
 }
@@ -1210,12 +1248,13 @@ int pra_flash_bwd_ext(const void* q, const void* k, const void* v, const void* d
                       const float* delta, void* dq, void* dk, void* dv, void* dsT, int B, int H, int Sq, int Sk, int D,
                       const int64_t* strides, float scale, int causal, int dt, const int* cu_q, const int* cu_k,
                       const void* mask, int64_t msb, int64_t msh, int64_t msq, int mask_f32, float p_drop,
-                      uint64_t seed, uint64_t offset, hipStream_t s) {
+                      uint64_t seed, uint64_t offset, uint32_t* dbits, hipStream_t s) {
   if (!(D == 64 || D == 128) || !(dt == kBF16 || dt == kF16) || !dsT) return -1;
   if (!(p_drop >= 0.f && p_drop < 1.f) || (!cu_q) != (!cu_k)) return -1;
   if (B * H == 0 || Sq == 0) return 0;
   fa::FaExt e{cu_q, cu_k, mask, msb, msh, msq, mask_f32, 1.f / scale,
-              (uint32_t)((double)p_drop * 4294967296.0), p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f, seed, offset};
+              (uint32_t)((double)p_drop * 4294967296.0), p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f, seed, offset,
+              dbits, (Sk + 31) / 32};
   PRA_FA_DISPATCH(launch_bwd_ext, q, k, v, dO, lse, delta, dq, dk, dv, dsT, B, H, Sq, Sk, strides, scale, e, s);
   return 0;
 }

@@ -1039,19 +1039,22 @@ class FlashAttnExtFn(torch.autograd.Function):
         lse = torch.empty((B, H, Sq), device=q.device, dtype=torch.float32)
         mk, msb, msh, msq, m32 = (None, 0, 0, 0, False) if mask is None else \
             _mask_strides(mask, B, H, Sq, Sk)
+        # dropout keep bits for the backward (1 bit per score: B*H*Sq*Sk/8 bytes)
+        dbits = torch.empty(B * H * Sq * (-(-Sk // 32)), device=q.device, dtype=torch.int32) \
+            if p_drop > 0 else torch.empty(0, device=q.device, dtype=torch.int32)
         L.flash_fwd_ext(_ptr(q), _ptr(k), _ptr(v), _ptr(o), _ptr(lse), B, H, Sq, Sk, D, st, float(scale),
                         int(causal), _dt(q), _ptr(cu_q) if varlen else 0, _ptr(cu_k) if varlen else 0,
                         _ptr(mk) if mk is not None else 0, msb, msh, msq, int(m32), float(p_drop),
-                        int(seed), int(offset), _stream())
+                        int(seed), int(offset), _ptr(dbits) if p_drop > 0 else 0, _stream())
         ctx.save_for_backward(q, k, v, o, lse, mk if mk is not None else torch.empty(0), cu_q if varlen else
-                              torch.empty(0), cu_k if varlen else torch.empty(0))
+                              torch.empty(0), cu_k if varlen else torch.empty(0), dbits)
         ctx.meta = (varlen, B, H, D, Sq, Sk, st, causal, scale, p_drop, seed, offset,
                     (msb, msh, msq, m32) if mk is not None else None)
         return o
 
     @staticmethod
     def backward(ctx, do):
-        q, k, v, o, lse, mk, cu_q, cu_k = ctx.saved_tensors
+        q, k, v, o, lse, mk, cu_q, cu_k, dbits = ctx.saved_tensors
         varlen, B, H, D, Sq, Sk, st, causal, scale, p_drop, seed, offset, mmeta = ctx.meta
         L = _native.lib()
         do = _like(do, q.dtype).contiguous()
@@ -1081,7 +1084,7 @@ class FlashAttnExtFn(torch.autograd.Function):
                         _ptr(dv), _ptr(ds), B, H, Sq, Sk, D, gst, float(scale), int(causal), _dt(q),
                         _ptr(cu_q) if varlen else 0, _ptr(cu_k) if varlen else 0,
                         _ptr(mk) if mmeta is not None else 0, msb, msh, msq, int(m32), float(p_drop),
-                        int(seed), int(offset), _stream())
+                        int(seed), int(offset), _ptr(dbits) if dbits.numel() else 0, _stream())
         return dq, dk, dv, None, None, None, None, None, None, None, None, None, None
 
 
@@ -1594,13 +1597,24 @@ def bias_grad(dy2, b):
     return db
 
 
+def _no_autocast_change(x, w):
+    """True when autocast is off, or on with both operands already in its dtype (O2 / bf16
+    models: autocast would not cast anything, so the fused kernels may run)."""
+    dev = x.device.type
+    if not torch.is_autocast_enabled(dev):
+        return True
+    return x.dtype == w.dtype == torch.get_autocast_dtype(dev)
+
+
 def linear(x, w, b=None):
     """[.., in] @ [in, out] (+ b) with fused dW accumulation (see LinearFn)."""
+    if b is not None and b.dtype != x.dtype and torch.is_autocast_enabled(x.device.type):
+        b = b.to(x.dtype)
     if w.requires_grad and torch.is_grad_enabled() and w.is_leaf and x.dtype == w.dtype and \
-            not torch.is_autocast_enabled(x.device.type):
+            _no_autocast_change(x, w):
         return LinearFn.apply(x, w, b)
     x2 = x.reshape(-1, x.shape[-1])
-    if x2.is_cuda and x.dtype == w.dtype and not torch.is_autocast_enabled(x.device.type):
+    if x2.is_cuda and x.dtype == w.dtype and _no_autocast_change(x, w):
         y = gemm(GEMM_FWD, x2, w, bias=b)
     else:
         y = torch.addmm(b, x2, w) if b is not None else torch.mm(x2, w)
@@ -1637,7 +1651,7 @@ class LinearNTFn(torch.autograd.Function):
 def linear_nt(x2, w):
     """[T, in] @ [out, in]^T with fused dW accumulation (see LinearNTFn)."""
     if w.requires_grad and torch.is_grad_enabled() and w.is_leaf and x2.dtype == w.dtype and \
-            not torch.is_autocast_enabled(x2.device.type):
+            _no_autocast_change(x2, w):
         return LinearNTFn.apply(x2, w)
     if x2.is_cuda and x2.dtype == w.dtype:
         return gemm(GEMM_NT, x2, w)

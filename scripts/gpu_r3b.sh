@@ -1,0 +1,14 @@
+#!/bin/bash
+# Full GPU suite on the current tree, then the three benches and the BERT profile.
+OUT=gpurun_out/${1:-r3b}
+mkdir -p $OUT
+export TMPDIR=/tmp
+fatal() { case $1 in 124|137|134|139) return 0;; esac; return 1; }
+step() { local name=$1 t=$2; shift 2; timeout -k 10 "$t" "$@" > $OUT/$name.log 2>&1; local rc=$?;
+         echo "[$name rc=$rc]"; tail -n 12 $OUT/$name.log; if fatal $rc; then exit $rc; fi; }
+step tests 900 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread
+step bert 300 python bench.py --model bert-base --steps 20 --warmup 5
+step bertprof 300 rocprofv3 --kernel-trace --stats -d $OUT/bprof -o bert --output-format csv -- python3 bench.py --model bert-base --steps 5 --warmup 2
+step gpt 300 python bench.py --steps 20 --warmup 5
+step fa 120 python -m scripts.fa_one 16 16 1024 128 1 50
+exit 0

@@ -1,0 +1,106 @@
+"""ZeRO-3 on the device with two ranks: PRA_DIST_BACKEND=gloo puts two rank processes on the one
+GPU of the box (RCCL refuses two ranks per device), so the real zero3=True schedule runs with
+device tensors -- per-unit all-gathers on the twin communicator, reduce-scatters of bf16
+gradients, gradient accumulation over two backward passes, the resident (no re-gather) mode --
+and must match a single-process run of the same model and data."""
+import json
+import os
+import socket
+import subprocess
+import sys
+import textwrap
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+SCRIPT = textwrap.dedent("""
+    import json, os, sys, torch
+    import paddle_ray_amd as paddle
+    from paddle_ray_amd.distributed import collective as C
+    from paddle_ray_amd.models import gpt_config, GPTForPretraining
+    from paddle_ray_amd.distributed.sharding import group_sharded_parallel
+    world = int(os.environ['WORLD_SIZE']); release = os.environ['RELEASE'] == '1'
+    if world > 1:
+        C.init_parallel_env()
+    rank = C.get_rank()
+    paddle.set_device('gpu:0')
+    paddle.seed(11)
+    paddle.set_default_dtype('bfloat16')
+    model = GPTForPretraining(gpt_config('gpt3-tiny', hidden_dropout=0.0, num_layers=3))
+    paddle.set_default_dtype('float32')
+    opt = paddle.optimizer.AdamW(1e-3, parameters=model.parameters(), multi_precision=True,
+                                 grad_clip=paddle.nn.ClipGradByGlobalNorm(1.0))
+    zero3 = None
+    if world > 1:
+        model, opt, _ = group_sharded_parallel(model, opt, 'p_g_os', segment_size=0,
+                                               release_after_forward=release)
+        zero3 = model._state.zero3 and len(model._state.unit_meta) == 3 and \\
+            model._state.ag_pg is not model._state.pg
+    g = torch.Generator(device='cuda').manual_seed(0)
+    ids = torch.randint(0, 1024, (4, 2, 33), device='cuda', generator=g)  # 2 micro-batches x 4 rows
+    losses = []
+    for step in range(3):
+        tot = 0.0
+        for mb in range(2):
+            x = ids[:, mb] if world == 1 else ids[rank * 2:(rank + 1) * 2, mb]
+            x = paddle.Tensor(x)
+            loss = model(x[:, :-1], x[:, 1:]) / 2
+            loss.backward()
+            tot += float(loss)
+        opt.step()
+        opt.clear_grad()
+        if world > 1:
+            t = torch.tensor([tot], device='cuda')
+            torch.distributed.all_reduce(t)
+            tot = float(t) / world
+        losses.append(tot)
+    sd = model.state_dict()
+    s = sum(float(v._t.float().abs().sum()) for v in sd.values())
+    if rank == 0:
+        print('RESULT ' + json.dumps({'losses': losses, 'psum': s, 'zero3': zero3}), flush=True)
+    if world > 1:
+        torch.distributed.barrier()
+        torch.distributed.destroy_process_group()
+""")
+
+
+def _port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(('127.0.0.1', 0))
+        return s.getsockname()[1]
+
+
+def _run(world, release):
+    port = str(_port())
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK='0', WORLD_SIZE=str(world), MASTER_ADDR='127.0.0.1',
+                   MASTER_PORT=port, PRA_DIST_BACKEND='gloo', RELEASE='1' if release else '0',
+                   PYTHONPATH=ROOT + os.pathsep + os.environ.get('PYTHONPATH', ''),
+                   HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get('HSA_ENABLE_IPC_MODE_LEGACY', '0'))
+        procs.append(subprocess.Popen([sys.executable, '-c', SCRIPT], env=env, cwd=ROOT, stdout=subprocess.PIPE,
+                                      stderr=subprocess.PIPE, text=True))
+    outs = []
+    for p in procs:
+        try:
+            o, e = p.communicate(timeout=100)
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+        assert p.returncode == 0, e[-3000:]
+        outs.append(o)
+    line = [l for l in outs[0].splitlines() if l.startswith('RESULT ')][-1]
+    return json.loads(line[7:])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('release', [True, False])
+def test_zero3_two_ranks_on_device_match_single(release):
+    ref = _run(1, release)
+    got = _run(2, release)
+    assert got['zero3'] is True, got
+    np.testing.assert_allclose(got['losses'], ref['losses'], rtol=2e-2, atol=2e-2)
+    assert abs(got['psum'] - ref['psum']) / ref['psum'] < 2e-2, (got['psum'], ref['psum'])
