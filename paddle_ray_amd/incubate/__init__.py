@@ -70,3 +70,7 @@ def graph_khop_sampler(row, colptr, input_nodes, sample_sizes, sorted_eids=None,
     if return_eids:
         out = out + (Tensor(torch.cat(eids) if eids else torch.zeros(0, dtype=torch.int64)),)
     return out
+
+
+from . import operators  # noqa: E402  (re-exports the functions above)
+from .operators import ResNetUnit, resnet_unit, unzip  # noqa: E402,F401
