@@ -965,7 +965,7 @@ class Executor:
 
 
 # =============================================================================
-# inference model save / load (.pdmodel JSON program + .pdiparams)
+# inference model save / load (.pdmodel ProgramDesc protobuf + .pdiparams)
 # =============================================================================
 def _qualname(fn, op_type=None):
     if op_type and ':' in op_type and not op_type.startswith('layer:'):
@@ -1114,27 +1114,121 @@ def _decode(obj, params):
     return obj
 
 
-def serialize_program(feed_vars, fetch_vars, program=None):
-    prog = program or default_main_program()
-    blk = prog.global_block()
-    required = [v.vid for v in fetch_vars]
+def _ordered_forward_ops(blk, required):
     from ..native import build_plan
     ops = [op for op in blk.ops if op.role == 'forward']
     order, _, _, _ = build_plan([o.in_vids for o in ops], [o.out_vids for o in ops], required, [])
+    return [ops[i] for i in order]
+
+
+class _DescWriter:
+    """Program -> ProgramDesc dict (static/program_desc.py documents the mapping)."""
+
+    def __init__(self, blk):
+        self.blk, self.names, self.taken, self.blocks = blk, {}, set(), []
+
+    def name(self, vid):
+        n = self.names.get(vid)
+        if n is None:
+            v = self.blk.vars.get(vid)
+            v = _ALL_VARS.get(vid) if v is None else v
+            n = v.name if v is not None and v.name else f'_pra_var_{vid}'
+            if n in self.taken or n in ('feed', 'fetch'):
+                n = f'{n}@{vid}'
+            self.names[vid] = n
+            self.taken.add(n)
+        return n
+
+    def var(self, vid, params):
+        from . import program_desc as PD
+        v = self.blk.vars.get(vid)
+        v = _ALL_VARS.get(vid) if v is None else v
+        shape = v.shape if v is not None else []
+        dt = dtype_to_str(v.dtype) if v is not None else 'float32'
+        return PD.var_desc(self.name(vid), shape, dt, stop_gradient=bool(v is None or v.stop_gradient),
+                           need_check_feed=bool(v is not None and getattr(v, 'is_data', False)))
+
+    def _names_in(self, obj, blocks_out, parent):
+        """Rewrite an _encode()d structure: var vids -> names, nested op lists -> sub-blocks."""
+        if isinstance(obj, list):
+            return [self._names_in(o, blocks_out, parent) for o in obj]
+        if isinstance(obj, dict):
+            if '__var__' in obj:
+                return {'__var__': self.name(obj['__var__'])}
+            if '__block__' in obj:
+                b = obj['__block__']
+                idx = self.block(b['ops'], parent, extra_vids=list(b['ph']) + list(b['cap']))
+                blocks_out.append(idx)
+                return {'__block__': {'idx': idx, 'ph': [self.name(v) for v in b['ph']],
+                                      'cap': [self.name(v) for v in b['cap']],
+                                      'out': self._names_in(b['out'], blocks_out, parent)}}
+            return {k: self._names_in(v, blocks_out, parent) for k, v in obj.items()}
+        return obj
+
+    def op(self, enc, idx):
+        from . import program_desc as PD
+        subs = []
+        call = {'args': self._names_in(enc['args'], subs, idx),
+                'kwargs': self._names_in(enc['kwargs'], subs, idx)}
+        attrs = [{'name': '__pra_call__', 'type': PD.ATTR['STRING'], 's': PD.dumps_call(call)}]
+        kw = enc['kwargs'].get('__dict__', {}) if isinstance(enc['kwargs'], dict) else {}
+        for k, v in sorted(kw.items()):
+            a = PD.scalar_attr(k, v)
+            if a is not None and not k.startswith('__'):
+                attrs.append(a)
+        if len(subs) == 1:
+            attrs.append({'name': 'sub_block', 'type': PD.ATTR['BLOCK'], 'block_idx': subs[0]})
+        elif subs:
+            attrs.append({'name': 'sub_blocks', 'type': PD.ATTR['BLOCKS'], 'blocks_idx': subs})
+        return {'type': enc['type'],
+                'inputs': [{'parameter': 'X', 'arguments': [self.name(v) for v in enc['in']]}],
+                'outputs': [{'parameter': 'Out', 'arguments': [self.name(v) for v in enc['out']]}],
+                'attrs': attrs}
+
+    def block(self, enc_ops, parent, extra_vids=(), params=None):
+        idx = len(self.blocks)
+        bd = {'idx': idx, 'parent_idx': parent, 'vars': [], 'ops': []}
+        self.blocks.append(bd)
+        bd['ops'] = [self.op(o, idx) for o in enc_ops]
+        vids = list(extra_vids)
+        for o in enc_ops:
+            vids += list(o['in']) + list(o['out'])
+        for vid in dict.fromkeys(vids):
+            if idx == 0 or vid not in self.blk.vars:
+                bd['vars'].append(self.var(vid, params))
+        return idx
+
+
+def serialize_program(feed_vars, fetch_vars, program=None):
+    """ProgramDesc protobuf bytes of the forward ops reaching ``fetch_vars`` (parity:
+    static/io.py serialize_program -> framework.proto ProgramDesc)."""
+    from . import program_desc as PD
+    prog = program or default_main_program()
+    blk = prog.global_block()
+    required = [v.vid for v in fetch_vars]
     params = {}
-    enc_ops = []
-    for oi in order:
-        op = ops[oi]
-        qn = _qualname(op.fn, op.type)
-        if qn not in _OP_TABLE:
-            raise TypeError(f"op {op.type!r} is not a registered static op; cannot serialize")
-        enc_ops.append({'type': qn, 'args': _encode(op.args, params),
-                        'kwargs': _encode(op.kwargs, params), 'in': op.in_vids, 'out': op.out_vids})
-    vars_ = {str(v.vid): {'name': v.name, 'shape': v.shape, 'dtype': dtype_to_str(v.dtype)}
-             for v in blk.vars.values()}
-    desc = {'version': 2, 'feeds': [v.vid for v in feed_vars], 'fetches': required,
-            'ops': enc_ops, 'vars': vars_, 'params': sorted(params)}
-    return json.dumps(desc).encode(), params
+    enc_ops = _encode_ops(_ordered_forward_ops(blk, required), params)
+    w = _DescWriter(blk)
+    w.block(enc_ops, -1, extra_vids=[v.vid for v in feed_vars] + required)
+    b0 = w.blocks[0]
+    b0['vars'] = [vd for vd in b0['vars']]
+    b0['vars'].insert(0, {'name': 'feed', 'persistable': True,
+                          'type': {'type': PD.VT_FEED_MINIBATCH}})
+    b0['vars'].insert(1, {'name': 'fetch', 'persistable': True, 'type': {'type': PD.VT_FETCH_LIST}})
+    for name, p in sorted(params.items()):
+        b0['vars'].append(PD.var_desc(name, list(p.shape), dtype_to_str(p.dtype), persistable=True,
+                                      is_parameter=True, stop_gradient=p.stop_gradient))
+    feeds = [{'type': 'feed', 'inputs': [{'parameter': 'X', 'arguments': ['feed']}],
+              'outputs': [{'parameter': 'Out', 'arguments': [w.name(v.vid)]}],
+              'attrs': [{'name': 'col', 'type': PD.ATTR['INT'], 'i': i}]}
+             for i, v in enumerate(feed_vars)]
+    fetches = [{'type': 'fetch', 'inputs': [{'parameter': 'X', 'arguments': [w.name(vid)]}],
+                'outputs': [{'parameter': 'Out', 'arguments': ['fetch']}],
+                'attrs': [{'name': 'col', 'type': PD.ATTR['INT'], 'i': i}]}
+               for i, vid in enumerate(required)]
+    b0['ops'] = feeds + b0['ops'] + fetches
+    desc = {'blocks': w.blocks, 'version': {'version': PD.PROGRAM_VERSION}}
+    return PD.encode('ProgramDesc', desc), params
 
 
 def serialize_persistables(feed_vars, fetch_vars, executor=None, program=None):
@@ -1160,7 +1254,8 @@ def save_inference_model(path_prefix, feed_vars, fetch_vars, executor=None, prog
     save(params, path_prefix + '.pdiparams')
 
 
-def deserialize_program(data, params=None):
+def _deserialize_json(data, params=None):
+    """The round-1/2 JSON op-list .pdmodel (still readable)."""
     desc = json.loads(data.decode() if isinstance(data, bytes) else data)
     prog = Program()
     blk = prog.global_block()
@@ -1182,6 +1277,84 @@ def deserialize_program(data, params=None):
         blk.ops.append(op)
     prog._feeds = [vmap[i] for i in desc['feeds']]
     prog._fetches = [vmap[i] for i in desc['fetches']]
+    prog._bump()
+    return prog
+
+
+def deserialize_program(data, params=None):
+    """Program from ProgramDesc protobuf bytes (or a legacy JSON .pdmodel). Ops are rebuilt
+    ONLY from registered op types (``_resolve``); parameters bind by name to ``params``."""
+    from . import program_desc as PD
+    if not PD.is_program_desc(data):
+        return _deserialize_json(data, params)
+    desc = PD.decode('ProgramDesc', bytes(data))
+    blocks = desc.get('blocks', [])
+    if not blocks:
+        raise ValueError("ProgramDesc has no blocks")
+    params = params or {}
+    prog = Program()
+    blk = prog.global_block()
+    vids = {}
+    feeds, fetches = {}, {}
+    for b in blocks:
+        for vd in b.get('vars', []):
+            name, shape, dt = PD.var_info(vd)
+            if dt is None or name in params or name in vids:
+                continue
+            v = Variable(blk, shape, dt, name=name, is_data=bool(vd.get('need_check_feed')))
+            vids[name] = v.vid
+            if b.get('idx', 0) == 0:
+                blk.vars[v.vid] = v
+            else:
+                blk.__dict__.setdefault('_sub_vars', []).append(v)  # keep them alive
+    for p in params.values():
+        prog._register_param(p)
+
+    def names_to_vids(obj):
+        if isinstance(obj, list):
+            return [names_to_vids(o) for o in obj]
+        if isinstance(obj, dict):
+            if '__var__' in obj:
+                return {'__var__': vids[obj['__var__']]}
+            if '__block__' in obj:
+                b = obj['__block__']
+                return {'__block__': {'ops': enc_block(b['idx']),
+                                      'ph': [vids[n] for n in b['ph']],
+                                      'cap': [vids[n] for n in b['cap']],
+                                      'out': names_to_vids(b['out'])}}
+            return {k: names_to_vids(v) for k, v in obj.items()}
+        return obj
+
+    def enc_op(od):
+        attrs = {a['name']: a for a in od.get('attrs', [])}
+        call = attrs.get('__pra_call__')
+        if call is None:
+            raise ValueError(f"op {od.get('type')!r} carries no __pra_call__ attribute: not a "
+                             "paddle_ray_amd program")
+        c = PD.loads_call(PD.attr_value(call))
+        slot = lambda vs: [vids[n] for s in vs for n in s.get('arguments', [])]  # noqa: E731
+        return {'type': od['type'], 'args': names_to_vids(c['args']),
+                'kwargs': names_to_vids(c['kwargs']), 'in': slot(od.get('inputs', [])),
+                'out': slot(od.get('outputs', []))}
+
+    def enc_block(idx):
+        return [enc_op(od) for od in blocks[idx].get('ops', [])]
+
+    for od in blocks[0].get('ops', []):
+        attrs = {a['name']: a for a in od.get('attrs', [])}
+        if od['type'] == 'feed':
+            feeds[PD.attr_value(attrs['col'])] = od['outputs'][0]['arguments'][0]
+            continue
+        if od['type'] == 'fetch':
+            fetches[PD.attr_value(attrs['col'])] = od['inputs'][0]['arguments'][0]
+            continue
+        o = enc_op(od)
+        blk.ops.append(OpDesc(o['type'], _resolve(o['type']), _decode(o['args'], params),
+                              _decode(o['kwargs'], params), o['in'], o['out'], None))
+    prog._feeds = [blk.vars[vids[feeds[i]]] for i in sorted(feeds)]
+    for v in prog._feeds:
+        v.__dict__['is_data'] = True
+    prog._fetches = [blk.vars[vids[fetches[i]]] for i in sorted(fetches)]
     prog._bump()
     return prog
 

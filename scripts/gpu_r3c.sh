@@ -6,7 +6,7 @@ export TMPDIR=/tmp
 fatal() { case $1 in 124|137|134|139) return 0;; esac; return 1; }
 step() { local name=$1 t=$2; shift 2; timeout -k 10 "$t" "$@" > $OUT/$name.log 2>&1; local rc=$?;
          echo "[$name rc=$rc]"; tail -n 12 $OUT/$name.log; if fatal $rc; then exit $rc; fi; }
-step tests 500 python -u -m pytest tests/test_flash_ext.py tests/test_zero3_gpu.py tests/test_kernels_gpu.py -m gpu -q --timeout 120 --timeout-method thread
+step tests 500 python -u -m pytest tests/test_flash_ext.py tests/test_zero3_gpu.py tests/test_kernels_gpu.py tests/test_resnet_unit.py -m gpu -q --timeout 120 --timeout-method thread
 step bert 300 python bench.py --model bert-base --steps 20 --warmup 5
 step bertprof 300 rocprofv3 --kernel-trace --stats -d $OUT/bprof -o bert --output-format csv -- python3 bench.py --model bert-base --steps 5 --warmup 2
 step gpt 300 python bench.py --steps 20 --warmup 5

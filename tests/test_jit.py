@@ -186,8 +186,12 @@ def test_dy2static_if_while_both_branches_after_save_load(tmp_path):
     np.testing.assert_allclose(e_neg, np.full((2, 4), -10.0))
     path = str(tmp_path / 'branchy')
     paddle.jit.save(net, path, input_spec=[InputSpec([None, 4], 'float32')])
-    ops = open(path + '.pdmodel').read()
-    assert 'conditional_block_op' in ops and 'while_op' in ops
+    from paddle_ray_amd.static import program_desc as PD
+    desc = PD.decode('ProgramDesc', open(path + '.pdmodel', 'rb').read())
+    types = [o['type'] for b in desc['blocks'] for o in b.get('ops', [])]
+    assert any('conditional_block_op' in t for t in types) and any('while_op' in t for t in types)
+    assert len(desc['blocks']) >= 3  # block 0 + the if-branches + the while body
+    assert all(b['parent_idx'] == (-1 if b['idx'] == 0 else b['parent_idx']) for b in desc['blocks'])
     ld = paddle.jit.load(path)
     np.testing.assert_allclose(ld(pos).numpy(), e_pos, rtol=1e-6)
     np.testing.assert_allclose(ld(neg).numpy(), e_neg, rtol=1e-6)

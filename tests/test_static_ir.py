@@ -74,14 +74,25 @@ def test_tampered_pdmodel_refused(static_mode, tmp_path):
     exe = static.Executor()
     path = str(tmp_path / 'm')
     static.save_inference_model(path, [x], [y], exe, program=main)
-    desc = json.loads(open(path + '.pdmodel', 'rb').read())
-    assert all('fn' not in o for o in desc['ops'])  # ops are named by registered type only
+    from paddle_ray_amd.static import program_desc as PD
+    raw = open(path + '.pdmodel', 'rb').read()
+    desc = PD.decode('ProgramDesc', raw)
+    ops = desc['blocks'][0]['ops']
+    assert ops[0]['type'] == 'feed' and ops[-1]['type'] == 'fetch'
     prog, _, fetch = static.load_inference_model(path, exe)  # the untampered model loads
+    k = next(i for i, o in enumerate(ops) if o['type'] not in ('feed', 'fetch'))
     for evil in ('os:system', 'posix:system', 'subprocess:check_output', 'builtins:eval'):
-        bad = dict(desc)
-        bad['ops'] = [dict(desc['ops'][0], type=evil, args=['touch ' + str(tmp_path / 'pwned')])] + \
-            desc['ops'][1:]
-        open(path + '.pdmodel', 'wb').write(json.dumps(bad).encode())
+        bad = [dict(o) for o in ops]
+        call = PD.dumps_call({'args': ['touch ' + str(tmp_path / 'pwned')], 'kwargs': {}})
+        bad[k] = dict(bad[k], type=evil, attrs=[{'name': '__pra_call__', 'type': 2, 's': call}])
+        d2 = dict(desc, blocks=[dict(desc['blocks'][0], ops=bad)] + desc['blocks'][1:])
+        open(path + '.pdmodel', 'wb').write(PD.encode('ProgramDesc', d2))
+        with pytest.raises(ValueError, match='not a registered'):
+            static.load_inference_model(path, exe)
+        # the legacy JSON op list is refused the same way
+        open(path + '.pdmodel', 'wb').write(json.dumps(
+            {'version': 2, 'feeds': [], 'fetches': [], 'vars': {}, 'params': [],
+             'ops': [{'type': evil, 'args': ['touch x'], 'kwargs': {}, 'in': [], 'out': []}]}).encode())
         with pytest.raises(ValueError, match='not a registered'):
             static.load_inference_model(path, exe)
     assert not (tmp_path / 'pwned').exists()
