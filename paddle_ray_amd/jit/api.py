@@ -15,11 +15,11 @@ reference's dy2static is used for:
   backward replays the second, returning input and parameter gradients (accumulated into
   ``.grad`` as usual). Parameters must keep their storage (optimizers update in place).
 * **Program export**: ``concrete_program`` / ``jit.save`` record the layer into a static
-  ``Program`` (static/graph.py) from ``InputSpec``s and write ``.pdmodel`` (JSON op list)
-  + ``.pdiparams``; ``jit.load`` returns a ``TranslatedLayer`` that replays the program
+  ``Program`` (static/graph.py) from ``InputSpec``s and write ``.pdmodel`` (a ProgramDesc
+  protobuf, static/program_desc.py) + ``.pdiparams``; ``jit.load`` returns a ``TranslatedLayer`` that replays the program
   eagerly, so it can run inference or be fine-tuned. Before recording, the function's
   tensor-valued ``if`` / ``while`` statements are converted (``dy2static.py``) into
-  ``static.nn.cond`` / ``while_loop`` sub-blocks, which serialize as nested op lists.
+  ``static.nn.cond`` / ``while_loop`` sub-blocks, which serialize as sub-BlockDescs.
 * Graph replay hands out fresh output tensors on every call, and a function that cannot be
   captured (host read of device data, data-dependent shapes) runs eagerly instead.
 """

@@ -23,8 +23,8 @@ and AMP casts match the forward. ``optimize`` consumes the ``param@GRAD`` vars. 
 backward of a training program can be captured as ONE HIP graph
 (``BuildStrategy.use_hip_graph``); the optimizer step runs after the replay.
 
-Serialized programs (``.pdmodel``) name ops only by their registered op type; loading
-resolves names through the static op table and refuses anything else.
+Serialized programs (``.pdmodel``, a framework.proto ProgramDesc written by
+static/program_desc.py) name ops only by their registered op type; loading resolves names through the static op table and refuses anything else.
 """
 import collections
 import contextlib
