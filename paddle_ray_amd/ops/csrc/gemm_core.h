@@ -89,9 +89,13 @@ constexpr int BM = 256, BN = 256, BKT = 64;  // the GEMM tile (conv configs belo
 //       512x64, 64x64 per wave): a 256-wide tile would leave half / three quarters of its
 //       MFMAs on padding columns. Their B operand must be K-contiguous (BK = true).
 // Each K-step stages A [BM][64] and B [BN][64] (or [64][BN]) images, double-buffered.
-template <int WR_, int WC_, int BM_ = 256, int BN_ = 256>
+//   ILV: one non-MFMA instruction (an LDS-DMA issue or a fragment read) after each MFMA of a
+//       segment instead of a burst between MFMA groups (one wave per SIMD has no partner wave
+//       to cover a burst)
+template <int WR_, int WC_, int BM_ = 256, int BN_ = 256, bool ILV_ = false>
 struct WCfg {
   static constexpr int WR = WR_, WC = WC_, NT = 64 * WR_ * WC_, BM = BM_, BN = BN_;
+  static constexpr bool ILV = ILV_;
   static constexpr int TI = BM_ / WR_ / 16, TJ = BN_ / WC_ / 16;  // 16x16 MFMA tiles per wave
   static constexpr int IMGA = BM_ * BKT * 2, IMGB = BN_ * BKT * 2, SLOT = IMGA + IMGB;
   static constexpr int NDA = IMGA / (NT * 16), NDB = IMGB / (NT * 16);  // glds per thread per K-step
@@ -99,7 +103,7 @@ struct WCfg {
   static constexpr int LDS = 2 * SLOT > EPI ? 2 * SLOT : EPI;
 };
 using W8 = WCfg<2, 4>;
-using W4 = WCfg<2, 2>;  // instantiated in gemm_w4.hip
+using W4 = WCfg<2, 2, 256, 256, true>;  // instantiated in gemm_w4.hip
 using C128 = WCfg<4, 2, 256, 128>;
 using C64 = WCfg<8, 1, 512, 64>;
 
@@ -382,6 +386,33 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_lds_kernel(const uint16_t* __r
     const char* bi = ai + IMGA;
     // DMA instructions per segment (DPSX > 0: front-load them into the first segments)
     constexpr int DPS = DPSX > 0 ? DPSX : (NDA + NDB + TI - 1) / TI;
+    if constexpr (CF::ILV) {
+      // segment i: MFMA j, then filler j -- the DMA pieces at even j, the two fragment reads at
+      // j = 1, 3 -- each pinned in place, so the matrix pipe never waits behind a burst
+#pragma unroll
+      for (int i = 0; i < TI; ++i) {
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) {
+          if constexpr (AGPR_ACC) mma_agpr<T>(cb[j], ca[i], acc[i][j]);
+          else acc[i][j] = mma<T>(cb[j], ca[i], acc[i][j]);
+          __builtin_amdgcn_sched_barrier(0);
+          if ((j & 1) == 0 && (j >> 1) < DPS && (dA || dB)) {
+            const int d = i * DPS + (j >> 1);
+            if (d < NDA) {
+              if (dA) da.issue1(soA, wave, kA, d);
+            } else if (d < NDA + NDB && dB) {
+              db.issue1(soB, wave, kB, d - NDA);
+            }
+          } else if (j == 1 && rd && i < TJ) {
+            nb[i] = frag<T, BK>(bi, wc * CW + i * 16, rs, lane);
+          } else if (j == 3 && rd) {
+            na[i] = frag<T, AK>(ai, wr * RW + i * 16, rs, lane);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < TI; ++i) {
       if (dA || dB) {

@@ -38,12 +38,16 @@
 extern "C" int pra_gemm_w4(int layout, const void* A, const void* B, const void* bias, void* C, void* Z,
                            float* colsum, int M, int N, int K, int lda, int ldb, int ldc, int ldz, int dtype,
                            int epi, int beta, int splits, float* ws, hipStream_t s);
+extern "C" int pra_gemm_w8i(int layout, const void* A, const void* B, const void* bias, void* C, void* Z,
+                            float* colsum, int M, int N, int K, int lda, int ldb, int ldc, int ldz, int dtype,
+                            int epi, int beta, int splits, float* ws, hipStream_t s);
 
 namespace pra {
 namespace {
 
-// Which layouts run the 4-wave configuration (bit = 1 << layout): PRA_GEMM_W4 at first use,
-// pra_gemm_set_w4 afterwards (A/B timing in one process).
+// Which layouts run the 4-wave configuration (bit = 1 << layout) or the 8-wave one with the
+// one-filler-per-MFMA schedule (bit = 16 << layout): PRA_GEMM_W4 at first use, pra_gemm_set_w4
+// afterwards (A/B timing in one process).
 int g_w4_mask = -1;
 int w4_mask() {
   if (g_w4_mask < 0) {
@@ -68,10 +72,14 @@ void launch_e(const void* A, const void* B, const void* bias, void* C, void* Z, 
   static const int ablate = getenv("PRA_GEMM_ABLATE") ? 0 : 1;  // 0: no DMA after the prologue (timing only)
   constexpr int layout = AK ? (BK ? 1 : 0) : 2;
   const bool w4 = std::is_same<T, bf16>::value && E != kRelu && (w4_mask() >> layout & 1);
+  const bool w8i = !w4 && std::is_same<T, bf16>::value && E != kRelu && (w4_mask() >> (layout + 4) & 1);
   if (splits > 1) {
     if (w4)
       pra_gemm_w4(layout, A, B, nullptr, nullptr, nullptr, nullptr, M, N, K, lda, ldb, ldc, ldz, kBF16, 0, 0,
                   splits, ws, s);
+    else if (w8i)
+      pra_gemm_w8i(layout, A, B, nullptr, nullptr, nullptr, nullptr, M, N, K, lda, ldb, ldc, ldz, kBF16, 0, 0,
+                   splits, ws, s);
     else
       gemm_lds_kernel<T, W8, AK, BK, kNone, false, true><<<tiles * splits, W8::NT, 0, s>>>(
           pa, pb, nullptr, nullptr, nullptr, nullptr, M, N, K, lda, ldb, ldc, ldz, splits, ws);
@@ -91,6 +99,9 @@ void launch_e(const void* A, const void* B, const void* bias, void* C, void* Z, 
   (void)four;
   if (w4 && pra_gemm_w4(layout, A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, kBF16, E, beta, 1, nullptr,
                         s) == 0)
+    return;
+  if (w8i && pra_gemm_w8i(layout, A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, kBF16, E, beta, 1, nullptr,
+                          s) == 0)
     return;
   if (beta) PRA_GEMM_LAUNCH(W8, true); else PRA_GEMM_LAUNCH(W8, false);
 #undef PRA_GEMM_LAUNCH

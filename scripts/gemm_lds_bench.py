@@ -73,42 +73,45 @@ def timeit(fn, iters):
 
 
 def main_w4():
-    """8-wave vs 4-wave configuration vs hipBLASLt, interleaved in one process."""
+    """Kernel configurations vs hipBLASLt, interleaved in one process: W8 (8 waves, burst
+    schedule), W4 (4 waves x 128x128, one filler per MFMA), W8I (8 waves, one filler per MFMA)."""
     dev = torch.device('cuda')
-    print("| GEMM | layout | M | N | K | err W8 | err W4 | W8 us | W4 us | hipBLASLt us | W4 PF/s | W4/W8 | W4 vs hipBLASLt |")
-    print("|---|---|---|---|---|---|---|---|---|---|---|---|---|", flush=True)
-    tot = [0.0, 0.0, 0.0]
+    cfgs = [('W8', 0), ('W4', 7), ('W8I', 7 << 4)]
+    hdr = ' | '.join(f'err {n}' for n, _ in cfgs) + ' | ' + ' | '.join(f'{n} us' for n, _ in cfgs)
+    print(f"| GEMM | layout | M | N | K | {hdr} | hipBLASLt us | best | best PF/s | best vs hipBLASLt |")
+    print("|---|---|---|---|---|" + "---|" * (2 * len(cfgs) + 4), flush=True)
+    tot = [0.0] * (len(cfgs) + 1)
     for name, layout, M, N, K in SHAPES:
-        L.gemm_set_w4(0)
-        e8 = check(name, layout, M, N, K, dev)
-        L.gemm_set_w4(7)
-        e4 = check(name, layout, M, N, K, dev)
+        errs = []
+        for _, mask in cfgs:
+            L.gemm_set_w4(mask)
+            errs.append(check(name, layout, M, N, K, dev))
         a, b = operands(layout, M, N, K, dev)
         c = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
 
-        def f8():
-            L.gemm_set_w4(0)
-            ours(layout, a, b, c, M, N, K)
-
-        def f4():
-            L.gemm_set_w4(7)
-            ours(layout, a, b, c, M, N, K)
-        fh = lambda: ref_mm(layout, a, b)  # noqa: E731
-        for f in (f8, f4, fh):
+        def mk(mask):
+            def f():
+                L.gemm_set_w4(mask)
+                ours(layout, a, b, c, M, N, K)
+            return f
+        fs = [mk(mask) for _, mask in cfgs] + [lambda: ref_mm(layout, a, b)]
+        for f in fs:
             f()
         torch.cuda.synchronize()
         it = 5 if M * N * K > 1e12 else 20
-        ts = [[], [], []]
+        ts = [[] for _ in fs]
         for _ in range(5):
-            for i, f in enumerate((f8, f4, fh)):
+            for i, f in enumerate(fs):
                 ts[i].append(timeit(f, it))
         m = [statistics.median(t) for t in ts]
-        for i in range(3):
+        for i in range(len(fs)):
             tot[i] += m[i]
         fl = 2.0 * M * N * K
-        print(f"| {name} | {layout} | {M} | {N} | {K} | {e8:.1e} | {e4:.1e} | {m[0] * 1e3:.1f} | {m[1] * 1e3:.1f} | "
-              f"{m[2] * 1e3:.1f} | {fl / m[1] / 1e12:.3f} | {m[0] / m[1]:.3f} | {m[2] / m[1]:.3f} |", flush=True)
-    print(f"\ntotal W8 {tot[0]:.3f} ms, W4 {tot[1]:.3f} ms, hipBLASLt {tot[2]:.3f} ms")
+        bi = min(range(len(cfgs)), key=lambda i: m[i])
+        print(f"| {name} | {layout} | {M} | {N} | {K} | " + ' | '.join(f'{e:.1e}' for e in errs) + ' | '
+              + ' | '.join(f'{x * 1e3:.1f}' for x in m[:-1]) + f" | {m[-1] * 1e3:.1f} | {cfgs[bi][0]} | "
+              f"{fl / m[bi] / 1e12:.3f} | {m[-1] / m[bi]:.3f} |", flush=True)
+    print('\ntotal ' + ', '.join(f'{n} {t:.3f} ms' for (n, _), t in zip(cfgs, tot)) + f', hipBLASLt {tot[-1]:.3f} ms')
     L.gemm_set_w4(0)
 
 
