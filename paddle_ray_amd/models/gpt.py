@@ -194,6 +194,9 @@ class GPTBlock(nn.Layer):
     def __init__(self, cfg, layer_idx):
         super().__init__()
         self.ln1 = nn.LayerNorm(cfg.hidden_size, cfg.layer_norm_eps)
+        # the fused path applies ln1 at the end of the PREVIOUS block (add+dropout+LN): its
+        # parameters are read outside this block's forward, so ZeRO-3 keeps them resident
+        self.ln1._zero3_resident = True
         self.attn = GPTAttention(cfg, layer_idx)
         self.ln2 = nn.LayerNorm(cfg.hidden_size, cfg.layer_norm_eps)
         self.mlp = GPTMLP(cfg)

@@ -100,8 +100,9 @@ class ShardedState:
       * backward: once the unit's gradients are accumulated the reduce-scatter is launched
         and the gathered buffer is freed; after the reduce-scatter completes the full
         gradient buffer is freed too — only owned shards stay resident between steps.
-    Small parameters (biases, norms, ``<= segment_size``) and parameters outside units
-    stay resident (gathered once per step after the optimizer update, like stage 2).
+    Small parameters (biases, norms, ``<= segment_size``), parameters outside units and those of
+    sublayers flagged ``_zero3_resident`` (read outside their unit's forward) stay resident
+    (gathered once per step after the optimizer update, like stage 2).
     ``dp_group``: hybrid dp x sharding — shard gradients are then averaged over the replicas.
     """
 
@@ -135,8 +136,12 @@ class ShardedState:
         if self.zero3:
             excl = tuple(exclude_layer) if exclude_layer else ()
             for u in _find_units(layer, excl):
+                # sublayers flagged _zero3_resident are read outside the unit's forward (e.g.
+                # GPT's next-block LayerNorm fused into the previous block): never released
+                shared = {id(p) for m in u.sublayers(include_self=True)
+                          if getattr(m, '_zero3_resident', False) for p in m.parameters()}
                 for p in u.parameters():
-                    if not p.stop_gradient and p._t.numel() > segment_size:
+                    if not p.stop_gradient and p._t.numel() > segment_size and id(p) not in shared:
                         unit_of.setdefault(id(p), len(self.units))
                 self.units.append(u)
         resident = [p for p in params if id(p) not in unit_of]

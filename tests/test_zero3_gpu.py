@@ -104,3 +104,22 @@ def test_zero3_two_ranks_on_device_match_single(release):
     assert got['zero3'] is True, got
     np.testing.assert_allclose(got['losses'], ref['losses'], rtol=2e-2, atol=2e-2)
     assert abs(got['psum'] - ref['psum']) / ref['psum'] < 2e-2, (got['psum'], ref['psum'])
+
+
+def test_zero3_two_ranks_cpu_fused_gpt_match_single():
+    """The same schedule over gloo on the CPU with segment_size=0 (every parameter, the
+    LayerNorms included, in its unit): GPT's fused path reads the NEXT block's ln1 inside the
+    current block, so those parameters must stay resident (``_zero3_resident``) -- reading them
+    while their unit's prefetch all-gather is in flight gave rank-timing-dependent losses."""
+    global SCRIPT
+    saved = SCRIPT
+    SCRIPT = (saved.replace("paddle.set_device('gpu:0')", "paddle.set_device('cpu')")
+              .replace("torch.Generator(device='cuda')", "torch.Generator()").replace("device='cuda'", "device='cpu'"))
+    try:
+        for release in (True, False):
+            ref = _run(1, release)
+            got = _run(2, release)
+            assert got['zero3'] is True, got
+            np.testing.assert_allclose(got['losses'], ref['losses'], rtol=2e-3, atol=2e-3)
+    finally:
+        SCRIPT = saved
