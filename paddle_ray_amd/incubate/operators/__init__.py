@@ -39,8 +39,16 @@ def _bn_vec(p):
 
 def _conv_bn(x, filt, scale, bias, mean, var, z, stride, padding, dilation, groups, momentum,
              eps, training, act):
-    """act(BN(conv(x)) + z) on channels-last tensors, filt in OHWI."""
+    """act(BN(conv(x)) + z) on channels-last tensors, filt in OHWI. Training KxK convolutions on
+    the device take the BN statistics from the convolution's epilogue (ops.fused.conv_bn_act_nhwc)."""
+    from ...ops import fused as K
     w = _u(filt).permute(0, 3, 1, 2)  # OIHW-shaped view of the OHWI storage
+    xt, rm = _u(x), _bn_vec(mean)
+    if (dilation == 1 and groups == 1 and isinstance(stride, int) and isinstance(padding, int)
+            and xt.dtype == w.dtype and K.conv_bn_stats_ok(xt, w, stride, padding, rm, training)):
+        return K.conv_bn_act_nhwc(xt, w, stride, padding, _bn_vec(scale), _bn_vec(bias), rm,
+                                  _bn_vec(var), training, momentum, eps,
+                                  _u(z) if z is not None else None, act == 'relu')
     c = F.conv2d(x, w, None, stride, padding, dilation, groups, data_format='NHWC')
     return F.fused_bn_add_act(c, z, _bn_vec(mean), _bn_vec(var), _bn_vec(scale), _bn_vec(bias),
                               training, momentum, eps, act, data_format='NHWC')

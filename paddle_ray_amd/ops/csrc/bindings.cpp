@@ -78,13 +78,17 @@ int pra_gemm_lds_splits(int, int, int);
 void pra_gemm_set_w4(int);
 int pra_gemm_get_w4();
 int pra_conv_lds(const void*, const void*, const void*, void*, int, int, int, int, int, int, int, int, int, int, int,
-                 int, float*, hipStream_t);
+                 int, float*, float*, const float*, hipStream_t);
+int pra_conv_lds_stat_rows(int, int);
 int pra_conv_lds_splits(int, int, int);
 int pra_conv_wgrad_lds(const void*, const void*, void*, int, int, int, int, int, int, int, int, int, int, int, float*,
                        hipStream_t);
 int pra_colsum_partials(const float*, void*, int, int, int, hipStream_t);
 void pra_bn_fwd_train(const void*, const void*, const void*, const void*, float*, float*, void*, uint8_t*, float*,
                       float*, float*, float*, int, int, int, float, float, int, int, int, hipStream_t);
+void pra_bn_fwd_parts(const void*, const void*, const void*, const void*, float*, float*, void*, uint8_t*, float*,
+                      float*, const float*, const float*, float*, int, int, int, float, float, int, int, int,
+                      hipStream_t);
 void pra_bn_fwd_infer(const void*, const void*, const void*, const void*, const float*, const float*, void*, float*,
                       int, int, float, int, int, int, hipStream_t);
 void pra_bn_bwd(const void*, const void*, const uint8_t*, const void*, const void*, const float*, const float*, void*,
@@ -112,9 +116,10 @@ PYBIND11_MODULE(_pra_hip, m) {
     check_launch("gemm_bias_act");
   });
   m.def("conv_lds", [](P x, P w, P bias, P y, int n, int h, int wd, int c, int cout, int kh, int kw, int st,
-                       int pad, int relu, int dt, int splits, P ws, P s) {
+                       int pad, int relu, int dt, int splits, P ws, P part, P kshift, P s) {
     if (pra_conv_lds(CV(x), CV(w), CV(bias), V(y), n, h, wd, c, cout, kh, kw, st, pad, relu, dt, splits,
-                     reinterpret_cast<float*>(ws), S(s)) != 0)
+                     reinterpret_cast<float*>(ws), reinterpret_cast<float*>(part),
+                     reinterpret_cast<const float*>(kshift), S(s)) != 0)
       throw std::invalid_argument("conv_lds: unsupported shape/dtype");
     check_launch("conv_lds");
   });
@@ -126,6 +131,7 @@ PYBIND11_MODULE(_pra_hip, m) {
     check_launch("conv_wgrad_lds");
   });
   m.def("conv_lds_splits", [](int m, int n, int k) { return pra_conv_lds_splits(m, n, k); });
+  m.def("conv_lds_stat_rows", [](int m, int n) { return pra_conv_lds_stat_rows(m, n); });
   m.def("gemm_lds_splits", [](int M, int N, int K) { return pra_gemm_lds_splits(M, N, K); });
   m.def("gemm_set_w4", [](int mask) { pra_gemm_set_w4(mask); });
   m.def("gemm_get_w4", []() { return pra_gemm_get_w4(); });
@@ -291,6 +297,13 @@ PYBIND11_MODULE(_pra_hip, m) {
     pra_bn_fwd_train(CV(x), CV(z), CV(w), CV(b), F(rm), F(rv), V(y), reinterpret_cast<uint8_t*>(mask), F(mean),
                      F(invstd), F(part), F(coef), M, C, nrb, eps, mom, relu, dt, dtw, S(s));
     check_launch("bn_fwd_train");
+  });
+  m.def("bn_fwd_parts", [](P x, P z, P w, P b, P rm, P rv, P y, P mask, P mean, P invstd, P part, P kshift, P coef,
+                           int M, int C, int nrb, float eps, float mom, int relu, int dt, int dtw, P s) {
+    pra_bn_fwd_parts(CV(x), CV(z), CV(w), CV(b), F(rm), F(rv), V(y), reinterpret_cast<uint8_t*>(mask), F(mean),
+                     F(invstd), reinterpret_cast<const float*>(part), reinterpret_cast<const float*>(kshift), F(coef),
+                     M, C, nrb, eps, mom, relu, dt, dtw, S(s));
+    check_launch("bn_fwd_parts");
   });
   m.def("bn_fwd_infer", [](P x, P z, P w, P b, P rm, P rv, P y, P coef, int M, int C, float eps, int relu, int dt,
                            int dtw, P s) {

@@ -177,13 +177,15 @@ __global__ void __launch_bounds__(1024) bn_fin_fwd_k(const float* __restrict__ p
                                                      float* __restrict__ rmean, float* __restrict__ rvar,
                                                      float* __restrict__ mean, float* __restrict__ invstd,
                                                      float* __restrict__ coef, int nrb, int M, int C, float eps,
-                                                     float momentum) {
+                                                     float momentum, const float* __restrict__ kshift = nullptr) {
   __shared__ double red[2048];
   const int c = blockIdx.x * 64 + (threadIdx.x & 63), rl = threadIdx.x >> 6;
   double S1, S2;
   merge_parts(part, nrb, C, c, rl, S1, S2, red);
   if (rl != 0 || c >= C) return;
-  const double K = (double)Cvt<T>::to(x[c]);
+  // the shift the partial sums were taken around: row 0 of x (bn_reduce_k) or, for statistics
+  // produced by a convolution epilogue, the running mean it was given
+  const double K = kshift ? (double)kshift[c] : (double)Cvt<T>::to(x[c]);
   const double d = S1 / M;
   double var = S2 / M - d * d;
   if (var < 0.0) var = 0.0;
@@ -395,7 +397,20 @@ void pra_bn_fwd_train(const void* x, const void* z, const void* w, const void* b
     hipLaunchKernelGGL((bn_reduce_k<T, 0, false>), rg, dim3(kRedThreads), 0, s, (const T*)x, nullptr, nullptr,
                        nullptr, nullptr, part, M, C, rpb);
     hipLaunchKernelGGL((bn_fin_fwd_k<T>), dim3((C + 63) / 64), dim3(1024), 0, s, part, (const T*)x, w, b, dtw, rmean,
-                       rvar, mean, invstd, coef, nrb, M, C, eps, momentum);
+                       rvar, mean, invstd, coef, nrb, M, C, eps, momentum, (const float*)nullptr);
+    launch_apply<T>(x, z, coef, y, mask, nvec, C, relu, s);
+  });
+}
+
+// Forward from statistics produced elsewhere (the implicit-GEMM convolution's epilogue): part
+// [2][nrb][C] = per-row-block sums of (x - kshift) and (x - kshift)^2; then finalize + apply.
+void pra_bn_fwd_parts(const void* x, const void* z, const void* w, const void* b, float* rmean, float* rvar, void* y,
+                      uint8_t* mask, float* mean, float* invstd, const float* part, const float* kshift, float* coef,
+                      int M, int C, int nrb, float eps, float momentum, int relu, int dt, int dtw, hipStream_t s) {
+  const uint32_t nvec = (uint32_t)((size_t)M * C / 8);
+  PRA_DISPATCH_FLOAT(dt, T, {
+    hipLaunchKernelGGL((bn_fin_fwd_k<T>), dim3((C + 63) / 64), dim3(1024), 0, s, part, (const T*)x, w, b, dtw, rmean,
+                       rvar, mean, invstd, coef, nrb, M, C, eps, momentum, kshift);
     launch_apply<T>(x, z, coef, y, mask, nvec, C, relu, s);
   });
 }

@@ -92,10 +92,11 @@ constexpr int BM = 256, BN = 256, BKT = 64;  // the GEMM tile (conv configs belo
 //   ILV: one non-MFMA instruction (an LDS-DMA issue or a fragment read) after each MFMA of a
 //       segment instead of a burst between MFMA groups (one wave per SIMD has no partner wave
 //       to cover a burst)
-template <int WR_, int WC_, int BM_ = 256, int BN_ = 256, bool ILV_ = false>
+//   BUF: operand DMA as MUBUF buffer_load ... lds instead of global_load_lds
+template <int WR_, int WC_, int BM_ = 256, int BN_ = 256, bool ILV_ = false, bool BUF_ = false>
 struct WCfg {
   static constexpr int WR = WR_, WC = WC_, NT = 64 * WR_ * WC_, BM = BM_, BN = BN_;
-  static constexpr bool ILV = ILV_;
+  static constexpr bool ILV = ILV_, BUF = BUF_;
   static constexpr int TI = BM_ / WR_ / 16, TJ = BN_ / WC_ / 16;  // 16x16 MFMA tiles per wave
   static constexpr int IMGA = BM_ * BKT * 2, IMGB = BN_ * BKT * 2, SLOT = IMGA + IMGB;
   static constexpr int NDA = IMGA / (NT * 16), NDB = IMGB / (NT * 16);  // glds per thread per K-step
@@ -131,7 +132,7 @@ __device__ __forceinline__ int kc_swz(int row) { return (row >> 1) & 7; }
 // whole 128-B lines of every row (BK = 64 bf16), so each L2 line is requested once.
 // KC image: position P (16-B chunk 0..2047) = row P>>3, slot P&7 holds global chunk (P&7)^kc_swz(row).
 // MC image: position P = k-row P>>5, slot P&31 holds global chunk (P&31)^mc_swz(k).
-template <bool KC, int NT, int NDMA>
+template <bool KC, int NT, int NDMA, bool BUF = false>
 struct Dma {
   uint32_t voff[NDMA];  // per-lane byte offsets of the chunks this thread stages
   uint64_t base;        // wave-uniform operand base (SGPRs); advanced per K-step
@@ -157,14 +158,23 @@ struct Dma {
   __device__ __forceinline__ void issue1(uint32_t lds_img, int wave, int kt, int n) {
     const uint64_t g = base + (uint64_t)kt * step;
     // readfirstlane returns int: go through uint32_t so the low word is ZERO-extended
-    const uint64_t gs = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(g >> 32)) << 32) |
-                        (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)g);
+    const uint32_t glo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)g);
+    const uint32_t ghi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(g >> 32));
     // wave-uniform LDS base in M0; the hardware adds lane*16. Issued from inline asm so the
     // compiler's waitcnt model does not see an LDS write in flight and never drains it with
     // vmcnt(0) ahead of the fragment reads: the explicit vmcnt in the K loop is the only wait.
     const uint32_t dst = __builtin_amdgcn_readfirstlane(lds_img + (n * NT + wave * 64) * 16);
-    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff[n]), "s"(gs), "s"(dst)
-                 : "memory");
+    if constexpr (BUF) {
+      // MUBUF form (raw buffer, stride 0, no range limit: the offsets are clamped in-bounds)
+      const u32x4 rs = {glo, ghi & 0xffffu, 0xffffffffu, 0x00020000u};
+      asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff[n]), "s"(rs),
+                   "s"(dst)
+                   : "memory");
+    } else {
+      const uint64_t gs = ((uint64_t)ghi << 32) | (uint64_t)glo;
+      asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff[n]), "s"(gs), "s"(dst)
+                   : "memory");
+    }
   }
 };
 
@@ -311,7 +321,9 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_lds_kernel(const uint16_t* __r
                                                           const uint16_t* __restrict__ bias, uint16_t* __restrict__ C,
                                                           uint16_t* __restrict__ Z, float* __restrict__ colsum,
                                                           int M, int N, int K, int lda, int ldb, int ldc, int ldz,
-                                                          int splits, float* __restrict__ ws, ConvGeom cg = {}) {
+                                                          int splits, float* __restrict__ ws, ConvGeom cg = {},
+                                                          float* __restrict__ colsq = nullptr,
+                                                          const float* __restrict__ cshift = nullptr) {
   constexpr int NT = CF::NT, TI = CF::TI, TJ = CF::TJ, NDA = CF::NDA, NDB = CF::NDB, WC = CF::WC;
   constexpr int BM = CF::BM, BN = CF::BN, IMGA = CF::IMGA, SLOT = CF::SLOT;
   constexpr int RW = TI * 16, CW = TJ * 16;  // rows / columns per wave
@@ -343,8 +355,8 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_lds_kernel(const uint16_t* __r
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6),
             wr = wave / WC, wc = wave % WC;
 
-  typename std::conditional<CONV, ConvDmaA<NT, NDA>, Dma<AK, NT, NDA>>::type da;
-  typename std::conditional<CONVW, ConvDmaBW<NT, NDB>, Dma<BK, NT, NDB>>::type db;
+  typename std::conditional<CONV, ConvDmaA<NT, NDA>, Dma<AK, NT, NDA, CF::BUF>>::type da;
+  typename std::conditional<CONVW, ConvDmaBW<NT, NDB>, Dma<BK, NT, NDB, CF::BUF>>::type db;
   if constexpr (CONV) da.init(A, cg, m0, M, tid);
   else if (AK) da.init(A, lda, m0, M - 1, tid);
   else da.init(A, lda, m0, M - 8, tid);
@@ -541,9 +553,15 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_lds_kernel(const uint16_t* __r
 #pragma unroll
     for (int e = 0; e < 4; ++e) { bv[2 * e] = to_f<T>(w4[e] & 0xffff); bv[2 * e + 1] = to_f<T>(w4[e] >> 16); }
   }
-  float cs[8];
+  // column statistics of the rounded output: colsum (bias gradient / BN sum) and, with colsq,
+  // the sum of squares, both of (o - cshift[n]) when a shift is given (shifted-data variance)
+  float cs[8], cq[8], ks[8];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) cs[e] = 0.f;
+  for (int e = 0; e < 8; ++e) { cs[e] = 0.f; cq[e] = 0.f; ks[e] = 0.f; }
+  if (cshift && ncol_ok) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) ks[e] = cshift[n + e];
+  }
 #pragma unroll
   for (int h = 0; h < BM / 128; ++h) {
     __builtin_amdgcn_s_waitcnt(0xC07F);
@@ -617,27 +635,47 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_lds_kernel(const uint16_t* __r
           // the bias gradient sums the ROUNDED output (what a separate reduction would read)
           const uint32_t w4[4] = {o.x, o.y, o.z, o.w};
 #pragma unroll
-          for (int e = 0; e < 4; ++e) { cs[2 * e] += to_f<T>(w4[e] & 0xffff); cs[2 * e + 1] += to_f<T>(w4[e] >> 16); }
+          for (int e = 0; e < 4; ++e) {
+            const float d0 = to_f<T>(w4[e] & 0xffff) - ks[2 * e], d1 = to_f<T>(w4[e] >> 16) - ks[2 * e + 1];
+            cs[2 * e] += d0;
+            cs[2 * e + 1] += d1;
+            if (colsq) { cq[2 * e] += d0 * d0; cq[2 * e + 1] += d1 * d1; }
+          }
         }
       }
     }
   }
-  if constexpr (TPR == 32) if (colsum) {
-    // threads sharing (tid & 31) own the same 8 columns: lanes l, l^32 then the waves via LDS
+  if (colsum) {
+    // threads with equal tid % TPR own the same 8 columns: reduce over the lanes l, l + TPR, ...
+    // of each wave, then over the waves through LDS (one 8-column group per lane < TPR)
 #pragma unroll
-    for (int e = 0; e < 8; ++e) cs[e] += __shfl_xor(cs[e], 32, 64);
+    for (int o = TPR; o < 64; o <<= 1)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        cs[e] += __shfl_xor(cs[e], o, 64);
+        if (colsq) cq[e] += __shfl_xor(cq[e], o, 64);
+      }
     __syncthreads();
-    if (lane < 32) {
+    if (lane < TPR) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) img[wave * 256 + lane * 8 + e] = cs[e];
+      for (int e = 0; e < 8; ++e) {
+        img[wave * BN + lane * 8 + e] = cs[e];
+        if (colsq) img[(NT / 64 + wave) * BN + lane * 8 + e] = cq[e];
+      }
     }
     __syncthreads();
-    if (tid < 256) {
-      float t = 0.f;
+    for (int t = tid; t < BN; t += NT) {
+      float a = 0.f, q = 0.f;
 #pragma unroll
-      for (int w = 0; w < NT / 64; ++w) t += img[w * 256 + tid];
-      const int nn = n0 + tid;
-      if (nn < N) colsum[(int64_t)tm * N + nn] = t;
+      for (int w = 0; w < NT / 64; ++w) {
+        a += img[w * BN + t];
+        if (colsq) q += img[(NT / 64 + w) * BN + t];
+      }
+      const int nn = n0 + t;
+      if (nn < N) {
+        colsum[(int64_t)tm * N + nn] = a;
+        if (colsq) colsq[(int64_t)tm * N + nn] = q;
+      }
     }
   }
 }

@@ -35,19 +35,17 @@
 // `beta=1` accumulates into C (dW += xᵀ·dy straight into the flat gradient buffer).
 #include "gemm_core.h"
 
-extern "C" int pra_gemm_w4(int layout, const void* A, const void* B, const void* bias, void* C, void* Z,
-                           float* colsum, int M, int N, int K, int lda, int ldb, int ldc, int ldz, int dtype,
-                           int epi, int beta, int splits, float* ws, hipStream_t s);
-extern "C" int pra_gemm_w8i(int layout, const void* A, const void* B, const void* bias, void* C, void* Z,
-                            float* colsum, int M, int N, int K, int lda, int ldb, int ldc, int ldz, int dtype,
-                            int epi, int beta, int splits, float* ws, hipStream_t s);
+extern "C" int pra_gemm_alt(int cfg, int layout, const void* A, const void* B, const void* bias, void* C, void* Z,
+                            float* colsum, int M, int N, int K, int lda, int ldb, int ldc, int ldz, int dtype, int epi,
+                            int beta, int splits, float* ws, hipStream_t s);
 
 namespace pra {
 namespace {
 
-// Which layouts run the 4-wave configuration (bit = 1 << layout) or the 8-wave one with the
-// one-filler-per-MFMA schedule (bit = 16 << layout): PRA_GEMM_W4 at first use, pra_gemm_set_w4
-// afterwards (A/B timing in one process).
+// Which layouts run an alternative configuration of gemm_w4.hip, 4 mask bits per config
+// (bit = 1 << (4 * cfg + layout)): cfg 0 = W4 (4 waves x 128x128), 1 = W8I (8 waves, one filler
+// per MFMA), 2 = W4B (W4 with MUBUF operand DMA), 3 = W8B (W8 with MUBUF operand DMA).
+// PRA_GEMM_W4 at first use, pra_gemm_set_w4 afterwards (A/B timing in one process).
 int g_w4_mask = -1;
 int w4_mask() {
   if (g_w4_mask < 0) {
@@ -66,19 +64,18 @@ void launch_e(const void* A, const void* B, const void* bias, void* C, void* Z, 
   auto pbias = static_cast<const uint16_t*>(bias);
   auto pc = static_cast<uint16_t*>(C);
   auto pz = static_cast<uint16_t*>(Z);
-  // W4 (1 wave/SIMD, 128x128 per wave, gemm_w4.hip) per layout mask; its round-2 measurement
-  // (12-45 % slower) was taken with the accumulators spilled to scratch by the compiler.
-  constexpr bool four = false;
+  // alternative configurations (gemm_w4.hip) per layout mask: W4's round-2 measurement (12-45 %
+  // slower) was taken with the accumulators spilled to scratch by the compiler; round 3
+  // (profiles/r3_gemm): W4 / W8I within +-3 % of W8, hipBLASLt still ahead on dy·Wᵀ.
   static const int ablate = getenv("PRA_GEMM_ABLATE") ? 0 : 1;  // 0: no DMA after the prologue (timing only)
   constexpr int layout = AK ? (BK ? 1 : 0) : 2;
-  const bool w4 = std::is_same<T, bf16>::value && E != kRelu && (w4_mask() >> layout & 1);
-  const bool w8i = !w4 && std::is_same<T, bf16>::value && E != kRelu && (w4_mask() >> (layout + 4) & 1);
+  int alt = -1;
+  if (std::is_same<T, bf16>::value && E != kRelu)
+    for (int c = 0; c < 4 && alt < 0; ++c)
+      if (w4_mask() >> (4 * c + layout) & 1) alt = c;
   if (splits > 1) {
-    if (w4)
-      pra_gemm_w4(layout, A, B, nullptr, nullptr, nullptr, nullptr, M, N, K, lda, ldb, ldc, ldz, kBF16, 0, 0,
-                  splits, ws, s);
-    else if (w8i)
-      pra_gemm_w8i(layout, A, B, nullptr, nullptr, nullptr, nullptr, M, N, K, lda, ldb, ldc, ldz, kBF16, 0, 0,
+    if (alt >= 0)
+      pra_gemm_alt(alt, layout, A, B, nullptr, nullptr, nullptr, nullptr, M, N, K, lda, ldb, ldc, ldz, kBF16, 0, 0,
                    splits, ws, s);
     else
       gemm_lds_kernel<T, W8, AK, BK, kNone, false, true><<<tiles * splits, W8::NT, 0, s>>>(
@@ -96,12 +93,8 @@ void launch_e(const void* A, const void* B, const void* bias, void* C, void* Z, 
 #define PRA_GEMM_LAUNCH(CFG, BETA_)                                                                         \
   gemm_lds_kernel<T, CFG, AK, BK, E, BETA_, false><<<tiles, CFG::NT, 0, s>>>(pa, pb, pbias, pc, pz, colsum, M, N, K, \
                                                                            lda, ldb, ldc, ldz, ablate, nullptr)
-  (void)four;
-  if (w4 && pra_gemm_w4(layout, A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, kBF16, E, beta, 1, nullptr,
-                        s) == 0)
-    return;
-  if (w8i && pra_gemm_w8i(layout, A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, kBF16, E, beta, 1, nullptr,
-                          s) == 0)
+  if (alt >= 0 && pra_gemm_alt(alt, layout, A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, kBF16, E, beta, 1,
+                               nullptr, s) == 0)
     return;
   if (beta) PRA_GEMM_LAUNCH(W8, true); else PRA_GEMM_LAUNCH(W8, false);
 #undef PRA_GEMM_LAUNCH
@@ -135,8 +128,9 @@ int launch_t(int layout, const void* A, const void* B, const void* bias, void* C
 
 template <typename T, typename CF, int E>
 void launch_conv_cfg(const void* xpad, const void* W, const void* bias, void* Y, int M, int N, int K,
-                     const ConvGeom& cg, int splits, float* ws, hipStream_t s) {
-  const int tiles = ((M + CF::BM - 1) / CF::BM) * ((N + CF::BN - 1) / CF::BN);
+                     const ConvGeom& cg, int splits, float* ws, float* part, const float* kshift, hipStream_t s) {
+  const int tiles_m = (M + CF::BM - 1) / CF::BM;
+  const int tiles = tiles_m * ((N + CF::BN - 1) / CF::BN);
   auto px = static_cast<const uint16_t*>(xpad);
   auto pw = static_cast<const uint16_t*>(W);
   auto pb = static_cast<const uint16_t*>(bias);
@@ -148,8 +142,11 @@ void launch_conv_cfg(const void* xpad, const void* W, const void* bias, void* Y,
     splitk_reduce_k<T, E, false><<<(int)((quads + 255) / 256), 256, 0, s>>>(ws, splits, pb, py, nullptr, M, N, N, N);
     return;
   }
+  // part (optional): per-tile-row BatchNorm statistics of the output, [2][tiles_m][N] = sums of
+  // (y - kshift) and (y - kshift)^2 over each tile's rows (kshift: the running mean)
   gemm_lds_kernel<T, CF, true, true, E, false, false, true><<<tiles, CF::NT, 0, s>>>(
-      px, pw, pb, py, nullptr, nullptr, M, N, K, 0, K, N, N, 1, nullptr, cg);
+      px, pw, pb, py, nullptr, part, M, N, K, 0, K, N, N, 1, nullptr, cg,
+      part ? part + (int64_t)tiles_m * N : nullptr, kshift);
 }
 
 // dW [Cout][KH*KW*C] = dy[pix][Cout]ᵀ · im2col(x)[pix][KH*KW*C] (TN, gathered B), split-K over pixels
@@ -174,12 +171,14 @@ void launch_conv_wgrad(const void* dy, const void* x, void* dW, int Mpix, int Co
 
 // tile by output channels: 512x64 for N <= 64, 256x128 for N <= 128, else 256x256 (split-K
 // only there: the narrow tiles serve the large-M early layers)
+inline int conv_tile_rows(int N) { return N <= 64 ? C64::BM : (N <= 128 ? C128::BM : W8::BM); }
+
 template <typename T, int E>
 int launch_conv(const void* xpad, const void* W, const void* bias, void* Y, int M, int N, int K, const ConvGeom& cg,
-                int splits, float* ws, hipStream_t s) {
-  if (N <= 64) launch_conv_cfg<T, C64, E>(xpad, W, bias, Y, M, N, K, cg, 1, nullptr, s);
-  else if (N <= 128) launch_conv_cfg<T, C128, E>(xpad, W, bias, Y, M, N, K, cg, 1, nullptr, s);
-  else launch_conv_cfg<T, W8, E>(xpad, W, bias, Y, M, N, K, cg, splits, ws, s);
+                int splits, float* ws, float* part, const float* kshift, hipStream_t s) {
+  if (N <= 64) launch_conv_cfg<T, C64, E>(xpad, W, bias, Y, M, N, K, cg, 1, nullptr, part, kshift, s);
+  else if (N <= 128) launch_conv_cfg<T, C128, E>(xpad, W, bias, Y, M, N, K, cg, 1, nullptr, part, kshift, s);
+  else launch_conv_cfg<T, W8, E>(xpad, W, bias, Y, M, N, K, cg, part ? 1 : splits, ws, part, kshift, s);
   return 0;
 }
 
@@ -193,9 +192,13 @@ int launch_conv(const void* xpad, const void* W, const void* bias, void* Y, int 
 // out-of-image sentinel above every valid one).
 // splits > 1 (Cout > 128 only): split-K through the fp32 workspace ws [splits][M][Cout]
 // (pra_conv_lds_splits gives the factor).
+// part / kshift (optional, no split-K): BatchNorm statistics of Y per tile row,
+// part [2][pra_conv_lds_stat_rows(M, Cout)][Cout] (see launch_conv_cfg).
+extern "C" int pra_conv_lds_stat_rows(int M, int Cout) { return (M + pra::conv_tile_rows(Cout) - 1) / pra::conv_tile_rows(Cout); }
+
 extern "C" int pra_conv_lds(const void* x, const void* W, const void* bias, void* Y, int Nimg, int H, int Wd,
                             int C, int Cout, int KH, int KW, int S, int P, int relu, int dtype, int splits, float* ws,
-                            hipStream_t s) {
+                            float* part, const float* kshift, hipStream_t s) {
   if (C % 64 || Cout % 8 || KH <= 0 || KW <= 0 || S <= 0 || P < 0 || H <= 0 || Wd <= 0) return -1;
   if (H >= 32768 || Wd >= 32768 || (long long)Nimg * H * Wd * C * 2 >= (1ll << 31)) return -1;
   const int Ho = (H + 2 * P - KH) / S + 1, Wo = (Wd + 2 * P - KW) / S + 1;
@@ -205,10 +208,10 @@ extern "C" int pra_conv_lds(const void* x, const void* W, const void* bias, void
   const int M = (int)Mll, K = KH * KW * C;
   if (splits > 1 && (Cout <= 128 || !ws)) return -1;
   pra::ConvGeom cg{Ho, Wo, H, Wd, C, KW, S, P};
-  if (dtype == pra::kBF16) return relu ? pra::launch_conv<pra::bf16, pra::kRelu>(x, W, bias, Y, M, Cout, K, cg, splits, ws, s)
-                                  : pra::launch_conv<pra::bf16, pra::kNone>(x, W, bias, Y, M, Cout, K, cg, splits, ws, s);
-  if (dtype == pra::kF16) return relu ? pra::launch_conv<pra::f16, pra::kRelu>(x, W, bias, Y, M, Cout, K, cg, splits, ws, s)
-                                 : pra::launch_conv<pra::f16, pra::kNone>(x, W, bias, Y, M, Cout, K, cg, splits, ws, s);
+  if (dtype == pra::kBF16) return relu ? pra::launch_conv<pra::bf16, pra::kRelu>(x, W, bias, Y, M, Cout, K, cg, splits, ws, part, kshift, s)
+                                  : pra::launch_conv<pra::bf16, pra::kNone>(x, W, bias, Y, M, Cout, K, cg, splits, ws, part, kshift, s);
+  if (dtype == pra::kF16) return relu ? pra::launch_conv<pra::f16, pra::kRelu>(x, W, bias, Y, M, Cout, K, cg, splits, ws, part, kshift, s)
+                                 : pra::launch_conv<pra::f16, pra::kNone>(x, W, bias, Y, M, Cout, K, cg, splits, ws, part, kshift, s);
   return -1;
 }
 

@@ -48,6 +48,8 @@ int launch_w4_l(const void* A, const void* B, const void* bias, void* C, void* Z
 }
 
 using W8I = WCfg<2, 4, 256, 256, true>;
+using W4B = WCfg<2, 2, 256, 256, true, true>;   // W4 with MUBUF operand DMA
+using W8B = WCfg<2, 4, 256, 256, false, true>;  // W8 (burst schedule) with MUBUF operand DMA
 
 template <typename CF>
 int launch_alt(int layout, const void* A, const void* B, const void* bias, void* C, void* Z, float* colsum, int M,
@@ -79,4 +81,17 @@ extern "C" int pra_gemm_w8i(int layout, const void* A, const void* B, const void
                             int splits, float* ws, hipStream_t s) {
   return pra::launch_alt<pra::W8I>(layout, A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, dtype, epi, beta,
                                    splits, ws, s);
+}
+
+// cfg: 0 = W4, 1 = W8I, 2 = W4B, 3 = W8B
+extern "C" int pra_gemm_alt(int cfg, int layout, const void* A, const void* B, const void* bias, void* C, void* Z,
+                            float* colsum, int M, int N, int K, int lda, int ldb, int ldc, int ldz, int dtype, int epi,
+                            int beta, int splits, float* ws, hipStream_t s) {
+  switch (cfg) {
+    case 0: return pra::launch_alt<pra::W4>(layout, A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, dtype, epi, beta, splits, ws, s);
+    case 1: return pra::launch_alt<pra::W8I>(layout, A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, dtype, epi, beta, splits, ws, s);
+    case 2: return pra::launch_alt<pra::W4B>(layout, A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, dtype, epi, beta, splits, ws, s);
+    case 3: return pra::launch_alt<pra::W8B>(layout, A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, dtype, epi, beta, splits, ws, s);
+    default: return -1;
+  }
 }

@@ -1016,6 +1016,9 @@ def _fa_next_rng(seed=None, numel=1):
     return seed, off
 
 
+_FA_DROP_BITS = __import__('os').environ.get('PRA_FA_DROP_BITS', '1') == '1'
+
+
 class FlashAttnExtFn(torch.autograd.Function):
     """Flash attention with an additive mask and/or in-kernel dropout, dense [B, S, H, D] or
     varlen packed [total, H, D] (cu_q / cu_k int32 [B+1]): one HIP forward, the dS^T backward."""
@@ -1039,13 +1042,14 @@ class FlashAttnExtFn(torch.autograd.Function):
         lse = torch.empty((B, H, Sq), device=q.device, dtype=torch.float32)
         mk, msb, msh, msq, m32 = (None, 0, 0, 0, False) if mask is None else \
             _mask_strides(mask, B, H, Sq, Sk)
-        # dropout keep bits for the backward (1 bit per score: B*H*Sq*Sk/8 bytes)
+        # dropout keep bits for the backward (1 bit per score: B*H*Sq*Sk/8 bytes); without them
+        # (PRA_FA_DROP_BITS=0) the dK/dV kernel regenerates the hash
         dbits = torch.empty(B * H * Sq * (-(-Sk // 32)), device=q.device, dtype=torch.int32) \
-            if p_drop > 0 else torch.empty(0, device=q.device, dtype=torch.int32)
+            if p_drop > 0 and _FA_DROP_BITS else torch.empty(0, device=q.device, dtype=torch.int32)
         L.flash_fwd_ext(_ptr(q), _ptr(k), _ptr(v), _ptr(o), _ptr(lse), B, H, Sq, Sk, D, st, float(scale),
                         int(causal), _dt(q), _ptr(cu_q) if varlen else 0, _ptr(cu_k) if varlen else 0,
                         _ptr(mk) if mk is not None else 0, msb, msh, msq, int(m32), float(p_drop),
-                        int(seed), int(offset), _ptr(dbits) if p_drop > 0 else 0, _stream())
+                        int(seed), int(offset), _ptr(dbits) if dbits.numel() else 0, _stream())
         ctx.save_for_backward(q, k, v, o, lse, mk if mk is not None else torch.empty(0), cu_q if varlen else
                               torch.empty(0), cu_k if varlen else torch.empty(0), dbits)
         ctx.meta = (varlen, B, H, D, Sq, Sk, st, causal, scale, p_drop, seed, offset,
@@ -1433,9 +1437,11 @@ def conv_kxk_supported(x, w, stride, padding):
             and x.numel() * 2 < 2 ** 31 and max(x.shape[1], x.shape[2]) < 32768)
 
 
-def _conv_lds(x, wk, bias, kh, kw, stride, pad, relu=False):
+def _conv_lds(x, wk, bias, kh, kw, stride, pad, relu=False, stats_shift=None):
     """y[N,Ho,Wo,Cout] = conv(x NHWC, wk [Cout, kh*kw*C] (OHWI)) via the implicit-GEMM kernel
-    (zero padding applied by the kernel's DMA range check, the input is read in place)."""
+    (zero padding applied by the kernel's DMA range check, the input is read in place).
+    stats_shift (fp32 [Cout], e.g. the BN running mean): the epilogue also returns the per-tile
+    BatchNorm partial sums part [2, rows, Cout] of (y - shift) and (y - shift)^2."""
     n, h, wd, c = x.shape
     cout = wk.shape[0]
     x = x.contiguous()
@@ -1445,11 +1451,16 @@ def _conv_lds(x, wk, bias, kh, kw, stride, pad, relu=False):
         bias = bias.to(x.dtype).contiguous()
     L = _native.lib()
     m = n * ho * wo
-    splits = L.conv_lds_splits(m, cout, kh * kw * c)
+    part = None
+    if stats_shift is not None:
+        splits = 1
+        part = torch.empty((2, L.conv_lds_stat_rows(m, cout), cout), device=x.device, dtype=torch.float32)
+    else:
+        splits = L.conv_lds_splits(m, cout, kh * kw * c)
     ws = torch.empty((splits, m, cout), device=x.device, dtype=torch.float32) if splits > 1 else None
     L.conv_lds(x.data_ptr(), wk.data_ptr(), _ptr(bias), y.data_ptr(), n, h, wd, c, cout, kh, kw,
-               stride, pad, int(relu), _dt(x), splits, _ptr(ws), _stream())
-    return y
+               stride, pad, int(relu), _dt(x), splits, _ptr(ws), _ptr(part), _ptr(stats_shift), _stream())
+    return y if stats_shift is None else (y, part)
 
 
 def _conv_wgrad_ok(x, dy, cout):
@@ -1524,6 +1535,60 @@ class ConvKxKFn(torch.autograd.Function):
         if hb and ctx.needs_input_grad[2]:
             db = dy.reshape(-1, cout).sum(0, dtype=torch.float32).to(dy.dtype)
         return dx, dw, db, None, None
+
+
+class ConvKxKStatsFn(ConvKxKFn):
+    """ConvKxKFn whose forward also returns the BatchNorm partial statistics of its output
+    (the implicit-GEMM epilogue's column sums around ``shift``; non-differentiable)."""
+
+    @staticmethod
+    def forward(ctx, x, w, bias, stride, pad, shift):
+        cout, cin, kh, kw = w.shape
+        x = x.contiguous()
+        wk = w.permute(0, 2, 3, 1).reshape(cout, kh * kw * cin).contiguous()
+        y, part = _conv_lds(x, wk, bias, kh, kw, stride, pad, stats_shift=shift)
+        ctx.save_for_backward(x, w)
+        ctx.meta = (stride, pad, bias is not None)
+        ctx.mark_non_differentiable(part)
+        return y, part
+
+    @staticmethod
+    def backward(ctx, dy, dpart):
+        return ConvKxKFn.backward(ctx, dy) + (None,)
+
+
+def conv_bn_act_nhwc(x, w, stride, padding, bn_w, bn_b, rmean, rvar, training, momentum=0.9,
+                     eps=1e-5, z=None, relu=True):
+    """act(BN(conv(x)) [+ z]) for channels-last KxK convolutions with the BatchNorm statistics
+    taken in the convolution's epilogue (parity: the reference's fused conv + BN-statistics
+    kernels, fluid/operators/fused/cudnn_norm_conv.cu.h / resnet_unit_op.cu): the separate
+    statistics pass over the conv output disappears; finalize + apply (+ residual + ReLU
+    keep-bits) run as in ``batch_norm_act``. Falls back to conv + batch_norm_act when the
+    shape is outside the kernel or statistics are not needed (eval)."""
+    if conv_bn_stats_ok(x, w, stride, padding, rmean, training):
+        y, part = ConvKxKStatsFn.apply(x, w, None, int(stride), int(padding), rmean)
+        return BatchNormActFn.apply(y, z, bn_w, bn_b, rmean, rvar, training, momentum, eps, relu,
+                                    _join_for(z) if z is not None else None, (part, rmean))
+    if w.shape[2] == w.shape[3] > 1 and conv_kxk_supported(x, w, stride, padding):
+        y = conv_kxk_nhwc(x, w, None, stride, padding)
+    elif w.shape[2:] == (1, 1) and padding == 0 and x.is_cuda and x.dtype in _HALF:
+        y = conv1x1_nhwc(x, w, None, (stride, stride))
+    else:
+        y = torch.nn.functional.conv2d(x.permute(0, 3, 1, 2), w, None, stride, padding).permute(0, 2, 3, 1)
+    return batch_norm_act(y, z, bn_w, bn_b, rmean, rvar, training, momentum, eps, relu)
+
+
+_CONV_BN_STATS = __import__('os').environ.get('PRA_CONV_BN_STATS', '1') == '1'
+
+
+def conv_bn_stats_ok(x, w, stride, padding, rmean, training):
+    """Whether conv_bn_act_nhwc takes the statistics-in-epilogue path (checked on the host
+    before any launch: the implicit-GEMM conv's shape contract, fp32 running mean, HIP BN).
+    PRA_CONV_BN_STATS=0 turns it off (separate statistics pass, for A/B timing)."""
+    return bool(_CONV_BN_STATS and training and rmean is not None and rmean.dtype == torch.float32 and rmean.is_contiguous()
+                and rmean.numel() == w.shape[0] and w.shape[2] == w.shape[3] > 1
+                and conv_kxk_supported(x, w, stride, padding)
+                and R.select_backend(x, 'batch_norm_fwd') == 'hip' and w.shape[0] % 8 == 0)
 
 
 def conv_kxk_nhwc(x, w, bias=None, stride=1, padding=0):
@@ -1954,6 +2019,23 @@ def _bn_fwd_hip(x2, z2, w, b, rmean, rvar, training, momentum, eps, relu):
     return y, mean, torch.rsqrt(rvar.float() + eps), None
 
 
+def _bn_fwd_parts_hip(x2, z2, w, b, rmean, rvar, momentum, eps, relu, part, kshift):
+    """Training BN forward from the per-tile partial sums a convolution epilogue produced
+    (part [2, rows, C] around kshift): finalize + apply kernels only."""
+    _check_dtypes('batch_norm', (x2, z2), (w, b))
+    L = _native.lib()
+    M, C = x2.shape
+    y = torch.empty_like(x2)
+    stat = torch.empty((4, C), device=x2.device, dtype=torch.float32)  # mean | invstd | scale | shift
+    mask = torch.empty(M * C // 8, device=x2.device, dtype=torch.uint8) if relu else None
+    z2 = z2.contiguous() if z2 is not None else None
+    L.bn_fwd_parts(_ptr(x2), _ptr(z2), _ptr(w), _ptr(b), _ptr(rmean), _ptr(rvar), _ptr(y), _ptr(mask),
+                   _ptr(stat[0]), _ptr(stat[1]), _ptr(part), _ptr(kshift), _ptr(stat[2]), M, C,
+                   part.shape[1], float(eps), float(momentum), int(relu), _dt(x2),
+                   _dt(w) if w is not None else 0, _stream())
+    return y, stat[0], stat[1], mask
+
+
 @R.register_kernel('batch_norm_bwd', 'hip', dtypes=_FLOATS)
 def _bn_bwd_hip(dy, y, mask, x2, w, mean, invstd, relu, need_dz, acc=None):
     """acc = (w.grad, b.grad): the scale / shift gradients are added into these in the
@@ -1989,7 +2071,7 @@ class BatchNormActFn(torch.autograd.Function):
     """y = act(BN(x) + z) over channels-last x[..., C]; running stats updated in place."""
 
     @staticmethod
-    def forward(ctx, x, z, w, b, rmean, rvar, training, momentum, eps, relu, join=None):
+    def forward(ctx, x, z, w, b, rmean, rvar, training, momentum, eps, relu, join=None, stats=None):
         ctx.join = join
         shp = x.shape
         C = shp[-1]
@@ -1997,8 +2079,13 @@ class BatchNormActFn(torch.autograd.Function):
         z2 = _like(z, x.dtype).reshape(-1, C) if z is not None else None
         if w is not None:
             b = _like(b, w.dtype)
-        y, mean, invstd, mask = R.dispatch('batch_norm_fwd', x2, x2, z2, w, b, rmean, rvar,
-                                           training, momentum, eps, relu)
+        if stats is not None and training:
+            # statistics already taken by the producing convolution's epilogue
+            y, mean, invstd, mask = _bn_fwd_parts_hip(x2, z2, w, b, rmean, rvar, momentum, eps, relu,
+                                                      *stats)
+        else:
+            y, mean, invstd, mask = R.dispatch('batch_norm_fwd', x2, x2, z2, w, b, rmean, rvar,
+                                               training, momentum, eps, relu)
         # ReLU backward needs only the keep-bits (1 B per 8 channels) when the kernel wrote them
         ctx.save_for_backward(x2, y if (relu and mask is None) else None, mask, w, mean, invstd)
         ctx.relu, ctx.shp, ctx.has_z = relu, shp, z is not None
@@ -2020,7 +2107,8 @@ class BatchNormActFn(torch.autograd.Function):
             if dz is not None and ctx.join is not None:
                 dz = ctx.join.add_tensor(dz, owned=True)
             return ((g * a).to(x2.dtype).view(ctx.shp), dz, dw if w is not None else None,
-                    g.sum(0).to(pdt) if ctx.has_b else None, None, None, None, None, None, None, None)
+                    g.sum(0).to(pdt) if ctx.has_b else None, None, None, None, None, None, None, None,
+                    None)
         acc = None
         b = ctx.b
         if (x2.is_cuda and w is not None and b is not None and ctx.needs_input_grad[2]
@@ -2040,7 +2128,7 @@ class BatchNormActFn(torch.autograd.Function):
         return (dx.view(ctx.shp), dz,
                 dw if (w is not None and ctx.needs_input_grad[2]) else None,
                 db if (ctx.has_b and ctx.needs_input_grad[3]) else None,
-                None, None, None, None, None, None, None)
+                None, None, None, None, None, None, None, None)
 
 
 def batch_norm_act(x, z, w, b, rmean, rvar, training, momentum=0.9, eps=1e-5, relu=False):

@@ -21,6 +21,30 @@ def _bn_act(bn, x, z=None, act='relu'):
                               act, bn._data_format)
 
 
+def _conv_bn_act(conv, bn, x, z=None, act='relu'):
+    """act(bn(conv(x)) + z); for a channels-last KxK convolution in training mode the BatchNorm
+    statistics come from the convolution's epilogue (ops.fused.conv_bn_act_nhwc), so the
+    separate statistics pass over the conv output is skipped."""
+    import torch
+    from ...framework.core import Tensor, _u
+    from ...ops import fused as K
+    xt = _u(x)
+    st, pd, dl = conv._stride, conv._padding, conv._dilation
+    st = st if isinstance(st, int) else (st[0] if len(set(st)) == 1 else None)
+    pd = pd if isinstance(pd, int) else (pd[0] if not isinstance(pd, str) and len(set(pd)) == 1 else None)
+    dl = dl if isinstance(dl, int) else (dl[0] if len(set(dl)) == 1 else None)
+    if (conv._data_format == 'NHWC' and conv._groups == 1 and conv.bias is None and dl == 1
+            and st is not None and pd is not None and isinstance(bn, nn.layer.norm._BatchNormBase)
+            and not isinstance(bn, nn.SyncBatchNorm) and bn.training and not bn._use_global_stats
+            and xt.is_cuda and xt.dtype == _u(conv.weight).dtype and xt.dtype in (torch.bfloat16, torch.float16)
+            and act in ('relu', None)):
+        y = K.conv_bn_act_nhwc(xt, _u(conv.weight), st, pd, _u(bn.weight), _u(bn.bias), _u(bn._mean),
+                               _u(bn._variance), True, bn._momentum, bn._epsilon,
+                               _u(z) if z is not None else None, act == 'relu')
+        return Tensor(y)
+    return _bn_act(bn, conv(x), z, act)
+
+
 class BasicBlock(nn.Layer):
     expansion = 1
 
@@ -40,10 +64,10 @@ class BasicBlock(nn.Layer):
 
     def forward(self, x):
         identity = x
-        out = _bn_act(self.bn1, self.conv1(x))
+        out = _conv_bn_act(self.conv1, self.bn1, x)
         if self.downsample is not None:
             identity = self.downsample(x)
-        return _bn_act(self.bn2, self.conv2(out), identity)
+        return _conv_bn_act(self.conv2, self.bn2, out, identity)
 
 
 class BottleneckBlock(nn.Layer):
@@ -72,7 +96,7 @@ class BottleneckBlock(nn.Layer):
         with _grad_join(x._t):
             identity = x
             out = _bn_act(self.bn1, self.conv1(x))
-            out = _bn_act(self.bn2, self.conv2(out))
+            out = _conv_bn_act(self.conv2, self.bn2, out)
             if self.downsample is not None:
                 identity = self.downsample(x)
             return _bn_act(self.bn3, self.conv3(out), identity)
