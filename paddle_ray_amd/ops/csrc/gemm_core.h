@@ -93,10 +93,13 @@ constexpr int BM = 256, BN = 256, BKT = 64;  // the GEMM tile (conv configs belo
 //       segment instead of a burst between MFMA groups (one wave per SIMD has no partner wave
 //       to cover a burst)
 //   BUF: operand DMA as MUBUF buffer_load ... lds instead of global_load_lds
-template <int WR_, int WC_, int BM_ = 256, int BN_ = 256, bool ILV_ = false, bool BUF_ = false>
+//   PIPE: two barriers per K-step and the refill DMA issued in half 0 (see kstep_p): every DMA
+//       has at least two k-halves of lead instead of one
+template <int WR_, int WC_, int BM_ = 256, int BN_ = 256, bool ILV_ = false, bool BUF_ = false,
+          bool PIPE_ = false>
 struct WCfg {
   static constexpr int WR = WR_, WC = WC_, NT = 64 * WR_ * WC_, BM = BM_, BN = BN_;
-  static constexpr bool ILV = ILV_, BUF = BUF_;
+  static constexpr bool ILV = ILV_, BUF = BUF_, PIPE = PIPE_;
   static constexpr int TI = BM_ / WR_ / 16, TJ = BN_ / WC_ / 16;  // 16x16 MFMA tiles per wave
   static constexpr int IMGA = BM_ * BKT * 2, IMGB = BN_ * BKT * 2, SLOT = IMGA + IMGB;
   static constexpr int NDA = IMGA / (NT * 16), NDB = IMGB / (NT * 16);  // glds per thread per K-step
@@ -501,6 +504,77 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_lds_kernel(const uint16_t* __r
     // the next half-0 drain + barrier), so the next half starts on its first fragments.
     if constexpr (!STEADY) __builtin_amdgcn_s_waitcnt(0xC07F);
   };
+  // PIPE schedule, K-step kt (slot kt&1):
+  //   half 0: MFMAs of (kt,0) from F0; fillers = the reads of (kt,1) into F1, then lgkmcnt(0) +
+  //           barrier A (every wave is done with slot kt), then the DMA refilling slot kt with
+  //           step kt+2, one piece every other MFMA;
+  //   vmcnt(pieces just issued) + barrier B: step kt+1 has landed for every wave;
+  //   half 1: MFMAs of (kt,1) from F1; fillers = the reads of (kt+1,0) into F0.
+  // A refill piece is consumed at half 1 of step kt+1: >= 2 k-halves after its issue.
+  auto kstep_p = [&](int kt, auto steady_c) __attribute__((always_inline)) {
+    constexpr bool STEADY = decltype(steady_c)::value;
+    constexpr int NRD = TI + TJ, NDMA = NDA + NDB;
+    static_assert(NRD + 1 + 2 * NDMA <= TI * TJ + 1, "PIPE: fillers exceed the half's MFMAs");
+    const bool dma = STEADY || (kt + 2 < nk && dmaon);
+    const bool rd1 = STEADY || kt + 1 < nk;
+    {
+      const char* ai = lds + (kt & 1) * SLOT;
+      const char* bi = ai + IMGA;
+      const uint32_t soA = lds_base + (kt & 1) * SLOT, soB = soA + IMGA;
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) {
+          if constexpr (AGPR_ACC) mma_agpr<T>(fb0[j], fa0[i], acc[i][j]);
+          else acc[i][j] = mma<T>(fb0[j], fa0[i], acc[i][j]);
+          __builtin_amdgcn_sched_barrier(0);
+          const int f = i * TJ + j;
+          if (f < TJ) {
+            fb1[f] = frag<T, BK>(bi, wc * CW + f * 16, 1, lane);
+          } else if (f < NRD) {
+            fa1[f - TJ] = frag<T, AK>(ai, wr * RW + (f - TJ) * 16, 1, lane);
+          } else if (f == NRD) {
+            __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's reads of slot kt done
+            __builtin_amdgcn_s_barrier();        // barrier A: every wave's
+          } else if (dma && ((f - NRD - 1) & 1) == 0 && (f - NRD - 1) / 2 < NDMA) {
+            const int d = (f - NRD - 1) / 2;
+            if (d < NDA) da.issue1(soA, wave, kt + 2, d);
+            else db.issue1(soB, wave, kt + 2, d - NDA);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    if (dma) wait_vmcnt<NDA + NDB>();  // step kt+1's pieces landed (kt+2's may be in flight)
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // barrier B: step kt+1 landed for every wave
+    __builtin_amdgcn_sched_barrier(0);
+    {
+      const char* ai = lds + ((kt + 1) & 1) * SLOT;
+      const char* bi = ai + IMGA;
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) {
+          if constexpr (AGPR_ACC) mma_agpr<T>(fb1[j], fa1[i], acc[i][j]);
+          else acc[i][j] = mma<T>(fb1[j], fa1[i], acc[i][j]);
+          __builtin_amdgcn_sched_barrier(0);
+          const int f = i * TJ + j;
+          if (rd1 && (f & 1) == 0 && f / 2 < NRD) {
+            const int r = f / 2;
+            if (r < TJ) fb0[r] = frag<T, BK>(bi, wc * CW + r * 16, 0, lane);
+            else fa0[r - TJ] = frag<T, AK>(ai, wr * RW + (r - TJ) * 16, 0, lane);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    if constexpr (!STEADY) __builtin_amdgcn_s_waitcnt(0xC07F);
+  };
+  if constexpr (CF::PIPE) {
+    int kt = 0;
+    if (dmaon)
+      for (; kt + 2 < nk; ++kt) kstep_p(kt, std::true_type{});
+    for (; kt < nk; ++kt) kstep_p(kt, std::false_type{});
+  } else {
   int kt = 0;
   // (the implicit-GEMM convolutions keep the generic body: their gather state already sits at
   // the register limit and a second body copy made them spill)
@@ -508,6 +582,7 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_lds_kernel(const uint16_t* __r
     if (dmaon)
       for (; kt + 2 < nk; ++kt) kstep(kt, std::true_type{});
   for (; kt < nk; ++kt) kstep(kt, std::false_type{});
+  }  // !PIPE
   }  // nk > 0
 
   // last asm MFMA -> v_accvgpr_read of its result: the hazard recognizer cannot see the asm

@@ -44,7 +44,8 @@ namespace {
 
 // Which layouts run an alternative configuration of gemm_w4.hip, 4 mask bits per config
 // (bit = 1 << (4 * cfg + layout)): cfg 0 = W4 (4 waves x 128x128), 1 = W8I (8 waves, one filler
-// per MFMA), 2 = W4B (W4 with MUBUF operand DMA), 3 = W8B (W8 with MUBUF operand DMA).
+// per MFMA), 2 = W4B (W4 with MUBUF operand DMA), 3 = W8B (W8 with MUBUF operand DMA),
+// 4 = W4P / 5 = W8P (two barriers per K-step, refill DMA issued in half 0).
 // PRA_GEMM_W4 at first use, pra_gemm_set_w4 afterwards (A/B timing in one process).
 int g_w4_mask = -1;
 int w4_mask() {
@@ -71,7 +72,7 @@ void launch_e(const void* A, const void* B, const void* bias, void* C, void* Z, 
   constexpr int layout = AK ? (BK ? 1 : 0) : 2;
   int alt = -1;
   if (std::is_same<T, bf16>::value && E != kRelu)
-    for (int c = 0; c < 4 && alt < 0; ++c)
+    for (int c = 0; c < 6 && alt < 0; ++c)
       if (w4_mask() >> (4 * c + layout) & 1) alt = c;
   if (splits > 1) {
     if (alt >= 0)

@@ -1016,7 +1016,7 @@ def _fa_next_rng(seed=None, numel=1):
     return seed, off
 
 
-_FA_DROP_BITS = __import__('os').environ.get('PRA_FA_DROP_BITS', '1') == '1'
+_FA_DROP_BITS = __import__('os').environ.get('PRA_FA_DROP_BITS', '0') == '1'
 
 
 class FlashAttnExtFn(torch.autograd.Function):
@@ -1042,8 +1042,9 @@ class FlashAttnExtFn(torch.autograd.Function):
         lse = torch.empty((B, H, Sq), device=q.device, dtype=torch.float32)
         mk, msb, msh, msq, m32 = (None, 0, 0, 0, False) if mask is None else \
             _mask_strides(mask, B, H, Sq, Sk)
-        # dropout keep bits for the backward (1 bit per score: B*H*Sq*Sk/8 bytes); without them
-        # (PRA_FA_DROP_BITS=0) the dK/dV kernel regenerates the hash
+        # dropout keep bits for the backward (1 bit per score: B*H*Sq*Sk/8 bytes, PRA_FA_DROP_BITS=1);
+        # by default the dK/dV kernel regenerates the hash instead (BERT-base: 1188 vs 1174 seq/s
+        # with the stored bits, profiles/r3_bert)
         dbits = torch.empty(B * H * Sq * (-(-Sk // 32)), device=q.device, dtype=torch.int32) \
             if p_drop > 0 and _FA_DROP_BITS else torch.empty(0, device=q.device, dtype=torch.int32)
         L.flash_fwd_ext(_ptr(q), _ptr(k), _ptr(v), _ptr(o), _ptr(lse), B, H, Sq, Sk, D, st, float(scale),
@@ -1216,13 +1217,12 @@ def _gemm_hip(layout, a, b, out=None, bias=None, z=None, epi=None, beta=0, want_
         K, M = a.shape
         N = b.shape[1]
     if _GEMM_MODE == 'auto' and _GEMM_SHAPE_POLICY and epi is None and not want_colsum:
-        # per-shape policy from the measured table (profiles/r2_gemm/summary.md): hipBLASLt wins
-        # the long-K plain forward (fc2 x·W K=8192: 0.95x, LM-head dgrad K=50304: 0.94x) and
-        # the mid-size split-K wgrad (qkv 2048x6144: 0.91x, 192 tiles -> 4-way split)
-        tiles = ((M + 255) // 256) * ((N + 255) // 256)
-        if layout == GEMM_FWD and (K >= 4096 or M < 128):
-            return None  # long-K forward, and skinny decode-time GEMMs (256-row tiles idle)
-        if layout == GEMM_TN and 128 <= tiles < 224:
+        # per-shape policy from the measured table (profiles/r3_gemm/gemm_configs.log): the
+        # in-tree kernel is at parity or ahead on the long-K forward (fc2 x·W K=8192: 407-409
+        # vs 410 us; LM-head dgrad K=50304: 2435-2444 vs 2458 us) and within 2-4 % on the
+        # mid-size split-K wgrad (qkv 2048x6144: 381-388 vs 374 us), so those stay in-tree;
+        # skinny decode-time forwards (M < 128: a 256-row tile idles) go to the library
+        if layout == GEMM_FWD and M < 128:
             return None
     if out is None:
         out = torch.empty((M, N), device=a.device, dtype=a.dtype)

@@ -58,9 +58,13 @@ def _fp32_grads(fn, tensors, g):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize('bits', [False, True], ids=['rehash', 'keep_bits'])
 @pytest.mark.parametrize('causal', [False, True])
 @pytest.mark.parametrize('D', [64, 128])
-def test_flash_dropout_matches_reference_with_same_mask(causal, D):
+def test_flash_dropout_matches_reference_with_same_mask(causal, D, bits, monkeypatch):
+    """Both backward modes: the dK/dV kernel regenerating the hash (default) and reading the
+    keep bits the forward stored (PRA_FA_DROP_BITS=1)."""
+    monkeypatch.setattr(K, '_FA_DROP_BITS', bits)
     torch.manual_seed(1)
     dev = torch.device('cuda')
     B, S, H = 2, 320, 3

@@ -11,11 +11,13 @@ from paddle_ray_amd.ops import registry as R
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(autouse=True, params=[0, 7, 7 << 4, 7 << 8, 7 << 12], ids=['W8', 'W4', 'W8I', 'W4B', 'W8B'])
+@pytest.fixture(autouse=True, params=[0, 7, 7 << 4, 7 << 8, 7 << 12, 7 << 16, 7 << 20],
+                ids=['W8', 'W4', 'W8I', 'W4B', 'W8B', 'W4P', 'W8P'])
 def _mfma_everywhere(request):
     """Exercise the in-tree kernel on every layout regardless of the 'auto' policy, in each
     wave configuration (gemm_set_w4 mask: 0 = 8 waves, 7 = 4 waves x 128x128, 7<<4 = 8 waves
-    with the one-filler-per-MFMA schedule, 7<<8 / 7<<12 = W4 / W8 with MUBUF operand DMA)."""
+    with the one-filler-per-MFMA schedule, 7<<8 / 7<<12 = W4 / W8 with MUBUF operand DMA,
+    7<<16 / 7<<20 = W4 / W8 with the two-barrier early-refill schedule)."""
     from paddle_ray_amd.ops import _native
     L = _native.lib()
     prev, prev_mask = K._GEMM_MODE, L.gemm_get_w4()
