@@ -147,9 +147,8 @@ class BertSelfAttention(nn.Layer):
             o = K.flash_attention_qkvpacked(qkv, causal=False)
         else:
             # padded batches (additive mask) / attention dropout: the flash kernel's extended path
-            q, k, v = qkv.unbind(2)
             m = None if attn_mask is None else _u(attn_mask)
-            o = K.flash_attention_ext(q, k, v, causal=False, attn_mask=m, dropout=drop)
+            o = K.flash_attention_ext_qkvpacked(qkv, causal=False, attn_mask=m, dropout=drop)
         return o.reshape(B, S, self.num_heads * self.head_dim)
 
     def forward(self, x, attn_mask=None):

@@ -44,18 +44,19 @@ void pra_sumsq_accum(const void*, float*, int64_t, int, hipStream_t);
 void pra_flash_bwd_pre(const void*, const void*, float*, int, int, int, int, int, hipStream_t);
 int pra_adl_supported(int);
 void pra_adl_fwd(const void*, const void*, const void*, const void*, const void*, void*, void*, float*, float*, int,
-                 int, float, float, uint64_t, uint64_t, int, int, hipStream_t);
+                 int, float, float, uint64_t, uint64_t, const uint64_t*, int, int, hipStream_t);
 void pra_adl_bwd(const void*, const void*, const void*, const void*, const float*, const float*, void*, void*, float*,
-                 float*, float*, int, int, int, float, uint64_t, uint64_t, int, int, hipStream_t);
+                 float*, float*, int, int, int, float, uint64_t, uint64_t, const uint64_t*, int, int, hipStream_t);
 void pra_colsum16(const float*, void*, int, int, int, int, hipStream_t);
 int pra_flash_fwd(const void*, const void*, const void*, void*, float*, int, int, int, int, int, const int64_t*, float,
                   int, int, hipStream_t);
 int pra_flash_fwd_ext(const void*, const void*, const void*, void*, float*, int, int, int, int, int, const int64_t*,
                       float, int, int, const int*, const int*, const void*, int64_t, int64_t, int64_t, int, float,
-                      uint64_t, uint64_t, uint32_t*, hipStream_t);
+                      uint64_t, uint64_t, uint32_t*, const uint64_t*, hipStream_t);
 int pra_flash_bwd_ext(const void*, const void*, const void*, const void*, const float*, const float*, void*, void*,
                       void*, void*, int, int, int, int, int, const int64_t*, float, int, int, const int*, const int*,
-                      const void*, int64_t, int64_t, int64_t, int, float, uint64_t, uint64_t, uint32_t*, hipStream_t);
+                      const void*, int64_t, int64_t, int64_t, int, float, uint64_t, uint64_t, uint32_t*, const uint64_t*,
+                      hipStream_t);
 int pra_flash_bwd(const void*, const void*, const void*, const void*, const void*, const float*, float*, void*, void*,
                   void*, void*, int, int, int, int, int, const int64_t*, float, int, int, hipStream_t);
 int pra_embedding_fwd(const int64_t*, const void*, void*, int64_t, int, int64_t, int64_t, int, hipStream_t);
@@ -198,6 +199,14 @@ PYBIND11_MODULE(_pra_hip, m) {
     check_launch("vp_ce_bwd");
   });
   m.def("build_info", []() { return std::string(pra_build_info()); });
+  // id of the stream capture in progress on s (0 when s is not capturing): the graph-safe dropout
+  // RNG advances its device step counter once per capture (ops/fused.py _graph_seq)
+  m.def("capture_id", [](P s) -> unsigned long long {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    unsigned long long id = 0;
+    if (hipStreamGetCaptureInfo(S(s), &st, &id) != hipSuccess || st != hipStreamCaptureStatusActive) return 0ull;
+    return id;
+  });
   m.def("mmha_splits", [](int B, int H, int t) { return pra_mmha_splits(B, H, t); });
   m.def("mmha_decode", [](P qkv, P cache, P mask, P ws, P out, int B, int H, int L, int D, int t, P t_dev,
                           int splits, int mask_len, float scale, int dt, P s) {
@@ -230,15 +239,15 @@ PYBIND11_MODULE(_pra_hip, m) {
   });
   m.def("adl_supported", [](int cols) { return pra_adl_supported(cols); });
   m.def("adl_fwd", [](P x, P h, P hb, P w, P b, P r, P y, P mean, P rstd, int rows, int cols, float eps, float p,
-                      uint64_t seed, uint64_t off, int dt, int dtw, P s) {
-    pra_adl_fwd(CV(x), CV(h), CV(hb), CV(w), CV(b), V(r), V(y), F(mean), F(rstd), rows, cols, eps, p, seed, off, dt,
-                dtw, S(s));
+                      uint64_t seed, uint64_t off, P dseq, int dt, int dtw, P s) {
+    pra_adl_fwd(CV(x), CV(h), CV(hb), CV(w), CV(b), V(r), V(y), F(mean), F(rstd), rows, cols, eps, p, seed, off,
+                reinterpret_cast<const uint64_t*>(dseq), dt, dtw, S(s));
     check_launch("adl_fwd");
   });
   m.def("adl_bwd", [](P dy, P dro, P r, P w, P mean, P rstd, P dri, P dh, P pw, P pb, P pbias, int rows, int cols,
-                      int nblk, float p, uint64_t seed, uint64_t off, int dt, int dtw, P s) {
+                      int nblk, float p, uint64_t seed, uint64_t off, P dseq, int dt, int dtw, P s) {
     pra_adl_bwd(CV(dy), CV(dro), CV(r), CV(w), CF(mean), CF(rstd), V(dri), V(dh), F(pw), F(pb), F(pbias), rows, cols,
-                nblk, p, seed, off, dt, dtw, S(s));
+                nblk, p, seed, off, reinterpret_cast<const uint64_t*>(dseq), dt, dtw, S(s));
     check_launch("adl_bwd");
   });
   m.def("colsum16", [](P part, P out, int nblk, int cols, int dt, P s) {
@@ -263,23 +272,26 @@ PYBIND11_MODULE(_pra_hip, m) {
   });
   m.def("flash_fwd_ext", [](P q, P k, P v, P o, P lse, int B, int H, int Sq, int Sk, int D, std::vector<int64_t> st,
                             float scale, int causal, int dt, P cu_q, P cu_k, P mask, int64_t msb, int64_t msh,
-                            int64_t msq, int mask_f32, float p_drop, uint64_t seed, uint64_t offset, P dbits, P s) {
+                            int64_t msq, int mask_f32, float p_drop, uint64_t seed, uint64_t offset, P dbits, P dseq,
+                            P s) {
     if (st.size() != 9) throw std::invalid_argument("flash_fwd_ext: need 9 strides");
     if (pra_flash_fwd_ext(CV(q), CV(k), CV(v), V(o), F(lse), B, H, Sq, Sk, D, st.data(), scale, causal, dt,
                           reinterpret_cast<const int*>(cu_q), reinterpret_cast<const int*>(cu_k), CV(mask), msb, msh,
-                          msq, mask_f32, p_drop, seed, offset, reinterpret_cast<uint32_t*>(dbits), S(s)) != 0)
+                          msq, mask_f32, p_drop, seed, offset, reinterpret_cast<uint32_t*>(dbits),
+                          reinterpret_cast<const uint64_t*>(dseq), S(s)) != 0)
       throw std::invalid_argument("flash_fwd_ext: unsupported arguments");
     check_launch("flash_fwd_ext");
   });
   m.def("flash_bwd_ext", [](P q, P k, P v, P dO, P lse, P delta, P dq, P dk, P dv, P dsT, int B, int H, int Sq, int Sk,
                             int D, std::vector<int64_t> st, float scale, int causal, int dt, P cu_q, P cu_k, P mask,
                             int64_t msb, int64_t msh, int64_t msq, int mask_f32, float p_drop, uint64_t seed,
-                            uint64_t offset, P dbits, P s) {
+                            uint64_t offset, P dbits, P dseq, P s) {
     if (st.size() != 18) throw std::invalid_argument("flash_bwd_ext: need 18 strides");
     if (pra_flash_bwd_ext(CV(q), CV(k), CV(v), CV(dO), CF(lse), CF(delta), V(dq), V(dk), V(dv), V(dsT), B, H, Sq, Sk,
                           D, st.data(), scale, causal, dt, reinterpret_cast<const int*>(cu_q),
                           reinterpret_cast<const int*>(cu_k), CV(mask), msb, msh, msq, mask_f32, p_drop, seed,
-                          offset, reinterpret_cast<uint32_t*>(dbits), S(s)) != 0)
+                          offset, reinterpret_cast<uint32_t*>(dbits), reinterpret_cast<const uint64_t*>(dseq),
+                          S(s)) != 0)
       throw std::invalid_argument("flash_bwd_ext: unsupported arguments");
     check_launch("flash_bwd_ext");
   });

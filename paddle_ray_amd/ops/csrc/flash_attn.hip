@@ -28,6 +28,8 @@
 #include "common.h"
 #include <stdlib.h>
 #include <type_traits>
+#include <algorithm>
+#include <cmath>
 
 namespace pra {
 namespace fa {
@@ -110,30 +112,53 @@ struct FaExt {
   int64_t msb, msh, msq;
   int mask_f32;
   float mask_mul;  // 1 / scale: the kernels add mask/scale to the raw q·k scores
-  uint32_t thr;    // dropout threshold on 32-bit uniforms (0 = no dropout)
-  float inv_keep;
+  uint32_t thr;    // dropout threshold on 16-bit uniforms, round(p * 65536) (0 = no dropout)
+  float inv_keep;  // 65536 / (65536 - thr)
   uint64_t seed, offset;
   // dropout keep bits the forward stores for the backward: [B*H][SqMax][dbits_ld] words, bit
   // (key & 31) of word (query, key >> 5); the dK/dV kernel reads them instead of re-hashing
   uint32_t* dbits;
   int dbits_ld;
+  int xf;  // feature set of the launch (XF_* below), chosen on the host
+  // graph replays: device step counter mixed into the seed (null in eager launches; see
+  // ops/graph_rng.py): a captured launch draws new bits on every replay
+  const uint64_t* dseq;
 };
+
+// Feature bits of an extended launch. Each combination runs its own copy of the tile loop, so
+// a feature that is off costs nothing inside the loop (runtime tests of ext.mask / ext.thr per
+// score element split the MFMA/VALU schedule: the extended kernels without extras ran 20 %
+// (fwd) / 42 % (bwd) slower than the plain ones at BERT-base shapes).
+//   XF_DROP : dropout on the probabilities
+//   XF_KMASK: additive mask that depends on the key only (msq == 0: [B|1, H|1, 1, Sk], the
+//             padding mask of BERT-style encoders): fwd stages the block's mask row in LDS once,
+//             dK/dV holds its lane's key value in a register
+//   XF_FMASK: general [B|1, H|1, Sq, Sk] mask, read per score element
+enum : int { XF_DROP = 1, XF_KMASK = 2, XF_FMASK = 4 };
 
 __device__ __forceinline__ uint32_t fa_mix32(uint32_t x) {
   x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
   return x;
 }
-// dropout multiplier of element (query q, key kk) of head row bh: 0 or 1/(1-p). One lowbias32
-// round over a multiply-xor fold of (seed, offset, bh, q, kk): ~8 VALU per element (the two-round
-// counter hash cost more than the attention math at head_dim 64); fwd and bwd call the same
-// function, so the backward regenerates the forward's bits exactly.
+// Dropout keep decision of element (query q, key kk) of head row bh. One lowbias32 round over a
+// multiply-xor fold of (seed, offset, bh, q, kk >> 1) yields the 16-bit uniforms of a PAIR of
+// adjacent keys (low half: even key, high half: odd key): one hash per two scores, against one
+// per score before (the two 32-bit multiplies of the mix are quarter-rate VALU and were the
+// dominant cost of dropout at head_dim 64). keep iff u16 >= thr (thr = round(p * 65536): the
+// dropout rate is p to within 2^-17, kept values scaled by the exact 1/(1-thr/65536)). fwd and
+// bwd call the same function, so a backward without stored bits regenerates them exactly.
 __device__ __forceinline__ uint32_t fa_key(const FaExt& e, int bh) {
-  return fa_mix32((uint32_t)e.seed ^ (uint32_t)(e.seed >> 32) * 0x27d4eb2fU ^
+  const uint64_t seed = e.dseq ? e.seed ^ (*e.dseq * 0x9E3779B97F4A7C15ull) : e.seed;
+  return fa_mix32((uint32_t)seed ^ (uint32_t)(seed >> 32) * 0x27d4eb2fU ^
                   (uint32_t)e.offset * 0x165667b1U ^ (uint32_t)bh * 0xc2b2ae3dU);
 }
+__device__ __forceinline__ uint32_t fa_hash2(uint32_t key, int q, int kpair) {
+  return fa_mix32(key ^ (uint32_t)q * 0x9e3779b1U ^ (uint32_t)kpair * 0x85ebca77U);
+}
+__device__ __forceinline__ float fa_keep(const FaExt& e, uint32_t u16) { return u16 >= e.thr ? e.inv_keep : 0.f; }
 __device__ __forceinline__ float fa_drop(const FaExt& e, uint32_t key, int q, int kk) {
-  const uint32_t r = fa_mix32(key ^ (uint32_t)q * 0x9e3779b1U ^ (uint32_t)kk * 0x85ebca77U);
-  return r >= e.thr ? e.inv_keep : 0.f;
+  const uint32_t hs = fa_hash2(key, q, kk >> 1);
+  return fa_keep(e, (kk & 1) ? (hs >> 16) : (hs & 0xffffu));
 }
 // additive mask value (already divided by the softmax scale) of (b, h, query q, key kk)
 template <typename T>
@@ -271,11 +296,15 @@ struct SwzDma {
   }
   // stage the tile whose first row is at byte offset row_bytes into the image at LDS byte address img
   __device__ __forceinline__ void issue(uint32_t img, uint32_t row_bytes, int wave) {
+    // the descriptor is wave-uniform, but the copies of the tile loop behind a switch on the
+    // feature set can leave it in VGPRs: pin it to SGPRs for the "s" constraint
+    const u32x4 srs = {(uint32_t)__builtin_amdgcn_readfirstlane(rs[0]), (uint32_t)__builtin_amdgcn_readfirstlane(rs[1]),
+                       (uint32_t)__builtin_amdgcn_readfirstlane(rs[2]), (uint32_t)__builtin_amdgcn_readfirstlane(rs[3])};
 #pragma unroll
     for (int n = 0; n < PER; ++n) {
       const uint32_t dst = __builtin_amdgcn_readfirstlane(img + 1024u * (n * (NT / 64) + wave));
       asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff[n] + row_bytes),
-                   "s"(rs), "s"(dst)
+                   "s"(srs), "s"(dst)
                    : "memory", "m0");
     }
   }
@@ -351,13 +380,32 @@ fwd_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restrict
     vd.issue(img + kTile * D * sizeof(T), (uint32_t)((int64_t)kt * kTile * vss * 2), wave);
   };
   if (ntiles > 0) stage(0);
+  // XF_KMASK: this (b, h)'s mask row, pre-multiplied by mask_mul, in LDS behind the K/V images
+  // (keys past Sk read 0; the launcher sizes the LDS to the 64-rounded Sk)
+  float* mrow = reinterpret_cast<float*>(smem + 4 * kTile * D * sizeof(T));
+  if constexpr (EXT) {
+    if (ext.xf & XF_KMASK) {
+      const int64_t mb = (int64_t)b * ext.msb + (int64_t)hh * ext.msh;
+      for (int j = threadIdx.x; j < ntiles * kTile; j += NW * 64) {
+        float m = 0.f;
+        if (j < Sk) {
+          m = ext.mask_f32 ? static_cast<const float*>(ext.mask)[mb + j]
+                           : Cvt<T>::to(static_cast<const T*>(ext.mask)[mb + j]);
+          m *= ext.mask_mul;
+        }
+        mrow[j] = m;
+      }
+    }
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
   const LaneOffs<D> lo(lane);
-  // one tile: the masked variant only for tiles that straddle Sk or the causal diagonal
-  auto tile = [&](int kt, auto mask_c) {
+  // one tile: the masked variant only for tiles that straddle Sk or the causal diagonal; XF =
+  // the extended features compiled into this copy of the loop
+  auto tile = [&](int kt, auto mask_c, auto xf_c) __attribute__((always_inline)) {
     constexpr bool MASK = decltype(mask_c)::value;
+    constexpr int XF = decltype(xf_c)::value;
     const int k0 = kt * kTile;
     const T* Ks = img0 + (2 * (kt & 1)) * kTile * D;
     const T* Vs = Ks + kTile * D;
@@ -417,8 +465,8 @@ fwd_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restrict
           s_acc[mt][i] = bad ? -INFINITY : s_acc[mt][i];
         }
     }
-    if constexpr (EXT) {
-      if (ext.mask && myq < Sq) {
+    if constexpr ((XF & XF_FMASK) != 0) {
+      if (myq < Sq) {
 #pragma unroll
         for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
@@ -427,6 +475,18 @@ fwd_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restrict
             if (mt < nlive && key < Sk) s_acc[mt][i] += fa_mask<T>(ext, b, hh, myq, key);
           }
       }
+    } else if constexpr ((XF & XF_KMASK) != 0) {
+      // element i <-> key k0 + 32mt + 8(i>>2) + 4h + (i&3): four float4 LDS reads per half
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const float4 m4 = *reinterpret_cast<const float4*>(mrow + k0 + 32 * mt + 8 * g + 4 * h);
+          s_acc[mt][4 * g + 0] += m4.x;
+          s_acc[mt][4 * g + 1] += m4.y;
+          s_acc[mt][4 * g + 2] += m4.z;
+          s_acc[mt][4 * g + 3] += m4.w;
+        }
     }
     float mx = -INFINITY;
 #pragma unroll
@@ -451,17 +511,18 @@ fwd_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restrict
       for (int i = 0; i < 16; ++i) {
         float p = fexp2(fmaf(s_acc[mt][i], scale_log2, -m_use));
         ps += p;  // the softmax denominator sums the undropped probabilities
-        if constexpr (EXT) {
-          if (ext.thr) {
-            const float z = fa_drop(ext, dkey, myq, k0 + 32 * mt + acc_row(i, h));
-            kbits[mt] |= (z != 0.f ? 1u : 0u) << acc_row(i, h);
-            p *= z;
-          }
+        if constexpr ((XF & XF_DROP) != 0) {
+          // elements i, i+1 (i even) are the adjacent keys of one hash pair
+          const int kk = k0 + 32 * mt + acc_row(i & ~1, h);
+          const uint32_t hs = fa_hash2(dkey, myq, kk >> 1);
+          const float z = fa_keep(ext, (i & 1) ? (hs >> 16) : (hs & 0xffffu));
+          kbits[mt] |= (z != 0.f ? 1u : 0u) << acc_row(i, h);
+          p *= z;
         }
         s_acc[mt][i] = p;
       }
-    if constexpr (EXT) {
-      if (ext.thr && ext.dbits) {  // both lane halves' 16 bits -> one word per (query, 32 keys)
+    if constexpr ((XF & XF_DROP) != 0) {
+      if (ext.dbits) {  // both lane halves' 16 bits -> one word per (query, 32 keys)
 #pragma unroll
         for (int mt = 0; mt < 2; ++mt) {
           const uint32_t w = kbits[mt] | __shfl_xor(kbits[mt], 32, 64);
@@ -490,8 +551,22 @@ fwd_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restrict
   int nfull = min(ntiles, Sk / kTile);
   if (CAUSAL) nfull = min(nfull, (q0 + off + 1) / kTile);
   if (nfull < 0) nfull = 0;
-  for (int kt = 0; kt < nfull; ++kt) tile(kt, std::false_type{});
-  for (int kt = nfull; kt < ntiles; ++kt) tile(kt, std::true_type{});
+  auto run = [&](auto xf_c) __attribute__((always_inline)) {
+    for (int kt = 0; kt < nfull; ++kt) tile(kt, std::false_type{}, xf_c);
+    for (int kt = nfull; kt < ntiles; ++kt) tile(kt, std::true_type{}, xf_c);
+  };
+  if constexpr (!EXT) {
+    run(std::integral_constant<int, 0>{});
+  } else {
+    switch (ext.xf) {
+      case XF_DROP: run(std::integral_constant<int, XF_DROP>{}); break;
+      case XF_KMASK: run(std::integral_constant<int, XF_KMASK>{}); break;
+      case XF_KMASK | XF_DROP: run(std::integral_constant<int, XF_KMASK | XF_DROP>{}); break;
+      case XF_FMASK: run(std::integral_constant<int, XF_FMASK>{}); break;
+      case XF_FMASK | XF_DROP: run(std::integral_constant<int, XF_FMASK | XF_DROP>{}); break;
+      default: run(std::integral_constant<int, 0>{}); break;
+    }
+  }
 
   if (myq < Sq) {
     const float inv = l_run > 0.f ? 1.f / l_run : 0.f;
@@ -735,7 +810,6 @@ bwd_dkdv_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __res
   const int off = Sk - Sq;
   const bool kvalid = mykey < Sk;
   const bool vl = EXT && ext.cu_q;
-  const uint32_t dkey = EXT ? fa_key(ext, bh) : 0u;  // per-(head row) dropout hash key
 
   const T* qb_ = vl ? q + qrow0 * qss + hh * qsh : q + b * qsb + hh * qsh;
   const T* kb_ = vl ? k + krow0 * kss + hh * ksh : k + b * ksb + hh * ksh;
@@ -822,8 +896,20 @@ bwd_dkdv_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __res
     *reinterpret_cast<u32x4*>(dsw + qh) = a;
     *reinterpret_cast<u32x4*>(dsw + 16 * (int64_t)Sqp + qh) = c;
   };
-  auto tile = [&](int it, auto mask_c) {
+  // XF_KMASK: the mask depends on the key only -> this lane's value, once
+  float kmv = 0.f;
+  if constexpr (EXT) {
+    if ((ext.xf & XF_KMASK) && kvalid) {
+      const int64_t i = (int64_t)b * ext.msb + (int64_t)hh * ext.msh + mykey;
+      kmv = (ext.mask_f32 ? static_cast<const float*>(ext.mask)[i] : Cvt<T>::to(static_cast<const T*>(ext.mask)[i])) *
+            ext.mask_mul;
+    }
+  }
+  // XF (extended features of this copy of the loop): with XF_DROP the keep bits are always
+  // the forward's stored ones (the launcher refuses dropout without them)
+  auto tile = [&](int it, auto mask_c, auto xf_c) __attribute__((always_inline)) {
     constexpr bool MASK = decltype(mask_c)::value;
+    constexpr int XF = decltype(xf_c)::value;
     const int buf = it & 1;
     const T* Qs = img0 + (2 * buf) * kTile * D;
     const T* Ds = Qs + kTile * D;
@@ -868,29 +954,29 @@ bwd_dkdv_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __res
           const float4 d4 = *reinterpret_cast<const float4*>(Dl + 32 * nt + 8 * g + 4 * h);
           const float la[4] = {l4.x, l4.y, l4.z, l4.w}, dl[4] = {d4.x, d4.y, d4.z, d4.w};
           uint4 mw = make_uint4(0u, 0u, 0u, 0u);
-          if constexpr (EXT)
-            if (dbits) mw = *reinterpret_cast<const uint4*>(Mb + buf * 256 + wave * 64 + 32 * nt + 8 * g + 4 * h);
+          if constexpr ((XF & XF_DROP) != 0)
+            mw = *reinterpret_cast<const uint4*>(Mb + buf * 256 + wave * 64 + 32 * nt + 8 * g + 4 * h);
           const uint32_t mwa[4] = {mw.x, mw.y, mw.z, mw.w};
 #pragma unroll
           for (int c = 0; c < 4; ++c) {
             const int i = 4 * g + c;
             const int qq = qs0 + 32 * nt + 8 * g + 4 * h + c;
             float sv = sa[nt][i];
-            if constexpr (EXT)
-              if (ext.mask && qq < Sq && kvalid) sv += fa_mask<T>(ext, b, hh, qq, mykey);
+            if constexpr ((XF & XF_FMASK) != 0) {
+              if (qq < Sq && kvalid) sv += fa_mask<T>(ext, b, hh, qq, mykey);
+            } else if constexpr ((XF & XF_KMASK) != 0) {
+              sv += kmv;
+            }
             float p = fexp2(fmaf(sv, scale_log2, -la[c]));
             if constexpr (MASK) {
               if (qq >= Sq || (CAUSAL && mykey > qq + off)) p = 0.f;
             }
-            if constexpr (EXT) {
-              if (ext.thr) {
-                // the forward's keep bit (stored) or the same hash (no bit store)
-                const float z = dbits ? ((mwa[c] >> (mykey & 31)) & 1u ? ext.inv_keep : 0.f)
-                                      : fa_drop(ext, dkey, qq, mykey);
-                sa[nt][i] = p * z;
-                da[nt][i] = p * (da[nt][i] * z - dl[c]);
-                continue;
-              }
+            if constexpr ((XF & XF_DROP) != 0) {
+              // the forward's keep bit
+              const float z = (mwa[c] >> (mykey & 31)) & 1u ? ext.inv_keep : 0.f;
+              sa[nt][i] = p * z;
+              da[nt][i] = p * (da[nt][i] * z - dl[c]);
+              continue;
             }
             sa[nt][i] = p;
             da[nt][i] = p * (da[nt][i] - dl[c]);
@@ -930,9 +1016,23 @@ bwd_dkdv_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __res
   }
   int it1 = ntiles;
   while (it1 > it0 && q_begin + (it1 - 1) * kTile + kTile > Sq) --it1;
-  for (int it = 0; it < it0; ++it) tile(it, std::true_type{});
-  for (int it = it0; it < it1; ++it) tile(it, std::false_type{});
-  for (int it = it1; it < ntiles; ++it) tile(it, std::true_type{});
+  auto run = [&](auto xf_c) __attribute__((always_inline)) {
+    for (int it = 0; it < it0; ++it) tile(it, std::true_type{}, xf_c);
+    for (int it = it0; it < it1; ++it) tile(it, std::false_type{}, xf_c);
+    for (int it = it1; it < ntiles; ++it) tile(it, std::true_type{}, xf_c);
+  };
+  if constexpr (!EXT) {
+    run(std::integral_constant<int, 0>{});
+  } else {
+    switch (ext.xf) {
+      case XF_DROP: run(std::integral_constant<int, XF_DROP>{}); break;
+      case XF_KMASK: run(std::integral_constant<int, XF_KMASK>{}); break;
+      case XF_KMASK | XF_DROP: run(std::integral_constant<int, XF_KMASK | XF_DROP>{}); break;
+      case XF_FMASK: run(std::integral_constant<int, XF_FMASK>{}); break;
+      case XF_FMASK | XF_DROP: run(std::integral_constant<int, XF_FMASK | XF_DROP>{}); break;
+      default: run(std::integral_constant<int, 0>{}); break;
+    }
+  }
 
   if (kvalid) {
     T* krow = (vl ? dk + krow0 * dkss : dk + (int64_t)b * dksb) + (int64_t)mykey * dkss + (int64_t)hh * dksh;
@@ -1164,7 +1264,8 @@ template <typename T, int D, bool C>
 static void launch_fwd_ext(const void* q, const void* k, const void* v, void* o, float* lse, int B, int H, int Sq,
                            int Sk, const int64_t* st, float scale, const FaExt& ext, hipStream_t s) {
   constexpr int NW = C ? 4 : 8;
-  const size_t lds = 4 * kTile * D * sizeof(T);
+  size_t lds = 4 * kTile * D * sizeof(T);
+  if (ext.xf & XF_KMASK) lds += (size_t)((Sk + kTile - 1) / kTile * kTile) * sizeof(float);  // mask row
   auto kern = fwd_kernel<T, D, C, NW, true>;
   hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   dim3 grid(B * H, (Sq + NW * 32 - 1) / (NW * 32));
@@ -1213,6 +1314,19 @@ using namespace pra;
     }                                                                                              \
   } while (0)
 
+// FaExt of one extended launch: dropout threshold on 16-bit uniforms, the feature set (XF_*)
+static fa::FaExt fa_ext(const int* cu_q, const int* cu_k, const void* mask, int64_t msb, int64_t msh, int64_t msq,
+                        int mask_f32, float scale, float p_drop, uint64_t seed, uint64_t offset, uint32_t* dbits,
+                        int Sk, const uint64_t* dseq) {
+  uint32_t thr = (uint32_t)std::min<long long>(65535, std::llround((double)p_drop * 65536.0));
+  int xf = 0;
+  if (thr > 0) xf |= fa::XF_DROP;
+  if (mask) xf |= (msq == 0 && Sk <= 4096) ? fa::XF_KMASK : fa::XF_FMASK;
+  return fa::FaExt{cu_q, cu_k, mask, msb, msh, msq, mask_f32, 1.f / scale, thr,
+                   thr > 0 ? (float)(65536.0 / (65536.0 - thr)) : 1.f, seed, offset, dbits, (Sk + 31) / 32, xf,
+                   dseq};
+}
+
 extern "C" {
 int pra_flash_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B, int H, int Sq, int Sk,
                   int D, const int64_t* strides, float scale, int causal, int dt, hipStream_t s) {
@@ -1232,13 +1346,12 @@ int pra_flash_fwd(const void* q, const void* k, const void* v, void* o, float* l
 int pra_flash_fwd_ext(const void* q, const void* k, const void* v, void* o, float* lse, int B, int H, int Sq, int Sk,
                       int D, const int64_t* strides, float scale, int causal, int dt, const int* cu_q,
                       const int* cu_k, const void* mask, int64_t msb, int64_t msh, int64_t msq, int mask_f32,
-                      float p_drop, uint64_t seed, uint64_t offset, uint32_t* dbits, hipStream_t s) {
+                      float p_drop, uint64_t seed, uint64_t offset, uint32_t* dbits, const uint64_t* dseq,
+                      hipStream_t s) {
   if (!(D == 64 || D == 128) || !(dt == kBF16 || dt == kF16)) return -1;
   if (!(p_drop >= 0.f && p_drop < 1.f) || (!cu_q) != (!cu_k)) return -1;
   if (B * H == 0 || Sq == 0) return 0;
-  fa::FaExt e{cu_q, cu_k, mask, msb, msh, msq, mask_f32, 1.f / scale,
-              (uint32_t)((double)p_drop * 4294967296.0), p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f, seed, offset,
-              dbits, (Sk + 31) / 32};
+  const fa::FaExt e = fa_ext(cu_q, cu_k, mask, msb, msh, msq, mask_f32, scale, p_drop, seed, offset, dbits, Sk, dseq);
   PRA_FA_DISPATCH(launch_fwd_ext, q, k, v, o, lse, B, H, Sq, Sk, strides, scale, e, s);
   return 0;
 }
@@ -1248,13 +1361,12 @@ int pra_flash_bwd_ext(const void* q, const void* k, const void* v, const void* d
                       const float* delta, void* dq, void* dk, void* dv, void* dsT, int B, int H, int Sq, int Sk, int D,
                       const int64_t* strides, float scale, int causal, int dt, const int* cu_q, const int* cu_k,
                       const void* mask, int64_t msb, int64_t msh, int64_t msq, int mask_f32, float p_drop,
-                      uint64_t seed, uint64_t offset, uint32_t* dbits, hipStream_t s) {
+                      uint64_t seed, uint64_t offset, uint32_t* dbits, const uint64_t* dseq, hipStream_t s) {
   if (!(D == 64 || D == 128) || !(dt == kBF16 || dt == kF16) || !dsT) return -1;
   if (!(p_drop >= 0.f && p_drop < 1.f) || (!cu_q) != (!cu_k)) return -1;
   if (B * H == 0 || Sq == 0) return 0;
-  fa::FaExt e{cu_q, cu_k, mask, msb, msh, msq, mask_f32, 1.f / scale,
-              (uint32_t)((double)p_drop * 4294967296.0), p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f, seed, offset,
-              dbits, (Sk + 31) / 32};
+  const fa::FaExt e = fa_ext(cu_q, cu_k, mask, msb, msh, msq, mask_f32, scale, p_drop, seed, offset, dbits, Sk, dseq);
+  if ((e.xf & fa::XF_DROP) && !dbits) return -3;  // the backward reads the forward's keep bits
   PRA_FA_DISPATCH(launch_bwd_ext, q, k, v, dO, lse, delta, dq, dk, dv, dsT, B, H, Sq, Sk, strides, scale, e, s);
   return 0;
 }

@@ -50,7 +50,9 @@ __global__ void __launch_bounds__(256) adl_fwd_k(const T* __restrict__ x, const 
                                                  const W* __restrict__ b, T* __restrict__ r_out,
                                                  T* __restrict__ y, float* __restrict__ mean,
                                                  float* __restrict__ rstd, int rows, int cols, float eps,
-                                                 uint32_t thr, float scale, uint64_t seed, uint64_t offset) {
+                                                 uint32_t thr, float scale, uint64_t seed, uint64_t offset,
+                                                 const uint64_t* __restrict__ dseq) {
+  if (dseq) seed ^= *dseq * 0x9E3779B97F4A7C15ull;  // graph replays: device step counter (see graph_seq)
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -132,7 +134,9 @@ __device__ __forceinline__ void adl_bwd_body(const T* __restrict__ dy, const T* 
                                              T* __restrict__ dr_in, T* __restrict__ dh,
                                              float* __restrict__ pw, float* __restrict__ pb,
                                              float* __restrict__ pbias, int rows, int cols, uint32_t thr,
-                                             float scale, uint64_t seed, uint64_t offset) {
+                                             float scale, uint64_t seed, uint64_t offset,
+                                             const uint64_t* __restrict__ dseq) {
+  if (dseq) seed ^= *dseq * 0x9E3779B97F4A7C15ull;
   extern __shared__ __attribute__((aligned(16))) float red_lds[];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   float aw[C][8], ab[C][8], ah[C][8];
@@ -248,16 +252,16 @@ __device__ __forceinline__ void adl_bwd_body(const T* __restrict__ dy, const T* 
   const T* __restrict__ dy, const T* __restrict__ dr_out, const T* __restrict__ r, const W* __restrict__ w,  \
       const float* __restrict__ mean, const float* __restrict__ rstd, T* __restrict__ dr_in, T* __restrict__ dh, \
       float* __restrict__ pw, float* __restrict__ pb, float* __restrict__ pbias, int rows, int cols, uint32_t thr, \
-      float scale, uint64_t seed, uint64_t offset
+      float scale, uint64_t seed, uint64_t offset, const uint64_t* __restrict__ dseq
 template <typename T, typename W, int C>
 __global__ void __launch_bounds__(256) adl_bwd_k(ADL_BWD_ARGS) {
   adl_bwd_body<T, W, C, false>(dy, dr_out, r, w, mean, rstd, dr_in, dh, pw, pb, pbias, rows, cols, thr, scale, seed,
-                               offset);
+                               offset, dseq);
 }
 template <typename T, typename W, int C>
 __global__ void __launch_bounds__(256, 3) adl_bwd2_k(ADL_BWD_ARGS) {
   adl_bwd_body<T, W, C, true>(dy, dr_out, r, w, mean, rstd, dr_in, dh, pw, pb, pbias, rows, cols, thr, scale, seed,
-                              offset);
+                              offset, dseq);
 }
 #undef ADL_BWD_ARGS
 
@@ -357,7 +361,7 @@ int pra_adl_supported(int cols) { return (cols % 8 == 0 && cols <= 4096) ? 1 : 0
 
 void pra_adl_fwd(const void* x, const void* h, const void* hbias, const void* w, const void* b, void* r_out,
                  void* y, float* mean, float* rstd, int rows, int cols, float eps, float p, uint64_t seed,
-                 uint64_t offset, int dt, int dtw, hipStream_t s) {
+                 uint64_t offset, const uint64_t* dseq, int dt, int dtw, hipStream_t s) {
   if (!rows) return;
   uint32_t thr = (h && p > 0.f) ? (uint32_t)(p * 65536.f + 0.5f) : 0u;
   float scale = thr ? 1.f / (1.f - p) : 1.f;
@@ -365,7 +369,7 @@ void pra_adl_fwd(const void* x, const void* h, const void* hbias, const void* w,
 #define K_FWD(CC, TX, TW)                                                                                  \
   hipLaunchKernelGGL((adl_fwd_k<TX, TW, CC>), grid, dim3(256), 0, s, (const TX*)x, (const TX*)h,             \
                      (const TX*)hbias, (const TW*)w, (const TW*)b, (TX*)r_out, (TX*)y, mean, rstd, rows, cols, \
-                     eps, thr, scale, seed, offset)
+                     eps, thr, scale, seed, offset, dseq)
   PRA_DISPATCH_FLOAT(dt, TX, {
     if (dtw == dt) { ADL_DISPATCH_C(cols, K_FWD, TX, TX); }
     else { ADL_DISPATCH_C(cols, K_FWD, TX, float); }
@@ -375,7 +379,8 @@ void pra_adl_fwd(const void* x, const void* h, const void* hbias, const void* w,
 
 void pra_adl_bwd(const void* dy, const void* dr_out, const void* r, const void* w, const float* mean,
                  const float* rstd, void* dr_in, void* dh, float* pw, float* pb, float* pbias, int rows, int cols,
-                 int nblk, float p, uint64_t seed, uint64_t offset, int dt, int dtw, hipStream_t s) {
+                 int nblk, float p, uint64_t seed, uint64_t offset, const uint64_t* dseq, int dt, int dtw,
+                 hipStream_t s) {
   if (!rows) return;
   uint32_t thr = (dh && p > 0.f) ? (uint32_t)(p * 65536.f + 0.5f) : 0u;
   float scale = thr ? 1.f / (1.f - p) : 1.f;
@@ -385,11 +390,11 @@ void pra_adl_bwd(const void* dy, const void* dr_out, const void* r, const void* 
   if (two)                                                                                                 \
     hipLaunchKernelGGL((adl_bwd2_k<TX, TW, CC>), dim3(nblk), dim3(256), lds, s, (const TX*)dy, (const TX*)dr_out, \
                        (const TX*)r, (const TW*)w, mean, rstd, (TX*)dr_in, (TX*)dh, pw, pb, pbias, rows, cols, thr, \
-                       scale, seed, offset);                                                               \
+                       scale, seed, offset, dseq);                                                         \
   else                                                                                                     \
     hipLaunchKernelGGL((adl_bwd_k<TX, TW, CC>), dim3(nblk), dim3(256), lds, s, (const TX*)dy, (const TX*)dr_out, \
                        (const TX*)r, (const TW*)w, mean, rstd, (TX*)dr_in, (TX*)dh, pw, pb, pbias, rows, cols, thr, \
-                       scale, seed, offset)
+                       scale, seed, offset, dseq)
   PRA_DISPATCH_FLOAT(dt, TX, {
     if (dtw == dt) { ADL_DISPATCH_C(cols, K_BWD, TX, TX); }
     else { ADL_DISPATCH_C(cols, K_BWD, TX, float); }

@@ -114,7 +114,7 @@ def _ln_fwd_hip(x2, w, b, eps):
     dtw = _dt(w) if w is not None else _dt(x2)
     if _adl_ok(cols):
         L.adl_fwd(_ptr(x2), 0, 0, _ptr(w), _ptr(b), 0, _ptr(y), _ptr(mean), _ptr(rstd), rows, cols,
-                  float(eps), 0.0, 0, 0, _dt(x2), dtw, _stream())
+                  float(eps), 0.0, 0, 0, 0, _dt(x2), dtw, _stream())
     else:
         L.layernorm_fwd(_ptr(x2), _ptr(w), _ptr(b), _ptr(y), _ptr(mean), _ptr(rstd), rows, cols,
                         float(eps), _dt(x2), dtw, _stream())
@@ -134,7 +134,7 @@ def _ln_bwd_hip(dy, x2, w, mean, rstd, need_dw, need_db):
         part = torch.empty((2, nblk, cols), device=x2.device, dtype=torch.float32)
         L.adl_bwd(_ptr(dy), 0, _ptr(x2), _ptr(w), _ptr(mean), _ptr(rstd), _ptr(dx), 0,
                   _ptr(part[0]) if (need_dw and w is not None) else 0,
-                  _ptr(part[1]) if need_db else 0, 0, rows, cols, nblk, 0.0, 0, 0, _dt(x2), dtw,
+                  _ptr(part[1]) if need_db else 0, 0, rows, cols, nblk, 0.0, 0, 0, 0, _dt(x2), dtw,
                   _stream())
         red = L.colsum16
     else:
@@ -188,6 +188,31 @@ def _dropout_seed():
     return int(torch.randint(0, 2 ** 62, (1,)).item())
 
 
+# Graph-safe dropout RNG. The kernels' seeds are host values, so a launch captured into a HIP
+# graph would replay ONE mask forever. Under capture every dropout kernel also reads a device
+# step counter (mixed into its seed in-kernel); the first dropout launch of each capture also
+# captures `counter += 1`, so every replay advances it once and all launches of that replay --
+# forward and backward, including recomputed segments -- read the same new value. Eager
+# launches pass a null pointer (host seed only). The counter is created outside any pool that a
+# graph could free (torch.empty under capture would come from the graph's private pool and is
+# never released: it stays referenced here).
+_GSEQ = {}
+
+
+def _graph_seq(dev):
+    """(device pointer of the step counter or 0, the counter tensor to keep alive or None)."""
+    if dev.type != 'cuda' or not torch.cuda.is_current_stream_capturing():
+        return 0, None
+    cid = _native.lib().capture_id(_stream())
+    st = _GSEQ.get(dev.index)
+    if st is None:
+        st = _GSEQ[dev.index] = [torch.empty(1, dtype=torch.int64, device=dev), 0]
+    if st[1] != cid:
+        st[0].add_(1)
+        st[1] = cid
+    return st[0].data_ptr(), st[0]
+
+
 def _hash_keep_ref(n, p, seed, device):
     """Reference of the kernel's counter-hash keep mask (for CPU + tests)."""
     import numpy as np
@@ -233,7 +258,7 @@ def _adl_bwd_ref(dy, dr_out, r, w, mean, rstd, p, seed, need_dw, need_db, need_d
 
 
 @R.register_kernel('add_dropout_ln_fwd', 'hip', dtypes=_FLOATS)
-def _adl_fwd_hip(x2, h2, hb, w, b, p, eps, seed):
+def _adl_fwd_hip(x2, h2, hb, w, b, p, eps, seed, dseq=0):
     _check_dtypes('add_dropout_layer_norm', (x2, h2), (x2, hb), (w, b))
     rows, cols = x2.shape
     if not _adl_ok(cols):
@@ -243,13 +268,13 @@ def _adl_fwd_hip(x2, h2, hb, w, b, p, eps, seed):
     mean = torch.empty(rows, device=x2.device, dtype=torch.float32)
     rstd = torch.empty(rows, device=x2.device, dtype=torch.float32)
     _native.lib().adl_fwd(_ptr(x2), _ptr(h2), _ptr(hb), _ptr(w), _ptr(b), _ptr(r), _ptr(y),
-                          _ptr(mean), _ptr(rstd), rows, cols, float(eps), float(p), seed, 0,
+                          _ptr(mean), _ptr(rstd), rows, cols, float(eps), float(p), seed, 0, dseq,
                           _dt(x2), _dt(w) if w is not None else _dt(x2), _stream())
     return r, y, mean, rstd
 
 
 @R.register_kernel('add_dropout_ln_bwd', 'hip', dtypes=_FLOATS)
-def _adl_bwd_hip(dy, dr_out, r, w, mean, rstd, p, seed, need_dw, need_db, need_dhb, into=None):
+def _adl_bwd_hip(dy, dr_out, r, w, mean, rstd, p, seed, need_dw, need_db, need_dhb, into=None, dseq=0):
     """into: (w.grad, b.grad, hb.grad) or None per slot — those column sums are ADDED into the
     existing gradient by the reduction kernel and None is returned in their place (no
     AccumulateGrad add kernels for the LayerNorm / bias parameters)."""
@@ -265,7 +290,7 @@ def _adl_bwd_hip(dy, dr_out, r, w, mean, rstd, p, seed, need_dw, need_db, need_d
     pdt = w.dtype if w is not None else r.dtype
     L.adl_bwd(_ptr(dy), _ptr(dr_out), _ptr(r), _ptr(w), _ptr(mean), _ptr(rstd), _ptr(dri),
               _ptr(dh), _ptr(part[0]) if need_dw else 0, _ptr(part[1]) if need_db else 0,
-              _ptr(part[2]) if need_dhb else 0, rows, cols, nblk, float(p), seed, 0, _dt(r),
+              _ptr(part[2]) if need_dhb else 0, rows, cols, nblk, float(p), seed, 0, dseq, _dt(r),
               _dt(w) if w is not None else _dt(r), _stream())
     outs, jobs = [], []
     into = into or (None, None, None)
@@ -307,10 +332,14 @@ class AddDropoutLNFn(torch.autograd.Function):
         if w is not None:
             b = _like(b, w.dtype)
         seed = _dropout_seed() if p > 0 else 0
-        r, y, mean, rstd = R.dispatch('add_dropout_ln_fwd', x2, x2, h2, hb, w, b, p, eps, seed)
+        dseq, ctx.gseq = _graph_seq(x.device) if p > 0 else (0, None)
+        if dseq and R.select_backend(x2, 'add_dropout_ln_fwd') == 'hip':
+            r, y, mean, rstd = _adl_fwd_hip(x2, h2, hb, w, b, p, eps, seed, dseq)
+        else:
+            r, y, mean, rstd = R.dispatch('add_dropout_ln_fwd', x2, x2, h2, hb, w, b, p, eps, seed)
         ctx.save_for_backward(r, w, mean, rstd)
         ctx.params = (w, b, hb)
-        ctx.p, ctx.seed, ctx.shp = p, seed, shp
+        ctx.p, ctx.seed, ctx.shp, ctx.dseq = p, seed, shp, dseq
         ctx.has_b, ctx.has_hb = b is not None, hb is not None
         return r.view(shp), y.view(shp)
 
@@ -327,7 +356,7 @@ class AddDropoutLNFn(torch.autograd.Function):
         if r.is_cuda and R.select_backend(r, 'add_dropout_ln_bwd') == 'hip':
             pw, pb, phb = ctx.params
             into = (_acc_target(pw), _acc_target(pb), _acc_target(phb))
-            dri, dh, dw, db, dhb = _adl_bwd_hip(*args[1:], into=into)
+            dri, dh, dw, db, dhb = _adl_bwd_hip(*args[1:], into=into, dseq=ctx.dseq)
         else:
             dri, dh, dw, db, dhb = R.dispatch('add_dropout_ln_bwd', *args)
         return dri.view(ctx.shp), dh.view(ctx.shp), dhb, dw, db, None, None
@@ -336,10 +365,8 @@ class AddDropoutLNFn(torch.autograd.Function):
 def add_dropout_layer_norm(x, h, hbias, w, b, p=0.0, eps=1e-5, training=True):
     """(r, y) with r = x + dropout(h + hbias), y = LayerNorm(r)·w + b."""
     p = p if training else 0.0
-    if p > 0 and x.is_cuda and torch.cuda.is_current_stream_capturing():
-        # the kernel's dropout seed is a host value: a captured HIP graph would replay ONE
-        # mask forever. Under capture use torch's graph-aware RNG (seed/offset advanced per
-        # replay) and the LayerNorm kernel.
+    if p > 0 and x.is_cuda and torch.cuda.is_current_stream_capturing() and not _adl_ok(x.shape[-1]):
+        # a width the kernel does not take: torch's graph-aware dropout RNG under capture
         hh = h if hbias is None else h + hbias.to(h.dtype)
         r = x + torch.nn.functional.dropout(hh.to(x.dtype), p, True)
         return r, layer_norm(r, w, b, eps)
@@ -957,16 +984,18 @@ def _mix32_t(x):
 
 
 def fa_dropout_mask_ref(seed, offset, bh, q, kk, p_drop):
-    """The keep multiplier (0 or 1/(1-p)) the flash kernels use for (head row bh, query q, key
-    kk) — a torch port of flash_attn.hip fa_key / fa_drop for references and tests. bh/q/kk:
-    int64 tensors (broadcastable)."""
-    thr = int(float(np.float32(p_drop)) * 4294967296.0)  # the kernel receives a float32 p
-    inv_keep = float(np.float32(1.0) / (np.float32(1.0) - np.float32(p_drop)))
+    """The keep multiplier (0 or 1/(1-thr/65536)) the flash kernels use for (head row bh, query q,
+    key kk) — a torch port of flash_attn.hip fa_key / fa_drop for references and tests: one hash
+    per pair of adjacent keys (kk >> 1), the low / high 16 bits as the even / odd key's uniform,
+    keep iff u16 >= thr = round(p * 65536). bh/q/kk: int64 tensors (broadcastable)."""
+    thr = min(65535, int(round(float(np.float32(p_drop)) * 65536.0)))  # the kernel receives a float32 p
+    inv_keep = float(np.float32(65536.0 / (65536.0 - thr)))
     s0 = (seed & _M32) ^ ((((seed >> 32) & _M32) * 0x27d4eb2f) & _M32) ^ \
         (((offset & _M32) * 0x165667b1) & _M32)
     key = _mix32_t(((bh & _M32) * 0xc2b2ae3d & _M32) ^ s0)
-    r = _mix32_t(key ^ (((q & _M32) * 0x9e3779b1) & _M32) ^ (((kk & _M32) * 0x85ebca77) & _M32))
-    return torch.where(r >= thr, inv_keep, 0.0)
+    r = _mix32_t(key ^ (((q & _M32) * 0x9e3779b1) & _M32) ^ ((((kk >> 1) & _M32) * 0x85ebca77) & _M32))
+    u = torch.where((kk & 1) == 1, r >> 16, r & 0xffff)
+    return torch.where(u >= thr, inv_keep, 0.0)
 
 
 def _fa_ext_ref_dense(q, k, v, causal, scale, mask=None, p_drop=0.0, seed=0, offset=0, bh0=None):
@@ -1016,7 +1045,6 @@ def _fa_next_rng(seed=None, numel=1):
     return seed, off
 
 
-_FA_DROP_BITS = __import__('os').environ.get('PRA_FA_DROP_BITS', '0') == '1'
 
 
 class FlashAttnExtFn(torch.autograd.Function):
@@ -1042,15 +1070,15 @@ class FlashAttnExtFn(torch.autograd.Function):
         lse = torch.empty((B, H, Sq), device=q.device, dtype=torch.float32)
         mk, msb, msh, msq, m32 = (None, 0, 0, 0, False) if mask is None else \
             _mask_strides(mask, B, H, Sq, Sk)
-        # dropout keep bits for the backward (1 bit per score: B*H*Sq*Sk/8 bytes, PRA_FA_DROP_BITS=1);
-        # by default the dK/dV kernel regenerates the hash instead (BERT-base: 1188 vs 1174 seq/s
-        # with the stored bits, profiles/r3_bert)
+        # dropout keep bits for the backward (1 bit per score: B*H*Sq*Sk/8 bytes, 12.6 MB at
+        # BERT-base bs32): the dK/dV kernel reads them instead of re-hashing every score
         dbits = torch.empty(B * H * Sq * (-(-Sk // 32)), device=q.device, dtype=torch.int32) \
-            if p_drop > 0 and _FA_DROP_BITS else torch.empty(0, device=q.device, dtype=torch.int32)
+            if p_drop > 0 else torch.empty(0, device=q.device, dtype=torch.int32)
+        dseq, ctx.gseq = _graph_seq(q.device) if p_drop > 0 else (0, None)
         L.flash_fwd_ext(_ptr(q), _ptr(k), _ptr(v), _ptr(o), _ptr(lse), B, H, Sq, Sk, D, st, float(scale),
                         int(causal), _dt(q), _ptr(cu_q) if varlen else 0, _ptr(cu_k) if varlen else 0,
                         _ptr(mk) if mk is not None else 0, msb, msh, msq, int(m32), float(p_drop),
-                        int(seed), int(offset), _ptr(dbits) if dbits.numel() else 0, _stream())
+                        int(seed), int(offset), _ptr(dbits) if dbits.numel() else 0, dseq, _stream())
         ctx.save_for_backward(q, k, v, o, lse, mk if mk is not None else torch.empty(0), cu_q if varlen else
                               torch.empty(0), cu_k if varlen else torch.empty(0), dbits)
         ctx.meta = (varlen, B, H, D, Sq, Sk, st, causal, scale, p_drop, seed, offset,
@@ -1059,38 +1087,65 @@ class FlashAttnExtFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, do):
-        q, k, v, o, lse, mk, cu_q, cu_k, dbits = ctx.saved_tensors
-        varlen, B, H, D, Sq, Sk, st, causal, scale, p_drop, seed, offset, mmeta = ctx.meta
-        L = _native.lib()
-        do = _like(do, q.dtype).contiguous()
-        delta = torch.empty((B, H, Sq), device=q.device, dtype=torch.float32)
-        if varlen:
-            dd = (do.float() * o.float()).sum(-1)                     # [total, H]
-            lens = (cu_q[1:] - cu_q[:-1]).long()
-            bidx = torch.repeat_interleave(torch.arange(B, device=q.device), lens)
-            qidx = torch.arange(q.shape[0], device=q.device) - cu_q.long()[bidx]
-            delta.view(B, H, Sq).permute(0, 2, 1)[bidx, qidx] = dd
-            dq = torch.empty_like(q)
-            dk = torch.empty_like(k)
-            dv = torch.empty_like(v)
-            gst = st + [0, dq.stride(0), dq.stride(1), 0, dk.stride(0), dk.stride(1), 0, dv.stride(0),
-                        dv.stride(1)]
+        dq, dk, dv = _fa_ext_backward(ctx, do)
+        return dq, dk, dv, None, None, None, None, None, None, None, None, None, None
+
+
+def _fa_ext_backward(ctx, do, outs=None):
+    """dq, dk, dv of FlashAttnExtFn (into ``outs`` = (dq, dk, dv) views when given, dense only)."""
+    q, k, v, o, lse, mk, cu_q, cu_k, dbits = ctx.saved_tensors
+    varlen, B, H, D, Sq, Sk, st, causal, scale, p_drop, seed, offset, mmeta = ctx.meta
+    L = _native.lib()
+    do = _like(do, q.dtype).contiguous()
+    delta = torch.empty((B, H, Sq), device=q.device, dtype=torch.float32)
+    if varlen:
+        dd = (do.float() * o.float()).sum(-1)                     # [total, H]
+        lens = (cu_q[1:] - cu_q[:-1]).long()
+        bidx = torch.repeat_interleave(torch.arange(B, device=q.device), lens)
+        qidx = torch.arange(q.shape[0], device=q.device) - cu_q.long()[bidx]
+        delta.view(B, H, Sq).permute(0, 2, 1)[bidx, qidx] = dd
+        dq = torch.empty_like(q)
+        dk = torch.empty_like(k)
+        dv = torch.empty_like(v)
+        gst = st + [0, dq.stride(0), dq.stride(1), 0, dk.stride(0), dk.stride(1), 0, dv.stride(0),
+                    dv.stride(1)]
+    else:
+        L.flash_bwd_pre(_ptr(o), _ptr(do), _ptr(delta), B, H, Sq, D, _dt(q), _stream())
+        if outs is not None:
+            dq, dk, dv = outs
         else:
-            L.flash_bwd_pre(_ptr(o), _ptr(do), _ptr(delta), B, H, Sq, D, _dt(q), _stream())
             dq = torch.empty((B, Sq, H, D), device=q.device, dtype=q.dtype)
             dk = torch.empty((B, Sk, H, D), device=q.device, dtype=q.dtype)
             dv = torch.empty((B, Sk, H, D), device=q.device, dtype=q.dtype)
-            gst = st + [dq.stride(0), dq.stride(1), dq.stride(2), dk.stride(0), dk.stride(1), dk.stride(2),
-                        dv.stride(0), dv.stride(1), dv.stride(2)]
-        ds = torch.empty(B * H * (-(-Sk // 128) * 128) * (-(-Sq // 256) * 256), device=q.device,
-                         dtype=q.dtype)
-        msb, msh, msq, m32 = mmeta if mmeta is not None else (0, 0, 0, False)
-        L.flash_bwd_ext(_ptr(q), _ptr(k), _ptr(v), _ptr(do), _ptr(lse), _ptr(delta), _ptr(dq), _ptr(dk),
-                        _ptr(dv), _ptr(ds), B, H, Sq, Sk, D, gst, float(scale), int(causal), _dt(q),
-                        _ptr(cu_q) if varlen else 0, _ptr(cu_k) if varlen else 0,
-                        _ptr(mk) if mmeta is not None else 0, msb, msh, msq, int(m32), float(p_drop),
-                        int(seed), int(offset), _ptr(dbits) if dbits.numel() else 0, _stream())
-        return dq, dk, dv, None, None, None, None, None, None, None, None, None, None
+        gst = st + [dq.stride(0), dq.stride(1), dq.stride(2), dk.stride(0), dk.stride(1), dk.stride(2),
+                    dv.stride(0), dv.stride(1), dv.stride(2)]
+    ds = torch.empty(B * H * (-(-Sk // 128) * 128) * (-(-Sq // 256) * 256), device=q.device,
+                     dtype=q.dtype)
+    msb, msh, msq, m32 = mmeta if mmeta is not None else (0, 0, 0, False)
+    L.flash_bwd_ext(_ptr(q), _ptr(k), _ptr(v), _ptr(do), _ptr(lse), _ptr(delta), _ptr(dq), _ptr(dk),
+                    _ptr(dv), _ptr(ds), B, H, Sq, Sk, D, gst, float(scale), int(causal), _dt(q),
+                    _ptr(cu_q) if varlen else 0, _ptr(cu_k) if varlen else 0,
+                    _ptr(mk) if mmeta is not None else 0, msb, msh, msq, int(m32), float(p_drop),
+                    int(seed), int(offset), _ptr(dbits) if dbits.numel() else 0, 0, _stream())
+    return dq, dk, dv
+
+
+class FlashAttnExtQKVFn(torch.autograd.Function):
+    """FlashAttnExtFn on a packed qkv [B, S, 3, H, D] (the fused QKV projection's output): the
+    backward writes dq / dk / dv straight into one packed gradient (no stack of three grads)."""
+
+    @staticmethod
+    def forward(ctx, qkv, mask, causal, scale, p_drop, seed, offset):
+        q, k, v = qkv.unbind(2)
+        S = qkv.shape[1]
+        return FlashAttnExtFn.forward(ctx, q, k, v, mask, None, None, S, S, causal, scale, p_drop, seed, offset)
+
+    @staticmethod
+    def backward(ctx, do):
+        dqkv = torch.empty(ctx.saved_tensors[0].shape[:2] + (3,) + ctx.saved_tensors[0].shape[2:],
+                           device=do.device, dtype=ctx.saved_tensors[0].dtype)
+        _fa_ext_backward(ctx, do, dqkv.unbind(2))
+        return dqkv, None, None, None, None, None, None
 
 
 def _fa_ext_ok(q, k, v):
@@ -1119,6 +1174,20 @@ def flash_attention_ext(q, k, v, causal=False, scale=None, attn_mask=None, dropo
     R._STATS[('flash_attn_ext', 'ref')] += 1
     o, _ = _fa_ext_ref_dense(q, k, v, causal, scale, attn_mask, dropout, sd, off)
     return o.to(q.dtype)
+
+
+def flash_attention_ext_qkvpacked(qkv, causal=False, scale=None, attn_mask=None, dropout=0.0, seed=None):
+    """flash_attention_ext on a packed qkv [B, S, 3, H, D] -> o [B, S, H, D]."""
+    if scale is None:
+        scale = 1.0 / math.sqrt(qkv.shape[-1])
+    q, k, v = qkv.unbind(2)
+    if not _fa_ext_ok(q, k, v) or (attn_mask is not None and attn_mask.dtype == torch.bool):
+        return flash_attention_ext(q, k, v, causal, scale, attn_mask, dropout, seed)
+    if attn_mask is not None and attn_mask.dtype not in (qkv.dtype, torch.float32):
+        attn_mask = attn_mask.to(qkv.dtype)
+    sd, off = _fa_next_rng(seed) if dropout > 0 else (0, 0)
+    R._STATS[('flash_attn_ext', 'hip')] += 1
+    return FlashAttnExtQKVFn.apply(qkv, attn_mask, causal, scale, float(dropout), sd, off)
 
 
 def flash_attn_varlen(q, k, v, cu_q, cu_k, max_sq, max_sk, causal=False, scale=None, dropout=0.0,

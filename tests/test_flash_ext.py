@@ -58,13 +58,11 @@ def _fp32_grads(fn, tensors, g):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize('bits', [False, True], ids=['rehash', 'keep_bits'])
 @pytest.mark.parametrize('causal', [False, True])
 @pytest.mark.parametrize('D', [64, 128])
-def test_flash_dropout_matches_reference_with_same_mask(causal, D, bits, monkeypatch):
-    """Both backward modes: the dK/dV kernel regenerating the hash (default) and reading the
-    keep bits the forward stored (PRA_FA_DROP_BITS=1)."""
-    monkeypatch.setattr(K, '_FA_DROP_BITS', bits)
+def test_flash_dropout_matches_reference_with_same_mask(causal, D):
+    """Forward draws the keep bits (one hash per key pair) and stores them; the dK/dV kernel
+    reads them. Same bits as the fp32 reference (fa_dropout_mask_ref)."""
     torch.manual_seed(1)
     dev = torch.device('cuda')
     B, S, H = 2, 320, 3
@@ -80,6 +78,34 @@ def test_flash_dropout_matches_reference_with_same_mask(causal, D, bits, monkeyp
                          (q, k, v), g)
     err = (o.float() - ro).abs().max().item() / ro.abs().max().item()
     assert err < 2e-2, err
+    for got, ref, n in zip((q.grad, k.grad, v.grad), rg, 'qkv'):
+        e = (got.float() - ref).abs().max().item() / ref.abs().max().item()
+        assert e < 3e-2, (n, e)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('drop', [0.0, 0.1])
+@pytest.mark.parametrize('mdtype', [torch.bfloat16, torch.float32])
+def test_flash_key_padding_mask(drop, mdtype):
+    """[B, 1, 1, Sk] key-padding mask (the XF_KMASK path: the forward's LDS mask row, the dK/dV
+    kernel's per-lane value), alone and with dropout, against the fp32 reference."""
+    torch.manual_seed(5)
+    dev = torch.device('cuda')
+    B, S, H, D = 3, 384, 2, 64
+    q, k, v = (torch.randn(B, S, H, D, device=dev, dtype=torch.bfloat16, requires_grad=True)
+               for _ in range(3))
+    m = torch.zeros(B, 1, 1, S, device=dev, dtype=mdtype)
+    m[0, ..., 300:] = float('-inf')
+    m[2, ..., 17:] = float('-inf')
+    m[1, ..., :5] = -3.0
+    seed, off = 99, 3
+    sc = 1 / math.sqrt(D)
+    o = K.FlashAttnExtFn.apply(q, k, v, m, None, None, S, S, False, sc, drop, seed, off)
+    g = torch.randn_like(o)
+    o.backward(g)
+    ro, rg = _fp32_grads(lambda a, b, c: K._fa_ext_ref_dense(a, b, c, False, sc, m.float(), drop, seed, off)[0],
+                         (q, k, v), g)
+    assert (o.float() - ro).abs().max().item() / ro.abs().max().item() < 2e-2
     for got, ref, n in zip((q.grad, k.grad, v.grad), rg, 'qkv'):
         e = (got.float() - ref).abs().max().item() / ref.abs().max().item()
         assert e < 3e-2, (n, e)
@@ -158,3 +184,62 @@ def test_gpt_attention_dropout_uses_flash_kernel():
     st = R.stats()
     assert st.get(('flash_attn_ext', 'hip'), 0) > 0, st
     assert np.isfinite(float(loss))
+
+
+@pytest.mark.gpu
+def test_packed_qkv_ext_matches_unpacked():
+    torch.manual_seed(7)
+    dev = torch.device('cuda')
+    B, S, H, D = 2, 256, 3, 64
+    qkv = torch.randn(B, S, 3, H, D, device=dev, dtype=torch.bfloat16, requires_grad=True)
+    m = torch.zeros(B, 1, 1, S, device=dev, dtype=torch.bfloat16)
+    m[1, ..., 200:] = float('-inf')
+    o = K.flash_attention_ext_qkvpacked(qkv, attn_mask=m, dropout=0.1, seed=11)
+    g = torch.randn_like(o)
+    o.backward(g)
+    K._FA_RNG_OFFSET[0] -= 1  # same offset for the unpacked call
+    q2 = qkv.detach().clone().requires_grad_(True)
+    q, k, v = q2.unbind(2)
+    o2 = K.flash_attention_ext(q, k, v, attn_mask=m, dropout=0.1, seed=11)
+    o2.backward(g)
+    assert torch.equal(o, o2)
+    assert torch.equal(qkv.grad, q2.grad)
+
+
+@pytest.mark.gpu
+def test_dropout_masks_change_across_graph_replays():
+    """Captured dropout launches (flash attention, add+dropout+LayerNorm) read the device step
+    counter: every replay draws new masks, forward and backward agree within a replay."""
+    torch.manual_seed(8)
+    dev = torch.device('cuda')
+    B, S, H, D = 2, 128, 2, 64
+    q, k, v = (torch.randn(B, S, H, D, device=dev, dtype=torch.bfloat16, requires_grad=True) for _ in range(3))
+    x = torch.randn(B * S, 256, device=dev, dtype=torch.bfloat16)
+    hh = torch.randn(B * S, 256, device=dev, dtype=torch.bfloat16, requires_grad=True)
+    w = torch.ones(256, device=dev, dtype=torch.bfloat16)
+    b = torch.zeros(256, device=dev, dtype=torch.bfloat16)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):  # warm up outside the capture
+        K.flash_attention_ext(q, k, v, dropout=0.5).sum().backward()
+        K.add_dropout_layer_norm(x, hh, None, w, b, 0.5)[0].float().sum().backward()
+    torch.cuda.current_stream().wait_stream(s)
+    q.grad = k.grad = v.grad = hh.grad = None
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        o = K.flash_attention_ext(q, k, v, dropout=0.5)
+        r, _ = K.add_dropout_layer_norm(x, hh, None, w, b, 0.5)
+        (o.float().sum() + r.float().sum()).backward()
+    outs = []
+    for _ in range(2):
+        g.replay()
+        torch.cuda.synchronize()
+        outs.append((o.clone(), r.clone(), v.grad.clone(), hh.grad.clone()))
+    (o1, r1, gv1, gh1), (o2, r2, gv2, gh2) = outs
+    assert not torch.equal(o1, o2) and not torch.equal(r1, r2)
+    # within a replay the backward used the forward's masks: dh is zero exactly where r == x
+    drop1 = (r1 == x)
+    # (a kept x + 2h can round back to x in bf16 for tiny h: allow a few such elements)
+    assert ((gh1 == 0) != drop1).float().mean().item() < 0.01
+    assert ((gh1 == 0) != (gh2 == 0)).float().mean().item() > 0.2
+    assert not torch.equal(gv1, gv2)
