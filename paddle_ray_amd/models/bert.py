@@ -190,8 +190,11 @@ class BertLayer(nn.Layer):
             a = K.linear(self.attn.context(x, attn_mask), self.attn.out_proj.weight._t)
             _, y1 = K.add_dropout_layer_norm(t, a, self.attn.out_proj.bias._t,
                                              self.ln1.weight._t, self.ln1.bias._t, p, self.eps)
-            hdn = self._ffn_hidden(Tensor(y1))
-            m = K.linear(hdn, self.fc2.weight._t)
+            if self.act == 'gelu':
+                # fc1 GEMM with the bias+GELU epilogue, fc2 GEMM (its bias goes to the ADL kernel)
+                m = K.mlp_gelu(y1, self.fc1.weight._t, self.fc1.bias._t, self.fc2.weight._t, False)
+            else:
+                m = K.linear(self._ffn_hidden(Tensor(y1)), self.fc2.weight._t)
             _, y2 = K.add_dropout_layer_norm(y1, m, self.fc2.bias._t, self.ln2.weight._t,
                                              self.ln2.bias._t, p, self.eps)
             return Tensor(y2)

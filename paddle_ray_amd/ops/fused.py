@@ -1293,6 +1293,10 @@ def _gemm_hip(layout, a, b, out=None, bias=None, z=None, epi=None, beta=0, want_
         # skinny decode-time forwards (M < 128: a 256-row tile idles) go to the library
         if layout == GEMM_FWD and M < 128:
             return None
+        # forward GEMMs that would need split-K (few 256x256 tiles over a long K: BERT's fc2
+        # 16384x768x3072 ran 138.7 us split 4-ways vs 73.6 us in hipBLASLt, profiles/r3g)
+        if layout == GEMM_FWD and ((M + 255) // 256) * ((N + 255) // 256) < 224 and K // 64 >= 16:
+            return None
     if out is None:
         out = torch.empty((M, N), device=a.device, dtype=a.dtype)
     elif not _gemm_operand_ok(out) or out.dtype != a.dtype or tuple(out.shape) != (M, N):
@@ -1488,6 +1492,57 @@ def conv1x1_nhwc(x, w, bias=None, stride=(1, 1)):
     return Conv1x1Fn.apply(x, w, bias, int(stride[0]), int(stride[1]), _join_for(x))
 
 
+class Conv1x1StatsFn(torch.autograd.Function):
+    """1x1 convolution whose forward also returns the BatchNorm partial statistics of its output:
+    the forward runs on the implicit-GEMM conv kernel (kh = kw = 1; its epilogue emits the per-tile
+    shifted sums / sums of squares, as ConvKxKStatsFn), so the BN statistics pass over the output
+    disappears; the backward is Conv1x1Fn's (dgrad GEMM joined into the block input's gradient,
+    wgrad accumulated in place)."""
+
+    @staticmethod
+    def forward(ctx, x, w, sh, sw, join, shift):
+        ctx.join = join
+        xs = x if (sh, sw) == (1, 1) else x[:, ::sh, ::sw, :]
+        xs = xs.contiguous()
+        n, h, wd, cin = xs.shape
+        cout = w.shape[0]
+        w2 = w.reshape(cout, cin)
+        y, part = _conv_lds(xs, w2, None, 1, 1, 1, 0, stats_shift=shift)
+        ctx.save_for_backward(xs.view(-1, cin), w2)
+        ctx.w = w
+        ctx.meta = (tuple(x.shape), tuple(xs.shape), tuple(w.shape), sh, sw, False)
+        ctx.mark_non_differentiable(part)
+        return y, part
+
+    @staticmethod
+    def backward(ctx, dy, dpart):
+        dx, dw, _, _, _, _ = Conv1x1Fn.backward(ctx, dy)
+        return dx, dw, None, None, None, None
+
+
+_CONV1X1_STATS = __import__('os').environ.get('PRA_CONV1X1_STATS', '1') == '1'
+
+
+def conv1x1_bn_stats_ok(x, w, stride, padding, rmean, training):
+    """1x1 conv + BN statistics in the conv epilogue (conv_bn_act_nhwc): channels-last half
+    input with C % 64 == 0 (the implicit-GEMM kernel's K step), fp32 running mean, HIP BN."""
+    return bool(_CONV1X1_STATS and _CONV_BN_STATS and training and padding == 0 and rmean is not None
+                and rmean.dtype == torch.float32 and rmean.is_contiguous() and rmean.numel() == w.shape[0]
+                and tuple(w.shape[2:]) == (1, 1) and x.is_cuda and x.dim() == 4 and x.dtype in _HALF
+                and w.dtype == x.dtype and x.shape[3] == w.shape[1] and x.shape[3] % 64 == 0
+                and w.shape[0] % 8 == 0 and x.numel() * 2 < 2 ** 31
+                and _conv1x1_stats_shape(x, w, stride)
+                and R.select_backend(x, 'batch_norm_fwd') == 'hip')
+
+
+def _conv1x1_stats_shape(x, w, stride):
+    """Shapes where the fused path measured faster forward+backward than hipBLASLt + the separate
+    statistics pass (profiles/r3g/conv1x1_bn_shapes.md, ResNet-50 bs 256): the 14x14 / 7x7 stages
+    and the wide (>= 512 channel) 28x28 outputs; the 56x56 stage stays on the library GEMM."""
+    m = x.shape[0] * ((x.shape[1] - 1) // stride + 1) * ((x.shape[2] - 1) // stride + 1)
+    return m <= 65536 or (m <= 262144 and w.shape[0] >= 512)
+
+
 # =============================================================================
 # KxK convolution (channels-last, groups 1, dilation 1) as an implicit GEMM on the LDS-DMA MFMA
 # kernel (gemm_lds.hip ConvDmaA): the im2col rows are gathered from the NHWC input by the
@@ -1636,6 +1691,10 @@ def conv_bn_act_nhwc(x, w, stride, padding, bn_w, bn_b, rmean, rvar, training, m
     shape is outside the kernel or statistics are not needed (eval)."""
     if conv_bn_stats_ok(x, w, stride, padding, rmean, training):
         y, part = ConvKxKStatsFn.apply(x, w, None, int(stride), int(padding), rmean)
+        return BatchNormActFn.apply(y, z, bn_w, bn_b, rmean, rvar, training, momentum, eps, relu,
+                                    _join_for(z) if z is not None else None, (part, rmean))
+    if conv1x1_bn_stats_ok(x, w, stride, padding, rmean, training):
+        y, part = Conv1x1StatsFn.apply(x, w, int(stride), int(stride), _join_for(x), rmean)
         return BatchNormActFn.apply(y, z, bn_w, bn_b, rmean, rvar, training, momentum, eps, relu,
                                     _join_for(z) if z is not None else None, (part, rmean))
     if w.shape[2] == w.shape[3] > 1 and conv_kxk_supported(x, w, stride, padding):
@@ -1866,8 +1925,8 @@ def _dgelu_db(dh, z, approximate, b=None):
 def mlp_gelu(x, w1, b1, w2, approximate=True):
     """gelu(x·W1 + b1)·W2 with the bias+GELU (and its backward) inside the GEMM epilogues."""
     if all(t.requires_grad for t in (w1, b1, w2)) and torch.is_grad_enabled() and \
-            all(t.is_leaf for t in (w1, b1, w2)) and x.dtype == w1.dtype and x.is_cuda and \
-            not torch.is_autocast_enabled(x.device.type):
+            all(t.is_leaf for t in (w1, b1, w2)) and x.dtype == w1.dtype == w2.dtype == b1.dtype and \
+            x.is_cuda and _no_autocast_change(x, w1):
         return MlpGeluFn.apply(x, w1, b1, w2, approximate)
     return linear(bias_gelu(linear(x, w1), b1, approximate), w2)
 

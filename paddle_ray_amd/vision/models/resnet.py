@@ -95,11 +95,16 @@ class BottleneckBlock(nn.Layer):
         # downsample conv or the residual add) instead of summed by separate add kernels
         with _grad_join(x._t):
             identity = x
-            out = _bn_act(self.bn1, self.conv1(x))
+            # every conv + BN pair takes its BN statistics from the conv epilogue (1x1 and 3x3)
+            out = _conv_bn_act(self.conv1, self.bn1, x)
             out = _conv_bn_act(self.conv2, self.bn2, out)
             if self.downsample is not None:
-                identity = self.downsample(x)
-            return _bn_act(self.bn3, self.conv3(out), identity)
+                ds = self.downsample
+                if len(ds) == 2 and isinstance(ds[0], nn.Conv2D):
+                    identity = _conv_bn_act(ds[0], ds[1], x, act=None)
+                else:
+                    identity = ds(x)
+            return _conv_bn_act(self.conv3, self.bn3, out, identity)
 
 
 class ResNet(nn.Layer):

@@ -25,6 +25,19 @@ SHAPES = [  # (name, layout, M, N, K)
     ('head.fwd', 1, T, 50304, 2048), ('head.dgrad', 0, T, 2048, 50304), ('head.wgrad', 2, 50304, 2048, T),
 ]
 
+# BERT-base (hidden 768, FFN 3072, bs 32 x 512 tokens; MLM head on 32 x 80 masked rows): --bert
+SHAPES_BERT = [
+    ('qkv.fwd', 0, T, 2304, 768), ('out.fwd', 0, T, 768, 768), ('fc1.fwd', 0, T, 3072, 768),
+    ('fc2.fwd', 0, T, 768, 3072),
+    ('qkv.dgrad', 1, T, 768, 2304), ('out.dgrad', 1, T, 768, 768), ('fc1.dgrad', 1, T, 768, 3072),
+    ('fc2.dgrad', 1, T, 3072, 768),
+    ('qkv.wgrad', 2, 768, 2304, T), ('out.wgrad', 2, 768, 768, T), ('fc1.wgrad', 2, 768, 3072, T),
+    ('fc2.wgrad', 2, 3072, 768, T),
+    ('mlm.fwd', 1, 2560, 30522 // 8 * 8, 768),
+]
+if '--bert' in sys.argv:
+    SHAPES = SHAPES_BERT
+
 
 def operands(layout, M, N, K, dev):
     g = torch.Generator(device=dev).manual_seed(M * 7 + N * 3 + K)
