@@ -8,6 +8,14 @@
 // torch.cuda.memory.CUDAPluggableAllocator (pra_alloc / pra_free) so every framework tensor
 // comes from it when enabled; statistics feed paddle.device.cuda.memory_* .
 //
+// Graph-capture pools: while a HIP graph is being captured, allocations on the capturing
+// streams come from a private arena keyed by the graph's pool id (the reference's
+// CUDAGraph-private memory pools; PyTorch's beginAllocateToPool / endAllocateToPool /
+// releasePool): blocks the graph uses are never handed to eager code, frees inside the capture
+// are reused in stream order within the same arena, and the arena's memory returns to the device
+// when the pool is released and its last block freed. No events are recorded for pool blocks (a
+// capturing stream cannot be queried). torch_hooks.cpp wires these entry points into PyTorch.
+//
 // Built twice: with hipcc against the HIP runtime (the real allocator), and with
 // -DPRA_ALLOC_HOST against malloc so the block bookkeeping is unit-tested on the CPU.
 #include <algorithm>
@@ -49,8 +57,22 @@ static void device_sync() {
 #include <hip/hip_runtime.h>
 typedef hipStream_t stream_t;
 typedef hipEvent_t event_t;
-static int backend_malloc(void** p, size_t n) { return hipMalloc(p, n) == hipSuccess ? 0 : 1; }
-static void backend_free(void* p) { (void)hipFree(p); }
+// hipMalloc / hipFree / hipDeviceSynchronize while a stream capture is open on this thread:
+// relaxed capture mode for the call (as PyTorch's caching allocator does), else the runtime
+// invalidates the capture ("potentially unsafe API" under the default global mode)
+struct RelaxedCapture {
+  hipStreamCaptureMode m = hipStreamCaptureModeRelaxed;
+  RelaxedCapture() { (void)hipThreadExchangeStreamCaptureMode(&m); }
+  ~RelaxedCapture() { (void)hipThreadExchangeStreamCaptureMode(&m); }
+};
+static int backend_malloc(void** p, size_t n) {
+  RelaxedCapture g;
+  return hipMalloc(p, n) == hipSuccess ? 0 : 1;
+}
+static void backend_free(void* p) {
+  RelaxedCapture g;
+  (void)hipFree(p);
+}
 static void backend_set_device(int d) { (void)hipSetDevice(d); }
 static event_t event_record(stream_t s) {
   event_t e = nullptr;
@@ -62,7 +84,10 @@ static bool event_done(event_t e) { return e == nullptr || hipEventQuery(e) == h
 static void event_destroy(event_t e) {
   if (e) (void)hipEventDestroy(e);
 }
-static void device_sync() { (void)hipDeviceSynchronize(); }
+static void device_sync() {
+  RelaxedCapture g;
+  (void)hipDeviceSynchronize();
+}
 #endif
 
 namespace {
@@ -96,6 +121,8 @@ struct Stats {
 struct DeviceAllocator {
   std::mutex mu;
   size_t growth = size_t(64) << 20;  // minimum chunk size
+  bool pool = false;                 // a graph-capture arena: no events, stream-order reuse only
+  bool released = false;             // pool released while blocks were still live
   // Events only matter once a second stream allocates: until then every block is reused in
   // stream order and frees record nothing. When a second stream first shows up the device
   // is synchronised once (all earlier, event-less frees are then complete).
@@ -117,6 +144,7 @@ struct DeviceAllocator {
   }
 
   void note_stream(stream_t s) {
+    if (pool) return;
     if (!seen_stream) {
       seen_stream = true;
       first_stream = s;
@@ -126,7 +154,7 @@ struct DeviceAllocator {
     }
   }
   event_t new_event(stream_t s) {
-    if (!multi_stream) return nullptr;
+    if (!multi_stream || pool) return nullptr;
 #ifdef PRA_ALLOC_HOST
     return event_record(s);
 #else
@@ -288,6 +316,8 @@ struct DeviceAllocator {
     insert_free(b);
   }
 
+  size_t live_count() const { return live.size(); }
+
   // bookkeeping invariant check (tests): blocks tile every chunk exactly, free sets agree
   bool check() {
     std::lock_guard<std::mutex> g(mu);
@@ -317,6 +347,11 @@ struct DeviceAllocator {
 
 std::mutex g_mu;
 std::map<int, DeviceAllocator*> g_dev;
+// graph-capture arenas per (device, pool id), and which arena owns each live pointer
+typedef std::pair<uint64_t, uint64_t> PoolId;
+std::map<std::pair<int, PoolId>, DeviceAllocator*> g_pools;
+std::mutex g_own_mu;
+std::unordered_map<void*, DeviceAllocator*> g_owner;
 
 DeviceAllocator* dev(int d) {
   std::lock_guard<std::mutex> g(g_mu);
@@ -326,6 +361,42 @@ DeviceAllocator* dev(int d) {
   if (const char* e = std::getenv("PRA_ALLOC_CHUNK_MB")) a->growth = size_t(std::atoll(e)) << 20;
   g_dev[d] = a;
   return a;
+}
+
+DeviceAllocator* pool_of(int d, PoolId id, bool create) {
+  std::lock_guard<std::mutex> g(g_mu);
+  auto key = std::make_pair(d, id);
+  auto it = g_pools.find(key);
+  if (it != g_pools.end()) return it->second;
+  if (!create) return nullptr;
+  DeviceAllocator* a = new DeviceAllocator();
+  a->pool = true;
+  a->growth = size_t(64) << 20;  // arenas grow like the device arena (64 MB chunks)
+  g_pools[key] = a;
+  return a;
+}
+
+// a released pool whose last block went away: return its memory to the device
+void maybe_drop_pool(int d, DeviceAllocator* a) {
+  bool drop = false;
+  {
+    std::lock_guard<std::mutex> g(a->mu);
+    drop = a->released && a->live_count() == 0;
+  }
+  if (!drop) return;
+  {
+    std::lock_guard<std::mutex> g(g_mu);
+    for (auto it = g_pools.begin(); it != g_pools.end(); ++it)
+      if (it->second == a && it->first.first == d) {
+        g_pools.erase(it);
+        break;
+      }
+  }
+  {
+    std::lock_guard<std::mutex> g(a->mu);
+    a->release_free_chunks();
+  }
+  delete a;
 }
 
 }  // namespace
@@ -338,7 +409,61 @@ void* pra_alloc(size_t size, int device, stream_t stream) {
 }
 void pra_free(void* ptr, size_t size, int device, stream_t stream) {
   (void)size;
+  DeviceAllocator* owner = nullptr;
+  {
+    std::lock_guard<std::mutex> g(g_own_mu);
+    auto it = g_owner.find(ptr);
+    if (it != g_owner.end()) {
+      owner = it->second;
+      g_owner.erase(it);
+    }
+  }
+  if (owner) {
+    owner->free_(ptr, stream);
+    maybe_drop_pool(device, owner);
+    return;
+  }
   dev(device)->free_(ptr, stream);
+}
+// graph-capture arenas (pool id = PyTorch's MempoolId_t pair)
+void* pra_alloc_pool(size_t size, int device, stream_t stream, uint64_t id0, uint64_t id1) {
+  backend_set_device(device);
+  DeviceAllocator* a = pool_of(device, PoolId(id0, id1), true);
+  void* p = a->alloc(size, stream);
+  if (p) {
+    std::lock_guard<std::mutex> g(g_own_mu);
+    g_owner[p] = a;
+  }
+  return p;
+}
+// the graph (and every private-pool user) is gone: free the arena once its blocks are
+void pra_pool_release(int device, uint64_t id0, uint64_t id1) {
+  DeviceAllocator* a = pool_of(device, PoolId(id0, id1), false);
+  if (!a) return;
+  {
+    std::lock_guard<std::mutex> g(a->mu);
+    a->released = true;
+  }
+  maybe_drop_pool(device, a);
+}
+// reserved / allocated bytes and arena count of the live pools of a device
+void pra_pool_stats(int device, int64_t* out) {
+  std::lock_guard<std::mutex> g(g_mu);
+  int64_t res = 0, used = 0, n = 0;
+  for (auto& kv : g_pools)
+    if (kv.first.first == device) {
+      std::lock_guard<std::mutex> g2(kv.second->mu);
+      res += kv.second->st.reserved;
+      used += kv.second->st.allocated;
+      n++;
+    }
+  out[0] = used;
+  out[1] = res;
+  out[2] = n;
+}
+int pra_pool_check(int device, uint64_t id0, uint64_t id1) {
+  DeviceAllocator* a = pool_of(device, PoolId(id0, id1), false);
+  return a ? (a->check() ? 1 : 0) : -1;
 }
 // stats: allocated, reserved, peak_allocated, peak_reserved, n_alloc, n_free, n_chunks,
 // n_backend_alloc, n_backend_free

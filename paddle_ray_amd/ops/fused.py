@@ -1274,7 +1274,7 @@ def _gemm_hip(layout, a, b, out=None, bias=None, z=None, epi=None, beta=0, want_
     Returns None when the shape/layout is outside what the kernel assumes (caller falls back)."""
     if _GEMM_MODE == 'blas' or not (_gemm_operand_ok(a) and _gemm_operand_ok(b)) or a.dtype != b.dtype:
         return None
-    if _GEMM_MODE == 'auto' and layout == GEMM_NT:
+    if _GEMM_MODE == 'auto' and layout == GEMM_NT and not (_MLP_DGELU_EPI and epi in ('dgelu', 'dgelu_tanh')):
         return None
     if layout == GEMM_FWD:
         M, K = a.shape
@@ -1293,9 +1293,7 @@ def _gemm_hip(layout, a, b, out=None, bias=None, z=None, epi=None, beta=0, want_
         # skinny decode-time forwards (M < 128: a 256-row tile idles) go to the library
         if layout == GEMM_FWD and M < 128:
             return None
-        # forward GEMMs that would need split-K (few 256x256 tiles over a long K: BERT's fc2
-        # 16384x768x3072 ran 138.7 us split 4-ways vs 73.6 us in hipBLASLt, profiles/r3g)
-        if layout == GEMM_FWD and ((M + 255) // 256) * ((N + 255) // 256) < 224 and K // 64 >= 16:
+        if _gemm_prefers_library(layout, M, N, K):
             return None
     if out is None:
         out = torch.empty((M, N), device=a.device, dtype=a.dtype)
@@ -1325,6 +1323,12 @@ def _gemm_hip(layout, a, b, out=None, bias=None, z=None, epi=None, beta=0, want_
     return out
 
 
+def _gemm_prefers_library(layout, M, N, K):
+    """Forward GEMMs that would need split-K (few 256x256 tiles over a long K): BERT's fc2
+    16384x768x3072 ran 138.7 us split 4-ways vs 73.6 us in hipBLASLt (profiles/r3g)."""
+    return layout == GEMM_FWD and ((M + 255) // 256) * ((N + 255) // 256) < 224 and K // 64 >= 16
+
+
 def gemm(layout, a, b, out=None, bias=None, z=None, epi=None, beta=0, want_colsum=False):
     """C (=|+=) epi(op(a)·op(b) + bias). layout: GEMM_FWD a[M,K]·b[K,N]; GEMM_NT a[M,K]·b[N,K]ᵀ;
     GEMM_TN a[K,M]ᵀ·b[K,N]. On the device this is the in-tree MFMA kernel; shapes it does not
@@ -1333,7 +1337,12 @@ def gemm(layout, a, b, out=None, bias=None, z=None, epi=None, beta=0, want_colsu
         r = _gemm_hip(layout, a, b, out, bias, z, epi, beta, want_colsum)
         if r is not None:
             return r
-        R._STATS[('gemm', 'hipblaslt' if _GEMM_MODE == 'auto' and layout == GEMM_NT else 'fallback')] += 1
+        lib = _GEMM_MODE == 'auto' and (layout == GEMM_NT or (
+            _GEMM_SHAPE_POLICY and epi is None and not want_colsum and a.dim() == 2 and
+            _gemm_prefers_library(layout, a.shape[0] if layout != GEMM_TN else a.shape[1],
+                                  b.shape[1] if layout != GEMM_NT else b.shape[0],
+                                  a.shape[1] if layout != GEMM_TN else a.shape[0])))
+        R._STATS[('gemm', 'hipblaslt' if lib else 'fallback')] += 1
     return _gemm_ref_fast(layout, a, b, out, bias, z, epi, beta, want_colsum)
 
 
@@ -1851,6 +1860,12 @@ def linear_nt(x2, w):
     return torch.mm(x2, w.t())
 
 
+# fc2 dgrad of the GELU MLP on the in-tree NT GEMM with gelu'(z) and the fc1 bias-gradient
+# column sums in its epilogue (PRA_MLP_DGELU_EPI=1) instead of hipBLASLt + bias_gelu_bwd_db
+# (measured on GPT-1.3B: 123.0K vs 124.4K tokens/s, twice on one box: off by default)
+_MLP_DGELU_EPI = __import__('os').environ.get('PRA_MLP_DGELU_EPI', '0') == '1'
+
+
 class MlpGeluFn(torch.autograd.Function):
     """y = gelu(x·W1 + b1)·W2 (fc2 bias left to the caller's fused residual kernel).
 
@@ -1879,7 +1894,7 @@ class MlpGeluFn(torch.autograd.Function):
         if not dy2.is_contiguous():
             dy2 = dy2.contiguous()
         x2 = x.reshape(-1, x.shape[-1])
-        if _GEMM_MODE == 'auto':
+        if _GEMM_MODE == 'auto' and not _MLP_DGELU_EPI:
             # dgrad on hipBLASLt, then ONE fused pass for gelu'(z) and the bias gradient
             dh = torch.mm(dy2, w2.t())
             dz, db1 = _dgelu_db(dh, z, ctx.approximate, ctx.b1)

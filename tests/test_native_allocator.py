@@ -142,3 +142,97 @@ def test_split_remainder_keeps_pending_gate(lib):
     finally:
         lib.pra_alloc_host_set_pending(0)
         lib.pra_alloc_host_complete_events()
+
+
+def test_pool_arena_host_bookkeeping(lib):
+    """Graph-capture arenas (host build): pool blocks come from their own chunks, are reused
+    inside the pool, never mix with the device arena, and the pool's memory goes back once it
+    is released and its last block freed."""
+    dev = 51
+    lib.pra_alloc_pool.restype = ctypes.c_void_p
+    lib.pra_alloc_pool.argtypes = [ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64,
+                                   ctypes.c_uint64]
+    lib.pra_pool_release.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64]
+    lib.pra_pool_check.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64]
+    e = _alloc(lib, dev, MB)
+    p1 = lib.pra_alloc_pool(MB, dev, None, 7, 0)
+    p2 = lib.pra_alloc_pool(3 * MB, dev, None, 7, 0)
+    assert p1 and p2 and not (e <= p1 < e + MB)
+    st = A.stats(dev, lib)
+    assert st['num_pools'] == 1 and st['pool_allocated'] >= 4 * MB and st['allocated'] == MB
+    lib.pra_free(p1, MB, dev, None)                       # freed inside the pool ...
+    p3 = lib.pra_alloc_pool(3 * MB // 2, dev, None, 7, 0)   # ... and reused by it (best fit)
+    assert p3 == p1
+    e2 = _alloc(lib, dev, 512 << 10)                       # the device arena never gets pool memory
+    assert not (p1 <= e2 < p1 + 4 * MB)
+    assert lib.pra_pool_check(dev, 7, 0) == 1
+    lib.pra_pool_release(dev, 7, 0)                         # graph gone, blocks still live
+    assert A.stats(dev, lib)['num_pools'] == 1
+    lib.pra_free(p2, 3 * MB, dev, None)
+    lib.pra_free(p3, 3 * MB // 2, dev, None)                # last block: the arena is dropped
+    st = A.stats(dev, lib)
+    assert st['num_pools'] == 0 and st['pool_reserved'] == 0
+    for p, n in ((e, MB), (e2, 512 << 10)):
+        lib.pra_free(p, n, dev, None)
+    assert lib.pra_alloc_check(dev) == 1
+
+
+_GPU_GRAPH_SCRIPT = r'''
+import torch
+import paddle_ray_amd as paddle
+from paddle_ray_amd.native import allocator as A
+assert A.enabled()
+x = torch.randn(1024, 1024, device='cuda')
+s = torch.cuda.Stream()
+s.wait_stream(torch.cuda.current_stream())
+with torch.cuda.stream(s):
+    for _ in range(2):
+        y = (x @ x).relu() @ x
+torch.cuda.current_stream().wait_stream(s)
+g = torch.cuda.CUDAGraph()
+with torch.cuda.graph(g):
+    t = (x @ x).relu()        # an intermediate freed inside the capture
+    y = t @ x
+    del t
+st = A.stats(0)
+assert st['num_pools'] == 1 and st['pool_allocated'] > 0, st
+eager = [torch.empty(1024, 1024, device='cuda') for _ in range(8)]   # never inside the pool
+g.replay()
+ref = (x @ x).relu() @ x
+torch.cuda.synchronize()
+assert torch.allclose(y, ref, rtol=1e-3, atol=1e-2)
+for e in eager:
+    e.fill_(7.0)
+g.replay(); torch.cuda.synchronize()
+assert torch.allclose(y, ref, rtol=1e-3, atol=1e-2)   # eager writes did not land in graph memory
+before = A.stats(0)['pool_allocated']
+del g, y
+import gc; gc.collect(); torch.cuda.synchronize()
+st = A.stats(0)
+# the graph's blocks went back (its arena stays while the BLAS workspace it created lives)
+assert st['pool_allocated'] < before, (before, st)
+# a jit.to_static training graph (forward + backward captured) on the native allocator
+from paddle_ray_amd.models import gpt_config, GPTForPretraining
+paddle.set_device('gpu:0')
+paddle.seed(0)
+m = GPTForPretraining(gpt_config('gpt3-tiny', hidden_dropout=0.0, attention_dropout=0.0))
+opt = paddle.optimizer.AdamW(1e-3, parameters=m.parameters())
+st = paddle.static.BuildStrategy(); st.use_hip_graph = True
+mg = paddle.jit.to_static(m, build_strategy=st)
+ids = paddle.randint(0, 1024, [4, 65])
+losses = []
+for _ in range(5):
+    loss = mg(ids[:, :-1], ids[:, 1:])
+    loss.backward(); opt.step(); opt.clear_grad()
+    losses.append(float(loss))
+assert losses[-1] < losses[0], losses
+print('OK', losses, A.stats(0)['num_pools'])
+'''
+
+
+@pytest.mark.gpu
+def test_graph_capture_pools_on_native_allocator_gpu():
+    env = dict(os.environ, PRA_ALLOCATOR='auto_growth')
+    r = subprocess.run([sys.executable, '-c', _GPU_GRAPH_SCRIPT], env=env, capture_output=True, text=True,
+                       timeout=300, cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    assert r.returncode == 0 and 'OK' in r.stdout, r.stdout[-2000:] + r.stderr[-3000:]
