@@ -110,13 +110,19 @@ class _GraphEntry:
         with torch.cuda.graph(self.graph):
             self.out = fn(*sargs, **skw)
 
-    def __call__(self, args, kwargs):
+    def replay_static(self, args, kwargs):
+        """Replay and return the graph's STATIC output buffers (rewritten by the next replay):
+        for callers that consume them before replaying again (the static Executor's optimizer
+        step reads the captured gradients in place)."""
         for buf, t in zip(self.static_in, _flat_tensors((args, kwargs), [])):
             buf.copy_(t._t, non_blocking=True)
         self.graph.replay()
+        return self.out
+
+    def __call__(self, args, kwargs):
         # the captured outputs are the graph's static buffers, rewritten by the next replay:
         # every call hands out its own copies (y1 = f(x1); y2 = f(x2) keeps y1)
-        return _clone_struct(self.out)
+        return _clone_struct(self.replay_static(args, kwargs))
 
 
 def _clone_struct(o):

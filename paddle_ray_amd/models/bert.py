@@ -105,15 +105,22 @@ class BertEmbeddings(nn.Layer):
     def forward(self, input_ids, token_type_ids=None, position_ids=None, task_type_ids=None,
                 past_key_values_length=None):
         ids = _u(input_ids)
-        if position_ids is None:
-            pos = torch.arange(ids.shape[-1], device=ids.device).unsqueeze(0)
-            if past_key_values_length:
-                pos = pos + past_key_values_length
+        S = ids.shape[-1]
+        x = _u(self.word_embeddings(Tensor(ids)))
+        # default position / token-type ids index the SAME rows for every sequence: a broadcast
+        # add of the table slice (its gradient is a sum over the batch) instead of a lookup whose
+        # backward sorts 16K copies of a few ids (a 16K-long run for token type 0)
+        off = int(past_key_values_length or 0)
+        if position_ids is None and off + S <= self.position_embeddings.weight.shape[0]:
+            x = x + _u(self.position_embeddings.weight)[off:off + S]
         else:
-            pos = _u(position_ids)
-        x = _u(self.word_embeddings(Tensor(ids))) + _u(self.position_embeddings(Tensor(pos)))
-        tt = torch.zeros_like(ids) if token_type_ids is None else _u(token_type_ids)
-        x = x + _u(self.token_type_embeddings(Tensor(tt)))
+            pos = _u(position_ids) if position_ids is not None else \
+                (torch.arange(S, device=ids.device) + off).unsqueeze(0)
+            x = x + _u(self.position_embeddings(Tensor(pos)))
+        if token_type_ids is None:
+            x = x + _u(self.token_type_embeddings.weight)[0]
+        else:
+            x = x + _u(self.token_type_embeddings(Tensor(_u(token_type_ids))))
         if self.use_task_id:
             tk = torch.zeros_like(ids) if task_type_ids is None else _u(task_type_ids)
             x = x + _u(self.task_type_embeddings(Tensor(tk)))

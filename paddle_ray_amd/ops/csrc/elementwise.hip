@@ -18,7 +18,7 @@ __device__ __forceinline__ float gelu_f(float x, int approx) {
     float t = tanh_fast(k0 * (x + k1 * x * x * x));
     return 0.5f * x * (1.f + t);
   }
-  return 0.5f * x * (1.f + erff(x * 0.7071067811865476f));
+  return gelu_erf_fast(x);
 }
 __device__ __forceinline__ float gelu_df(float x, int approx) {
   if (approx) {
@@ -26,7 +26,7 @@ __device__ __forceinline__ float gelu_df(float x, int approx) {
     float t = tanh_fast(k0 * (x + k1 * x * x * x));
     return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k0 * (1.f + 3.f * k1 * x * x);
   }
-  return 0.5f * (1.f + erff(x * 0.7071067811865476f)) + x * 0.3989422804014327f * __expf(-0.5f * x * x);
+  return dgelu_erf_fast(x);
 }
 
 template <typename T>

@@ -51,7 +51,7 @@ enum Act : int { kNone = 0, kGeluErf = 1, kGeluTanh = 2, kRelu = 3 };
 
 template <int ACT>
 __device__ __forceinline__ float act(float x) {
-  if (ACT == kGeluErf) return 0.5f * x * (1.f + erff(x * 0.70710678118654752f));
+  if (ACT == kGeluErf) return gelu_erf_fast(x);
   if (ACT == kGeluTanh) return 0.5f * x * (1.f + tanhf(0.79788456080286536f * (x + 0.044715f * x * x * x)));
   if (ACT == kRelu) return fmaxf(x, 0.f);
   return x;

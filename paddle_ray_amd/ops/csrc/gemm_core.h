@@ -67,10 +67,8 @@ __device__ __forceinline__ float dgelu_tanh(float x) {
   const float t = fast_tanh(u);
   return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * 0.79788456080286536f * (1.f + 0.134145f * x * x);
 }
-__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
-__device__ __forceinline__ float dgelu_erf(float x) {
-  return 0.5f * (1.f + erff(x * 0.70710678118654752f)) + x * 0.3989422804014327f * __expf(-0.5f * x * x);
-}
+__device__ __forceinline__ float gelu_erf(float x) { return gelu_erf_fast(x); }
+__device__ __forceinline__ float dgelu_erf(float x) { return dgelu_erf_fast(x); }
 
 template <int E>
 __device__ __forceinline__ float act(float x) {

@@ -869,7 +869,9 @@ class Executor:
                 else:
                     with torch.no_grad():
                         g = cache[key] = _GraphEntry(fn, tuple(vals), {})
-            res = g(tuple(vals), {})
+            # static buffers: the fetches are copied out here, the gradients feed the optimizer
+            # ops below before the next replay (no per-step clone of every gradient)
+            res = g.replay_static(tuple(vals), {})
             outs = [Tensor(o._t.clone()) for o in res[:nf]]
             if opt_ops:
                 genv = {v.vid: t for v, t in zip(opt_in, res[nf:])}

@@ -161,7 +161,7 @@ def test_pool_arena_host_bookkeeping(lib):
     st = A.stats(dev, lib)
     assert st['num_pools'] == 1 and st['pool_allocated'] >= 4 * MB and st['allocated'] == MB
     lib.pra_free(p1, MB, dev, None)                       # freed inside the pool ...
-    p3 = lib.pra_alloc_pool(3 * MB // 2, dev, None, 7, 0)   # ... and reused by it (best fit)
+    p3 = lib.pra_alloc_pool(MB, dev, None, 7, 0)            # ... and reused by it (best fit)
     assert p3 == p1
     e2 = _alloc(lib, dev, 512 << 10)                       # the device arena never gets pool memory
     assert not (p1 <= e2 < p1 + 4 * MB)
@@ -169,7 +169,7 @@ def test_pool_arena_host_bookkeeping(lib):
     lib.pra_pool_release(dev, 7, 0)                         # graph gone, blocks still live
     assert A.stats(dev, lib)['num_pools'] == 1
     lib.pra_free(p2, 3 * MB, dev, None)
-    lib.pra_free(p3, 3 * MB // 2, dev, None)                # last block: the arena is dropped
+    lib.pra_free(p3, MB, dev, None)                         # last block: the arena is dropped
     st = A.stats(dev, lib)
     assert st['num_pools'] == 0 and st['pool_reserved'] == 0
     for p, n in ((e, MB), (e2, 512 << 10)):
