@@ -38,6 +38,7 @@ void pra_bias_gelu_fwd(const void*, const void*, void*, int64_t, int, int, int, 
 void pra_bias_gelu_bwd(const void*, const void*, const void*, void*, int64_t, int, int, int, hipStream_t);
 void pra_adamw_mt(const int64_t*, const float*, const int64_t*, int, float, float, float, float, float, float, float,
                   const float*, hipStream_t);
+void pra_zero_mt(const int64_t*, int, hipStream_t);
 void pra_momentum_mt(const int64_t*, const float*, const int64_t*, int, float, float, int, float, const float*,
                      hipStream_t);
 void pra_sumsq_accum(const void*, float*, int64_t, int, hipStream_t);
@@ -222,6 +223,10 @@ PYBIND11_MODULE(_pra_hip, m) {
   m.def("bias_gelu_bwd", [](P dy, P x, P b, P dx, int64_t rows, int cols, int dt, int approx, P s) {
     pra_bias_gelu_bwd(CV(dy), CV(x), CV(b), V(dx), rows, cols, dt, approx, S(s));
     check_launch("bias_gelu_bwd");
+  });
+  m.def("zero_mt", [](P chunks, int n, P s) {
+    pra_zero_mt(I64(chunks), n, S(s));
+    check_launch("zero_mt");
   });
   m.def("adamw_mt", [](P tab, P ftab, P chunks, int nch, float lr, float b1, float b2, float eps, float bc1, float bc2,
                        float gs, P s, P gsp) {

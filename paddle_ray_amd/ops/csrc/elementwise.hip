@@ -280,6 +280,17 @@ __global__ void __launch_bounds__(256) adamw_mt_k(const int64_t* __restrict__ ta
   }
 }
 
+// Multi-tensor zero fill (optimizer.clear_grad): one launch for every gradient instead of one
+// fill kernel per tensor (ResNet-50: ~180 tiny launches per step). ch[2b] = address of block b's
+// piece, ch[2b + 1] = its byte count (<= 64 KB); 16-B stores where aligned, bytes for the tail.
+__global__ void __launch_bounds__(256) zero_mt_k(const int64_t* __restrict__ ch) {
+  char* p = reinterpret_cast<char*>(ch[2 * blockIdx.x]);
+  const int64_t n = ch[2 * blockIdx.x + 1];
+  const int64_t n16 = (reinterpret_cast<uintptr_t>(p) & 15) == 0 ? n / 16 : 0;
+  for (int64_t i = threadIdx.x; i < n16; i += blockDim.x) reinterpret_cast<uint4*>(p)[i] = make_uint4(0, 0, 0, 0);
+  for (int64_t i = n16 * 16 + threadIdx.x; i < n; i += blockDim.x) p[i] = 0;
+}
+
 // tab[t] = {master_or_param, grad, velocity, 0, lowp, n, gdt, pdt}; ftab = {wd, lr_mul}
 __global__ void __launch_bounds__(256) momentum_mt_k(const int64_t* __restrict__ tab, const float* __restrict__ ftab,
                                                      const int64_t* __restrict__ chunks, float lr, float mu,
@@ -417,6 +428,9 @@ void pra_adamw_mt(const int64_t* tab, const float* ftab, const int64_t* chunks, 
   if (!nchunks) return;
   hipLaunchKernelGGL(adamw_mt_k, dim3(nchunks), dim3(256), 0, s, tab, ftab, chunks, lr, b1, b2, eps, bc1, bc2,
                      gscale, gscale_ptr);
+}
+void pra_zero_mt(const int64_t* chunks, int nchunks, hipStream_t s) {
+  if (nchunks > 0) hipLaunchKernelGGL(zero_mt_k, dim3(nchunks), dim3(256), 0, s, chunks);
 }
 void pra_momentum_mt(const int64_t* tab, const float* ftab, const int64_t* chunks, int nchunks, float lr, float mu,
                      int nesterov, float gscale, const float* gscale_ptr, hipStream_t s) {

@@ -240,26 +240,31 @@ extern "C" int pra_conv_wgrad_lds(const void* dy, const void* x, void* dW, int N
 extern "C" int pra_gemm_lds_splits(int M, int N, int K);
 extern "C" int pra_conv_lds_splits(int M, int Cout, int K) { return Cout <= 128 ? 1 : pra_gemm_lds_splits(M, Cout, K); }
 
-// Split-K factor for a problem: 1 unless the tile grid leaves CUs idle (fewer than ~256 tiles on
-// a long K loop); then the factor that best fills whole rounds of 256 workgroups.
+// Split-K factor for a problem: 1 unless the tile grid leaves CUs idle (fewer than ~224 tiles
+// on a K loop of >= 16 steps); then the factor that minimises a simple time model:
+//   rounds of 256 workgroups x (K-steps per split x 1.5 us + 3 us per-tile overhead)
+//   + the fp32 partial round trip through HBM ((splits + 1) x M x N x 4 B at 5 TB/s),
+// each split keeping >= 8 K-steps and the workspace <= 256 MB. The model reproduces the measured
+// BERT wgrad times (profiles/r3g/gemm_bert_shapes.md: 768x768x16384 55 vs 53 us at 8 splits) and
+// leaves every GPT-1.3B shape's factor unchanged; it lets few-tile / very-long-K products (BERT's
+// 768x768 wgrad, ResNet's 1x1 weight gradients) fill the chip instead of 8 splits x few tiles.
 extern "C" int pra_gemm_lds_splits(int M, int N, int K) {
   const int tiles = ((M + 255) / 256) * ((N + 255) / 256), nk = K / 64;
   if (tiles >= 224 || nk < 16) return 1;
   int best = 1;
-  double best_eff = 0.0;
-  for (int sp = 1; sp <= 8; ++sp) {
+  double best_t = 1e30;
+  for (int sp = 1; sp <= 256; ++sp) {
     if (nk / sp < 8) break;
-    const double w = (double)tiles * sp / 256.0;
-    const double eff = w / __builtin_ceil(w) * (1.0 - 0.03 * (sp - 1));
-    if (eff > best_eff + 1e-9) { best_eff = eff; best = sp; }
-  }
-  // few output tiles over a very long K (conv weight gradients: K = N*H*W up to ~800K):
-  // split further until the chip is covered, each split still >= 64 K-steps
-  if (tiles * best < 256 && nk / best >= 128) {
-    int sp = (256 + tiles - 1) / tiles;
-    if (sp > nk / 64) sp = nk / 64;
-    if (sp > 256) sp = 256;
-    if (sp > best) best = sp;
+    const double ws = (double)sp * M * N * 4.0;
+    if (sp > 1 && ws > 256.0 * (1 << 20)) break;
+    const double rounds = __builtin_ceil((double)tiles * sp / 256.0);
+    const double per = __builtin_ceil((double)nk / sp) * 1.5 + 3.0;
+    const double red = sp > 1 ? (double)(sp + 1) * M * N * 4.0 / 5e12 * 1e6 : 0.0;
+    const double t = rounds * per + red;
+    if (t < best_t - 1e-9) {
+      best_t = t;
+      best = sp;
+    }
   }
   return best;
 }

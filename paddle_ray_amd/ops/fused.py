@@ -1992,6 +1992,30 @@ def _mt_table(cols, n_list, extra_f, device, chunk=65536):
     return dev_tab, dev_f, dev_ch, len(chunks)
 
 
+_ZERO_PLAN = {}
+
+
+def zero_tensors(ts):
+    """Zero a list of device tensors in ONE launch (multi-tensor fill over a cached device table
+    of 64 KB pieces; the table is rebuilt only when the set of storages changes)."""
+    ts = [t for t in ts if t.numel()]
+    if not ts:
+        return
+    if not (ts[0].is_cuda and _native.available() and all(t.is_contiguous() and t.is_cuda for t in ts)):
+        torch._foreach_zero_(ts)
+        return
+    key = tuple((t.data_ptr(), t.numel() * t.element_size()) for t in ts)
+    plan = _ZERO_PLAN.get(key)
+    if plan is None:
+        import numpy as np
+        pieces = [(p + o, min(65536, n - o)) for p, n in key for o in range(0, n, 65536)]
+        tab = torch.from_numpy(np.array(pieces, dtype=np.int64).reshape(-1, 2)).to(ts[0].device)
+        if len(_ZERO_PLAN) > 8:
+            _ZERO_PLAN.clear()
+        plan = _ZERO_PLAN[key] = (tab, len(pieces))
+    _native.lib().zero_mt(_ptr(plan[0]), plan[1], _stream())
+
+
 @R.register_kernel('adamw_mt', 'hip')
 def _adamw_mt_hip(tab, ftab, ch, nch, lr, b1, b2, eps, bc1, bc2, grad_scale, scale_t, outs):
     """Multi-tensor AdamW over a device pointer table (one launch for every parameter);

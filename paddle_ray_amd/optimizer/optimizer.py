@@ -158,7 +158,8 @@ class Optimizer:
         if set_to_zero:
             gs = [p._t.grad for p in self._parameter_list if p._t.grad is not None]
             if gs:
-                torch._foreach_zero_(gs)  # multi-tensor launches, not one fill per parameter
+                from ..ops.fused import zero_tensors
+                zero_tensors(gs)  # one multi-tensor launch, not one fill per parameter
             return
         for p in self._parameter_list:
             p._t.grad = None
