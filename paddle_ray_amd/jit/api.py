@@ -107,8 +107,11 @@ class _GraphEntry:
                 fn(*sargs, **skw)
         torch.cuda.current_stream().wait_stream(s)
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
-            self.out = fn(*sargs, **skw)
+        from ..ops.fused import managed_graph_rng
+        with managed_graph_rng() as rng:
+            with torch.cuda.graph(self.graph):
+                self.out = fn(*sargs, **skw)
+        self.rng_dev = torch.device('cuda', torch.cuda.current_device()) if rng['used'] else None
 
     def replay_static(self, args, kwargs):
         """Replay and return the graph's STATIC output buffers (rewritten by the next replay):
@@ -116,6 +119,9 @@ class _GraphEntry:
         step reads the captured gradients in place)."""
         for buf, t in zip(self.static_in, _flat_tensors((args, kwargs), [])):
             buf.copy_(t._t, non_blocking=True)
+        if self.rng_dev is not None:  # new dropout masks for this replay
+            from ..ops.fused import graph_seq_advance
+            graph_seq_advance(self.rng_dev)
         self.graph.replay()
         return self.out
 
@@ -185,15 +191,19 @@ class _TrainGraph:
             torch.cuda.current_stream().wait_stream(s)
             pool = torch.cuda.graph_pool_handle()
             self.fwd_graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.fwd_graph, pool=pool):
-                out = fn(*sargs, **skw)
+            from ..ops.fused import managed_graph_rng
+            with managed_graph_rng() as rng:
+                with torch.cuda.graph(self.fwd_graph, pool=pool):
+                    out = fn(*sargs, **skw)
+            self.rng_dev = torch.device('cuda', torch.cuda.current_device()) if rng['used'] else None
             self.out_struct = out
             self.static_out = [o._t for o in _flat_tensors(out, [])]
             self.static_gout = [torch.empty_like(o) for o in self.static_out]
             self.bwd_graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.bwd_graph, pool=pool):
-                grads = torch.autograd.grad(self.static_out, wrt, self.static_gout,
-                                            allow_unused=True)
+            with managed_graph_rng():  # reads the forward's counter value, never advances it
+                with torch.cuda.graph(self.bwd_graph, pool=pool):
+                    grads = torch.autograd.grad(self.static_out, wrt, self.static_gout,
+                                                allow_unused=True)
             self.static_grads = [g if g is not None else None for g in grads]
         finally:
             for p, g in zip(ptens, saved_grads):
@@ -207,6 +217,9 @@ class _TrainGraph:
                 n_in = len(entry.static_in)
                 for buf, t in zip(entry.static_in, tensors[:n_in]):
                     buf.detach().copy_(t, non_blocking=True)
+                if entry.rng_dev is not None:  # new dropout masks for this step
+                    from ..ops.fused import graph_seq_advance
+                    graph_seq_advance(entry.rng_dev)
                 entry.fwd_graph.replay()
                 return tuple(o.detach() for o in entry.static_out)
 

@@ -196,21 +196,51 @@ def _dropout_seed():
 # launches pass a null pointer (host seed only). The counter is created outside any pool that a
 # graph could free (torch.empty under capture would come from the graph's private pool and is
 # never released: it stays referenced here).
+# The framework's own graph entries (jit / static Executor) capture under managed_graph_rng():
+# no advance is captured; their replay advances the counter eagerly before a graph whose capture
+# used it (graph_seq_advance), and a training pair advances only before the FORWARD graph, so a
+# backward graph (and any recompute inside it) reads the forward's value.
 _GSEQ = {}
+_GSEQ_MANAGED = [None]
 
 
 def _graph_seq(dev):
     """(device pointer of the step counter or 0, the counter tensor to keep alive or None)."""
     if dev.type != 'cuda' or not torch.cuda.is_current_stream_capturing():
         return 0, None
-    cid = _native.lib().capture_id(_stream())
     st = _GSEQ.get(dev.index)
     if st is None:
         st = _GSEQ[dev.index] = [torch.empty(1, dtype=torch.int64, device=dev), 0]
-    if st[1] != cid:
+    managed = _GSEQ_MANAGED[0]
+    if managed is not None:
+        managed['used'] = True
+        return st[0].data_ptr(), st[0]
+    cid = _native.lib().capture_id(_stream())
+    if st[1] != cid:  # a user capture: its first dropout launch captures the advance
         st[0].add_(1)
         st[1] = cid
     return st[0].data_ptr(), st[0]
+
+
+class managed_graph_rng:
+    """Context for a capture whose replays advance the dropout step counter eagerly
+    (``used`` tells whether any captured launch reads it)."""
+
+    def __enter__(self):
+        self.prev, self.state = _GSEQ_MANAGED[0], {'used': False}
+        _GSEQ_MANAGED[0] = self.state
+        return self.state
+
+    def __exit__(self, *exc):
+        _GSEQ_MANAGED[0] = self.prev
+        return False
+
+
+def graph_seq_advance(dev):
+    """Advance the dropout step counter of ``dev`` (eager launch before a managed replay)."""
+    st = _GSEQ.get(dev.index)
+    if st is not None:
+        st[0].add_(1)
 
 
 def _hash_keep_ref(n, p, seed, device):

@@ -243,3 +243,24 @@ def test_dropout_masks_change_across_graph_replays():
     assert ((gh1 == 0) != drop1).float().mean().item() < 0.01
     assert ((gh1 == 0) != (gh2 == 0)).float().mean().item() > 0.2
     assert not torch.equal(gv1, gv2)
+
+
+@pytest.mark.gpu
+def test_framework_graph_entry_advances_dropout_per_replay():
+    """The framework's own captures (jit / static Executor graph entries) advance the dropout
+    step counter eagerly before each replay: successive replays draw new masks."""
+    from paddle_ray_amd.framework.core import Tensor
+    from paddle_ray_amd.jit.api import _GraphEntry
+    torch.manual_seed(9)
+    q = torch.randn(2, 128, 2, 64, device='cuda', dtype=torch.bfloat16)
+
+    def fn(t):
+        x = t._t
+        return Tensor(K.flash_attention_ext(x, x, x, dropout=0.5))
+    g = _GraphEntry(fn, (Tensor(q),), {})
+    assert g.rng_dev is not None
+    o1 = g((Tensor(q),), {})._t
+    o2 = g((Tensor(q),), {})._t
+    torch.cuda.synchronize()
+    assert not torch.equal(o1, o2)
+    assert torch.isfinite(o1.float()).all() and torch.isfinite(o2.float()).all()
