@@ -283,6 +283,18 @@ def _emit(b, func, args, kwargs, out):
         dim, idx = int(a[1]) % a[0].dim(), int(a[2])
         g = b.node('Gather', [t(a[0]), b.ints([idx % a[0].shape[dim]])], axis=dim)
         return b.node('Reshape', [g, b.ints(out.shape)])
+    if op in ('unbind', 'split', 'split_with_sizes'):
+        x = a[0]
+        outs_t = list(out)
+        dim = int(a[1] if op == 'unbind' else (a[2] if len(a) > 2 else kwargs.get('dim', 0))) % x.dim()
+        sizes = [o.shape[dim] if op != 'unbind' else 1 for o in outs_t]
+        names = [b.fresh('split') for _ in outs_t]
+        b.node('Split', [t(x), b.ints(sizes)], names, axis=dim)
+        if op == 'unbind':
+            names = [b.node('Reshape', [nm, b.ints(o.shape)]) for nm, o in zip(names, outs_t)]
+        return names
+    if op == 'masked_fill':
+        return b.node('Where', [t(a[1]), operand(a[2], a[0]), t(a[0])])
     if op == 'cat':
         dim = int(a[1]) if len(a) > 1 else kwargs.get('dim', 0)
         return b.node('Concat', [t(x) for x in a[0]], axis=dim % out.dim())
@@ -300,6 +312,14 @@ def _emit(b, func, args, kwargs, out):
         if onnx_op == 'ReduceSum':
             return b.node(onnx_op, [t(a[0]), b.ints(axes)], keepdims=int(keep))
         return b.node(onnx_op, [t(a[0])], axes=axes, keepdims=int(keep))
+    if op == 'logsumexp':
+        dims = a[1] if len(a) > 1 else kwargs.get('dim')
+        keep = bool(a[2]) if len(a) > 2 else kwargs.get('keepdim', False)
+        axes = [int(d) % a[0].dim() for d in (dims if isinstance(dims, (list, tuple)) else [dims])]
+        return b.node('ReduceLogSumExp', [t(a[0])], axes=axes, keepdims=int(keep))
+    if op == 'nan_to_num':
+        x = t(a[0])
+        return b.node('Where', [b.node('IsNaN', [x]), b.scalar(0.0, a[0]), x])
     if op in ('var', 'std'):
         x = a[0]
         dims = a[1] if len(a) > 1 and a[1] is not None else kwargs.get('dim', list(range(x.dim())))
@@ -544,6 +564,13 @@ def run(model, inputs):
             y = x[tuple(sl)]
         elif op == 'Gather':
             y = np.take(x, ins[1].astype(np.int64), axis=A('axis', 0))
+        elif op == 'Split':
+            ax = A('axis', 0)
+            cuts = np.cumsum([int(v) for v in ins[1]])[:-1]
+            parts = np.split(x, cuts, axis=ax)
+            for nm, part in zip(nd['output'], parts):
+                env[nm] = part
+            continue
         elif op == 'Concat':
             y = np.concatenate(ins, axis=A('axis'))
         elif op in ('GreaterOrEqual', 'Greater', 'LessOrEqual', 'Less', 'Equal', 'And', 'Or'):
@@ -557,6 +584,15 @@ def run(model, inputs):
         elif op in ('ReduceMean', 'ReduceMax'):
             f = np.mean if op == 'ReduceMean' else np.max
             y = f(x, axis=tuple(A('axes')), keepdims=bool(A('keepdims', 1)))
+        elif op == 'ReduceLogSumExp':
+            ax = tuple(A('axes'))
+            mx = np.max(x, axis=ax, keepdims=True)
+            mx = np.where(np.isfinite(mx), mx, 0)
+            y = np.log(np.sum(np.exp(x - mx), axis=ax, keepdims=True)) + mx
+            if not A('keepdims', 1):
+                y = np.squeeze(y, axis=ax)
+        elif op == 'IsNaN':
+            y = np.isnan(x)
         elif op == 'ReduceSum':
             y = np.sum(x, axis=tuple(int(v) for v in ins[1]), keepdims=bool(A('keepdims', 1)))
         elif op == 'Conv':

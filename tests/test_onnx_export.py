@@ -117,3 +117,25 @@ def test_bytes_parse_with_google_protobuf(tmp_path):
     assert w.data_type == 1 and len(w.raw_data) == 4 * int(np.prod(list(w.dims)))
     # and our decoder reads what protobuf re-serialises
     assert O._dec('ModelProto', m.SerializeToString())['graph']['node'][0]['op_type'] == ops[0]
+
+
+def test_gpt_and_bert_export(tmp_path):
+    """Attention models (causal GPT with the tied LM head, BERT encoder + pooler): the flash
+    attention reference path (masked scores, logsumexp, softmax) exports and matches."""
+    from paddle_ray_amd.models import gpt_config, GPTForPretraining, BertModel, bert_config
+    paddle.seed(0)
+    ids = np.random.RandomState(0).randint(0, 1000, (2, 16)).astype(np.int64)
+    m = GPTForPretraining(gpt_config('gpt3-tiny', hidden_dropout=0.0, attention_dropout=0.0))
+    m.eval()
+    fn = O.export(m, str(tmp_path / 'gpt'), [InputSpec([2, 16], 'int64')], opset_version=13)
+    y, = O.run(fn, [ids])
+    np.testing.assert_allclose(y, m(paddle.to_tensor(ids)).numpy(), rtol=1e-4, atol=1e-4)
+    cfg = bert_config('bert-base-uncased', num_hidden_layers=1, hidden_dropout_prob=0.0,
+                      attention_probs_dropout_prob=0.0)
+    bm = BertModel(cfg)
+    bm.eval()
+    fn = O.export(bm, str(tmp_path / 'bert'), [InputSpec([2, 16], 'int64')], opset_version=13)
+    seq, pooled = O.run(fn, [ids])
+    rs, rp = bm(paddle.to_tensor(ids))
+    np.testing.assert_allclose(seq, rs.numpy(), rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(pooled, rp.numpy(), rtol=1e-4, atol=1e-4)
