@@ -196,6 +196,8 @@ def _is_const(b, x):
 def _emit(b, func, args, kwargs, out):
     """Append the ONNX nodes of one aten op; returns the output name (or list of names)."""
     op = func.overloadpacket.__name__
+    if op.endswith('_') and not op.startswith('_'):
+        op = op[:-1]  # in-place form (relu_, add_, ...): same node, the result is rebound
     a = list(args)
     t = lambda x: b.name_of(x)  # noqa: E731
     rank = out.dim() if isinstance(out, torch.Tensor) else None
@@ -244,6 +246,14 @@ def _emit(b, func, args, kwargs, out):
                                   b.node('Add', [b.node('Tanh', [inner]), b.scalar(1.0, a[0])])])
         e = b.node('Erf', [b.node('Mul', [x, b.scalar(0.7071067811865476, a[0])])])
         return b.node('Mul', [b.node('Mul', [x, b.scalar(0.5, a[0])]), b.node('Add', [e, b.scalar(1.0, a[0])])])
+    if op in ('hardswish', 'hardsigmoid'):
+        x = t(a[0])
+        hs = b.node('Div', [b.node('Clip', [b.node('Add', [x, b.scalar(3.0, a[0])]), b.scalar(0.0, a[0]),
+                                           b.scalar(6.0, a[0])]), b.scalar(6.0, a[0])])
+        return b.node('Mul', [x, hs]) if op == 'hardswish' else hs
+    if op == 'silu':
+        x = t(a[0])
+        return b.node('Mul', [x, b.node('Sigmoid', [x])])
     if op in ('hardtanh', 'clamp'):
         lo = a[1] if len(a) > 1 else kwargs.get('min')
         hi = a[2] if len(a) > 2 else kwargs.get('max')
@@ -362,9 +372,14 @@ def _emit(b, func, args, kwargs, out):
         return b.node('AveragePool', [t(x)], kernel_shape=k, strides=s, pads=p * 2,
                       count_include_pad=int(incl))
     if op in ('_adaptive_avg_pool2d', 'adaptive_avg_pool2d'):
-        if tuple(out.shape[-2:]) != (1, 1):
-            raise NotImplementedError('onnx export: adaptive_avg_pool2d to an output other than 1x1')
-        return b.node('GlobalAveragePool', [t(a[0])])
+        if tuple(out.shape[-2:]) == (1, 1):
+            return b.node('GlobalAveragePool', [t(a[0])])
+        ih, iw = a[0].shape[-2:]
+        oh, ow = out.shape[-2:]
+        if ih % oh or iw % ow:
+            raise NotImplementedError('onnx export: adaptive_avg_pool2d with a non-divisible output size')
+        k = [ih // oh, iw // ow]
+        return b.node('AveragePool', [t(a[0])], kernel_shape=k, strides=k, pads=[0, 0, 0, 0])
     if op == 'native_layer_norm':
         x, shape, w, bias, eps = a[:5]
         axes = list(range(x.dim() - len(shape), x.dim()))
@@ -423,27 +438,45 @@ def to_model_proto(layer, input_spec, opset_version=13):
                 if isinstance(x, torch.Tensor)]
     # only the operations the outputs depend on (index bound checks, asserts and other host-side
     # reads of device values are dead code for the graph)
+    # which recorded values depend on the inputs (everything else folds into initializers)
+    derived = {id(x) for x in examples}
     producer = {}
     for k, (func, args, kwargs, res) in enumerate(rec.log):
+        live = any(id(x) in derived for x in tensors_in(args, kwargs))
         for r in (res if isinstance(res, (list, tuple)) else [res]):
             if isinstance(r, torch.Tensor):
-                producer[id(r)] = k
+                if live:
+                    derived.add(id(r))
+                # an in-place op returns its input: the value keeps its producer chain, the op joins it
+                producer.setdefault(id(r), k) if func.overloadpacket.__name__.endswith('_') else \
+                    producer.__setitem__(id(r), k)
+    inplace_of = {}
+    for k, (func, args, kwargs, res) in enumerate(rec.log):
+        if func.overloadpacket.__name__.endswith('_') and isinstance(res, torch.Tensor):
+            inplace_of.setdefault(producer.get(id(res)), []).append(k)
     needed, stack = set(), [producer[id(o)] for o in outs if id(o) in producer]
     while stack:
         k = stack.pop()
         if k in needed:
             continue
         needed.add(k)
+        stack.extend(inplace_of.get(k, []))
         stack.extend(producer[id(x)] for x in tensors_in(rec.log[k][1], rec.log[k][2]) if id(x) in producer)
     for k, (func, args, kwargs, res) in enumerate(rec.log):
         if k not in needed:
             continue
         flat_in = tensors_in(args, kwargs)
         res_list = list(res) if isinstance(res, (list, tuple)) else [res]
-        if func.overloadpacket.__name__ in _SHAPE_ONLY:
+        opname = func.overloadpacket.__name__
+        if opname in _SHAPE_ONLY:
+            derived.difference_update(id(r) for r in res_list if isinstance(r, torch.Tensor))
             continue  # reads only its input's (static) shape: the output is a constant
-        if all(id(x) not in b.names or id(x) in b.const for x in flat_in):
+        if not any(id(x) in derived for x in flat_in):
             continue  # depends only on parameters / constants: its outputs fold into initializers
+        if opname == 'as_strided_' and isinstance(res, torch.Tensor):
+            src = b.names[id(args[0])]
+            b.names[id(res)] = b.node('Reshape', [src, b.ints(res.shape)])
+            continue
         names = _emit(b, func, args, kwargs, res)
         names = names if isinstance(names, list) else [names]
         for r, nm in zip(res_list, names):

@@ -139,3 +139,15 @@ def test_gpt_and_bert_export(tmp_path):
     rs, rp = bm(paddle.to_tensor(ids))
     np.testing.assert_allclose(seq, rs.numpy(), rtol=1e-4, atol=1e-4)
     np.testing.assert_allclose(pooled, rp.numpy(), rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize('name', ['mobilenet_v2', 'mobilenet_v3_small', 'resnet50_nhwc'])
+def test_vision_zoo_export(name, tmp_path):
+    """Depthwise convs, hardswish / SE blocks, channels-last ResNet (permutes, in-place restrides)."""
+    from paddle_ray_amd.vision import models as M
+    paddle.seed(0)
+    if name == 'resnet50_nhwc':
+        m, shape = M.resnet50(num_classes=10, data_format='NHWC'), [1, 32, 32, 3]
+    else:
+        m, shape = getattr(M, name)(num_classes=10), [1, 3, 32, 32]
+    _check(m, shape, tmp_path, tol=2e-3)
