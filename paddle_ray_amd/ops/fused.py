@@ -2031,7 +2031,8 @@ def zero_tensors(ts):
     ts = [t for t in ts if t.numel()]
     if not ts:
         return
-    if not (ts[0].is_cuda and _native.available() and all(t.is_contiguous() and t.is_cuda for t in ts)):
+    if not (ts[0].is_cuda and _native.available() and len(_ZERO_CHECKED) == 1 and
+            all(t.is_contiguous() and t.is_cuda for t in ts)):
         torch._foreach_zero_(ts)
         return
     key = tuple((t.data_ptr(), t.numel() * t.element_size()) for t in ts)
@@ -2044,6 +2045,18 @@ def zero_tensors(ts):
             _ZERO_PLAN.clear()
         plan = _ZERO_PLAN[key] = (tab, len(pieces))
     _native.lib().zero_mt(_ptr(plan[0]), plan[1], _stream())
+    if not _ZERO_CHECKED[0]:
+        # first use in the process: confirm the launch zeroed everything (one sync), else keep
+        # the library fill from then on
+        _ZERO_CHECKED[0] = True
+        if any(int(torch.count_nonzero(t)) for t in ts):
+            import warnings
+            warnings.warn('zero_mt kernel left nonzeros: using torch._foreach_zero_')
+            _ZERO_CHECKED.append('off')
+            torch._foreach_zero_(ts)
+
+
+_ZERO_CHECKED = [False]
 
 
 @R.register_kernel('adamw_mt', 'hip')
