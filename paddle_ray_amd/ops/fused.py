@@ -1323,8 +1323,6 @@ def _gemm_hip(layout, a, b, out=None, bias=None, z=None, epi=None, beta=0, want_
         # skinny decode-time forwards (M < 128: a 256-row tile idles) go to the library
         if layout == GEMM_FWD and M < 128:
             return None
-        if _gemm_prefers_library(layout, M, N, K):
-            return None
     if out is None:
         out = torch.empty((M, N), device=a.device, dtype=a.dtype)
     elif not _gemm_operand_ok(out) or out.dtype != a.dtype or tuple(out.shape) != (M, N):
@@ -1353,12 +1351,6 @@ def _gemm_hip(layout, a, b, out=None, bias=None, z=None, epi=None, beta=0, want_
     return out
 
 
-def _gemm_prefers_library(layout, M, N, K):
-    """Forward GEMMs that would need split-K (few 256x256 tiles over a long K): BERT's fc2
-    16384x768x3072 ran 138.7 us split 4-ways vs 73.6 us in hipBLASLt (profiles/r3g)."""
-    return layout == GEMM_FWD and ((M + 255) // 256) * ((N + 255) // 256) < 224 and K // 64 >= 16
-
-
 def gemm(layout, a, b, out=None, bias=None, z=None, epi=None, beta=0, want_colsum=False):
     """C (=|+=) epi(op(a)·op(b) + bias). layout: GEMM_FWD a[M,K]·b[K,N]; GEMM_NT a[M,K]·b[N,K]ᵀ;
     GEMM_TN a[K,M]ᵀ·b[K,N]. On the device this is the in-tree MFMA kernel; shapes it does not
@@ -1367,12 +1359,7 @@ def gemm(layout, a, b, out=None, bias=None, z=None, epi=None, beta=0, want_colsu
         r = _gemm_hip(layout, a, b, out, bias, z, epi, beta, want_colsum)
         if r is not None:
             return r
-        lib = _GEMM_MODE == 'auto' and (layout == GEMM_NT or (
-            _GEMM_SHAPE_POLICY and epi is None and not want_colsum and a.dim() == 2 and
-            _gemm_prefers_library(layout, a.shape[0] if layout != GEMM_TN else a.shape[1],
-                                  b.shape[1] if layout != GEMM_NT else b.shape[0],
-                                  a.shape[1] if layout != GEMM_TN else a.shape[0])))
-        R._STATS[('gemm', 'hipblaslt' if lib else 'fallback')] += 1
+        R._STATS[('gemm', 'hipblaslt' if _GEMM_MODE == 'auto' and layout == GEMM_NT else 'fallback')] += 1
     return _gemm_ref_fast(layout, a, b, out, bias, z, epi, beta, want_colsum)
 
 
