@@ -201,6 +201,7 @@ class ShardedState:
         self._rs_window = []
         self.peak_resident_bytes = 0
         self.on_params_loaded = []
+        self.step_overlap = None  # _StepOverlap, set by a one-rank ShardedOptimizer
         if self.zero3:
             for u in self.unit_meta:
                 self._hooks.append(u.layer.register_forward_pre_hook(self._make_pre(u)))
@@ -348,6 +349,12 @@ class ShardedState:
             self.gather_works.pop(gi).wait()
 
     def before_forward(self):
+        ov = self.step_overlap
+        if ov is not None:
+            if any(not g.grads_released and g.grads_missing() for g in self.groups):
+                ov.sync()
+            else:
+                ov.before_forward()
         for g in self.groups:
             if not g.grads_released and g.grads_missing():
                 g.grad_buf.zero_()
@@ -369,6 +376,8 @@ class ShardedState:
 
     def sync_params(self):
         """Make every parameter hold its full current value (resident and unit groups)."""
+        if self.step_overlap is not None:
+            self.step_overlap.sync()
         if self.params_stale:
             self.launch_gathers()
         for u in self.unit_meta:
@@ -400,6 +409,121 @@ class ShardedState:
                 g.param_shard.copy_(g.shard(g.param_buf))
         for cb in self.on_params_loaded:
             cb()
+
+
+class _StepOverlap:
+    """One-GPU optimizer / next-forward overlap (``PRA_OPT_OVERLAP=1``, opt-in; applies with one
+    rank, no dp replicas, no offload, device update kernels).
+
+    The update of step t is queued on a side HIP stream in the NEXT forward's order: the root
+    parameters (embeddings, final norm, head) first, then unit 0, 1, ... (the repeated blocks,
+    ``_find_units``), one multi-tensor launch per phase with an event after each. The next
+    forward waits for the root and unit-0 phases before it starts and each unit waits, in its
+    forward pre-hook, for its own phase and the next unit's (GPT applies block 0's LayerNorm
+    before calling it and fuses the next block's LayerNorm into the previous block); the last
+    unit waits for everything. Gradient zeroing from ``clear_grad`` follows the updates on the same
+    stream. The update is an HBM-bound stream over 28 B per parameter (fp32 master + moments,
+    bf16 grad and copy) while the forward GEMMs are MFMA-bound, so the two share the chip
+    instead of running back to back. Anything that reads parameters, gradients or optimizer
+    state from outside a forward (state dicts, a second optimizer step) first joins the side
+    stream (``sync``). Units must only read their own, earlier units' or the next unit's
+    parameters.
+
+    Measured on GPT-3 1.3B (profiles/r3j/opt_overlap_ab.md): the phases do run under the
+    forward, but sharing the CUs slows both sides (forward GEMMs 2-3x, the update 1.5x) and the
+    forward is gated on the update's progress, so the step is ~1 ms slower than the serial
+    update (132.1 vs 131.1 ms): off by default."""
+
+    @classmethod
+    def maybe(cls, opt):
+        import os
+        st = opt.state
+        if os.environ.get('PRA_OPT_OVERLAP', '0') != '1' or opt._offload or st.world != 1 \
+                or st.dp_world != 1 or not st.groups or st.groups[0].device.type != 'cuda' \
+                or not _native.available() or opt._kind not in ('AdamW', 'Momentum', 'SGD') \
+                or opt._mp_pg is not None or opt._norm_pgs:
+            return None
+        units = _find_units(st.layer)
+        if len(units) < 2:
+            return None
+        return cls(opt, units)
+
+    def __init__(self, opt, units):
+        st = opt.state
+        unit_of = {}
+        for ui, u in enumerate(units):
+            for p in u.parameters():
+                unit_of.setdefault(id(p), ui)
+        nph = len(units) + 1
+        self.phase_pieces = [[] for _ in range(nph)]
+        for i, (gi, p, lo, hi, plo) in enumerate(opt._pieces):
+            self.phase_pieces[unit_of.get(id(p), -1) + 1].append(i)
+        self.plans = [None] * nph
+        self.device = st.groups[0].device
+        self.stream = torch.cuda.Stream(device=self.device)
+        self.events = [None] * nph
+        self.final = None
+        self.hooks = [u.register_forward_pre_hook(self._make_wait(ui, len(units)))
+                      for ui, u in enumerate(units)]
+
+    def _make_wait(self, ui, n):
+        def hook(layer, inputs):
+            if ui == n - 1:
+                self.sync()
+            else:
+                self._wait(ui + 2)
+        return hook
+
+    def _wait(self, ph):
+        ev = self.events[min(ph, len(self.events) - 1)]
+        if ev is not None:
+            torch.cuda.current_stream(self.device).wait_event(ev)
+
+    def before_forward(self):
+        self._wait(1)  # root and unit 0 (GPT applies block 0's ln1 before calling the block)
+
+    def sync(self):
+        """The caller's stream waits for every queued update and zeroing."""
+        if self.final is not None:
+            torch.cuda.current_stream(self.device).wait_event(self.final)
+            self.final = None
+            self.events = [None] * len(self.events)
+
+    def run(self, opt, lr, scale_t, launch):
+        """Queue the update: ``launch(plan)`` issues one phase's multi-tensor kernel."""
+        main = torch.cuda.current_stream(self.device)
+        s = self.stream
+        s.wait_stream(main)
+        if scale_t is not None:
+            scale_t.record_stream(s)
+        with torch.cuda.stream(s):
+            for ph, idx in enumerate(self.phase_pieces):
+                if not idx:
+                    continue
+                if self.plans[ph] is None:
+                    self.plans[ph] = opt._build_plan(idx)
+                launch(self.plans[ph])
+                ev = torch.cuda.Event()
+                ev.record(s)
+                self.events[ph] = ev
+        self.final = torch.cuda.Event()
+        self.final.record(s)
+
+    def zero_grads(self, st):
+        """clear_grad after a queued update: zero on the side stream, behind the updates."""
+        if self.final is None:
+            return False
+        s = self.stream
+        with torch.cuda.stream(s):
+            K.zero_tensors([g.grad_buf for g in st.groups if not g.grads_released])
+        for g in st.groups:
+            if not g.grads_released:
+                g.reattach_grads()
+        self.final = torch.cuda.Event()
+        self.final.record(s)
+        # the last phase's event now also covers the zeroing (the backward runs after it)
+        self.events[-1] = self.final
+        return True
 
 
 class ShardedOptimizer:
@@ -435,6 +559,8 @@ class ShardedOptimizer:
         self._plan = None
         self._step = 0
         state.on_params_loaded.append(self._refresh_masters)
+        self._overlap = _StepOverlap.maybe(self)
+        state.step_overlap = self._overlap
 
     def _refresh_masters(self):
         with torch.no_grad():
@@ -458,6 +584,13 @@ class ShardedOptimizer:
         return self._inner._parameter_list
 
     def clear_grad(self, set_to_zero=True):
+        ov = self._overlap
+        if ov is not None and set_to_zero and ov.zero_grads(self.state):
+            if self.state.reducer is not None:
+                self.state.reducer.reset_accumulation()
+            return
+        if ov is not None:
+            ov.sync()
         self.state.zero_grad()
 
     def _scaler_grads(self):
@@ -530,10 +663,18 @@ class ShardedOptimizer:
         self._step += 1
         o = self._inner
         o._step_count = self._step
+        ov = self._overlap
+        if ov is not None:
+            ov.sync()  # a second step before the next forward: the previous update comes first
         coef = self._clip_coef()
         lr = o.get_lr()
         dev = st.groups[0].device if st.groups else None
         coupled = self._kind == 'Adam' and o._weight_decay
+        if ov is not None:
+            scale_t = None if coef is None else coef.to(torch.float32).reshape(()).contiguous()
+            ov.run(self, lr, scale_t, lambda plan: self._launch(plan, lr, scale_t))
+            st.after_step()
+            return
         if self._offload:
             self._step_offload(lr, coef)
         elif dev is not None and dev.type == 'cuda' and _native.available() and not coupled:
@@ -611,35 +752,32 @@ class ShardedOptimizer:
         return [m if m is not None else g.param_shard
                 for m, g in zip(self._masters, self.state.groups)]
 
-    def _step_hip(self, lr, scale_t=None):
+    def _build_plan(self, idx=None):
+        """Multi-tensor descriptor tables for the pieces ``idx`` (default: all)."""
+        cols = [[], [], [], [], [], [], [], []]
+        wds, lrms = [], []
+        for i in (range(len(self._pieces)) if idx is None else idx):
+            gi, p, lo, hi, plo = self._pieces[i]
+            master, grad, m, v, lowp = self._piece_views(gi, lo, hi)
+            cols[0].append(master.data_ptr())
+            cols[1].append(grad.data_ptr())
+            cols[2].append(m.data_ptr())
+            cols[3].append(0 if v is None else v.data_ptr())
+            cols[4].append(0 if lowp is None else lowp.data_ptr())
+            cols[5].append(hi - lo)
+            cols[6].append(K._DT[grad.dtype])
+            cols[7].append(K._DT[(lowp if lowp is not None else master).dtype])
+            wd = self._wd(p)
+            if self._kind == 'Adam':
+                wd = 0.0  # coupled L2 handled in _step_hip (rare); AdamW decoupled in-kernel
+            wds.append(wd)
+            lrms.append(p.optimize_attr.get('learning_rate', 1.0))
+        return K._mt_table(cols, cols[5], [wds, lrms], self.state.groups[0].device)
+
+    def _launch(self, plan, lr, scale_t):
         o = self._inner
-        if self._plan is None:
-            cols = [[], [], [], [], [], [], [], []]
-            wds, lrms = [], []
-            for gi, p, lo, hi, plo in self._pieces:
-                master, grad, m, v, lowp = self._piece_views(gi, lo, hi)
-                cols[0].append(master.data_ptr())
-                cols[1].append(grad.data_ptr())
-                cols[2].append(m.data_ptr())
-                cols[3].append(0 if v is None else v.data_ptr())
-                cols[4].append(0 if lowp is None else lowp.data_ptr())
-                cols[5].append(hi - lo)
-                cols[6].append(K._DT[grad.dtype])
-                cols[7].append(K._DT[(lowp if lowp is not None else master).dtype])
-                wd = self._wd(p)
-                if self._kind == 'Adam':
-                    wd = 0.0  # coupled L2 handled below (rare); AdamW decoupled in-kernel
-                wds.append(wd)
-                lrms.append(p.optimize_attr.get('learning_rate', 1.0))
-            self._plan = K._mt_table(cols, cols[5], [wds, lrms], self.state.groups[0].device)
-        tab, ftab, ch, nch = self._plan
+        tab, ftab, ch, nch = plan
         if self._kind in ('Adam', 'AdamW'):
-            if self._kind == 'Adam' and o._weight_decay:
-                for gi, p, lo, hi, plo in self._pieces:
-                    w = self._wd(p)
-                    if w:
-                        master, grad, m, v, lowp = self._piece_views(gi, lo, hi)
-                        grad.add_(master.to(grad.dtype), alpha=w)
             b1, b2 = o._beta1, o._beta2
             R.dispatch('adamw_mt', tab, tab, ftab, ch, nch, lr, b1, b2, o._epsilon,
                        1 - b1 ** self._step, 1 - b2 ** self._step, 1.0, scale_t,
@@ -648,6 +786,18 @@ class ShardedOptimizer:
             R.dispatch('momentum_mt', tab, tab, ftab, ch, nch, lr, getattr(o, '_momentum', 0.0),
                        getattr(o, '_use_nesterov', False), 1.0, scale_t,
                        self._updated_shards())
+
+    def _step_hip(self, lr, scale_t=None):
+        o = self._inner
+        if self._plan is None:
+            self._plan = self._build_plan()
+        if self._kind == 'Adam' and o._weight_decay:
+            for gi, p, lo, hi, plo in self._pieces:
+                w = self._wd(p)
+                if w:
+                    master, grad, m, v, lowp = self._piece_views(gi, lo, hi)
+                    grad.add_(master.to(grad.dtype), alpha=w)
+        self._launch(self._plan, lr, scale_t)
 
     def minimize(self, loss, *a, **k):
         loss.backward()
@@ -677,6 +827,8 @@ class ShardedOptimizer:
         ``.pdopt`` written here resumes under ANY sharding degree (or none: the plain optimizer
         reads the same keys). ``full=False`` returns this rank's raw shards only."""
         st = self.state
+        if self._overlap is not None:
+            self._overlap.sync()
         sd = {}
         if not full:
             for gi in range(len(st.groups)):
@@ -719,6 +871,8 @@ class ShardedOptimizer:
 
     def set_state_dict(self, sd):
         st = self.state
+        if self._overlap is not None:
+            self._overlap.sync()
         k1, k2 = self._acc_keys()
         per_param = any(isinstance(k, str) and k.endswith(f'_{k1}_0') for k in sd)
         masters_sd = sd.get('master_weights', {})
