@@ -105,6 +105,7 @@ struct Block {
   Block* next;
   stream_t stream;  // stream of the last user
   event_t event;    // recorded on `stream` when freed (cross-stream reuse gate)
+  std::vector<stream_t> rec;  // other streams that used the block (record_stream)
 };
 
 struct Chunk {
@@ -133,6 +134,9 @@ struct DeviceAllocator {
   std::map<stream_t, std::set<std::pair<size_t, Block*>>> free_sets;
   std::unordered_map<void*, Block*> live;
   std::vector<Chunk*> chunks;
+  // freed blocks that record_stream tied to other streams: they stay allocated until the
+  // events recorded on those streams at free time complete (PyTorch's recordStream contract)
+  std::vector<std::pair<Block*, std::vector<event_t>>> deferred;
   Stats st;
 
   static size_t round(size_t n) { return ((n ? n : 1) + kAlign - 1) / kAlign * kAlign; }
@@ -261,11 +265,13 @@ struct DeviceAllocator {
   void* alloc(size_t size, stream_t s) {
     std::lock_guard<std::mutex> g(mu);
     note_stream(s);
+    if (!deferred.empty()) process_deferred();
     const size_t n = round(size);
     Block* b = find(n, s);
     if (!b) {
       if (!grow(n)) {  // out of memory: wait for pending frees, drop free chunks, retry
         device_sync();
+        process_deferred();
         release_free_chunks();
         if (!grow(n)) return nullptr;
       }
@@ -275,17 +281,64 @@ struct DeviceAllocator {
     return take(b, n, s)->ptr;
   }
 
+  // another stream uses a live block: its free must wait for that stream's work too
+  bool record_stream(void* p, stream_t s2) {
+    std::lock_guard<std::mutex> g(mu);
+    auto it = live.find(p);
+    if (it == live.end()) return false;
+    Block* b = it->second;
+    if (pool || s2 == b->stream) return true;
+    note_stream(s2);
+    if (std::find(b->rec.begin(), b->rec.end(), s2) == b->rec.end()) b->rec.push_back(s2);
+    return true;
+  }
+
+  void process_deferred() {
+    std::vector<std::pair<Block*, std::vector<event_t>>> keep;
+    for (auto& d : deferred) {
+      bool done = true;
+      for (event_t e : d.second) done = done && event_done(e);
+      if (!done) {
+        keep.push_back(std::move(d));
+        continue;
+      }
+      for (event_t e : d.second)
+        if (e) event_pool.push_back(e);
+      // a fresh gate on the freeing stream: neighbours freed there since then may merge in,
+      // and the merged block must wait for their work too
+      Block* b = d.first;
+      drop_event(b);
+      release(b, b->stream, new_event(b->stream));
+    }
+    deferred.swap(keep);
+  }
+
   void free_(void* p, stream_t s) {
     std::lock_guard<std::mutex> g(mu);
     auto it = live.find(p);
     if (it == live.end()) return;
     Block* b = it->second;
     live.erase(it);
-    st.allocated -= (int64_t)b->size;
     st.n_free++;
+    if (!b->rec.empty()) {
+      std::vector<event_t> evs;
+      for (stream_t r : b->rec)
+        if (r != s) evs.push_back(new_event(r));
+      b->rec.clear();
+      b->stream = s;
+      b->event = new_event(s);
+      deferred.push_back({b, std::move(evs)});
+      return;
+    }
+    release(b, s, new_event(s));
+  }
+
+  // a freed block (no other stream still using it) joins the free lists of stream s
+  void release(Block* b, stream_t s, event_t ev) {
+    st.allocated -= (int64_t)b->size;
     b->free = true;
     b->stream = s;
-    b->event = new_event(s);
+    b->event = ev;
     // coalesce with free neighbours freed on the same stream, or whose pending work is done
     // (their event completed: any stream may take them, so the merged block can be s's)
     auto mergeable = [&](Block* o) {
@@ -424,6 +477,21 @@ void pra_free(void* ptr, size_t size, int device, stream_t stream) {
     return;
   }
   dev(device)->free_(ptr, stream);
+}
+// PyTorch recordStream: the block at ptr is also used by stream s (device arenas only; graph
+// pools reuse in capture order)
+void pra_record_stream(void* ptr, stream_t stream) {
+  {
+    std::lock_guard<std::mutex> g(g_own_mu);
+    if (g_owner.count(ptr)) return;
+  }
+  std::vector<DeviceAllocator*> devs;
+  {
+    std::lock_guard<std::mutex> g(g_mu);
+    for (auto& kv : g_dev) devs.push_back(kv.second);
+  }
+  for (DeviceAllocator* a : devs)
+    if (a->record_stream(ptr, stream)) return;
 }
 // graph-capture arenas (pool id = PyTorch's MempoolId_t pair)
 void* pra_alloc_pool(size_t size, int device, stream_t stream, uint64_t id0, uint64_t id1) {

@@ -5,7 +5,8 @@
 // cannot set:
 //   beginAllocateToPool(device, pool, filter): allocations on streams the filter accepts (the
 //     streams being captured) go to the pool's private arena until endAllocateToPool;
-//   releasePool(device, pool): the graph is gone; the arena is freed with its last block.
+//   releasePool(device, pool): the graph is gone; the arena is freed with its last block;
+//   recordStream(ptr, stream): the block's free waits for that stream's work as well.
 // Parity: the reference's CUDAGraph private memory pools (paddle/fluid/memory/allocation/
 // allocator_facade.cc, PrepareMemoryPoolForCUDAGraph / RemoveMemoryPoolOfCUDAGraph).
 #include <torch/extension.h>
@@ -21,6 +22,7 @@ typedef void* (*alloc_t)(size_t, int, hipStream_t);
 typedef void (*free_t)(void*, size_t, int, hipStream_t);
 typedef void* (*alloc_pool_t)(size_t, int, hipStream_t, uint64_t, uint64_t);
 typedef void (*release_t)(int, uint64_t, uint64_t);
+typedef void (*record_t)(void*, hipStream_t);
 
 struct Active {
   c10::hip::MempoolId_t id;
@@ -30,7 +32,7 @@ std::mutex g_mu;
 std::map<int, std::vector<Active>> g_active;  // pools being allocated into, per device
 int64_t g_pool_allocs = 0;
 
-bool install(uintptr_t a, uintptr_t f, uintptr_t ap, uintptr_t rel) {
+bool install(uintptr_t a, uintptr_t f, uintptr_t ap, uintptr_t rel, uintptr_t rec) {
   const alloc_t A = reinterpret_cast<alloc_t>(a);
   const free_t F = reinterpret_cast<free_t>(f);
   const alloc_pool_t AP = reinterpret_cast<alloc_pool_t>(ap);
@@ -67,6 +69,10 @@ bool install(uintptr_t a, uintptr_t f, uintptr_t ap, uintptr_t rel) {
       }
   });
   pa->set_release_pool([R](int d, c10::hip::MempoolId_t id) { R(d, id.first, id.second); });
+  if (rec) {
+    const record_t RS = reinterpret_cast<record_t>(rec);
+    pa->set_record_stream_fn([RS](void* p, hipStream_t s) { RS(p, s); });
+  }
   torch::cuda::CUDAPluggableAllocator::changeCurrentAllocator(alloc);
   return true;
 }

@@ -10,12 +10,14 @@ Parity: the reference's FLAGS_allocator_strategy='auto_growth' allocator
 (alloc/torch_hooks.cpp, ``_pra_alloc_torch``), which route every allocation made on a capturing
 stream into a private arena per graph pool (released with the graph), so captured graphs never
 share memory with eager code. Without that module (ctypes-only pluggable allocator) enabling
-refuses, since captures would be unsafe. Measured against PyTorch's caching allocator (profiles/r3h/ab_results.txt): GPT-1.3B 124.2K vs
-124.4K tokens/s, ResNet-50 8431 vs 8423 img/s, BERT-base (HIP-graph static executor) 1473 vs
-1592 seq/s -- opt-in until the graph-replay gap is understood. Limitation: no
-``record_stream`` — a tensor freed while
-a SIDE stream still uses it must be synchronised by its owner (the framework's own collectives
-wait on their works before buffers are released).
+refuses, since captures would be unsafe. ``Tensor.record_stream`` is honoured: a block freed
+while other streams recorded on it is held back until events recorded on those streams at free
+time complete (as PyTorch's caching allocator does; RCCL's stream use depends on it).
+Measured against PyTorch's caching allocator (profiles/r3h/ab_results.txt, profiles/r3j/):
+GPT-1.3B 124.2K vs 124.4K tokens/s, ResNet-50 8431 vs 8423 img/s, BERT-base (HIP-graph static
+executor) 1698.6 vs 1697.4 seq/s (an earlier 1473 vs 1592 gap is gone since the Executor hands
+captured gradients to the optimizer in place). Opt-in: the round-end multi-GPU runs have not
+exercised it yet.
 """
 import ctypes
 import os
@@ -47,6 +49,7 @@ def load(host=False):
                                        ctypes.c_uint64]
         lib.pra_pool_release.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64]
     lib.pra_pool_stats.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_int64)]
+    lib.pra_record_stream.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
     return lib
 
 
@@ -70,7 +73,7 @@ def enable():
                            'run python -m paddle_ray_amd.native.build')
     lib = load()
     addr = [ctypes.cast(getattr(lib, n), ctypes.c_void_p).value
-            for n in ('pra_alloc', 'pra_free', 'pra_alloc_pool', 'pra_pool_release')]
+            for n in ('pra_alloc', 'pra_free', 'pra_alloc_pool', 'pra_pool_release', 'pra_record_stream')]
     if not h.install(*addr):
         raise RuntimeError('native allocator: torch rejected the pluggable allocator')
     _state['lib'] = lib

@@ -144,6 +144,33 @@ def test_split_remainder_keeps_pending_gate(lib):
         lib.pra_alloc_host_complete_events()
 
 
+def test_record_stream_defers_reuse(lib):
+    """Tensor.record_stream: a block used by a second stream is not reused -- by any stream,
+    its own included -- until the work that stream had queued at free time is done."""
+    dev = 42
+    lib.pra_alloc_set_growth(dev, 4 * MB)
+    s1, s2 = 0x1000, 0x2000
+    a = _alloc(lib, dev, 1 * MB, s1)
+    warm = _alloc(lib, dev, 1 * MB, s2)       # second stream: events from now on
+    lib.pra_record_stream(ctypes.c_void_p(a), ctypes.c_void_p(s2))
+    lib.pra_alloc_host_set_pending(1)
+    try:
+        lib.pra_free(a, MB, dev, ctypes.c_void_p(s1))
+        assert A.stats(dev, lib)['allocated'] == 2 * MB     # held back, still counted
+        b = _alloc(lib, dev, 1 * MB, s1)                    # same stream: may NOT reuse a
+        assert b != a
+        assert lib.pra_alloc_check(dev) == 1
+        lib.pra_alloc_host_complete_events()
+        c = _alloc(lib, dev, 1 * MB, s1)                    # s2's work done: a is free again
+        assert c == a
+        for p, s in ((b, s1), (c, s1), (warm, s2)):
+            lib.pra_free(p, MB, dev, ctypes.c_void_p(s))
+        assert lib.pra_alloc_check(dev) == 1 and A.stats(dev, lib)['allocated'] == 0
+    finally:
+        lib.pra_alloc_host_set_pending(0)
+        lib.pra_alloc_host_complete_events()
+
+
 def test_pool_arena_host_bookkeeping(lib):
     """Graph-capture arenas (host build): pool blocks come from their own chunks, are reused
     inside the pool, never mix with the device arena, and the pool's memory goes back once it
