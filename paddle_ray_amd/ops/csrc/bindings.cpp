@@ -83,6 +83,7 @@ int pra_conv_lds(const void*, const void*, const void*, void*, int, int, int, in
                  int, float*, float*, const float*, hipStream_t);
 int pra_conv_lds_stat_rows(int, int);
 int pra_conv_lds_splits(int, int, int);
+int pra_conv_wgrad_rows(int);
 int pra_conv_wgrad_lds(const void*, const void*, void*, int, int, int, int, int, int, int, int, int, int, int, float*,
                        hipStream_t);
 int pra_colsum_partials(const float*, void*, int, int, int, hipStream_t);
@@ -133,6 +134,7 @@ PYBIND11_MODULE(_pra_hip, m) {
     check_launch("conv_wgrad_lds");
   });
   m.def("conv_lds_splits", [](int m, int n, int k) { return pra_conv_lds_splits(m, n, k); });
+  m.def("conv_wgrad_rows", [](int cout) { return pra_conv_wgrad_rows(cout); });
   m.def("conv_lds_stat_rows", [](int m, int n) { return pra_conv_lds_stat_rows(m, n); });
   m.def("gemm_lds_splits", [](int M, int N, int K) { return pra_gemm_lds_splits(M, N, K); });
   m.def("gemm_set_w4", [](int mask) { pra_gemm_set_w4(mask); });

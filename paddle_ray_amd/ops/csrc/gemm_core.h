@@ -132,9 +132,11 @@ __device__ __forceinline__ int kc_swz(int row) { return (row >> 1) & 7; }
 // Per-thread DMA plan for one operand image (NDMA glds per thread per K-step). A K-step moves
 // whole 128-B lines of every row (BK = 64 bf16), so each L2 line is requested once.
 // KC image: position P (16-B chunk 0..2047) = row P>>3, slot P&7 holds global chunk (P&7)^kc_swz(row).
-// MC image: position P = k-row P>>5, slot P&31 holds global chunk (P&31)^mc_swz(k).
-template <bool KC, int NT, int NDMA, bool BUF = false>
+// MC image (MCW columns: 256, or 128 for narrow tiles): position P = k-row P/(MCW/8), slot
+// P%(MCW/8) holds global chunk (P%(MCW/8))^mc_swz(k) (mc_swz < 16 keeps it inside a 128-wide row).
+template <bool KC, int NT, int NDMA, bool BUF = false, int MCW = 256>
 struct Dma {
+  static constexpr int MCC = MCW / 8;  // 16-B chunks per k-row of the MC image
   uint32_t voff[NDMA];  // per-lane byte offsets of the chunks this thread stages
   uint64_t base;        // wave-uniform operand base (SGPRs); advanced per K-step
   uint64_t step;        // bytes per K-step
@@ -147,7 +149,7 @@ struct Dma {
         const int r = min(r0 + row, rmax);
         voff[n] = (uint32_t)(((int64_t)r * ld + 8 * c) * 2);
       } else {
-        const int k = P >> 5, c = (P & 31) ^ mc_swz(k);
+        const int k = P / MCC, c = (P % MCC) ^ mc_swz(k);
         const int col = min(r0 + 8 * c, rmax);  // rmax = last valid 8-aligned chunk start
         voff[n] = (uint32_t)(((int64_t)k * ld + col) * 2);
       }
@@ -295,7 +297,7 @@ struct ConvDmaBW {
 };
 
 // Fragment for rows [r0, r0+16) (row = lane&15), k = 32*s + 8*(lane>>4) + j of a K-step.
-template <typename T, bool KC>
+template <typename T, bool KC, int MCW = 256>
 __device__ __forceinline__ typename V8<T>::type frag(const char* img, int r0, int s, int lane) {
   typedef typename V8<T>::type v8;
   if (KC) {
@@ -307,9 +309,9 @@ __device__ __forceinline__ typename V8<T>::type frag(const char* img, int r0, in
     const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
     const int k = 32 * s + 8 * g + q, x = mc_swz(k);  // mc_swz(k) == mc_swz(k + 4)
     const int c = ((r0 >> 3) + (p >> 1)) ^ x;
-    const char* a0 = img + k * 512 + c * 16 + 8 * (p & 1);
+    const char* a0 = img + k * (2 * MCW) + c * 16 + 8 * (p & 1);
     const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)a0);
-    const v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(a0 + 4 * 512));
+    const v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(a0 + 4 * (2 * MCW)));
     const u32x2 ul = __builtin_bit_cast(u32x2, lo), uh = __builtin_bit_cast(u32x2, hi);
     const u32x4 u = {ul[0], ul[1], uh[0], uh[1]};
     return __builtin_bit_cast(v8, u);
@@ -329,6 +331,7 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_lds_kernel(const uint16_t* __r
   constexpr int BM = CF::BM, BN = CF::BN, IMGA = CF::IMGA, SLOT = CF::SLOT;
   constexpr int RW = TI * 16, CW = TJ * 16;  // rows / columns per wave
   static_assert(BK || BN == 256, "the M/N-contiguous B image is 256 columns wide");
+  static_assert(AK || BM == 256 || BM == 128, "the M-contiguous A image is 256 or 128 columns wide");
   static_assert(!CONVW || (!BK && NDB == 4), "conv wgrad gathers the 256-wide B image");
   static_assert(TJ <= TI && 128 % RW == 0 && NDA >= 1 && NDB >= 1, "wave layout");
   __shared__ __attribute__((aligned(1024))) char lds[CF::LDS];
@@ -356,7 +359,7 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_lds_kernel(const uint16_t* __r
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6),
             wr = wave / WC, wc = wave % WC;
 
-  typename std::conditional<CONV, ConvDmaA<NT, NDA>, Dma<AK, NT, NDA, CF::BUF>>::type da;
+  typename std::conditional<CONV, ConvDmaA<NT, NDA>, Dma<AK, NT, NDA, CF::BUF, (AK ? 256 : BM)>>::type da;
   typename std::conditional<CONVW, ConvDmaBW<NT, NDB>, Dma<BK, NT, NDB, CF::BUF>>::type db;
   if constexpr (CONV) da.init(A, cg, m0, M, tid);
   else if (AK) da.init(A, lda, m0, M - 1, tid);
@@ -386,7 +389,7 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_lds_kernel(const uint16_t* __r
 #pragma unroll
     for (int j = 0; j < TJ; ++j) fb[j] = frag<T, BK>(bi, wc * CW + j * 16, s, lane);
 #pragma unroll
-    for (int i = 0; i < TI; ++i) fa[i] = frag<T, AK>(ai, wr * RW + i * 16, s, lane);
+    for (int i = 0; i < TI; ++i) fa[i] = frag<T, AK, (AK ? 256 : BM)>(ai, wr * RW + i * 16, s, lane);
   };
   // 32 MFMAs of one k-half, interleaved segment by segment with (optionally) the fragment reads
   // of the next k-half and one LDS-DMA instruction of the next K-step every other segment, so
@@ -419,7 +422,7 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_lds_kernel(const uint16_t* __r
           } else if (j == 1 && rd && i < TJ) {
             nb[i] = frag<T, BK>(bi, wc * CW + i * 16, rs, lane);
           } else if (j == 3 && rd) {
-            na[i] = frag<T, AK>(ai, wr * RW + i * 16, rs, lane);
+            na[i] = frag<T, AK, (AK ? 256 : BM)>(ai, wr * RW + i * 16, rs, lane);
           }
           __builtin_amdgcn_sched_barrier(0);
         }
@@ -440,7 +443,7 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_lds_kernel(const uint16_t* __r
       }
       if (rd) {
         if (i < TJ) nb[i] = frag<T, BK>(bi, wc * CW + i * 16, rs, lane);
-        na[i] = frag<T, AK>(ai, wr * RW + i * 16, rs, lane);
+        na[i] = frag<T, AK, (AK ? 256 : BM)>(ai, wr * RW + i * 16, rs, lane);
       }
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -530,7 +533,7 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_lds_kernel(const uint16_t* __r
           if (f < TJ) {
             fb1[f] = frag<T, BK>(bi, wc * CW + f * 16, 1, lane);
           } else if (f < NRD) {
-            fa1[f - TJ] = frag<T, AK>(ai, wr * RW + (f - TJ) * 16, 1, lane);
+            fa1[f - TJ] = frag<T, AK, (AK ? 256 : BM)>(ai, wr * RW + (f - TJ) * 16, 1, lane);
           } else if (f == NRD) {
             __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's reads of slot kt done
             __builtin_amdgcn_s_barrier();        // barrier A: every wave's
@@ -560,7 +563,7 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_lds_kernel(const uint16_t* __r
           if (rd1 && (f & 1) == 0 && f / 2 < NRD) {
             const int r = f / 2;
             if (r < TJ) fb0[r] = frag<T, BK>(bi, wc * CW + r * 16, 0, lane);
-            else fa0[r - TJ] = frag<T, AK>(ai, wr * RW + (r - TJ) * 16, 0, lane);
+            else fa0[r - TJ] = frag<T, AK, (AK ? 256 : BM)>(ai, wr * RW + (r - TJ) * 16, 0, lane);
           }
           __builtin_amdgcn_sched_barrier(0);
         }

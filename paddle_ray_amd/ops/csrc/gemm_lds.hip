@@ -150,24 +150,35 @@ void launch_conv_cfg(const void* xpad, const void* W, const void* bias, void* Y,
       part ? part + (int64_t)tiles_m * N : nullptr, kshift);
 }
 
+// 128 x 256 tiles (8 waves of 64 x 64, 128-wide M-contiguous dy image) for the weight gradient of
+// narrow convolutions (Cout <= 128), where the 256-row tile idles half or more of its MFMA rows
+using WG128 = WCfg<2, 4, 128, 256>;
+inline int conv_wgrad_rows(int Cout) { return Cout <= 128 ? WG128::BM : W8::BM; }
+
 // dW [Cout][KH*KW*C] = dy[pix][Cout]ᵀ · im2col(x)[pix][KH*KW*C] (TN, gathered B), split-K over pixels
-template <typename T>
-void launch_conv_wgrad(const void* dy, const void* x, void* dW, int Mpix, int Cout, int Nk, const ConvGeom& cg,
-                       int splits, float* ws, hipStream_t s) {
-  const int tiles = ((Cout + BM - 1) / BM) * ((Nk + BN - 1) / BN);
+template <typename T, typename CF>
+void launch_conv_wgrad_cfg(const void* dy, const void* x, void* dW, int Mpix, int Cout, int Nk, const ConvGeom& cg,
+                           int splits, float* ws, hipStream_t s) {
+  const int tiles = ((Cout + CF::BM - 1) / CF::BM) * ((Nk + CF::BN - 1) / CF::BN);
   auto pdy = static_cast<const uint16_t*>(dy);
   auto px = static_cast<const uint16_t*>(x);
   auto pw = static_cast<uint16_t*>(dW);
   if (splits > 1) {
-    gemm_lds_kernel<T, W8, false, false, kNone, false, true, false, 0, true><<<tiles * splits, W8::NT, 0, s>>>(
+    gemm_lds_kernel<T, CF, false, false, kNone, false, true, false, 0, true><<<tiles * splits, CF::NT, 0, s>>>(
         pdy, px, nullptr, nullptr, nullptr, nullptr, Cout, Nk, Mpix, Cout, 0, Nk, Nk, splits, ws, cg);
     const int64_t quads = (int64_t)Cout * Nk / 4;
     splitk_reduce_k<T, kNone, false><<<(int)((quads + 255) / 256), 256, 0, s>>>(ws, splits, nullptr, pw, nullptr, Cout,
                                                                                Nk, Nk, Nk);
     return;
   }
-  gemm_lds_kernel<T, W8, false, false, kNone, false, false, false, 0, true><<<tiles, W8::NT, 0, s>>>(
+  gemm_lds_kernel<T, CF, false, false, kNone, false, false, false, 0, true><<<tiles, CF::NT, 0, s>>>(
       pdy, px, nullptr, pw, nullptr, nullptr, Cout, Nk, Mpix, Cout, 0, Nk, Nk, 1, nullptr, cg);
+}
+template <typename T>
+void launch_conv_wgrad(const void* dy, const void* x, void* dW, int Mpix, int Cout, int Nk, const ConvGeom& cg,
+                       int splits, float* ws, hipStream_t s) {
+  if (Cout <= 128) launch_conv_wgrad_cfg<T, WG128>(dy, x, dW, Mpix, Cout, Nk, cg, splits, ws, s);
+  else launch_conv_wgrad_cfg<T, W8>(dy, x, dW, Mpix, Cout, Nk, cg, splits, ws, s);
 }
 
 // tile by output channels: 512x64 for N <= 64, 256x128 for N <= 128, else 256x256 (split-K
@@ -219,6 +230,8 @@ extern "C" int pra_conv_lds(const void* x, const void* W, const void* bias, void
 // Convolution weight gradient on the same kernel: dW (OHWI, [Cout][KH*KW*C]) from dy
 // [N*Ho*Wo][Cout] and x [N][H][W][C]. Requires C % 64 == 0, Cout % 8 == 0, Cout >= 8, N*Ho*Wo
 // % 64 == 0, x < 2 GB. splits > 1: fp32 workspace ws [splits][Cout][KH*KW*C].
+// output-channel rows per weight-gradient tile (the caller sizes split-K from it)
+extern "C" int pra_conv_wgrad_rows(int Cout) { return pra::conv_wgrad_rows(Cout); }
 extern "C" int pra_conv_wgrad_lds(const void* dy, const void* x, void* dW, int Nimg, int H, int Wd, int C, int Cout,
                                   int KH, int KW, int S, int P, int dtype, int splits, float* ws, hipStream_t s) {
   if (C % 64 || Cout % 8 || Cout < 8 || KH <= 0 || KW <= 0 || S <= 0 || P < 0 || H <= 0 || Wd <= 0) return -1;

@@ -1615,9 +1615,11 @@ def _conv_lds(x, wk, bias, kh, kw, stride, pad, relu=False, stats_shift=None):
 
 def _conv_wgrad_ok(x, dy, cout):
     n, h, wd, c = x.shape
-    # Cout >= 256 only: the 256-row tile idles 3/4 (1/2) of its MFMA rows at Cout 64 (128), where
-    # MIOpen's wgrad is faster (profiles/r2_conv/conv3x3_wgrad.log)
-    return (_CONV_WGRAD == 'mfma' and c % 64 == 0 and cout >= 256 and cout % 8 == 0
+    # Cout <= 128 runs 128-row tiles (the 256-row tile idled 1/2 - 3/4 of its MFMA rows there and
+    # lost to MIOpen at Cout 64: profiles/r3j/conv3x3_wgrad_shapes.md); PRA_CONV_WGRAD_NARROW=0
+    # keeps those shapes on MIOpen for A/B
+    narrow_ok = cout >= 256 or (_CONV_WGRAD_NARROW and cout % 64 == 0)
+    return (_CONV_WGRAD == 'mfma' and c % 64 == 0 and narrow_ok and cout % 8 == 0
             and x.numel() * 2 < 2 ** 31
             and (dy.shape[0] * dy.shape[1] * dy.shape[2]) % 64 == 0 and max(h, wd) < 32768)
 
@@ -1632,7 +1634,8 @@ def _conv_wgrad_lds(dy, x, kh, kw, stride, pad):
     nk = kh * kw * c
     # fill ONE wave of <= 256 workgroups (a 257th starts a second round), each split >= 16
     # K-steps of 64 pixels (profiles/r2_conv/conv3x3_wgrad.log)
-    tiles = ((cout + 255) // 256) * ((nk + 255) // 256)
+    rows = L.conv_wgrad_rows(cout)
+    tiles = ((cout + rows - 1) // rows) * ((nk + 255) // 256)
     splits = max(1, min(256 // tiles, mpix // (64 * 16), 256)) if tiles < 224 else 1
     ws = torch.empty((splits, cout, nk), device=x.device, dtype=torch.float32) if splits > 1 else None
     dw = torch.empty((cout, kh, kw, c), device=x.device, dtype=x.dtype)
@@ -1643,6 +1646,7 @@ def _conv_wgrad_lds(dy, x, kh, kw, stride, pad):
 
 # weight gradient of KxK convs: 'mfma' = implicit GEMM on the in-tree kernel, 'miopen' = MIOpen
 _CONV_WGRAD = __import__('os').environ.get('PRA_CONV_WGRAD', 'mfma')
+_CONV_WGRAD_NARROW = __import__('os').environ.get('PRA_CONV_WGRAD_NARROW', '1') == '1'
 
 
 class ConvKxKFn(torch.autograd.Function):

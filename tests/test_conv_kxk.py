@@ -50,7 +50,10 @@ def test_conv_kxk_fwd_bwd(case, dtype):
 @pytest.mark.gpu
 @pytest.mark.parametrize("case", [(2, 8, 8, 64, 64, 3, 1, 1), (4, 16, 16, 64, 128, 3, 2, 1),
                                   (2, 16, 16, 128, 256, 3, 1, 1), (16, 4, 4, 256, 64, 3, 1, 0),
-                                  (1, 16, 8, 64, 72, 5, 1, 2)])
+                                  (1, 16, 8, 64, 72, 5, 1, 2),
+                                  # narrow 128-row tiles with split-K over the pixels
+                                  (8, 32, 32, 64, 64, 3, 1, 1), (8, 32, 32, 128, 128, 3, 1, 1),
+                                  (4, 16, 16, 128, 96, 3, 2, 1)])
 def test_conv_wgrad_lds(case):
     n, h, w_, cin, cout, k, s, p = case
     torch.manual_seed(0)
