@@ -56,6 +56,15 @@ int w4_mask() {
   return g_w4_mask;
 }
 
+// 128 x 256 tiles (8 waves of 64 x 64, 128-wide M-contiguous dy image) for weight gradients with
+// at most 128 output rows (narrow convolutions, Cout <= 128), where the 256-row tile idles half or
+// more of its MFMA rows. PRA_GEMM_NARROW=0 keeps the TN GEMMs on the 256-row tile (A/B).
+using WG128 = WCfg<2, 4, 128, 256>;
+bool narrow_tn() {
+  static const bool on = !getenv("PRA_GEMM_NARROW") || atoi(getenv("PRA_GEMM_NARROW")) != 0;
+  return on;
+}
+
 template <typename T, bool AK, bool BK, int E>
 void launch_e(const void* A, const void* B, const void* bias, void* C, void* Z, float* colsum, int M, int N, int K,
               int lda, int ldb, int ldc, int ldz, int beta, int splits, float* ws, hipStream_t s) {
@@ -74,10 +83,15 @@ void launch_e(const void* A, const void* B, const void* bias, void* C, void* Z, 
   if (std::is_same<T, bf16>::value && E != kRelu)
     for (int c = 0; c < 6 && alt < 0; ++c)
       if (w4_mask() >> (4 * c + layout) & 1) alt = c;
+  // TN GEMMs with <= 128 rows (one tile row either way, so split-K factors and workspaces match)
+  const bool narrow = !AK && !BK && E == kNone && M <= 128 && alt < 0 && narrow_tn();
   if (splits > 1) {
     if (alt >= 0)
       pra_gemm_alt(alt, layout, A, B, nullptr, nullptr, nullptr, nullptr, M, N, K, lda, ldb, ldc, ldz, kBF16, 0, 0,
                    splits, ws, s);
+    else if (narrow)
+      gemm_lds_kernel<T, WG128, AK, BK, kNone, false, true><<<tiles * splits, WG128::NT, 0, s>>>(
+          pa, pb, nullptr, nullptr, nullptr, nullptr, M, N, K, lda, ldb, ldc, ldz, splits, ws);
     else
       gemm_lds_kernel<T, W8, AK, BK, kNone, false, true><<<tiles * splits, W8::NT, 0, s>>>(
           pa, pb, nullptr, nullptr, nullptr, nullptr, M, N, K, lda, ldb, ldc, ldz, splits, ws);
@@ -97,6 +111,12 @@ void launch_e(const void* A, const void* B, const void* bias, void* C, void* Z, 
   if (alt >= 0 && pra_gemm_alt(alt, layout, A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, kBF16, E, beta, 1,
                                nullptr, s) == 0)
     return;
+  if constexpr (!AK && !BK && E == kNone) {
+    if (narrow) {
+      if (beta) PRA_GEMM_LAUNCH(WG128, true); else PRA_GEMM_LAUNCH(WG128, false);
+      return;
+    }
+  }
   if (beta) PRA_GEMM_LAUNCH(W8, true); else PRA_GEMM_LAUNCH(W8, false);
 #undef PRA_GEMM_LAUNCH
 }
@@ -150,9 +170,6 @@ void launch_conv_cfg(const void* xpad, const void* W, const void* bias, void* Y,
       part ? part + (int64_t)tiles_m * N : nullptr, kshift);
 }
 
-// 128 x 256 tiles (8 waves of 64 x 64, 128-wide M-contiguous dy image) for the weight gradient of
-// narrow convolutions (Cout <= 128), where the 256-row tile idles half or more of its MFMA rows
-using WG128 = WCfg<2, 4, 128, 256>;
 inline int conv_wgrad_rows(int Cout) { return Cout <= 128 ? WG128::BM : W8::BM; }
 
 // dW [Cout][KH*KW*C] = dy[pix][Cout]ᵀ · im2col(x)[pix][KH*KW*C] (TN, gathered B), split-K over pixels

@@ -109,6 +109,19 @@ def test_beta_accumulate_and_split_k():
     _close(c, _ref(1, a, b) + c0.float())
 
 
+@pytest.mark.parametrize('M,N,Kd', [(64, 256, 50176), (128, 512, 12544), (120, 264, 1024), (64, 1024, 256)])
+def test_narrow_tn_128_row_tiles(M, N, Kd):
+    """xᵀ·dy with <= 128 output rows (ResNet's 64 / 128-channel 1x1 weight gradients) on the
+    128-row tile: split-K (long pixel axis) and single-pass, plain and beta=1."""
+    torch.manual_seed(4)
+    a, b = _operands(2, M, N, Kd)
+    _close(K._gemm_hip(2, a, b), _ref(2, a, b))
+    c0 = _r(M, N)
+    c = c0.clone()
+    K._gemm_hip(2, a, b, out=c, beta=1)
+    _close(c, _ref(2, a, b) + c0.float())
+
+
 def test_linear_fn_grads():
     torch.manual_seed(4)
     x = _r(4, 128, 256).requires_grad_(True)
