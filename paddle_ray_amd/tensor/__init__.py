@@ -260,6 +260,10 @@ Tensor.mod = math.remainder
 Tensor.floor_divide = math.floor_divide
 Tensor.floor_mod = math.remainder
 Tensor.exp_ = math.exp_
+Tensor.erfinv_ = math.erfinv_
+Tensor.remainder_ = math.remainder_
+Tensor.lerp_ = math.lerp_
+Tensor.put_along_axis_ = manipulation.put_along_axis_
 Tensor.sqrt_ = math.sqrt_
 Tensor.tanh_ = math.tanh_
 Tensor.sigmoid_ = math.sigmoid_

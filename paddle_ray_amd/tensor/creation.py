@@ -23,6 +23,16 @@ def _dev():
     return _default_device()
 
 
+def create_tensor(dtype, name=None, persistable=False):
+    """An empty tensor of ``dtype`` to be filled later, e.g. by ``paddle.assign`` (parity:
+    python/paddle/tensor/creation.py create_tensor; dygraph form: shape [0])."""
+    t = zeros([0], dtype=dtype)
+    t.persistable = bool(persistable)
+    if name is not None:
+        t.name = name
+    return t
+
+
 def zeros(shape, dtype=None, name=None):
     return Tensor(torch.zeros(_shape(shape), dtype=_dt(dtype), device=_dev()))
 
@@ -137,7 +147,11 @@ def assign(x, output=None):
             t = t.to(get_default_dtype())
     if output is not None:
         with torch.no_grad():
-            output._t.copy_(t)
+            if output._t.shape != t.shape and output._t.numel() == 0:
+                # an empty placeholder (create_tensor): takes the value's shape, keeps its dtype
+                output._t.set_(t.to(output._t.dtype).contiguous())
+            else:
+                output._t.copy_(t)
         return output
     return Tensor(t)
 

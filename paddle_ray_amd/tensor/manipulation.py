@@ -282,6 +282,13 @@ def put_along_axis(arr, indices, values, axis, reduce='assign', include_self=Tru
     return Tensor(a.scatter_reduce(axis, i, v, red, include_self=include_self))
 
 
+def put_along_axis_(arr, indices, values, axis, reduce='assign', include_self=True,
+                    broadcast=True):
+    """In-place put_along_axis (parity: python/paddle/tensor/manipulation.py put_along_axis_)."""
+    arr._t.copy_(_t(put_along_axis(arr, indices, values, axis, reduce, include_self, broadcast)))
+    return arr
+
+
 def take(x, index, mode='raise', name=None):
     t, i = _t(x).flatten(), _t(index).long()
     n = t.numel()

@@ -254,6 +254,30 @@ def fill_(x, value):
     return x
 
 
+def erfinv_(x, name=None):
+    """In-place erfinv (parity: python/paddle/tensor/math.py erfinv_)."""
+    x._t.erfinv_()
+    return x
+
+
+def remainder_(x, y, name=None):
+    """In-place floor-mod x %= y (parity: python/paddle/tensor/math.py remainder_)."""
+    x._t.copy_(torch.remainder(x._t, _t(y, like=x._t)))
+    return x
+
+
+def lerp_(x, y, weight, name=None):
+    """In-place x += weight * (y - x) (parity: python/paddle/tensor/math.py lerp_)."""
+    x._t.lerp_(_t(y, like=x._t), _t(weight, like=x._t))
+    return x
+
+
+def rank(input):
+    """Number of dimensions as a 0-D int32 tensor (parity: python/paddle/tensor/attribute.py rank)."""
+    t = _t(input)
+    return Tensor(torch.tensor(t.dim(), dtype=torch.int32, device=t.device))
+
+
 def as_complex(x, name=None):
     return Tensor(torch.view_as_complex(_t(x)))
 
