@@ -1,9 +1,10 @@
 """paddle.jit (parity: python/paddle/jit/api.py, python/paddle/jit/translated_layer.py,
 python/paddle/jit/dy2static/program_translator.py).
 
-MI355X design — no AST transcription. ``to_static`` keeps eager semantics for training
-(the PyTorch-ROCm autograd tape already drives our HIP kernels) and adds two things the
-reference's dy2static is used for:
+MI355X design. ``to_static`` keeps eager semantics for training (the PyTorch-ROCm autograd
+tape already drives our HIP kernels); tensor-valued ``if`` / ``while`` are transcribed only for
+program export (``jit/dy2static.py``, applied by ``jit.save`` / ``concrete_program``). It adds
+the things the reference's dy2static is used for:
 
 * **HIP-graph replay** for gradient-free calls on the GPU: the first call for a given
   input signature captures the whole forward into a ``torch.cuda.CUDAGraph`` (= hipGraph

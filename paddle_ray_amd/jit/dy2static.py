@@ -368,7 +368,7 @@ def _tuple(names, ctx):
 
 
 def _call(fn, args):
-    return ast.Call(func=ast.Attribute(value=ast.Name('__pra_jst', ast.Load()), attr=fn,
+    return ast.Call(func=ast.Attribute(value=ast.Name('_pra_jst', ast.Load()), attr=fn,
                                        ctx=ast.Load()), args=args, keywords=[])
 
 
@@ -389,6 +389,11 @@ def _source_tree(fn):
 
 @functools.lru_cache(maxsize=None)
 def _convert_code(func):
+    """Compile the converted ``func`` inside a factory whose parameters are the original's free
+    variables (+ ``_pra_jst``), itself inside a class statement named like the owning class:
+    the rebuilt function then has real closure cells (``nonlocal`` writes, zero-argument
+    ``super()`` through ``__class__``) and the owner's private-name mangling. Returns the inner
+    code object, or None when there is nothing to convert."""
     import sys
     tree, fdef = _source_tree(func)
     fdef.body = _fold_early_returns(fdef.body)
@@ -396,9 +401,33 @@ def _convert_code(func):
     fdef.body = [x for s in fdef.body for x in _as_list(tr.visit(s))]
     if tr.n == 0:
         return None
-    ast.fix_missing_locations(tree)
-    code = compile(tree, filename=f'<dy2static {func.__qualname__}>', mode='exec')
-    return code, fdef.name, sys.modules[__name__]
+    params = [n for n in func.__code__.co_freevars if n != '__class__'] + ['_pra_jst']
+    factory = ast.FunctionDef(
+        name='_pra_factory',
+        args=ast.arguments(posonlyargs=[], args=[ast.arg(arg=p) for p in params], vararg=None,
+                           kwonlyargs=[], kw_defaults=[], kwarg=None, defaults=[]),
+        body=[fdef, ast.Return(value=ast.Name(fdef.name, ast.Load()))], decorator_list=[],
+        returns=None, type_comment=None)
+    parts = func.__qualname__.split('.')
+    owner = parts[-2] if len(parts) >= 2 and parts[-2] != '<locals>' else None
+    body = [ast.ClassDef(name=owner, bases=[], keywords=[], body=[factory], decorator_list=[])] \
+        if owner else [factory]
+    mod = ast.Module(body=body, type_ignores=[])
+    ast.fix_missing_locations(mod)
+    code = compile(mod, filename=f'<dy2static {func.__qualname__}>', mode='exec')
+
+    def find(c, name):
+        for k in c.co_consts:
+            if isinstance(k, types.CodeType):
+                if k.co_name == name:
+                    return k
+                r = find(k, name)
+                if r is not None:
+                    return r
+        return None
+    fac = find(code, '_pra_factory')
+    inner = next(k for k in fac.co_consts if isinstance(k, types.CodeType) and k.co_name == fdef.name)
+    return inner, sys.modules[__name__]
 
 
 def _as_list(x):
@@ -407,30 +436,30 @@ def _as_list(x):
 
 def convert_function(fn):
     """The control-flow-converted twin of ``fn`` (a function or bound method); ``fn`` itself
-    when it has nothing to convert or its source is unavailable."""
+    when it has nothing to convert, its source is unavailable, or its closure cannot be rebuilt.
+    The twin runs in ``fn``'s own globals with ``fn``'s own closure cells."""
     bound = getattr(fn, '__self__', None) if inspect.ismethod(fn) else None
     func = fn.__func__ if bound is not None else fn
     if not inspect.isfunction(func):
         return fn
     try:
         r = _convert_code(func)
-    except (OSError, TypeError, SyntaxError, IndentationError):
+    except (OSError, TypeError, SyntaxError, IndentationError, StopIteration):
         return fn
     if r is None:
         return fn
-    code, name, jst = r
-    glb = dict(func.__globals__)
-    if func.__closure__:
-        for n, c in zip(func.__code__.co_freevars, func.__closure__):
-            try:
-                glb[n] = c.cell_contents
-            except ValueError:  # an empty cell
-                pass
-    glb['__pra_jst'] = jst
-    ns = {}
-    exec(code, glb, ns)
-    new = ns[name]
-    new.__defaults__ = func.__defaults__
+    inner, jst = r
+    cells = dict(zip(func.__code__.co_freevars, func.__closure__ or ()))
+    closure = []
+    for n in inner.co_freevars:
+        if n == '_pra_jst':
+            closure.append(types.CellType(jst))
+        elif n in cells:
+            closure.append(cells[n])
+        else:  # (e.g. __class__ without the original's cell): keep the unconverted function
+            return fn
+    new = types.FunctionType(inner, func.__globals__, func.__name__, func.__defaults__, tuple(closure))
     new.__kwdefaults__ = func.__kwdefaults__
+    new.__qualname__ = func.__qualname__
     new._pra_converted = True
     return types.MethodType(new, bound) if bound is not None else new

@@ -1062,19 +1062,17 @@ def _mask_strides(mask, B, H, Sq, Sk):
     return m, m.stride(0), m.stride(1), m.stride(2), m.dtype == torch.float32
 
 
-_FA_RNG_OFFSET = [0]
-
-
 def _fa_next_rng(seed=None, numel=1):
-    """(seed, offset) for one dropout call: the generator's seed, and an offset advanced per call
-    (the Philox-offset discipline of the reference's flash_attn kernels)."""
+    """(seed, offset) for one dropout call. Without an explicit seed, a fresh per-call seed is
+    drawn from the host generator (`_dropout_seed`), i.e. from the RNG state that paddle.seed
+    sets, that recompute saves / restores around a re-run segment and that the model-parallel
+    RNG tracker swaps per rank: a recomputed forward draws the same mask as the original one, and
+    tensor-parallel ranks draw different masks for their local heads (the reference's flash_attn
+    kernels take (seed, offset) from the same generator, paddle/phi/kernels/gpu/flash_attn_kernel.cu).
+    An explicit seed is used as given with offset 0 (bit-exact replays in tests)."""
     if seed is None:
-        seed = int(torch.initial_seed()) & ((1 << 63) - 1)
-    off = _FA_RNG_OFFSET[0]
-    _FA_RNG_OFFSET[0] += 1
-    return seed, off
-
-
+        return _dropout_seed() & ((1 << 63) - 1), 0
+    return int(seed), 0
 
 
 class FlashAttnExtFn(torch.autograd.Function):
@@ -1196,11 +1194,26 @@ def flash_attention_ext(q, k, v, causal=False, scale=None, attn_mask=None, dropo
             ~attn_mask, float('-inf'))
     if attn_mask is not None and attn_mask.dtype not in (q.dtype, torch.float32):
         attn_mask = attn_mask.to(q.dtype)
-    sd, off = _fa_next_rng(seed) if dropout > 0 else (0, 0)
     if _fa_ext_ok(q, k, v):
+        sd, off = _fa_next_rng(seed) if dropout > 0 else (0, 0)
         R._STATS[('flash_attn_ext', 'hip')] += 1
         return FlashAttnExtFn.apply(q, k, v, attn_mask, None, None, Sq, Sk, causal, scale,
                                     float(dropout), sd, off)
+    if q.is_cuda and seed is None:
+        # outside what the kernel covers (head_dim not 64/128, fp32, strided inputs) and no
+        # bit-exact dropout requested: torch's memory-efficient SDPA, never the O(S^2) fp32
+        # reference that keeps scores, probabilities and mask alive for autograd
+        R._STATS[('flash_attn_ext', 'sdpa')] += 1
+        qt, kt, vt = (t.transpose(1, 2) for t in (q, k, v))
+        am = None if attn_mask is None else attn_mask.to(q.dtype)
+        if causal and am is not None:  # mask + causal: fold the causal part into the mask
+            cm = torch.ones(Sq, Sk, dtype=torch.bool, device=q.device).triu(Sk - Sq + 1)
+            am = am.masked_fill(cm, float('-inf'))
+        o = torch.nn.functional.scaled_dot_product_attention(
+            qt, kt, vt, attn_mask=am, dropout_p=float(dropout), is_causal=bool(causal) and am is None,
+            scale=scale)
+        return o.transpose(1, 2)
+    sd, off = _fa_next_rng(seed) if dropout > 0 else (0, 0)
     R._STATS[('flash_attn_ext', 'ref')] += 1
     o, _ = _fa_ext_ref_dense(q, k, v, causal, scale, attn_mask, dropout, sd, off)
     return o.to(q.dtype)

@@ -108,7 +108,7 @@ class ShardedState:
 
     def __init__(self, layer, level, group=None, segment_bytes=128 << 20, grad_fp32=False,
                  dp_group=None, segment_size=2 ** 20, exclude_layer=None,
-                 release_after_forward='auto'):
+                 release_after_forward=True):
         from ..distributed import collective as C
         self.layer = layer
         self.stage = LEVELS[level] if isinstance(level, str) else int(level)
@@ -211,22 +211,24 @@ class ShardedState:
                     self.groups[gi].release_grads()
 
     def _resolve_release(self, mode):
-        """``release_after_forward``: True frees every unit after its forward and re-gathers
-        it in backward (minimum memory); False keeps the gathered units resident from their
-        forward to their gradient reduce-scatter (no backward re-gather traffic); 'auto' keeps
+        """``release_after_forward``: True (the default, as the reference's ForwardPostHooks,
+        group_sharded_stage3.py:828) frees every unit after its forward and re-gathers it in
+        backward (minimum memory); False keeps the gathered units resident from their forward to
+        their gradient reduce-scatter (no backward re-gather traffic); 'auto' (opt-in) keeps
         them when the full unit parameters fit in ``PRA_ZERO3_RESIDENT_FRAC`` (default 0.25) of
-        the device memory — SURVEY §3: with 288 GB per MI355X a 1.3B model's gathered bf16
-        weights (2.6 GB) are about 1 % of HBM."""
-        if mode != 'auto':
-            return bool(mode)
+        the device memory LEFT FREE at wrap time — SURVEY §3: with 288 GB per MI355X a 1.3B
+        model's gathered bf16 weights (2.6 GB) are about 1 % of HBM. ``PRA_ZERO3_RESIDENT=1``
+        turns the resident mode on (0: off) whatever the argument."""
         env = __import__('os').environ.get('PRA_ZERO3_RESIDENT')
         if env is not None:
             return env in ('0', 'false', 'False')
+        if mode != 'auto':
+            return bool(mode)
         if not self.zero3 or not self.groups or self.groups[0].device.type != 'cuda':
             return True
         unit_bytes = sum(self.groups[gi].numel * self.groups[gi].param_buf.element_size()
                          for u in self.unit_meta for gi in u.gids)
-        total = torch.cuda.get_device_properties(self.groups[0].device).total_memory
+        total = torch.cuda.mem_get_info(self.groups[0].device)[0]
         frac = float(__import__('os').environ.get('PRA_ZERO3_RESIDENT_FRAC', '0.25'))
         return unit_bytes > frac * total
 
@@ -475,9 +477,13 @@ class _StepOverlap:
         return hook
 
     def _wait(self, ph):
-        ev = self.events[min(ph, len(self.events) - 1)]
-        if ev is not None:
-            torch.cuda.current_stream(self.device).wait_event(ev)
+        # the latest recorded event at or before phase ph: a phase with no trainable pieces
+        # records none, and must not let the reader skip an earlier phase still being written
+        for i in range(min(ph, len(self.events) - 1), -1, -1):
+            ev = self.events[i]
+            if ev is not None:
+                torch.cuda.current_stream(self.device).wait_event(ev)
+                return
 
     def before_forward(self):
         self._wait(1)  # root and unit 0 (GPT applies block 0's ln1 before calling the block)
@@ -974,7 +980,7 @@ class ShardedModel(Layer):
 def group_sharded_parallel(model, optimizer, level, scaler=None, group=None, offload=False,
                            sync_buffers=False, buffer_max_size=2 ** 23, segment_size=2 ** 20,
                            sync_comm=False, dp_group=None, exclude_layer=None,
-                           bucket_mb=128, release_after_forward='auto'):
+                           bucket_mb=128, release_after_forward=True):
     """paddle.distributed.sharding.group_sharded_parallel (parity:
     python/paddle/distributed/sharding/group_sharded.py). ``offload=True`` keeps the fp32
     master weights and optimizer moments in host memory (the update runs on the CPU)."""

@@ -197,8 +197,7 @@ def test_packed_qkv_ext_matches_unpacked():
     o = K.flash_attention_ext_qkvpacked(qkv, attn_mask=m, dropout=0.1, seed=11)
     g = torch.randn_like(o)
     o.backward(g)
-    K._FA_RNG_OFFSET[0] -= 1  # same offset for the unpacked call
-    q2 = qkv.detach().clone().requires_grad_(True)
+    q2 =qkv.detach().clone().requires_grad_(True)
     q, k, v = q2.unbind(2)
     o2 = K.flash_attention_ext(q, k, v, attn_mask=m, dropout=0.1, seed=11)
     o2.backward(g)
@@ -264,3 +263,44 @@ def test_framework_graph_entry_advances_dropout_per_replay():
     torch.cuda.synchronize()
     assert not torch.equal(o1, o2)
     assert torch.isfinite(o1.float()).all() and torch.isfinite(o2.float()).all()
+
+
+def _recompute_dropout_case(dev):
+    """A block of flash attention with dropout: the gradients with recompute (the segment re-runs
+    in backward) must equal the gradients without it, i.e. the re-run draws the same mask."""
+    from paddle_ray_amd.parallel.recompute import recompute
+    dt = torch.bfloat16 if dev.type == 'cuda' else torch.float32
+    B, S, H, D = 2, 64, 2, 64
+    torch.manual_seed(3)
+    x = torch.randn(B, S, H * D, device=dev, dtype=dt)
+    w = torch.randn(H * D, 3 * H * D, device=dev, dtype=dt) * 0.05
+
+    def block(xx, ww):
+        xx, ww = getattr(xx, '_t', xx), getattr(ww, '_t', ww)  # (recompute passes paddle Tensors)
+        q, k, v = (xx @ ww).view(B, S, 3, H, D).unbind(2)
+        return K.flash_attention_ext(q, k, v, causal=True, dropout=0.3).reshape(B, S, H * D)
+
+    grads = []
+    for use_rc in (False, True):
+        paddle.seed(11)
+        xx = x.clone().requires_grad_(True)
+        ww = w.clone().requires_grad_(True)
+        out = recompute(block, xx, ww) if use_rc else block(xx, ww)
+        out = out._t if hasattr(out, '_t') else out
+        (out.float() ** 2).sum().backward()
+        grads.append((out.detach().float(), xx.grad.float(), ww.grad.float()))
+    for a, b in zip(*grads):
+        assert torch.equal(a, b)
+    # and a different seed draws a different mask
+    paddle.seed(12)
+    o3 = block(x, w)
+    assert not torch.equal(o3.float(), grads[0][0])
+
+
+def test_recompute_flash_dropout_same_mask_cpu():
+    _recompute_dropout_case(torch.device('cpu'))
+
+
+@pytest.mark.gpu
+def test_recompute_flash_dropout_same_mask_gpu():
+    _recompute_dropout_case(torch.device('cuda'))

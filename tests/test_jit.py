@@ -217,3 +217,76 @@ def test_dy2static_converter_units():
     assert getattr(cg, '_pra_converted', False)
     for x, n in ((3, 5), (1, 2), (4, 0)):
         assert cg(x, n) == g(x, n)
+
+
+_DY2S_GLOBAL_HITS = 0
+
+
+class _PlainParent(paddle.nn.Layer):
+    def __init__(self):
+        super().__init__()
+        self.l = paddle.nn.Linear(4, 4)
+
+    def forward(self, x):
+        return self.l(x) + 1.0
+
+
+class _BranchyChild(_PlainParent):
+    """Converted forward with zero-argument super(), a private (mangled) attribute and a
+    ``global`` write: the twin must keep the class cell, the owner's mangling and the real
+    module globals."""
+
+    def __init__(self):
+        super().__init__()
+        self.__scale = 3.0
+
+    def forward(self, x):
+        global _DY2S_GLOBAL_HITS
+        _DY2S_GLOBAL_HITS += 1
+        if x.mean() > 0:
+            x = x * self.__scale
+        else:
+            x = x - 1.0
+        return super().forward(x)
+
+
+def test_dy2static_super_private_global(tmp_path):
+    from paddle_ray_amd.jit.dy2static import convert_function
+    paddle.seed(0)
+    net = _BranchyChild()
+    net.l.weight.set_value(np.eye(4, dtype='float32'))
+    net.l.bias.set_value(np.zeros(4, 'float32'))
+    pos = paddle.to_tensor(np.full((2, 4), 1.0, 'float32'))
+    f = convert_function(net.forward)
+    assert getattr(f, '_pra_converted', False)
+    before = _DY2S_GLOBAL_HITS
+    np.testing.assert_allclose(f(pos).numpy(), net(pos).numpy())
+    assert _DY2S_GLOBAL_HITS == before + 2  # the twin wrote the module's real global
+    path = str(tmp_path / 'child')
+    paddle.jit.save(net, path, input_spec=[InputSpec([None, 4], 'float32')])
+    ld = paddle.jit.load(path)
+    neg = paddle.to_tensor(np.full((2, 4), -1.0, 'float32'))
+    for x in (pos, neg):
+        np.testing.assert_allclose(ld(x).numpy(), net(x).numpy(), rtol=1e-6)
+
+
+def test_dy2static_nonlocal_closure():
+    from paddle_ray_amd.jit.dy2static import convert_function
+    calls = [0]
+    k = 2.0
+
+    def g(x):
+        nonlocal k
+        calls[0] += 1
+        if x.sum() > 0:
+            y = x * k
+        else:
+            y = x
+        k = k + 1.0
+        return y
+
+    cg = convert_function(g)
+    assert getattr(cg, '_pra_converted', False)
+    out = cg(paddle.ones([2]))
+    np.testing.assert_allclose(out.numpy(), [2.0, 2.0])
+    assert k == 3.0 and calls[0] == 1  # the nonlocal write reached the real cell
