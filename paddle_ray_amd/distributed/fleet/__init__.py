@@ -25,7 +25,7 @@ class DistributedStrategy:
         self.hybrid_configs = {'dp_degree': -1, 'mp_degree': 1, 'pp_degree': 1,
                                'sharding_degree': 1}
         self.pipeline_configs = {'micro_batch_size': 1, 'accumulate_steps': 1,
-                                 'schedule_mode': '1F1B'}
+                                 'schedule_mode': '1F1B', 'enable_partial_send_recv': True}
         self.sharding = False
         self.sharding_configs = {'sharding_degree': 1, 'stage': 1, 'segment_broadcast_MB': 32}
         self.amp = False

@@ -1,8 +1,8 @@
 """Transformer layers (parity: python/paddle/nn/layer/transformer.py).
 
-MultiHeadAttention uses the gfx950 flash-attention kernel when there is no
-explicit attn_mask and no attention dropout; masked/dropout paths use a
-composed softmax(QK^T)V.
+MultiHeadAttention runs on the gfx950 flash-attention kernels: the plain kernel without a
+mask or dropout, the extended kernel (additive / padding mask, in-kernel dropout) otherwise.
+Only ``need_weights=True`` (the probabilities are returned) uses a composed softmax(QK^T)V.
 """
 import collections
 import copy
@@ -74,10 +74,8 @@ class MultiHeadAttention(Layer):
                 cache = self.Cache(Tensor(k), Tensor(v))
         drop = self.dropout if self.training else 0.0
         weights = None
-        if attn_mask is None and drop == 0.0 and not self.need_weights and q.is_cuda and \
-                q.dtype in (torch.bfloat16, torch.float16):
-            o = K.flash_attention(q, k, v, causal=False)
-        else:
+        if self.need_weights:
+            # the probabilities are an output: the composed softmax(QK^T)V path
             qt, kt, vt = (t.transpose(1, 2) for t in (q, k, v))
             s = torch.matmul(qt, kt.transpose(-1, -2)) * (self.head_dim ** -0.5)
             m = _convert_attention_mask(attn_mask, s.dtype)
@@ -88,6 +86,15 @@ class MultiHeadAttention(Layer):
             if drop:
                 p = torch.nn.functional.dropout(p, drop, True)
             o = torch.matmul(p, vt).transpose(1, 2)
+        elif attn_mask is None and drop == 0.0 and q.is_cuda and \
+                q.dtype in (torch.bfloat16, torch.float16):
+            o = K.flash_attention(q, k, v, causal=False)
+        else:
+            # additive / boolean padding masks and attention dropout: the flash kernel's extended
+            # path (mask added to the scaled scores, dropout bits drawn in-kernel); on the host
+            # and for head dims the kernel does not cover, the same math in fp32 / torch SDPA
+            m = _convert_attention_mask(attn_mask, q.dtype if q.is_cuda else torch.float32)
+            o = K.flash_attention_ext(q, k, v, causal=False, attn_mask=m, dropout=drop).to(q.dtype)
         o = o.reshape(o.shape[0], o.shape[1], self.embed_dim)
         out = self.out_proj(Tensor(o))
         outs = [out]

@@ -236,9 +236,19 @@ class _P2P:
     soon as its send has completed (checked at every new send), not at batch end.
     Activations may be tuples; only floating tensors carry gradients back."""
 
-    def __init__(self, hcg, virtual=1):
+    def __init__(self, hcg, virtual=1, partial=True):
         from ..distributed import collective as C
         self.hcg = hcg
+        # partial send/recv (parity: pp_utils/p2p_communication.py:180-295): the activation at a
+        # stage boundary is identical on every tensor-parallel rank, so each mp rank moves only
+        # its 1/mp slice over its own pipe channel and the receiving stage all-gathers the
+        # slices over the mp group (xGMI point-to-point bytes / mp; the all-gather rides the
+        # mp group's links, which sit idle at the pipeline boundary)
+        mg = hcg.get_model_parallel_group() if hasattr(hcg, 'get_model_parallel_group') else None
+        self.mp = mg.nranks if (partial and mg is not None) else 1
+        self.mp_rank = hcg.get_model_parallel_rank() if self.mp > 1 else 0
+        self.mp_pg = mg.process_group if self.mp > 1 else None
+        self.bytes_sent = 0   # activation / gradient payload bytes this rank has sent (stats)
         self.stage = hcg.get_stage_id()
         self.nstages = hcg.get_pipe_parallel_world_size()
         g = hcg.get_pipe_parallel_group()
@@ -273,14 +283,30 @@ class _P2P:
     def _prune(self):
         self.pending = [(w, t) for w, t in self.pending if not w.is_completed()]
 
-    def _isend(self, t, peer, pg, what):
+    def _partial_ok(self, t):
+        return self.mp > 1 and t.numel() > 0 and t.numel() % self.mp == 0
+
+    def _isend(self, t, peer, pg, what, partial=False):
         t = t.detach().contiguous()
+        if partial and self._partial_ok(t):
+            t = t.view(-1).chunk(self.mp)[self.mp_rank]   # this mp rank's slice (contiguous)
+            what = what + '.partial'
         self._prune()
         w = _watchdog.track(f'pp.{what}', dist.isend(t, peer, group=pg), 2)
+        if what != 'meta':
+            self.bytes_sent += t.numel() * t.element_size()
         self.pending.append((w, t))
         self.peak_pending = max(self.peak_pending, len(self.pending))
 
-    def _recv(self, t, peer, pg, what):
+    def _recv(self, t, peer, pg, what, partial=False):
+        if partial and self._partial_ok(t):
+            flat = t.view(-1)
+            mine = flat.chunk(self.mp)[self.mp_rank]
+            _watchdog.track(f'pp.{what}.partial', dist.irecv(mine, peer, group=pg), 2).wait()
+            # every mp rank received its own slice: gather the whole activation
+            _watchdog.track(f'pp.{what}.allgather', dist.all_gather_into_tensor(
+                flat, mine.clone(), group=self.mp_pg, async_op=True), self.mp).wait()
+            return t
         _watchdog.track(f'pp.{what}', dist.irecv(t, peer, group=pg), 2).wait()
         return t
 
@@ -299,7 +325,7 @@ class _P2P:
             self._isend(m.to(self.dev), peer, pg, 'meta')
             self.meta_sent.add(pg)
         for t in ts:
-            self._isend(t, peer, pg, 'send_fwd')
+            self._isend(t, peer, pg, 'send_fwd', partial=True)
 
     def recv_acts(self, src_stage):
         pg = self._ch('act', src_stage, self.stage)
@@ -315,7 +341,8 @@ class _P2P:
             self.meta_from[pg] = meta
         out = []
         for shp, dt in self.meta_from[pg]:
-            t = self._recv(torch.empty(shp, dtype=dt, device=self.dev), peer, pg, 'recv_fwd')
+            t = self._recv(torch.empty(shp, dtype=dt, device=self.dev), peer, pg, 'recv_fwd',
+                           partial=True)
             out.append(t.requires_grad_(t.is_floating_point()))
         return out
 
@@ -323,12 +350,12 @@ class _P2P:
         pg = self._ch('grad', self.stage, dst_stage)
         peer = self.ranks[dst_stage % self.nstages]
         for g in grads:
-            self._isend(g, peer, pg, 'send_bwd')
+            self._isend(g, peer, pg, 'send_bwd', partial=True)
 
     def recv_grads(self, like, src_stage):
         pg = self._ch('grad', src_stage, self.stage)
         peer = self.ranks[src_stage % self.nstages]
-        return [self._recv(torch.empty_like(t), peer, pg, 'recv_bwd') for t in like
+        return [self._recv(torch.empty_like(t), peer, pg, 'recv_bwd', partial=True) for t in like
                 if t.is_floating_point()]
 
     def new_batch(self):
@@ -371,7 +398,8 @@ class PipelineParallel(Layer):
         self.is_first = hcg.is_first_stage()
         self.is_last = hcg.is_last_stage()
         V = layers._num_virtual if isinstance(layers, PipelineLayer) else 1
-        self._p2p = _P2P(hcg, V) if hcg.get_pipe_parallel_world_size() > 1 else None
+        self._p2p = _P2P(hcg, V, partial=bool(cfg.get('enable_partial_send_recv', True))) \
+            if hcg.get_pipe_parallel_world_size() > 1 else None
         self.total_loss = None
         self.peak_live_units = 0
         self._dp_group = hcg.get_data_parallel_group()

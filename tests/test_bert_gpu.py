@@ -1,6 +1,6 @@
 """BERT encoder layer on the device: the fused path (packed-QKV flash attention with the key
-padding mask, GEMM+bias+GELU epilogue MLP, add+dropout+LayerNorm kernels) against the unfused
-torch composition of the same layer, forward and backward."""
+padding mask, GEMM+bias+GELU epilogue MLP, add+dropout+LayerNorm kernels) against an fp32 copy of
+the same layer on the unfused torch composition, forward and backward."""
 import pytest
 import torch
 
@@ -21,22 +21,25 @@ def test_bert_layer_fused_matches_unfused():
     mask = torch.zeros(B, 1, 1, S, device='cuda', dtype=torch.bfloat16)
     mask[1, ..., 200:] = -1e4
     g = torch.randn(B, S, cfg.hidden_size, device='cuda', dtype=torch.bfloat16)
-    outs = []
-    for fused in (True, False):
-        layer.fused = fused
-        xi = paddle.Tensor(x.clone().requires_grad_(True))
-        y = layer(xi, paddle.Tensor(mask))
-        y._t.backward(g)
-        grads = [p.grad._t.float().clone() if hasattr(p.grad, '_t') else p.grad.float().clone()
-                 for p in (layer.fc1.weight, layer.fc1.bias, layer.attn.qkv_proj.weight)]
-        outs.append((y._t.float(), xi._t.grad.float(), grads))
-        for p in layer.parameters():
-            p.clear_gradient()
-    (y1, dx1, g1), (y2, dx2, g2) = outs
+    import copy
+    ref = copy.deepcopy(layer)
+    ref.to(dtype='float32')   # fp32 reference: the unfused torch composition in fp32
+    ref.fused = False
+    layer.fused = True
+    xi = paddle.Tensor(x.clone().requires_grad_(True))
+    y = layer(xi, paddle.Tensor(mask))
+    y._t.backward(g)
+    xr = paddle.Tensor(x.float().clone().requires_grad_(True))
+    yr = ref(xr, paddle.Tensor(mask.float()))
+    yr._t.backward(g.float())
+
+    def grads(m):
+        return [p.grad._t.float() if hasattr(p.grad, '_t') else p.grad.float()
+                for p in (m.fc1.weight, m.fc1.bias, m.attn.qkv_proj.weight)]
 
     def rel(a, b):
-        return ((a - b).abs().max() / b.abs().max().clamp_min(1e-6)).item()
-    assert rel(y1, y2) < 3e-2
-    assert rel(dx1, dx2) < 5e-2
-    for a, b in zip(g1, g2):
+        return ((a.float() - b).abs().max() / b.abs().max().clamp_min(1e-6)).item()
+    assert rel(y._t, yr._t) < 3e-2
+    assert rel(xi._t.grad, xr._t.grad) < 5e-2
+    for a, b in zip(grads(layer), grads(ref)):
         assert rel(a, b) < 5e-2

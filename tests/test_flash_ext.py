@@ -304,3 +304,38 @@ def test_recompute_flash_dropout_same_mask_cpu():
 @pytest.mark.gpu
 def test_recompute_flash_dropout_same_mask_gpu():
     _recompute_dropout_case(torch.device('cuda'))
+
+
+@pytest.mark.gpu
+def test_transformer_encoder_mask_dropout_on_flash_ext():
+    """nn.TransformerEncoderLayer with a key-padding mask and attention dropout runs the extended
+    flash kernel (registry: flash_attn_ext/hip) and matches an fp32 host copy of the same layer
+    that applies the SAME dropout bits (same host seed, fa_dropout_mask_ref)."""
+    from paddle_ray_amd.ops import registry as R
+    import copy
+    paddle.seed(21)
+    d, nh, B, S = 256, 4, 2, 128
+    layer = paddle.nn.TransformerEncoderLayer(d, nh, 512, dropout=0.0, attn_dropout=0.2)
+    layer.train()
+    ref = copy.deepcopy(layer)
+    layer.to(device='gpu', dtype='bfloat16')
+    x = paddle.randn([B, S, d])
+    mask = np.zeros((B, 1, 1, S), 'float32')
+    mask[1, ..., 100:] = -1e9
+    xg = paddle.to_tensor(x.numpy(), place='gpu').astype('bfloat16')
+    xg.stop_gradient = False
+    R.reset_stats()
+    paddle.seed(77)
+    y = layer(xg, paddle.to_tensor(mask, place='gpu').astype('bfloat16'))
+    assert R.stats().get(('flash_attn_ext', 'hip'), 0) > 0, R.stats()
+    g = paddle.randn(y.shape)
+    y.backward(paddle.to_tensor(g.numpy(), place='gpu').astype('bfloat16'))
+    xc = paddle.to_tensor(x.numpy())
+    xc.stop_gradient = False
+    paddle.seed(77)
+    yr = ref(xc, paddle.to_tensor(mask))
+    yr.backward(g)
+    yv, yrv = y.astype('float32').numpy(), yr.numpy()
+    assert np.abs(yv - yrv).max() / np.abs(yrv).max() < 3e-2
+    gx, gxr = xg.grad.astype('float32').numpy(), xc.grad.numpy()
+    assert np.abs(gx - gxr).max() / np.abs(gxr).max() < 5e-2
