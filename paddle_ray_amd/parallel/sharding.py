@@ -532,6 +532,18 @@ class _StepOverlap:
         return True
 
 
+class _ShardPiece:
+    """Stand-in parameter for one owned shard piece, handed to an element-wise inner optimizer's
+    ``_update`` (its accumulators are keyed by ``name``; ``_t`` is the fp32 target slice)."""
+
+    def __init__(self, name, t, param):
+        self.name = name
+        self._t = t
+        self.optimize_attr = getattr(param, 'optimize_attr', {'learning_rate': 1.0})
+        self.stop_gradient = False
+        self.param = param
+
+
 class ShardedOptimizer:
     """Owned-shard optimizer driving the fused multi-tensor HIP kernel.
 
@@ -544,8 +556,18 @@ class ShardedOptimizer:
         self._inner = optimizer
         self.state = state
         self._kind = type(optimizer).__name__
-        if self._kind not in ('Adam', 'AdamW', 'Momentum', 'SGD'):
-            raise NotImplementedError(f"sharding does not support {self._kind} yet")
+        # Adam / AdamW / Momentum / SGD run the multi-tensor HIP kernels over the flat shards;
+        # every other optimizer (Lamb, Adagrad, Adadelta, Adamax, RMSProp: the reference wraps
+        # any inner optimizer, dygraph_sharding_optimizer.py:29-212) runs its own per-element
+        # update on this rank's shard pieces, with its accumulators kept as flat per-group
+        # shards (so checkpoints gather / re-slice them like the moments); Lamb's trust ratio
+        # needs whole-parameter norms: one all-reduce of the per-parameter partial sums
+        from ..optimizer.optimizer import _ForeachOpt
+        self._generic = self._kind not in ('Adam', 'AdamW', 'Momentum', 'SGD')
+        if self._generic and not isinstance(optimizer, _ForeachOpt):
+            raise NotImplementedError(f"sharding does not support {self._kind}")
+        if self._generic and offload:
+            raise NotImplementedError(f"sharding offload supports Adam/AdamW/Momentum/SGD, not {self._kind}")
         self._offload = bool(offload)
         self._mp_pg = None if mp_group is None or mp_group.nranks == 1 else mp_group.process_group
         self._norm_pgs = [g.process_group for g in norm_groups if g is not None and g.nranks > 1]
@@ -557,16 +579,97 @@ class ShardedOptimizer:
             master = shard.detach().float().clone().to(sdev) \
                 if (shard.dtype != torch.float32 or self._offload) else None
             self._masters.append(master)
-            self._m.append(torch.zeros(g.shard_numel, dtype=torch.float32, device=sdev))
+            self._m.append(torch.zeros(g.shard_numel, dtype=torch.float32, device=sdev)
+                           if not self._generic else None)
             self._v.append(torch.zeros(g.shard_numel, dtype=torch.float32, device=sdev)
                            if self._kind in ('Adam', 'AdamW') else None)
             for (p, lo, hi, plo) in g.params_in_shard():
                 self._pieces.append((gi, p, lo, hi, plo))
+        self._gen_acc = {}
+        self._shadows = []
+        if self._generic:
+            init = {'moment': getattr(optimizer, '_init_acc', 0.0)} if self._kind == 'Adagrad' else {}
+            for name in type(optimizer)._acc_names:
+                if name == 'mean_grad' and not getattr(optimizer, '_centered', False):
+                    continue
+                self._gen_acc[name] = [torch.full((g.shard_numel,), float(init.get(name, 0.0)),
+                                                  dtype=torch.float32, device=g.device)
+                                       for g in state.groups]
+            for i, (gi, p, lo, hi, plo) in enumerate(self._pieces):
+                sh = _ShardPiece(f'{p.name}@{gi}.{lo}', self._target(gi, lo, hi), p)
+                for name, bufs in self._gen_acc.items():
+                    optimizer._accumulators.setdefault(name, {})[sh.name] = bufs[gi][lo:hi]
+                self._shadows.append(sh)
         self._plan = None
         self._step = 0
         state.on_params_loaded.append(self._refresh_masters)
         self._overlap = _StepOverlap.maybe(self)
         state.step_overlap = self._overlap
+
+    def _target(self, gi, lo, hi):
+        """The fp32 tensor the update writes for a piece: its master slice, else its shard."""
+        m = self._masters[gi] if gi < len(self._masters) else None
+        return m[lo:hi] if m is not None else self.state.groups[gi].param_shard[lo:hi]
+
+    def _step_generic(self, lr, coef):
+        """Per-piece update of any element-wise inner optimizer (its own ``_update``) on this
+        rank's owned shard pieces; Lamb with whole-parameter trust ratios."""
+        st, o = self.state, self._inner
+        c = None if coef is None else coef.to(torch.float32)
+        lamb = self._kind == 'Lamb'
+        upds, wsq, usq = [], {}, {}
+        for (gi, p, lo, hi, plo), sh in zip(self._pieces, self._shadows):
+            grad = st.shard_grads[gi][lo:hi].float()
+            if c is not None:
+                grad = grad * c
+            w = self._target(gi, lo, hi)
+            lrp = lr * p.optimize_attr.get('learning_rate', 1.0)
+            if lamb:
+                m = o._accumulators['moment1'][sh.name]
+                v = o._accumulators['moment2'][sh.name]
+                m.mul_(o._beta1).add_((1 - o._beta1) * grad)
+                v.mul_(o._beta2).add_((1 - o._beta2) * grad * grad)
+                mh = m / (1 - o._beta1 ** self._step)
+                vh = v / (1 - o._beta2 ** self._step)
+                wd = 0.0 if (o._exclude is not None and o._exclude(p)) else o._wd
+                r = mh / (vh.sqrt() + o._epsilon) + wd * w.float()
+                key = id(p)
+                wsq[key] = wsq.get(key, 0.0) + (w.float() * w.float()).sum()
+                usq[key] = usq.get(key, 0.0) + (r * r).sum()
+                upds.append((w, r, lrp, key))
+            else:
+                wd = self._wd(p)
+                if wd:
+                    grad = grad + wd * w.float()
+                w.add_(o._update(sh, grad, w.float(), lrp).to(w.dtype))
+        if lamb:
+            # the pieces of one parameter may sit on several ranks: whole-parameter norms from
+            # one all-reduce of [n_params, 2] partial sums (same parameter order on every rank)
+            allp = [id(q) for g in st.groups for q in g.params]
+            pos = {k: i for i, k in enumerate(allp)}
+            dev = st.groups[0].device
+            sums = torch.zeros(len(allp), 2, dtype=torch.float32, device=dev)
+            for k in wsq:
+                sums[pos[k], 0] += wsq[k]
+                sums[pos[k], 1] += usq[k]
+            if st.world > 1:
+                dist.all_reduce(sums, group=st.pg)
+            norms = {k: sums[pos[k]].sqrt() for k in wsq}
+            for w, r, lrp, key in upds:
+                wn, rn = norms[key][0], norms[key][1]
+                trust = torch.where((wn > 0) & (rn > 0), wn / rn, torch.ones_like(wn))
+                w.add_((-lrp * trust * r).to(w.dtype))
+        with torch.no_grad():
+            for gi, g in enumerate(st.groups):
+                if self._masters[gi] is not None:
+                    g.param_shard.copy_(self._masters[gi].to(g.param_shard.device, g.param_shard.dtype))
+
+    def _acc_bufs(self, gi):
+        """[(checkpoint accumulator name, flat shard buffer)] of group gi."""
+        if self._generic:
+            return [(n, bufs[gi]) for n, bufs in self._gen_acc.items()]
+        k1, k2 = self._acc_keys()
+        return [(k, b) for k, b in ((k1, self._m[gi]), (k2, self._v[gi])) if k is not None and b is not None]
 
     def _refresh_masters(self):
         with torch.no_grad():
@@ -676,6 +779,12 @@ class ShardedOptimizer:
         lr = o.get_lr()
         dev = st.groups[0].device if st.groups else None
         coupled = self._kind == 'Adam' and o._weight_decay
+        if self._generic:
+            if ov is not None:
+                ov.sync()
+            self._step_generic(lr, coef)
+            st.after_step()
+            return
         if ov is not None:
             scale_t = None if coef is None else coef.to(torch.float32).reshape(()).contiguous()
             ov.run(self, lr, scale_t, lambda plan: self._launch(plan, lr, scale_t))
@@ -838,17 +947,20 @@ class ShardedOptimizer:
         sd = {}
         if not full:
             for gi in range(len(st.groups)):
-                sd[f'shard{gi}_moment1'] = Tensor(self._m[gi])
+                if self._generic:
+                    for key, buf in self._acc_bufs(gi):
+                        sd[f'shard{gi}_{key}'] = Tensor(buf)
+                else:
+                    sd[f'shard{gi}_moment1'] = Tensor(self._m[gi])
                 if self._v[gi] is not None:
                     sd[f'shard{gi}_moment2'] = Tensor(self._v[gi])
                 if self._masters[gi] is not None:
                     sd[f'shard{gi}_master'] = Tensor(self._masters[gi])
             sd['@rank'], sd['@world'] = st.rank, st.world
         else:
-            k1, k2 = self._acc_keys()
             masters = {}
             for gi, g in enumerate(st.groups):
-                bufs = [(k1, self._m[gi]), (k2, self._v[gi]), ('master', self._masters[gi])]
+                bufs = self._acc_bufs(gi) + [('master', self._masters[gi])]
                 for key, buf in bufs:
                     if key is None or buf is None:
                         continue
@@ -879,15 +991,15 @@ class ShardedOptimizer:
         st = self.state
         if self._overlap is not None:
             self._overlap.sync()
-        k1, k2 = self._acc_keys()
-        per_param = any(isinstance(k, str) and k.endswith(f'_{k1}_0') for k in sd)
+        knames = [k for k, _ in self._acc_bufs(0)] if st.groups else []
+        per_param = any(isinstance(k, str) and any(k.endswith(f'_{n}_0') for n in knames) for k in sd)
         masters_sd = sd.get('master_weights', {})
         with torch.no_grad():
             for gi, g in enumerate(st.groups):
                 if per_param:
                     # slice this rank's owned pieces out of the full per-parameter tensors
                     for p, lo, hi, plo in g.params_in_shard():
-                        for key, buf in ((k1, self._m[gi]), (k2, self._v[gi])):
+                        for key, buf in self._acc_bufs(gi):
                             name = f'{p.name}_{key}_0'
                             if key is None or buf is None or name not in sd:
                                 continue
@@ -898,9 +1010,9 @@ class ShardedOptimizer:
                             self._masters[gi][lo:hi].copy_(src.to(self._masters[gi].device,
                                                                   torch.float32))
                 else:
-                    for key, buf in ((f'shard{gi}_moment1', self._m[gi]),
-                                     (f'shard{gi}_moment2', self._v[gi]),
-                                     (f'shard{gi}_master', self._masters[gi])):
+                    shard_bufs = [(f'shard{gi}_{k}', b) for k, b in self._acc_bufs(gi)] if self._generic else \
+                        [(f'shard{gi}_moment1', self._m[gi]), (f'shard{gi}_moment2', self._v[gi])]
+                    for key, buf in shard_bufs + [(f'shard{gi}_master', self._masters[gi])]:
                         if key in sd and buf is not None:
                             buf.copy_(_u(sd[key]).to(buf.device))
         step = sd.get('@step')

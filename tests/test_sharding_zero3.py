@@ -240,3 +240,75 @@ def test_amp_custom_lists_cpu():
     with pytest.raises(ValueError):
         with paddle.amp.auto_cast(custom_white_list={'a'}, custom_black_list={'a'}):
             pass
+
+
+# -- sharding over any inner optimizer (dygraph_sharding_optimizer.py:29-212) -------------------
+_GENERIC = {
+    'Lamb': lambda paddle, ps: paddle.optimizer.Lamb(0.01, lamb_weight_decay=0.01, parameters=ps,
+                                                    grad_clip=paddle.nn.ClipGradByGlobalNorm(0.5)),
+    'Adagrad': lambda paddle, ps: paddle.optimizer.Adagrad(0.05, parameters=ps, initial_accumulator_value=0.1),
+    'RMSProp': lambda paddle, ps: paddle.optimizer.RMSProp(0.01, momentum=0.5, centered=True, parameters=ps),
+    'Adamax': lambda paddle, ps: paddle.optimizer.Adamax(0.01, parameters=ps, weight_decay=0.01),
+    'Adadelta': lambda paddle, ps: paddle.optimizer.Adadelta(0.5, parameters=ps),
+}
+
+
+def _generic_single(name, steps=3):
+    import paddle_ray_amd as paddle
+    import paddle_ray_amd.nn.functional as F
+    m = _deep_mlp()
+    o = _GENERIC[name](paddle, m.parameters())
+    xs, ys = _data()
+    for _ in range(steps):
+        loss = F.mse_loss(m(paddle.to_tensor(xs)), paddle.to_tensor(ys))
+        loss.backward()
+        o.step()
+        o.clear_grad()
+    return [p.numpy() for p in m.parameters()], _by_index(m, o.state_dict())
+
+
+def _by_index(m, sd):
+    """optimizer state keyed by (parameter position, accumulator) (names differ per process)"""
+    names = {p.name: i for i, p in enumerate(m.parameters())}
+    out = {}
+    for k, v in sd.items():
+        if not hasattr(v, 'numpy'):
+            continue
+        for n, i in names.items():
+            if k.startswith(n + '_'):
+                out[f'{i}:{k[len(n) + 1:]}'] = v.numpy()
+    return out
+
+
+def _generic_worker(rank, world, name, level, steps=3):
+    import paddle_ray_amd as paddle
+    import paddle_ray_amd.nn.functional as F
+    from paddle_ray_amd.distributed.sharding import group_sharded_parallel
+    m = _deep_mlp()
+    o = _GENERIC[name](paddle, m.parameters())
+    sm, so, _ = group_sharded_parallel(m, o, level, segment_size=0, bucket_mb=1)
+    xs, ys = _data()
+    for _ in range(steps):
+        # the full batch on every rank: the sharded gradient average equals the single-process one
+        loss = F.mse_loss(sm(paddle.to_tensor(xs)), paddle.to_tensor(ys))
+        loss.backward()
+        so.step()
+        so.clear_grad()
+    sd = sm.state_dict()
+    osd = so.state_dict()
+    return {'params': [sd[k].numpy() for k in sd],
+            'opt': _by_index(m, osd)}
+
+
+@pytest.mark.parametrize('name', sorted(_GENERIC))
+@pytest.mark.parametrize('level', ['os_g', 'p_g_os'])
+def test_sharding_wraps_any_inner_optimizer(tmp_path, name, level):
+    ref, ref_opt = _generic_single(name)
+    res = run_ranks(_generic_worker, 2, tmp_path, (name, level))
+    for r in res:
+        for a, b in zip(r['params'], ref):
+            np.testing.assert_allclose(a, b, rtol=2e-5, atol=2e-6)
+        # the gathered optimizer state uses the plain optimizer's per-parameter keys and values
+        assert set(ref_opt) <= set(r['opt']), sorted(set(ref_opt) - set(r['opt']))
+        for k, v in ref_opt.items():
+            np.testing.assert_allclose(r['opt'][k], v, rtol=2e-5, atol=2e-6)
