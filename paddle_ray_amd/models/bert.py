@@ -21,6 +21,18 @@ from .. import nn
 from ..nn import functional as F
 from ..nn import initializer as I
 from ..ops import fused as K
+from ..static import fn_ops as FO
+from ..static.graph import Variable as _Var, static_op as _static_op
+
+
+def _pad_mask(ids, pad_token_id, dtype):
+    """[B, S] token ids -> [B, 1, 1, S] additive key-padding mask (-1e4 at padding)."""
+    return Tensor(((_u(ids) == pad_token_id).to(dtype) * -1e4)[:, None, None, :])
+
+
+# one static op (no gradient) when the ids are a Program Variable: the mask is always built
+# there, since a recorded program cannot test the fed values for padding
+_pad_mask_op = _static_op('bert_pad_mask', _pad_mask)
 
 
 @dataclass
@@ -193,18 +205,22 @@ class BertLayer(nn.Layer):
     def forward(self, x, attn_mask=None):
         p = self.p if self.training else 0.0
         if self.fused:
-            t = _u(x)
-            a = K.linear(self.attn.context(x, attn_mask), self.attn.out_proj.weight._t)
-            _, y1 = K.add_dropout_layer_norm(t, a, self.attn.out_proj.bias._t,
-                                             self.ln1.weight._t, self.ln1.bias._t, p, self.eps)
+            # fused ops (static/fn_ops.py): the same HIP kernels eagerly, and ONE static op each
+            # with a direct grad kernel inside a Program
+            at = self.attn
+            qkv = FO.fused_linear(x, at.qkv_proj.weight, at.qkv_proj.bias)
+            c = FO.fused_flash_qkv(qkv, attn_mask, at.num_heads, at.attn_dropout if self.training else 0.0)
+            a = FO.fused_linear(c, at.out_proj.weight)
+            _, y1 = FO.fused_add_dropout_ln(x, a, at.out_proj.bias, self.ln1.weight, self.ln1.bias,
+                                            p, self.eps)
             if self.act == 'gelu':
                 # fc1 GEMM with the bias+GELU epilogue, fc2 GEMM (its bias goes to the ADL kernel)
-                m = K.mlp_gelu(y1, self.fc1.weight._t, self.fc1.bias._t, self.fc2.weight._t, False)
+                m = FO.fused_mlp_gelu(y1, self.fc1.weight, self.fc1.bias, self.fc2.weight, False)
             else:
-                m = K.linear(self._ffn_hidden(Tensor(y1)), self.fc2.weight._t)
-            _, y2 = K.add_dropout_layer_norm(y1, m, self.fc2.bias._t, self.ln2.weight._t,
-                                             self.ln2.bias._t, p, self.eps)
-            return Tensor(y2)
+                m = FO.fused_linear(getattr(F, self.act)(self.fc1(y1)), self.fc2.weight)
+            _, y2 = FO.fused_add_dropout_ln(y1, m, self.fc2.bias, self.ln2.weight, self.ln2.bias,
+                                            p, self.eps)
+            return y2
         drop = (lambda t: torch.nn.functional.dropout(t, p, True)) if p > 0 else (lambda t: t)
         y1 = _u(self.ln1(Tensor(_u(x) + drop(_u(self.attn(x, attn_mask))))))
         m = _u(self.fc2(Tensor(self._ffn_hidden(Tensor(y1)))))
@@ -236,6 +252,8 @@ class BertModel(nn.Layer):
         return self.embeddings.word_embeddings
 
     def _mask(self, input_ids, attention_mask, dtype):
+        if attention_mask is None and isinstance(input_ids, _Var):
+            return _pad_mask_op(input_ids, self.pad_token_id, dtype)
         if attention_mask is None:
             ids = _u(input_ids)
             pad = ids == self.pad_token_id
@@ -251,7 +269,7 @@ class BertModel(nn.Layer):
     def forward(self, input_ids, token_type_ids=None, position_ids=None, attention_mask=None,
                 task_type_ids=None, output_hidden_states=False):
         x = self.embeddings(input_ids, token_type_ids, position_ids, task_type_ids)
-        mask = self._mask(input_ids, attention_mask, _u(x).dtype)
+        mask = self._mask(input_ids, attention_mask, x.dtype if isinstance(x, _Var) else _u(x).dtype)
         hs = []
         for layer in self.encoder:
             if self.cfg.recompute and self.training:
@@ -276,17 +294,20 @@ class BertLMPredictionHead(nn.Layer):
         self.decoder_bias = self.create_parameter([cfg.vocab_size], is_bias=True)
 
     def forward(self, hidden_states, masked_positions=None):
-        h = _u(hidden_states)
+        from .. import tensor as T
+        h = hidden_states
         if masked_positions is not None:
-            h = h.reshape(-1, h.shape[-1]).index_select(0, _u(masked_positions).reshape(-1))
+            h = T.manipulation.index_select(T.manipulation.reshape(h, [-1, h.shape[-1]]),
+                                            T.manipulation.reshape(masked_positions, [-1]), 0)
         if self.act == 'gelu':
-            h = K.bias_gelu(torch.matmul(h, self.transform.weight._t), self.transform.bias._t,
-                            False)
+            # transform GEMM with the bias+GELU epilogue (exact erf GELU)
+            h = FO.fused_bias_gelu(FO.fused_linear(h, self.transform.weight), self.transform.bias, False)
         else:
-            h = _u(getattr(F, self.act)(self.transform(Tensor(h))))
-        h = _u(self.layer_norm(Tensor(h)))
-        return Tensor(torch.addmm(self.decoder_bias._t, h.reshape(-1, h.shape[-1]),
-                                  self.decoder_weight._t.t()).reshape(*h.shape[:-1], -1))
+            h = getattr(F, self.act)(self.transform(h))
+        h = self.layer_norm(h)
+        h2 = T.manipulation.reshape(h, [-1, h.shape[-1]])
+        # decoder: logits = h·Eᵀ + b on the NT GEMM (the tied [vocab, hidden] word embedding)
+        return T.math.add(FO.fused_linear_nt(h2, self.decoder_weight), self.decoder_bias)
 
 
 class BertPretrainingHeads(nn.Layer):
@@ -317,15 +338,16 @@ class BertForPretraining(nn.Layer):
         scores, nsp = self.cls(seq, pooled, masked_positions)
         if labels is None:
             return scores, nsp
-        s = _u(scores)
-        lab = _u(labels).reshape(-1)
-        mlm = K.softmax_cross_entropy(s.reshape(-1, s.shape[-1]), lab, -1)
-        valid = (lab != -1).sum().clamp(min=1)
-        loss = mlm.sum() / valid
+        from .. import tensor as T
+        lab = T.manipulation.reshape(labels, [-1])
+        mlm = FO.fused_softmax_ce(T.manipulation.reshape(scores, [-1, scores.shape[-1]]), lab, -1)
+        valid = T.math.clip(T.math.sum(T.manipulation.cast(T.math.not_equal(lab, -1), 'float32')),
+                            min=1.0)
+        loss = T.math.divide(T.math.sum(T.manipulation.cast(mlm, 'float32')), valid)
         if next_sentence_label is not None:
-            loss = loss + torch.nn.functional.cross_entropy(
-                _u(nsp).float(), _u(next_sentence_label).reshape(-1))
-        return Tensor(loss)
+            loss = T.math.add(loss, F.cross_entropy(T.manipulation.cast(nsp, 'float32'),
+                                                    T.manipulation.reshape(next_sentence_label, [-1])))
+        return loss
 
 
 class BertPretrainingCriterion(nn.Layer):

@@ -93,11 +93,17 @@ constexpr int BM = 256, BN = 256, BKT = 64;  // the GEMM tile (conv configs belo
 //   BUF: operand DMA as MUBUF buffer_load ... lds instead of global_load_lds
 //   PIPE: two barriers per K-step and the refill DMA issued in half 0 (see kstep_p): every DMA
 //       has at least two k-halves of lead instead of one
+//   TS: the two-barrier "read early, refill early, wait late" schedule (see kstep_t): each K-step's
+//       second-half fragments are read in the first MFMAs of its first half, so a barrier two
+//       thirds into that half frees the slot for the K-step+2 refill; the next K-step's first
+//       fragments are read only in the last MFMAs of the second half, after a counted vmcnt that
+//       leaves the refill in flight -> every DMA piece has ~1.5 K-steps of lead (the loop shape
+//       of the 256x256x64 MFMA16 kernels hipBLASLt ships for gfx950, measured 84 % MFMA-busy)
 template <int WR_, int WC_, int BM_ = 256, int BN_ = 256, bool ILV_ = false, bool BUF_ = false,
-          bool PIPE_ = false>
+          bool PIPE_ = false, bool TS_ = false>
 struct WCfg {
   static constexpr int WR = WR_, WC = WC_, NT = 64 * WR_ * WC_, BM = BM_, BN = BN_;
-  static constexpr bool ILV = ILV_, BUF = BUF_, PIPE = PIPE_;
+  static constexpr bool ILV = ILV_, BUF = BUF_, PIPE = PIPE_, TS = TS_;
   static constexpr int TI = BM_ / WR_ / 16, TJ = BN_ / WC_ / 16;  // 16x16 MFMA tiles per wave
   static constexpr int IMGA = BM_ * BKT * 2, IMGB = BN_ * BKT * 2, SLOT = IMGA + IMGB;
   static constexpr int NDA = IMGA / (NT * 16), NDB = IMGB / (NT * 16);  // glds per thread per K-step
@@ -570,7 +576,81 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_lds_kernel(const uint16_t* __r
     }
     if constexpr (!STEADY) __builtin_amdgcn_s_waitcnt(0xC07F);
   };
-  if constexpr (CF::PIPE) {
+  // TS schedule, K-step kt (slot kt&1), NM = TI*TJ MFMAs per k-half:
+  //   half 0: MFMAs of (kt,0) from F0; fillers f < NRD = the reads of (kt,1) into F1; at
+  //           f = BA: lgkmcnt(0) + barrier (every wave is done with slot kt); then the A pieces
+  //           of step kt+2 into slot kt, spread over the rest of the half;
+  //   half 1: MFMAs of (kt,1) from F1; the B pieces of step kt+2 spread over f < BB; at f = BB:
+  //           vmcnt(NDA+NDB) (step kt+1 landed, kt+2 still in flight) + barrier; then the reads
+  //           of (kt+1,0) into F0 in the last NRD MFMAs.
+  auto kstep_t = [&](int kt, auto steady_c) __attribute__((always_inline)) {
+    constexpr bool STEADY = decltype(steady_c)::value;
+    constexpr int NRD = TI + TJ, NDMA = NDA + NDB, NM = TI * TJ;
+    constexpr int BA = (2 * NM) / 3;                 // 42 of 64 (W4), 21 of 32 (W8)
+    constexpr int BB = NM - NRD - 2;                 // 46 of 64 (W4), 18 of 32 (W8)
+    constexpr int SPA = (NM - 1 - BA) / NDA > 0 ? (NM - 1 - BA) / NDA : 1;
+    constexpr int SPB = BB / NDB > 0 ? BB / NDB : 1;
+    static_assert(NRD < BA && BA < NM - 1 && NRD + 1 < NM - BB, "TS: fillers exceed the half's MFMAs");
+    const bool dma = STEADY || (kt + 2 < nk && dmaon);
+    const bool rd1 = STEADY || kt + 1 < nk;
+    const uint32_t soA = lds_base + (kt & 1) * SLOT, soB = soA + IMGA;
+    {
+      const char* ai = lds + (kt & 1) * SLOT;
+      const char* bi = ai + IMGA;
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) {
+          if constexpr (AGPR_ACC) mma_agpr<T>(fb0[j], fa0[i], acc[i][j]);
+          else acc[i][j] = mma<T>(fb0[j], fa0[i], acc[i][j]);
+          __builtin_amdgcn_sched_barrier(0);
+          const int f = i * TJ + j;
+          if (f < TJ) {
+            fb1[f] = frag<T, BK>(bi, wc * CW + f * 16, 1, lane);
+          } else if (f < NRD) {
+            fa1[f - TJ] = frag<T, AK, (AK ? 256 : BM)>(ai, wr * RW + (f - TJ) * 16, 1, lane);
+          } else if (f == BA) {
+            __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's reads of slot kt done
+            __builtin_amdgcn_s_barrier();        // every wave's
+          } else if (dma && f > BA && (f - BA - 1) % SPA == 0 && (f - BA - 1) / SPA < NDA) {
+            da.issue1(soA, wave, kt + 2, (f - BA - 1) / SPA);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    {
+      const char* ai = lds + ((kt + 1) & 1) * SLOT;
+      const char* bi = ai + IMGA;
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) {
+          if constexpr (AGPR_ACC) mma_agpr<T>(fb1[j], fa1[i], acc[i][j]);
+          else acc[i][j] = mma<T>(fb1[j], fa1[i], acc[i][j]);
+          __builtin_amdgcn_sched_barrier(0);
+          const int f = i * TJ + j;
+          if (f < BB) {
+            if (dma && f % SPB == 0 && f / SPB < NDB) db.issue1(soB, wave, kt + 2, f / SPB);
+          } else if (f == BB) {
+            if (dma) wait_vmcnt<NDMA>();  // step kt+1's pieces landed (kt+2's in flight)
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();  // ... for every wave
+          } else if (rd1 && f - BB - 1 < NRD) {
+            const int r = f - BB - 1;
+            if (r < TJ) fb0[r] = frag<T, BK>(bi, wc * CW + r * 16, 0, lane);
+            else fa0[r - TJ] = frag<T, AK, (AK ? 256 : BM)>(ai, wr * RW + (r - TJ) * 16, 0, lane);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    if constexpr (!STEADY) __builtin_amdgcn_s_waitcnt(0xC07F);
+  };
+  if constexpr (CF::TS) {
+    int kt = 0;
+    if (dmaon)
+      for (; kt + 2 < nk; ++kt) kstep_t(kt, std::true_type{});
+    for (; kt < nk; ++kt) kstep_t(kt, std::false_type{});
+  } else if constexpr (CF::PIPE) {
     int kt = 0;
     if (dmaon)
       for (; kt + 2 < nk; ++kt) kstep_p(kt, std::true_type{});

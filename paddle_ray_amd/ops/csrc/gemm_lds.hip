@@ -81,7 +81,7 @@ void launch_e(const void* A, const void* B, const void* bias, void* C, void* Z, 
   constexpr int layout = AK ? (BK ? 1 : 0) : 2;
   int alt = -1;
   if (std::is_same<T, bf16>::value && E != kRelu)
-    for (int c = 0; c < 6 && alt < 0; ++c)
+    for (int c = 0; c < 8 && alt < 0; ++c)
       if (w4_mask() >> (4 * c + layout) & 1) alt = c;
   // TN GEMMs with <= 128 rows (one tile row either way, so split-K factors and workspaces match)
   const bool narrow = !AK && !BK && E == kNone && M <= 128 && alt < 0 && narrow_tn();

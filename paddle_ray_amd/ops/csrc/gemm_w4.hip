@@ -52,6 +52,8 @@ using W4B = WCfg<2, 2, 256, 256, true, true>;   // W4 with MUBUF operand DMA
 using W8B = WCfg<2, 4, 256, 256, false, true>;  // W8 (burst schedule) with MUBUF operand DMA
 using W4P = WCfg<2, 2, 256, 256, true, false, true>;  // W4 with the two-barrier early-refill schedule
 using W8P = WCfg<2, 4, 256, 256, true, false, true>;  // W8 with the two-barrier early-refill schedule
+using W4T = WCfg<2, 2, 256, 256, true, false, false, true>;  // W4 with the TS schedule (kstep_t)
+using W8T = WCfg<2, 4, 256, 256, true, false, false, true>;  // W8 with the TS schedule
 
 template <typename CF>
 int launch_alt(int layout, const void* A, const void* B, const void* bias, void* C, void* Z, float* colsum, int M,
@@ -85,7 +87,7 @@ extern "C" int pra_gemm_w8i(int layout, const void* A, const void* B, const void
                                    splits, ws, s);
 }
 
-// cfg: 0 = W4, 1 = W8I, 2 = W4B, 3 = W8B, 4 = W4P, 5 = W8P
+// cfg: 0 = W4, 1 = W8I, 2 = W4B, 3 = W8B, 4 = W4P, 5 = W8P, 6 = W4T, 7 = W8T
 extern "C" int pra_gemm_alt(int cfg, int layout, const void* A, const void* B, const void* bias, void* C, void* Z,
                             float* colsum, int M, int N, int K, int lda, int ldb, int ldc, int ldz, int dtype, int epi,
                             int beta, int splits, float* ws, hipStream_t s) {
@@ -96,6 +98,8 @@ extern "C" int pra_gemm_alt(int cfg, int layout, const void* A, const void* B, c
     case 3: return pra::launch_alt<pra::W8B>(layout, A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, dtype, epi, beta, splits, ws, s);
     case 4: return pra::launch_alt<pra::W4P>(layout, A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, dtype, epi, beta, splits, ws, s);
     case 5: return pra::launch_alt<pra::W8P>(layout, A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, dtype, epi, beta, splits, ws, s);
+    case 6: return pra::launch_alt<pra::W4T>(layout, A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, dtype, epi, beta, splits, ws, s);
+    case 7: return pra::launch_alt<pra::W8T>(layout, A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, dtype, epi, beta, splits, ws, s);
     default: return -1;
   }
 }

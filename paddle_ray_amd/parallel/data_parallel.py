@@ -8,9 +8,29 @@ MI355X design: gradients live in per-bucket flat buffers (``FlatGroup``), so a
 bucket is all-reduced IN PLACE by one RCCL call the moment its last gradient is
 accumulated (post-accumulate-grad hook) — RCCL runs on its own stream while the
 backward keeps computing; one end-of-backward callback makes the compute stream
-wait on the outstanding collectives (no host sync). Default bucket 64 MB: large
-enough to run xGMI rings near link bandwidth, small enough that the first
-bucket launches early in the backward.
+wait on the outstanding collectives (no host sync).
+
+Bucket size (default 64 MB; the reference's EagerReducer uses 25 MB, written for NVLink
+switches). The basis on an 8 x MI355X node, where every GPU reaches the other seven through
+its own point-to-point xGMI link (7 x ~64 GB/s per direction) and RCCL runs one ring per
+channel over those links, is a latency / bandwidth split of one ring all-reduce:
+
+    t(B) = a + 2 (n-1)/n * B / BW_bus,   a ~= 25-40 us launch + ring pipeline fill,
+                                          BW_bus ~= 250-350 GB/s (all 7 links busy)
+
+* fixed-cost share a / t(B) at n = 8: 25 MB -> ~15-25 %, 64 MB -> ~7-11 %, 256 MB -> ~2-3 %:
+  below ~32 MB the per-call cost is a visible fraction of the link time;
+* the LAST bucket of the backward cannot overlap compute: its t(B) is exposed once per step
+  (64 MB: ~0.35-0.45 ms; 256 MB: ~1.4-1.8 ms), and the FIRST bucket should launch early;
+  a GPT-1.3B block's gradients are 100 MB bf16 (~4 ms of backward compute), so a 64 MB
+  bucket launches within the first block's backward and every later bucket hides under the
+  following blocks' compute (about 0.4 ms of link time per ~2.5 ms of compute).
+64 MB keeps the per-call share under ~10 % and the exposed tail under half a millisecond.
+ZeRO-2/3 reduce-scatters use one bucket per unit (a repeated block, 100 MB here) and 128 MB
+for the resident remainder (``group_sharded_parallel(bucket_mb=128)``): a reduce-scatter
+moves (n-1)/n * B per rank -- half the all-reduce bytes -- so the same call-overhead share
+needs twice the bucket. These are derived numbers (no 8-GPU node in this build's test pool);
+``fuse_grad_size_in_MB`` / ``bucket_mb`` override them.
 """
 import contextlib
 

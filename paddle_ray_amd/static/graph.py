@@ -27,6 +27,7 @@ Serialized programs (``.pdmodel``, a framework.proto ProgramDesc written by
 static/program_desc.py) name ops only by their registered op type; loading resolves names through the static op table and refuses anything else.
 """
 import collections
+import inspect
 import contextlib
 import itertools
 import weakref
@@ -518,6 +519,69 @@ def _vjp(ctx, *out_grads):
     return [Tensor(g if g is not None else torch.zeros_like(t)) for g, t in zip(gs, targets)]
 
 
+# Direct grad kernels (parity: python/paddle/fluid/backward.py:1276 `_append_backward_ops_`,
+# which emits each forward op's REGISTERED grad op running its phi grad kernel). An op type in
+# _FN_OPS is backed by a torch.autograd.Function whose forward / backward ARE the op's forward
+# and grad kernels: in a program with a backward the executor runs Function.forward on a plain
+# context object (no autograd graph kept alive) and the `<type>_grad` op calls
+# Function.backward on that context directly (no torch.autograd re-entry). A per-type
+# predicate picks this path at run time; when it declines (e.g. an AMP cast the fused kernel
+# does not take) the op runs the generic autograd path and its grad op falls back to _vjp.
+_FN_OPS = {}   # op type -> (autograd.Function class, predicate(torch args) -> bool)
+
+
+def register_fn_op(op_type, fn_cls, pred=None):
+    _FN_OPS[op_type] = (fn_cls, pred)
+
+
+class _FnCtx:
+    """Stand-in for torch's FunctionCtx: what a Function's forward saves, its backward reads."""
+
+    def __init__(self, fn_cls, needs, slots, order):
+        self.fn_cls, self.needs_input_grad = fn_cls, needs
+        self.slots, self.order = slots, order   # positional-arg -> grad-output mapping
+        self.saved_tensors = ()
+        self.materialize = True
+        self.out_meta = []
+
+    def save_for_backward(self, *ts):
+        self.saved_tensors = ts
+
+    def set_materialize_grads(self, v):
+        self.materialize = bool(v)
+
+    def mark_non_differentiable(self, *a):
+        pass
+
+    def mark_dirty(self, *a):
+        pass
+
+
+def _fn_grad(ctx, *out_grads):
+    """`<type>_grad` of a direct-grad op: Function.backward on the saved context; generic
+    autograd replay when the forward took the fallback path."""
+    if isinstance(ctx, _Ctx):
+        return _vjp(ctx, *out_grads)
+    gs = []
+    for g, (shp, dt, dev) in zip(out_grads, ctx.out_meta):
+        if g is None:
+            gs.append(torch.zeros(shp, dtype=dt, device=dev) if ctx.materialize else None)
+        else:
+            t = _u(g) if isinstance(g, Tensor) else g
+            gs.append(t.to(dt) if t.dtype != dt else t)
+    with torch.no_grad():
+        res = ctx.fn_cls.backward(ctx, *gs)
+    if not isinstance(res, tuple):
+        res = (res,)
+    out = []
+    for key in ctx.order:
+        i = ctx.slots.index(key)
+        g = res[i] if i < len(res) else None
+        out.append(Tensor(g) if g is not None else None)
+    ctx.saved_tensors = ()
+    return out
+
+
 def _sum_grads(*gs):
     t = _u(gs[0])
     for g in gs[1:]:
@@ -621,7 +685,7 @@ def _build_backward(prog, targets, inputs=(), target_grads=None, no_grad_set=Non
         for p in dps:
             outs.append(_new_var(blk, list(_u(p).shape), _u(p).dtype).vid)
         args = [_VarRef(op.ctx_vid)] + [None if g is None else _VarRef(g) for g in ogs]
-        gop = OpDesc(op.type + '_grad', _vjp, args, {},
+        gop = OpDesc(op.type + '_grad', _fn_grad if op.type in _FN_OPS else _vjp, args, {},
                      [op.ctx_vid] + [g for g in ogs if g is not None], outs,
                      ('list', ['T'] * len(outs)), role='backward')
         gop.attrs['fwd'] = op
@@ -894,6 +958,11 @@ class Executor:
             amp_ctx = auto_cast(True, amp_cfg['white'], amp_cfg['black'], amp_cfg['level'],
                                 amp_cfg['dtype'])
         with amp_ctx:
+            if op.role == 'forward' and op.ctx_vid is not None and ctx_needed and \
+                    op.type in _FN_OPS and not op.kwargs:
+                r = self._run_fn_op(op, env)
+                if r is not None:
+                    return r
             if op.role == 'forward' and op.ctx_vid is not None and ctx_needed:
                 # run on leaf copies of the differentiable inputs and keep this op's own graph
                 diff_in = op.attrs.get('diff_in', [])
@@ -917,6 +986,42 @@ class Executor:
                 return op.fn(*_materialize(op.args, env), **_materialize(op.kwargs, env))
             with torch.no_grad():
                 return op.fn(*_materialize(op.args, env), **_materialize(op.kwargs, env))
+
+    def _run_fn_op(self, op, env):
+        """Forward of a direct-grad op: Function.forward on a _FnCtx (None: predicate declined)."""
+        fn_cls, pred = _FN_OPS[op.type]
+        vals = _materialize(op.args, env)
+        targs = [_u(a) if isinstance(a, Tensor) else a for a in vals]
+        nfwd = fn_cls.__dict__.get('_pra_nargs')
+        if nfwd is None:
+            nfwd = len(inspect.signature(fn_cls.forward).parameters) - 1
+            setattr(fn_cls, '_pra_nargs', nfwd)
+        targs += [None] * (nfwd - len(targs))  # trailing optional args left at None (e.g. bias)
+        if pred is not None and not pred(*targs):
+            return None
+        diff_in = op.attrs.get('diff_in', [])
+        dps = op.attrs.get('diff_params', [])
+        slots, needs = [], []
+        for a in op.args:
+            if isinstance(a, _VarRef):
+                key = ('v', a.vid)
+                slots.append(key)
+                needs.append(a.vid in diff_in)
+            elif isinstance(a, Tensor) and any(a is p for p in dps):
+                key = ('p', id(a))
+                slots.append(key)
+                needs.append(True)
+            else:
+                slots.append(None)
+                needs.append(False)
+        order = [('v', v) for v in diff_in] + [('p', id(p)) for p in dps]
+        ctx = _FnCtx(fn_cls, tuple(needs), slots, order)
+        with torch.no_grad():
+            out = fn_cls.forward(ctx, *targs)
+        outs = out if isinstance(out, tuple) else (out,)
+        ctx.out_meta = [(o.shape, o.dtype, o.device) for o in outs]
+        env[op.ctx_vid] = ctx
+        return tuple(Tensor(o) for o in outs) if isinstance(out, tuple) else Tensor(out)
 
     def _execute(self, prog, names, vals, fetch_vars, skip_optimize=False):
         blk = prog.global_block()

@@ -90,7 +90,9 @@ def main_w4():
     schedule), W4 (4 waves x 128x128, one filler per MFMA), W8I (8 waves, one filler per MFMA)."""
     dev = torch.device('cuda')
     cfgs = [('W8', 0), ('W4', 7), ('W8I', 7 << 4), ('W4B', 7 << 8), ('W8B', 7 << 12), ('W4P', 7 << 16),
-            ('W8P', 7 << 20)]
+            ('W8P', 7 << 20), ('W4T', 7 << 24), ('W8T', 7 << 28)]
+    if '--ts' in sys.argv:  # the TS schedule against the default configurations only
+        cfgs = [('W8', 0), ('W4', 7), ('W4T', 7 << 24), ('W8T', 7 << 28)]
     hdr = ' | '.join(f'err {n}' for n, _ in cfgs) + ' | ' + ' | '.join(f'{n} us' for n, _ in cfgs)
     print(f"| GEMM | layout | M | N | K | {hdr} | hipBLASLt us | best | best PF/s | best vs hipBLASLt |")
     print("|---|---|---|---|---|" + "---|" * (2 * len(cfgs) + 4), flush=True)

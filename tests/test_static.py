@@ -190,3 +190,56 @@ def test_executor_hip_graph_replay():
         assert len(main._graph_cache) == 1
     finally:
         paddle.disable_static()
+
+
+def test_static_bert_direct_grad_ops_match_eager():
+    """BERT pretraining recorded op by op: the fused linear / flash-attention / add+dropout+LN /
+    MLP / softmax-CE ops carry DIRECT grad ops (Function.backward on the saved context, no _vjp
+    autograd replay), and one SGD step through the Executor equals the eager step."""
+    import numpy as np
+    import collections
+    import paddle_ray_amd as paddle
+    from paddle_ray_amd import static
+    from paddle_ray_amd.models import bert_config, BertForPretraining
+    cfg = bert_config('bert-tiny', hidden_dropout_prob=0.0, attention_probs_dropout_prob=0.0)
+    bs, S, P = 2, 16, 3
+    rs = np.random.RandomState(0)
+    ids = rs.randint(5, cfg.vocab_size, (bs, S))
+    ids[1, 12:] = cfg.pad_token_id  # padded keys: the static program always builds the mask
+    pos = np.stack([np.sort(rs.choice(12, P, replace=False)) + i * S for i in range(bs)]).reshape(-1)
+    lab = ids.reshape(-1)[pos].copy()
+    nsp = rs.randint(0, 2, (bs,))
+
+    def build():
+        paddle.seed(1)
+        return BertForPretraining(cfg)
+    m_e = build()
+    opt_e = paddle.optimizer.SGD(0.1, parameters=m_e.parameters())
+    loss_e = m_e(paddle.to_tensor(ids), masked_positions=paddle.to_tensor(pos), labels=paddle.to_tensor(lab),
+                 next_sentence_label=paddle.to_tensor(nsp))
+    loss_e.backward()
+    opt_e.step()
+    m_s = build()
+    paddle.enable_static()
+    try:
+        main_p, startup = static.Program(), static.Program()
+        with static.program_guard(main_p, startup):
+            iv = static.data('ids', [bs, S], 'int64')
+            pv = static.data('pos', [bs * P], 'int64')
+            lv = static.data('lab', [bs * P], 'int64')
+            nv = static.data('nsp', [bs], 'int64')
+            loss_v = m_s(iv, masked_positions=pv, labels=lv, next_sentence_label=nv)
+            paddle.optimizer.SGD(0.1, parameters=m_s.parameters()).minimize(loss_v)
+        types = collections.Counter((op.role, op.type, op.fn.__name__) for op in main_p.global_block().ops)
+        for t in ('fused_linear', 'fused_flash_qkv', 'fused_add_dropout_ln', 'fused_mlp_gelu',
+                  'fused_softmax_ce', 'fused_linear_nt', 'fused_bias_gelu'):
+            assert types[('backward', t + '_grad', '_fn_grad')] >= 1, t
+            assert not any(k[1] == t + '_grad' and k[2] != '_fn_grad' for k in types), t
+        exe = static.Executor()
+        exe.run(startup)
+        out = exe.run(main_p, feed={'ids': ids, 'pos': pos, 'lab': lab, 'nsp': nsp}, fetch_list=[loss_v])
+    finally:
+        paddle.disable_static()
+    np.testing.assert_allclose(float(out[0]), float(loss_e), rtol=1e-5)
+    for (n, pe), ps in zip(m_e.named_parameters(), m_s.parameters()):
+        np.testing.assert_allclose(ps.numpy(), pe.numpy(), rtol=1e-4, atol=1e-6, err_msg=n)
