@@ -2,9 +2,9 @@
 
 Parity: the reference's FLAGS_allocator_strategy='auto_growth' allocator
 (paddle/fluid/memory/allocation/auto_growth_best_fit_allocator.cc) with stream-safe reuse
-(stream_safe_cuda_allocator.cc). Enable it for a process with ``PRA_ALLOCATOR=auto_growth``
-(read when paddle_ray_amd is imported, before the first device allocation) or by calling
-``enable()`` before any GPU tensor exists; it then backs every PyTorch-ROCm tensor through
+(stream_safe_cuda_allocator.cc). It is the default on a GPU host (installed when
+paddle_ray_amd is imported, before the first device allocation; ``PRA_ALLOCATOR=caching``
+opts out), or ``enable()`` before any GPU tensor exists; it then backs every PyTorch-ROCm tensor through
 ``torch.cuda.memory.CUDAPluggableAllocator``. ``PRA_ALLOC_CHUNK_MB`` sets the growth chunk
 (default 64 MB). HIP-graph capture: the allocator is installed through the C++ hooks
 (alloc/torch_hooks.cpp, ``_pra_alloc_torch``), which route every allocation made on a capturing
@@ -16,8 +16,7 @@ time complete (as PyTorch's caching allocator does; RCCL's stream use depends on
 Measured against PyTorch's caching allocator (profiles/r3h/ab_results.txt, profiles/r3j/):
 GPT-1.3B 124.2K vs 124.4K tokens/s, ResNet-50 8431 vs 8423 img/s, BERT-base (HIP-graph static
 executor) 1698.6 vs 1697.4 seq/s (an earlier 1473 vs 1592 gap is gone since the Executor hands
-captured gradients to the optimizer in place). Opt-in: the round-end multi-GPU runs have not
-exercised it yet.
+captured gradients to the optimizer in place).
 """
 import ctypes
 import os
@@ -105,5 +104,29 @@ def reset_peak(device=0, lib=None):
 
 
 def maybe_enable_from_env():
-    if os.environ.get('PRA_ALLOCATOR', '') in ('auto_growth', 'native'):
-        enable()
+    """The native allocator is the DEFAULT on a GPU host (reference default
+    FLAGS_allocator_strategy=auto_growth, paddle/phi/core/flags.cc:489). Opt out with
+    ``PRA_ALLOCATOR=caching`` (or ``FLAGS_allocator_strategy=naive_best_fit``): PyTorch's caching
+    allocator. No GPU, or the graph-pool hooks not built: the caching allocator, with a warning
+    in the latter case. Runs at import, before any device allocation (device_count() does not
+    initialise the GPU)."""
+    choice = os.environ.get('PRA_ALLOCATOR', '').strip().lower()
+    strat = os.environ.get('FLAGS_allocator_strategy', '').strip().lower()
+    if choice in ('caching', 'torch', 'off', '0') or (not choice and strat == 'naive_best_fit'):
+        return False
+    if os.environ.get('PRA_FORCE_CPU') == '1':
+        return False
+    try:
+        import torch
+        if torch.cuda.device_count() == 0:
+            return False
+    except Exception:
+        return False
+    if choice in ('auto_growth', 'native'):
+        return enable()   # explicitly requested: fail loudly
+    if hooks() is None or not os.path.exists(library_path()):
+        import warnings
+        warnings.warn('native allocator not built (python -m paddle_ray_amd.native.build): '
+                      'using the PyTorch caching allocator')
+        return False
+    return enable()

@@ -80,6 +80,21 @@ __device__ __forceinline__ float act(float x) {
 
 constexpr int BM = 256, BN = 256, BKT = 64;  // the GEMM tile (conv configs below narrow BN)
 
+// Phase stamps for diagnostic builds only (gemm_probe.hip defines PRA_GEMM_STAMPS 1; the
+// library's kernels compile them out): lane 0 of wave 0 of each workgroup writes 8 words into
+// the (otherwise unused) ws buffer of a non-split launch: shader clock at entry / loop start /
+// loop end / exit, the 100 MHz real-time clock at entry / exit, HW_ID and XCC_ID.
+#ifndef PRA_GEMM_STAMPS
+#define PRA_GEMM_STAMPS 0
+#endif
+#define PRA_STAMP(k, v)                                                                            \
+  do {                                                                                             \
+    if constexpr (PRA_GEMM_STAMPS) {                                                               \
+      if (threadIdx.x == 0)                                                                        \
+        reinterpret_cast<volatile unsigned long long*>(ws)[(size_t)blockIdx.x * 8 + (k)] = (v);   \
+    }                                                                                              \
+  } while (0)
+
 // Wave layouts of a BM_ x BN_ tile: WR x WC waves, each (BM_/WR) x (BN_/WC) outputs.
 //   W8: 256x256, 2 x 4 waves (128x64 each, 2 waves/SIMD, 32 accumulators)
 //   W4: 256x256, 2 x 2 waves (128x128 each, 1 wave/SIMD, 64 accumulators in AGPRs)
@@ -343,6 +358,10 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_lds_kernel(const uint16_t* __r
   __shared__ __attribute__((aligned(1024))) char lds[CF::LDS];
   typedef typename V8<T>::type v8;
   const uint32_t lds_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)lds;
+  PRA_STAMP(0, __builtin_amdgcn_s_memtime());
+  PRA_STAMP(4, __builtin_amdgcn_s_memrealtime());
+  PRA_STAMP(6, (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4));
+  PRA_STAMP(7, (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 20));
 
   const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;
   const int nb = gridDim.x;
@@ -480,6 +499,7 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_lds_kernel(const uint16_t* __r
   }
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
+  PRA_STAMP(1, __builtin_amdgcn_s_memtime());
   read_frags(fa0, fb0, 0, 0);
 
   // K-step kt (slot kt&1): half 0 computes (kt,0) from F0 while reading (kt,1) into F1; then the
@@ -665,6 +685,7 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_lds_kernel(const uint16_t* __r
   for (; kt < nk; ++kt) kstep(kt, std::false_type{});
   }  // !PIPE
   }  // nk > 0
+  PRA_STAMP(2, __builtin_amdgcn_s_memtime());
 
   // last asm MFMA -> v_accvgpr_read of its result: the hazard recognizer cannot see the asm
   if constexpr (AGPR_ACC) asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
@@ -834,6 +855,9 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_lds_kernel(const uint16_t* __r
       }
     }
   }
+  if constexpr (PRA_GEMM_STAMPS) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  PRA_STAMP(3, __builtin_amdgcn_s_memtime());
+  PRA_STAMP(5, __builtin_amdgcn_s_memrealtime());
 }
 
 // split-K combine: C[m][n..n+3] = epi(sum_s ws[s][m][n..n+3] + bias) (+ C if BETA)

@@ -1,0 +1,39 @@
+// Diagnostic build of the LDS-DMA MFMA GEMM with per-workgroup phase stamps (PRA_STAMP in
+// gemm_core.h): where a tile's time goes (prologue / K loop / epilogue, launch gaps per CU).
+// Timing tools only (scripts/gemm_stamps.py); no framework op calls it.
+#define PRA_GEMM_STAMPS 1
+#include "gemm_core.h"
+
+namespace pra {
+namespace {
+using PW4 = WCfg<2, 2, 256, 256, true>;
+using PW4T = WCfg<2, 2, 256, 256, true, false, false, true>;
+
+template <typename CF, bool AK, bool BK>
+void probe_launch(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
+                  unsigned long long* stamps, hipStream_t s) {
+  const int tiles = ((M + 255) / 256) * ((N + 255) / 256);
+  gemm_lds_kernel<bf16, CF, AK, BK, kNone, false, false><<<tiles, CF::NT, 0, s>>>(
+      static_cast<const uint16_t*>(A), static_cast<const uint16_t*>(B), nullptr, static_cast<uint16_t*>(C), nullptr,
+      nullptr, M, N, K, lda, ldb, ldc, ldc, 1, reinterpret_cast<float*>(stamps));
+}
+}  // namespace
+}  // namespace pra
+
+// cfg: 0 = W8, 1 = W4, 2 = W4T; layout 0 (x·W) or 1 (dy·Wᵀ). stamps: 8 words per workgroup.
+// Returns the number of workgroups (or -1).
+extern "C" int pra_gemm_probe(int cfg, int layout, const void* A, const void* B, void* C, int M, int N, int K, int lda,
+                              int ldb, int ldc, unsigned long long* stamps, hipStream_t s) {
+  if (M % 256 || N % 256 || K % 64 || (layout != 0 && layout != 1)) return -1;
+  const int tiles = (M / 256) * (N / 256);
+  if (layout == 0) {
+    if (cfg == 0) pra::probe_launch<pra::W8, true, false>(A, B, C, M, N, K, lda, ldb, ldc, stamps, s);
+    else if (cfg == 1) pra::probe_launch<pra::PW4, true, false>(A, B, C, M, N, K, lda, ldb, ldc, stamps, s);
+    else pra::probe_launch<pra::PW4T, true, false>(A, B, C, M, N, K, lda, ldb, ldc, stamps, s);
+  } else {
+    if (cfg == 0) pra::probe_launch<pra::W8, true, true>(A, B, C, M, N, K, lda, ldb, ldc, stamps, s);
+    else if (cfg == 1) pra::probe_launch<pra::PW4, true, true>(A, B, C, M, N, K, lda, ldb, ldc, stamps, s);
+    else pra::probe_launch<pra::PW4T, true, true>(A, B, C, M, N, K, lda, ldb, ldc, stamps, s);
+  }
+  return tiles;
+}
