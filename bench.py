@@ -35,6 +35,8 @@ def parse():
     p.add_argument('--recompute', action='store_true')
     p.add_argument('--zero3-release', action='store_true',
                    help='release gathered ZeRO-3 units after forward (reference schedule)')
+    p.add_argument('--no-graph', action='store_true',
+                   help='BERT: run the static Executor op by op (no HIP-graph replay)')
     p.add_argument('--profile-dir', default=None)
     p.add_argument('--no-tuned-gemms', action='store_true',
                    help='skip the committed MI355X TunableOp GEMM solutions')
@@ -364,7 +366,7 @@ def bench_bert(a, paddle, torch, dist, C, world, rank, dev):
     exe = static.Executor()
     exe.run(startup)
     prog = main_p
-    if dev.type == 'cuda':
+    if dev.type == 'cuda' and not a.no_graph:
         prog = static.CompiledProgram(main_p)
         prog._build_strategy.use_hip_graph = True
     rs = np.random.RandomState(rank)
@@ -390,7 +392,7 @@ def bench_bert(a, paddle, torch, dist, C, world, rank, dev):
             "ms_per_step": round(dt / a.steps * 1000, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
             "config": {"model": name, "global_batch": bs * world, "seq_len": S,
-                       "parallelism": f"dp{world}", "executor": "static Program, HIP graph",
+                       "parallelism": f"dp{world}", "executor": "static Program, " + ("op by op" if a.no_graph else "HIP graph"),
                        "amp": "O2 bf16 (fp32 master weights)",
                        "masked_positions_per_seq": P},
             "tokens_per_sec": round(sps * S, 1), "final_loss": float(last[0])}

@@ -528,6 +528,8 @@ def _vjp(ctx, *out_grads):
 # predicate picks this path at run time; when it declines (e.g. an AMP cast the fused kernel
 # does not take) the op runs the generic autograd path and its grad op falls back to _vjp.
 _FN_OPS = {}   # op type -> (autograd.Function class, predicate(torch args) -> bool)
+# PRA_STATIC_DIRECT_GRAD=0: every direct-grad op takes the generic autograd path (A/B timing)
+_DIRECT_GRAD = __import__('os').environ.get('PRA_STATIC_DIRECT_GRAD', '1') != '0'
 
 
 def register_fn_op(op_type, fn_cls, pred=None):
@@ -989,6 +991,8 @@ class Executor:
 
     def _run_fn_op(self, op, env):
         """Forward of a direct-grad op: Function.forward on a _FnCtx (None: predicate declined)."""
+        if not _DIRECT_GRAD:
+            return None
         fn_cls, pred = _FN_OPS[op.type]
         vals = _materialize(op.args, env)
         targs = [_u(a) if isinstance(a, Tensor) else a for a in vals]
