@@ -602,10 +602,55 @@ class Tensor:
         self._t.data = _u(v)
 
     def is_dense(self):
-        return True
+        return self._t.layout == torch.strided
 
     def is_sparse(self):
-        return self._t.is_sparse
+        return self._t.layout in (torch.sparse_coo, torch.sparse_csr)
+
+    # -- sparse tensor surface (parity: SparseCooTensor / SparseCsrTensor methods) ---------------
+    def is_sparse_coo(self):
+        return self._t.layout == torch.sparse_coo
+
+    def is_sparse_csr(self):
+        return self._t.layout == torch.sparse_csr
+
+    def indices(self):
+        t = self._t.coalesce() if self._t.layout == torch.sparse_coo else self._t.to_sparse_coo().coalesce()
+        return Tensor(t.indices())
+
+    def values(self):
+        t = self._t
+        if t.layout == torch.sparse_coo:
+            return Tensor(t.coalesce().values())
+        return Tensor(t.values())
+
+    def crows(self):
+        return Tensor(self._t.crow_indices())
+
+    def cols(self):
+        return Tensor(self._t.col_indices())
+
+    def nnz(self):
+        t = self._t
+        return int(t.coalesce()._nnz() if t.layout == torch.sparse_coo else t._nnz())
+
+    def to_dense(self):
+        return Tensor(self._t.to_dense() if self.is_sparse() else self._t)
+
+    def to_sparse_coo(self, sparse_dim=None):
+        t = self._t
+        if t.layout == torch.sparse_csr:
+            return Tensor(t.to_sparse_coo().coalesce())
+        if t.layout == torch.sparse_coo:
+            return Tensor(t)
+        return Tensor(t.to_sparse(sparse_dim if sparse_dim is not None else t.dim()).coalesce())
+
+    def to_sparse_csr(self):
+        t = self._t
+        if t.layout == torch.sparse_csr:
+            return Tensor(t)
+        return Tensor(t.to_dense().to_sparse_csr() if t.dim() > 2 and t.layout == torch.sparse_coo
+                      else t.to_sparse_csr())
 
     def _is_initialized(self):
         return True

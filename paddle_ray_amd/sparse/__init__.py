@@ -78,7 +78,51 @@ def transpose(x, perm, name=None):
 
 
 def reshape(x, shape, name=None):
-    return Tensor(_u(x).to_dense().reshape(shape).to_sparse())
+    """Reshape the SPARSE dims of a COO tensor without densifying: every index tuple is
+    linearised over the old sparse shape and unravelled over the new one (dense trailing dims,
+    e.g. channels, must be unchanged). CSR inputs go through COO."""
+    t = _u(x)
+    csr = t.layout == torch.sparse_csr
+    t = (t.to_sparse_coo() if csr else t).coalesce()
+    sd, dd = t.sparse_dim(), t.dense_dim()
+    old_sp = list(t.shape[:sd])
+    dense = list(t.shape[sd:])
+    shape = list(shape)
+    n_sp = 1
+    for v in old_sp:
+        n_sp *= v
+    if -1 in shape:
+        known = 1
+        for v in shape:
+            if v != -1:
+                known *= v
+        shape[shape.index(-1)] = (n_sp * max(1, _prod(dense))) // known
+    if dd:
+        if shape[len(shape) - dd:] != dense:
+            raise ValueError(f"sparse reshape keeps the dense dims {dense}; got {shape}")
+        new_sp = shape[:len(shape) - dd]
+    else:
+        new_sp = shape
+    if _prod(new_sp) != n_sp:
+        raise ValueError(f"cannot reshape sparse dims {old_sp} into {new_sp}")
+    idx = t.indices()
+    lin = torch.zeros(idx.shape[1], dtype=torch.int64, device=idx.device)
+    for d, n in enumerate(old_sp):
+        lin = lin * n + idx[d]
+    out = []
+    for n in reversed(new_sp):
+        out.append(lin % n)
+        lin = lin // n
+    nidx = torch.stack(out[::-1]) if out else idx[:0]
+    r = torch.sparse_coo_tensor(nidx, t.values(), new_sp + dense).coalesce()
+    return Tensor(r.to_sparse_csr() if csr and len(new_sp) == 2 and not dd else r)
+
+
+def _prod(v):
+    p = 1
+    for x in v:
+        p *= x
+    return p
 
 
 def coalesce(x, name=None):

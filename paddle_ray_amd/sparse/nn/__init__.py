@@ -2,9 +2,10 @@
 
 Sparse COO tensors here are torch sparse tensors whose sparse dims are (N, D, H, W) and
 whose dense dim is the channel (NDHWC, values [nnz, C]) -- the reference's layout for 3-D
-point-cloud / voxel networks. Convolutions compute on the densified grid and keep the
-sparse-conv output pattern: a regular Conv3D activates every output site reached by an
-active input site, a submanifold conv keeps exactly the input's active sites.
+point-cloud / voxel networks. Convolutions and max pooling run on the active sites only through
+a rulebook (sparse/rulebook.py: gather - GEMM - scatter per kernel offset, O(nnz x kernel
+volume)): a regular Conv3D activates every output site reached by an active input site, a
+submanifold conv keeps exactly the input's active sites.
 """
 import torch
 import torch.nn.functional as TF
@@ -61,26 +62,15 @@ class functional:
 
     @staticmethod
     def _conv(x, weight, bias, stride, padding, dilation, groups, subm):
+        """Rulebook gather-GEMM-scatter on the active sites (sparse/rulebook.py)."""
+        from ..rulebook import sparse_conv3d
         t = _coo(x)
-        dense = t.to_dense()  # [N, D, H, W, C]
+        N, D, H, W = t.shape[:4]
         w = _u(weight)  # [kD, kH, kW, Cin/groups, Cout]
-        stride, padding, dilation = _triple(stride), _triple(padding), _triple(dilation)
-        if subm:
-            stride = (1, 1, 1)
-            padding = tuple(d * (k - 1) // 2 for d, k in zip(dilation, w.shape[:3]))
-        inp = dense.permute(0, 4, 1, 2, 3)
-        out = TF.conv3d(inp, w.permute(4, 3, 0, 1, 2), None, stride, padding, dilation, groups)
-        out = out.permute(0, 2, 3, 4, 1)
-        if bias is not None:
-            out = out + _u(bias)
-        occ = torch.zeros(dense.shape[:4], dtype=dense.dtype, device=dense.device)
-        occ[tuple(t.indices())] = 1.0
-        if subm:
-            active = occ > 0
-        else:
-            k = torch.ones((1, 1) + tuple(w.shape[:3]), dtype=occ.dtype, device=occ.device)
-            active = TF.conv3d(occ[:, None], k, None, stride, padding, dilation)[:, 0] > 0
-        return _from_dense(out, active)
+        out, oc, osp = sparse_conv3d(t.values(), t.indices().t(), N, (D, H, W), w,
+                                     None if bias is None else _u(bias), stride, padding, dilation,
+                                     groups, subm)
+        return Tensor(torch.sparse_coo_tensor(oc.t(), out, (N,) + tuple(osp) + (w.shape[-1],)).coalesce())
 
     @staticmethod
     def conv3d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1,
@@ -96,18 +86,14 @@ class functional:
     def max_pool3d(x, kernel_size, stride=None, padding=0, ceil_mode=False,
                    data_format='NDHWC', name=None):
         """Max over the ACTIVE sites of each window; windows without one stay inactive."""
+        from ..rulebook import sparse_max_pool3d
+        if ceil_mode:
+            raise NotImplementedError("sparse max_pool3d: ceil_mode")
         t = _coo(x)
-        dense = t.to_dense()
-        occ = torch.zeros(dense.shape[:4], dtype=torch.bool, device=dense.device)
-        occ[tuple(t.indices())] = True
-        neg = torch.finfo(dense.dtype).min
-        filled = torch.where(occ[..., None], dense, torch.full_like(dense, neg))
-        k = _triple(kernel_size)
-        s = _triple(stride) if stride is not None else k
-        p = _triple(padding)
-        out = TF.max_pool3d(filled.permute(0, 4, 1, 2, 3), k, s, p, ceil_mode=ceil_mode)
-        act = TF.max_pool3d(occ[:, None].float(), k, s, p, ceil_mode=ceil_mode)[:, 0] > 0
-        return _from_dense(out.permute(0, 2, 3, 4, 1), act)
+        N, D, H, W = t.shape[:4]
+        out, oc, osp = sparse_max_pool3d(t.values(), t.indices().t(), N, (D, H, W), kernel_size, stride,
+                                         _triple(padding))
+        return Tensor(torch.sparse_coo_tensor(oc.t(), out, (N,) + tuple(osp) + (t.shape[-1],)).coalesce())
 
     @staticmethod
     def attention(query, key, value, sparse_mask, key_padding_mask=None, attn_mask=None,

@@ -99,3 +99,49 @@ def test_distribution_transforms():
         return paddle.to_tensor(42.0)
     assert float(D.kl_divergence(MyNormal(0.0, 1.0), MyNormal(1.0, 1.0))) == 42.0
     assert abs(float(D.kl_divergence(D.Normal(0.0, 1.0), D.Normal(1.0, 1.0))) - 0.5) < 1e-6
+
+
+def test_sparse_conv_rulebook_large_grid_and_grads():
+    """Rulebook convolution on a 1 x 256^3 grid with 64 active sites (a dense grid would be 16M
+    sites x C): output pattern, values against a dense conv3d of the small neighbourhood, and
+    gradients through gather/GEMM/scatter."""
+    import torch
+    import paddle_ray_amd.sparse as sp
+    rs = np.random.RandomState(0)
+    pts = np.unique(rs.randint(0, 256, (64, 3)), axis=0)
+    idx = torch.tensor(np.concatenate([np.zeros((len(pts), 1), np.int64), pts], 1).T)
+    vals = torch.randn(len(pts), 4, dtype=torch.float64, requires_grad=True)
+    x = paddle.Tensor(torch.sparse_coo_tensor(idx, vals, (1, 256, 256, 256, 4)).coalesce())
+    w = torch.randn(3, 3, 3, 4, 5, dtype=torch.float64, requires_grad=True)
+    y = sp.nn.functional.subm_conv3d(x, paddle.Tensor(w), padding=1)
+    yt = y._t
+    assert yt._nnz() == len(pts) and torch.equal(yt.indices(), x._t.indices())
+    # reference for one site: sum over its active neighbours
+    ci = x._t.indices().t()
+    site = ci[0]
+    ref = torch.zeros(5, dtype=torch.float64)
+    for j, c in enumerate(ci):
+        d = (c[1:] - site[1:] + 1)
+        if bool(((d >= 0) & (d <= 2)).all()):
+            ref = ref + x._t.values()[j] @ w[d[0], d[1], d[2]]
+    np.testing.assert_allclose(yt.values()[0].detach().numpy(), ref.detach().numpy(), rtol=1e-10)
+    yt.values().sum().backward()
+    assert vals.grad is not None and w.grad is not None and float(w.grad.abs().sum()) > 0
+    z = sp.nn.functional.conv3d(x, paddle.Tensor(w.detach()), stride=2)
+    assert z._t.shape[1:4] == (127, 127, 127) and z._t._nnz() <= 27 * len(pts)
+
+
+def test_sparse_reshape_keeps_sparsity():
+    import torch
+    import paddle_ray_amd.sparse as sp
+    d = torch.zeros(4, 6)
+    d[1, 2], d[3, 5], d[0, 0] = 1.0, 2.0, 3.0
+    x = paddle.Tensor(d.to_sparse())
+    y = sp.reshape(x, [3, 8])
+    assert y.is_sparse_coo() and y.nnz() == 3
+    np.testing.assert_allclose(y.to_dense().numpy(), d.reshape(3, 8).numpy())
+    y2 = sp.reshape(x, [2, -1, 3])
+    np.testing.assert_allclose(y2.to_dense().numpy(), d.reshape(2, 4, 3).numpy())
+    c = sp.reshape(paddle.Tensor(d.to_sparse_csr()), [8, 3])
+    assert c.is_sparse_csr()
+    np.testing.assert_allclose(c.to_dense().numpy(), d.reshape(8, 3).numpy())
