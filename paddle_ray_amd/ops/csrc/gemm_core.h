@@ -114,11 +114,13 @@ constexpr int BM = 256, BN = 256, BKT = 64;  // the GEMM tile (conv configs belo
 //       fragments are read only in the last MFMAs of the second half, after a counted vmcnt that
 //       leaves the refill in flight -> every DMA piece has ~1.5 K-steps of lead (the loop shape
 //       of the 256x256x64 MFMA16 kernels hipBLASLt ships for gfx950, measured 84 % MFMA-busy)
+//   SC1: operand DMA with the sc1 cache policy (bypass the CU's vector L1: LDS-DMA data never
+//       benefits from L1, and the loads then do not evict / thrash it)
 template <int WR_, int WC_, int BM_ = 256, int BN_ = 256, bool ILV_ = false, bool BUF_ = false,
-          bool PIPE_ = false, bool TS_ = false>
+          bool PIPE_ = false, bool TS_ = false, bool SC1_ = false>
 struct WCfg {
   static constexpr int WR = WR_, WC = WC_, NT = 64 * WR_ * WC_, BM = BM_, BN = BN_;
-  static constexpr bool ILV = ILV_, BUF = BUF_, PIPE = PIPE_, TS = TS_;
+  static constexpr bool ILV = ILV_, BUF = BUF_, PIPE = PIPE_, TS = TS_, SC1 = SC1_;
   static constexpr int TI = BM_ / WR_ / 16, TJ = BN_ / WC_ / 16;  // 16x16 MFMA tiles per wave
   static constexpr int IMGA = BM_ * BKT * 2, IMGB = BN_ * BKT * 2, SLOT = IMGA + IMGB;
   static constexpr int NDA = IMGA / (NT * 16), NDB = IMGB / (NT * 16);  // glds per thread per K-step
@@ -155,7 +157,7 @@ __device__ __forceinline__ int kc_swz(int row) { return (row >> 1) & 7; }
 // KC image: position P (16-B chunk 0..2047) = row P>>3, slot P&7 holds global chunk (P&7)^kc_swz(row).
 // MC image (MCW columns: 256, or 128 for narrow tiles): position P = k-row P/(MCW/8), slot
 // P%(MCW/8) holds global chunk (P%(MCW/8))^mc_swz(k) (mc_swz < 16 keeps it inside a 128-wide row).
-template <bool KC, int NT, int NDMA, bool BUF = false, int MCW = 256>
+template <bool KC, int NT, int NDMA, bool BUF = false, int MCW = 256, bool SC1 = false>
 struct Dma {
   static constexpr int MCC = MCW / 8;  // 16-B chunks per k-row of the MC image
   uint32_t voff[NDMA];  // per-lane byte offsets of the chunks this thread stages
@@ -188,10 +190,20 @@ struct Dma {
     // compiler's waitcnt model does not see an LDS write in flight and never drains it with
     // vmcnt(0) ahead of the fragment reads: the explicit vmcnt in the K loop is the only wait.
     const uint32_t dst = __builtin_amdgcn_readfirstlane(lds_img + (n * NT + wave * 64) * 16);
-    if constexpr (BUF) {
+    if constexpr (BUF && SC1) {
+      const u32x4 rs = {glo, ghi & 0xffffu, 0xffffffffu, 0x00020000u};
+      asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen sc1 lds" ::"v"(voff[n]),
+                   "s"(rs), "s"(dst)
+                   : "memory");
+    } else if constexpr (BUF) {
       // MUBUF form (raw buffer, stride 0, no range limit: the offsets are clamped in-bounds)
       const u32x4 rs = {glo, ghi & 0xffffu, 0xffffffffu, 0x00020000u};
       asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff[n]), "s"(rs),
+                   "s"(dst)
+                   : "memory");
+    } else if constexpr (SC1) {
+      const uint64_t gs = ((uint64_t)ghi << 32) | (uint64_t)glo;
+      asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1 sc1" ::"v"(voff[n]), "s"(gs),
                    "s"(dst)
                    : "memory");
     } else {
@@ -384,8 +396,8 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_lds_kernel(const uint16_t* __r
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6),
             wr = wave / WC, wc = wave % WC;
 
-  typename std::conditional<CONV, ConvDmaA<NT, NDA>, Dma<AK, NT, NDA, CF::BUF, (AK ? 256 : BM)>>::type da;
-  typename std::conditional<CONVW, ConvDmaBW<NT, NDB>, Dma<BK, NT, NDB, CF::BUF>>::type db;
+  typename std::conditional<CONV, ConvDmaA<NT, NDA>, Dma<AK, NT, NDA, CF::BUF, (AK ? 256 : BM), CF::SC1>>::type da;
+  typename std::conditional<CONVW, ConvDmaBW<NT, NDB>, Dma<BK, NT, NDB, CF::BUF, 256, CF::SC1>>::type db;
   if constexpr (CONV) da.init(A, cg, m0, M, tid);
   else if (AK) da.init(A, lda, m0, M - 1, tid);
   else da.init(A, lda, m0, M - 8, tid);

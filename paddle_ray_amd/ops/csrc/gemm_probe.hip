@@ -8,6 +8,9 @@ namespace pra {
 namespace {
 using PW4 = WCfg<2, 2, 256, 256, true>;
 using PW4T = WCfg<2, 2, 256, 256, true, false, false, true>;
+using PW4S = WCfg<2, 2, 256, 256, true, true, false, false, true>;     // W4, MUBUF + sc1 DMA
+using PW8S = WCfg<2, 4, 256, 256, false, false, false, false, true>;   // W8, sc1 DMA
+using PW4TS = WCfg<2, 2, 256, 256, true, true, false, true, true>;     // W4T, MUBUF + sc1 DMA
 
 template <typename CF, bool AK, bool BK>
 void probe_launch(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
@@ -20,20 +23,31 @@ void probe_launch(const void* A, const void* B, void* C, int M, int N, int K, in
 }  // namespace
 }  // namespace pra
 
-// cfg: 0 = W8, 1 = W4, 2 = W4T; layout 0 (x·W) or 1 (dy·Wᵀ). stamps: 8 words per workgroup.
+// cfg: 0 = W8, 1 = W4, 2 = W4T, 3 = W4S, 4 = W8S, 5 = W4TS; layout 0 (x·W) or 1 (dy·Wᵀ).
+// stamps: 8 words per workgroup.
 // Returns the number of workgroups (or -1).
 extern "C" int pra_gemm_probe(int cfg, int layout, const void* A, const void* B, void* C, int M, int N, int K, int lda,
                               int ldb, int ldc, unsigned long long* stamps, hipStream_t s) {
   if (M % 256 || N % 256 || K % 64 || (layout != 0 && layout != 1)) return -1;
   const int tiles = (M / 256) * (N / 256);
   if (layout == 0) {
-    if (cfg == 0) pra::probe_launch<pra::W8, true, false>(A, B, C, M, N, K, lda, ldb, ldc, stamps, s);
-    else if (cfg == 1) pra::probe_launch<pra::PW4, true, false>(A, B, C, M, N, K, lda, ldb, ldc, stamps, s);
-    else pra::probe_launch<pra::PW4T, true, false>(A, B, C, M, N, K, lda, ldb, ldc, stamps, s);
+    switch (cfg) {
+      case 0: pra::probe_launch<pra::W8, true, false>(A, B, C, M, N, K, lda, ldb, ldc, stamps, s); break;
+      case 1: pra::probe_launch<pra::PW4, true, false>(A, B, C, M, N, K, lda, ldb, ldc, stamps, s); break;
+      case 2: pra::probe_launch<pra::PW4T, true, false>(A, B, C, M, N, K, lda, ldb, ldc, stamps, s); break;
+      case 3: pra::probe_launch<pra::PW4S, true, false>(A, B, C, M, N, K, lda, ldb, ldc, stamps, s); break;
+      case 4: pra::probe_launch<pra::PW8S, true, false>(A, B, C, M, N, K, lda, ldb, ldc, stamps, s); break;
+      default: pra::probe_launch<pra::PW4TS, true, false>(A, B, C, M, N, K, lda, ldb, ldc, stamps, s); break;
+    }
   } else {
-    if (cfg == 0) pra::probe_launch<pra::W8, true, true>(A, B, C, M, N, K, lda, ldb, ldc, stamps, s);
-    else if (cfg == 1) pra::probe_launch<pra::PW4, true, true>(A, B, C, M, N, K, lda, ldb, ldc, stamps, s);
-    else pra::probe_launch<pra::PW4T, true, true>(A, B, C, M, N, K, lda, ldb, ldc, stamps, s);
+    switch (cfg) {
+      case 0: pra::probe_launch<pra::W8, true, true>(A, B, C, M, N, K, lda, ldb, ldc, stamps, s); break;
+      case 1: pra::probe_launch<pra::PW4, true, true>(A, B, C, M, N, K, lda, ldb, ldc, stamps, s); break;
+      case 2: pra::probe_launch<pra::PW4T, true, true>(A, B, C, M, N, K, lda, ldb, ldc, stamps, s); break;
+      case 3: pra::probe_launch<pra::PW4S, true, true>(A, B, C, M, N, K, lda, ldb, ldc, stamps, s); break;
+      case 4: pra::probe_launch<pra::PW8S, true, true>(A, B, C, M, N, K, lda, ldb, ldc, stamps, s); break;
+      default: pra::probe_launch<pra::PW4TS, true, true>(A, B, C, M, N, K, lda, ldb, ldc, stamps, s); break;
+    }
   }
   return tiles;
 }

@@ -65,5 +65,5 @@ if __name__ == '__main__':
     if len(sys.argv) > 4:
         shapes = [tuple(int(x) for x in sys.argv[1:5])]
     for sh in shapes:
-        for cfg in (0, 1, 2):
+        for cfg in (0, 1, 2, 3, 4, 5):
             run(cfg, *sh)
