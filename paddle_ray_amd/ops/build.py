@@ -75,7 +75,19 @@ def _hipcc_version():
     return 'unknown'
 
 
+def _stamp_path():
+    return _out_path() + '.sources'
+
+
 def build(force=False, verbose=True):
+    # fast path: the library next to the sources was linked from exactly these sources (the
+    # sidecar travels with the .so; the object cache under build/ does not reach the GPU box)
+    if not force and os.path.exists(_out_path()) and os.path.exists(_stamp_path()):
+        with open(_stamp_path()) as f:
+            if f.read().strip() == sources_hash():
+                if verbose:
+                    print(f"up to date {_out_path()} (sources {sources_hash()[:12]})")
+                return _out_path()
     import pybind11
     os.makedirs(BUILD, exist_ok=True)
     try:
@@ -125,6 +137,8 @@ def build(force=False, verbose=True):
     manifest.update(keys)
     with open(_manifest_path(), 'w') as f:
         json.dump(manifest, f, indent=1)
+    with open(_stamp_path(), 'w') as f:
+        f.write(info['sources_sha256'] + '\n')
     if verbose:
         print(f"built {out} ({len(jobs)} objects recompiled, sources {info['sources_sha256'][:12]})")
     return out
