@@ -1818,8 +1818,9 @@ def install_static_hooks():
     from ..tensor import creation, math, manipulation, linalg as tlinalg, random as trandom
     from ..nn import functional as NF
     from ..incubate.nn import functional as IF
-    from .. import fft as FFT, linalg as LA, metric as MET
-    modules = [creation, math, manipulation, tlinalg, trandom, NF, IF, FFT]
+    from .. import linalg as LA, metric as MET
+    # paddle.fft records its own fft_c2c / fft_r2c / fft_c2r primitive ops
+    modules = [creation, math, manipulation, tlinalg, trandom, NF, IF]
     mapping = {}
     for mod in modules:
         for name, obj in list(vars(mod).items()):
