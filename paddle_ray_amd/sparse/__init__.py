@@ -1,7 +1,12 @@
-"""paddle.sparse (parity: python/paddle/sparse/*): COO/CSR tensors on PyTorch-ROCm sparse storage."""
+"""paddle.sparse (parity: python/paddle/sparse/*): COO/CSR tensors on PyTorch-ROCm sparse storage.
+
+Unary ops map the stored values (the reference's values-only unary kernels); binary ops, the
+products (SpMM / SpGEMM / SDDMM), transpose and reshape compute on the coordinates directly
+(sparse/ops.py, sparse/rulebook.py) -- nothing is densified."""
 import torch
 
 from ..framework.core import Tensor, _u, convert_dtype, _default_device
+from . import ops as _K
 
 
 def sparse_coo_tensor(indices, values, shape=None, dtype=None, place=None, stop_gradient=True):
@@ -46,35 +51,73 @@ def cast(x, index_dtype=None, value_dtype=None, name=None):
     return _vals_op(lambda v: v.to(convert_dtype(value_dtype)) if value_dtype else v)(x)
 
 
-def _bin(fn):
-    def op(x, y, name=None):
-        return Tensor(fn(_u(x), _u(y)))
-    return op
+def _sparse(t):
+    return t.layout in (torch.sparse_coo, torch.sparse_csr)
 
 
-add, subtract, multiply, divide = _bin(torch.add), _bin(torch.sub), _bin(torch.mul), \
-    _bin(torch.div)
+def _bin(op, dense_fn):
+    def f(x, y, name=None):
+        a, b = _u(x), _u(y)
+        if _sparse(a) and _sparse(b):
+            return Tensor(_K.elementwise(op, a, b))
+        if _sparse(a) or _sparse(b):       # mixed: the result is dense, like the reference
+            a = a.to_dense() if _sparse(a) else a
+            b = b.to_dense() if _sparse(b) else b
+        return Tensor(dense_fn(a, b))
+    f.__name__ = op
+    f.__doc__ = f"Sparse {op}: merged coordinate patterns (sparse/ops.py elementwise)."
+    return f
+
+
+add, subtract, multiply, divide = (_bin(n, f) for n, f in (('add', torch.add), ('subtract', torch.sub),
+                                                           ('multiply', torch.mul),
+                                                           ('divide', torch.div)))
 
 
 def matmul(x, y, name=None):
-    return Tensor(torch.sparse.mm(_u(x), _u(y)) if _u(x).is_sparse else torch.matmul(_u(x), _u(y)))
+    """sparse @ dense (SpMM), sparse @ sparse (SpGEMM, result in x's layout), dense @ sparse."""
+    a, b = _u(x), _u(y)
+    if _sparse(a) and _sparse(b):
+        return Tensor(_K.spgemm(a, b))
+    if _sparse(a):
+        return Tensor(_K.spmm(a, b))
+    if _sparse(b):
+        return Tensor(_K.dense_spmm(a, b))
+    return Tensor(torch.matmul(a, b))
 
 
 def masked_matmul(x, y, mask, name=None):
-    return Tensor(torch.sparse.sampled_addmm(_u(mask).to_sparse_csr(), _u(x), _u(y),
-                                             beta=0.0))
+    """(x @ y) evaluated only at ``mask``'s coordinates (SDDMM); result has mask's layout."""
+    return Tensor(_K.sddmm(_u(x), _u(y), _u(mask)))
 
 
 def mv(x, vec, name=None):
-    return Tensor(torch.mv(_u(x), _u(vec)))
+    return Tensor(_K.spmm(_u(x), _u(vec)))
 
 
 def addmm(input, x, y, beta=1.0, alpha=1.0, name=None):
-    return Tensor(torch.sparse.addmm(_u(input), _u(x), _u(y), beta=beta, alpha=alpha))
+    """beta * input + alpha * (x @ y); sparse input with sparse x, y stays sparse."""
+    inp, prod = _u(input), _u(matmul(x, y))
+    if _sparse(inp) and _sparse(prod):
+        return Tensor(_K.elementwise('add', _vals_scale(inp, beta), _vals_scale(prod, alpha)))
+    inp = inp.to_dense() if _sparse(inp) else inp
+    prod = prod.to_dense() if _sparse(prod) else prod
+    return Tensor(beta * inp + alpha * prod)
+
+
+def _vals_scale(t, s):
+    idx, v, shape, layout = _K.coo_parts(t)
+    return _K.make(idx, v * s, shape, layout, coalesced=True)
 
 
 def transpose(x, perm, name=None):
-    return Tensor(_u(x).permute(*perm))
+    """Permute the sparse dims by permuting the coordinate rows (dense dims stay last)."""
+    idx, v, shape, layout = _K.coo_parts(_u(x))
+    sd = idx.shape[0]
+    perm = [p % len(shape) for p in perm]
+    if sorted(perm[:sd]) != list(range(sd)) or perm[sd:] != list(range(sd, len(shape))):
+        raise ValueError(f"sparse transpose permutes the sparse dims only; got perm {perm}")
+    return Tensor(_K.make(idx[perm[:sd]], v, tuple(shape[p] for p in perm), layout))
 
 
 def reshape(x, shape, name=None):

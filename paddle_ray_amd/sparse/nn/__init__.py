@@ -54,11 +54,11 @@ class functional:
     @staticmethod
     def softmax(x, axis=-1, name=None):
         """Softmax over the stored entries of each row (missing entries are -inf)."""
+        from ..ops import row_softmax
         t = _u(x)
-        csr = t.layout == torch.sparse_csr
-        coo = t.to_sparse_coo().coalesce() if csr else t.coalesce()
-        out = torch.sparse.softmax(coo, dim=axis if axis >= 0 else coo.dim() + axis)
-        return Tensor(out.to_sparse_csr() if csr else out)
+        if axis not in (-1, t.dim() - 1):
+            raise ValueError("sparse softmax supports the last axis only (as the reference)")
+        return Tensor(row_softmax(t))
 
     @staticmethod
     def _conv(x, weight, bias, stride, padding, dilation, groups, subm):
@@ -98,20 +98,12 @@ class functional:
     @staticmethod
     def attention(query, key, value, sparse_mask, key_padding_mask=None, attn_mask=None,
                   name=None):
-        """softmax(QK^T / sqrt(d)) V restricted to the sparsity pattern of ``sparse_mask``
-        ([B*H, S, S] CSR); q/k/v are [B, H, S, D]."""
-        q, k, v = _u(query), _u(key), _u(value)
-        B, H, S, Dh = q.shape
-        m = _u(sparse_mask)
-        m = (m.to_dense() if m.layout != torch.strided else m).reshape(B, H, S, S) != 0
-        s = torch.matmul(q, k.transpose(-1, -2)) / (Dh ** 0.5)
-        s = s.masked_fill(~m, float('-inf'))
-        if key_padding_mask is not None:
-            s = s.masked_fill(_u(key_padding_mask).reshape(B, 1, 1, S) == 0, float('-inf'))
-        if attn_mask is not None:
-            s = s.masked_fill(_u(attn_mask).reshape(1, 1, S, S) == 0, float('-inf'))
-        a = torch.nan_to_num(torch.softmax(s, -1))
-        return Tensor(torch.matmul(a, v))
+        """softmax(QK^T / sqrt(d)) V on the coordinates of ``sparse_mask`` ([B*H, S, S] CSR /
+        COO) only: SDDMM, row softmax and SpMM over the stored entries (sparse/ops.py)."""
+        from ..ops import attention
+        kp = None if key_padding_mask is None else _u(key_padding_mask)
+        am = None if attn_mask is None else _u(attn_mask)
+        return Tensor(attention(_u(query), _u(key), _u(value), _u(sparse_mask), kp, am))
 
 
 class ReLU(Layer):
