@@ -78,6 +78,8 @@ int pra_gemm_lds(int, const void*, const void*, const void*, void*, void*, float
                  int, int, int, int, float*, hipStream_t);
 int pra_gemm_lds_splits(int, int, int);
 void pra_gemm_set_w4(int);
+void pra_gemm_set_pts(int);
+int pra_gemm_get_pts();
 int pra_gemm_probe(int, int, const void*, const void*, void*, int, int, int, int, int, int, unsigned long long*,
                    hipStream_t);
 int pra_gemm_get_w4();
@@ -140,6 +142,8 @@ PYBIND11_MODULE(_pra_hip, m) {
   m.def("conv_lds_stat_rows", [](int m, int n) { return pra_conv_lds_stat_rows(m, n); });
   m.def("gemm_lds_splits", [](int M, int N, int K) { return pra_gemm_lds_splits(M, N, K); });
   m.def("gemm_set_w4", [](int mask) { pra_gemm_set_w4(mask); });
+  m.def("gemm_set_pts", [](int mask) { pra_gemm_set_pts(mask); });
+  m.def("gemm_get_pts", []() { return pra_gemm_get_pts(); });
   m.def("gemm_probe", [](int cfg, int layout, P a, P b, P c, int M, int N, int K, int lda, int ldb, int ldc, P st,
                          P stream) {
     return pra_gemm_probe(cfg, layout, CV(a), CV(b), V(c), M, N, K, lda, ldb, ldc,

@@ -91,7 +91,21 @@ constexpr int BM = 256, BN = 256, BKT = 64;  // the GEMM tile (conv configs belo
   do {                                                                                             \
     if constexpr (PRA_GEMM_STAMPS) {                                                               \
       if (threadIdx.x == 0)                                                                        \
-        reinterpret_cast<volatile unsigned long long*>(ws)[(size_t)blockIdx.x * 8 + (k)] = (v);   \
+        reinterpret_cast<volatile unsigned long long*>(ws)[(size_t)blockIdx.x * 16 + (k)] = (v);  \
+    }                                                                                              \
+  } while (0)
+// in-loop section clocks (default K-step body): PRA_TMARK(i) takes shader clock mark i of the
+// K-step, PRA_TACC adds the three section lengths to per-thread sums stored at words 8..10
+#define PRA_TMARK(i)                                                                               \
+  do {                                                                                             \
+    if constexpr (PRA_GEMM_STAMPS) pra_tm[i] = __builtin_amdgcn_s_memtime();                      \
+  } while (0)
+#define PRA_TACC()                                                                                 \
+  do {                                                                                             \
+    if constexpr (PRA_GEMM_STAMPS) {                                                               \
+      pra_ts[0] += pra_tm[1] - pra_tm[0];                                                          \
+      pra_ts[1] += pra_tm[2] - pra_tm[1];                                                          \
+      pra_ts[2] += pra_tm[3] - pra_tm[2];                                                          \
     }                                                                                              \
   } while (0)
 
@@ -370,6 +384,9 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_lds_kernel(const uint16_t* __r
   __shared__ __attribute__((aligned(1024))) char lds[CF::LDS];
   typedef typename V8<T>::type v8;
   const uint32_t lds_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)lds;
+  unsigned long long pra_tm[4] = {0, 0, 0, 0}, pra_ts[3] = {0, 0, 0};
+  (void)pra_tm;
+  (void)pra_ts;
   PRA_STAMP(0, __builtin_amdgcn_s_memtime());
   PRA_STAMP(4, __builtin_amdgcn_s_memrealtime());
   PRA_STAMP(6, (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4));
@@ -526,18 +543,23 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_lds_kernel(const uint16_t* __r
   // wave-uniform branches per K-step in the steady state). The last two steps run the generic body.
   auto kstep = [&](int kt, auto steady_c) __attribute__((always_inline)) {
     constexpr bool STEADY = decltype(steady_c)::value;
+    PRA_TMARK(0);
     half(fa0, fb0, fa1, fb1, true, kt, 1, false, 0, false, 0);
     __builtin_amdgcn_sched_barrier(0);
+    PRA_TMARK(1);
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): (kt,1) fragments landed; slot kt reads done
     if (STEADY || kt + 1 < nk) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // step kt+1 landed (this wave)
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
+    PRA_TMARK(2);
     if constexpr (STEADY) {
       half(fa1, fb1, fa0, fb0, true, kt + 1, 0, true, kt + 2, true, kt + 2);
     } else {
       half(fa1, fb1, fa0, fb0, kt + 1 < nk, kt + 1, 0, kt + 2 < nk && dmaon, kt + 2, kt + 2 < nk && dmaon, kt + 2);
     }
     __builtin_amdgcn_sched_barrier(0);
+    PRA_TMARK(3);
+    PRA_TACC();
     // (kt+1,0) fragments landed. The steady body leaves this to the compiler's per-register
     // lgkmcnt(N) before each consuming MFMA (no LDS-safety role: slot kt+1 is refilled only after
     // the next half-0 drain + barrier), so the next half starts on its first fragments.
@@ -608,72 +630,68 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_lds_kernel(const uint16_t* __r
     }
     if constexpr (!STEADY) __builtin_amdgcn_s_waitcnt(0xC07F);
   };
-  // TS schedule, K-step kt (slot kt&1), NM = TI*TJ MFMAs per k-half:
-  //   half 0: MFMAs of (kt,0) from F0; fillers f < NRD = the reads of (kt,1) into F1; at
-  //           f = BA: lgkmcnt(0) + barrier (every wave is done with slot kt); then the A pieces
-  //           of step kt+2 into slot kt, spread over the rest of the half;
-  //   half 1: MFMAs of (kt,1) from F1; the B pieces of step kt+2 spread over f < BB; at f = BB:
-  //           vmcnt(NDA+NDB) (step kt+1 landed, kt+2 still in flight) + barrier; then the reads
-  //           of (kt+1,0) into F0 in the last NRD MFMAs.
+  // TS schedule, K-step kt (slot kt&1): one run of F = 2*NM MFMAs (NM = TI*TJ per k-half; the
+  // first NM from F0 = (kt,0), the rest from F1 = (kt,1)), one filler slot after each MFMA f:
+  //   f < NRD:        the reads of (kt,1) into F1 (slot kt is then fully in registers)
+  //   f == BA:        lgkmcnt(0) + barrier: every wave is done with slot kt
+  //   BA < f < BB:    the NDMA pieces of step kt+2 into slot kt, one every SP MFMAs (an LDS-DMA
+  //                   issue needs ~60 cycles of MFMA cover; denser spacing stalls the matrix pipe)
+  //   f == BB:        vmcnt(NDMA) (step kt+1 landed, kt+2 in flight) + barrier
+  //   BB < f <= BB+NRD: the reads of (kt+1,0) into F0 (free since MFMA NM-1)
+  // Every piece has ~1.5 K-steps of lead and no fragment read shares a stretch with DMA issue
+  // (the loop shape of the 256x256x64 MFMA16 kernels hipBLASLt ships for gfx950).
   auto kstep_t = [&](int kt, auto steady_c) __attribute__((always_inline)) {
     constexpr bool STEADY = decltype(steady_c)::value;
-    constexpr int NRD = TI + TJ, NDMA = NDA + NDB, NM = TI * TJ;
-    constexpr int BA = (2 * NM) / 3;                 // 42 of 64 (W4), 21 of 32 (W8)
-    constexpr int BB = NM - NRD - 2;                 // 46 of 64 (W4), 18 of 32 (W8)
-    constexpr int SPA = (NM - 1 - BA) / NDA > 0 ? (NM - 1 - BA) / NDA : 1;
-    constexpr int SPB = BB / NDB > 0 ? BB / NDB : 1;
-    static_assert(NRD < BA && BA < NM - 1 && NRD + 1 < NM - BB, "TS: fillers exceed the half's MFMAs");
+    constexpr int NRD = TI + TJ, NDMA = NDA + NDB, NM = TI * TJ, F = 2 * NM;
+    constexpr int BA = NRD + 4;                      // 20 of 128 (W4), 16 of 64 (W8)
+    constexpr int BB = F - NRD - 3;                  // 109 (W4), 49 (W8)
+    constexpr int SP = (BB - BA - 1) / NDMA > 0 ? (BB - BA - 1) / NDMA : 1;  // 5 (W4), 4 (W8)
+    static_assert(BB >= NM && BA + 1 + (NDMA - 1) * SP < BB, "TS: fillers exceed the K-step's MFMAs");
     const bool dma = STEADY || (kt + 2 < nk && dmaon);
     const bool rd1 = STEADY || kt + 1 < nk;
     const uint32_t soA = lds_base + (kt & 1) * SLOT, soB = soA + IMGA;
-    {
-      const char* ai = lds + (kt & 1) * SLOT;
-      const char* bi = ai + IMGA;
+    const char* ai = lds + (kt & 1) * SLOT;
+    const char* bi = ai + IMGA;
+    const char* an = lds + ((kt + 1) & 1) * SLOT;
+    const char* bn = an + IMGA;
 #pragma unroll
-      for (int i = 0; i < TI; ++i)
+    for (int h = 0; h < 2; ++h)
 #pragma unroll
-        for (int j = 0; j < TJ; ++j) {
-          if constexpr (AGPR_ACC) mma_agpr<T>(fb0[j], fa0[i], acc[i][j]);
-          else acc[i][j] = mma<T>(fb0[j], fa0[i], acc[i][j]);
-          __builtin_amdgcn_sched_barrier(0);
-          const int f = i * TJ + j;
-          if (f < TJ) {
-            fb1[f] = frag<T, BK>(bi, wc * CW + f * 16, 1, lane);
-          } else if (f < NRD) {
-            fa1[f - TJ] = frag<T, AK, (AK ? 256 : BM)>(ai, wr * RW + (f - TJ) * 16, 1, lane);
-          } else if (f == BA) {
-            __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's reads of slot kt done
-            __builtin_amdgcn_s_barrier();        // every wave's
-          } else if (dma && f > BA && (f - BA - 1) % SPA == 0 && (f - BA - 1) / SPA < NDA) {
-            da.issue1(soA, wave, kt + 2, (f - BA - 1) / SPA);
-          }
-          __builtin_amdgcn_sched_barrier(0);
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      const int f = h * NM + i * TJ + j;
+      if (h == 0) {
+        if constexpr (AGPR_ACC) mma_agpr<T>(fb0[j], fa0[i], acc[i][j]);
+        else acc[i][j] = mma<T>(fb0[j], fa0[i], acc[i][j]);
+      } else {
+        if constexpr (AGPR_ACC) mma_agpr<T>(fb1[j], fa1[i], acc[i][j]);
+        else acc[i][j] = mma<T>(fb1[j], fa1[i], acc[i][j]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if (f < TJ) {
+        fb1[f] = frag<T, BK>(bi, wc * CW + f * 16, 1, lane);
+      } else if (f < NRD) {
+        fa1[f - TJ] = frag<T, AK, (AK ? 256 : BM)>(ai, wr * RW + (f - TJ) * 16, 1, lane);
+      } else if (f == BA) {
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's reads of slot kt done
+        __builtin_amdgcn_s_barrier();        // every wave's
+      } else if (f > BA && f < BB) {
+        const int d = (f - BA - 1) / SP;
+        if (dma && (f - BA - 1) % SP == 0 && d < NDMA) {
+          if (d < NDA) da.issue1(soA, wave, kt + 2, d);
+          else db.issue1(soB, wave, kt + 2, d - NDA);
         }
-    }
-    {
-      const char* ai = lds + ((kt + 1) & 1) * SLOT;
-      const char* bi = ai + IMGA;
-#pragma unroll
-      for (int i = 0; i < TI; ++i)
-#pragma unroll
-        for (int j = 0; j < TJ; ++j) {
-          if constexpr (AGPR_ACC) mma_agpr<T>(fb1[j], fa1[i], acc[i][j]);
-          else acc[i][j] = mma<T>(fb1[j], fa1[i], acc[i][j]);
-          __builtin_amdgcn_sched_barrier(0);
-          const int f = i * TJ + j;
-          if (f < BB) {
-            if (dma && f % SPB == 0 && f / SPB < NDB) db.issue1(soB, wave, kt + 2, f / SPB);
-          } else if (f == BB) {
-            if (dma) wait_vmcnt<NDMA>();  // step kt+1's pieces landed (kt+2's in flight)
-            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __builtin_amdgcn_s_barrier();  // ... for every wave
-          } else if (rd1 && f - BB - 1 < NRD) {
-            const int r = f - BB - 1;
-            if (r < TJ) fb0[r] = frag<T, BK>(bi, wc * CW + r * 16, 0, lane);
-            else fa0[r - TJ] = frag<T, AK, (AK ? 256 : BM)>(ai, wr * RW + (r - TJ) * 16, 0, lane);
-          }
-          __builtin_amdgcn_sched_barrier(0);
-        }
+      } else if (f == BB) {
+        if (dma) wait_vmcnt<NDMA>();  // step kt+1's pieces landed (kt+2's in flight)
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();  // ... for every wave
+      } else if (rd1 && f > BB && f - BB - 1 < NRD) {
+        const int r = f - BB - 1;
+        if (r < TJ) fb0[r] = frag<T, BK>(bn, wc * CW + r * 16, 0, lane);
+        else fa0[r - TJ] = frag<T, AK, (AK ? 256 : BM)>(an, wr * RW + (r - TJ) * 16, 0, lane);
+      }
+      __builtin_amdgcn_sched_barrier(0);
     }
     if constexpr (!STEADY) __builtin_amdgcn_s_waitcnt(0xC07F);
   };
@@ -698,6 +716,9 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_lds_kernel(const uint16_t* __r
   }  // !PIPE
   }  // nk > 0
   PRA_STAMP(2, __builtin_amdgcn_s_memtime());
+  PRA_STAMP(8, pra_ts[0]);
+  PRA_STAMP(9, pra_ts[1]);
+  PRA_STAMP(10, pra_ts[2]);
 
   // last asm MFMA -> v_accvgpr_read of its result: the hazard recognizer cannot see the asm
   if constexpr (AGPR_ACC) asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");

@@ -39,19 +39,44 @@ extern "C" int pra_gemm_alt(int cfg, int layout, const void* A, const void* B, c
                             float* colsum, int M, int N, int K, int lda, int ldb, int ldc, int ldz, int dtype, int epi,
                             int beta, int splits, float* ws, hipStream_t s);
 
+extern "C" int pra_gemm_pts_w4(int layout, const void* A, const void* B, const void* bias, void* C, void* Z,
+                               float* colsum, int M, int N, int K, int lda, int ldb, int ldc, int ldz, int dtype,
+                               int epi, int beta, hipStream_t s);
+extern "C" int pra_gemm_pts_w8(int layout, const void* A, const void* B, const void* bias, void* C, void* Z,
+                               float* colsum, int M, int N, int K, int lda, int ldb, int ldc, int ldz, int dtype,
+                               int epi, int beta, hipStream_t s);
+
 namespace pra {
 namespace {
+
+// Persistent TS kernel (gemm_pts.h) per layout, bit = 1 << layout: one workgroup per CU walks
+// its tiles with the next tile's operand DMA overlapping the epilogue. dy·Wᵀ runs the 4-wave
+// configuration (bit 4 of the mask switches it to 8 waves), x·W and xᵀ·dy the 8-wave one.
+// PRA_GEMM_PTS at first use (default 0 until measured; 7: every layout), pra_gemm_set_pts afterwards.
+int g_pts_mask = -1;
+int pts_mask() {
+  if (g_pts_mask < 0) {
+    const char* e = getenv("PRA_GEMM_PTS");
+    g_pts_mask = e ? atoi(e) : 0;
+  }
+  return g_pts_mask;
+}
 
 // Which layouts run an alternative configuration of gemm_w4.hip, 4 mask bits per config
 // (bit = 1 << (4 * cfg + layout)): cfg 0 = W4 (4 waves x 128x128), 1 = W8I (8 waves, one filler
 // per MFMA), 2 = W4B (W4 with MUBUF operand DMA), 3 = W8B (W8 with MUBUF operand DMA),
 // 4 = W4P / 5 = W8P (two barriers per K-step, refill DMA issued in half 0).
-// PRA_GEMM_W4 at first use, pra_gemm_set_w4 afterwards (A/B timing in one process).
+// 6 = W4T / 7 = W8T (the TS schedule: reads of a K-step early, refill spread one piece per 5 / 4
+// MFMAs, counted vmcnt late; gemm_core.h kstep_t).
+// Default (profiles/r4g/ts.log, 15 GPT shapes): W8T for x·W and xᵀ·dy, W4T for dy·Wᵀ -- 1.8-2 %
+// under the W8 baseline overall, best on 13 of 15 shapes.
+// PRA_GEMM_W4 at first use (0 = the W8 baseline), pra_gemm_set_w4 afterwards (A/B timing in one process).
+constexpr int kDefaultAltMask = (1 << (4 * 7 + 0)) | (1 << (4 * 6 + 1)) | (1 << (4 * 7 + 2));
 int g_w4_mask = -1;
 int w4_mask() {
   if (g_w4_mask < 0) {
     const char* e = getenv("PRA_GEMM_W4");
-    g_w4_mask = e ? atoi(e) : 0;
+    g_w4_mask = e ? atoi(e) : kDefaultAltMask;
   }
   return g_w4_mask;
 }
@@ -108,6 +133,12 @@ void launch_e(const void* A, const void* B, const void* bias, void* C, void* Z, 
 #define PRA_GEMM_LAUNCH(CFG, BETA_)                                                                         \
   gemm_lds_kernel<T, CFG, AK, BK, E, BETA_, false><<<tiles, CFG::NT, 0, s>>>(pa, pb, pbias, pc, pz, colsum, M, N, K, \
                                                                            lda, ldb, ldc, ldz, ablate, nullptr)
+  if (std::is_same<T, bf16>::value && E != kRelu && (pts_mask() >> layout & 1)) {
+    const bool w4 = layout == 1 && !(pts_mask() & 16);
+    if ((w4 ? pra_gemm_pts_w4 : pra_gemm_pts_w8)(layout, A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, kBF16,
+                                                 E, beta, s) == 0)
+      return;
+  }
   if (alt >= 0 && pra_gemm_alt(alt, layout, A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, kBF16, E, beta, 1,
                                nullptr, s) == 0)
     return;
@@ -335,4 +366,6 @@ extern "C" int pra_colsum_partials(const float* part, void* out, int P, int N, i
 }
 
 extern "C" void pra_gemm_set_w4(int mask) { pra::g_w4_mask = mask; }
+extern "C" void pra_gemm_set_pts(int mask) { pra::g_pts_mask = mask; }
+extern "C" int pra_gemm_get_pts() { return pra::pts_mask(); }
 extern "C" int pra_gemm_get_w4() { return pra::w4_mask(); }

@@ -24,7 +24,7 @@ void probe_launch(const void* A, const void* B, void* C, int M, int N, int K, in
 }  // namespace pra
 
 // cfg: 0 = W8, 1 = W4, 2 = W4T, 3 = W4S, 4 = W8S, 5 = W4TS; layout 0 (x·W) or 1 (dy·Wᵀ).
-// stamps: 8 words per workgroup.
+// stamps: 16 words per workgroup.
 // Returns the number of workgroups (or -1).
 extern "C" int pra_gemm_probe(int cfg, int layout, const void* A, const void* B, void* C, int M, int N, int K, int lda,
                               int ldb, int ldc, unsigned long long* stamps, hipStream_t s) {

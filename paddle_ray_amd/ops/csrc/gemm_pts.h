@@ -1,0 +1,335 @@
+// Persistent TS GEMM (PTS): one 256x256-tile workgroup per CU walks its tiles back to back.
+//
+// Why: on the GPT shapes the per-tile overhead of the one-launch-per-tile kernel (gemm_lds_kernel)
+// is ~20k shader cycles -- a 5-8k-cycle DMA prologue, a 10-13k-cycle LDS-staged epilogue and a
+// ~1.3k-cycle launch gap (profiles/r4/gemm_stamps_*.log) -- 20-25 % of a K=2048 tile's K loop.
+// hipBLASLt's gfx950 kernels are persistent (profiles/r4/pmc_fc1_dgrad: 256 workgroups, 2 tiles
+// each). Here the K-step stream simply continues across tiles:
+//   * the K loop is the TS schedule of gemm_core.h (kstep_t): a K-step's fragments are read in its
+//     first MFMAs, the refill of step kt+2 is spread one piece per 5 (W4) / 4 (W8) MFMAs, the
+//     counted vmcnt comes late;
+//   * in a tile's last two K-steps the refill pieces are the NEXT tile's steps 0 and 1 (slot =
+//     step parity, K/64 even), so the next tile starts computing right after the epilogue, its
+//     operands already in LDS (its first fragments are read after the epilogue: registers);
+//   * the epilogue never touches the two LDS slots (they hold the next tile's steps): bias /
+//     activation / dGELU / beta run on the accumulators in registers, v_permlane16_swap pairs the
+//     4-column pieces of adjacent 16-column blocks so every lane stores 8 consecutive outputs
+//     (16-B stores, 64 B per row per instruction); the dGELU column sums (bias gradient) reduce
+//     across lanes by shuffles and across the two wave rows through a 1-KB LDS area beside the
+//     slots, one partial row per tile ([tiles_m][N], as gemm_lds_kernel);
+//   * the first K-step of a tile runs its first-half MFMAs with a zero accumulator input (no
+//     accumulator clearing pass).
+// Tile order: workgroup b serves tiles w, w + G, w + 2G, ... with w the XCD-major rank of b, so the
+// workgroups of one XCD always work on a contiguous run of the 8-row-grouped tile order (L2 reuse).
+// Requirements (checked by the host entry): K % 128 == 0 and K >= 256, bf16/f16, no split-K.
+#pragma once
+#include "gemm_core.h"
+
+namespace pra {
+namespace {
+
+template <typename T>
+__device__ __forceinline__ void mma_agpr_z(typename V8<T>::type a, typename V8<T>::type b, f32x4& c);
+template <>
+__device__ __forceinline__ void mma_agpr_z<bf16>(V8<bf16>::type a, V8<bf16>::type b, f32x4& c) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=a"(c) : "v"(a), "v"(b));
+}
+template <>
+__device__ __forceinline__ void mma_agpr_z<f16>(V8<f16>::type a, V8<f16>::type b, f32x4& c) {
+  asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, 0" : "=a"(c) : "v"(a), "v"(b));
+}
+
+template <typename T, typename CF, bool AK, bool BK, int E, bool BETA>
+__global__ __launch_bounds__(CF::NT, 1) void gemm_pts_kernel(const uint16_t* __restrict__ A,
+                                                             const uint16_t* __restrict__ B,
+                                                             const uint16_t* __restrict__ bias,
+                                                             uint16_t* __restrict__ C, uint16_t* __restrict__ Z,
+                                                             float* __restrict__ colsum, int M, int N, int K, int lda,
+                                                             int ldb, int ldc, int ldz) {
+  constexpr int NT = CF::NT, TI = CF::TI, TJ = CF::TJ, NDA = CF::NDA, NDB = CF::NDB, WC = CF::WC;
+  constexpr int BM = CF::BM, BN = CF::BN, IMGA = CF::IMGA, SLOT = CF::SLOT;
+  constexpr int RW = TI * 16, CW = TJ * 16;
+  constexpr bool DG = (E == kDGeluErf || E == kDGeluTanh);
+  constexpr bool AGPR_ACC = CF::WR * CF::WC == 4;
+  static_assert(BM == 256 && BN == 256 && TJ % 2 == 0 && CF::WR == 2, "pts: 256x256 tiles, 2 wave rows");
+  __shared__ __attribute__((aligned(1024))) char lds[2 * SLOT + BN * 4];
+  typedef typename V8<T>::type v8;
+  const uint32_t lds_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)lds;
+
+  const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN, ntiles = tiles_m * tiles_n;
+  const int G = gridDim.x;
+  int pid;
+  {  // XCD-major rank of this workgroup (bijective for any G)
+    const int q = G >> 3, r = G & 7, xcd = blockIdx.x & 7;
+    pid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (blockIdx.x >> 3);
+  }
+  if (pid >= ntiles) return;
+  auto tile_mn = [&](int p, int& tm, int& tn) {
+    const int group = 8 * tiles_n, gi = p / group, first_m = gi * 8;
+    const int gm = min(tiles_m - first_m, 8);
+    tm = first_m + (p % group) % gm;
+    tn = (p % group) / gm;
+  };
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), wr = wave / WC,
+            wc = wave % WC;
+
+  typedef Dma<AK, NT, NDA, CF::BUF, (AK ? 256 : BM), CF::SC1> DmaA;
+  typedef Dma<BK, NT, NDB, CF::BUF, 256, CF::SC1> DmaB;
+  DmaA da;
+  DmaB db;
+  auto dma_init = [&](DmaA& xa, DmaB& xb, int tm, int tn) {
+    const int m0 = tm * BM, n0 = tn * BN;
+    if (AK) xa.init(A, lda, m0, M - 1, tid);
+    else xa.init(A, lda, m0, M - 8, tid);
+    if (BK) xb.init(B, ldb, n0, N - 1, tid);
+    else xb.init(B, ldb, n0, N - 8, tid);
+  };
+  const int nk = K / BKT;  // even, >= 4
+
+  f32x4 acc[TI][TJ];
+  v8 fa0[TI], fb0[TJ], fa1[TI], fb1[TJ];
+
+  int tm, tn;
+  tile_mn(pid, tm, tn);
+  dma_init(da, db, tm, tn);
+  // prologue of the first tile: steps 0 and 1 in flight, step 0's first fragments in registers
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+#pragma unroll
+    for (int n = 0; n < NDA; ++n) da.issue1(lds_base + t * SLOT, wave, t, n);
+#pragma unroll
+    for (int n = 0; n < NDB; ++n) db.issue1(lds_base + t * SLOT + IMGA, wave, t, n);
+  }
+  wait_vmcnt<NDA + NDB>();
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+  {
+    const char* ai = lds;
+    const char* bi = ai + IMGA;
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) fb0[j] = frag<T, BK>(bi, wc * CW + j * 16, 0, lane);
+#pragma unroll
+    for (int i = 0; i < TI; ++i) fa0[i] = frag<T, AK, (AK ? 256 : BM)>(ai, wr * RW + i * 16, 0, lane);
+  }
+
+  // one TS K-step (see gemm_core.h kstep_t); FIRST: the half-0 MFMAs start from a zero
+  // accumulator. Outside STEADY the refill target (this tile's step kt+2, the next tile's step
+  // kt+2-nk, or none) and the next-fragment reads are runtime choices.
+  auto kstep = [&](int kt, auto steady_c, auto first_c, bool dcur, bool dnext, bool rd1)
+      __attribute__((always_inline)) {
+    constexpr bool STEADY = decltype(steady_c)::value, FIRST = decltype(first_c)::value;
+    constexpr int NRD = TI + TJ, NDMA = NDA + NDB, NM = TI * TJ, F = 2 * NM;
+    constexpr int BA = NRD + 4, BB = F - NRD - 3;
+    constexpr int SP = (BB - BA - 1) / NDMA > 0 ? (BB - BA - 1) / NDMA : 1;
+    static_assert(BB >= NM && BA + 1 + (NDMA - 1) * SP < BB, "pts: fillers exceed the K-step's MFMAs");
+    if constexpr (STEADY) {
+      dcur = true;
+      dnext = false;
+      rd1 = true;
+    }
+    const bool dma = dcur || dnext;
+    const uint32_t soA = lds_base + (kt & 1) * SLOT, soB = soA + IMGA;
+    const char* ai = lds + (kt & 1) * SLOT;
+    const char* bi = ai + IMGA;
+    const char* an = lds + ((kt + 1) & 1) * SLOT;
+    const char* bn = an + IMGA;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) {
+          const int f = h * NM + i * TJ + j;
+          if (h == 0) {
+            if constexpr (FIRST) {
+              if constexpr (AGPR_ACC) mma_agpr_z<T>(fb0[j], fa0[i], acc[i][j]);
+              else acc[i][j] = mma<T>(fb0[j], fa0[i], f32x4{0.f, 0.f, 0.f, 0.f});
+            } else {
+              if constexpr (AGPR_ACC) mma_agpr<T>(fb0[j], fa0[i], acc[i][j]);
+              else acc[i][j] = mma<T>(fb0[j], fa0[i], acc[i][j]);
+            }
+          } else {
+            if constexpr (AGPR_ACC) mma_agpr<T>(fb1[j], fa1[i], acc[i][j]);
+            else acc[i][j] = mma<T>(fb1[j], fa1[i], acc[i][j]);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+          if (f < TJ) {
+            fb1[f] = frag<T, BK>(bi, wc * CW + f * 16, 1, lane);
+          } else if (f < NRD) {
+            fa1[f - TJ] = frag<T, AK, (AK ? 256 : BM)>(ai, wr * RW + (f - TJ) * 16, 1, lane);
+          } else if (f == BA) {
+            __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's reads of slot kt done
+            __builtin_amdgcn_s_barrier();        // every wave's
+          } else if (f > BA && f < BB) {
+            const int d = (f - BA - 1) / SP;
+            if (dma && (f - BA - 1) % SP == 0 && d < NDMA) {
+              // (dnext: da / db already describe the next tile)
+              const int st = dnext ? kt + 2 - nk : kt + 2;
+              if (d < NDA) da.issue1(soA, wave, st, d);
+              else db.issue1(soB, wave, st, d - NDA);
+            }
+          } else if (f == BB) {
+            if (dma) wait_vmcnt<NDMA>();  // step kt+1's pieces landed (the refill still in flight)
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();  // ... for every wave
+          } else if (rd1 && f > BB && f - BB - 1 < NRD) {
+            const int r = f - BB - 1;
+            if (r < TJ) fb0[r] = frag<T, BK>(bn, wc * CW + r * 16, 0, lane);
+            else fa0[r - TJ] = frag<T, AK, (AK ? 256 : BM)>(an, wr * RW + (r - TJ) * 16, 0, lane);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+    if constexpr (!STEADY) __builtin_amdgcn_s_waitcnt(0xC07F);
+  };
+
+  float* xlds = reinterpret_cast<float*>(lds + 2 * SLOT);  // [BN] column-sum exchange
+  while (true) {
+    const int npid = pid + G;
+    const bool has_next = npid < ntiles;
+    int ntm = 0, ntn = 0;
+    kstep(0, std::true_type{}, std::true_type{}, true, false, true);
+    for (int kt = 1; kt + 2 < nk; ++kt) kstep(kt, std::true_type{}, std::false_type{}, true, false, true);
+    // this tile's last refill was step nk-1 (issued in step nk-3): the DMA state moves to the next tile
+    if (has_next) {
+      tile_mn(npid, ntm, ntn);
+      dma_init(da, db, ntm, ntn);
+    }
+    kstep(nk - 2, std::false_type{}, std::false_type{}, false, has_next, true);
+    kstep(nk - 1, std::false_type{}, std::false_type{}, false, has_next, false);
+
+    // ---- epilogue from registers: acc[i][j][r] = C[m0 + wr*RW + i*16 + (lane&15)][n0 + wc*CW + j*16 + 4*(lane>>4) + r]
+    if constexpr (AGPR_ACC) asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
+    const int m0 = tm * BM, n0 = tn * BN;
+    const int lrow = lane & 15, g = lane >> 4;
+    const int rb = m0 + wr * RW + lrow;
+    const int cbase = n0 + wc * CW;
+    // after the swap a lane holds 8 consecutive columns of block jp + ((lane >> 4) & 1)
+    const int sw_col = ((lane >> 4) & 1) * 16 + 8 * (lane >> 5);
+    float cs[TJ][4];
+#pragma unroll
+    for (int j = 0; j < TJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) cs[j][r] = 0.f;
+    uint2 bvp[TJ];  // this lane's 4 bias values per block, packed (unpacked where used)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      const int n = cbase + j * 16 + 4 * g;
+      bvp[j] = make_uint2(0u, 0u);
+      if (bias && n < N) bvp[j] = *reinterpret_cast<const uint2*>(bias + n);
+    }
+#pragma unroll
+    for (int i = 0; i < TI; ++i) {
+      const int m = rb + i * 16;
+      const bool mok = m < M;
+      const int64_t mr = mok ? m : 0;
+#pragma unroll
+      for (int jp = 0; jp < TJ; jp += 2) {
+        // this lane's 8-byte operand loads of the pair (dGELU: Z, beta: C)
+        uint2 gz[2];
+        if constexpr (DG || BETA) {
+#pragma unroll
+          for (int u = 0; u < 2; ++u) {
+            const int n = cbase + (jp + u) * 16 + 4 * g;
+            gz[u] = make_uint2(0u, 0u);
+            if (mok && n < N)
+              gz[u] = DG ? *reinterpret_cast<const uint2*>(Z + mr * ldz + n)
+                         : *reinterpret_cast<const uint2*>(C + mr * ldc + n);
+          }
+        }
+        uint32_t pc[2][2], pz[2][2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int j = jp + u;
+          float v[4] = {acc[i][j][0] + to_f<T>(bvp[j].x & 0xffff), acc[i][j][1] + to_f<T>(bvp[j].x >> 16),
+                        acc[i][j][2] + to_f<T>(bvp[j].y & 0xffff), acc[i][j][3] + to_f<T>(bvp[j].y >> 16)};
+          if constexpr (DG) {
+            const float z[4] = {to_f<T>(gz[u].x & 0xffff), to_f<T>(gz[u].x >> 16), to_f<T>(gz[u].y & 0xffff),
+                                to_f<T>(gz[u].y >> 16)};
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] *= (E == kDGeluErf) ? dgelu_erf(z[r]) : dgelu_tanh(z[r]);
+          } else if constexpr (E != kNone) {
+            pz[u][0] = pack2<T>(v[0], v[1]);
+            pz[u][1] = pack2<T>(v[2], v[3]);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = act<E>(v[r]);
+          }
+          if constexpr (BETA && !DG) {
+            v[0] += to_f<T>(gz[u].x & 0xffff);
+            v[1] += to_f<T>(gz[u].x >> 16);
+            v[2] += to_f<T>(gz[u].y & 0xffff);
+            v[3] += to_f<T>(gz[u].y >> 16);
+          }
+          pc[u][0] = pack2<T>(v[0], v[1]);
+          pc[u][1] = pack2<T>(v[2], v[3]);
+          if (DG && colsum && mok) {
+            cs[j][0] += to_f<T>(pc[u][0] & 0xffff);
+            cs[j][1] += to_f<T>(pc[u][0] >> 16);
+            cs[j][2] += to_f<T>(pc[u][1] & 0xffff);
+            cs[j][3] += to_f<T>(pc[u][1] >> 16);
+          }
+        }
+        // rows 1 and 3 (lanes 16-31, 48-63) take block jp+1's first 4 columns from rows 0 / 2,
+        // which take block jp's last 4 columns: every lane then holds 8 consecutive columns
+        const int nc = cbase + jp * 16 + sw_col;
+        {
+          auto r0 = __builtin_amdgcn_permlane16_swap(pc[0][0], pc[1][0], false, false);
+          auto r1 = __builtin_amdgcn_permlane16_swap(pc[0][1], pc[1][1], false, false);
+          if (mok && nc < N)
+            *reinterpret_cast<uint4*>(C + mr * ldc + nc) = make_uint4(r0[0], r1[0], r0[1], r1[1]);
+        }
+        if constexpr (!DG && E != kNone) {
+          if (Z) {
+            auto r0 = __builtin_amdgcn_permlane16_swap(pz[0][0], pz[1][0], false, false);
+            auto r1 = __builtin_amdgcn_permlane16_swap(pz[0][1], pz[1][1], false, false);
+            if (mok && nc < N)
+              *reinterpret_cast<uint4*>(Z + mr * ldz + nc) = make_uint4(r0[0], r1[0], r0[1], r1[1]);
+          }
+        }
+      }
+    }
+    if constexpr (DG) {
+      if (colsum) {
+        // lanes with equal lane >> 4 own the same 4 columns of each block: reduce over lane & 15,
+        // then wave row 1 hands its sums to wave row 0 through LDS
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1)
+#pragma unroll
+          for (int j = 0; j < TJ; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) cs[j][r] += __shfl_xor(cs[j][r], o, 64);
+        if (wr == 1 && lrow == 0) {
+#pragma unroll
+          for (int j = 0; j < TJ; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) xlds[wc * CW + j * 16 + 4 * g + r] = cs[j][r];
+        }
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        __builtin_amdgcn_s_barrier();
+        if (wr == 0 && lrow == 0) {
+#pragma unroll
+          for (int j = 0; j < TJ; ++j) {
+            const int n = cbase + j * 16 + 4 * g;
+            if (n < N) {
+#pragma unroll
+              for (int r = 0; r < 4; ++r)
+                colsum[(int64_t)tm * N + n + r] = cs[j][r] + xlds[wc * CW + j * 16 + 4 * g + r];
+            }
+          }
+        }
+      }
+    }
+    if (!has_next) break;
+    // the next tile's step 0 landed in slot 0 before the last K-step's second barrier: its first
+    // fragments are read only now, so they do not occupy registers through the epilogue
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) fb0[j] = frag<T, BK>(lds + IMGA, wc * CW + j * 16, 0, lane);
+#pragma unroll
+    for (int i = 0; i < TI; ++i) fa0[i] = frag<T, AK, (AK ? 256 : BM)>(lds, wr * RW + i * 16, 0, lane);
+    pid = npid;
+    tm = ntm;
+    tn = ntn;
+  }
+}
+
+}  // namespace
+}  // namespace pra

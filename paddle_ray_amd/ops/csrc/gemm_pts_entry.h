@@ -1,0 +1,66 @@
+// Launch side of the persistent TS GEMM (gemm_pts.h): one translation unit per wave configuration.
+#pragma once
+#include "gemm_pts.h"
+
+namespace pra {
+namespace {
+using W4T = WCfg<2, 2, 256, 256, true, false, false, true>;
+using W8T = WCfg<2, 4, 256, 256, true, false, false, true>;
+
+int num_cus() {
+  static int n = 0;
+  if (!n) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+  }
+  return n;
+}
+
+template <typename CF, typename T, bool AK, bool BK, int E, bool BETA>
+void launch_pts(const void* A, const void* B, const void* bias, void* C, void* Z, float* colsum, int M, int N, int K,
+                int lda, int ldb, int ldc, int ldz, hipStream_t s) {
+  const int tiles = ((M + 255) / 256) * ((N + 255) / 256);
+  const int grid = tiles < num_cus() ? tiles : num_cus();
+  gemm_pts_kernel<T, CF, AK, BK, E, BETA><<<grid, CF::NT, 0, s>>>(
+      static_cast<const uint16_t*>(A), static_cast<const uint16_t*>(B), static_cast<const uint16_t*>(bias),
+      static_cast<uint16_t*>(C), static_cast<uint16_t*>(Z), colsum, M, N, K, lda, ldb, ldc, ldz);
+}
+
+template <typename CF, typename T, bool AK, bool BK>
+int launch_pts_e(const void* A, const void* B, const void* bias, void* C, void* Z, float* colsum, int M, int N, int K,
+                 int lda, int ldb, int ldc, int ldz, int epi, int beta, hipStream_t s) {
+  if (beta && epi != kNone) return -1;
+  switch (epi) {
+    case kNone:
+      if (beta) launch_pts<CF, T, AK, BK, kNone, true>(A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, s);
+      else launch_pts<CF, T, AK, BK, kNone, false>(A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, s);
+      return 0;
+    case kGeluErf: launch_pts<CF, T, AK, BK, kGeluErf, false>(A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, s); return 0;
+    case kGeluTanh: launch_pts<CF, T, AK, BK, kGeluTanh, false>(A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, s); return 0;
+    case kDGeluErf: launch_pts<CF, T, AK, BK, kDGeluErf, false>(A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, s); return 0;
+    case kDGeluTanh: launch_pts<CF, T, AK, BK, kDGeluTanh, false>(A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, s); return 0;
+    default: return -1;  // ReLU: the per-tile kernel
+  }
+}
+}  // namespace
+}  // namespace pra
+
+// Entry (same contract as pra_gemm_lds with splits = 1, bf16 only). Returns -1 (nothing launched)
+// outside what the persistent kernel assumes: K % 128 != 0 or K < 256, beta with an activation,
+// a layout this configuration is not built for (LAYOUTS bit mask).
+#define PRA_GEMM_PTS_ENTRY(NAME, CFG, LAYOUTS)                                                              \
+  extern "C" int NAME(int layout, const void* A, const void* B, const void* bias, void* C, void* Z,            \
+                      float* colsum, int M, int N, int K, int lda, int ldb, int ldc, int ldz, int dtype,       \
+                      int epi, int beta, hipStream_t s) {                                                      \
+    if (dtype != pra::kBF16 || (K % 128) || K < 256 || !((LAYOUTS >> layout) & 1)) return -1;                 \
+    switch (layout) {                                                                                          \
+      case 0: if constexpr (LAYOUTS & 1) return pra::launch_pts_e<CFG, pra::bf16, true, false>(A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, epi, beta, s); \
+              return -1;                                                                                       \
+      case 1: if constexpr ((LAYOUTS >> 1) & 1) return pra::launch_pts_e<CFG, pra::bf16, true, true>(A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, epi, beta, s); \
+              return -1;                                                                                       \
+      case 2: if constexpr ((LAYOUTS >> 2) & 1) return pra::launch_pts_e<CFG, pra::bf16, false, false>(A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, epi, beta, s); \
+              return -1;                                                                                       \
+      default: return -1;                                                                                      \
+    }                                                                                                          \
+  }

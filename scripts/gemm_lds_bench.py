@@ -86,40 +86,47 @@ def timeit(fn, iters):
 
 
 def main_w4():
-    """Kernel configurations vs hipBLASLt, interleaved in one process: W8 (8 waves, burst
-    schedule), W4 (4 waves x 128x128, one filler per MFMA), W8I (8 waves, one filler per MFMA)."""
+    """Kernel configurations vs hipBLASLt, interleaved in one process. A configuration is
+    (name, alt-config mask for pra_gemm_set_w4, persistent-kernel mask for pra_gemm_set_pts)."""
     dev = torch.device('cuda')
-    cfgs = [('W8', 0), ('W4', 7), ('W8I', 7 << 4), ('W4B', 7 << 8), ('W8B', 7 << 12), ('W4P', 7 << 16),
-            ('W8P', 7 << 20), ('W4T', 7 << 24), ('W8T', 7 << 28)]
+    cfgs = [('W8', 0, 0), ('W4', 7, 0), ('W8I', 7 << 4, 0), ('W4B', 7 << 8, 0), ('W8B', 7 << 12, 0),
+            ('W4P', 7 << 16, 0), ('W8P', 7 << 20, 0), ('W4T', 7 << 24, 0), ('W8T', 7 << 28, 0)]
     if '--ts' in sys.argv:  # the TS schedule against the default configurations only
-        cfgs = [('W8', 0), ('W4', 7), ('W4T', 7 << 24), ('W8T', 7 << 28)]
-    hdr = ' | '.join(f'err {n}' for n, _ in cfgs) + ' | ' + ' | '.join(f'{n} us' for n, _ in cfgs)
+        cfgs = [('W8', 0, 0), ('W4', 7, 0), ('W4T', 7 << 24, 0), ('W8T', 7 << 28, 0)]
+    if '--pts' in sys.argv:  # persistent TS kernel vs per-tile TS (default alt mask) vs the W8 baseline
+        ts = (1 << 28) | (1 << 25) | (1 << 30)
+        cfgs = [('W8', 0, 0), ('TS', ts, 0), ('PTS', ts, 7), ('PTS8', ts, 7 | 16)]
+    hdr = ' | '.join(f'err {c[0]}' for c in cfgs) + ' | ' + ' | '.join(f'{c[0]} us' for c in cfgs)
     print(f"| GEMM | layout | M | N | K | {hdr} | hipBLASLt us | best | best PF/s | best vs hipBLASLt |")
     print("|---|---|---|---|---|" + "---|" * (2 * len(cfgs) + 4), flush=True)
     tot = [0.0] * (len(cfgs) + 1)
+
+    def setc(c):
+        L.gemm_set_w4(c[1])
+        L.gemm_set_pts(c[2])
     for name, layout, M, N, K in SHAPES:
         errs = []
-        for _, mask in cfgs:
-            L.gemm_set_w4(mask)
+        for c in cfgs:
+            setc(c)
             errs.append(check(name, layout, M, N, K, dev))
         a, b = operands(layout, M, N, K, dev)
-        c = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        c_out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
 
-        def mk(mask):
+        def mk(cf):
             def f():
-                L.gemm_set_w4(mask)
-                ours(layout, a, b, c, M, N, K)
+                setc(cf)
+                ours(layout, a, b, c_out, M, N, K)
             return f
-        fs = [mk(mask) for _, mask in cfgs] + [lambda: ref_mm(layout, a, b)]
+        fs = [mk(c) for c in cfgs] + [lambda: ref_mm(layout, a, b)]
         for f in fs:
             f()
         torch.cuda.synchronize()
         it = 5 if M * N * K > 1e12 else 20
-        ts = [[] for _ in fs]
+        ts_ = [[] for _ in fs]
         for _ in range(5):
             for i, f in enumerate(fs):
-                ts[i].append(timeit(f, it))
-        m = [statistics.median(t) for t in ts]
+                ts_[i].append(timeit(f, it))
+        m = [statistics.median(t) for t in ts_]
         for i in range(len(fs)):
             tot[i] += m[i]
         fl = 2.0 * M * N * K
@@ -127,7 +134,7 @@ def main_w4():
         print(f"| {name} | {layout} | {M} | {N} | {K} | " + ' | '.join(f'{e:.1e}' for e in errs) + ' | '
               + ' | '.join(f'{x * 1e3:.1f}' for x in m[:-1]) + f" | {m[-1] * 1e3:.1f} | {cfgs[bi][0]} | "
               f"{fl / m[bi] / 1e12:.3f} | {m[-1] / m[bi]:.3f} |", flush=True)
-    print('\ntotal ' + ', '.join(f'{n} {t:.3f} ms' for (n, _), t in zip(cfgs, tot)) + f', hipBLASLt {tot[-1]:.3f} ms')
+    print('\ntotal ' + ', '.join(f'{c[0]} {t:.3f} ms' for c, t in zip(cfgs, tot)) + f', hipBLASLt {tot[-1]:.3f} ms')
     L.gemm_set_w4(0)
 
 

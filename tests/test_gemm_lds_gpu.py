@@ -11,20 +11,28 @@ from paddle_ray_amd.ops import registry as R
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(autouse=True, params=[0, 7, 7 << 4, 7 << 8, 7 << 12, 7 << 16, 7 << 20],
-                ids=['W8', 'W4', 'W8I', 'W4B', 'W8B', 'W4P', 'W8P'])
+_TS = (1 << 28) | (1 << 25) | (1 << 30)   # per-tile TS schedule: W8T for x·W / xᵀ·dy, W4T for dy·Wᵀ
+
+
+@pytest.fixture(autouse=True, params=[(0, 0), (7, 0), (7 << 4, 0), (7 << 8, 0), (7 << 12, 0), (7 << 16, 0),
+                                      (7 << 20, 0), (_TS, 0), (_TS, 7), (_TS, 7 | 16)],
+                ids=['W8', 'W4', 'W8I', 'W4B', 'W8B', 'W4P', 'W8P', 'TS', 'PTS', 'PTS8'])
 def _mfma_everywhere(request):
     """Exercise the in-tree kernel on every layout regardless of the 'auto' policy, in each
     wave configuration (gemm_set_w4 mask: 0 = 8 waves, 7 = 4 waves x 128x128, 7<<4 = 8 waves
     with the one-filler-per-MFMA schedule, 7<<8 / 7<<12 = W4 / W8 with MUBUF operand DMA,
-    7<<16 / 7<<20 = W4 / W8 with the two-barrier early-refill schedule)."""
+    7<<16 / 7<<20 = W4 / W8 with the two-barrier early-refill schedule, TS = the default TS
+    schedule) and with the persistent TS kernel (gemm_set_pts: 7 = every layout, +16 = 8 waves
+    for dy·Wᵀ too)."""
     from paddle_ray_amd.ops import _native
     L = _native.lib()
-    prev, prev_mask = K._GEMM_MODE, L.gemm_get_w4()
+    prev, prev_mask, prev_pts = K._GEMM_MODE, L.gemm_get_w4(), L.gemm_get_pts()
     K._GEMM_MODE = 'mfma'
-    L.gemm_set_w4(request.param)
+    L.gemm_set_w4(request.param[0])
+    L.gemm_set_pts(request.param[1])
     yield
     L.gemm_set_w4(prev_mask)
+    L.gemm_set_pts(prev_pts)
     K._GEMM_MODE = prev
 
 
@@ -183,3 +191,38 @@ def test_mlp_gelu_fused(approx, mode):
     K.mlp_gelu(x, w1, b1, w2, approx).backward(gy)
     for got, ref in ((w1.grad, w1f.grad), (b1.grad, b1f.grad), (w2.grad, w2f.grad)):
         _close(got, 2 * ref, tol=3e-2)
+
+
+@pytest.mark.parametrize('layout', [0, 1, 2])
+def test_many_tiles_per_workgroup(layout):
+    """More 256x256 tiles than CUs (17 x 18 = 306 > 256): the persistent kernel's workgroups walk
+    two tiles, refilling the next tile's operands under the epilogue; ragged last row / column."""
+    torch.manual_seed(7)
+    M, N, Kd = 4168, 4360, 384
+    a, b = _operands(layout, M, N, Kd)
+    ref = _ref(layout, a, b)
+    _close(K._gemm_hip(layout, a, b), ref)
+    c0 = _r(M, N)
+    c = c0.clone()
+    K._gemm_hip(layout, a, b, out=c, beta=1)
+    _close(c, ref + c0.float())
+
+
+def test_many_tiles_epilogues():
+    """bias + GELU with the pre-activation, and dGELU + column sums, over 306 tiles."""
+    torch.manual_seed(8)
+    M, N, Kd = 4168, 4360, 256
+    a, b = _operands(0, M, N, Kd)
+    bias = _r(N)
+    z = torch.empty(M, N, device='cuda', dtype=torch.bfloat16)
+    y = K._gemm_hip(0, a, b, bias=bias, z=z, epi='gelu_tanh')
+    pre = _ref(0, a, b) + bias.float()
+    _close(z, pre)
+    _close(y, torch.nn.functional.gelu(pre, approximate='tanh'))
+    dy, w = _r(M, Kd), _r(N, Kd)
+    zz = _r(M, N, scale=3.0)
+    out, cs = K._gemm_hip(1, dy, w, z=zz, epi='dgelu', want_colsum=True)
+    zf = zz.float().requires_grad_(True)
+    ref, = torch.autograd.grad(torch.nn.functional.gelu(zf), zf, _ref(1, dy, w))
+    _close(out, ref)
+    _close(cs, out.float().sum(0), tol=1e-3)
