@@ -1803,7 +1803,7 @@ class LinearFn(torch.autograd.Function):
         dx = gemm(GEMM_NT, dy2, w).view(x.shape) if ctx.needs_input_grad[0] else None
         dw = None
         if ctx.needs_input_grad[1]:
-            g = w.grad
+            g = w.grad if w.is_leaf else None
             if _acc_grad_ok(g, w, dy2.dtype):
                 # returning None still runs W's AccumulateGrad node, which fires its
                 # post-accumulate hooks after this in-place accumulation
@@ -1846,8 +1846,11 @@ def linear(x, w, b=None):
     """[.., in] @ [in, out] (+ b) with fused dW accumulation (see LinearFn)."""
     if b is not None and b.dtype != x.dtype and torch.is_autocast_enabled(x.device.type):
         b = b.to(x.dtype)
-    if w.requires_grad and torch.is_grad_enabled() and w.is_leaf and x.dtype == w.dtype and \
-            _no_autocast_change(x, w):
+    if torch.is_grad_enabled() and (x.requires_grad or w.requires_grad or (b is not None and b.requires_grad)) \
+            and x.dtype == w.dtype and _no_autocast_change(x, w):
+        # any operand that needs a gradient goes through the autograd Function (a frozen
+        # weight with a trainable input, or a non-leaf weight, included: the raw GEMM below
+        # records no graph)
         return LinearFn.apply(x, w, b)
     x2 = x.reshape(-1, x.shape[-1])
     if x2.is_cuda and x.dtype == w.dtype and _no_autocast_change(x, w):
@@ -1876,7 +1879,7 @@ class LinearNTFn(torch.autograd.Function):
         dx = gemm(GEMM_FWD, dy, w) if ctx.needs_input_grad[0] else None
         dw = None
         if ctx.needs_input_grad[1]:
-            g = w.grad
+            g = w.grad if w.is_leaf else None
             if _acc_grad_ok(g, w, dy.dtype):
                 gemm(GEMM_TN, dy, x, out=g, beta=1)
             else:
@@ -1886,7 +1889,7 @@ class LinearNTFn(torch.autograd.Function):
 
 def linear_nt(x2, w):
     """[T, in] @ [out, in]^T with fused dW accumulation (see LinearNTFn)."""
-    if w.requires_grad and torch.is_grad_enabled() and w.is_leaf and x2.dtype == w.dtype and \
+    if torch.is_grad_enabled() and (x2.requires_grad or w.requires_grad) and x2.dtype == w.dtype and \
             _no_autocast_change(x2, w):
         return LinearNTFn.apply(x2, w)
     if x2.is_cuda and x2.dtype == w.dtype:

@@ -1,8 +1,12 @@
 """Linear algebra (parity: python/paddle/tensor/linalg.py, python/paddle/linalg.py).
 
-``matmul`` is the framework GEMM entry: it goes through the kernel registry
-(``ops.registry``) so bf16/fp16 GEMMs on the HIP device land on hipBLASLt and
-fused-epilogue variants on our MFMA kernels.
+``matmul`` / ``mm`` with a 2-D right operand in bf16/fp16 on the device run the framework GEMM
+(``ops.fused.linear`` / ``linear_nt``: the in-tree MFMA kernel through the registry, hipBLASLt
+where the shape policy prefers it, autograd through LinearFn / LinearNTFn); batched products and
+the factorisations / solvers (inv, det, svd, qr, lu, cholesky, eig*, lstsq, ...) are the
+rocSOLVER / hipBLAS-backed torch.linalg routines with Paddle's argument and return conventions
+(``slogdet`` stacked [sign, logabsdet], 1-based int32 LU pivots, ``triangular_solve`` transpose
+flag, ``norm`` p / axis combinations).
 """
 import torch
 
@@ -14,9 +18,20 @@ def _t(x):
     return x._t if isinstance(x, Tensor) else torch.as_tensor(x)
 
 
+def _gemm_ok(a, b):
+    return (a.is_cuda and b.is_cuda and a.dtype == b.dtype and a.dtype in (torch.bfloat16, torch.float16)
+            and a.dim() >= 2 and b.dim() == 2)
+
+
 @_amp_op('matmul')
 def matmul(x, y, transpose_x=False, transpose_y=False, name=None):
     a, b = _t(x), _t(y)
+    if not transpose_x and _gemm_ok(a, b):
+        from ..ops import fused as _K
+        if transpose_y:
+            y2 = _K.linear_nt(a.reshape(-1, a.shape[-1]), b)
+            return Tensor(y2.view(*a.shape[:-1], b.shape[0]))
+        return Tensor(_K.linear(a, b))
     if transpose_x:
         a = a.transpose(-1, -2) if a.dim() > 1 else a
     if transpose_y:
@@ -26,7 +41,7 @@ def matmul(x, y, transpose_x=False, transpose_y=False, name=None):
 
 @_amp_op('mm')
 def mm(input, mat2, name=None):
-    return Tensor(torch.matmul(_t(input), _t(mat2)))
+    return matmul(input, mat2)
 
 
 @_amp_op('bmm')

@@ -487,3 +487,51 @@ def test_flash_attention_dq_paths_agree(causal, Sq, Sk, D, monkeypatch):
     torch.testing.assert_close(a[2], b[2], atol=0, rtol=0)
     torch.testing.assert_close(a[1].float(), b[1].float(), atol=2e-2, rtol=2e-2)
     torch.testing.assert_close(a[0].float(), b[0].float(), atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('case', ['frozen_w', 'nonleaf_w'])
+def test_linear_grads_frozen_or_nonleaf_weight(case):
+    """A frozen weight with a trainable input, and a non-leaf (computed) weight, still get
+    correct gradients through the fused linear / linear_nt paths."""
+    from paddle_ray_amd.ops import fused as K
+    torch.manual_seed(11)
+    x = torch.randn(64, 128, device='cuda', dtype=torch.bfloat16, requires_grad=True)
+    w0 = torch.randn(128, 256, device='cuda', dtype=torch.bfloat16, requires_grad=(case == 'nonleaf_w'))
+    w = w0 * 2 if case == 'nonleaf_w' else w0
+    gy = torch.randn(64, 256, device='cuda', dtype=torch.bfloat16)
+    K.linear(x, w).backward(gy)
+    xf = x.detach().float().requires_grad_(True)
+    wf = w0.detach().float().requires_grad_(True)
+    (xf @ (wf * 2 if case == 'nonleaf_w' else wf)).backward(gy.float())
+    torch.testing.assert_close(x.grad.float(), xf.grad, atol=0.5, rtol=3e-2)
+    if case == 'nonleaf_w':
+        torch.testing.assert_close(w0.grad.float(), wf.grad, atol=1.0, rtol=3e-2)
+    x.grad = None
+    e = torch.randn(256, 128, device='cuda', dtype=torch.bfloat16)   # frozen tied embedding
+    K.linear_nt(x, e).backward(gy)
+    torch.testing.assert_close(x.grad.float(), gy.float() @ e.float(), atol=0.5, rtol=3e-2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('ty', [False, True])
+def test_paddle_matmul_device_gemm(ty):
+    """paddle.matmul with a 2-D right operand in bf16 runs the framework GEMM (registry 'gemm'
+    dispatches) with correct values and gradients, transpose_y included."""
+    import paddle_ray_amd as paddle
+    torch.manual_seed(12)
+    a = torch.randn(4, 64, 128, device='cuda', dtype=torch.bfloat16, requires_grad=True)
+    b = torch.randn(256, 128, device='cuda', dtype=torch.bfloat16) if ty else \
+        torch.randn(128, 256, device='cuda', dtype=torch.bfloat16)
+    b.requires_grad_(True)
+    R.reset_stats()
+    y = paddle.matmul(paddle.Tensor(a), paddle.Tensor(b), transpose_y=ty)._t
+    assert sum(v for (op, _), v in R.stats().items() if op == 'gemm') >= 1
+    gy = torch.randn_like(y)
+    y.backward(gy)
+    af, bf = a.detach().float().requires_grad_(True), b.detach().float().requires_grad_(True)
+    yf = af @ (bf.t() if ty else bf)
+    yf.backward(gy.float())
+    torch.testing.assert_close(y.float(), yf, atol=0.5, rtol=3e-2)
+    torch.testing.assert_close(a.grad.float(), af.grad, atol=0.5, rtol=3e-2)
+    torch.testing.assert_close(b.grad.float(), bf.grad, atol=1.0, rtol=3e-2)
