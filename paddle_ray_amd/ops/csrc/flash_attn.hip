@@ -310,6 +310,27 @@ struct SwzDma {
   }
 };
 
+// One 4-byte-per-lane LDS-DMA: lane l's dword at byte offset voff of the buffer rs lands at LDS
+// byte dst + 4*l (offsets past the descriptor's range read 0). Issued from asm like SwzDma, so the
+// compiler's waitcnt model never sees it: the loops' explicit counted vmcnt are its only waits.
+__device__ __forceinline__ void dma_dword(const u32x4& rs, uint32_t voff, uint32_t dst) {
+  const u32x4 srs = {(uint32_t)__builtin_amdgcn_readfirstlane(rs[0]), (uint32_t)__builtin_amdgcn_readfirstlane(rs[1]),
+                     (uint32_t)__builtin_amdgcn_readfirstlane(rs[2]), (uint32_t)__builtin_amdgcn_readfirstlane(rs[3])};
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dword %0, %1, 0 offen lds" ::"v"(voff), "s"(srs),
+               "s"(__builtin_amdgcn_readfirstlane(dst))
+               : "memory", "m0");
+}
+__device__ __forceinline__ u32x4 raw_desc(const void* base, uint64_t bytes) {
+  const uint64_t bb = (uint64_t)base;
+  return u32x4{(uint32_t)bb, (uint32_t)(bb >> 32) & 0xffffu, (uint32_t)bytes, 0x00020000u};
+}
+// s_waitcnt vmcnt(N), other counters unconstrained
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | 0x70 | 0xF00);
+}
+
 // ============================================================================
 // forward
 // ============================================================================
@@ -841,34 +862,35 @@ bwd_dkdv_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __res
   SwzDma<D, 256> qd, dd;
   qd.init(qb_, qss, Sq, wave, lane);
   dd.init(dob_, HD, Sq, wave, lane);
-  float lreg = 0.f, dreg = 0.f;
-  uint32_t mreg = 0u;
   // EXT + dropout: the forward's keep-bit words of the tile's 64 queries x this block's 4 key
-  // words ([2][4 waves][64] after the dS^T stage), loaded with lse / delta
+  // words ([2][4 waves][64] after the dS^T stage), staged with lse / delta
   const bool dbits = EXT && ext.thr && ext.dbits;
   uint32_t* Mb = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(Dlb + 2 * kTile) + 4 * 32 * 80);
+  const uint32_t mb0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)Mb;
+  const uint32_t lsb0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)Lsb;
+  const uint32_t dlb0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)Dlb;
+  // lse / delta / keep bits of the tile's 64 queries go to LDS by LDS-DMA too (rows >= Sq read 0;
+  // the tail tile masks them): no register-staged loads in the loop, so no compiler-placed
+  // vmcnt(0) ever waits for the Q / dO pieces just issued (it did: the loads' destination
+  // registers are loop-carried, and the waitcnt pass drains everything before rewriting them)
+  const u32x4 lse_rs = raw_desc(lse + (int64_t)bh * SqM, (uint64_t)Sq * 4);
+  const u32x4 dl_rs = raw_desc(delta + (int64_t)bh * SqM, (uint64_t)Sq * 4);
+  const u32x4 mb_rs = dbits ? raw_desc(ext.dbits + (int64_t)bh * SqM * ext.dbits_ld, (uint64_t)Sq * ext.dbits_ld * 4)
+                            : u32x4{0u, 0u, 0u, 0u};
   auto load_tile = [&](int qs0) {
-    const uint32_t img = lds0 + (uint32_t)((2 * (((qs0 - q_begin) / kTile) & 1)) * kTile * D * sizeof(T));
+    const int nb = ((qs0 - q_begin) / kTile) & 1;
+    const uint32_t img = lds0 + (uint32_t)((2 * nb) * kTile * D * sizeof(T));
     qd.issue(img, (uint32_t)((int64_t)qs0 * qss * 2), wave);
     dd.issue(img + kTile * D * sizeof(T), (uint32_t)((int64_t)qs0 * HD * 2), wave);
-    if (threadIdx.x < kTile) {
-      const int qq = qs0 + threadIdx.x;
-      lreg = qq < Sq ? lse[(int64_t)bh * SqM + qq] : INFINITY;  // scaled at store (no wait here)
-      dreg = qq < Sq ? delta[(int64_t)bh * SqM + qq] : 0.f;
-    }
+    if (wave == 0) dma_dword(lse_rs, (uint32_t)(qs0 + lane) * 4u, lsb0 + nb * kTile * 4);
+    if (wave == 1) dma_dword(dl_rs, (uint32_t)(qs0 + lane) * 4u, dlb0 + nb * kTile * 4);
     if (dbits) {
-      const int qq = qs0 + (threadIdx.x & 63), kw = (kblk0 >> 5) + (threadIdx.x >> 6);
-      mreg = qq < Sq && kw < ext.dbits_ld ? ext.dbits[((int64_t)bh * SqM + qq) * ext.dbits_ld + kw] : 0u;
+      const int kw = (kblk0 >> 5) + wave;
+      const uint32_t off = kw < ext.dbits_ld ? (uint32_t)(((int64_t)(qs0 + lane) * ext.dbits_ld + kw) * 4) : 0x80000000u;
+      dma_dword(mb_rs, off, mb0 + (nb * 256 + wave * 64) * 4);
     }
   };
-  auto store_tile = [&](int buf) {
-    if (threadIdx.x < kTile) {
-      Lsb[buf * kTile + threadIdx.x] = lreg * LOG2E;
-      Dlb[buf * kTile + threadIdx.x] = dreg;
-    }
-    if (dbits) Mb[buf * 256 + threadIdx.x] = mreg;
-  };
-  if (ntiles > 0) { load_tile(q_begin); store_tile(0); }
+  if (ntiles > 0) load_tile(q_begin);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
@@ -952,7 +974,8 @@ bwd_dkdv_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __res
         for (int g = 0; g < 4; ++g) {
           const float4 l4 = *reinterpret_cast<const float4*>(Ls + 32 * nt + 8 * g + 4 * h);
           const float4 d4 = *reinterpret_cast<const float4*>(Dl + 32 * nt + 8 * g + 4 * h);
-          const float la[4] = {l4.x, l4.y, l4.z, l4.w}, dl[4] = {d4.x, d4.y, d4.z, d4.w};
+          const float la[4] = {l4.x * LOG2E, l4.y * LOG2E, l4.z * LOG2E, l4.w * LOG2E},
+                      dl[4] = {d4.x, d4.y, d4.z, d4.w};
           uint4 mw = make_uint4(0u, 0u, 0u, 0u);
           if constexpr ((XF & XF_DROP) != 0)
             mw = *reinterpret_cast<const uint4*>(Mb + buf * 256 + wave * 64 + 32 * nt + 8 * g + 4 * h);
@@ -1002,11 +1025,13 @@ bwd_dkdv_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __res
         if constexpr (WDS) flush_ds(qs0 + 32 * nt);
       }
     }
-    // the idle buffer was last read before the previous barrier: its Q/dO DMA was issued at the
-    // top of this tile, lse/delta are written now
-    if (it + 1 < ntiles) store_tile(buf ^ 1);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    // the idle buffer was last read before the previous barrier; its DMA (Q / dO / lse / delta /
+    // keep bits) was issued at the top of this tile. Only the 4 dS^T stores of this tile (WDS) are
+    // younger: leave them in flight.
+    if constexpr (WDS) wait_vm<4>();
+    else wait_vm<0>();
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS reads of the tile are done
+    __builtin_amdgcn_s_barrier();
   };
   // query tiles that straddle the causal diagonal of this 128-key block (the first ones) or
   // Sq (the last one) need the mask; separate loops keep one body copy live at a time

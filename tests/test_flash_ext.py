@@ -330,11 +330,14 @@ def test_transformer_encoder_mask_dropout_on_flash_ext():
     assert R.stats().get(('flash_attn_ext', 'hip'), 0) > 0, R.stats()
     g = paddle.randn(y.shape)
     y.backward(paddle.to_tensor(g.numpy(), place='gpu').astype('bfloat16'))
-    xc = paddle.to_tensor(x.numpy())
+    # the reference runs on the HOST (fp32 dense path, same host-drawn seed -> same keep bits);
+    # on a GPU host the default place is the device, where fp32 would take torch SDPA instead
+    ref.to(device='cpu')
+    xc = paddle.to_tensor(x.numpy(), place='cpu')
     xc.stop_gradient = False
     paddle.seed(77)
-    yr = ref(xc, paddle.to_tensor(mask))
-    yr.backward(g)
+    yr = ref(xc, paddle.to_tensor(mask, place='cpu'))
+    yr.backward(paddle.to_tensor(g.numpy(), place='cpu'))
     yv, yrv = y.astype('float32').numpy(), yr.numpy()
     assert np.abs(yv - yrv).max() / np.abs(yrv).max() < 3e-2
     gx, gxr = xg.grad.astype('float32').numpy(), xc.grad.numpy()
