@@ -2329,7 +2329,7 @@ class BatchNormActFn(torch.autograd.Function):
         acc = None
         b = ctx.b
         if (x2.is_cuda and w is not None and b is not None and ctx.needs_input_grad[2]
-                and ctx.needs_input_grad[3] and _acc_grad_ok(w.grad, w, w.dtype)
+                and ctx.needs_input_grad[3] and w.is_leaf and b.is_leaf and _acc_grad_ok(w.grad, w, w.dtype)
                 and _acc_grad_ok(b.grad, b, w.dtype) and R.select_backend(x2, 'batch_norm_bwd') == 'hip'):
             acc = (w.grad, b.grad)  # scale/shift grads accumulated in the finalize kernel
         if acc is not None:
