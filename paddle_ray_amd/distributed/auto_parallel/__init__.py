@@ -14,6 +14,10 @@ mesh axis (RCCL over xGMI; the gather is autograd-aware, its backward is the loc
 by a local slice. The Engine data-parallelises over mesh axis 0 (the batch axis, as in the
 reference's default DP completion) and all-reduces each gradient over the mesh axes its
 parameter is replicated on, so tensor-parallel (sharded) parameters sync only over DP.
+
+Static programs take the reference's route: in static mode `shard_tensor` only annotates, and
+`parallelize(program)` runs completion + partitioning + reshard (static_passes.py) to produce this
+rank's program with local parameter shards and the collectives the placements imply.
 """
 import copy
 import os
@@ -246,6 +250,12 @@ def shard_tensor(x, process_mesh=None, shard_spec=None):
     mesh = process_mesh or get_current_process_mesh()
     assert mesh is not None, "shard_tensor needs a process_mesh (argument or `with mesh:`)"
     assert isinstance(mesh, ProcessMesh), f"process_mesh {mesh} is not a ProcessMesh"
+    from ...static import _STATIC
+    from ...static.graph import Variable
+    if isinstance(x, Variable) or (_STATIC[0] and isinstance(x, Parameter)):
+        # static program: annotate only; the Partitioner builds this rank's program
+        from .static_passes import annotate
+        return annotate(x, mesh, shard_spec)
     if isinstance(x, np.ndarray):
         x = Tensor(torch.as_tensor(x))
     elif not isinstance(x, Tensor):
@@ -348,3 +358,4 @@ def fetch(tensor, name=None, logging=False):
 
 from .strategy import Strategy  # noqa: E402
 from .engine import Engine  # noqa: E402
+from .static_passes import DistributedContext, Completer, Partitioner, parallelize  # noqa: E402

@@ -1,0 +1,173 @@
+"""Static-mode auto parallel: annotate a serial program, complete, partition per rank
+(parity: reference test/auto_parallel/test_completion.py, test_partitioner.py,
+test_dist_*_reshard). The partitioned programs must compute the serial loss and, after one
+optimizer step, hold exactly the slices of the serially updated parameters."""
+import numpy as np
+import pytest
+
+from dist_utils import run_ranks
+
+pytestmark = pytest.mark.timeout(300) if hasattr(pytest.mark, 'timeout') else []
+
+B, H, F_, C = 8, 6, 8, 4
+
+
+def _build(specs, mesh):
+    """Serial MLP + cross-entropy, annotated with `specs` (None = leave replicated)."""
+    import paddle_ray_amd as paddle
+    import paddle_ray_amd.nn as nn
+    import paddle_ray_amd.nn.functional as F
+    from paddle_ray_amd import static
+    from paddle_ray_amd.distributed import auto_parallel as ap
+    paddle.seed(7)
+    main = static.Program()
+    with static.program_guard(main):
+        x = static.data('x', [B, H], 'float32')
+        y = static.data('y', [B, 1], 'int64')
+        l1, l2 = nn.Linear(H, F_), nn.Linear(F_, C)
+        for t, key in ((x, 'x'), (y, 'y'), (l1.weight, 'w1'), (l1.bias, 'b1'), (l2.weight, 'w2')):
+            if specs.get(key) is not None:
+                ap.shard_tensor(t, mesh, specs[key])
+        h = F.gelu(l1(x))
+        loss = F.cross_entropy(l2(h), y)
+    return main, x, y, h, loss, (l1.weight, l1.bias, l2.weight, l2.bias)
+
+
+def _data():
+    rs = np.random.RandomState(3)
+    return rs.randn(B, H).astype('float32'), rs.randint(0, C, (B, 1)).astype('int64')
+
+
+def _slice(a, mapping, mesh_shape, coord):
+    for i, d in enumerate(mapping):
+        if d >= 0:
+            n = a.shape[i] // mesh_shape[d]
+            a = np.take(a, range(coord[d] * n, (coord[d] + 1) * n), axis=i)
+    return a
+
+
+def _run(rank, world, mesh_ids, names, specs):
+    import paddle_ray_amd as paddle
+    from paddle_ray_amd import static
+    from paddle_ray_amd.distributed import auto_parallel as ap
+    paddle.enable_static()
+    mesh = ap.ProcessMesh(mesh_ids, names)
+    main, x, y, h, loss, params = _build(specs, mesh)
+    dist, vmap, part = ap.parallelize(main)
+    local = [part.local_param(p) for p in params]
+    with static.program_guard(dist):
+        paddle.optimizer.SGD(0.5, parameters=local).minimize(vmap[loss])
+    with static.program_guard(main):
+        paddle.optimizer.SGD(0.5, parameters=list(params)).minimize(loss)
+    exe = static.Executor()
+    xv, yv = _data()
+    ref_loss, = exe.run(main, feed={'x': xv, 'y': yv}, fetch_list=[loss])
+    d_loss, = exe.run(dist, feed={'x': xv, 'y': yv}, fetch_list=[vmap[loss]])
+    coord = mesh.coord()
+    errs = []
+    for p, lp in zip(params, local):
+        want = _slice(p.numpy(), part.ctx.get(p), mesh.shape, coord)
+        got = lp.numpy()
+        assert got.shape == want.shape, (got.shape, want.shape)
+        errs.append(float(np.abs(got - want).max()))
+    mapping = {'h': part.ctx.get(h), 'w2': part.ctx.get(params[2])}
+    comm = [op.type for op in dist.global_block().ops
+            if op.role == 'forward' and op.type.startswith('ap_')]
+    paddle.disable_static()
+    return {'ref': float(ref_loss), 'loss': float(d_loss), 'errs': errs, 'map': mapping,
+            'comm': comm, 'shapes': [list(lp.shape) for lp in local]}
+
+
+def test_completion_rules_single_process():
+    import paddle_ray_amd as paddle
+    from paddle_ray_amd.distributed import auto_parallel as ap
+    paddle.enable_static()
+    try:
+        mesh = ap.ProcessMesh([[0, 1], [2, 3]], ['dp', 'mp'])
+        main, x, y, h, loss, (w1, b1, w2, b2) = _build(
+            {'x': ['dp', None], 'w1': [None, 'mp'], 'b1': ['mp'], 'w2': ['mp', None]}, mesh)
+        ctx = ap.DistributedContext(main)
+        ap.Completer(ctx).complete_forward_annotation()
+        assert ctx.shard_spec(h) == ['dp', 'mp']          # batch from x, column from w1
+        assert ctx.get(loss) == []
+        plans = {op.type.rsplit(':', 1)[-1]: (req, outs, partial) for op, req, outs, partial in ctx.plans}
+        req, outs, partial = plans['cross_entropy']
+        assert outs == [[]] and partial == {0: 'avg'}      # mean over the dp-split batch
+        lin2 = [p for p in ctx.plans if p[0].type.endswith(':linear')][1]
+        assert lin2[2] == [[0, -1]] and lin2[3] == {1: 'sum'}   # row-parallel: partial over mp
+    finally:
+        paddle.disable_static()
+
+
+@pytest.mark.parametrize('kind', ['tp', 'dp'])
+def test_partitioned_step_matches_serial_2ranks(tmp_path, kind):
+    specs = {'tp': {'w1': [None, 'x'], 'b1': ['x'], 'w2': ['x', None]},
+             'dp': {'x': ['x', None], 'y': ['x', None]}}[kind]
+    res = run_ranks(_run, 2, tmp_path, args=([0, 1], ['x'], specs))
+    for o in res:
+        assert abs(o['loss'] - o['ref']) < 1e-5, o
+        assert max(o['errs']) < 1e-5, o
+    if kind == 'tp':
+        assert res[0]['shapes'][0] == [H, F_ // 2] and res[0]['shapes'][2] == [F_ // 2, C]
+        # Megatron MLP on a data input (no grad): one forward all-reduce after the
+        # row-parallel matmul and nothing else
+        assert res[0]['comm'] == ['ap_allreduce'], res[0]['comm']
+        assert res[0]['map']['h'] == [-1, 0]
+    else:
+        assert res[0]['shapes'][0] == [H, F_]
+        assert set(res[0]['comm']) == {'ap_slice', 'ap_identity', 'ap_allreduce'}, res[0]['comm']
+
+
+def test_partitioned_step_hybrid_2x2(tmp_path):
+    specs = {'x': ['dp', None], 'y': ['dp', None], 'w1': [None, 'mp'], 'b1': ['mp'],
+             'w2': ['mp', None]}
+    res = run_ranks(_run, 4, tmp_path, args=([[0, 1], [2, 3]], ['dp', 'mp'], specs))
+    for o in res:
+        assert abs(o['loss'] - o['ref']) < 1e-5, o
+        assert max(o['errs']) < 1e-5, o
+        assert o['map']['h'] == [0, 1]
+
+
+def _run_reshard(rank, world):
+    """Column-parallel layer on an activation, then a softmax that needs the whole row:
+    the partitioner inserts identity (bwd all-reduce) on the activation and an all-gather
+    before the softmax."""
+    import paddle_ray_amd as paddle
+    import paddle_ray_amd.nn as nn
+    import paddle_ray_amd.nn.functional as F
+    from paddle_ray_amd import static
+    from paddle_ray_amd.distributed import auto_parallel as ap
+    paddle.enable_static()
+    paddle.seed(11)
+    mesh = ap.ProcessMesh([0, 1], ['mp'])
+    main = static.Program()
+    with static.program_guard(main):
+        x = static.data('x', [B, H], 'float32')
+        l0, l1, l2 = nn.Linear(H, H), nn.Linear(H, F_), nn.Linear(F_, C)
+        ap.shard_tensor(l1.weight, mesh, [None, 'mp'])
+        s = F.softmax(l1(F.relu(l0(x))), axis=-1)
+        loss = paddle.mean(paddle.sum(l2(s) * l2(s), axis=-1))
+    params = [l0.weight, l0.bias, l1.weight, l1.bias, l2.weight, l2.bias]
+    dist, vmap, part = ap.parallelize(main)
+    local = [part.local_param(p) for p in params]
+    with static.program_guard(dist):
+        paddle.optimizer.SGD(0.5, parameters=local).minimize(vmap[loss])
+    with static.program_guard(main):
+        paddle.optimizer.SGD(0.5, parameters=params).minimize(loss)
+    exe = static.Executor()
+    xv = _data()[0]
+    ref, = exe.run(main, feed={'x': xv}, fetch_list=[loss])
+    got, = exe.run(dist, feed={'x': xv}, fetch_list=[vmap[loss]])
+    errs = [float(np.abs(lp.numpy() - _slice(p.numpy(), part.ctx.get(p), mesh.shape, mesh.coord())).max())
+            for p, lp in zip(params, local)]
+    comm = [op.type for op in dist.global_block().ops
+            if op.role == 'forward' and op.type.startswith('ap_')]
+    paddle.disable_static()
+    return {'ref': float(ref), 'loss': float(got), 'errs': errs, 'comm': comm}
+
+
+def test_partitioner_reshard_before_softmax(tmp_path):
+    for o in run_ranks(_run_reshard, 2, tmp_path):
+        assert abs(o['loss'] - o['ref']) < 1e-5, o
+        assert max(o['errs']) < 1e-5, o
+        assert o['comm'] == ['ap_identity', 'ap_gather'], o['comm']
