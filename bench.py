@@ -385,6 +385,8 @@ def bench_bert(a, paddle, torch, dist, C, world, rank, dev):
         last[0] = exe.run(prog, feed=feed, fetch_list=[loss_v], return_numpy=False)[0]
 
     dt = _timed(step, a, torch, dist, world, dev)
+    if a.profile_dir:
+        _op_profile(step, a, torch, rank)   # per-op tables need --no-graph (a graph replay is one op)
     paddle.disable_static()
     sps = bs * world * a.steps / dt
     return {"metric": "samples/sec BERT-base static+AMP", "value": round(sps, 2),

@@ -54,6 +54,10 @@ namespace {
 // configuration (bit 4 of the mask switches it to 8 waves), x·W and xᵀ·dy the 8-wave one.
 // PRA_GEMM_PTS at first use (default 0 until measured; 7: every layout), pra_gemm_set_pts afterwards.
 int g_pts_mask = -1;
+// per call: epi bit 8 (kPersistBit) asks for the persistent kernel regardless of the mask (the
+// framework's shape policy picks it for short-K dy·Wᵀ, where it measured ahead of hipBLASLt)
+constexpr int kPersistBit = 256;
+thread_local bool g_force_pts = false;
 int pts_mask() {
   if (g_pts_mask < 0) {
     const char* e = getenv("PRA_GEMM_PTS");
@@ -133,7 +137,7 @@ void launch_e(const void* A, const void* B, const void* bias, void* C, void* Z, 
 #define PRA_GEMM_LAUNCH(CFG, BETA_)                                                                         \
   gemm_lds_kernel<T, CFG, AK, BK, E, BETA_, false><<<tiles, CFG::NT, 0, s>>>(pa, pb, pbias, pc, pz, colsum, M, N, K, \
                                                                            lda, ldb, ldc, ldz, ablate, nullptr)
-  if (std::is_same<T, bf16>::value && E != kRelu && (pts_mask() >> layout & 1)) {
+  if (std::is_same<T, bf16>::value && E != kRelu && (g_force_pts || (pts_mask() >> layout & 1))) {
     const bool w4 = layout == 1 && !(pts_mask() & 16);
     if ((w4 ? pra_gemm_pts_w4 : pra_gemm_pts_w8)(layout, A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, kBF16,
                                                  E, beta, s) == 0)
@@ -335,6 +339,7 @@ extern "C" int pra_gemm_lds_splits(int M, int N, int K) {
 //      4/5 dgelu(erf/tanh): C = acc * gelu'(Z) (Z required). colsum (optional, fp32
 //      [ceil(M/256)][N]) receives per-tile column partial sums of the stored C.
 // splits > 1: split-K through the fp32 workspace ws [splits][M][N] (not with dgelu/colsum).
+// epi | 256: run the persistent kernel (gemm_pts.h) for this call when it takes the shape.
 // Returns -1 (nothing launched) for shapes outside what the kernel assumes: K % 64, N % 8 and every
 // leading dimension % 8 (16-B rows), M-contiguous operands need their MN extent >= 8.
 extern "C" int pra_gemm_lds(int layout, const void* A, const void* B, const void* bias, void* C, void* Z, float* colsum,
@@ -343,12 +348,18 @@ extern "C" int pra_gemm_lds(int layout, const void* A, const void* B, const void
   if (M <= 0 || N <= 0 || K <= 0 || (K & 63) || (N & 7) || (lda & 7) || (ldb & 7) || (ldc & 7) || (ldz & 7)) return -1;
   if (layout == 2 && (M < 8 || (M & 7))) return -1;
   if ((layout == 0 || layout == 2) && N < 8) return -1;
-  if ((epi == 4 || epi == 5) && !Z) return -1;
-  if (splits > 1 && (!ws || epi >= 4 || colsum || ldc != N)) return -1;
+  const int e = epi & 255;
+  if ((e == 4 || e == 5) && !Z) return -1;
+  if (splits > 1 && (!ws || e >= 4 || colsum || ldc != N)) return -1;
   // K-contiguous operands are addressed with 32-bit per-lane byte offsets from their base
   if ((layout == 0 || layout == 1) && (int64_t)M * lda * 2 >= (int64_t)1 << 32) return -1;
   if (layout == 1 && (int64_t)N * ldb * 2 >= (int64_t)1 << 32) return -1;
   if (splits < 1) splits = 1;
+  struct ForcePts {  // scoped: the flag never outlives this call
+    explicit ForcePts(bool on) { pra::g_force_pts = on; }
+    ~ForcePts() { pra::g_force_pts = false; }
+  } force_pts((epi & pra::kPersistBit) != 0 && splits == 1);
+  epi &= ~pra::kPersistBit;
   if (dtype == pra::kBF16)
     return pra::launch_t<pra::bf16>(layout, A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, epi, beta, splits, ws, s);
   if (dtype == pra::kF16)

@@ -352,6 +352,8 @@ def _acc_target(p):
 
 
 class AddDropoutLNFn(torch.autograd.Function):
+    none_grads_ok = True   # backward takes g_r / g_y = None (static graph: no zero fill)
+
     @staticmethod
     def forward(ctx, x, h, hb, w, b, p, eps):
         shp = x.shape
@@ -1317,7 +1319,9 @@ def _gemm_hip(layout, a, b, out=None, bias=None, z=None, epi=None, beta=0, want_
     Returns None when the shape/layout is outside what the kernel assumes (caller falls back)."""
     if _GEMM_MODE == 'blas' or not (_gemm_operand_ok(a) and _gemm_operand_ok(b)) or a.dtype != b.dtype:
         return None
-    if _GEMM_MODE == 'auto' and layout == GEMM_NT and not (_MLP_DGELU_EPI and epi in ('dgelu', 'dgelu_tanh')):
+    persist = _GEMM_MODE == 'auto' and layout == GEMM_NT and _nt_in_tree(a, b)
+    if _GEMM_MODE == 'auto' and layout == GEMM_NT and not persist and \
+            not (_MLP_DGELU_EPI and epi in ('dgelu', 'dgelu_tanh')):
         return None
     if layout == GEMM_FWD:
         M, K = a.shape
@@ -1354,7 +1358,7 @@ def _gemm_hip(layout, a, b, out=None, bias=None, z=None, epi=None, beta=0, want_
     try:
         L.gemm_lds(layout, a.data_ptr(), b.data_ptr(), _ptr(bias), out.data_ptr(), _ptr(z), _ptr(part),
                    M, N, K, a.stride(0), b.stride(0), out.stride(0), N if z is None else z.stride(0),
-                   _dt(a), e, int(beta), splits, _ptr(ws), _stream())
+                   _dt(a), e | (_PERSIST_BIT if persist else 0), int(beta), splits, _ptr(ws), _stream())
     except ValueError:
         return None
     if want_colsum:
@@ -1362,6 +1366,20 @@ def _gemm_hip(layout, a, b, out=None, bias=None, z=None, epi=None, beta=0, want_
         L.colsum_partials(part.data_ptr(), cs.data_ptr(), part.shape[0], N, 0, _stream())
         return out, cs
     return out
+
+
+# dy·Wᵀ shape policy (PRA_GEMM_NT_SHORTK=0 turns it off): with a short contraction (K <= 1024:
+# BERT-base's 768-wide dgrads and the MLM head's h·Eᵀ) the in-tree persistent kernel (one
+# workgroup per CU walking its tiles, next tile's DMA under the epilogue) measured ahead of
+# hipBLASLt: 22.5 / 61.6 / 98.5 us vs 24.5 / 63.6 / 130.9 us (profiles/r4/gemm_pts_bert.log);
+# at GPT-1.3B's K = 2048..8192 hipBLASLt's stream-K kernel stays ahead (gemm_pts_15shapes.log).
+_NT_SHORTK = __import__('os').environ.get('PRA_GEMM_NT_SHORTK', '1') == '1'
+_PERSIST_BIT = 256
+
+
+def _nt_in_tree(a, b):
+    K = a.shape[1]
+    return _NT_SHORTK and a.dtype == torch.bfloat16 and 256 <= K <= 1024 and K % 128 == 0
 
 
 def gemm(layout, a, b, out=None, bias=None, z=None, epi=None, beta=0, want_colsum=False):
@@ -1901,6 +1919,11 @@ def linear_nt(x2, w):
 # column sums in its epilogue (PRA_MLP_DGELU_EPI=1) instead of hipBLASLt + bias_gelu_bwd_db
 # (measured on GPT-1.3B: 123.0K vs 124.4K tokens/s, twice on one box: off by default)
 _MLP_DGELU_EPI = __import__('os').environ.get('PRA_MLP_DGELU_EPI', '0') == '1'
+# PRA_MLP_DGELU_SHORTK=1: the same fusion only where the dgrad runs in-tree anyway (K <= 1024,
+# BERT-base). Measured off by default: the persistent kernel's dGELU(erf) epilogue (Z read +
+# erf-GELU' + column sums, not overlapped with MFMA) took 140 us vs 64 + 61 us for hipBLASLt +
+# bias_gelu_bwd_db at [16384, 3072] x 768 (BERT 1751 vs 1771 seq/s, profiles/r4/bert_nt_policy.md)
+_MLP_DGELU_SHORTK = __import__('os').environ.get('PRA_MLP_DGELU_SHORTK', '0') == '1'
 
 
 class MlpGeluFn(torch.autograd.Function):
@@ -1931,8 +1954,9 @@ class MlpGeluFn(torch.autograd.Function):
         if not dy2.is_contiguous():
             dy2 = dy2.contiguous()
         x2 = x.reshape(-1, x.shape[-1])
-        if _GEMM_MODE == 'auto' and not _MLP_DGELU_EPI:
+        if _GEMM_MODE == 'auto' and not _MLP_DGELU_EPI and not (_MLP_DGELU_SHORTK and _nt_in_tree(dy2, w2)):
             # dgrad on hipBLASLt, then ONE fused pass for gelu'(z) and the bias gradient
+            # (a short-K dgrad runs in-tree with gelu'(z) and the bias column sums in its epilogue)
             dh = torch.mm(dy2, w2.t())
             dz, db1 = _dgelu_db(dh, z, ctx.approximate, ctx.b1)
         else:

@@ -565,9 +565,13 @@ def _fn_grad(ctx, *out_grads):
     if isinstance(ctx, _Ctx):
         return _vjp(ctx, *out_grads)
     gs = []
+    # a Function whose backward takes None for an unused output (``none_grads_ok``) is not
+    # handed a zero tensor: e.g. the residual output of add+dropout+LayerNorm in a post-LN
+    # encoder, which would otherwise cost a [tokens, hidden] fill per layer
+    keep_none = getattr(ctx.fn_cls, 'none_grads_ok', False)
     for g, (shp, dt, dev) in zip(out_grads, ctx.out_meta):
         if g is None:
-            gs.append(torch.zeros(shp, dtype=dt, device=dev) if ctx.materialize else None)
+            gs.append(torch.zeros(shp, dtype=dt, device=dev) if ctx.materialize and not keep_none else None)
         else:
             t = _u(g) if isinstance(g, Tensor) else g
             gs.append(t.to(dt) if t.dtype != dt else t)

@@ -226,3 +226,23 @@ def test_many_tiles_epilogues():
     ref, = torch.autograd.grad(torch.nn.functional.gelu(zf), zf, _ref(1, dy, w))
     _close(out, ref)
     _close(cs, out.float().sum(0), tol=1e-3)
+
+
+@pytest.mark.parametrize('Kd,in_tree', [(768, True), (1024, True), (2048, False)])
+def test_auto_policy_short_k_dgrad(Kd, in_tree):
+    """'auto': dy·Wᵀ with K <= 1024 runs the in-tree persistent kernel (ahead of hipBLASLt at
+    BERT-base widths), longer K goes to hipBLASLt; the dGELU epilogue path follows the same rule."""
+    K._GEMM_MODE = 'auto'
+    torch.manual_seed(9)
+    dy, w = _r(2048, Kd), _r(1280, Kd)
+    R.reset_stats()
+    y = K.gemm(K.GEMM_NT, dy, w)
+    st = R.stats()
+    assert (st.get(('gemm', 'hipblaslt'), 0) == 0) == in_tree, st
+    _close(y, _ref(1, dy, w))
+    z = _r(2048, 1280, scale=3.0)
+    out, cs = K.gemm(K.GEMM_NT, dy, w, z=z, epi='dgelu', want_colsum=True)
+    zf = z.float().requires_grad_(True)
+    ref, = torch.autograd.grad(torch.nn.functional.gelu(zf), zf, _ref(1, dy, w))
+    _close(out, ref)
+    _close(cs.float(), out.float().sum(0), tol=2e-3)
