@@ -27,6 +27,7 @@
 // wave (one wave per SIMD, 256 + accumulator registers).
 #include "common.h"
 #include <stdlib.h>
+#include <string.h>
 #include <type_traits>
 #include <algorithm>
 #include <cmath>
@@ -1087,15 +1088,15 @@ bwd_dkdv_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __res
 // (buffer_load ... lds: no VGPR staging, no ds_write) with per-lane source offsets that
 // realise the swizzle, and the buffer range check zero-fills key rows >= Sk.
 // ============================================================================
-template <typename T, int D, bool CAUSAL, bool EXT = false>
-__global__ void __launch_bounds__(512, 1)
+template <typename T, int D, bool CAUSAL, bool EXT = false, int NW = 8, int NBUF = 3>
+__global__ void __launch_bounds__(NW * 64, 1)
 bwd_dq_ds_kernel(const T* __restrict__ k, const T* __restrict__ dsT, T* __restrict__ dq, int H, int SqM, int SkM,
                  int Sqp, int64_t dsbh, int64_t ksb, int64_t kss, int64_t ksh, int64_t dqsb, int64_t dqss,
                  int64_t dqsh, float scale, FaExt ext = {}) {
-  constexpr int NW = 8, NT = NW * 64, BM = NW * 32, ND = D / 32, BUF = kTile * D + kTile * BM;
-  // 3-slot ring, tiles staged two ahead: the per-tile MFMA work (16 per wave) is far shorter
-  // than a DMA round trip, so one tile in flight per CU left the kernel latency-bound
-  constexpr int NBUF = 3;
+  constexpr int NT = NW * 64, BM = NW * 32, ND = D / 32, BUF = kTile * D + kTile * BM;
+  // NBUF-slot ring, tiles staged NBUF-1 ahead: the per-tile MFMA work (16 per wave) is far
+  // shorter than a DMA round trip, so one tile in flight per CU left the kernel latency-bound
+  static_assert(NBUF >= 2 && NBUF <= 4, "ring depth");
   extern __shared__ __attribute__((aligned(1024))) char smem[];
   T* img0 = reinterpret_cast<T*>(smem);  // [NBUF][K image 64*D | dS^T image 64*BM]
   const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
@@ -1142,13 +1143,14 @@ bwd_dq_ds_kernel(const T* __restrict__ k, const T* __restrict__ dsT, T* __restri
   // DMA instructions per wave and stage: vmcnt(PER) leaves the newest stage in flight
   constexpr int PER = SwzDma<D, NT>::PER + SwzDma<BM, NT>::PER;
   static_assert(PER < 16, "vmcnt field");
-  if (ntiles > 0) stage(0);
-  if (ntiles > 1) {
-    stage(1);
-    __builtin_amdgcn_s_waitcnt(0x0F70 | PER);  // tile 0 landed, tile 1 in flight
-  } else {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
+  static_assert(PER * (NBUF - 1) < 64, "vmcnt field");
+  // prologue: tiles 0 .. NBUF-2 staged; wait for tile 0 only
+  int staged = 0;
+  for (; staged < NBUF - 1 && staged < ntiles; ++staged) stage(staged);
+  if (staged == NBUF - 1 && NBUF == 4) wait_vm<2 * PER>();
+  else if (staged == NBUF - 1 && NBUF == 3) wait_vm<PER>();
+  else if (staged == 2 && NBUF == 4) wait_vm<PER>();
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
   auto tile = [&](int kt, auto mask_c) {
@@ -1156,8 +1158,8 @@ bwd_dq_ds_kernel(const T* __restrict__ k, const T* __restrict__ dsT, T* __restri
     const int k0 = kt * kTile;
     const T* Ks = img0 + (kt % NBUF) * BUF;
     const T* Ss = Ks + kTile * D;
-    const bool ahead = kt + 2 < ntiles;
-    if (ahead) stage(kt + 2);  // slot (kt+2)%3 was last read in tile kt-1, before the last barrier
+    const bool ahead = kt + NBUF - 1 < ntiles;
+    if (ahead) stage(kt + NBUF - 1);  // slot (kt+NBUF-1)%NBUF was last read in tile kt-1, before the last barrier
     int nlive = 2;
     if constexpr (MASK) {
       int kmax = Sk - 1;
@@ -1188,8 +1190,10 @@ bwd_dq_ds_kernel(const T* __restrict__ k, const T* __restrict__ dsT, T* __restri
         for (int dt = 0; dt < ND; ++dt) acc_q[dt] = mfma<T>(af[dt], bf, acc_q[dt]);
       }
     }
-    // this wave's DMA of tile kt+1 landed (tile kt+2's may stay in flight)
-    if (ahead) __builtin_amdgcn_s_waitcnt(0x0F70 | PER);
+    // this wave's DMA of tile kt+1 landed (the younger stages may stay in flight)
+    const int inflight = min(ntiles - 1 - (kt + 1), NBUF - 2);  // stages issued after tile kt+1's
+    if (NBUF == 4 && inflight >= 2) wait_vm<2 * PER>();
+    else if (inflight >= 1) wait_vm<PER>();
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   };
@@ -1234,6 +1238,42 @@ static void launch_fwd(const void* q, const void* k, const void* v, void* o, flo
   else launch_fwd_nw<T, D, C, 8>(q, k, v, o, lse, B, H, Sq, Sk, st, scale, s);
 }
 
+// dQ = dS K launch shape: waves per block x ring depth. PRA_FA_DQ = "8x3" (default: 256 queries
+// per block, two tiles in flight), "8x2", "4x3", "4x4" (128 queries, three in flight) -- A/B knob.
+static int dq_variant() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("PRA_FA_DQ");
+    v = 0;
+    if (e && !strcmp(e, "8x2")) v = 1;
+    else if (e && !strcmp(e, "4x3")) v = 2;
+    else if (e && !strcmp(e, "4x4")) v = 3;
+  }
+  return v;
+}
+
+template <typename T, int D, bool C, bool EXT, int NW, int NBUF>
+static void launch_dq_ds_cfg(const void* k, void* dsT, void* dq, int B, int H, int Sq, int Sk, int Sqp, int64_t dsbh,
+                             const int64_t* st, float scale, const FaExt& ext, hipStream_t s) {
+  const size_t lds = (size_t)NBUF * (kTile * D + kTile * NW * 32) * sizeof(T);
+  auto kern = bwd_dq_ds_kernel<T, D, C, EXT, NW, NBUF>;
+  hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL(kern, dim3(B * H, (Sq + NW * 32 - 1) / (NW * 32)), dim3(NW * 64), lds, s, (const T*)k,
+                     (const T*)dsT, (T*)dq, H, Sq, Sk, Sqp, dsbh, st[3], st[4], st[5], st[9], st[10], st[11], scale,
+                     ext);
+}
+
+template <typename T, int D, bool C, bool EXT>
+static void launch_dq_ds(const void* k, void* dsT, void* dq, int B, int H, int Sq, int Sk, int Sqp, int64_t dsbh,
+                         const int64_t* st, float scale, const FaExt& ext, hipStream_t s) {
+  switch (dq_variant()) {
+    case 1: launch_dq_ds_cfg<T, D, C, EXT, 8, 2>(k, dsT, dq, B, H, Sq, Sk, Sqp, dsbh, st, scale, ext, s); break;
+    case 2: launch_dq_ds_cfg<T, D, C, EXT, 4, 3>(k, dsT, dq, B, H, Sq, Sk, Sqp, dsbh, st, scale, ext, s); break;
+    case 3: launch_dq_ds_cfg<T, D, C, EXT, 4, 4>(k, dsT, dq, B, H, Sq, Sk, Sqp, dsbh, st, scale, ext, s); break;
+    default: launch_dq_ds_cfg<T, D, C, EXT, 8, 3>(k, dsT, dq, B, H, Sq, Sk, Sqp, dsbh, st, scale, ext, s); break;
+  }
+}
+
 template <typename T, int D, bool C>
 static void launch_bwd(const void* q, const void* k, const void* v, const void* dO, const void* o, const float* lse,
                        float* delta, void* dq, void* dk, void* dv, void* dsT, int B, int H, int Sq, int Sk,
@@ -1252,13 +1292,7 @@ static void launch_bwd(const void* q, const void* k, const void* v, const void* 
                          st[3], st[4], st[5], st[6], st[7], st[8], st[12], st[13], st[14], st[15], st[16], st[17],
                          scale, sl2, (T*)dsT, Sqp, dsbh, FaExt{});
     }
-    {
-      const size_t lds = 3 * (kTile * D + kTile * 256) * sizeof(T);
-      auto kern = bwd_dq_ds_kernel<T, D, C>;
-      hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      hipLaunchKernelGGL(kern, dim3(B * H, (Sq + 255) / 256), dim3(512), lds, s, (const T*)k, (const T*)dsT,
-                         (T*)dq, H, Sq, Sk, Sqp, dsbh, st[3], st[4], st[5], st[9], st[10], st[11], scale, FaExt{});
-    }
+    launch_dq_ds<T, D, C, false>(k, dsT, dq, B, H, Sq, Sk, Sqp, dsbh, st, scale, FaExt{}, s);
     return;
   }
   {
@@ -1314,13 +1348,7 @@ static void launch_bwd_ext(const void* q, const void* k, const void* v, const vo
                        st[3], st[4], st[5], st[6], st[7], st[8], st[12], st[13], st[14], st[15], st[16], st[17],
                        scale, sl2, (T*)dsT, Sqp, dsbh, ext);
   }
-  {
-    const size_t lds = 3 * (kTile * D + kTile * 256) * sizeof(T);
-    auto kern = bwd_dq_ds_kernel<T, D, C, true>;
-    hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(kern, dim3(B * H, (Sq + 255) / 256), dim3(512), lds, s, (const T*)k, (const T*)dsT,
-                       (T*)dq, H, Sq, Sk, Sqp, dsbh, st[3], st[4], st[5], st[9], st[10], st[11], scale, ext);
-  }
+  launch_dq_ds<T, D, C, true>(k, dsT, dq, B, H, Sq, Sk, Sqp, dsbh, st, scale, ext, s);
 }
 
 }  // namespace fa
