@@ -57,9 +57,9 @@ int pra_flash_fwd_ext(const void*, const void*, const void*, void*, float*, int,
 int pra_flash_bwd_ext(const void*, const void*, const void*, const void*, const float*, const float*, void*, void*,
                       void*, void*, int, int, int, int, int, const int64_t*, float, int, int, const int*, const int*,
                       const void*, int64_t, int64_t, int64_t, int, float, uint64_t, uint64_t, uint32_t*, const uint64_t*,
-                      hipStream_t);
+                      float*, hipStream_t);
 int pra_flash_bwd(const void*, const void*, const void*, const void*, const void*, const float*, float*, void*, void*,
-                  void*, void*, int, int, int, int, int, const int64_t*, float, int, int, hipStream_t);
+                  void*, void*, int, int, int, int, int, const int64_t*, float, int, int, float*, hipStream_t);
 int pra_embedding_fwd(const int64_t*, const void*, void*, int64_t, int, int64_t, int64_t, int, hipStream_t);
 int pra_embedding_bwd(const int64_t*, const int64_t*, const void*, void*, int64_t, int, int64_t, int64_t, int, int,
                       int, float*, hipStream_t);
@@ -303,21 +303,21 @@ PYBIND11_MODULE(_pra_hip, m) {
   m.def("flash_bwd_ext", [](P q, P k, P v, P dO, P lse, P delta, P dq, P dk, P dv, P dsT, int B, int H, int Sq, int Sk,
                             int D, std::vector<int64_t> st, float scale, int causal, int dt, P cu_q, P cu_k, P mask,
                             int64_t msb, int64_t msh, int64_t msq, int mask_f32, float p_drop, uint64_t seed,
-                            uint64_t offset, P dbits, P dseq, P s) {
+                            uint64_t offset, P dbits, P dseq, P s, P bsum) {
     if (st.size() != 18) throw std::invalid_argument("flash_bwd_ext: need 18 strides");
     if (pra_flash_bwd_ext(CV(q), CV(k), CV(v), CV(dO), CF(lse), CF(delta), V(dq), V(dk), V(dv), V(dsT), B, H, Sq, Sk,
                           D, st.data(), scale, causal, dt, reinterpret_cast<const int*>(cu_q),
                           reinterpret_cast<const int*>(cu_k), CV(mask), msb, msh, msq, mask_f32, p_drop, seed,
                           offset, reinterpret_cast<uint32_t*>(dbits), reinterpret_cast<const uint64_t*>(dseq),
-                          S(s)) != 0)
+                          F(bsum), S(s)) != 0)
       throw std::invalid_argument("flash_bwd_ext: unsupported arguments");
     check_launch("flash_bwd_ext");
   });
   m.def("flash_bwd", [](P q, P k, P v, P dO, P o, P lse, P delta, P dq, P dk, P dv, P dsT, int B, int H, int Sq,
-                        int Sk, int D, std::vector<int64_t> st, float scale, int causal, int dt, P s) {
+                        int Sk, int D, std::vector<int64_t> st, float scale, int causal, int dt, P s, P bsum) {
     if (st.size() != 18) throw std::invalid_argument("flash_bwd: need 18 strides");
     if (pra_flash_bwd(CV(q), CV(k), CV(v), CV(dO), CV(o), CF(lse), F(delta), V(dq), V(dk), V(dv), V(dsT), B, H, Sq, Sk, D, st.data(),
-                      scale, causal, dt, S(s)) != 0)
+                      scale, causal, dt, F(bsum), S(s)) != 0)
       throw std::invalid_argument("flash_bwd: unsupported head_dim/dtype");
     check_launch("flash_bwd");
   });

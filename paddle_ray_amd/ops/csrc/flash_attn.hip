@@ -124,6 +124,11 @@ struct FaExt {
   // graph replays: device step counter mixed into the seed (null in eager launches; see
   // ops/graph_rng.py): a captured launch draws new bits on every replay
   const uint64_t* dseq;
+  // packed-QKV bias gradient (Sq == Sk, no varlen): column-sum partials of the rounded dQ / dK / dV,
+  // one fp32 row per (batch, 128-row block): bsum[(b * bsum_nblk + blk) * 3HD + which * HD + h * D + d]
+  // (which = 0 / 1 / 2 for q / k / v), reduced into the bias gradient by colsum16(_acc)
+  float* bsum;
+  int bsum_nblk;
 };
 
 // Feature bits of an extended launch. Each combination runs its own copy of the tile loop, so
@@ -1060,22 +1065,50 @@ bwd_dkdv_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __res
     }
   }
 
-  if (kvalid) {
-    T* krow = (vl ? dk + krow0 * dkss : dk + (int64_t)b * dksb) + (int64_t)mykey * dkss + (int64_t)hh * dksh;
-    T* vrow = (vl ? dv + krow0 * dvss : dv + (int64_t)b * dvsb) + (int64_t)mykey * dvss + (int64_t)hh * dvsh;
+  // bias-gradient partials: this block's 128 rounded dK / dV rows go through two padded [128][D+4]
+  // LDS stages (the tile images are free now), then thread t sums column t of [dK | dV]
+  constexpr int RP = D + 4;
+  T* sk = img0;
+  T* sv = img0 + 128 * RP;
+  const bool bs = ext.bsum != nullptr;  // uniform
+  if (bs) {
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __syncthreads();  // every wave's reads of the last tile's images (and the dS^T stage) are done
+  }
+  T* krow = (vl ? dk + krow0 * dkss : dk + (int64_t)b * dksb) + (int64_t)mykey * dkss + (int64_t)hh * dksh;
+  T* vrow = (vl ? dv + krow0 * dvss : dv + (int64_t)b * dvsb) + (int64_t)mykey * dvss + (int64_t)hh * dvsh;
+  const int srow = wave * 32 + r;
 #pragma unroll
-    for (int dt = 0; dt < ND; ++dt)
+  for (int dt = 0; dt < ND; ++dt)
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int d = 32 * dt + 8 * g + 4 * h;
-        uint2 wk, wv;
-        wk.x = pack2<T>(acc_k[dt][4 * g + 0] * scale, acc_k[dt][4 * g + 1] * scale);
-        wk.y = pack2<T>(acc_k[dt][4 * g + 2] * scale, acc_k[dt][4 * g + 3] * scale);
-        wv.x = pack2<T>(acc_v[dt][4 * g + 0], acc_v[dt][4 * g + 1]);
-        wv.y = pack2<T>(acc_v[dt][4 * g + 2], acc_v[dt][4 * g + 3]);
+    for (int g = 0; g < 4; ++g) {
+      const int d = 32 * dt + 8 * g + 4 * h;
+      uint2 wk, wv;
+      wk.x = pack2<T>(acc_k[dt][4 * g + 0] * scale, acc_k[dt][4 * g + 1] * scale);
+      wk.y = pack2<T>(acc_k[dt][4 * g + 2] * scale, acc_k[dt][4 * g + 3] * scale);
+      wv.x = pack2<T>(acc_v[dt][4 * g + 0], acc_v[dt][4 * g + 1]);
+      wv.y = pack2<T>(acc_v[dt][4 * g + 2], acc_v[dt][4 * g + 3]);
+      if (kvalid) {
         *reinterpret_cast<uint2*>(krow + d) = wk;
         *reinterpret_cast<uint2*>(vrow + d) = wv;
       }
+      if (bs) {
+        const uint2 z = make_uint2(0u, 0u);
+        *reinterpret_cast<uint2*>(sk + srow * RP + d) = kvalid ? wk : z;
+        *reinterpret_cast<uint2*>(sv + srow * RP + d) = kvalid ? wv : z;
+      }
+    }
+  if (bs) {
+    __syncthreads();
+    const int col = threadIdx.x;
+    if (col < 2 * D) {
+      const T* src = col < D ? sk + col : sv + (col - D);
+      float a = 0.f;
+#pragma unroll 8
+      for (int i = 0; i < 128; ++i) a += Cvt<T>::to(src[i * RP]);
+      const int64_t HD = (int64_t)H * D;
+      ext.bsum[((int64_t)b * ext.bsum_nblk + kb) * 3 * HD + (col < D ? 1 : 2) * HD + (int64_t)hh * D + (col % D)] = a;
+    }
   }
 }
 
@@ -1203,18 +1236,40 @@ bwd_dq_ds_kernel(const T* __restrict__ k, const T* __restrict__ dsT, T* __restri
   for (int kt = 0; kt < nfull; ++kt) tile(kt, std::false_type{});
   for (int kt = nfull; kt < ntiles; ++kt) tile(kt, std::true_type{});
 
-  if (myq < Sq) {
-    T* row = (vl ? dq + qrow0 * dqss : dq + (int64_t)b * dqsb) + (int64_t)myq * dqss + (int64_t)hh * dqsh;
+  // bias-gradient partials (see FaExt::bsum): the block's BM rounded dQ rows through a padded
+  // [BM][D+4] LDS stage, column sums per 128-row half
+  constexpr int RP = D + 4;
+  static_assert(BM * RP <= NBUF * BUF, "dQ stage fits the ring");
+  T* sq = img0;
+  const bool bs = ext.bsum != nullptr;  // uniform
+  if (bs) {
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __syncthreads();
+  }
+  const bool qvalid = myq < Sq;
+  T* row = (vl ? dq + qrow0 * dqss : dq + (int64_t)b * dqsb) + (int64_t)myq * dqss + (int64_t)hh * dqsh;
 #pragma unroll
-    for (int dt = 0; dt < ND; ++dt)
+  for (int dt = 0; dt < ND; ++dt)
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int d = 32 * dt + 8 * g + 4 * h;
-        uint2 w;
-        w.x = pack2<T>(acc_q[dt][4 * g + 0] * scale, acc_q[dt][4 * g + 1] * scale);
-        w.y = pack2<T>(acc_q[dt][4 * g + 2] * scale, acc_q[dt][4 * g + 3] * scale);
-        *reinterpret_cast<uint2*>(row + d) = w;
-      }
+    for (int g = 0; g < 4; ++g) {
+      const int d = 32 * dt + 8 * g + 4 * h;
+      uint2 w;
+      w.x = pack2<T>(acc_q[dt][4 * g + 0] * scale, acc_q[dt][4 * g + 1] * scale);
+      w.y = pack2<T>(acc_q[dt][4 * g + 2] * scale, acc_q[dt][4 * g + 3] * scale);
+      if (qvalid) *reinterpret_cast<uint2*>(row + d) = w;
+      if (bs) *reinterpret_cast<uint2*>(sq + (wave * 32 + r) * RP + d) = qvalid ? w : make_uint2(0u, 0u);
+    }
+  if (bs) {
+    __syncthreads();
+    for (int t = threadIdx.x; t < D * (BM / 128); t += NT) {
+      const int half = t / D, col = t % D, blk = (q0 >> 7) + half;
+      if (blk >= ext.bsum_nblk) continue;
+      const T* src = sq + half * 128 * RP + col;
+      float a = 0.f;
+#pragma unroll 8
+      for (int i = 0; i < 128; ++i) a += Cvt<T>::to(src[i * RP]);
+      ext.bsum[((int64_t)b * ext.bsum_nblk + blk) * 3 * (int64_t)H * D + (int64_t)hh * D + col] = a;
+    }
   }
 }
 
@@ -1277,9 +1332,12 @@ static void launch_dq_ds(const void* k, void* dsT, void* dq, int B, int H, int S
 template <typename T, int D, bool C>
 static void launch_bwd(const void* q, const void* k, const void* v, const void* dO, const void* o, const float* lse,
                        float* delta, void* dq, void* dk, void* dv, void* dsT, int B, int H, int Sq, int Sk,
-                       const int64_t* st, float scale, hipStream_t s) {
+                       const int64_t* st, float scale, float* bsum, hipStream_t s) {
   const float sl2 = scale * 1.4426950408889634f;
   if (dsT) {
+    FaExt be{};
+    be.bsum = bsum;
+    be.bsum_nblk = (Sk + 127) / 128;
     // dK/dV first (stores dS^T), then dQ = dS K; `delta` is an input here
     const int Sqp = (Sq + 255) / 256 * 256;
     const int64_t dsbh = (int64_t)((Sk + 127) / 128 * 128) * Sqp;
@@ -1290,9 +1348,9 @@ static void launch_bwd(const void* q, const void* k, const void* v, const void* 
       hipLaunchKernelGGL(kern, dim3(B * H, (Sk + 127) / 128), dim3(256), lds, s, (const T*)q, (const T*)k,
                          (const T*)v, (const T*)dO, lse, delta, (T*)dk, (T*)dv, H, Sq, Sk, st[0], st[1], st[2],
                          st[3], st[4], st[5], st[6], st[7], st[8], st[12], st[13], st[14], st[15], st[16], st[17],
-                         scale, sl2, (T*)dsT, Sqp, dsbh, FaExt{});
+                         scale, sl2, (T*)dsT, Sqp, dsbh, be);
     }
-    launch_dq_ds<T, D, C, false>(k, dsT, dq, B, H, Sq, Sk, Sqp, dsbh, st, scale, FaExt{}, s);
+    launch_dq_ds<T, D, C, false>(k, dsT, dq, B, H, Sq, Sk, Sqp, dsbh, st, scale, be, s);
     return;
   }
   {
@@ -1409,27 +1467,34 @@ int pra_flash_fwd_ext(const void* q, const void* k, const void* v, void* o, floa
   return 0;
 }
 // Extended backward (same extras as the forward; `delta` = rowsum(dO*O) [B, H, Sq] is an input,
-// dsT the dS^T scratch of B*H*roundup(Sk,128)*roundup(Sq,256) elements)
+// dsT the dS^T scratch of B*H*roundup(Sk,128)*roundup(Sq,256) elements). bsum (optional, both
+// backward entries): [B * ceil(S/128)][3*H*D] fp32 column-sum partials of the packed dQKV, the
+// bias gradient of the QKV projection before its row reduction (FaExt::bsum).
 int pra_flash_bwd_ext(const void* q, const void* k, const void* v, const void* dO, const float* lse,
                       const float* delta, void* dq, void* dk, void* dv, void* dsT, int B, int H, int Sq, int Sk, int D,
                       const int64_t* strides, float scale, int causal, int dt, const int* cu_q, const int* cu_k,
                       const void* mask, int64_t msb, int64_t msh, int64_t msq, int mask_f32, float p_drop,
-                      uint64_t seed, uint64_t offset, uint32_t* dbits, const uint64_t* dseq, hipStream_t s) {
+                      uint64_t seed, uint64_t offset, uint32_t* dbits, const uint64_t* dseq, float* bsum,
+                      hipStream_t s) {
   if (!(D == 64 || D == 128) || !(dt == kBF16 || dt == kF16) || !dsT) return -1;
   if (!(p_drop >= 0.f && p_drop < 1.f) || (!cu_q) != (!cu_k)) return -1;
+  if (bsum && (cu_q || Sq != Sk)) return -4;  // bias partials: packed self-attention only
   if (B * H == 0 || Sq == 0) return 0;
-  const fa::FaExt e = fa_ext(cu_q, cu_k, mask, msb, msh, msq, mask_f32, scale, p_drop, seed, offset, dbits, Sk, dseq);
+  fa::FaExt e = fa_ext(cu_q, cu_k, mask, msb, msh, msq, mask_f32, scale, p_drop, seed, offset, dbits, Sk, dseq);
+  e.bsum = bsum;
+  e.bsum_nblk = (Sk + 127) / 128;
   if ((e.xf & fa::XF_DROP) && !dbits) return -3;  // the backward reads the forward's keep bits
   PRA_FA_DISPATCH(launch_bwd_ext, q, k, v, dO, lse, delta, dq, dk, dv, dsT, B, H, Sq, Sk, strides, scale, e, s);
   return 0;
 }
 int pra_flash_bwd(const void* q, const void* k, const void* v, const void* dO, const void* o, const float* lse,
                   float* delta, void* dq, void* dk, void* dv, void* dsT, int B, int H, int Sq, int Sk, int D,
-                  const int64_t* strides, float scale, int causal, int dt, hipStream_t s) {
+                  const int64_t* strides, float scale, int causal, int dt, float* bsum, hipStream_t s) {
   if (!(D == 64 || D == 128) || !(dt == kBF16 || dt == kF16)) return -1;
   if (dsT && o) return -2;
+  if (bsum && (!dsT || Sq != Sk)) return -4;  // bias partials: the dS^T path, self-attention
   if (B * H == 0 || Sq == 0) return 0;
-  PRA_FA_DISPATCH(launch_bwd, q, k, v, dO, o, lse, delta, dq, dk, dv, dsT, B, H, Sq, Sk, strides, scale, s);
+  PRA_FA_DISPATCH(launch_bwd, q, k, v, dO, o, lse, delta, dq, dk, dv, dsT, B, H, Sq, Sk, strides, scale, bsum, s);
   return 0;
 }
 }

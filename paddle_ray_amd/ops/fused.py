@@ -916,7 +916,10 @@ _FA_DS_MAX_BYTES = int(os.environ.get('PRA_FA_DS_MAX_MB', '4096')) << 20
 
 
 @R.register_kernel('flash_attn_bwd', 'hip', dtypes=_HALF)
-def _fa_bwd_hip(do, q, k, v, o, lse, causal, scale, dq=None, dk=None, dv=None):
+def _fa_bwd_hip(do, q, k, v, o, lse, causal, scale, dq=None, dk=None, dv=None, bsum=None):
+    """bsum (optional, [B * ceil(S/128), 3*H*D] fp32, packed self-attention only): receives the
+    column-sum partials of dQ/dK/dV, i.e. the QKV-projection bias gradient before its row
+    reduction (filled only on the dS^T path; ``bsum.filled`` tells the caller)."""
     do = _like(do, q.dtype)
     _check_dtypes('flash_attention_grad', (q, k), (q, v), (q, o))
     if not _fa_supported(q, k, v):
@@ -937,6 +940,7 @@ def _fa_bwd_hip(do, q, k, v, o, lse, causal, scale, dq=None, dk=None, dv=None):
     else:
         # delta is computed by the dQ sweep kernel itself (written for the dK/dV kernel)
         o_arg, ds_arg = _ptr(o), 0
+    bs_arg = _ptr(bsum) if (bsum is not None and ds_arg and Sq == Sk) else 0
     if dq is None:
         dq = torch.empty((B, Sq, H, D), device=q.device, dtype=q.dtype)
         dk = torch.empty((B, Sk, H, D), device=q.device, dtype=q.dtype)
@@ -945,8 +949,40 @@ def _fa_bwd_hip(do, q, k, v, o, lse, causal, scale, dq=None, dk=None, dv=None):
           v.stride(0), v.stride(1), v.stride(2), dq.stride(0), dq.stride(1), dq.stride(2),
           dk.stride(0), dk.stride(1), dk.stride(2), dv.stride(0), dv.stride(1), dv.stride(2)]
     L.flash_bwd(_ptr(q), _ptr(k), _ptr(v), _ptr(do), o_arg, _ptr(lse), _ptr(delta), _ptr(dq), _ptr(dk),
-                _ptr(dv), ds_arg, B, H, Sq, Sk, D, st, float(scale), int(causal), _dt(q), _stream())
-    return dq, dk, dv
+                _ptr(dv), ds_arg, B, H, Sq, Sk, D, st, float(scale), int(causal), _dt(q), _stream(), bs_arg)
+    return (dq, dk, dv, bool(bs_arg)) if bsum is not None else (dq, dk, dv)
+
+
+# QKV-projection bias gradient from the flash backward: the dQ / dK / dV kernels sum the rounded
+# packed gradient's columns per 128-row block, so the Linear's bias_grad skips its own pass over
+# the [tokens, 3*H*D] gradient (PRA_FA_BIAS_PART=0: the separate colsum kernel)
+_FA_BIAS_PART = os.environ.get('PRA_FA_BIAS_PART', '1') == '1'
+
+
+def _qkv_bias_part(qkv):
+    """fp32 partial buffer for a packed [B, S, 3, H, D] gradient, or None when not applicable."""
+    if not _FA_BIAS_PART or not qkv.is_cuda:
+        return None
+    B, S, _, H, D = qkv.shape
+    return torch.empty((B * (-(-S // 128)), 3 * H * D), device=qkv.device, dtype=torch.float32)
+
+
+def _tag_bias_part(dqkv, part):
+    dqkv._pra_bias_part = (part, dqkv._version)
+
+
+def _bias_part_of(dy2):
+    """The flash backward's column-sum partials behind ``dy2`` (a [rows, 3*H*D] view of the
+    packed dQKV it wrote), if that gradient is unmodified since; else None."""
+    base = dy2 if dy2._base is None else dy2._base
+    tag = getattr(base, '_pra_bias_part', None)
+    if tag is None:
+        return None
+    part, ver = tag
+    if base._version != ver or base.numel() != dy2.numel() or part.shape[1] != dy2.shape[-1] or \
+            dy2.data_ptr() != base.data_ptr():
+        return None
+    return part
 
 
 class FlashAttnQKVPackedFn(torch.autograd.Function):
@@ -968,7 +1004,10 @@ class FlashAttnQKVPackedFn(torch.autograd.Function):
         if R.select_backend(qkv, 'flash_attn_bwd') == 'hip' and _fa_supported(q, k, v):
             dqkv = torch.empty_like(qkv)
             dq, dk, dv = dqkv.unbind(2)
-            _fa_bwd_hip(do, q, k, v, o, lse, ctx.causal, ctx.scale, dq, dk, dv)
+            part = _qkv_bias_part(qkv)
+            r = _fa_bwd_hip(do, q, k, v, o, lse, ctx.causal, ctx.scale, dq, dk, dv, bsum=part)
+            if part is not None and r[3]:
+                _tag_bias_part(dqkv, part)
             return dqkv, None, None
         dq, dk, dv = _fa_bwd_ref(do, q, k, v, o, lse, ctx.causal, ctx.scale)
         return torch.stack([dq, dk, dv], 2), None, None
@@ -1121,8 +1160,9 @@ class FlashAttnExtFn(torch.autograd.Function):
         return dq, dk, dv, None, None, None, None, None, None, None, None, None, None
 
 
-def _fa_ext_backward(ctx, do, outs=None):
-    """dq, dk, dv of FlashAttnExtFn (into ``outs`` = (dq, dk, dv) views when given, dense only)."""
+def _fa_ext_backward(ctx, do, outs=None, bsum=None):
+    """dq, dk, dv of FlashAttnExtFn (into ``outs`` = (dq, dk, dv) views when given, dense only;
+    ``bsum``: packed-QKV bias partials as in _fa_bwd_hip, dense self-attention only)."""
     q, k, v, o, lse, mk, cu_q, cu_k, dbits = ctx.saved_tensors
     varlen, B, H, D, Sq, Sk, st, causal, scale, p_drop, seed, offset, mmeta = ctx.meta
     L = _native.lib()
@@ -1156,7 +1196,8 @@ def _fa_ext_backward(ctx, do, outs=None):
                     _ptr(dv), _ptr(ds), B, H, Sq, Sk, D, gst, float(scale), int(causal), _dt(q),
                     _ptr(cu_q) if varlen else 0, _ptr(cu_k) if varlen else 0,
                     _ptr(mk) if mmeta is not None else 0, msb, msh, msq, int(m32), float(p_drop),
-                    int(seed), int(offset), _ptr(dbits) if dbits.numel() else 0, 0, _stream())
+                    int(seed), int(offset), _ptr(dbits) if dbits.numel() else 0, 0, _stream(),
+                    _ptr(bsum) if (bsum is not None and not varlen and Sq == Sk) else 0)
     return dq, dk, dv
 
 
@@ -1174,7 +1215,10 @@ class FlashAttnExtQKVFn(torch.autograd.Function):
     def backward(ctx, do):
         dqkv = torch.empty(ctx.saved_tensors[0].shape[:2] + (3,) + ctx.saved_tensors[0].shape[2:],
                            device=do.device, dtype=ctx.saved_tensors[0].dtype)
-        _fa_ext_backward(ctx, do, dqkv.unbind(2))
+        part = _qkv_bias_part(dqkv)
+        _fa_ext_backward(ctx, do, dqkv.unbind(2), bsum=part)
+        if part is not None:
+            _tag_bias_part(dqkv, part)
         return dqkv, None, None, None, None, None, None
 
 
@@ -1839,9 +1883,13 @@ def bias_grad(dy2, b):
     if not (dy2.is_cuda and cols % 8 == 0 and dy2.dtype in _DT and _native.available()):
         return dy2.sum(0)
     L = _native.lib()
-    nrb = max(1, min(256, rows // 32))
-    part = torch.empty((nrb, cols), device=dy2.device, dtype=torch.float32)
-    L.colsum_rows(_ptr(dy2), _ptr(part), rows, cols, nrb, _dt(dy2), _stream())
+    part = _bias_part_of(dy2)   # the flash backward already summed this packed dQKV's columns
+    if part is not None:
+        nrb = part.shape[0]
+    else:
+        nrb = max(1, min(256, rows // 32))
+        part = torch.empty((nrb, cols), device=dy2.device, dtype=torch.float32)
+        L.colsum_rows(_ptr(dy2), _ptr(part), rows, cols, nrb, _dt(dy2), _stream())
     g = b.grad if b.is_leaf else None
     if _acc_grad_ok(g, b, dy2.dtype):
         L.colsum16_acc(_ptr(part), _ptr(g), nrb, cols, _dt(g), _stream())

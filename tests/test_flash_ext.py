@@ -45,7 +45,7 @@ def test_sdpa_mask_and_dropout_api_cpu():
     m[:, :, :, 6:] = float('-inf')
     o = F.scaled_dot_product_attention(q, q, q, attn_mask=m, training=False)
     ref, _ = K._fa_ext_ref_dense(q._t, q._t, q._t, False, 1 / 4.0, m._t)
-    np.testing.assert_allclose(o.numpy(), ref.numpy(), rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(o.numpy(), ref.cpu().numpy(), rtol=1e-5, atol=1e-6)
     out, _ = F.flash_attention(q, q, q, dropout=0.5, causal=True)
     assert out.shape == [2, 8, 2, 16]
 

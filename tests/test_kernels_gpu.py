@@ -535,3 +535,46 @@ def test_paddle_matmul_device_gemm(ty):
     torch.testing.assert_close(y.float(), yf, atol=0.5, rtol=3e-2)
     torch.testing.assert_close(a.grad.float(), af.grad, atol=0.5, rtol=3e-2)
     torch.testing.assert_close(b.grad.float(), bf.grad, atol=1.0, rtol=3e-2)
+
+
+@pytest.mark.parametrize('path', ['plain', 'ext'])
+@pytest.mark.parametrize('S,D', [(384, 64), (256, 128)])
+def test_qkv_bias_grad_from_flash_partials(path, S, D):
+    """The QKV projection's bias gradient taken from the flash backward's column-sum partials
+    equals the column sum of the packed dQKV it wrote (fp32 sum of the rounded values), also for
+    a sequence that leaves the last dQ block half empty (S = 384)."""
+    torch.manual_seed(11)
+    B, H = 2, 4
+    HD = H * D
+    x = (torch.randn(B, S, HD, device='cuda') * 0.5).to(torch.bfloat16).requires_grad_(True)
+    w = (torch.randn(HD, 3 * HD, device='cuda') * 0.05).to(torch.bfloat16).requires_grad_(True)
+    b = torch.zeros(3 * HD, device='cuda', dtype=torch.bfloat16, requires_grad=True)
+    seen = {}
+    qkv = F.linear(x, w, b)
+    def keep(g):
+        seen['g'] = g.detach().float().clone()
+    qkv.register_hook(keep)
+    q5 = qkv.view(B, S, 3, H, D)
+    if path == 'plain':
+        o = F.flash_attention_qkvpacked(q5, causal=True)
+    else:
+        mask = torch.zeros(B, 1, 1, S, device='cuda', dtype=torch.bfloat16)
+        mask[1, ..., S - 40:] = float('-inf')
+        o = F.flash_attention_ext_qkvpacked(q5, attn_mask=mask, dropout=0.1)
+    o.float().square().sum().backward()
+    ref = seen['g'].reshape(-1, 3 * HD).sum(0)
+    err = (b.grad.float() - ref).abs().max().item()
+    assert err <= 2e-2 * max(ref.abs().max().item(), 1e-3), (err, ref.abs().max().item())
+    # the partials path was taken (the tagged gradient reached bias_grad)
+    F._FA_BIAS_PART = False
+    try:
+        b2 = b.detach().clone().requires_grad_(True)
+        qkv2 = F.linear(x.detach(), w.detach(), b2)
+        q52 = qkv2.view(B, S, 3, H, D)
+        if path == 'plain':
+            o2 = F.flash_attention_qkvpacked(q52, causal=True)
+            o2.float().square().sum().backward()
+            err2 = (b2.grad.float() - b.grad.float()).abs().max().item()
+            assert err2 <= 1e-2 * max(ref.abs().max().item(), 1e-3), err2
+    finally:
+        F._FA_BIAS_PART = True
