@@ -1862,7 +1862,10 @@ class LinearFn(torch.autograd.Function):
         if not dy2.is_contiguous():
             dy2 = dy2.contiguous()
         x2 = x.reshape(-1, x.shape[-1])
-        dx = gemm(GEMM_NT, dy2, w).view(x.shape) if ctx.needs_input_grad[0] else None
+        dx = None
+        if ctx.needs_input_grad[0]:
+            acc = _dx_acc(ctx, x)
+            dx = gemm(GEMM_NT, dy2, w, out=acc, beta=1 if acc is not None else 0).view(x.shape)
         dw = None
         if ctx.needs_input_grad[1]:
             g = w.grad if w.is_leaf else None
@@ -1874,6 +1877,17 @@ class LinearFn(torch.autograd.Function):
                 dw = gemm(GEMM_TN, x2, dy2)
         db = bias_grad(dy2, ctx.b) if ctx.has_b and ctx.needs_input_grad[2] else None
         return dx, dw, db
+
+
+def _dx_acc(ctx, x):
+    """Static-graph gradient-sum fusion (static/graph.py _ACC_DX_OPS): the other partial
+    gradient of input ``x`` as a [rows, in] buffer the dgrad GEMM accumulates into (beta=1), or
+    None. Marks it consumed so the executor does not add it again."""
+    acc = getattr(ctx, 'dx_acc', None)
+    if acc is None or acc.dtype != x.dtype or tuple(acc.shape) != tuple(x.shape) or not acc.is_contiguous():
+        return None
+    ctx.dx_acc_used = True
+    return acc.view(-1, acc.shape[-1])
 
 
 def bias_grad(dy2, b):
@@ -2017,7 +2031,8 @@ class MlpGeluFn(torch.autograd.Function):
             gemm(GEMM_TN, h, dy2, out=g2, beta=1)
         else:
             dw2 = gemm(GEMM_TN, h, dy2)
-        dx = gemm(GEMM_NT, dz, w1).view(x.shape)
+        acc = _dx_acc(ctx, x)
+        dx = gemm(GEMM_NT, dz, w1, out=acc, beta=1 if acc is not None else 0).view(x.shape)
         g1 = w1.grad
         if _acc_grad_ok(g1, w1, dz.dtype):
             gemm(GEMM_TN, x2, dz, out=g1, beta=1)

@@ -532,6 +532,13 @@ _FN_OPS = {}   # op type -> (autograd.Function class, predicate(torch args) -> b
 _DIRECT_GRAD = __import__('os').environ.get('PRA_STATIC_DIRECT_GRAD', '1') != '0'
 
 
+# direct-grad op types whose backward folds an existing partial gradient of their first input
+# into the input gradient (_fn_grad ``acc``)
+# (PRA_STATIC_GRAD_FOLD=0: separate `sum` ops, A/B timing)
+_ACC_DX_OPS = {'fused_linear', 'fused_mlp_gelu'} \
+    if __import__('os').environ.get('PRA_STATIC_GRAD_FOLD', '1') != '0' else set()
+
+
 def register_fn_op(op_type, fn_cls, pred=None):
     _FN_OPS[op_type] = (fn_cls, pred)
 
@@ -559,11 +566,18 @@ class _FnCtx:
         pass
 
 
-def _fn_grad(ctx, *out_grads):
+def _fn_grad(ctx, *out_grads, acc=None):
     """`<type>_grad` of a direct-grad op: Function.backward on the saved context; generic
-    autograd replay when the forward took the fallback path."""
+    autograd replay when the forward took the fallback path. ``acc`` (see _ACC_DX_OPS): the
+    other partial gradient of the op's first input, folded into its input gradient -- by the
+    Function itself when it can (a beta=1 GEMM into ``acc``), else by one add here."""
     if isinstance(ctx, _Ctx):
-        return _vjp(ctx, *out_grads)
+        res = _vjp(ctx, *out_grads)
+        if acc is not None:
+            res[0] = Tensor(_u(res[0]) + _u(acc).to(_u(res[0]).dtype))
+        return res
+    ctx.dx_acc = _u(acc) if acc is not None else None
+    ctx.dx_acc_used = False
     gs = []
     # a Function whose backward takes None for an unused output (``none_grads_ok``) is not
     # handed a zero tensor: e.g. the residual output of add+dropout+LayerNorm in a post-LN
@@ -584,7 +598,11 @@ def _fn_grad(ctx, *out_grads):
         i = ctx.slots.index(key)
         g = res[i] if i < len(res) else None
         out.append(Tensor(g) if g is not None else None)
+    if acc is not None and not ctx.dx_acc_used:
+        a = _u(acc)
+        out[0] = Tensor(a) if out[0] is None else Tensor(_u(out[0]) + a.to(_u(out[0]).dtype))
     ctx.saved_tensors = ()
+    ctx.dx_acc = None
     return out
 
 
@@ -669,6 +687,7 @@ def _build_backward(prog, targets, inputs=(), target_grads=None, no_grad_set=Non
         add_partial(t.vid, g.vid)
     for op in path:
         ogs = [final_grad(o) for o in op.out_vids]
+        acc_in = None
         if all(g is None for g in ogs):
             continue
         diff_in = []
@@ -691,13 +710,25 @@ def _build_backward(prog, targets, inputs=(), target_grads=None, no_grad_set=Non
         for p in dps:
             outs.append(_new_var(blk, list(_u(p).shape), _u(p).dtype).vid)
         args = [_VarRef(op.ctx_vid)] + [None if g is None else _VarRef(g) for g in ogs]
-        gop = OpDesc(op.type + '_grad', _fn_grad if op.type in _FN_OPS else _vjp, args, {},
-                     [op.ctx_vid] + [g for g in ogs if g is not None], outs,
+        # gradient-sum fusion: when the op's first input already has exactly one partial
+        # gradient from a later consumer (a residual stream feeding both a Linear / MLP and an
+        # add+LayerNorm), the grad op folds it into its input gradient (beta=1 GEMM) and the
+        # separate `sum` op disappears
+        if op.type in _ACC_DX_OPS and op.type in _FN_OPS and diff_in and op.args and \
+                isinstance(op.args[0], _VarRef) and op.args[0].vid == diff_in[0] and \
+                diff_in[0] not in final and len(partial.get(diff_in[0], [])) == 1:
+            acc_in = partial[diff_in[0]][0]
+        gop = OpDesc(op.type + '_grad', _fn_grad if op.type in _FN_OPS else _vjp, args,
+                     {'acc': _VarRef(acc_in)} if acc_in is not None else {},
+                     [op.ctx_vid] + [g for g in ogs if g is not None] +
+                     ([acc_in] if acc_in is not None else []), outs,
                      ('list', ['T'] * len(outs)), role='backward')
         gop.attrs['fwd'] = op
         if 'amp' in op.attrs:
             gop.attrs['amp'] = op.attrs['amp']
         blk.ops.append(gop)
+        if acc_in is not None:
+            partial[diff_in[0]] = []   # outs[0] now carries the folded partial as well
         for i, gv in zip(diff_in, outs[:len(diff_in)]):
             add_partial(i, gv)
         for p, gv in zip(dps, outs[len(diff_in):]):

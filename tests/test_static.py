@@ -235,6 +235,11 @@ def test_static_bert_direct_grad_ops_match_eager():
                   'fused_softmax_ce', 'fused_linear_nt', 'fused_bias_gelu'):
             assert types[('backward', t + '_grad', '_fn_grad')] >= 1, t
             assert not any(k[1] == t + '_grad' and k[2] != '_fn_grad' for k in types), t
+        # gradient-sum fusion: the residual stream's second partial gradient is folded into the
+        # Linear / MLP dgrad (beta=1 GEMM) instead of a separate `sum` op
+        ops = main_p.global_block().ops
+        folded = [op for op in ops if op.type in ('fused_linear_grad', 'fused_mlp_gelu_grad') and 'acc' in op.kwargs]
+        assert len(folded) >= 2 * cfg.num_hidden_layers, len(folded)
         exe = static.Executor()
         exe.run(startup)
         out = exe.run(main_p, feed={'ids': ids, 'pos': pos, 'lab': lab, 'nsp': nsp}, fetch_list=[loss_v])
