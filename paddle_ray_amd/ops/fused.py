@@ -2017,9 +2017,9 @@ class MlpGeluFn(torch.autograd.Function):
             dy2 = dy2.contiguous()
         x2 = x.reshape(-1, x.shape[-1])
         if _GEMM_MODE == 'auto' and not _MLP_DGELU_EPI and not (_MLP_DGELU_SHORTK and _nt_in_tree(dy2, w2)):
-            # dgrad on hipBLASLt, then ONE fused pass for gelu'(z) and the bias gradient
-            # (a short-K dgrad runs in-tree with gelu'(z) and the bias column sums in its epilogue)
-            dh = torch.mm(dy2, w2.t())
+            # dgrad (hipBLASLt, or the in-tree persistent kernel for a short K: the gemm() shape
+            # policy), then ONE fused pass for gelu'(z) and the bias gradient
+            dh = gemm(GEMM_NT, dy2, w2)
             dz, db1 = _dgelu_db(dh, z, ctx.approximate, ctx.b1)
         else:
             dz, db1 = gemm(GEMM_NT, dy2, w2, z=z, epi='dgelu_tanh' if ctx.approximate else 'dgelu',
