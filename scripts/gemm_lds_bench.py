@@ -202,6 +202,9 @@ def fused_main():
 
     if '--w4' in sys.argv:
         _native.lib().gemm_set_w4(7)
+    F._GEMM_MODE = 'mfma'   # the in-tree kernel for the NT dGELU GEMM too (the 'auto' policy would skip it)
+    if '--pts' in sys.argv:
+        _native.lib().gemm_set_pts(2)
     print("\n| fused op | ours us | hipBLASLt + separate kernel us | ratio |\n|---|---|---|---|")
     for name, fo, fh in (('fc1 fwd +bias+GELU+Z', ours_fwd, blas_fwd), ('fc2 dgrad +dGELU+db', ours_bwd, blas_bwd)):
         fo(); fh()
