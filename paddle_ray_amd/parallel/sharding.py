@@ -721,13 +721,53 @@ class ShardedOptimizer:
             return 0.0
         return wd
 
+    def _clip_local(self):
+        """ClipGradByValue / ClipGradByNorm on the owned gradient shards (reference
+        python/paddle/nn/clip.py semantics). By value is element-wise: each rank clamps its own
+        pieces. By norm is per parameter: the squared norms of every parameter's pieces are
+        summed in one vector all-reduce (plus the model-parallel group for TP-split parameters),
+        then each piece is scaled by clip_norm / max(||g_p||, clip_norm). Returns True when it
+        handled the clip."""
+        from ..nn.clip import ClipGradByValue, ClipGradByNorm
+        clip = self._inner._grad_clip
+        st = self.state
+        gs = st.shard_grads
+        if isinstance(clip, ClipGradByValue):
+            for gi, p, lo, hi, _ in self._pieces:
+                if getattr(p, 'need_clip', True):
+                    gs[gi][lo:hi].clamp_(clip.min, clip.max)
+            return True
+        if not isinstance(clip, ClipGradByNorm):
+            return False
+        params = [p for g in st.groups for p in g.params]  # same order on every rank
+        index = {id(p): i for i, p in enumerate(params)}
+        dev = gs[0].device if gs else torch.device('cpu')
+        sq = torch.zeros(len(params), dtype=torch.float32, device=dev)
+        for gi, p, lo, hi, _ in self._pieces:
+            if hi > lo:
+                sq[index[id(p)]] += gs[gi][lo:hi].float().square().sum()
+        if st.world > 1:
+            dist.all_reduce(sq, group=st.pg)
+        if self._mp_pg is not None:
+            split = torch.tensor([bool(getattr(p, 'is_distributed', False)) for p in params], device=dev)
+            part = torch.where(split, sq, torch.zeros_like(sq))
+            dist.all_reduce(part, group=self._mp_pg)
+            sq = torch.where(split, part, sq)
+        scale = clip.clip_norm / torch.clamp(torch.sqrt(sq), min=clip.clip_norm)
+        for gi, p, lo, hi, _ in self._pieces:
+            if getattr(p, 'need_clip', True) and hi > lo:
+                gs[gi][lo:hi].mul_(scale[index[id(p)]].to(gs[gi].dtype))
+        return True
+
     def _clip_coef(self):
         from ..nn.clip import ClipGradByGlobalNorm
         clip = self._inner._grad_clip
         if clip is None:
             return None
+        if self._clip_local():
+            return None
         if not isinstance(clip, ClipGradByGlobalNorm):
-            raise NotImplementedError("sharding supports ClipGradByGlobalNorm only")
+            raise NotImplementedError("sharding supports ClipGradByGlobalNorm / ClipGradByNorm / ClipGradByValue")
         st = self.state
         dev = st.shard_grads[0].device if st.shard_grads else torch.device('cpu')
 

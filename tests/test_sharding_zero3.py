@@ -312,3 +312,51 @@ def test_sharding_wraps_any_inner_optimizer(tmp_path, name, level):
         assert set(ref_opt) <= set(r['opt']), sorted(set(ref_opt) - set(r['opt']))
         for k, v in ref_opt.items():
             np.testing.assert_allclose(r['opt'][k], v, rtol=2e-5, atol=2e-6)
+
+
+def _clip_opt(paddle, params, kind):
+    clip = paddle.nn.ClipGradByValue(0.05) if kind == 'value' else paddle.nn.ClipGradByNorm(0.1)
+    return paddle.optimizer.AdamW(0.01, weight_decay=0.01, parameters=params, grad_clip=clip)
+
+
+def _clip_single(kind, steps=3):
+    import paddle_ray_amd as paddle
+    import paddle_ray_amd.nn.functional as F
+    m = _deep_mlp()
+    o = _clip_opt(paddle, m.parameters(), kind)
+    xs, ys = _data()
+    for _ in range(steps):
+        F.mse_loss(m(paddle.to_tensor(xs)), paddle.to_tensor(ys)).backward()
+        o.step()
+        o.clear_grad()
+    return [p.numpy() for p in m.parameters()]
+
+
+def _clip_worker(rank, world, kind, level, steps=3):
+    import paddle_ray_amd as paddle
+    import paddle_ray_amd.nn.functional as F
+    from paddle_ray_amd.distributed.sharding import group_sharded_parallel
+    m = _deep_mlp()
+    o = _clip_opt(paddle, m.parameters(), kind)
+    sm, so, _ = group_sharded_parallel(m, o, level, segment_size=0, bucket_mb=1)
+    xs, ys = _data()
+    n = len(xs) // world
+    xs, ys = xs[rank * n:(rank + 1) * n], ys[rank * n:(rank + 1) * n]
+    for _ in range(steps):
+        F.mse_loss(sm(paddle.to_tensor(xs)), paddle.to_tensor(ys)).backward()
+        so.step()
+        so.clear_grad()
+    sd = sm.state_dict()
+    return [sd[k].numpy() for k in sd]
+
+
+@pytest.mark.parametrize('kind', ['value', 'norm'])
+@pytest.mark.parametrize('level', ['os', 'os_g', 'p_g_os'])
+def test_sharding_clip_by_value_and_norm(tmp_path, kind, level):
+    """ClipGradByValue (element-wise on each rank's shard pieces) and ClipGradByNorm (per
+    parameter: squared norms of a parameter's pieces summed across ranks) under sharding give
+    the single-process result; the 6-layer MLP's parameters straddle the 2 ranks' shards."""
+    ref = _clip_single(kind)
+    for r in run_ranks(_clip_worker, 2, tmp_path, (kind, level)):
+        for a, b in zip(r, ref):
+            np.testing.assert_allclose(a, b, rtol=2e-4, atol=2e-5)
