@@ -800,6 +800,17 @@ bwd_dq_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restr
 // ============================================================================
 // WDS: also store dS^T (bf16/f16, unscaled) to dsT[bh][key][query] (row pitch Sqp, Skp rows) for
 // bwd_dq_ds_kernel, which then forms dQ = dS K without recomputing S and dP.
+// dK/dV kernel LDS: [2][Q | dO] tile images, lse / delta [2][64] each, the dS^T stage (4 waves x
+// 32 rows x 80 B), the keep-bit words (EXT), then the block's K / V images ([2][64][D] each)
+template <typename T, int D, bool EXT>
+__host__ __device__ constexpr int kKvOff() {
+  return 4 * kTile * D * (int)sizeof(T) + 4 * kTile * 4 + 4 * 32 * 80 + (EXT ? 2 * 256 * 4 : 0);
+}
+template <typename T, int D, bool EXT>
+__host__ __device__ constexpr int kDkdvLds() {
+  return kKvOff<T, D, EXT>() + 4 * kTile * D * (int)sizeof(T);
+}
+
 template <typename T, int D, bool CAUSAL, bool WDS, bool EXT = false>
 __global__ void __launch_bounds__(256, 1)
 bwd_dkdv_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restrict__ v, const T* __restrict__ dO,
@@ -844,16 +855,13 @@ bwd_dkdv_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __res
   const int64_t HD = (int64_t)H * D;
   const T* dob_ = dO + qrow0 * HD + (int64_t)hh * D;
 
-  typename V8<T>::type kf[NS], vf[NS];
-  {
-    const int kk = kvalid ? mykey : 0;
-#pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      kf[s] = frag_global<T>(kb_ + (int64_t)kk * kss, 16 * s + 8 * h, kvalid);
-      vf[s] = frag_global<T>(vb_ + (int64_t)kk * vss, 16 * s + 8 * h, kvalid);
-    }
-  }
-  wait_vmem_all();
+  // the block's 128 K and V rows live in LDS (two swizzled [64][D] images each, staged once by
+  // LDS-DMA below; rows >= Sk read as zero) and each tile re-reads the wave's fragments: holding
+  // them in registers for the whole kernel (64 VGPRs at D = 128) pushed the S / dP accumulators
+  // into AGPRs, and every softmax element then paid v_accvgpr reads / writes
+  const T* kvimg = reinterpret_cast<const T*>(smem + kKvOff<T, D, EXT>());
+  const T* Kw = kvimg + (wave >> 1) * kTile * D;        // image holding this wave's 32 keys
+  const T* Vw = kvimg + (2 + (wave >> 1)) * kTile * D;
   f32x16 acc_k[ND], acc_v[ND];
 #pragma unroll
   for (int i = 0; i < ND; ++i) { acc_k[i] = f32x16{}; acc_v[i] = f32x16{}; }
@@ -896,6 +904,18 @@ bwd_dkdv_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __res
       dma_dword(mb_rs, off, mb0 + (nb * 256 + wave * 64) * 4);
     }
   };
+  {
+    SwzDma<D, 256> kd2, vd2;
+    kd2.init(kb_, kss, Sk, wave, lane);
+    vd2.init(vb_, vss, Sk, wave, lane);
+    const uint32_t kv0 = lds0 + (uint32_t)kKvOff<T, D, EXT>();
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      kd2.issue(kv0 + (uint32_t)(j * kTile * D * sizeof(T)), (uint32_t)((int64_t)(kblk0 + 64 * j) * kss * 2), wave);
+      vd2.issue(kv0 + (uint32_t)((2 + j) * kTile * D * sizeof(T)), (uint32_t)((int64_t)(kblk0 + 64 * j) * vss * 2),
+                wave);
+    }
+  }
   if (ntiles > 0) load_tile(q_begin);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -957,6 +977,12 @@ bwd_dkdv_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __res
       // VALU: seeding the accumulator with -delta cost a v_xor + a v_accvgpr_write per element
       // (the S/dP accumulators live in AGPRs at this register pressure)
       f32x16 sa[2], da[2];
+      typename V8<T>::type kf[NS], vf[NS];
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        kf[s] = frag_rows<T, D>(Kw, lo, wave & 1, s);
+        vf[s] = frag_rows<T, D>(Vw, lo, wave & 1, s);
+      }
 #pragma unroll
       for (int nt = 0; nt < 2; ++nt) {
         sa[nt] = f32x16{};
@@ -1342,7 +1368,7 @@ static void launch_bwd(const void* q, const void* k, const void* v, const void* 
     const int Sqp = (Sq + 255) / 256 * 256;
     const int64_t dsbh = (int64_t)((Sk + 127) / 128 * 128) * Sqp;
     {
-      const size_t lds = 4 * kTile * D * sizeof(T) + 4 * kTile * sizeof(float) + 4 * 32 * 80;  // + dS^T stage
+      const size_t lds = kDkdvLds<T, D, false>();
       auto kern = bwd_dkdv_kernel<T, D, C, true>;
       hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       hipLaunchKernelGGL(kern, dim3(B * H, (Sk + 127) / 128), dim3(256), lds, s, (const T*)q, (const T*)k,
@@ -1366,7 +1392,7 @@ static void launch_bwd(const void* q, const void* k, const void* v, const void* 
     go(std::integral_constant<int, 8>{});
   }
   {
-    const size_t lds = 4 * kTile * D * sizeof(T) + 4 * kTile * sizeof(float);
+    const size_t lds = kDkdvLds<T, D, false>();
     auto kern = bwd_dkdv_kernel<T, D, C, false>;
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(kern, dim3(B * H, (Sk + 127) / 128), dim3(256), lds, s, (const T*)q, (const T*)k,
@@ -1398,7 +1424,7 @@ static void launch_bwd_ext(const void* q, const void* k, const void* v, const vo
   const int Sqp = (Sq + 255) / 256 * 256;
   const int64_t dsbh = (int64_t)((Sk + 127) / 128 * 128) * Sqp;
   {
-    const size_t lds = 4 * kTile * D * sizeof(T) + 4 * kTile * sizeof(float) + 4 * 32 * 80 + 2 * 256 * 4;
+    const size_t lds = kDkdvLds<T, D, true>();
     auto kern = bwd_dkdv_kernel<T, D, C, true, true>;
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(kern, dim3(B * H, (Sk + 127) / 128), dim3(256), lds, s, (const T*)q, (const T*)k,
