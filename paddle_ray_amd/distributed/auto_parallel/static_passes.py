@@ -16,10 +16,11 @@ Flow (what the reference's Parallelizer does for a static program)::
 
 Placement is a ``dims_mapping`` per tensor dim (-1 replicated, d = split over mesh dim d).
 Completion walks the forward ops once and applies a per-op rule: elementwise ops merge their
-operands' mappings (broadcast from the right), matmul / linear take batch dims from x and the
-output column from the weight and turn a contraction dim split on both sides into a PARTIAL sum,
-reductions over a split dim are partial, softmax / layer_norm / cross-entropy need their
-normalised axis whole, transpose permutes, everything else runs replicated.
+operands' mappings (broadcast from the right; a python-scalar operand keeps the tensor's),
+matmul / linear take batch dims from x and the output column from the weight and turn a
+contraction dim split on both sides into a PARTIAL sum, reductions over a split dim are partial,
+softmax / layer_norm / cross-entropy need their normalised axis whole, transpose permutes, an
+embedding with a hidden-split table yields hidden-split rows, everything else runs replicated.
 
 Partitioning re-records each op in a new Program through the normal static recording (so shape
 inference yields the local shapes) and inserts the communication the placements imply:
@@ -292,6 +293,14 @@ class Completer:
         if name in _BINARY and len(ins) == 2 and one:
             out = _merge(ins, nd_out[0])
             return [_align(out, len(i)) for i in ins], [out], {}
+        if name in _BINARY and len(ins) == 1 and one and len(ins[0]) == nd_out[0]:
+            return [list(ins[0])], [list(ins[0])], {}      # tensor (op) python scalar
+        if name == 'embedding' and len(ins) >= 2 and one:
+            ids, w = ins[0], ins[1]
+            if len(w) == 2 and w[0] < 0 and (w[1] < 0 or w[1] not in ids):
+                # hidden-split table: each rank looks up its columns for the ids it holds
+                return [list(ids), list(w)], [list(ids) + [w[1]]], {}
+            return self._replicated(ins, nd_out)
         if name in _REDUCE and len(ins) == 1 and one:
             x, nd = ins[0], len(ins[0])
             ia, ik = _REDUCE[name]

@@ -171,3 +171,49 @@ def test_partitioner_reshard_before_softmax(tmp_path):
         assert abs(o['loss'] - o['ref']) < 1e-5, o
         assert max(o['errs']) < 1e-5, o
         assert o['comm'] == ['ap_identity', 'ap_gather'], o['comm']
+
+
+def _run_embed(rank, world):
+    """Hidden-split embedding table -> scalar scale (keeps the split) -> row-parallel linear:
+    one all-reduce in the forward, and one SGD step equals the serial step."""
+    import paddle_ray_amd as paddle
+    import paddle_ray_amd.nn as nn
+    import paddle_ray_amd.nn.functional as F
+    from paddle_ray_amd import static
+    from paddle_ray_amd.distributed import auto_parallel as ap
+    paddle.enable_static()
+    paddle.seed(5)
+    mesh = ap.ProcessMesh([0, 1], ['mp'])
+    V, S_ = 32, 6
+    main = static.Program()
+    with static.program_guard(main):
+        ids = static.data('ids', [B, S_], 'int64')
+        lbl = static.data('lbl', [B, S_, 1], 'int64')
+        emb, head = nn.Embedding(V, H), nn.Linear(H, C)
+        ap.shard_tensor(emb.weight, mesh, [None, 'mp'])
+        ap.shard_tensor(head.weight, mesh, ['mp', None])
+        loss = F.cross_entropy(head(emb(ids) * 0.5), lbl)
+    params = [emb.weight, head.weight, head.bias]
+    dist, vmap, part = ap.parallelize(main)
+    local = [part.local_param(p) for p in params]
+    with static.program_guard(dist):
+        paddle.optimizer.SGD(0.5, parameters=local).minimize(vmap[loss])
+    with static.program_guard(main):
+        paddle.optimizer.SGD(0.5, parameters=params).minimize(loss)
+    rs = np.random.RandomState(9)
+    feed = {'ids': rs.randint(0, V, (B, S_)).astype('int64'), 'lbl': rs.randint(0, C, (B, S_, 1)).astype('int64')}
+    exe = static.Executor()
+    ref, = exe.run(main, feed=feed, fetch_list=[loss])
+    got, = exe.run(dist, feed=feed, fetch_list=[vmap[loss]])
+    errs = [float(np.abs(lp.numpy() - _slice(p.numpy(), part.ctx.get(p), mesh.shape, mesh.coord())).max())
+            for p, lp in zip(params, local)]
+    comm = [op.type for op in dist.global_block().ops if op.role == 'forward' and op.type.startswith('ap_')]
+    paddle.disable_static()
+    return {'ref': float(ref), 'loss': float(got), 'errs': errs, 'comm': comm}
+
+
+def test_partitioner_hidden_split_embedding(tmp_path):
+    for o in run_ranks(_run_embed, 2, tmp_path):
+        assert abs(o['loss'] - o['ref']) < 1e-5, o
+        assert max(o['errs']) < 1e-5, o
+        assert o['comm'] == ['ap_allreduce'], o['comm']
