@@ -1,6 +1,13 @@
 """auto_parallel.Engine (parity: reference python/paddle/distributed/auto_parallel/engine.py:
 Engine(model, loss, optimizer, metrics, cluster, strategy) with fit/evaluate/predict/save/load).
 
+Static mode (``paddle.enable_static()`` before the model is built, so ``shard_tensor`` only
+annotates): ``prepare(inputs_spec, labels_spec)`` records the serial program from the model and
+loss, completes and partitions it for this rank (static_passes.parallelize: local parameter
+shards, reshard, the implied all-reduces -- the reference's static flow), binds the optimizer to
+the local parameters and appends backward + update; fit / evaluate then feed every rank the
+whole batch and the program slices what each rank owns.
+
 Eager MI355X design: no program completion/partitioning. Batches are split over mesh axis 0
 (DistributedBatchSampler with that axis' size/coordinate); after backward every gradient is
 all-reduced (mean) over the mesh axes its parameter is replicated on and data is split over —
@@ -162,9 +169,55 @@ class Engine:
             out[name] = t.numpy() if isinstance(t, Tensor) else t
         return out
 
+    # ------------------------------------------------------------------ static programs
+    @staticmethod
+    def _static_on():
+        from ...static import _STATIC
+        return _STATIC[0]
+
+    def _build_static(self, inputs_spec, labels_spec):
+        """Serial program from the model + loss, completed and partitioned for this rank."""
+        from ... import static
+        from .static_passes import parallelize
+        assert inputs_spec, "a static Engine needs inputs_spec (paddle.static.InputSpec list)"
+        serial = static.Program()
+        with static.program_guard(serial):
+            ins = [static.data(sp.name or f'input{i}', list(sp.shape), sp.dtype)
+                   for i, sp in enumerate(_to_list(inputs_spec))]
+            lbs = [static.data(sp.name or f'label{i}', list(sp.shape), sp.dtype)
+                   for i, sp in enumerate(_to_list(labels_spec))]
+            outs = self._model(*ins)
+            loss = self._compute_loss(outs, lbs)
+        dist, vmap, part = parallelize(serial)
+        local = [part.local_param(p) for p in self._model.parameters() if id(p) in part.params]
+        self._dist = {'program': dist, 'feeds': [v.name for v in ins + lbs], 'n_in': len(ins),
+                      'loss': vmap[loss], 'outs': [vmap[o] for o in _to_list(outs)],
+                      'partitioner': part, 'serial': serial, 'params': local}
+        eval_prog = dist.clone(for_test=True)
+        if self._optimizer is not None:
+            opt = self._optimizer
+            opt._param_groups = []                     # update this rank's shards
+            opt._add_param_group({'params': [p for p in local if not p.stop_gradient]})
+            with static.program_guard(dist):
+                opt.minimize(vmap[loss], parameters=[p for p in local if not p.stop_gradient])
+        self._dist['eval_program'] = eval_prog
+        self._exe = static.Executor()
+
+    def _static_feed(self, batch, split):
+        inputs, labels = self._split(batch, split)
+        vals = [x.numpy() if isinstance(x, Tensor) else np.asarray(x) for x in inputs + labels]
+        return dict(zip(self._dist['feeds'], vals))
+
+    def local_parameters(self):
+        """This rank's parameter shards of the partitioned static program."""
+        return list(self._dist['params']) if getattr(self, '_dist', None) else list(self._model.parameters())
+
     # ------------------------------------------------------------------ public API
     def prepare(self, inputs_spec=None, labels_spec=None, inputs=None, labels=None, main_program=None,
                 startup_program=None, mode='train'):
+        if self._static_on():
+            self._build_static(inputs_spec, labels_spec)
+            return self
         self._resolve_mesh()
         return self
 
@@ -172,6 +225,9 @@ class Engine:
             log_freq=10, save_dir=None, save_freq=1, valid_data=None, valid_sample_split=None, valid_freq=1,
             valid_steps=None, collate_fn=None, callbacks=None, verbose=2, nvprof_range=None):
         assert self._optimizer is not None, "fit() needs an optimizer"
+        if getattr(self, '_dist', None) is not None:
+            return self._fit_static(train_data, train_sample_split, batch_size, epochs, steps_per_epoch,
+                                    log_freq, collate_fn, verbose)
         self._model.train()
         loader = self._loader(train_data, batch_size, False, collate_fn)
         history = {'loss': []}
@@ -201,9 +257,40 @@ class Engine:
         self.history = history
         return history
 
+    def _static_loader(self, data, batch_size, collate_fn):
+        from ...io import DataLoader, BatchSampler, Dataset
+        if not isinstance(data, Dataset) and hasattr(data, '__iter__') and not hasattr(data, '__getitem__'):
+            return data
+        # every rank is fed the whole batch: the partitioned program slices its own share
+        return DataLoader(data, batch_sampler=BatchSampler(data, batch_size=batch_size, shuffle=False),
+                          collate_fn=collate_fn)
+
+    def _fit_static(self, data, split, batch_size, epochs, steps_per_epoch, log_freq, collate_fn, verbose):
+        d = self._dist
+        history = {'loss': []}
+        for epoch in range(epochs):
+            for step, batch in enumerate(self._static_loader(data, batch_size, collate_fn)):
+                if steps_per_epoch is not None and step >= steps_per_epoch:
+                    break
+                loss, = self._exe.run(d['program'], feed=self._static_feed(batch, split), fetch_list=[d['loss']])
+                history['loss'].append(float(loss))
+                if verbose and log_freq and step % log_freq == 0 and C.get_rank() == 0:
+                    print(f"[Engine] epoch {epoch} step {step} loss {float(loss):.6f}")
+        self.history = history
+        return history
+
     @torch.no_grad()
     def evaluate(self, valid_data, valid_sample_split=None, batch_size=1, steps=None, log_freq=10,
                  collate_fn=None, callbacks=None, verbose=2):
+        if getattr(self, '_dist', None) is not None:
+            d, losses = self._dist, []
+            for step, batch in enumerate(self._static_loader(valid_data, batch_size, collate_fn)):
+                if steps is not None and step >= steps:
+                    break
+                loss, = self._exe.run(d['eval_program'], feed=self._static_feed(batch, valid_sample_split),
+                                      fetch_list=[d['loss']])
+                losses.append(float(loss))
+            return {'loss': float(np.mean(losses))} if losses else {}
         self._model.eval()
         loader = self._loader(valid_data, batch_size, False, collate_fn)
         for m in self._metrics:

@@ -157,6 +157,10 @@ def annotate(t, mesh, shard_spec):
     shape = [s if s >= 0 else full for s in t.shape]   # unknown dims: checked when fed
     mapping = _spec_to_mapping(shard_spec, shape, mesh)
     prog.__dict__.setdefault('_dist_annotations', {})[_key(t)] = (mesh, mapping, t)
+    if isinstance(t, Parameter):
+        # a parameter may be annotated where the model is built and used in another program
+        # (auto_parallel.Engine records its own): the placement travels with the parameter
+        t.__dict__['_pra_placement'] = (mesh, list(mapping))
     return t
 
 
@@ -168,7 +172,11 @@ class DistributedContext:
 
     def __init__(self, program=None, mesh=None):
         self.program = program or G.default_main_program()
-        ann = self.program.__dict__.get('_dist_annotations', {})
+        ann = dict(self.program.__dict__.get('_dist_annotations', {}))
+        for p in self.program._params.values():
+            pl = p.__dict__.get('_pra_placement')
+            if pl is not None and _key(p) not in ann:
+                ann[_key(p)] = (pl[0], pl[1], p)
         if mesh is None:
             meshes = {hash(m): m for m, _, _ in ann.values()}
             assert len(meshes) <= 1, "one process mesh per program"

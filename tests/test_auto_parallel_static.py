@@ -217,3 +217,63 @@ def test_partitioner_hidden_split_embedding(tmp_path):
         assert abs(o['loss'] - o['ref']) < 1e-5, o
         assert max(o['errs']) < 1e-5, o
         assert o['comm'] == ['ap_allreduce'], o['comm']
+
+
+def _engine_static(rank, world, annotate):
+    """auto_parallel.Engine on a static program: the model is built in static mode (shard_tensor
+    annotates its weights), prepare() completes + partitions, fit() trains."""
+    import paddle_ray_amd as paddle
+    import paddle_ray_amd.nn as nn
+    import paddle_ray_amd.nn.functional as F
+    from paddle_ray_amd.distributed import auto_parallel as ap
+    from paddle_ray_amd.static import InputSpec
+    from paddle_ray_amd.io import Dataset
+    paddle.enable_static()
+    paddle.seed(3)
+    mesh = ap.ProcessMesh([0, 1], ['mp'])
+
+    class MLP(nn.Layer):
+        def __init__(self):
+            super().__init__()
+            self.l1, self.l2 = nn.Linear(H, F_), nn.Linear(F_, C)
+            if annotate:
+                ap.shard_tensor(self.l1.weight, mesh, [None, 'mp'])
+                ap.shard_tensor(self.l1.bias, mesh, ['mp'])
+                ap.shard_tensor(self.l2.weight, mesh, ['mp', None])
+
+        def forward(self, x):
+            return self.l2(F.relu(self.l1(x)))
+
+    class DS(Dataset):
+        def __init__(self):
+            rs = np.random.RandomState(0)
+            self.x = rs.randn(32, H).astype('float32')
+            self.y = rs.randint(0, C, (32, 1)).astype('int64')
+
+        def __getitem__(self, i):
+            return self.x[i], self.y[i]
+
+        def __len__(self):
+            return 32
+
+    model = MLP()
+    opt = paddle.optimizer.SGD(0.2, parameters=model.parameters())
+    eng = ap.Engine(model, nn.CrossEntropyLoss(), opt)
+    eng.prepare([InputSpec([B, H], 'float32', 'x')], [InputSpec([B, 1], 'int64', 'y')])
+    hist = eng.fit(DS(), batch_size=B, epochs=2, verbose=0)
+    ev = eng.evaluate(DS(), batch_size=B, verbose=0)
+    shapes = [list(p.shape) for p in eng.local_parameters()]
+    paddle.disable_static()
+    return {'loss': hist['loss'], 'eval': ev['loss'], 'shapes': shapes}
+
+
+def test_engine_static_partitioned_matches_serial(tmp_path):
+    (tmp_path / 'ref').mkdir()
+    (tmp_path / 'tp').mkdir()
+    ref = run_ranks(_engine_static, 2, tmp_path / 'ref', (False,))[0]
+    res = run_ranks(_engine_static, 2, tmp_path / 'tp', (True,))
+    assert res[0]['shapes'][0] == [H, F_ // 2] and res[0]['shapes'][2] == [F_ // 2, C]
+    for o in res:
+        np.testing.assert_allclose(o['loss'], ref['loss'], rtol=1e-5, atol=1e-6)
+        assert abs(o['eval'] - ref['eval']) < 1e-5
+    assert ref['loss'][-1] < ref['loss'][0]
