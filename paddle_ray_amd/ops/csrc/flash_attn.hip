@@ -539,12 +539,15 @@ fwd_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restrict
         float p = fexp2(fmaf(s_acc[mt][i], scale_log2, -m_use));
         ps += p;  // the softmax denominator sums the undropped probabilities
         if constexpr ((XF & XF_DROP) != 0) {
-          // elements i, i+1 (i even) are the adjacent keys of one hash pair
+          // elements i, i+1 (i even) are the adjacent keys of one hash pair. A dropped score
+          // is zeroed here; the kept ones are scaled by 1/(1-p) once, in the output
+          // normalisation. The keep bit goes to bit acc_row(i, 0) (constant); the lane half's
+          // 4h offset is applied to the whole word below.
           const int kk = k0 + 32 * mt + acc_row(i & ~1, h);
           const uint32_t hs = fa_hash2(dkey, myq, kk >> 1);
-          const float z = fa_keep(ext, (i & 1) ? (hs >> 16) : (hs & 0xffffu));
-          kbits[mt] |= (z != 0.f ? 1u : 0u) << acc_row(i, h);
-          p *= z;
+          const bool keep = ((i & 1) ? (hs >> 16) : (hs & 0xffffu)) >= ext.thr;
+          kbits[mt] |= keep ? (1u << acc_row(i, 0)) : 0u;
+          p = keep ? p : 0.f;
         }
         s_acc[mt][i] = p;
       }
@@ -552,7 +555,8 @@ fwd_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restrict
       if (ext.dbits) {  // both lane halves' 16 bits -> one word per (query, 32 keys)
 #pragma unroll
         for (int mt = 0; mt < 2; ++mt) {
-          const uint32_t w = kbits[mt] | __shfl_xor(kbits[mt], 32, 64);
+          const uint32_t kb = kbits[mt] << (4 * h);
+          const uint32_t w = kb | __shfl_xor(kb, 32, 64);
           if (h == 0 && myq < Sq && mt < nlive)
             ext.dbits[((int64_t)bh * SqM + myq) * ext.dbits_ld + (k0 >> 5) + mt] = w;
         }
@@ -596,7 +600,10 @@ fwd_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restrict
   }
 
   if (myq < Sq) {
-    const float inv = l_run > 0.f ? 1.f / l_run : 0.f;
+    float inv = l_run > 0.f ? 1.f / l_run : 0.f;
+    if constexpr (EXT) {
+      if (ext.xf & XF_DROP) inv *= ext.inv_keep;  // the kept probabilities' 1/(1-p)
+    }
     T* orow = o + (qrow0 + myq) * ((int64_t)H * D) + (int64_t)hh * D;
 #pragma unroll
     for (int dt = 0; dt < ND; ++dt)
