@@ -819,7 +819,7 @@ __host__ __device__ constexpr int kDkdvLds() {
 }
 
 template <typename T, int D, bool CAUSAL, bool WDS, bool EXT = false>
-__global__ void __launch_bounds__(256, 1)
+__global__ void __launch_bounds__(256, D == 64 ? 2 : 1)
 bwd_dkdv_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restrict__ v, const T* __restrict__ dO,
                 const float* __restrict__ lse, const float* __restrict__ delta, T* __restrict__ dk,
                 T* __restrict__ dv, int H, int SqM, int SkM, int64_t qsb, int64_t qss, int64_t qsh, int64_t ksb,
