@@ -2,7 +2,8 @@
 Engine(model, loss, optimizer, metrics, cluster, strategy) with fit/evaluate/predict/save/load).
 
 Static mode (``paddle.enable_static()`` before the model is built, so ``shard_tensor`` only
-annotates): ``prepare(inputs_spec, labels_spec)`` records the serial program from the model and
+annotates; reference engine.py:513 _build, :670 _plan, :698 _parallel, :1272 prepare):
+``prepare(inputs_spec, labels_spec)`` records the serial program from the model and
 loss, completes and partitions it for this rank (static_passes.parallelize: local parameter
 shards, reshard, the implied all-reduces -- the reference's static flow), binds the optimizer to
 the local parameters and appends backward + update; fit / evaluate then feed every rank the

@@ -166,7 +166,7 @@ def annotate(t, mesh, shard_spec):
 
 class DistributedContext:
     """Placements of a serial program's tensors on one process mesh (reference
-    dist_context.py DistributedContext). ``mapping[key]`` = dims_mapping; ``plans`` = per
+    python/paddle/distributed/auto_parallel/dist_context.py:51 DistributedContext). ``mapping[key]`` = dims_mapping; ``plans`` = per
     forward op the operand placements it runs with, its output placements and its partial
     (pending all-reduce) mesh dims."""
 
@@ -240,7 +240,8 @@ def _align(out, nd_in):
 
 
 class Completer:
-    """Forward placement completion (reference completion.py Completer): one pass over the
+    """Forward placement completion (reference auto_parallel/completion.py:107 Completer,
+    :936 complete_forward_annotation): one pass over the
     forward ops in program order, each op's SPMD rule mapping operand placements to the
     placements it runs with and produces."""
 
@@ -374,8 +375,9 @@ def _needs_grad(a):
 
 
 class Partitioner:
-    """This rank's program from a completed serial program (reference partitioner.py for the
-    local shapes / parameters, reshard.py for the inserted communication). ``partition()``
+    """This rank's program from a completed serial program (reference auto_parallel/
+    partitioner.py:38 Partitioner / :69 partition for the local shapes / parameters,
+    reshard.py:1006 Resharder / :2672 reshard for the inserted communication). ``partition()``
     returns ``(program, var_map)``: ``var_map[serial_var]`` is its local Variable."""
 
     def __init__(self, ctx, rank=None):
