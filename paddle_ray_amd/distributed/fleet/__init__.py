@@ -36,9 +36,15 @@ class DistributedStrategy:
         self.gradient_merge = False
         self.gradient_merge_configs = {'k_steps': 1, 'avg': True}
         self.lamb = False
+        self.lamb_configs = {'lamb_weight_decay': 0.01, 'exclude_from_weight_decay': []}
         self.lars = False
+        self.lars_configs = {'lars_coeff': 0.001, 'lars_weight_decay': 0.0005, 'epsilon': 0.0,
+                             'exclude_from_weight_decay': []}
         self.dgc = False
+        self.dgc_configs = {'rampup_begin_step': 0, 'rampup_step': 1, 'sparsity': [0.999]}
         self.localsgd = False
+        self.localsgd_configs = {'k_steps': 1, 'begin_step': 1}
+        self.adaptive_localsgd = False
         self.fuse_all_reduce_ops = True
         self.fuse_grad_size_in_MB = 64
         self.find_unused_parameters = False
@@ -255,8 +261,22 @@ class Fleet:
         if strategy is not None:
             self._strategy = strategy
         if self._hcg is None:
-            return optimizer
+            from ...static import _static_mode_enabled
+            if not _static_mode_enabled():
+                return optimizer
+            self.init(is_collective=True, strategy=self._strategy)
         hcg, st = self._hcg, self._strategy
+        from .meta_optimizers import apply_optimizer_swaps
+        from ...static import _static_mode_enabled
+        if _static_mode_enabled():
+            # static programs: the meta-optimizer chain runs at minimize() (meta_optimizers.py)
+            opt = StaticFleetOptimizer(optimizer, hcg, st)
+            self._wrapped_optimizer = opt
+            return opt
+        if st.localsgd:
+            raise NotImplementedError("strategy.localsgd is a static-graph meta optimizer "
+                                      "(reference localsgd_optimizer.py); in dygraph use DataParallel")
+        optimizer = apply_optimizer_swaps(optimizer, st)
         state = getattr(self, '_sharded_state', None)
         if state is not None:
             from ...parallel.sharding import ShardedOptimizer
@@ -287,6 +307,13 @@ class Fleet:
         if state is not None:
             return state.reducer if state.stage in (1, 2) else None
         return getattr(m, '_reducer', None)
+
+    def minimize(self, loss, startup_program=None, parameter_list=None, no_grad_set=None):
+        """fleet.minimize (reference fleet.py:1216): the distributed optimizer's minimize."""
+        opt = getattr(self, '_wrapped_optimizer', None)
+        if opt is None:
+            raise RuntimeError("call fleet.distributed_optimizer(optimizer) before fleet.minimize")
+        return opt.minimize(loss, startup_program, parameter_list, no_grad_set)
 
     def distributed_scaler(self, scaler):
         """HybridParallelGradScaler: found_inf is MAX-reduced over every hybrid group."""
@@ -522,8 +549,35 @@ class HybridParallelOptimizer:
     def clear_grad(self, set_to_zero=True):
         self._inner_opt.clear_grad(set_to_zero)
 
-    def minimize(self, loss, *a, **k):
-        return self._inner_opt.minimize(loss, *a, **k)
+    def minimize(self, loss, startup_program=None, parameters=None, no_grad_set=None):
+        from ...static import _static_mode_enabled
+        if _static_mode_enabled():
+            from .meta_optimizers import static_minimize
+            return static_minimize(self._inner_opt, loss, self._strategy, self._hcg, parameters)
+        return self._inner_opt.minimize(loss, startup_program, parameters, no_grad_set)
+
+    def __getattr__(self, k):
+        return getattr(self._inner_opt, k)
+
+
+class StaticFleetOptimizer:
+    """``fleet.distributed_optimizer`` in static mode: ``minimize`` appends the backward and the
+    collective-training rewrite of meta_optimizers.static_minimize (bucketed async gradient
+    all-reduce, gradient merge, sharding stage 1, localsgd, lamb / lars swaps, amp)."""
+
+    def __init__(self, optimizer, hcg, strategy):
+        from .meta_optimizers import apply_optimizer_swaps
+        from ...static.amp import OptimizerWithMixedPrecision
+        if isinstance(optimizer, OptimizerWithMixedPrecision):
+            optimizer._optimizer = apply_optimizer_swaps(optimizer._optimizer, strategy)
+            self._inner_opt = optimizer
+        else:
+            self._inner_opt = apply_optimizer_swaps(optimizer, strategy)
+        self._hcg, self._strategy = hcg, strategy
+
+    def minimize(self, loss, startup_program=None, parameter_list=None, no_grad_set=None):
+        from .meta_optimizers import static_minimize
+        return static_minimize(self._inner_opt, loss, self._strategy, self._hcg, parameter_list)
 
     def __getattr__(self, k):
         return getattr(self._inner_opt, k)

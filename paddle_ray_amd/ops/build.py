@@ -17,6 +17,7 @@ import concurrent.futures as cf
 import hashlib
 import json
 import os
+import re
 import subprocess
 import sys
 import sysconfig
@@ -64,6 +65,7 @@ def _run(cmd):
     return r
 
 
+@__import__('functools').lru_cache(None)
 def _hipcc_version():
     try:
         r = subprocess.run([HIPCC, '--version'], capture_output=True, text=True)
@@ -79,12 +81,43 @@ def _stamp_path():
     return _out_path() + '.sources'
 
 
+_HIP_FLAGS = ('-O3', '-fPIC', '-std=c++17', '-munsafe-fp-atomics')
+
+
+def _toolchain_key():
+    """hipcc version + compile flags: part of the library stamp, so a ROCm / flag change
+    rebuilds instead of keeping a library compiled by another toolchain."""
+    return hashlib.sha256((_hipcc_version() + '\0' + ' '.join(_HIP_FLAGS) + '\0' + ARCH).encode()).hexdigest()[:16]
+
+
+def _stamp():
+    return sources_hash() + ' ' + _toolchain_key()
+
+
+_INC = re.compile(r'^\s*#\s*include\s+"([^"]+)"')
+
+
+def _header_closure(src, seen=None):
+    """The in-tree headers ``src`` includes, transitively (per-object rebuild keys: a header
+    edit recompiles only the translation units that include it)."""
+    seen = set() if seen is None else seen
+    with open(src) as f:
+        for line in f:
+            m = _INC.match(line)
+            if m:
+                h = os.path.join(CSRC, m.group(1))
+                if os.path.exists(h) and h not in seen:
+                    seen.add(h)
+                    _header_closure(h, seen)
+    return sorted(seen)
+
+
 def build(force=False, verbose=True):
     # fast path: the library next to the sources was linked from exactly these sources (the
     # sidecar travels with the .so; the object cache under build/ does not reach the GPU box)
     if not force and os.path.exists(_out_path()) and os.path.exists(_stamp_path()):
         with open(_stamp_path()) as f:
-            if f.read().strip() == sources_hash():
+            if f.read().strip() == _stamp():
                 if verbose:
                     print(f"up to date {_out_path()} (sources {sources_hash()[:12]})")
                 return _out_path()
@@ -95,16 +128,14 @@ def build(force=False, verbose=True):
             manifest = json.load(f)
     except (OSError, ValueError):
         manifest = {}
-    headers = sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith('.h'))
     hip_srcs = sorted(f for f in os.listdir(CSRC) if f.endswith('.hip'))
     jobs, keys, objs = [], {}, []
     for f in hip_srcs:
         src = os.path.join(CSRC, f)
         obj = os.path.join(BUILD, f.replace('.hip', '.o'))
         objs.append(obj)
-        cmd = [HIPCC, f'--offload-arch={ARCH}', '-O3', '-fPIC', '-std=c++17', '-c', src, '-o', obj,
-               '-I', CSRC, '-munsafe-fp-atomics']
-        keys[os.path.basename(obj)] = _digest([src] + headers, cmd)
+        cmd = [HIPCC, f'--offload-arch={ARCH}', *_HIP_FLAGS, '-c', src, '-o', obj, '-I', CSRC]
+        keys[os.path.basename(obj)] = _digest([src] + _header_closure(src), cmd + [_hipcc_version()])
         if force or _needs(obj, keys[os.path.basename(obj)], manifest):
             jobs.append(cmd)
     bsrc = os.path.join(CSRC, 'bindings.cpp')
@@ -138,7 +169,7 @@ def build(force=False, verbose=True):
     with open(_manifest_path(), 'w') as f:
         json.dump(manifest, f, indent=1)
     with open(_stamp_path(), 'w') as f:
-        f.write(info['sources_sha256'] + '\n')
+        f.write(_stamp() + '\n')
     if verbose:
         print(f"built {out} ({len(jobs)} objects recompiled, sources {info['sources_sha256'][:12]})")
     return out

@@ -38,6 +38,15 @@ int launch_w4_l(const void* A, const void* B, const void* bias, void* C, void* Z
     case kGeluTanh: launch_w4<CF, T, AK, BK, kGeluTanh>(A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, beta, splits, ws, s); return 0;
     case kDGeluErf: launch_w4<CF, T, AK, BK, kDGeluErf>(A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, beta, splits, ws, s); return 0;
     case kDGeluTanh: launch_w4<CF, T, AK, BK, kDGeluTanh>(A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, beta, splits, ws, s); return 0;
+    case kGeluErfD:
+      if constexpr (AK && !BK) { launch_w4<CF, T, AK, BK, kGeluErfD>(A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, beta, splits, ws, s); return 0; }
+      return -1;
+    case kGeluTanhD:
+      if constexpr (AK && !BK) { launch_w4<CF, T, AK, BK, kGeluTanhD>(A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, beta, splits, ws, s); return 0; }
+      return -1;
+    case kMulZ:
+      if constexpr (AK && BK) { launch_w4<CF, T, AK, BK, kMulZ>(A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, beta, splits, ws, s); return 0; }
+      return -1;
     default: return -1;  // (ReLU: the 8-wave kernel)
   }
 }

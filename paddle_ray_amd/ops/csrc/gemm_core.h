@@ -52,7 +52,18 @@ template <> __device__ __forceinline__ uint32_t pack2<f16>(float a, float b) {
   return (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)a) | ((uint32_t)__builtin_bit_cast(uint16_t, (_Float16)b) << 16);
 }
 
-enum Epi : int { kNone = 0, kGeluErf = 1, kGeluTanh = 2, kRelu = 3, kDGeluErf = 4, kDGeluTanh = 5 };
+// kGelu*D: forward GELU whose Z output receives gelu'(pre-activation) instead of the pre-activation
+// (the only thing the backward needs from it); kMulZ: C = acc * Z, the backward's dGELU as one
+// multiply (with the derivative saved by the forward, the dgrad epilogue carries no transcendental
+// work: profiles/r4/fused_dgelu_epilogue.md measured that VALU serialised behind the K loop).
+enum Epi : int {
+  kNone = 0, kGeluErf = 1, kGeluTanh = 2, kRelu = 3, kDGeluErf = 4, kDGeluTanh = 5,
+  kGeluErfD = 6, kGeluTanhD = 7, kMulZ = 8
+};
+// epilogues that read Z and scale the product by a per-element factor (the dgrad side)
+constexpr bool epi_scales(int E) { return E == kDGeluErf || E == kDGeluTanh || E == kMulZ; }
+// forward GELUs that store the derivative into Z
+constexpr bool epi_gd(int E) { return E == kGeluErfD || E == kGeluTanhD; }
 
 // tanh(u) = 1 - 2 / (exp(2u) + 1): one v_exp + one v_rcp (saturates cleanly at +-1)
 __device__ __forceinline__ float fast_tanh(float u) {
@@ -72,10 +83,34 @@ __device__ __forceinline__ float dgelu_erf(float x) { return dgelu_erf_fast(x); 
 
 template <int E>
 __device__ __forceinline__ float act(float x) {
-  if (E == kGeluErf) return gelu_erf(x);
-  if (E == kGeluTanh) return gelu_tanh(x);
+  if (E == kGeluErf || E == kGeluErfD) return gelu_erf(x);
+  if (E == kGeluTanh || E == kGeluTanhD) return gelu_tanh(x);
   if (E == kRelu) return fmaxf(x, 0.f);
   return x;
+}
+// gelu(x) and gelu'(x) sharing the one transcendental
+template <int E>
+__device__ __forceinline__ float act_d(float x, float& d) {
+  if constexpr (E == kGeluTanhD) {
+    const float u = 0.79788456080286536f * (x + 0.044715f * x * x * x);
+    const float t = fast_tanh(u);
+    const float h = 0.5f * (1.f + t);
+    d = h + 0.5f * x * (1.f - t * t) * 0.79788456080286536f * (1.f + 0.134145f * x * x);
+    return x * h;
+  } else {
+    const float u = x * 0.70710678118654752f;
+    const float e = __expf(-u * u);
+    const float h = 0.5f * (1.f + erf_from_exp(u, e));
+    d = h + x * 0.3989422804014327f * e;
+    return x * h;
+  }
+}
+// the dgrad-side factor of Z
+template <int E>
+__device__ __forceinline__ float zfac(float z) {
+  if constexpr (E == kMulZ) return z;
+  else if constexpr (E == kDGeluErf) return dgelu_erf(z);
+  else return dgelu_tanh(z);
 }
 
 constexpr int BM = 256, BN = 256, BKT = 64;  // the GEMM tile (conv configs below narrow BN)
@@ -801,7 +836,7 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_lds_kernel(const uint16_t* __r
         moff[u] = (int64_t)(ok[u] ? m : 0);
         lo[u] = *reinterpret_cast<const f32x4*>(img + rr * PITCH + ucol);
         hi[u] = *reinterpret_cast<const f32x4*>(img + rr * PITCH + ucol + 4);
-        if (E == kDGeluErf || E == kDGeluTanh) {
+        if (epi_scales(E)) {
           if (ok[u]) gz[u] = *reinterpret_cast<const uint4*>(Z + moff[u] * ldz + n);
         } else if (BETA) {
           if (ok[u]) gz[u] = *reinterpret_cast<const uint4*>(C + moff[u] * ldc + n);
@@ -814,14 +849,22 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_lds_kernel(const uint16_t* __r
         float v[8] = {lo[u][0], lo[u][1], lo[u][2], lo[u][3], hi[u][0], hi[u][1], hi[u][2], hi[u][3]};
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] += bv[e];
-        if (E == kDGeluErf || E == kDGeluTanh) {
+        if constexpr (epi_scales(E)) {
           const uint32_t w4[4] = {gz[u].x, gz[u].y, gz[u].z, gz[u].w};
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const float z0 = to_f<T>(w4[e] & 0xffff), z1 = to_f<T>(w4[e] >> 16);
-            v[2 * e] *= (E == kDGeluErf) ? dgelu_erf(z0) : dgelu_tanh(z0);
-            v[2 * e + 1] *= (E == kDGeluErf) ? dgelu_erf(z1) : dgelu_tanh(z1);
+            v[2 * e] *= zfac<E>(z0);
+            v[2 * e + 1] *= zfac<E>(z1);
           }
+        } else if constexpr (epi_gd(E)) {
+          float d[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = act_d<E>(v[e], d[e]);
+          uint4 o;
+          o.x = pack2<T>(d[0], d[1]); o.y = pack2<T>(d[2], d[3]);
+          o.z = pack2<T>(d[4], d[5]); o.w = pack2<T>(d[6], d[7]);
+          *reinterpret_cast<uint4*>(Z + m * ldz + n) = o;
         } else if (E != kNone) {
           if (Z) {
             uint4 o;
@@ -832,7 +875,7 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_lds_kernel(const uint16_t* __r
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] = act<E>(v[e]);
         }
-        if (BETA && !(E == kDGeluErf || E == kDGeluTanh)) {
+        if (BETA && !epi_scales(E)) {
           const uint32_t w4[4] = {gz[u].x, gz[u].y, gz[u].z, gz[u].w};
 #pragma unroll
           for (int e = 0; e < 4; ++e) { v[2 * e] += to_f<T>(w4[e] & 0xffff); v[2 * e + 1] += to_f<T>(w4[e] >> 16); }
@@ -911,7 +954,15 @@ __global__ void splitk_reduce_k(const float* __restrict__ ws, int splits, const 
     v[0] += to_f<T>(bb.x & 0xffff); v[1] += to_f<T>(bb.x >> 16);
     v[2] += to_f<T>(bb.y & 0xffff); v[3] += to_f<T>(bb.y >> 16);
   }
-  if (E != kNone) {
+  if constexpr (epi_gd(E)) {
+    float d[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = act_d<E>(v[r], d[r]);
+    uint2 o;
+    o.x = pack2<T>(d[0], d[1]);
+    o.y = pack2<T>(d[2], d[3]);
+    *reinterpret_cast<uint2*>(Z + (int64_t)m * ldz + n) = o;
+  } else if (E != kNone) {
     if (Z) {
       uint2 o;
       o.x = pack2<T>(v[0], v[1]);

@@ -166,6 +166,16 @@ int launch_l(const void* A, const void* B, const void* bias, void* C, void* Z, f
     case kRelu: launch_e<T, AK, BK, kRelu>(A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, beta, splits, ws, s); break;
     case kDGeluErf: launch_e<T, AK, BK, kDGeluErf>(A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, beta, splits, ws, s); break;
     case kDGeluTanh: launch_e<T, AK, BK, kDGeluTanh>(A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, beta, splits, ws, s); break;
+    // derivative-saving forward GELU (x·W only) and its multiply-by-Z dgrad (dy·Wᵀ only)
+    case kGeluErfD:
+      if constexpr (AK && !BK) { launch_e<T, AK, BK, kGeluErfD>(A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, beta, splits, ws, s); break; }
+      return -1;
+    case kGeluTanhD:
+      if constexpr (AK && !BK) { launch_e<T, AK, BK, kGeluTanhD>(A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, beta, splits, ws, s); break; }
+      return -1;
+    case kMulZ:
+      if constexpr (AK && BK) { launch_e<T, AK, BK, kMulZ>(A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, beta, splits, ws, s); break; }
+      return -1;
     default: return -1;
   }
   return 0;
@@ -336,7 +346,9 @@ extern "C" int pra_gemm_lds_splits(int M, int N, int K) {
 
 // layout: 0 = A[M][K]·B[K][N] (forward), 1 = A[M][K]·B[N][K]ᵀ (dgrad / NT), 2 = A[K][M]ᵀ·B[K][N] (wgrad).
 // epi: 0 none, 1 gelu(erf), 2 gelu(tanh), 3 relu (Z receives the pre-activation if given),
-//      4/5 dgelu(erf/tanh): C = acc * gelu'(Z) (Z required). colsum (optional, fp32
+//      4/5 dgelu(erf/tanh): C = acc * gelu'(Z) (Z required),
+//      6/7 gelu(erf/tanh) with Z = gelu'(pre-activation) (x·W only, Z required),
+//      8 C = acc * Z (dy·Wᵀ only, Z required: the saved derivative). colsum (optional, fp32
 //      [ceil(M/256)][N]) receives per-tile column partial sums of the stored C.
 // splits > 1: split-K through the fp32 workspace ws [splits][M][N] (not with dgelu/colsum).
 // epi | 256: run the persistent kernel (gemm_pts.h) for this call when it takes the shape.
@@ -349,7 +361,8 @@ extern "C" int pra_gemm_lds(int layout, const void* A, const void* B, const void
   if (layout == 2 && (M < 8 || (M & 7))) return -1;
   if ((layout == 0 || layout == 2) && N < 8) return -1;
   const int e = epi & 255;
-  if ((e == 4 || e == 5) && !Z) return -1;
+  if (e >= 4 && e <= 8 && !Z) return -1;
+  if (e > 8) return -1;
   if (splits > 1 && (!ws || e >= 4 || colsum || ldc != N)) return -1;
   // K-contiguous operands are addressed with 32-bit per-lane byte offsets from their base
   if ((layout == 0 || layout == 1) && (int64_t)M * lda * 2 >= (int64_t)1 << 32) return -1;

@@ -39,6 +39,15 @@ __device__ __forceinline__ void mma_agpr_z<f16>(V8<f16>::type a, V8<f16>::type b
   asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, 0" : "=a"(c) : "v"(a), "v"(b));
 }
 
+// inclusive scan over the 16 lanes of a DPP row: lane 15 of each row returns the row's sum
+__device__ __forceinline__ float row16_sum(float x) {
+  x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x111, 0xf, 0xf, true));
+  x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x112, 0xf, 0xf, true));
+  x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x114, 0xf, 0xf, true));
+  x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x118, 0xf, 0xf, true));
+  return x;
+}
+
 template <typename T, typename CF, bool AK, bool BK, int E, bool BETA>
 __global__ __launch_bounds__(CF::NT, 1) void gemm_pts_kernel(const uint16_t* __restrict__ A,
                                                              const uint16_t* __restrict__ B,
@@ -49,10 +58,9 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_pts_kernel(const uint16_t* __r
   constexpr int NT = CF::NT, TI = CF::TI, TJ = CF::TJ, NDA = CF::NDA, NDB = CF::NDB, WC = CF::WC;
   constexpr int BM = CF::BM, BN = CF::BN, IMGA = CF::IMGA, SLOT = CF::SLOT;
   constexpr int RW = TI * 16, CW = TJ * 16;
-  constexpr bool DG = (E == kDGeluErf || E == kDGeluTanh);
   constexpr bool AGPR_ACC = CF::WR * CF::WC == 4;
   static_assert(BM == 256 && BN == 256 && TJ % 2 == 0 && CF::WR == 2, "pts: 256x256 tiles, 2 wave rows");
-  __shared__ __attribute__((aligned(1024))) char lds[2 * SLOT + BN * 4];
+  __shared__ __attribute__((aligned(1024))) char lds[2 * SLOT + 2 * BN * 4];
   typedef typename V8<T>::type v8;
   const uint32_t lds_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)lds;
 
@@ -112,12 +120,41 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_pts_kernel(const uint16_t* __r
     for (int i = 0; i < TI; ++i) fa0[i] = frag<T, AK, (AK ? 256 : BM)>(ai, wr * RW + i * 16, 0, lane);
   }
 
+  // The epilogue's Z (scaling epilogues) / C (beta) operand of the current tile: loaded into
+  // registers in the last K-step, in the MFMA slots after its final barrier (the fragment
+  // registers of the next K-step are free there: the next tile's first fragments are read after
+  // the epilogue), so the loads' latency and bandwidth overlap the last 16-18 MFMAs instead of
+  // stalling a serialised epilogue (measured at 16384 x 8192 x 2048: reading Z inside the
+  // epilogue cost ~100 us over the plain GEMM, beta=1 ~60 us).
+  // Rows are streamed through a 3-deep register ring (16-row block i + 2 loads while block i is
+  // processed; blocks 0 and 1 come from the K loop): the whole tile at once (128 VGPRs) spilled.
+  constexpr bool ZOP = epi_scales(E) || BETA;
+  constexpr bool DG = epi_scales(E);
+  constexpr int NH = DG ? TJ / 2 : 1, JH = TJ / NH;  // epilogue column passes (one block pair each), blocks per pass
+  constexpr int ZR = 3;                          // ring depth (pass-rows in flight)
+  uint2 gza[ZOP ? ZR : 1][ZOP ? JH : 1];
+  const uint16_t* zp = nullptr;
+  int zr0 = 0, zc0 = 0, zld = 0;
+  // element l = q * JH + jq of pass-row q = hp * TI + i (16-row block i, column pass hp)
+  auto zload = [&](int l) __attribute__((always_inline)) {
+    if constexpr (ZOP) {
+      const int q = l / JH, jq = l % JH, hp = q / TI, i = q % TI, j = hp * JH + jq;
+      if (q < NH * TI) {
+        gza[q % ZR][jq] = make_uint2(0u, 0u);
+        if (zr0 + i * 16 < M && zc0 + j * 16 < N)
+          gza[q % ZR][jq] = *reinterpret_cast<const uint2*>(zp + (int64_t)(i * 16) * zld + j * 16);
+      }
+    }
+  };
+
   // one TS K-step (see gemm_core.h kstep_t); FIRST: the half-0 MFMAs start from a zero
   // accumulator. Outside STEADY the refill target (this tile's step kt+2, the next tile's step
-  // kt+2-nk, or none) and the next-fragment reads are runtime choices.
-  auto kstep = [&](int kt, auto steady_c, auto first_c, bool dcur, bool dnext, bool rd1)
+  // kt+2-nk, or none) and the next-fragment reads are runtime choices. ZPRE: issue the epilogue
+  // operand loads (zload) after the final barrier (the tile's last K-step).
+  auto kstep = [&](int kt, auto steady_c, auto first_c, bool dcur, bool dnext, bool rd1, auto zpre_c)
       __attribute__((always_inline)) {
     constexpr bool STEADY = decltype(steady_c)::value, FIRST = decltype(first_c)::value;
+    constexpr bool ZPRE = decltype(zpre_c)::value && ZOP;
     constexpr int NRD = TI + TJ, NDMA = NDA + NDB, NM = TI * TJ, F = 2 * NM;
     constexpr int BA = NRD + 4, BB = F - NRD - 3;
     constexpr int SP = (BB - BA - 1) / NDMA > 0 ? (BB - BA - 1) / NDMA : 1;
@@ -176,26 +213,39 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_pts_kernel(const uint16_t* __r
             const int r = f - BB - 1;
             if (r < TJ) fb0[r] = frag<T, BK>(bn, wc * CW + r * 16, 0, lane);
             else fa0[r - TJ] = frag<T, AK, (AK ? 256 : BM)>(an, wr * RW + (r - TJ) * 16, 0, lane);
+          } else if (ZPRE && f > BB) {
+            // the ring's first ZR - 1 pass-rows, spread over the slots after the barrier
+            constexpr int LPS = ((ZR - 1) * JH + (F - BB - 2)) / (F - BB - 1);  // loads per slot
+#pragma unroll
+            for (int q = 0; q < LPS; ++q)
+              if ((f - BB - 1) * LPS + q < (ZR - 1) * JH) zload((f - BB - 1) * LPS + q);
           }
           __builtin_amdgcn_sched_barrier(0);
         }
     if constexpr (!STEADY) __builtin_amdgcn_s_waitcnt(0xC07F);
   };
 
-  float* xlds = reinterpret_cast<float*>(lds + 2 * SLOT);  // [BN] column-sum exchange
+  float* xlds = reinterpret_cast<float*>(lds + 2 * SLOT);  // [2][BN] column sums per wave row
   while (true) {
     const int npid = pid + G;
     const bool has_next = npid < ntiles;
     int ntm = 0, ntn = 0;
-    kstep(0, std::true_type{}, std::true_type{}, true, false, true);
-    for (int kt = 1; kt + 2 < nk; ++kt) kstep(kt, std::true_type{}, std::false_type{}, true, false, true);
+    kstep(0, std::true_type{}, std::true_type{}, true, false, true, std::false_type{});
+    for (int kt = 1; kt + 2 < nk; ++kt)
+      kstep(kt, std::true_type{}, std::false_type{}, true, false, true, std::false_type{});
     // this tile's last refill was step nk-1 (issued in step nk-3): the DMA state moves to the next tile
     if (has_next) {
       tile_mn(npid, ntm, ntn);
       dma_init(da, db, ntm, ntn);
     }
-    kstep(nk - 2, std::false_type{}, std::false_type{}, false, has_next, true);
-    kstep(nk - 1, std::false_type{}, std::false_type{}, false, has_next, false);
+    if constexpr (ZOP) {
+      zr0 = tm * BM + wr * RW + (lane & 15);
+      zc0 = tn * BN + wc * CW + 4 * (lane >> 4);
+      zld = epi_scales(E) ? ldz : ldc;
+      zp = (epi_scales(E) ? Z : C) + (int64_t)(zr0 < M ? zr0 : 0) * zld + zc0;
+    }
+    kstep(nk - 2, std::false_type{}, std::false_type{}, false, has_next, true, std::false_type{});
+    kstep(nk - 1, std::false_type{}, std::false_type{}, false, has_next, false, std::true_type{});
 
     // ---- epilogue from registers: acc[i][j][r] = C[m0 + wr*RW + i*16 + (lane&15)][n0 + wc*CW + j*16 + 4*(lane>>4) + r]
     if constexpr (AGPR_ACC) asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
@@ -205,117 +255,132 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_pts_kernel(const uint16_t* __r
     const int cbase = n0 + wc * CW;
     // after the swap a lane holds 8 consecutive columns of block jp + ((lane >> 4) & 1)
     const int sw_col = ((lane >> 4) & 1) * 16 + 8 * (lane >> 5);
-    float cs[TJ][4];
-#pragma unroll
-    for (int j = 0; j < TJ; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) cs[j][r] = 0.f;
     uint2 bvp[TJ];  // this lane's 4 bias values per block, packed (unpacked where used)
 #pragma unroll
     for (int j = 0; j < TJ; ++j) {
       const int n = cbase + j * 16 + 4 * g;
       bvp[j] = make_uint2(0u, 0u);
-      if (bias && n < N) bvp[j] = *reinterpret_cast<const uint2*>(bias + n);
+      if (!DG && bias && n < N) bvp[j] = *reinterpret_cast<const uint2*>(bias + n);
     }
+    // The scaling (dgrad) epilogues walk the tile in NH column passes so that only TJ / NH blocks'
+    // column sums are live at a time (all TJ of them pushed the kernel past 256 VGPRs: per-tile
+    // scratch spills of loop-invariant state).
 #pragma unroll
-    for (int i = 0; i < TI; ++i) {
-      const int m = rb + i * 16;
-      const bool mok = m < M;
-      const int64_t mr = mok ? m : 0;
+    for (int hp = 0; hp < NH; ++hp) {
+      float cs[JH][4];
 #pragma unroll
-      for (int jp = 0; jp < TJ; jp += 2) {
-        // this lane's 8-byte operand loads of the pair (dGELU: Z, beta: C)
-        uint2 gz[2];
-        if constexpr (DG || BETA) {
+      for (int j = 0; j < JH; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) cs[j][r] = 0.f;
+#pragma unroll
+      for (int i = 0; i < TI; ++i) {
+        if constexpr (ZOP) __builtin_amdgcn_sched_barrier(0);  // keep the ring's loads in place
+        const int m = rb + i * 16;
+        const bool mok = m < M;
+        const int64_t mr = mok ? m : 0;
+        if constexpr (ZOP) {
+          // ring: pass-row q + ZR - 1's loads go out before pass-row q is consumed
+#pragma unroll
+          for (int j = 0; j < JH; ++j) zload((hp * TI + i + ZR - 1) * JH + j);
+        }
+#pragma unroll
+        for (int jq = 0; jq < JH; jq += 2) {
+          const int jp = hp * JH + jq;
+          uint2 gz[2];
+          if constexpr (ZOP) {
+            gz[0] = gza[(hp * TI + i) % ZR][jq];
+            gz[1] = gza[(hp * TI + i) % ZR][jq + 1];
+          }
+          uint32_t pc[2][2], pz[2][2];
 #pragma unroll
           for (int u = 0; u < 2; ++u) {
-            const int n = cbase + (jp + u) * 16 + 4 * g;
-            gz[u] = make_uint2(0u, 0u);
-            if (mok && n < N)
-              gz[u] = DG ? *reinterpret_cast<const uint2*>(Z + mr * ldz + n)
-                         : *reinterpret_cast<const uint2*>(C + mr * ldc + n);
-          }
-        }
-        uint32_t pc[2][2], pz[2][2];
+            const int j = jp + u;
+            // (the scaling epilogues are dgrads: no bias term)
+            float v[4];
+            if constexpr (DG) {
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          const int j = jp + u;
-          float v[4] = {acc[i][j][0] + to_f<T>(bvp[j].x & 0xffff), acc[i][j][1] + to_f<T>(bvp[j].x >> 16),
-                        acc[i][j][2] + to_f<T>(bvp[j].y & 0xffff), acc[i][j][3] + to_f<T>(bvp[j].y >> 16)};
-          if constexpr (DG) {
-            const float z[4] = {to_f<T>(gz[u].x & 0xffff), to_f<T>(gz[u].x >> 16), to_f<T>(gz[u].y & 0xffff),
-                                to_f<T>(gz[u].y >> 16)};
+              for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r];
+            } else {
+              v[0] = acc[i][j][0] + to_f<T>(bvp[j].x & 0xffff);
+              v[1] = acc[i][j][1] + to_f<T>(bvp[j].x >> 16);
+              v[2] = acc[i][j][2] + to_f<T>(bvp[j].y & 0xffff);
+              v[3] = acc[i][j][3] + to_f<T>(bvp[j].y >> 16);
+            }
+            if constexpr (DG) {
+              const float z[4] = {to_f<T>(gz[u].x & 0xffff), to_f<T>(gz[u].x >> 16), to_f<T>(gz[u].y & 0xffff),
+                                  to_f<T>(gz[u].y >> 16)};
 #pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] *= (E == kDGeluErf) ? dgelu_erf(z[r]) : dgelu_tanh(z[r]);
-          } else if constexpr (E != kNone) {
-            pz[u][0] = pack2<T>(v[0], v[1]);
-            pz[u][1] = pack2<T>(v[2], v[3]);
+              for (int r = 0; r < 4; ++r) v[r] *= zfac<E>(z[r]);
+              // bias-gradient column sums of the fp32 products (rows past M contribute zeros)
+              if (mok) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] = act<E>(v[r]);
+                for (int r = 0; r < 4; ++r) cs[jq + u][r] += v[r];
+              }
+            } else if constexpr (epi_gd(E)) {
+              float d[4];
+#pragma unroll
+              for (int r = 0; r < 4; ++r) v[r] = act_d<E>(v[r], d[r]);
+              pz[u][0] = pack2<T>(d[0], d[1]);
+              pz[u][1] = pack2<T>(d[2], d[3]);
+            } else if constexpr (E != kNone) {
+              pz[u][0] = pack2<T>(v[0], v[1]);
+              pz[u][1] = pack2<T>(v[2], v[3]);
+#pragma unroll
+              for (int r = 0; r < 4; ++r) v[r] = act<E>(v[r]);
+            }
+            if constexpr (BETA && !DG) {
+              v[0] += to_f<T>(gz[u].x & 0xffff);
+              v[1] += to_f<T>(gz[u].x >> 16);
+              v[2] += to_f<T>(gz[u].y & 0xffff);
+              v[3] += to_f<T>(gz[u].y >> 16);
+            }
+            pc[u][0] = pack2<T>(v[0], v[1]);
+            pc[u][1] = pack2<T>(v[2], v[3]);
           }
-          if constexpr (BETA && !DG) {
-            v[0] += to_f<T>(gz[u].x & 0xffff);
-            v[1] += to_f<T>(gz[u].x >> 16);
-            v[2] += to_f<T>(gz[u].y & 0xffff);
-            v[3] += to_f<T>(gz[u].y >> 16);
-          }
-          pc[u][0] = pack2<T>(v[0], v[1]);
-          pc[u][1] = pack2<T>(v[2], v[3]);
-          if (DG && colsum && mok) {
-            cs[j][0] += to_f<T>(pc[u][0] & 0xffff);
-            cs[j][1] += to_f<T>(pc[u][0] >> 16);
-            cs[j][2] += to_f<T>(pc[u][1] & 0xffff);
-            cs[j][3] += to_f<T>(pc[u][1] >> 16);
-          }
-        }
-        // rows 1 and 3 (lanes 16-31, 48-63) take block jp+1's first 4 columns from rows 0 / 2,
-        // which take block jp's last 4 columns: every lane then holds 8 consecutive columns
-        const int nc = cbase + jp * 16 + sw_col;
-        {
-          auto r0 = __builtin_amdgcn_permlane16_swap(pc[0][0], pc[1][0], false, false);
-          auto r1 = __builtin_amdgcn_permlane16_swap(pc[0][1], pc[1][1], false, false);
-          if (mok && nc < N)
-            *reinterpret_cast<uint4*>(C + mr * ldc + nc) = make_uint4(r0[0], r1[0], r0[1], r1[1]);
-        }
-        if constexpr (!DG && E != kNone) {
-          if (Z) {
-            auto r0 = __builtin_amdgcn_permlane16_swap(pz[0][0], pz[1][0], false, false);
-            auto r1 = __builtin_amdgcn_permlane16_swap(pz[0][1], pz[1][1], false, false);
+          // rows 1 and 3 (lanes 16-31, 48-63) take block jp+1's first 4 columns from rows 0 / 2,
+          // which take block jp's last 4 columns: every lane then holds 8 consecutive columns
+          const int nc = cbase + jp * 16 + sw_col;
+          {
+            auto r0 = __builtin_amdgcn_permlane16_swap(pc[0][0], pc[1][0], false, false);
+            auto r1 = __builtin_amdgcn_permlane16_swap(pc[0][1], pc[1][1], false, false);
             if (mok && nc < N)
-              *reinterpret_cast<uint4*>(Z + mr * ldz + nc) = make_uint4(r0[0], r1[0], r0[1], r1[1]);
+              *reinterpret_cast<uint4*>(C + mr * ldc + nc) = make_uint4(r0[0], r1[0], r0[1], r1[1]);
+          }
+          if constexpr (!DG && E != kNone) {
+            if (Z) {
+              auto r0 = __builtin_amdgcn_permlane16_swap(pz[0][0], pz[1][0], false, false);
+              auto r1 = __builtin_amdgcn_permlane16_swap(pz[0][1], pz[1][1], false, false);
+              if (mok && nc < N)
+                *reinterpret_cast<uint4*>(Z + mr * ldz + nc) = make_uint4(r0[0], r1[0], r0[1], r1[1]);
+            }
+          }
+        }
+      }
+      if constexpr (DG) {
+        if (colsum) {
+          // lanes with equal lane >> 4 own the same 4 columns of each block: reduce over lane & 15
+          // (one DPP row: row_shr 1/2/4/8 inclusive scan, lane 15 of the row ends with the total;
+          // v_add_f32_dpp, no ds_bpermute), lane 15 parks the pass's sums in its wave row's LDS row
+#pragma unroll
+          for (int j = 0; j < JH; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) cs[j][r] = row16_sum(cs[j][r]);
+          if (lrow == 15) {
+#pragma unroll
+            for (int j = 0; j < JH; ++j)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) xlds[wr * BN + wc * CW + (hp * JH + j) * 16 + 4 * g + r] = cs[j][r];
           }
         }
       }
     }
     if constexpr (DG) {
       if (colsum) {
-        // lanes with equal lane >> 4 own the same 4 columns of each block: reduce over lane & 15,
-        // then wave row 1 hands its sums to wave row 0 through LDS
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1)
-#pragma unroll
-          for (int j = 0; j < TJ; ++j)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) cs[j][r] += __shfl_xor(cs[j][r], o, 64);
-        if (wr == 1 && lrow == 0) {
-#pragma unroll
-          for (int j = 0; j < TJ; ++j)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) xlds[wc * CW + j * 16 + 4 * g + r] = cs[j][r];
-        }
+        // the two wave rows' sums -> this tile's partial row (one column per thread, coalesced)
         __builtin_amdgcn_s_waitcnt(0xC07F);
         __builtin_amdgcn_s_barrier();
-        if (wr == 0 && lrow == 0) {
-#pragma unroll
-          for (int j = 0; j < TJ; ++j) {
-            const int n = cbase + j * 16 + 4 * g;
-            if (n < N) {
-#pragma unroll
-              for (int r = 0; r < 4; ++r)
-                colsum[(int64_t)tm * N + n + r] = cs[j][r] + xlds[wc * CW + j * 16 + 4 * g + r];
-            }
-          }
-        }
+        for (int t = tid; t < BN; t += NT)
+          if (n0 + t < N) colsum[(int64_t)tm * N + n0 + t] = xlds[t] + xlds[BN + t];
       }
     }
     if (!has_next) break;

@@ -40,6 +40,15 @@ int launch_pts_e(const void* A, const void* B, const void* bias, void* C, void* 
     case kGeluTanh: launch_pts<CF, T, AK, BK, kGeluTanh, false>(A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, s); return 0;
     case kDGeluErf: launch_pts<CF, T, AK, BK, kDGeluErf, false>(A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, s); return 0;
     case kDGeluTanh: launch_pts<CF, T, AK, BK, kDGeluTanh, false>(A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, s); return 0;
+    case kGeluErfD:
+      if constexpr (AK && !BK) { launch_pts<CF, T, AK, BK, kGeluErfD, false>(A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, s); return 0; }
+      return -1;
+    case kGeluTanhD:
+      if constexpr (AK && !BK) { launch_pts<CF, T, AK, BK, kGeluTanhD, false>(A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, s); return 0; }
+      return -1;
+    case kMulZ:
+      if constexpr (AK && BK) { launch_pts<CF, T, AK, BK, kMulZ, false>(A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, s); return 0; }
+      return -1;
     default: return -1;  // ReLU: the per-tile kernel
   }
 }

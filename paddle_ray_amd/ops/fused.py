@@ -1314,7 +1314,10 @@ def flash_attn_varlen_ref(q, k, v, cu_q, cu_k, causal, scale, dropout=0.0, seed=
 # MFMA GEMM (ops/csrc/gemm_lds.hip): the training GEMMs of every Linear
 # =============================================================================
 GEMM_FWD, GEMM_NT, GEMM_TN = 0, 1, 2  # x·W, dy·Wᵀ (or h·Eᵀ), xᵀ·dy
-EPI = {None: 0, 'gelu': 1, 'gelu_tanh': 2, 'relu': 3, 'dgelu': 4, 'dgelu_tanh': 5}
+EPI = {None: 0, 'gelu': 1, 'gelu_tanh': 2, 'relu': 3, 'dgelu': 4, 'dgelu_tanh': 5,
+       # forward GELU whose z output receives gelu'(pre-activation) (x·W only), and the dgrad
+       # epilogue that multiplies by that saved derivative (dy·Wᵀ only)
+       'gelu_d': 6, 'gelu_tanh_d': 7, 'mulz': 8}
 # PRA_GEMM: 'auto' (default) = the in-tree MFMA kernel for every layout/epilogue where it measured
 # at or above hipBLASLt on MI355X (forward x·W incl. the fused bias+GELU epilogue, wgrad xᵀ·dy with
 # beta=1 accumulation), hipBLASLt for the dgrad dy·Wᵀ layout where it is still faster
@@ -1335,7 +1338,16 @@ def _gemm_ref(layout, a, b, out=None, bias=None, z=None, epi=None, beta=0, want_
     if bias is not None:
         y = y + bias.float()
     cs = None
-    if epi in ('dgelu', 'dgelu_tanh'):
+    if epi == 'mulz':
+        y = y * z.float()
+    elif epi in ('gelu_d', 'gelu_tanh_d'):
+        yf = y.detach().requires_grad_(True)
+        with torch.enable_grad():
+            g = torch.nn.functional.gelu(yf, approximate='tanh' if epi == 'gelu_tanh_d' else 'none')
+            d, = torch.autograd.grad(g.sum(), yf)
+        z.copy_(d.to(z.dtype))
+        y = g.detach()
+    elif epi in ('dgelu', 'dgelu_tanh'):
         zf = z.float().requires_grad_(True)
         with torch.enable_grad():
             g = torch.nn.functional.gelu(zf, approximate='tanh' if epi == 'dgelu_tanh' else 'none')
@@ -1363,9 +1375,12 @@ def _gemm_hip(layout, a, b, out=None, bias=None, z=None, epi=None, beta=0, want_
     Returns None when the shape/layout is outside what the kernel assumes (caller falls back)."""
     if _GEMM_MODE == 'blas' or not (_gemm_operand_ok(a) and _gemm_operand_ok(b)) or a.dtype != b.dtype:
         return None
-    persist = _GEMM_MODE == 'auto' and layout == GEMM_NT and _nt_in_tree(a, b)
-    if _GEMM_MODE == 'auto' and layout == GEMM_NT and not persist and \
+    persist = layout == GEMM_NT and ((_GEMM_MODE == 'auto' and _nt_in_tree(a, b)) or
+                                     (epi == 'mulz' and _MLP_MULZ_PTS))
+    if _GEMM_MODE == 'auto' and layout == GEMM_NT and not persist and epi != 'mulz' and \
             not (_MLP_DGELU_EPI and epi in ('dgelu', 'dgelu_tanh')):
+        return None
+    if epi in ('gelu_d', 'gelu_tanh_d') and layout != GEMM_FWD or epi == 'mulz' and layout != GEMM_NT:
         return None
     if layout == GEMM_FWD:
         M, K = a.shape
@@ -1988,6 +2003,14 @@ _MLP_DGELU_EPI = __import__('os').environ.get('PRA_MLP_DGELU_EPI', '0') == '1'
 _MLP_DGELU_SHORTK = __import__('os').environ.get('PRA_MLP_DGELU_SHORTK', '0') == '1'
 
 
+# The forward GEMM's epilogue saves gelu'(z) instead of z (the backward needs nothing else from
+# z), so the fc2 dgrad epilogue is one multiply + the bias-gradient column sums and runs in-tree
+# (PRA_MLP_SAVE_D=0: save z, dGELU recomputed in the backward as before)
+_MLP_SAVE_D = __import__('os').environ.get('PRA_MLP_SAVE_D', '1') == '1'
+# kernel for that dgrad: 1 = the persistent kernel (next tile's DMA under the epilogue), 0 = per-tile
+_MLP_MULZ_PTS = __import__('os').environ.get('PRA_MLP_MULZ_PTS', '1') == '1'
+
+
 class MlpGeluFn(torch.autograd.Function):
     """y = gelu(x·W1 + b1)·W2 (fc2 bias left to the caller's fused residual kernel).
 
@@ -2001,7 +2024,9 @@ class MlpGeluFn(torch.autograd.Function):
         x2 = x.reshape(-1, x.shape[-1])
         M, F = x2.shape[0], w1.shape[1]
         z = torch.empty((M, F), device=x.device, dtype=x.dtype)
-        h = gemm(GEMM_FWD, x2, w1, bias=b1, z=z, epi='gelu_tanh' if approximate else 'gelu')
+        ctx.save_d = _MLP_SAVE_D and x2.is_cuda and x2.dtype == torch.bfloat16
+        epi = 'gelu_tanh' if approximate else 'gelu'
+        h = gemm(GEMM_FWD, x2, w1, bias=b1, z=z, epi=epi + '_d' if ctx.save_d else epi)
         y = gemm(GEMM_FWD, h, w2)
         ctx.save_for_backward(x, z, h)
         ctx.w1, ctx.w2, ctx.b1 = w1, w2, b1
@@ -2016,7 +2041,11 @@ class MlpGeluFn(torch.autograd.Function):
         if not dy2.is_contiguous():
             dy2 = dy2.contiguous()
         x2 = x.reshape(-1, x.shape[-1])
-        if _GEMM_MODE == 'auto' and not _MLP_DGELU_EPI and not (_MLP_DGELU_SHORTK and _nt_in_tree(dy2, w2)):
+        if ctx.save_d:
+            # z holds gelu'(pre-activation): dz = dh * z and the fc1 bias gradient in the epilogue
+            dz, db1 = gemm(GEMM_NT, dy2, w2, z=z, epi='mulz', want_colsum=True)
+            db1 = db1.to(dz.dtype)
+        elif _GEMM_MODE == 'auto' and not _MLP_DGELU_EPI and not (_MLP_DGELU_SHORTK and _nt_in_tree(dy2, w2)):
             # dgrad (hipBLASLt, or the in-tree persistent kernel for a short K: the gemm() shape
             # policy), then ONE fused pass for gelu'(z) and the bias gradient
             dh = gemm(GEMM_NT, dy2, w2)

@@ -195,13 +195,15 @@ class Optimizer:
             if k == '@step':
                 self._step_count = int(v)
                 continue
-            for acc in self._acc_names:
-                suf = f'_{acc}_0'
+            accs = [(a, a) for a in self._acc_names] + list(getattr(self, '_acc_aliases', {}).items())
+            for stored, acc in sorted(accs, key=lambda x: -len(x[0])):   # longest suffix first
+                suf = f'_{stored}_0'
                 if k.endswith(suf):
                     pn = k[:-len(suf)]
                     src = _u(v) if isinstance(v, Tensor) else torch.as_tensor(np.asarray(v))
                     dev = names[pn]._t.device if pn in names else src.device
                     self._accumulators.setdefault(acc, {})[pn] = src.to(dev).float().clone()
+                    break
         self._fused_plan = None
 
     set_dict = set_state_dict
@@ -423,7 +425,10 @@ class Adagrad(_ForeachOpt):
 
 
 class Adadelta(_ForeachOpt):
-    _acc_names = ('avg_squared_grad', 'avg_squared_update')
+    # the reference's accumulator names (adadelta.py:109-110): keys `{param}__avg_squared_grad_0`
+    _acc_names = ('_avg_squared_grad', '_avg_squared_update')
+    # checkpoints written before the rename used the names without the leading underscore
+    _acc_aliases = {'avg_squared_grad': '_avg_squared_grad', 'avg_squared_update': '_avg_squared_update'}
 
     def __init__(self, learning_rate=0.001, epsilon=1.0e-6, rho=0.95, parameters=None,
                  weight_decay=None, grad_clip=None, name=None, multi_precision=False):
@@ -431,8 +436,8 @@ class Adadelta(_ForeachOpt):
         self._epsilon, self._rho = epsilon, rho
 
     def _update(self, p, g, w, lr):
-        a = self._acc('avg_squared_grad', p)
-        u = self._acc('avg_squared_update', p)
+        a = self._acc('_avg_squared_grad', p)
+        u = self._acc('_avg_squared_update', p)
         a.mul_(self._rho).add_((1 - self._rho) * g * g)
         upd = -torch.sqrt((u + self._epsilon) / (a + self._epsilon)) * g
         u.mul_(self._rho).add_((1 - self._rho) * upd * upd)
@@ -500,3 +505,34 @@ class Lamb(_ForeachOpt):
         wn, rn = w.norm(), r.norm()
         trust = torch.where((wn > 0) & (rn > 0), wn / rn, torch.ones_like(wn))
         return -lr * trust * r
+
+
+class LarsMomentum(_ForeachOpt):
+    """Momentum with layer-wise adaptive rate scaling (parity: fluid/optimizer.py:1786
+    LarsMomentumOptimizer; the `strategy.lars` meta-optimizer's replacement of Momentum):
+
+        local_lr = lr * lars_coeff * ||w|| / (||g|| + lars_weight_decay * ||w|| + epsilon)
+        v = mu * v + local_lr * (g + lars_weight_decay * w);   w -= v
+
+    (local_lr = lr when ||w|| or ||g|| is 0; parameters whose name contains an entry of
+    ``exclude_from_weight_decay`` get lars_weight_decay = 0). Accumulator key: velocity."""
+    _acc_names = ('velocity',)
+
+    def __init__(self, learning_rate=0.001, momentum=0.9, lars_coeff=0.001, lars_weight_decay=0.0005,
+                 parameters=None, grad_clip=None, name=None, exclude_from_weight_decay=None,
+                 epsilon=0.0, multi_precision=False, rescale_grad=1.0):
+        super().__init__(learning_rate, parameters, None, grad_clip, name, multi_precision)
+        self._momentum, self._lars_coeff, self._lars_wd = momentum, lars_coeff, lars_weight_decay
+        self._exclude = list(exclude_from_weight_decay or [])
+        self._epsilon, self._rescale_grad = epsilon, rescale_grad
+
+    def _update(self, p, g, w, lr):
+        g = g * self._rescale_grad
+        wd = 0.0 if any(n in p.name for n in self._exclude) else self._lars_wd
+        v = self._acc('velocity', p)
+        pn, gn = w.norm(), g.norm()
+        local = torch.where((pn > 0) & (gn > 0),
+                            lr * self._lars_coeff * pn / (gn + wd * pn + self._epsilon),
+                            torch.full_like(pn, lr))
+        v.mul_(self._momentum).add_(local * (g + wd * w))
+        return -v

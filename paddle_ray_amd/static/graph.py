@@ -938,6 +938,8 @@ class Executor:
             use_graph = program._build_strategy.use_hip_graph
             program = program._program
         prog = program or default_main_program()
+        if prog.__dict__.get('_no_graph'):
+            use_graph = False   # fleet collective programs (meta_optimizers.static_minimize)
         if prog._is_startup or not prog.global_block().ops and not fetch_list:
             return []
         feed = feed or {}
@@ -1089,7 +1091,10 @@ class Executor:
                     sync()
                     self._op_costs.append((op.type, (time.perf_counter() - t0) * 1e3))
                 if op.out_vids:
-                    flat, _ = _flatten_out(res)
+                    if isinstance(res, list) and len(res) == len(op.out_vids) and any(r is None for r in res):
+                        flat = res   # an op that produced no value for some outputs this run
+                    else:
+                        flat, _ = _flatten_out(res)
                     for vid, t in zip(op.out_vids, flat):
                         env[vid] = t
                 for vid in free_after[pos]:

@@ -1,0 +1,14 @@
+#!/bin/bash
+# Round 5: trimmed PTS dgrad epilogue (no bias pass, fp32 column sums, DPP row reduction).
+OUT=gpurun_out/${1:-r5c}
+mkdir -p $OUT
+export TMPDIR=/tmp
+fatal() { case $1 in 124|137|134|139) return 0;; esac; return 1; }
+step() { local name=$1 t=$2; shift 2; timeout -k 10 "$t" "$@" > $OUT/$name.log 2>&1; local rc=$?;
+         echo "[$name rc=$rc]"; grep -v amdgpu.ids $OUT/$name.log | tail -n 12; if fatal $rc; then exit $rc; fi; }
+step gemm_tests 400 python -u -m pytest tests/test_gemm_lds_gpu.py -x -q --timeout 120 --timeout-method thread
+step mlp_gpt 200 python scripts/gemm_mlp_bench.py
+step mlp_bert 200 python scripts/gemm_mlp_bench.py --bert
+step bench_new 300 python bench.py --gpus 1 --steps 20 --warmup 5
+PRA_MLP_SAVE_D=0 step bench_old 300 python bench.py --gpus 1 --steps 20 --warmup 5
+exit 0

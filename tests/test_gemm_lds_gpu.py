@@ -96,7 +96,37 @@ def test_dgelu_epilogue_and_bias_grad(epi):
     g = torch.nn.functional.gelu(zf, approximate='tanh' if epi == 'dgelu_tanh' else 'none')
     ref, = torch.autograd.grad(g, zf, _ref(1, dy, w))
     _close(out, ref)
-    _close(cs, out.float().sum(0), tol=1e-3)
+    _close(cs, ref.sum(0), tol=2e-2)
+    _close(cs, out.float().sum(0), tol=1e-2)
+
+
+@pytest.mark.parametrize('epi', ['gelu_d', 'gelu_tanh_d'])
+@pytest.mark.parametrize('M,N,Kd', [(600, 264, 384), (4168, 4360, 256)])
+def test_gelu_derivative_epilogue(epi, M, N, Kd):
+    """x·W + b -> gelu, with z receiving gelu'(pre-activation) (the MLP forward that saves the
+    derivative for its backward), ragged tiles and (4168 x 4360) more tiles than CUs."""
+    torch.manual_seed(12)
+    a, b = _operands(0, M, N, Kd)
+    bias = _r(N)
+    z = torch.empty(M, N, device='cuda', dtype=torch.bfloat16)
+    y = K._gemm_hip(0, a, b, bias=bias, z=z, epi=epi)
+    pre = (_ref(0, a, b) + bias.float()).requires_grad_(True)
+    g = torch.nn.functional.gelu(pre, approximate='tanh' if epi == 'gelu_tanh_d' else 'none')
+    d, = torch.autograd.grad(g.sum(), pre)
+    _close(y, g.detach())
+    _close(z, d)
+
+
+@pytest.mark.parametrize('M,N,Kd', [(600, 264, 384), (4168, 4360, 256), (2048, 1280, 2048)])
+def test_mulz_epilogue_and_bias_grad(M, N, Kd):
+    """dz = (dy·Wᵀ) * z with the saved derivative z, plus the bias-gradient column sums."""
+    torch.manual_seed(13)
+    dy, w = _r(M, Kd), _r(N, Kd)
+    z = _r(M, N, scale=1.2)
+    out, cs = K._gemm_hip(1, dy, w, z=z, epi='mulz', want_colsum=True)
+    ref = _ref(1, dy, w) * z.float()
+    _close(out, ref)
+    _close(cs, ref.sum(0), tol=2e-2)
 
 
 def test_beta_accumulate_and_split_k():
@@ -167,10 +197,12 @@ def test_linear_nt_head_grads():
     _close(e.grad, ef.grad + g0.float())
 
 
+@pytest.mark.parametrize('save_d', [True, False])
 @pytest.mark.parametrize('mode', ['mfma', 'auto'])
 @pytest.mark.parametrize('approx', [True, False])
-def test_mlp_gelu_fused(approx, mode):
+def test_mlp_gelu_fused(approx, mode, save_d, monkeypatch):
     K._GEMM_MODE = mode
+    monkeypatch.setattr(K, '_MLP_SAVE_D', save_d)
     torch.manual_seed(6)
     x = _r(2, 256, 256).requires_grad_(True)
     w1, b1, w2 = _r(256, 1024).requires_grad_(True), _r(1024).requires_grad_(True), \
@@ -225,7 +257,7 @@ def test_many_tiles_epilogues():
     zf = zz.float().requires_grad_(True)
     ref, = torch.autograd.grad(torch.nn.functional.gelu(zf), zf, _ref(1, dy, w))
     _close(out, ref)
-    _close(cs, out.float().sum(0), tol=1e-3)
+    _close(cs, ref.sum(0), tol=2e-2)
 
 
 @pytest.mark.parametrize('Kd,in_tree', [(768, True), (1024, True), (2048, False)])
@@ -245,4 +277,4 @@ def test_auto_policy_short_k_dgrad(Kd, in_tree):
     zf = z.float().requires_grad_(True)
     ref, = torch.autograd.grad(torch.nn.functional.gelu(zf), zf, _ref(1, dy, w))
     _close(out, ref)
-    _close(cs.float(), out.float().sum(0), tol=2e-3)
+    _close(cs.float(), ref.sum(0), tol=2e-2)
