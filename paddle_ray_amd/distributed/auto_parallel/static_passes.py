@@ -429,6 +429,7 @@ class Partitioner:
         if not ctx.plans:
             Completer(ctx).complete_forward_annotation(serial)
         dist, vmap = G.Program(), {}
+        sync = {}   # local parameter name -> mesh dims its gradient is all-reduced over
         with G.program_guard(dist):
             for vid, v in list(serial.global_block().vars.items()):
                 if v.__dict__.get('is_data'):
@@ -436,10 +437,28 @@ class Partitioner:
                     nv.stop_gradient = v.stop_gradient
                     m = ctx.get(v)
                     vmap[vid] = self._reshard(nv, [-1] * len(m), m)
-            for op, req, outs, partial in ctx.plans:
+            def grad_dims(op, partial, outs, pos, want):
+                # replicated over a mesh dim the op's result is split / partial over: the
+                # operand's gradient is a partial sum there (identity fwd, all-reduce bwd; a
+                # bias added after the all-reduce only sees the split dims)
                 name = op.type.rsplit(':', 1)[-1]
                 split_dims = {d for m in outs for d in m if d >= 0}
-                out_dims = split_dims | set(partial)
+                bias_pos = None
+                if partial and name == 'linear':
+                    bias_pos = 2 if len(op.args) > 2 else ('bias' if 'bias' in op.kwargs else None)
+                dims = split_dims if pos == bias_pos else split_dims | set(partial)
+                return frozenset(dims - {w for w in want if w >= 0})
+            # Parameters whose every use needs the same gradient reduction (the data-parallel
+            # case): no per-use identity op; their gradients are all-reduced in flat buckets,
+            # asynchronously, inside the backward (meta_optimizers.insert_grad_sync at minimize)
+            uses = {}
+            for op, req, outs, partial in ctx.plans:
+                for (pos, a), want in zip(_tensor_args(op), req):
+                    if isinstance(a, Parameter) and _needs_grad(a):
+                        uses.setdefault(id(a), set()).add(grad_dims(op, partial, outs, pos, want))
+            deferred = {pid: next(iter(ds)) for pid, ds in uses.items() if len(ds) == 1 and next(iter(ds))}
+            for op, req, outs, partial in ctx.plans:
+                name = op.type.rsplit(':', 1)[-1]
                 top = (G._VarRef, Tensor)            # top-level operands: placed by the plan below
                 args = [a if isinstance(a, top) else self._nested(a, vmap) for a in op.args]
                 kw = {k: a if isinstance(a, top) else self._nested(a, vmap) for k, a in op.kwargs.items()}
@@ -450,12 +469,11 @@ class Partitioner:
                 for (pos, a), want in zip(_tensor_args(op), req):
                     val = self._operand(a, want, vmap)
                     if _needs_grad(a):
-                        # replicated over a mesh dim the op's result is split / partial over:
-                        # its gradient is a partial sum there -> identity fwd, all-reduce bwd
-                        # (a bias added after the all-reduce only sees the split dims)
-                        dims = split_dims if pos == bias_pos else out_dims
-                        for d in sorted(dims - {w for w in want if w >= 0}):
-                            val = _comm('ap_identity', val, mesh, d)
+                        if isinstance(a, Parameter) and id(a) in deferred:
+                            sync[self._param(a).name] = sorted(deferred[id(a)])
+                        else:
+                            for d in sorted(grad_dims(op, partial, outs, pos, want)):
+                                val = _comm('ap_identity', val, mesh, d)
                     if pos == bias_pos:
                         bias, val = val, None
                     if isinstance(pos, int):
@@ -471,6 +489,10 @@ class Partitioner:
                 for ov, nv in zip(op.out_vids, flat):
                     vmap[ov] = nv
         dist.__dict__['_dist_context'] = ctx
+        if sync:
+            groups = {d: mesh.axis_group(d) for ds in sync.values() for d in ds}
+            dist.__dict__['_ap_grad_sync'] = {n: [groups[d] for d in ds if groups[d] is not None]
+                                              for n, ds in sync.items()}
         return dist, _VarMap(vmap)
 
 

@@ -77,9 +77,11 @@ def apply_optimizer_swaps(opt, strategy):
 
 # -- communication state of one rewritten program ---------------------------------------------------
 class _CommState:
-    def __init__(self, pg, nranks, k_steps=1, avg=True):
+    def __init__(self, pg, nranks, k_steps=1, avg=True, rank_avg=True, extra_pgs=()):
         self.pg, self.nranks = pg, nranks
         self.k_steps, self.avg = max(1, int(k_steps)), avg
+        self.rank_avg = rank_avg          # divide the all-reduced sum by nranks
+        self.extra_pgs = list(extra_pgs)  # further groups reduced after the first (2-D meshes)
         self.works = {}
         self.merged = {}    # bucket -> persistent flat accumulation buffer (gradient merge)
         self.micro = 0      # completed runs
@@ -120,7 +122,7 @@ def _sync_split(state, layout, *flats):
             state.works.pop(b, None)
         return [None] * n
     scale = 1.0
-    if state.nranks > 1:
+    if state.nranks > 1 and state.rank_avg:
         scale /= state.nranks
     if state.k_steps > 1 and state.avg:
         scale /= state.k_steps
@@ -130,6 +132,8 @@ def _sync_split(state, layout, *flats):
         w = state.works.pop(b, None)
         if w is not None:
             w.wait()
+        for pg in state.extra_pgs:
+            dist.all_reduce(f, group=pg)
         if scale != 1.0:
             f.mul_(scale)
         off = 0
@@ -266,6 +270,60 @@ def _bucket_plan(blk, n_before, pg_items, bucket_bytes):
     return out
 
 
+def _insert_bucketed(blk, n_before, pg, state, bucket_bytes, tag=''):
+    """Insert one async all-reduce op per gradient bucket (right after the bucket's last
+    producer) and the joining sync op; returns (params, reduced grad vars) in bucket order."""
+    from ...static import graph as G
+    plan = _bucket_plan(blk, n_before, pg, bucket_bytes)
+    layout, flat_vids, inserts = [], [], []
+    for b, (pos, items) in enumerate(plan):
+        fv = G._new_var(blk, [sum(_u(p).numel() for p, _ in items)], _u(items[0][0]).dtype,
+                        f'coalesced_grad{tag}_{b}')
+        op = G.OpDesc('c_allreduce_coalesced', _bucket_allreduce,
+                      [state, b] + [G._VarRef(g.vid) for _, g in items], {},
+                      [g.vid for _, g in items], [fv.vid], 'T', role='backward')
+        inserts.append((pos, op))
+        layout.append([(p.name, _u(p).numel(), tuple(_u(p).shape)) for p, _ in items])
+        flat_vids.append(fv.vid)
+    for pos, op in sorted(inserts, key=lambda x: -x[0]):   # back to front: positions stay valid
+        blk.ops.insert(pos, op)
+    state.buckets = layout
+    order = [p for _, items in plan for p, _ in items]
+    outs = [G._new_var(blk, list(_u(p).shape), _u(p).dtype, p.name + '@GRAD@REDUCED') for p in order]
+    sync = G.OpDesc('c_sync_comm_stream', _sync_split, [state, layout] + [G._VarRef(v) for v in flat_vids],
+                    {}, list(flat_vids), [g.vid for g in outs], ('list', ['T'] * len(outs)),
+                    role='backward')
+    blk.ops.append(sync)
+    return order, outs
+
+
+def insert_grad_sync(prog, n_before, pg, sync, bucket_mb=_DEFAULT_BUCKET_MB):
+    """Static auto-parallel: the gradients of parameters replicated over mesh axes (data
+    parallel) are SUMMED over those axes' groups (the loss's own 1/n already scales them) in
+    flat buckets, asynchronously inside the backward (parity: auto_parallel_data_parallel_
+    optimization.py:57,132 `_fuse_allreduce`, GradientsGroup :727). ``sync``: local parameter
+    name -> [Group, ...]. Returns (params, grad vars) for the optimize op."""
+    blk = prog.global_block()
+    byname = {p.name: (p, g) for p, g in pg}
+    keyed = {}
+    for name, groups in sync.items():
+        if name in byname and groups:
+            keyed.setdefault(tuple(id(g) for g in groups), (groups, []))[1].append(byname[name])
+    states = []
+    done = {}
+    for t, (key, (groups, items)) in enumerate(sorted(keyed.items(), key=lambda kv: kv[0])):
+        st = _CommState(groups[0].process_group, groups[0].nranks, rank_avg=False,
+                        extra_pgs=[g.process_group for g in groups[1:]])
+        ps, gs = _insert_bucketed(blk, n_before, items, st, int(bucket_mb * (1 << 20)), tag=f'_{t}')
+        for p, g in zip(ps, gs):
+            done[p.name] = g
+        states.append(st)
+    prog.__dict__['_ap_grad_states'] = states
+    prog.__dict__['_no_graph'] = True
+    params = [p for p, _ in pg]
+    return params, [done.get(p.name, g) for p, g in pg]
+
+
 def static_minimize(opt, loss, strategy, hcg, parameters=None):
     """Rewrite the program of ``loss`` for collective training (see the module docstring)."""
     from ...static import graph as G
@@ -333,32 +391,7 @@ def static_minimize(opt, loss, strategy, hcg, parameters=None):
         mb = getattr(strategy, 'fuse_grad_size_in_MB', _DEFAULT_BUCKET_MB) or _DEFAULT_BUCKET_MB
         if not getattr(strategy, 'fuse_all_reduce_ops', True):
             mb = 0   # one bucket per gradient (reference: unfused c_allreduce_sum per grad)
-        plan = _bucket_plan(blk, n_before, pg, int(mb * (1 << 20)))
-        layout = []
-        flat_vids = []
-        # insert back to front so earlier positions stay valid
-        inserts = []
-        for b, (pos, items) in enumerate(plan):
-            fv = G._new_var(blk, [sum(_u(p).numel() for p, _ in items)], _u(items[0][0]).dtype,
-                            f'coalesced_grad_{b}')
-            op = G.OpDesc('c_allreduce_coalesced', _bucket_allreduce,
-                          [state, b] + [G._VarRef(g.vid) for _, g in items], {},
-                          [g.vid for _, g in items], [fv.vid], 'T', role='backward')
-            inserts.append((pos, op))
-            layout.append([(p.name, _u(p).numel(), tuple(_u(p).shape)) for p, _ in items])
-            flat_vids.append(fv.vid)
-        for pos, op in sorted(inserts, key=lambda x: -x[0]):
-            blk.ops.insert(pos, op)
-        state.buckets = layout
-        order = [p for _, items in plan for p, _ in items]
-        outs = []
-        for p in order:
-            outs.append(G._new_var(blk, list(_u(p).shape), _u(p).dtype, p.name + '@GRAD@REDUCED'))
-        sync = G.OpDesc('c_sync_comm_stream', _sync_split, [state, layout] + [G._VarRef(v) for v in flat_vids],
-                        {}, list(flat_vids), [g.vid for g in outs], ('list', ['T'] * len(outs)),
-                        role='backward')
-        blk.ops.append(sync)
-        params, gvars = order, outs
+        params, gvars = _insert_bucketed(blk, n_before, pg, state, int(mb * (1 << 20)))
     op = G.OpDesc('fleet_optimize', _fleet_optimize, [state, opt, params] + [G._VarRef(g.vid) for g in gvars],
                   {'scaler': scaler}, [g.vid for g in gvars], [], 'C', role='optimize')
     blk.ops.append(op)

@@ -812,10 +812,18 @@ def _static_minimize(opt, loss, parameters=None, scaler=None, loss_scale=1.0):
         ps = parameters or [p for p in prog.all_parameters() if not p.stop_gradient]
         opt._param_groups = []
         opt._add_param_group({'params': list(ps)})
-    pg = append_backward(loss, parameters, loss_scale=loss_scale)
     blk = prog.global_block()
+    n_before = len(blk.ops)
+    pg = append_backward(loss, parameters, loss_scale=loss_scale)
     params = [p for p, _ in pg]
     gvars = [g for _, g in pg]
+    sync = prog.__dict__.get('_ap_grad_sync')
+    if sync:
+        # auto-parallel partitioned program: bucketed async gradient all-reduce over the mesh
+        # axes the parameters are replicated on (static_passes.Partitioner records them)
+        from ..distributed.fleet.meta_optimizers import insert_grad_sync
+        params, gvars = insert_grad_sync(prog, n_before, pg, sync,
+                                         prog.__dict__.get('_ap_bucket_mb', 32))
     op = OpDesc('optimize', _optimize_fn, [opt, params] + [_VarRef(g.vid) for g in gvars],
                 {'scaler': scaler}, [g.vid for g in gvars], [], 'C', role='optimize')
     blk.ops.append(op)

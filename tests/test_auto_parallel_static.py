@@ -73,9 +73,10 @@ def _run(rank, world, mesh_ids, names, specs):
     mapping = {'h': part.ctx.get(h), 'w2': part.ctx.get(params[2])}
     comm = [op.type for op in dist.global_block().ops
             if op.role == 'forward' and op.type.startswith('ap_')]
+    ops = [op.type for op in dist.global_block().ops]
     paddle.disable_static()
     return {'ref': float(ref_loss), 'loss': float(d_loss), 'errs': errs, 'map': mapping,
-            'comm': comm, 'shapes': [list(lp.shape) for lp in local]}
+            'comm': comm, 'ops': ops, 'shapes': [list(lp.shape) for lp in local]}
 
 
 def test_completion_rules_single_process():
@@ -115,7 +116,10 @@ def test_partitioned_step_matches_serial_2ranks(tmp_path, kind):
         assert res[0]['map']['h'] == [-1, 0]
     else:
         assert res[0]['shapes'][0] == [H, F_]
-        assert set(res[0]['comm']) == {'ap_slice', 'ap_identity', 'ap_allreduce'}, res[0]['comm']
+        # replicated parameters: no per-parameter identity / backward all-reduce op; their
+        # gradients go through the bucketed async all-reduce inserted at minimize
+        assert set(res[0]['comm']) == {'ap_slice', 'ap_allreduce'}, res[0]['comm']
+        assert 'c_allreduce_coalesced' in res[0]['ops']
 
 
 def test_partitioned_step_hybrid_2x2(tmp_path):
@@ -277,3 +281,52 @@ def test_engine_static_partitioned_matches_serial(tmp_path):
         np.testing.assert_allclose(o['loss'], ref['loss'], rtol=1e-5, atol=1e-6)
         assert abs(o['eval'] - ref['eval']) < 1e-5
     assert ref['loss'][-1] < ref['loss'][0]
+
+
+def _run_dp_trace(rank, world, bucket_mb):
+    """Data-parallel partitioned step under CommTrace: the gradient all-reduces."""
+    import paddle_ray_amd as paddle
+    from paddle_ray_amd import static
+    from paddle_ray_amd.distributed import auto_parallel as ap
+    from paddle_ray_amd.distributed.comm_trace import CommTrace
+    paddle.enable_static()
+    mesh = ap.ProcessMesh(list(range(world)), ['dp'])
+    main, x, y, h, loss, params = _build({'x': ['dp', None], 'y': ['dp', None]}, mesh)
+    dist, vmap, part = ap.parallelize(main)
+    dist.__dict__['_ap_bucket_mb'] = bucket_mb
+    local = [part.local_param(p) for p in params]
+    with static.program_guard(dist):
+        paddle.optimizer.SGD(0.5, parameters=local).minimize(vmap[loss])
+    with static.program_guard(main):
+        paddle.optimizer.SGD(0.5, parameters=list(params)).minimize(loss)
+    exe = static.Executor()
+    xv, yv = _data()
+    exe.run(main, feed={'x': xv, 'y': yv}, fetch_list=[loss])
+    with CommTrace() as tr:
+        exe.run(dist, feed={'x': xv, 'y': yv}, fetch_list=[vmap[loss]])
+    ars = [(r.bytes, r.async_op, tuple(r.ranks)) for r in tr.ops('all_reduce')]
+    ops = [op.type for op in dist.global_block().ops]
+    errs = [float(np.abs(lp.numpy() - p.numpy()).max()) for p, lp in zip(params, local)]
+    paddle.disable_static()
+    return {'ars': ars, 'ops': ops, 'errs': errs,
+            'pbytes': [int(np.prod(p.shape)) * 4 for p in local]}
+
+
+@pytest.mark.parametrize('bucket_mb,nb', [(32, 1), (1e-6, 4)])
+def test_auto_parallel_dp_bucketed_grad_allreduce(tmp_path, bucket_mb, nb):
+    """world 4, pure data parallel: the replicated parameters' gradients are all-reduced in
+    `nb` flat buckets (async, issued from inside the backward), not one synchronous all-reduce
+    per parameter; the partitioned step still matches the serial one."""
+    res = run_ranks(_run_dp_trace, 4, tmp_path, args=(bucket_mb,))
+    for o in res:
+        assert max(o['errs']) < 1e-5, o
+        grad_ars = [a for a in o['ars'] if a[1]]          # the async (gradient) all-reduces
+        assert len(grad_ars) == nb, o['ars']
+        assert sum(a[0] for a in grad_ars) == sum(o['pbytes'])
+        assert all(a[2] == (0, 1, 2, 3) for a in grad_ars)
+        ops = o['ops']
+        ar = [i for i, t in enumerate(ops) if t == 'c_allreduce_coalesced']
+        grads = [i for i, t in enumerate(ops) if t.endswith('_grad') or t == 'grad']
+        assert len(ar) == nb and ops.count('ap_identity') == 0
+        if nb > 1:
+            assert ar[0] < grads[-1], ops           # the first bucket leaves before the backward ends
