@@ -238,8 +238,12 @@ def bench_gpt(a, paddle, torch, dist, C, world, rank, dev):
                                       f"_dp{world}",
                        "micro_batch_per_gpu": a.micro_batch, "hidden_dropout": a.dropout,
                        "optimizer": "AdamW fp32-master, global-norm clip",
-                       "zero3_params": "released after forward" if a.zero3_release
-                       else "gathered units resident forward->backward"},
+                       # at world 1 there is nothing to shard (parallel/sharding.py turns the
+                       # stage off, as the reference would): the step is plain training
+                       "zero3_active": bool(world > 1 and a.level == 'p_g_os'),
+                       "zero3_params": ("released after forward" if a.zero3_release
+                                        else "gathered units resident forward->backward (non-default)")
+                       if world > 1 and a.level == 'p_g_os' else "n/a (world 1)"},
             "tokens_per_sec_per_gpu": round(tps / world, 2),
             "mfu_bf16_dense": round(mfu, 4), "final_loss": round(last_loss, 4)}
 
@@ -362,6 +366,12 @@ def bench_bert(a, paddle, torch, dist, C, world, rank, dev):
         opt = static.amp.decorate(paddle.optimizer.AdamW(1e-4, parameters=model.parameters(),
                                                          multi_precision=True),
                                   use_bf16=True, use_pure_fp16=True)
+        if world > 1:
+            # static-mode fleet data parallel: bucketed async gradient all-reduce inside the
+            # backward (distributed/fleet/meta_optimizers.py)
+            from paddle_ray_amd.distributed import fleet
+            fleet.init(is_collective=True)
+            opt = fleet.distributed_optimizer(opt)
         opt.minimize(loss_v)
     exe = static.Executor()
     exe.run(startup)

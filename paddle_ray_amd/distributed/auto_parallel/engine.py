@@ -181,6 +181,13 @@ class Engine:
         from ... import static
         from .static_passes import parallelize
         assert inputs_spec, "a static Engine needs inputs_spec (paddle.static.InputSpec list)"
+        st = self._strategy
+        for opt_name in ('amp', 'recompute', 'gradient_merge'):
+            cfg = getattr(st, opt_name, None) if st is not None else None
+            if cfg is not None and getattr(cfg, 'enable', False):
+                raise NotImplementedError(
+                    f"auto_parallel.Engine in static mode: strategy.{opt_name} is not applied to the "
+                    "partitioned program; run the Engine in dygraph mode for it")
         serial = static.Program()
         with static.program_guard(serial):
             ins = [static.data(sp.name or f'input{i}', list(sp.shape), sp.dtype)
@@ -192,6 +199,7 @@ class Engine:
         dist, vmap, part = parallelize(serial)
         local = [part.local_param(p) for p in self._model.parameters() if id(p) in part.params]
         self._dist = {'program': dist, 'feeds': [v.name for v in ins + lbs], 'n_in': len(ins),
+                      'label_specs': list(_to_list(labels_spec)),
                       'loss': vmap[loss], 'outs': [vmap[o] for o in _to_list(outs)],
                       'partitioner': part, 'serial': serial, 'params': local}
         eval_prog = dist.clone(for_test=True)
@@ -314,6 +322,20 @@ class Engine:
     @torch.no_grad()
     def predict(self, test_data, test_sample_split=None, batch_size=1, steps=None, collate_fn=None,
                 callbacks=None, verbose=2):
+        if getattr(self, '_dist', None) is not None:
+            # the partitioned eval program, fetching the model outputs (whole on every rank)
+            d, outputs = self._dist, []
+            n_in = d['n_in']
+            for step, batch in enumerate(self._static_loader(test_data, batch_size, collate_fn)):
+                if steps is not None and step >= steps:
+                    break
+                inputs, _ = self._split(batch, test_sample_split if test_sample_split is not None
+                                        else len(_to_list(batch)))
+                vals = [x.numpy() if isinstance(x, Tensor) else np.asarray(x) for x in inputs[:n_in]]
+                feed = dict(zip(d['feeds'][:n_in], vals))   # labels: not on the outputs' path
+                outs = self._exe.run(d['eval_program'], feed=feed, fetch_list=d['outs'])
+                outputs.append([np.asarray(o) for o in outs])
+            return outputs
         self._model.eval()
         loader = self._loader(test_data, batch_size, False, collate_fn)
         outputs = []
@@ -326,8 +348,70 @@ class Engine:
             outputs.append([o.numpy() for o in _to_list(outs)])
         return outputs
 
+    # -- checkpoints of a partitioned static program: the trained values live in this rank's
+    # parameter shards (Partitioner.local_param), not in the serial model. save() gathers every
+    # shard along its dims_mapping into the FULL tensor (serial names, reference .pdparams /
+    # .pdopt layout; rank 0 writes), load() slices the full tensors back into the shards (and
+    # the serial parameters), so a checkpoint resumes on any mesh (parity: the reference Engine's
+    # save/load + auto_parallel/dist_saver.py merge of the per-rank files).
+    def _shard_of(self, p):
+        part = self._dist['partitioner']
+        return part.params.get(id(p))
+
+    def _gather_full(self, t, mapping):
+        from . import _GatherAxis
+        mesh = self._dist['partitioner'].ctx.mesh
+        for i, d in enumerate(mapping or []):
+            if d >= 0:
+                g = mesh.axis_group(d)
+                if g is not None:
+                    t = _GatherAxis.apply(t.contiguous(), i, g)
+        return t
+
+    def _slice_local(self, t, mapping):
+        mesh = self._dist['partitioner'].ctx.mesh
+        coord = mesh.coord()
+        for i, d in enumerate(mapping or []):
+            if d >= 0:
+                n = t.shape[i] // mesh.shape[d]
+                t = t.narrow(i, coord[d] * n, n)
+        return t.contiguous()
+
+    def _dist_state(self, training):
+        model_sd, by_name = {}, {}
+        for k, p in self._model.state_dict().items():
+            lp = self._shard_of(p)
+            if lp is None:
+                model_sd[k] = p
+                continue
+            full = self._gather_full(_u(lp).detach(), lp.__dict__.get('_dist_mapping'))
+            model_sd[k] = Tensor(full)
+            by_name[lp.name] = lp
+        opt_sd = None
+        if training and self._optimizer is not None:
+            opt_sd = {}
+            for k, v in self._optimizer.state_dict().items():
+                if k == 'master_weights':
+                    opt_sd[k] = {pn: Tensor(self._gather_full(_u(t), by_name[pn].__dict__.get('_dist_mapping')))
+                                 if pn in by_name else t for pn, t in v.items()}
+                    continue
+                pn = next((n for n in by_name if isinstance(v, Tensor) and k.startswith(n + '_') and
+                           tuple(_u(v).shape) == tuple(_u(by_name[n]).shape)), None)
+                opt_sd[k] = Tensor(self._gather_full(_u(v), by_name[pn].__dict__.get('_dist_mapping'))) \
+                    if pn is not None else v
+        return model_sd, opt_sd
+
     def save(self, path, training=True):
         from ...framework.io import save
+        if getattr(self, '_dist', None) is not None:
+            model_sd, opt_sd = self._dist_state(training)   # collective: every rank gathers
+            if C.get_rank() == 0:
+                save(model_sd, path + '.pdparams')
+                if opt_sd is not None:
+                    save(opt_sd, path + '.pdopt')
+            if C.get_world_size() > 1:
+                C.barrier()
+            return
         save(self._model.state_dict(), path + '.pdparams')
         if training and self._optimizer is not None:
             save(self._optimizer.state_dict(), path + '.pdopt')
@@ -335,7 +419,33 @@ class Engine:
     def load(self, path, strict=True, load_optimizer=True):
         import os
         from ...framework.io import load
-        self._model.set_state_dict(load(path + '.pdparams'))
+        sd = load(path + '.pdparams')
+        self._model.set_state_dict(sd)
+        if getattr(self, '_dist', None) is not None:
+            by_name = {}
+            with torch.no_grad():
+                for k, p in self._model.state_dict().items():
+                    lp = self._shard_of(p)
+                    if lp is None:
+                        continue
+                    full = _u(p).detach()
+                    _u(lp).copy_(self._slice_local(full, lp.__dict__.get('_dist_mapping')))
+                    by_name[lp.name] = lp
+            if load_optimizer and self._optimizer is not None and os.path.exists(path + '.pdopt'):
+                osd = load(path + '.pdopt')
+                local = {}
+                for k, v in osd.items():
+                    if k == 'master_weights':
+                        local[k] = {pn: Tensor(self._slice_local(_u(t), by_name[pn].__dict__.get('_dist_mapping')))
+                                    if pn in by_name else t for pn, t in v.items()}
+                        continue
+                    pn = next((n for n in by_name if k.startswith(n + '_')), None)
+                    if pn is not None and isinstance(v, Tensor) and _u(v).dim() == _u(by_name[pn]).dim() \
+                            and _u(v).dim() > 0 and _u(v).numel() > 1:
+                        v = Tensor(self._slice_local(_u(v), by_name[pn].__dict__.get('_dist_mapping')))
+                    local[k] = v
+                self._optimizer.set_state_dict(local)
+            return
         if load_optimizer and self._optimizer is not None and os.path.exists(path + '.pdopt'):
             self._optimizer.set_state_dict(load(path + '.pdopt'))
 

@@ -725,9 +725,9 @@ class ShardedOptimizer:
         """ClipGradByValue / ClipGradByNorm on the owned gradient shards (reference
         python/paddle/nn/clip.py semantics). By value is element-wise: each rank clamps its own
         pieces. By norm is per parameter: the squared norms of every parameter's pieces are
-        summed in one vector all-reduce (plus the model-parallel group for TP-split parameters),
-        then each piece is scaled by clip_norm / max(||g_p||, clip_norm). Returns True when it
-        handled the clip."""
+        summed in one vector all-reduce over the sharding group (a TP-split parameter keeps its
+        mp-local norm, as the reference's per-tensor clip), then each piece is scaled by
+        clip_norm / max(||g_p||, clip_norm). Returns True when it handled the clip."""
         from ..nn.clip import ClipGradByValue, ClipGradByNorm
         clip = self._inner._grad_clip
         st = self.state
@@ -748,11 +748,9 @@ class ShardedOptimizer:
                 sq[index[id(p)]] += gs[gi][lo:hi].float().square().sum()
         if st.world > 1:
             dist.all_reduce(sq, group=st.pg)
-        if self._mp_pg is not None:
-            split = torch.tensor([bool(getattr(p, 'is_distributed', False)) for p in params], device=dev)
-            part = torch.where(split, sq, torch.zeros_like(sq))
-            dist.all_reduce(part, group=self._mp_pg)
-            sq = torch.where(split, part, sq)
+        # (no model-parallel reduction: the reference's ClipGradByNorm clips each LOCAL tensor by
+        # its own norm -- HybridParallelClipGrad wraps only ClipGradByGlobalNorm -- so a
+        # TP-split parameter is clipped by the norm of this mp rank's slice)
         scale = clip.clip_norm / torch.clamp(torch.sqrt(sq), min=clip.clip_norm)
         for gi, p, lo, hi, _ in self._pieces:
             if getattr(p, 'need_clip', True) and hi > lo:

@@ -223,7 +223,7 @@ def test_partitioner_hidden_split_embedding(tmp_path):
         assert o['comm'] == ['ap_allreduce'], o['comm']
 
 
-def _engine_static(rank, world, annotate):
+def _engine_static(rank, world, annotate, ckpt=None):
     """auto_parallel.Engine on a static program: the model is built in static mode (shard_tensor
     annotates its weights), prepare() completes + partitions, fit() trains."""
     import paddle_ray_amd as paddle
@@ -260,15 +260,36 @@ def _engine_static(rank, world, annotate):
         def __len__(self):
             return 32
 
+    specs = ([InputSpec([B, H], 'float32', 'x')], [InputSpec([B, 1], 'int64', 'y')])
     model = MLP()
-    opt = paddle.optimizer.SGD(0.2, parameters=model.parameters())
+    opt = paddle.optimizer.Momentum(0.2, momentum=0.9, parameters=model.parameters())
     eng = ap.Engine(model, nn.CrossEntropyLoss(), opt)
-    eng.prepare([InputSpec([B, H], 'float32', 'x')], [InputSpec([B, 1], 'int64', 'y')])
+    eng.prepare(*specs)
     hist = eng.fit(DS(), batch_size=B, epochs=2, verbose=0)
     ev = eng.evaluate(DS(), batch_size=B, verbose=0)
     shapes = [list(p.shape) for p in eng.local_parameters()]
+    out = {'loss': hist['loss'], 'eval': ev['loss'], 'shapes': shapes}
+    if ckpt is not None:
+        # save after fit (gathered full tensors), predict through the partitioned program, then
+        # a fresh engine (other init) loads the checkpoint: same predictions, same next step
+        pred = eng.predict(DS(), batch_size=B)
+        eng.save(ckpt)
+        more = eng.fit(DS(), batch_size=B, epochs=1, steps_per_epoch=2, verbose=0)['loss']
+        paddle.seed(99)
+        with paddle.utils.unique_name.guard():   # a fresh process's parameter names (.pdopt keys)
+            model2 = MLP()
+        opt2 = paddle.optimizer.Momentum(0.2, momentum=0.9, parameters=model2.parameters())
+        eng2 = ap.Engine(model2, nn.CrossEntropyLoss(), opt2)
+        eng2.prepare(*specs)
+        eng2.load(ckpt)
+        pred2 = eng2.predict(DS(), batch_size=B)
+        more2 = eng2.fit(DS(), batch_size=B, epochs=1, steps_per_epoch=2, verbose=0)['loss']
+        from paddle_ray_amd.framework.io import load
+        saved = {k: v.numpy() for k, v in load(ckpt + '.pdparams').items()}
+        out.update(pred=[p[0] for p in pred], pred2=[p[0] for p in pred2], more=more, more2=more2,
+                   saved=saved)
     paddle.disable_static()
-    return {'loss': hist['loss'], 'eval': ev['loss'], 'shapes': shapes}
+    return out
 
 
 def test_engine_static_partitioned_matches_serial(tmp_path):
@@ -281,6 +302,24 @@ def test_engine_static_partitioned_matches_serial(tmp_path):
         np.testing.assert_allclose(o['loss'], ref['loss'], rtol=1e-5, atol=1e-6)
         assert abs(o['eval'] - ref['eval']) < 1e-5
     assert ref['loss'][-1] < ref['loss'][0]
+
+
+def test_engine_static_save_load_predict(tmp_path):
+    """the static Engine saves the TRAINED shards (gathered to full tensors, same
+    file as an unpartitioned run), load() puts a checkpoint back into the shards, predict()
+    runs the partitioned program."""
+    (tmp_path / 'ref').mkdir()
+    (tmp_path / 'tp').mkdir()
+    ref = run_ranks(_engine_static, 2, tmp_path / 'ref', (False, str(tmp_path / 'ref' / 'ck')))[0]
+    res = run_ranks(_engine_static, 2, tmp_path / 'tp', (True, str(tmp_path / 'tp' / 'ck')))
+    for k, v in ref['saved'].items():
+        np.testing.assert_allclose(res[0]['saved'][k], v, rtol=1e-5, atol=1e-6)
+    for o in res + [ref]:
+        for a, b in zip(o['pred'], o['pred2']):
+            np.testing.assert_allclose(a, b, rtol=1e-6, atol=1e-6)
+        np.testing.assert_allclose(o['more'], o['more2'], rtol=1e-5, atol=1e-6)
+    for a, b in zip(res[0]['pred'], ref['pred']):
+        np.testing.assert_allclose(a, b, rtol=1e-5, atol=1e-5)
 
 
 def _run_dp_trace(rank, world, bucket_mb):
