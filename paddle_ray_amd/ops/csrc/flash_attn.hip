@@ -807,19 +807,26 @@ bwd_dq_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restr
 // ============================================================================
 // WDS: also store dS^T (bf16/f16, unscaled) to dsT[bh][key][query] (row pitch Sqp, Skp rows) for
 // bwd_dq_ds_kernel, which then forms dQ = dS K without recomputing S and dP.
-// dK/dV kernel LDS: [2][Q | dO] tile images, lse / delta [2][64] each, the dS^T stage (4 waves x
+// dK/dV kernel LDS: [2][Q | dO] tile images, lse / delta [2][64] each, the dS^T stage (NWV waves x
 // 32 rows x 80 B), the keep-bit words (EXT), then the block's K / V images ([2][64][D] each)
-template <typename T, int D, bool EXT>
+template <typename T, int D, bool EXT, int NWV = 4>
 __host__ __device__ constexpr int kKvOff() {
-  return 4 * kTile * D * (int)sizeof(T) + 4 * kTile * 4 + 4 * 32 * 80 + (EXT ? 2 * 256 * 4 : 0);
+  return 4 * kTile * D * (int)sizeof(T) + 4 * kTile * 4 + NWV * 32 * 80 + (EXT ? 2 * 256 * 4 : 0);
 }
-template <typename T, int D, bool EXT>
+template <typename T, int D, bool EXT, int NWV = 4>
 __host__ __device__ constexpr int kDkdvLds() {
-  return kKvOff<T, D, EXT>() + 4 * kTile * D * (int)sizeof(T);
+  return kKvOff<T, D, EXT, NWV>() + 4 * kTile * D * (int)sizeof(T);
 }
+// Query-split dK/dV (QS, head_dim 128): 8 waves per 128-key block, the pair (w, w + 4) sharing
+// 32 keys and each taking one 32-query half of every tile, so a wave holds ONE half's S / dP
+// accumulators (the dK / dV partials of its half) and the kernel runs two waves per SIMD: one
+// wave's softmax VALU, LDS reads and barrier waits hide under its partner's MFMAs (at one wave
+// per SIMD the dK/dV kernel measured ~25 % MFMA busy, profiles/r4/fa_pmc/summary.md). The pair's
+// partials are summed through LDS once at the end.
+__host__ __device__ constexpr int dkdv_waves(bool qs) { return qs ? 8 : 4; }
 
-template <typename T, int D, bool CAUSAL, bool WDS, bool EXT = false>
-__global__ void __launch_bounds__(256, D == 64 ? 2 : 1)
+template <typename T, int D, bool CAUSAL, bool WDS, bool EXT = false, bool QS = false>
+__global__ void __launch_bounds__(64 * dkdv_waves(QS), (D == 64 && !QS) ? 2 : 1)
 bwd_dkdv_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restrict__ v, const T* __restrict__ dO,
                 const float* __restrict__ lse, const float* __restrict__ delta, T* __restrict__ dk,
                 T* __restrict__ dv, int H, int SqM, int SkM, int64_t qsb, int64_t qss, int64_t qsh, int64_t ksb,
@@ -836,11 +843,14 @@ bwd_dkdv_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __res
   constexpr int NS = D / 16, ND = D / 32;
   const float LOG2E = 1.4426950408889634f;
 
+  constexpr int NWV = dkdv_waves(QS), NTH = 64 * NWV;
   const int kb = blockIdx.y;  // causal: key block 0 sweeps the most query tiles, launched first
   const int bh = blockIdx.x, b = bh / H, hh = bh % H;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+  // kw: the wave's 32-key group; qh (QS): the 32-query half of every tile it takes
+  const int kw = QS ? (wave & 3) : wave, qh = QS ? (wave >> 2) : 0;
   const int kblk0 = kb * 128;
-  const int mykey = kblk0 + wave * 32 + r;
+  const int mykey = kblk0 + kw * 32 + r;
   int Sq = SqM, Sk = SkM;
   int64_t qrow0 = (int64_t)b * SqM, krow0 = 0;
   if constexpr (EXT) {
@@ -866,9 +876,9 @@ bwd_dkdv_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __res
   // LDS-DMA below; rows >= Sk read as zero) and each tile re-reads the wave's fragments: holding
   // them in registers for the whole kernel (64 VGPRs at D = 128) pushed the S / dP accumulators
   // into AGPRs, and every softmax element then paid v_accvgpr reads / writes
-  const T* kvimg = reinterpret_cast<const T*>(smem + kKvOff<T, D, EXT>());
-  const T* Kw = kvimg + (wave >> 1) * kTile * D;        // image holding this wave's 32 keys
-  const T* Vw = kvimg + (2 + (wave >> 1)) * kTile * D;
+  const T* kvimg = reinterpret_cast<const T*>(smem + kKvOff<T, D, EXT, NWV>());
+  const T* Kw = kvimg + (kw >> 1) * kTile * D;          // image holding this wave's 32 keys
+  const T* Vw = kvimg + (2 + (kw >> 1)) * kTile * D;
   f32x16 acc_k[ND], acc_v[ND];
 #pragma unroll
   for (int i = 0; i < ND; ++i) { acc_k[i] = f32x16{}; acc_v[i] = f32x16{}; }
@@ -880,13 +890,13 @@ bwd_dkdv_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __res
   // Q / dO tiles by LDS-DMA straight into the swizzled images (rows >= Sq read as zero);
   // the tile's 64 lse / delta values go through registers
   const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
-  SwzDma<D, 256> qd, dd;
+  SwzDma<D, NTH> qd, dd;
   qd.init(qb_, qss, Sq, wave, lane);
   dd.init(dob_, HD, Sq, wave, lane);
   // EXT + dropout: the forward's keep-bit words of the tile's 64 queries x this block's 4 key
   // words ([2][4 waves][64] after the dS^T stage), staged with lse / delta
   const bool dbits = EXT && ext.thr && ext.dbits;
-  uint32_t* Mb = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(Dlb + 2 * kTile) + 4 * 32 * 80);
+  uint32_t* Mb = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(Dlb + 2 * kTile) + NWV * 32 * 80);
   const uint32_t mb0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)Mb;
   const uint32_t lsb0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)Lsb;
   const uint32_t dlb0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)Dlb;
@@ -905,17 +915,17 @@ bwd_dkdv_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __res
     dd.issue(img + kTile * D * sizeof(T), (uint32_t)((int64_t)qs0 * HD * 2), wave);
     if (wave == 0) dma_dword(lse_rs, (uint32_t)(qs0 + lane) * 4u, lsb0 + nb * kTile * 4);
     if (wave == 1) dma_dword(dl_rs, (uint32_t)(qs0 + lane) * 4u, dlb0 + nb * kTile * 4);
-    if (dbits) {
-      const int kw = (kblk0 >> 5) + wave;
-      const uint32_t off = kw < ext.dbits_ld ? (uint32_t)(((int64_t)(qs0 + lane) * ext.dbits_ld + kw) * 4) : 0x80000000u;
+    if (dbits && wave < 4) {
+      const int kwd = (kblk0 >> 5) + wave;
+      const uint32_t off = kwd < ext.dbits_ld ? (uint32_t)(((int64_t)(qs0 + lane) * ext.dbits_ld + kwd) * 4) : 0x80000000u;
       dma_dword(mb_rs, off, mb0 + (nb * 256 + wave * 64) * 4);
     }
   };
   {
-    SwzDma<D, 256> kd2, vd2;
+    SwzDma<D, NTH> kd2, vd2;
     kd2.init(kb_, kss, Sk, wave, lane);
     vd2.init(vb_, vss, Sk, wave, lane);
-    const uint32_t kv0 = lds0 + (uint32_t)kKvOff<T, D, EXT>();
+    const uint32_t kv0 = lds0 + (uint32_t)kKvOff<T, D, EXT, NWV>();
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       kd2.issue(kv0 + (uint32_t)(j * kTile * D * sizeof(T)), (uint32_t)((int64_t)(kblk0 + 64 * j) * kss * 2), wave);
@@ -935,7 +945,7 @@ bwd_dkdv_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __res
   // Rows up to the 128-rounded Sk are allocated.
   constexpr int SP = 80;  // stage row pitch, bytes
   char* stage = reinterpret_cast<char*>(Dlb + 2 * kTile) + wave * 32 * SP;
-  T* dsw = WDS ? dsT + (int64_t)bh * dsbh + (int64_t)(kblk0 + wave * 32 + (lane >> 2)) * Sqp + 8 * (lane & 3)
+  T* dsw = WDS ? dsT + (int64_t)bh * dsbh + (int64_t)(kblk0 + kw * 32 + (lane >> 2)) * Sqp + 8 * (lane & 3)
                : nullptr;
   // packed dS fragment of k-step ks (keys on lanes, queries 16ks + 4h + {0..3, 8..11} of the half)
   auto store_ds = [&](const typename V8<T>::type& sf, int ks) {
@@ -972,7 +982,70 @@ bwd_dkdv_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __res
     const float* Dl = Dlb + buf * kTile;
     const int qs0 = q_begin + it * kTile;
     if (it + 1 < ntiles) load_tile(qs0 + kTile);
-    {
+    if constexpr (QS) {
+      // one 32-query half (qh) of the tile: S^T / dP^T of the wave's 32 keys, softmax, then the
+      // dV / dK updates; the k-step fragments are read as they are consumed (no fragment set
+      // held across the tile: the wave stays within 256 registers)
+      const int nt = qh;
+      f32x16 sa = f32x16{}, da = f32x16{};
+#pragma unroll
+      for (int s2 = 0; s2 < NS; ++s2) {
+        const typename V8<T>::type kf = frag_rows<T, D>(Kw, lo, kw & 1, s2);
+        const typename V8<T>::type qf = frag_rows<T, D>(Qs, lo, nt, s2);
+        const typename V8<T>::type vf = frag_rows<T, D>(Vw, lo, kw & 1, s2);
+        const typename V8<T>::type df = frag_rows<T, D>(Ds, lo, nt, s2);
+        sa = mfma<T>(qf, kf, sa);
+        da = mfma<T>(df, vf, da);
+      }
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const float4 l4 = *reinterpret_cast<const float4*>(Ls + 32 * nt + 8 * g + 4 * h);
+        const float4 d4 = *reinterpret_cast<const float4*>(Dl + 32 * nt + 8 * g + 4 * h);
+        const float la[4] = {l4.x * LOG2E, l4.y * LOG2E, l4.z * LOG2E, l4.w * LOG2E},
+                    dl[4] = {d4.x, d4.y, d4.z, d4.w};
+        uint4 mw = make_uint4(0u, 0u, 0u, 0u);
+        if constexpr ((XF & XF_DROP) != 0)
+          mw = *reinterpret_cast<const uint4*>(Mb + buf * 256 + kw * 64 + 32 * nt + 8 * g + 4 * h);
+        const uint32_t mwa[4] = {mw.x, mw.y, mw.z, mw.w};
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const int i = 4 * g + c;
+          const int qq = qs0 + 32 * nt + 8 * g + 4 * h + c;
+          float sv = sa[i];
+          if constexpr ((XF & XF_FMASK) != 0) {
+            if (qq < Sq && kvalid) sv += fa_mask<T>(ext, b, hh, qq, mykey);
+          } else if constexpr ((XF & XF_KMASK) != 0) {
+            sv += kmv;
+          }
+          float p = fexp2(fmaf(sv, scale_log2, -la[c]));
+          if constexpr (MASK) {
+            if (qq >= Sq || (CAUSAL && mykey > qq + off)) p = 0.f;
+          }
+          if constexpr ((XF & XF_DROP) != 0) {
+            const float z = (mwa[c] >> (mykey & 31)) & 1u ? ext.inv_keep : 0.f;
+            sa[i] = p * z;
+            da[i] = p * (da[i] * z - dl[c]);
+            continue;
+          }
+          sa[i] = p;
+          da[i] = p * (da[i] - dl[c]);
+        }
+      }
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const typename V8<T>::type pf = pack_frag<T>(sa, 8 * ks);
+        const typename V8<T>::type sf = pack_frag<T>(da, 8 * ks);
+        if constexpr (WDS) store_ds(sf, ks);
+#pragma unroll
+        for (int dt = 0; dt < ND; ++dt) {
+          const typename V8<T>::type dtr = frag_tr<T, D>(Ds, lo, dt, 2 * nt + ks);
+          const typename V8<T>::type qtr = frag_tr<T, D>(Qs, lo, dt, 2 * nt + ks);
+          acc_v[dt] = mfma<T>(dtr, pf, acc_v[dt]);
+          acc_k[dt] = mfma<T>(qtr, sf, acc_k[dt]);
+        }
+      }
+      if constexpr (WDS) flush_ds(qs0 + 32 * nt);
+    } else {
       // software-pipelined tile: S/dP of BOTH 32-query halves first, then each half's softmax
       // VALU sits behind the other half's MFMAs in program order (nothing pins the order there),
       // so the matrix pipe keeps running while the exps issue. Masked tiles (causal diagonal,
@@ -1017,7 +1090,7 @@ bwd_dkdv_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __res
                       dl[4] = {d4.x, d4.y, d4.z, d4.w};
           uint4 mw = make_uint4(0u, 0u, 0u, 0u);
           if constexpr ((XF & XF_DROP) != 0)
-            mw = *reinterpret_cast<const uint4*>(Mb + buf * 256 + wave * 64 + 32 * nt + 8 * g + 4 * h);
+            mw = *reinterpret_cast<const uint4*>(Mb + buf * 256 + kw * 64 + 32 * nt + 8 * g + 4 * h);
           const uint32_t mwa[4] = {mw.x, mw.y, mw.z, mw.w};
 #pragma unroll
           for (int c = 0; c < 4; ++c) {
@@ -1065,9 +1138,9 @@ bwd_dkdv_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __res
       }
     }
     // the idle buffer was last read before the previous barrier; its DMA (Q / dO / lse / delta /
-    // keep bits) was issued at the top of this tile. Only the 4 dS^T stores of this tile (WDS) are
-    // younger: leave them in flight.
-    if constexpr (WDS) wait_vm<4>();
+    // keep bits) was issued at the top of this tile. Only the dS^T stores of this tile (WDS: 2 per
+    // 32-query half, QS waves store one half) are younger: leave them in flight.
+    if constexpr (WDS) wait_vm<QS ? 2 : 4>();
     else wait_vm<0>();
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS reads of the tile are done
     __builtin_amdgcn_s_barrier();
@@ -1098,19 +1171,48 @@ bwd_dkdv_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __res
     }
   }
 
+  if constexpr (QS) {
+    // the pair's partial dK / dV (the two query halves) summed through LDS: the upper-half wave
+    // parks its accumulators ([kw][register][lane] fp32, conflict-free), its partner adds them
+    float* xa = reinterpret_cast<float*>(smem);
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __syncthreads();  // every wave is done with the tile images and the dS^T stage
+    if (qh == 1) {
+#pragma unroll
+      for (int dt = 0; dt < ND; ++dt)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          xa[((kw * 2 * ND + dt) * 16 + e) * 64 + lane] = acc_k[dt][e];
+          xa[((kw * 2 * ND + ND + dt) * 16 + e) * 64 + lane] = acc_v[dt][e];
+        }
+    }
+    __syncthreads();
+    if (qh == 0) {
+#pragma unroll
+      for (int dt = 0; dt < ND; ++dt)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          acc_k[dt][e] += xa[((kw * 2 * ND + dt) * 16 + e) * 64 + lane];
+          acc_v[dt][e] += xa[((kw * 2 * ND + ND + dt) * 16 + e) * 64 + lane];
+        }
+    }
+    __syncthreads();  // the partial area is read before the stages below reuse it
+  }
   // bias-gradient partials: this block's 128 rounded dK / dV rows go through two padded [128][D+4]
   // LDS stages (the tile images are free now), then thread t sums column t of [dK | dV]
   constexpr int RP = D + 4;
   T* sk = img0;
   T* sv = img0 + 128 * RP;
   const bool bs = ext.bsum != nullptr;  // uniform
-  if (bs) {
+  if (bs && !QS) {
     __builtin_amdgcn_s_waitcnt(0xC07F);
     __syncthreads();  // every wave's reads of the last tile's images (and the dS^T stage) are done
   }
+  const bool writer = !QS || qh == 0;   // QS: the lower-half wave of each pair holds the sums
   T* krow = (vl ? dk + krow0 * dkss : dk + (int64_t)b * dksb) + (int64_t)mykey * dkss + (int64_t)hh * dksh;
   T* vrow = (vl ? dv + krow0 * dvss : dv + (int64_t)b * dvsb) + (int64_t)mykey * dvss + (int64_t)hh * dvsh;
-  const int srow = wave * 32 + r;
+  const int srow = kw * 32 + r;
+  if (writer)
 #pragma unroll
   for (int dt = 0; dt < ND; ++dt)
 #pragma unroll
@@ -1362,6 +1464,17 @@ static void launch_dq_ds(const void* k, void* dsT, void* dq, int B, int H, int S
   }
 }
 
+// PRA_FA_DKDV_QS=0: head_dim 128 dK/dV on the 4-wave kernel (one wave per SIMD) instead of the
+// query-split 8-wave one (A/B knob)
+static bool dkdv_qs() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("PRA_FA_DKDV_QS");
+    v = (e && !strcmp(e, "0")) ? 0 : 1;
+  }
+  return v == 1;
+}
+
 template <typename T, int D, bool C>
 static void launch_bwd(const void* q, const void* k, const void* v, const void* dO, const void* o, const float* lse,
                        float* delta, void* dq, void* dk, void* dv, void* dsT, int B, int H, int Sq, int Sk,
@@ -1374,15 +1487,18 @@ static void launch_bwd(const void* q, const void* k, const void* v, const void* 
     // dK/dV first (stores dS^T), then dQ = dS K; `delta` is an input here
     const int Sqp = (Sq + 255) / 256 * 256;
     const int64_t dsbh = (int64_t)((Sk + 127) / 128 * 128) * Sqp;
-    {
-      const size_t lds = kDkdvLds<T, D, false>();
-      auto kern = bwd_dkdv_kernel<T, D, C, true>;
+    auto go = [&](auto qs_c) {
+      constexpr bool QS = decltype(qs_c)::value;
+      const size_t lds = kDkdvLds<T, D, false, dkdv_waves(QS)>();
+      auto kern = bwd_dkdv_kernel<T, D, C, true, false, QS>;
       hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      hipLaunchKernelGGL(kern, dim3(B * H, (Sk + 127) / 128), dim3(256), lds, s, (const T*)q, (const T*)k,
-                         (const T*)v, (const T*)dO, lse, delta, (T*)dk, (T*)dv, H, Sq, Sk, st[0], st[1], st[2],
-                         st[3], st[4], st[5], st[6], st[7], st[8], st[12], st[13], st[14], st[15], st[16], st[17],
-                         scale, sl2, (T*)dsT, Sqp, dsbh, be);
-    }
+      hipLaunchKernelGGL(kern, dim3(B * H, (Sk + 127) / 128), dim3(64 * dkdv_waves(QS)), lds, s, (const T*)q,
+                         (const T*)k, (const T*)v, (const T*)dO, lse, delta, (T*)dk, (T*)dv, H, Sq, Sk, st[0], st[1],
+                         st[2], st[3], st[4], st[5], st[6], st[7], st[8], st[12], st[13], st[14], st[15], st[16],
+                         st[17], scale, sl2, (T*)dsT, Sqp, dsbh, be);
+    };
+    if (D == 128 && dkdv_qs()) go(std::true_type{});
+    else go(std::false_type{});
     launch_dq_ds<T, D, C, false>(k, dsT, dq, B, H, Sq, Sk, Sqp, dsbh, st, scale, be, s);
     return;
   }
@@ -1398,15 +1514,19 @@ static void launch_bwd(const void* q, const void* k, const void* v, const void* 
     };
     go(std::integral_constant<int, 8>{});
   }
-  {
-    const size_t lds = kDkdvLds<T, D, false>();
-    auto kern = bwd_dkdv_kernel<T, D, C, false>;
+  auto go = [&](auto qs_c) {
+    constexpr bool QS = decltype(qs_c)::value;
+    const size_t lds = kDkdvLds<T, D, false, dkdv_waves(QS)>();
+    auto kern = bwd_dkdv_kernel<T, D, C, false, false, QS>;
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(kern, dim3(B * H, (Sk + 127) / 128), dim3(256), lds, s, (const T*)q, (const T*)k,
-                       (const T*)v, (const T*)dO, lse, delta, (T*)dk, (T*)dv, H, Sq, Sk, st[0], st[1], st[2],
-                       st[3], st[4], st[5], st[6], st[7], st[8], st[12], st[13], st[14], st[15], st[16], st[17],
-                       scale, sl2, (T*)nullptr, 0, (int64_t)0, FaExt{});
-  }
+    hipLaunchKernelGGL(kern, dim3(B * H, (Sk + 127) / 128), dim3(64 * dkdv_waves(QS)), lds, s, (const T*)q,
+                       (const T*)k, (const T*)v, (const T*)dO, lse, delta, (T*)dk, (T*)dv, H, Sq, Sk, st[0], st[1],
+                       st[2], st[3], st[4], st[5], st[6], st[7], st[8], st[12], st[13], st[14], st[15], st[16],
+                       st[17], scale, sl2, (T*)nullptr, 0, (int64_t)0, FaExt{});
+  };
+  // (the same dK/dV kernel as the dS^T path: dV is bit-identical between the two dQ paths)
+  if (D == 128 && dkdv_qs()) go(std::true_type{});
+  else go(std::false_type{});
 }
 
 // extended variants (varlen / additive mask / dropout): forward + the dS^T backward
@@ -1430,15 +1550,18 @@ static void launch_bwd_ext(const void* q, const void* k, const void* v, const vo
   const float sl2 = scale * 1.4426950408889634f;
   const int Sqp = (Sq + 255) / 256 * 256;
   const int64_t dsbh = (int64_t)((Sk + 127) / 128 * 128) * Sqp;
-  {
-    const size_t lds = kDkdvLds<T, D, true>();
-    auto kern = bwd_dkdv_kernel<T, D, C, true, true>;
+  auto go = [&](auto qs_c) {
+    constexpr bool QS = decltype(qs_c)::value;
+    const size_t lds = kDkdvLds<T, D, true, dkdv_waves(QS)>();
+    auto kern = bwd_dkdv_kernel<T, D, C, true, true, QS>;
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(kern, dim3(B * H, (Sk + 127) / 128), dim3(256), lds, s, (const T*)q, (const T*)k,
-                       (const T*)v, (const T*)dO, lse, delta, (T*)dk, (T*)dv, H, Sq, Sk, st[0], st[1], st[2],
-                       st[3], st[4], st[5], st[6], st[7], st[8], st[12], st[13], st[14], st[15], st[16], st[17],
-                       scale, sl2, (T*)dsT, Sqp, dsbh, ext);
-  }
+    hipLaunchKernelGGL(kern, dim3(B * H, (Sk + 127) / 128), dim3(64 * dkdv_waves(QS)), lds, s, (const T*)q,
+                       (const T*)k, (const T*)v, (const T*)dO, lse, delta, (T*)dk, (T*)dv, H, Sq, Sk, st[0], st[1],
+                       st[2], st[3], st[4], st[5], st[6], st[7], st[8], st[12], st[13], st[14], st[15], st[16],
+                       st[17], scale, sl2, (T*)dsT, Sqp, dsbh, ext);
+  };
+  if (D == 128 && dkdv_qs()) go(std::true_type{});
+  else go(std::false_type{});
   launch_dq_ds<T, D, C, true>(k, dsT, dq, B, H, Sq, Sk, Sqp, dsbh, st, scale, ext, s);
 }
 

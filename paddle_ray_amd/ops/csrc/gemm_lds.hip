@@ -138,7 +138,10 @@ void launch_e(const void* A, const void* B, const void* bias, void* C, void* Z, 
   gemm_lds_kernel<T, CFG, AK, BK, E, BETA_, false><<<tiles, CFG::NT, 0, s>>>(pa, pb, pbias, pc, pz, colsum, M, N, K, \
                                                                            lda, ldb, ldc, ldz, ablate, nullptr)
   if (std::is_same<T, bf16>::value && E != kRelu && (g_force_pts || (pts_mask() >> layout & 1))) {
-    const bool w4 = layout == 1 && !(pts_mask() & 16);
+    // 4 waves (128x128 per wave, AGPR accumulators) for dy·Wᵀ unless mask bit 16, and for x·W
+    // with mask bit 32 or a per-call persistent request (the fused GELU forward: 486 vs 517 us
+    // per-tile at 16384 x 8192 x 2048, profiles/r5/gemm_fwd_probe.log); 8 waves otherwise
+    const bool w4 = (layout == 1 && !(pts_mask() & 16)) || (layout == 0 && ((pts_mask() & 32) || g_force_pts));
     if ((w4 ? pra_gemm_pts_w4 : pra_gemm_pts_w8)(layout, A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, kBF16,
                                                  E, beta, s) == 0)
       return;

@@ -1375,8 +1375,9 @@ def _gemm_hip(layout, a, b, out=None, bias=None, z=None, epi=None, beta=0, want_
     Returns None when the shape/layout is outside what the kernel assumes (caller falls back)."""
     if _GEMM_MODE == 'blas' or not (_gemm_operand_ok(a) and _gemm_operand_ok(b)) or a.dtype != b.dtype:
         return None
-    persist = layout == GEMM_NT and ((_GEMM_MODE == 'auto' and _nt_in_tree(a, b)) or
-                                     (epi == 'mulz' and _MLP_MULZ_PTS))
+    persist = (layout == GEMM_NT and ((_GEMM_MODE == 'auto' and _nt_in_tree(a, b)) or
+                                      (epi == 'mulz' and _MLP_MULZ_PTS))) or \
+        (layout == GEMM_FWD and epi in ('gelu_d', 'gelu_tanh_d') and _MLP_MULZ_PTS)
     if _GEMM_MODE == 'auto' and layout == GEMM_NT and not persist and epi != 'mulz' and \
             not (_MLP_DGELU_EPI and epi in ('dgelu', 'dgelu_tanh')):
         return None
@@ -1420,6 +1421,8 @@ def _gemm_hip(layout, a, b, out=None, bias=None, z=None, epi=None, beta=0, want_
                    _dt(a), e | (_PERSIST_BIT if persist else 0), int(beta), splits, _ptr(ws), _stream())
     except ValueError:
         return None
+    if want_colsum == 'part':
+        return out, part      # [ceil(M/256), N] fp32 per-tile-row column sums
     if want_colsum:
         cs = torch.empty(N, device=a.device, dtype=torch.float32)
         L.colsum_partials(part.data_ptr(), cs.data_ptr(), part.shape[0], N, 0, _stream())
@@ -2043,8 +2046,15 @@ class MlpGeluFn(torch.autograd.Function):
         x2 = x.reshape(-1, x.shape[-1])
         if ctx.save_d:
             # z holds gelu'(pre-activation): dz = dh * z and the fc1 bias gradient in the epilogue
-            dz, db1 = gemm(GEMM_NT, dy2, w2, z=z, epi='mulz', want_colsum=True)
-            db1 = db1.to(dz.dtype)
+            r = _gemm_hip(GEMM_NT, dy2, w2, z=z, epi='mulz', want_colsum='part') \
+                if R.select_backend(dy2, 'gemm') == 'hip' else None
+            if r is not None:
+                # the per-tile-row partials go straight into b1.grad (one launch)
+                dz, part = r
+                db1 = _colsum_rows_to_grad(part, ctx.b1, dz.dtype)
+            else:
+                dz, db1 = gemm(GEMM_NT, dy2, w2, z=z, epi='mulz', want_colsum=True)
+                db1 = db1.to(dz.dtype)
         elif _GEMM_MODE == 'auto' and not _MLP_DGELU_EPI and not (_MLP_DGELU_SHORTK and _nt_in_tree(dy2, w2)):
             # dgrad (hipBLASLt, or the in-tree persistent kernel for a short K: the gemm() shape
             # policy), then ONE fused pass for gelu'(z) and the bias gradient
@@ -2068,6 +2078,20 @@ class MlpGeluFn(torch.autograd.Function):
         else:
             dw1 = gemm(GEMM_TN, x2, dz)
         return dx, dw1, db1, dw2, None
+
+
+def _colsum_rows_to_grad(part, b, dtype):
+    """Bias gradient from fp32 partial rows [P, N]: added into ``b.grad`` when it exists (None
+    returned), else returned in ``dtype``."""
+    L = _native.lib()
+    nrb, cols = part.shape
+    g = b.grad if (b is not None and b.is_leaf) else None
+    if b is not None and _acc_grad_ok(g, b, dtype):
+        L.colsum16_acc(_ptr(part), _ptr(g), nrb, cols, _dt(g), _stream())
+        return None
+    db = torch.empty(cols, device=part.device, dtype=dtype)
+    L.colsum16(_ptr(part), _ptr(db), nrb, cols, _dt(db), _stream())
+    return db
 
 
 def _dgelu_db(dh, z, approximate, b=None):
