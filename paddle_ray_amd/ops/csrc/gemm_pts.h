@@ -255,12 +255,15 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_pts_kernel(const uint16_t* __r
     const int cbase = n0 + wc * CW;
     // after the swap a lane holds 8 consecutive columns of block jp + ((lane >> 4) & 1)
     const int sw_col = ((lane >> 4) & 1) * 16 + 8 * (lane >> 5);
-    uint2 bvp[TJ];  // this lane's 4 bias values per block, packed (unpacked where used)
+    // this lane's 4 bias values per block, packed (unpacked where used); weight gradients
+    // (xᵀ·dy) and the scaling dgrad epilogues never carry a bias: no registers for it there
+    constexpr bool HB = !DG && (AK || BK);
+    uint2 bvp[HB ? TJ : 1];
 #pragma unroll
-    for (int j = 0; j < TJ; ++j) {
+    for (int j = 0; j < (HB ? TJ : 1); ++j) {
       const int n = cbase + j * 16 + 4 * g;
       bvp[j] = make_uint2(0u, 0u);
-      if (!DG && bias && n < N) bvp[j] = *reinterpret_cast<const uint2*>(bias + n);
+      if (HB && bias && n < N) bvp[j] = *reinterpret_cast<const uint2*>(bias + n);
     }
     // The scaling (dgrad) epilogues walk the tile in NH column passes so that only TJ / NH blocks'
     // column sums are live at a time (all TJ of them pushed the kernel past 256 VGPRs: per-tile
@@ -274,7 +277,7 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_pts_kernel(const uint16_t* __r
         for (int r = 0; r < 4; ++r) cs[j][r] = 0.f;
 #pragma unroll
       for (int i = 0; i < TI; ++i) {
-        if constexpr (ZOP) __builtin_amdgcn_sched_barrier(0);  // keep the ring's loads in place
+        __builtin_amdgcn_sched_barrier(0);  // one 16-row block at a time (ring loads stay in place; no accumulator hoisting)
         const int m = rb + i * 16;
         const bool mok = m < M;
         const int64_t mr = mok ? m : 0;
@@ -300,11 +303,14 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_pts_kernel(const uint16_t* __r
             if constexpr (DG) {
 #pragma unroll
               for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r];
-            } else {
+            } else if constexpr (HB) {
               v[0] = acc[i][j][0] + to_f<T>(bvp[j].x & 0xffff);
               v[1] = acc[i][j][1] + to_f<T>(bvp[j].x >> 16);
               v[2] = acc[i][j][2] + to_f<T>(bvp[j].y & 0xffff);
               v[3] = acc[i][j][3] + to_f<T>(bvp[j].y >> 16);
+            } else {
+#pragma unroll
+              for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r];
             }
             if constexpr (DG) {
               const float z[4] = {to_f<T>(gz[u].x & 0xffff), to_f<T>(gz[u].x >> 16), to_f<T>(gz[u].y & 0xffff),

@@ -1439,9 +1439,16 @@ _NT_SHORTK = __import__('os').environ.get('PRA_GEMM_NT_SHORTK', '1') == '1'
 _PERSIST_BIT = 256
 
 
+# (PRA_GEMM_NT_MAXK: the bound. Round 5 measured 3072 -- BERT's 2304 / 3072-deep dgrads and
+# GPT's 2048-deep out-projection dgrad, at parity in isolation -- 0.3 % slower in both steps:
+# GPT 130.80 / 130.63 vs 130.41 / 130.33 ms, BERT 16.93 / 16.95 vs 16.87 / 16.86 ms,
+# profiles/r5/nt_maxk_ab.log)
+_NT_MAXK = int(__import__('os').environ.get('PRA_GEMM_NT_MAXK', '1024'))
+
+
 def _nt_in_tree(a, b):
     K = a.shape[1]
-    return _NT_SHORTK and a.dtype == torch.bfloat16 and 256 <= K <= 1024 and K % 128 == 0
+    return _NT_SHORTK and a.dtype == torch.bfloat16 and 256 <= K <= _NT_MAXK and K % 128 == 0
 
 
 def gemm(layout, a, b, out=None, bias=None, z=None, epi=None, beta=0, want_colsum=False):
