@@ -84,12 +84,13 @@ int pra_gemm_probe(int, int, const void*, const void*, void*, int, int, int, int
                    hipStream_t);
 int pra_gemm_get_w4();
 int pra_conv_lds(const void*, const void*, const void*, void*, int, int, int, int, int, int, int, int, int, int, int,
-                 int, float*, float*, const float*, hipStream_t);
+                 int, float*, float*, const float*, int, hipStream_t);
 int pra_conv_lds_stat_rows(int, int);
 int pra_conv_lds_splits(int, int, int);
 int pra_conv_wgrad_rows(int);
 int pra_conv_wgrad_lds(const void*, const void*, void*, int, int, int, int, int, int, int, int, int, int, int, float*,
-                       hipStream_t);
+                       int, hipStream_t);
+int pra_space_to_depth2(const void*, void*, int, int, int, int, int, int, int, hipStream_t);
 int pra_colsum_partials(const float*, void*, int, int, int, hipStream_t);
 void pra_bn_fwd_train(const void*, const void*, const void*, const void*, float*, float*, void*, uint8_t*, float*,
                       float*, float*, float*, int, int, int, float, float, int, int, int, hipStream_t);
@@ -123,19 +124,24 @@ PYBIND11_MODULE(_pra_hip, m) {
     check_launch("gemm_bias_act");
   });
   m.def("conv_lds", [](P x, P w, P bias, P y, int n, int h, int wd, int c, int cout, int kh, int kw, int st,
-                       int pad, int relu, int dt, int splits, P ws, P part, P kshift, P s) {
+                       int pad, int relu, int dt, int splits, P ws, P part, P kshift, int pp, P s) {
     if (pra_conv_lds(CV(x), CV(w), CV(bias), V(y), n, h, wd, c, cout, kh, kw, st, pad, relu, dt, splits,
                      reinterpret_cast<float*>(ws), reinterpret_cast<float*>(part),
-                     reinterpret_cast<const float*>(kshift), S(s)) != 0)
+                     reinterpret_cast<const float*>(kshift), pp, S(s)) != 0)
       throw std::invalid_argument("conv_lds: unsupported shape/dtype");
     check_launch("conv_lds");
   });
   m.def("conv_wgrad_lds", [](P dy, P x, P dw, int n, int h, int wd, int c, int cout, int kh, int kw, int st, int pad,
-                             int dt, int splits, P ws, P s) {
+                             int dt, int splits, P ws, int pp, P s) {
     if (pra_conv_wgrad_lds(CV(dy), CV(x), V(dw), n, h, wd, c, cout, kh, kw, st, pad, dt, splits,
-                           reinterpret_cast<float*>(ws), S(s)) != 0)
+                           reinterpret_cast<float*>(ws), pp, S(s)) != 0)
       throw std::invalid_argument("conv_wgrad_lds: unsupported shape/dtype");
     check_launch("conv_wgrad_lds");
+  });
+  m.def("space_to_depth2", [](P x, P y, int n, int h, int w, int c, int pad, int co, int dt, P s) {
+    if (pra_space_to_depth2(CV(x), V(y), n, h, w, c, pad, co, dt, S(s)) != 0)
+      throw std::invalid_argument("space_to_depth2: unsupported geometry");
+    check_launch("space_to_depth2");
   });
   m.def("conv_lds_splits", [](int m, int n, int k) { return pra_conv_lds_splits(m, n, k); });
   m.def("conv_wgrad_rows", [](int cout) { return pra_conv_wgrad_rows(cout); });

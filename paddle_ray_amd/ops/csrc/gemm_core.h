@@ -269,8 +269,12 @@ struct Dma {
 // pixel: the LDS-DMA gathers rows straight from x (per-lane source offsets), nothing is
 // materialised. The zero padding is the buffer descriptor's range check: a tap that falls
 // outside the image gets an offset past num_records and the DMA writes zeros to LDS.
+// PP: the input's pixel pitch in elements (its stored channel count). PP == C for a plain
+// convolution; PP < C lets a K-step of C = 64 columns span 64 / PP adjacent pixels of a
+// narrow-channel input (the space-to-depth stem: a 4-wide tap row of 16-channel pixels is one
+// contiguous 128-B segment), with taps counted in units of C columns.
 struct ConvGeom {
-  int Ho, Wo, H, W, C, KW, S, P;
+  int Ho, Wo, H, W, C, KW, S, P, PP;
 };
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -291,13 +295,13 @@ struct ConvDmaA {
       const int m = min(m0 + row, M - 1);
       const int wo = m % g.Wo, t = m / g.Wo, ho = t % g.Ho, img = t / g.Ho;
       const int hi = ho * g.S - g.P, wi = wo * g.S - g.P;
-      pix[n] = ((img * g.H + hi) * g.W + wi) * g.C + 8 * c;
+      pix[n] = ((img * g.H + hi) * g.W + wi) * g.PP + 8 * c;
       hw[n] = ((uint32_t)hi << 16) | ((uint32_t)wi & 0xffffu);
     }
     const uint64_t b = (uint64_t)x;
     rs[0] = __builtin_amdgcn_readfirstlane((uint32_t)b);
     rs[1] = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32)) & 0xffffu;  // stride 0
-    rs[2] = __builtin_amdgcn_readfirstlane((uint32_t)((int64_t)M / (g.Ho * g.Wo) * g.H * g.W * g.C * 2));
+    rs[2] = __builtin_amdgcn_readfirstlane((uint32_t)((int64_t)M / (g.Ho * g.Wo) * g.H * g.W * g.PP * 2));
     rs[3] = 0x00020000u;
     kt0 = 0;
   }
@@ -307,7 +311,7 @@ struct ConvDmaA {
     const int tap = k0 / g.C, cin0 = k0 - tap * g.C, kh = tap / g.KW, kw = tap - kh * g.KW;
     const int hi = ((int)hw[n] >> 16) + kh, wi = (int)(int16_t)(hw[n] & 0xffffu) + kw;
     const bool ok = (unsigned)hi < (unsigned)g.H && (unsigned)wi < (unsigned)g.W;
-    const uint32_t voff = ok ? (uint32_t)(pix[n] + (kh * g.W + kw) * g.C + cin0) * 2u : 0x80000000u;
+    const uint32_t voff = ok ? (uint32_t)(pix[n] + (kh * g.W + kw) * g.PP + cin0) * 2u : 0x80000000u;
     const uint32_t dst = __builtin_amdgcn_readfirstlane(lds_img + (n * NT + wave * 64) * 16);
     asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(rs),
                  "s"(dst)
@@ -332,7 +336,7 @@ struct ConvDmaBW {
   int dH, dW;           // 64 pixels = dH output rows + dW output columns
   __device__ __forceinline__ void seek(int n, int pix) {
     const int wo = pix % g.Wo, t = pix / g.Wo, ho = t % g.Ho, im = t / g.Ho;
-    base[n] = ((im * g.H + ho * g.S) * g.W + wo * g.S) * g.C;
+    base[n] = ((im * g.H + ho * g.S) * g.W + wo * g.S) * g.PP;
     hw[n] = ((uint32_t)ho << 16) | (uint32_t)wo;
   }
   __device__ __forceinline__ void init(const uint16_t* x, const ConvGeom& cg, int n0, int K, int tid) {
@@ -340,7 +344,7 @@ struct ConvDmaBW {
     const int k = tid >> 5, c = (tid & 31) ^ mc_swz(k);  // same column for every chunk
     const int col = n0 + 8 * c;
     const int tap = col / g.C, cin = col - tap * g.C, kh = tap / g.KW, kw = tap - kh * g.KW;
-    colterm = ((kh - g.P) * g.W + (kw - g.P)) * g.C + cin;
+    colterm = ((kh - g.P) * g.W + (kw - g.P)) * g.PP + cin;
     kp = ((uint32_t)(kh - g.P) << 16) | ((uint32_t)(kw - g.P) & 0xffffu);
     dH = 64 / g.Wo;
     dW = 64 - dH * g.Wo;
@@ -349,7 +353,7 @@ struct ConvDmaBW {
     const uint64_t b = (uint64_t)x;
     rs[0] = __builtin_amdgcn_readfirstlane((uint32_t)b);
     rs[1] = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32)) & 0xffffu;
-    rs[2] = __builtin_amdgcn_readfirstlane((uint32_t)((int64_t)K / (g.Ho * g.Wo) * g.H * g.W * g.C * 2));
+    rs[2] = __builtin_amdgcn_readfirstlane((uint32_t)((int64_t)K / (g.Ho * g.Wo) * g.H * g.W * g.PP * 2));
     rs[3] = 0x00020000u;
   }
   __device__ __forceinline__ void advance(int ksteps) {
@@ -367,12 +371,12 @@ struct ConvDmaBW {
                  "s"(dst)
                  : "memory");
     // this chunk's next staged K-step is 64 pixels further (carries, no divisions)
-    const int SC = g.S * g.C, SWC = g.S * g.W * g.C;
+    const int SC = g.S * g.PP, SWC = g.S * g.W * g.PP;
     wo += dW;
     ho += dH;
     int b = base[n] + dW * SC + dH * SWC;
     if (wo >= g.Wo) { wo -= g.Wo; ho += 1; b += SWC - g.Wo * SC; }
-    while (ho >= g.Ho) { ho -= g.Ho; b += g.H * g.W * g.C - g.Ho * SWC; }
+    while (ho >= g.Ho) { ho -= g.Ho; b += g.H * g.W * g.PP - g.Ho * SWC; }
     base[n] = b;
     hw[n] = ((uint32_t)ho << 16) | (uint32_t)wo;
   }

@@ -273,18 +273,24 @@ int launch_conv(const void* xpad, const void* W, const void* bias, void* Y, int 
 // part [2][pra_conv_lds_stat_rows(M, Cout)][Cout] (see launch_conv_cfg).
 extern "C" int pra_conv_lds_stat_rows(int M, int Cout) { return (M + pra::conv_tile_rows(Cout) - 1) / pra::conv_tile_rows(Cout); }
 
+// pp (0 = C): the input's pixel pitch when it is narrower than C (see ConvGeom::PP): then
+// KW == 1, P == 0, a tap row is C / pp adjacent pixels and Wo = (Wd - C / pp) / S + 1.
 extern "C" int pra_conv_lds(const void* x, const void* W, const void* bias, void* Y, int Nimg, int H, int Wd,
                             int C, int Cout, int KH, int KW, int S, int P, int relu, int dtype, int splits, float* ws,
-                            float* part, const float* kshift, hipStream_t s) {
+                            float* part, const float* kshift, int pp, hipStream_t s) {
+  if (pp <= 0) pp = C;
   if (C % 64 || Cout % 8 || KH <= 0 || KW <= 0 || S <= 0 || P < 0 || H <= 0 || Wd <= 0) return -1;
-  if (H >= 32768 || Wd >= 32768 || (long long)Nimg * H * Wd * C * 2 >= (1ll << 31)) return -1;
-  const int Ho = (H + 2 * P - KH) / S + 1, Wo = (Wd + 2 * P - KW) / S + 1;
+  if (pp != C && (pp % 8 || C % pp || KW != 1 || P != 0)) return -1;
+  if (H >= 32768 || Wd >= 32768 || (long long)Nimg * H * Wd * pp * 2 >= (1ll << 31)) return -1;
+  // (pp mode: a tap row is C / pp pixels wide)
+  const int Ho = (H + 2 * P - KH) / S + 1, Wo = (pp != C ? Wd - C / pp : Wd + 2 * P - KW) / S + 1;
   if (Ho <= 0 || Wo <= 0) return -1;
+  if (pp != C && (Wo - 1) * S + C / pp > Wd) return -1;
   const long long Mll = (long long)Nimg * Ho * Wo;
   if (Mll >= (1ll << 31)) return -1;
   const int M = (int)Mll, K = KH * KW * C;
   if (splits > 1 && (Cout <= 128 || !ws)) return -1;
-  pra::ConvGeom cg{Ho, Wo, H, Wd, C, KW, S, P};
+  pra::ConvGeom cg{Ho, Wo, H, Wd, C, KW, S, P, pp};
   if (dtype == pra::kBF16) return relu ? pra::launch_conv<pra::bf16, pra::kRelu>(x, W, bias, Y, M, Cout, K, cg, splits, ws, part, kshift, s)
                                   : pra::launch_conv<pra::bf16, pra::kNone>(x, W, bias, Y, M, Cout, K, cg, splits, ws, part, kshift, s);
   if (dtype == pra::kF16) return relu ? pra::launch_conv<pra::f16, pra::kRelu>(x, W, bias, Y, M, Cout, K, cg, splits, ws, part, kshift, s)
@@ -298,16 +304,21 @@ extern "C" int pra_conv_lds(const void* x, const void* W, const void* bias, void
 // output-channel rows per weight-gradient tile (the caller sizes split-K from it)
 extern "C" int pra_conv_wgrad_rows(int Cout) { return pra::conv_wgrad_rows(Cout); }
 extern "C" int pra_conv_wgrad_lds(const void* dy, const void* x, void* dW, int Nimg, int H, int Wd, int C, int Cout,
-                                  int KH, int KW, int S, int P, int dtype, int splits, float* ws, hipStream_t s) {
+                                  int KH, int KW, int S, int P, int dtype, int splits, float* ws, int pp,
+                                  hipStream_t s) {
+  if (pp <= 0) pp = C;
   if (C % 64 || Cout % 8 || Cout < 8 || KH <= 0 || KW <= 0 || S <= 0 || P < 0 || H <= 0 || Wd <= 0) return -1;
-  if (H >= 32768 || Wd >= 32768 || (long long)Nimg * H * Wd * C * 2 >= (1ll << 31)) return -1;
-  const int Ho = (H + 2 * P - KH) / S + 1, Wo = (Wd + 2 * P - KW) / S + 1;
+  if (pp != C && (pp % 8 || C % pp || KW != 1 || P != 0)) return -1;
+  if (H >= 32768 || Wd >= 32768 || (long long)Nimg * H * Wd * pp * 2 >= (1ll << 31)) return -1;
+  // (pp mode: a tap row is C / pp pixels wide)
+  const int Ho = (H + 2 * P - KH) / S + 1, Wo = (pp != C ? Wd - C / pp : Wd + 2 * P - KW) / S + 1;
   if (Ho <= 0 || Wo <= 0) return -1;
+  if (pp != C && (Wo - 1) * S + C / pp > Wd) return -1;
   const long long Mll = (long long)Nimg * Ho * Wo;
   if (Mll >= (1ll << 31) || Mll % 64 || (long long)Mll * Cout * 2 >= (1ll << 32)) return -1;
   if (splits > 1 && !ws) return -1;
   const int Nk = KH * KW * C;
-  pra::ConvGeom cg{Ho, Wo, H, Wd, C, KW, S, P};
+  pra::ConvGeom cg{Ho, Wo, H, Wd, C, KW, S, P, pp};
   if (dtype == pra::kBF16) pra::launch_conv_wgrad<pra::bf16>(dy, x, dW, (int)Mll, Cout, Nk, cg, splits, ws, s);
   else if (dtype == pra::kF16) pra::launch_conv_wgrad<pra::f16>(dy, x, dW, (int)Mll, Cout, Nk, cg, splits, ws, s);
   else return -1;

@@ -87,6 +87,55 @@ __global__ void __launch_bounds__(256) max_pool_bwd_k(const T* __restrict__ dy, 
   store8<T>(dx + v * 8, acc);
 }
 
+
+// 2x2 space-to-depth with zero padding, channels-last: x [N][H][W][C] ->
+// y [N][(H+2P)/2][(W+2P)/2][CO], y[n][i][j][(2dy+dx)*C + c] = x[n][2i+dy-P][2j+dx-P][c] (zero
+// outside the image and in the channels 4C..CO-1). Feeds the stride-2 stem convolution as a
+// stride-1 one on the 16-channel image (gemm_lds.hip pixel-pitch mode). One lane per output
+// pixel, 16-B stores.
+template <typename T>
+__global__ void __launch_bounds__(256) s2d2_k(const T* __restrict__ x, T* __restrict__ y, int H, int W, int C, int P,
+                                              int Hs, int Ws, int CO, int64_t npix) {
+  const int64_t pix = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (pix >= npix) return;
+  const int j = (int)(pix % Ws);
+  const int64_t t = pix / Ws;
+  const int i = (int)(t % Hs);
+  const int64_t n = t / Hs;
+  for (int q = 0; q < CO / 8; ++q) {
+    uint32_t w4[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      uint16_t h2[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int k = q * 8 + 2 * e + u, blk = k / C, c = k - blk * C;
+        const int hh = 2 * i + (blk >> 1) - P, ww = 2 * j + (blk & 1) - P;
+        h2[u] = 0;
+        if (blk < 4 && (unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W)
+          h2[u] = reinterpret_cast<const uint16_t*>(x)[((n * H + hh) * W + ww) * C + c];
+      }
+      w4[e] = (uint32_t)h2[0] | ((uint32_t)h2[1] << 16);
+    }
+    *reinterpret_cast<uint4*>(y + pix * CO + q * 8) = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+  }
+}
+
+}  // namespace pra
+
+extern "C" int pra_space_to_depth2(const void* x, void* y, int N, int H, int W, int C, int P, int CO, int dt,
+                                   hipStream_t s) {
+  if (N <= 0 || H <= 0 || W <= 0 || C <= 0 || P < 0 || CO % 8 || CO < 4 * C || (H + 2 * P) % 2 || (W + 2 * P) % 2)
+    return -1;
+  if (dt != pra::kBF16 && dt != pra::kF16) return -1;
+  const int Hs = (H + 2 * P) / 2, Ws = (W + 2 * P) / 2;
+  const int64_t npix = (int64_t)N * Hs * Ws;
+  pra::s2d2_k<uint16_t><<<(unsigned)((npix + 255) / 256), 256, 0, s>>>(
+      static_cast<const uint16_t*>(x), static_cast<uint16_t*>(y), H, W, C, P, Hs, Ws, CO, npix);
+  return 0;
+}
+
+namespace pra {
 }  // namespace pra
 
 using pra::PoolGeom;

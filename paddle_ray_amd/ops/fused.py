@@ -1687,7 +1687,7 @@ def conv_kxk_supported(x, w, stride, padding):
             and x.numel() * 2 < 2 ** 31 and max(x.shape[1], x.shape[2]) < 32768)
 
 
-def _conv_lds(x, wk, bias, kh, kw, stride, pad, relu=False, stats_shift=None):
+def _conv_lds(x, wk, bias, kh, kw, stride, pad, relu=False, stats_shift=None, cv=None):
     """y[N,Ho,Wo,Cout] = conv(x NHWC, wk [Cout, kh*kw*C] (OHWI)) via the implicit-GEMM kernel
     (zero padding applied by the kernel's DMA range check, the input is read in place).
     stats_shift (fp32 [Cout], e.g. the BN running mean): the epilogue also returns the per-tile
@@ -1695,7 +1695,13 @@ def _conv_lds(x, wk, bias, kh, kw, stride, pad, relu=False, stats_shift=None):
     n, h, wd, c = x.shape
     cout = wk.shape[0]
     x = x.contiguous()
-    ho, wo = (h + 2 * pad - kh) // stride + 1, (wd + 2 * pad - kw) // stride + 1
+    pp = 0
+    if cv is not None and cv != c:
+        # pixel-pitch mode (gemm_lds.hip ConvGeom::PP): taps of cv columns = cv // c adjacent pixels
+        pp, c = c, cv
+        ho, wo = (h - kh) // stride + 1, (wd - c // pp) // stride + 1
+    else:
+        ho, wo = (h + 2 * pad - kh) // stride + 1, (wd + 2 * pad - kw) // stride + 1
     y = torch.empty((n, ho, wo, cout), device=x.device, dtype=x.dtype)
     if bias is not None and (bias.dtype != x.dtype or not bias.is_contiguous()):
         bias = bias.to(x.dtype).contiguous()
@@ -1709,7 +1715,7 @@ def _conv_lds(x, wk, bias, kh, kw, stride, pad, relu=False, stats_shift=None):
         splits = L.conv_lds_splits(m, cout, kh * kw * c)
     ws = torch.empty((splits, m, cout), device=x.device, dtype=torch.float32) if splits > 1 else None
     L.conv_lds(x.data_ptr(), wk.data_ptr(), _ptr(bias), y.data_ptr(), n, h, wd, c, cout, kh, kw,
-               stride, pad, int(relu), _dt(x), splits, _ptr(ws), _ptr(part), _ptr(stats_shift), _stream())
+               stride, pad, int(relu), _dt(x), splits, _ptr(ws), _ptr(part), _ptr(stats_shift), pp, _stream())
     return y if stats_shift is None else (y, part)
 
 
@@ -1724,10 +1730,13 @@ def _conv_wgrad_ok(x, dy, cout):
             and (dy.shape[0] * dy.shape[1] * dy.shape[2]) % 64 == 0 and max(h, wd) < 32768)
 
 
-def _conv_wgrad_lds(dy, x, kh, kw, stride, pad):
+def _conv_wgrad_lds(dy, x, kh, kw, stride, pad, cv=None):
     """dW [Cout, kh, kw, C] (OHWI) = dyᵀ · im2col(x) on the implicit-GEMM kernel (split-K over
-    the output pixels, im2col rows gathered by the DMA)."""
+    the output pixels, im2col rows gathered by the DMA). cv: pixel-pitch mode (see _conv_lds)."""
     n, h, wd, c = x.shape
+    pp = 0
+    if cv is not None and cv != c:
+        pp, c = c, cv
     cout = dy.shape[3]
     L = _native.lib()
     mpix = dy.shape[0] * dy.shape[1] * dy.shape[2]
@@ -1740,7 +1749,7 @@ def _conv_wgrad_lds(dy, x, kh, kw, stride, pad):
     ws = torch.empty((splits, cout, nk), device=x.device, dtype=torch.float32) if splits > 1 else None
     dw = torch.empty((cout, kh, kw, c), device=x.device, dtype=x.dtype)
     L.conv_wgrad_lds(dy.data_ptr(), x.data_ptr(), dw.data_ptr(), n, h, wd, c, cout, kh, kw, stride, pad,
-                     _dt(x), splits, _ptr(ws), _stream())
+                     _dt(x), splits, _ptr(ws), pp, _stream())
     return dw
 
 
@@ -1811,6 +1820,108 @@ class ConvKxKStatsFn(ConvKxKFn):
         return ConvKxKFn.backward(ctx, dy) + (None,)
 
 
+# =============================================================================
+# Narrow-input stride-2 convolution (the ResNet stem: 7x7/2 over 3 channels) as a stride-1
+# convolution over the 2x2 space-to-depth image (16 channels, zero-padded), on the implicit-GEMM
+# kernel in pixel-pitch mode: a row of ceil(K/2) taps x 16 channels is ONE contiguous 128-B
+# segment, so the LDS-DMA gathers it like a 64-channel tap (gemm_lds.hip ConvGeom::PP). The
+# reference runs this layer on cuDNN (phi gpudnn conv kernels); here no library conv is left.
+# =============================================================================
+_S2D_CO = 16
+
+
+def stem_conv_supported(x, w, stride, padding):
+    if not (x.is_cuda and x.dim() == 4 and w.dim() == 4 and x.dtype in _HALF and w.dtype == x.dtype):
+        return False
+    cout, cin, kh, kw = w.shape
+    kt = (kh + 1) // 2
+    n, h, wd, c = x.shape
+    return (stride == 2 and kh == kw and c == cin and 4 * cin <= _S2D_CO and kt * _S2D_CO == 64
+            and cout % 8 == 0 and (h + 2 * padding) % 2 == 0 and (wd + 2 * padding) % 2 == 0
+            and (h + 2 * padding - kh) // 2 + 1 == (h + 2 * padding) // 2 - kt + 1
+            and (wd + 2 * padding - kw) // 2 + 1 == (wd + 2 * padding) // 2 - kt + 1
+            and n * ((h + 2 * padding) // 2) * ((wd + 2 * padding) // 2) * _S2D_CO * 2 < 2 ** 31)
+
+
+_STEM_IDX = {}
+
+
+def _stem_index(w):
+    """Gather index of the stride-1 filter [Cout, kt, 1, kt*16] over w.flatten() (-1: zero tap):
+    w'[o][KY][kx*16 + (2dy+dx)*Cin + c] = w[o][c][2KY+dy][2kx+dx]."""
+    cout, cin, kh, kw = w.shape
+    key = (cout, cin, kh, kw, w.device)
+    idx = _STEM_IDX.get(key)
+    if idx is None:
+        kt = (kh + 1) // 2
+        idx = torch.full((cout, kt, kt * _S2D_CO), -1, dtype=torch.long)
+        for KY in range(kt):
+            for kx in range(kt):
+                for dy in range(2):
+                    for dx in range(2):
+                        ky, kxx = 2 * KY + dy, 2 * kx + dx
+                        if ky >= kh or kxx >= kw:
+                            continue
+                        for c in range(cin):
+                            col = kx * _S2D_CO + (2 * dy + dx) * cin + c
+                            idx[:, KY, col] = torch.arange(cout) * cin * kh * kw + (c * kh + ky) * kw + kxx
+        idx = _STEM_IDX[key] = idx.to(w.device)
+    return idx
+
+
+class StemConvFn(torch.autograd.Function):
+    """y = conv2d(x, w, stride 2, padding p) for a narrow channels-last input, through the
+    space-to-depth stride-1 form; optional BN partial statistics of y (epilogue column sums
+    around ``shift``). dx is not formed (the stem's input is data); dW = dyᵀ · im2col(s2d(x))
+    on the weight-gradient kernel, scattered back to [Cout, Cin, K, K]."""
+
+    @staticmethod
+    def forward(ctx, x, w, pad, shift):
+        n, h, wd, c = x.shape
+        cout, cin, kh, kw = w.shape
+        kt = (kh + 1) // 2
+        L = _native.lib()
+        hs, ws = (h + 2 * pad) // 2, (wd + 2 * pad) // 2
+        xs = torch.empty((n, hs, ws, _S2D_CO), device=x.device, dtype=x.dtype)
+        L.space_to_depth2(x.data_ptr(), xs.data_ptr(), n, h, wd, c, pad, _S2D_CO, _dt(x), _stream())
+        idx = _stem_index(w)
+        wflat = w.reshape(-1)
+        wk = torch.where(idx >= 0, wflat[idx.clamp(min=0)], torch.zeros((), dtype=w.dtype, device=w.device))
+        wk = wk.reshape(cout, kt * kt * _S2D_CO).contiguous()
+        r = _conv_lds(xs, wk, None, kt, 1, 1, 0, stats_shift=shift, cv=kt * _S2D_CO)
+        ctx.save_for_backward(xs, idx, x, w)
+        ctx.meta = (kt, w.shape, pad)
+        if shift is None:
+            return r, None
+        y, part = r
+        ctx.mark_non_differentiable(part)
+        return y, part
+
+    @staticmethod
+    def backward(ctx, dy, dpart):
+        xs, idx, x, w = ctx.saved_tensors
+        kt, wshape, pad = ctx.meta
+        dw = None
+        if ctx.needs_input_grad[1]:
+            dy = dy.contiguous()
+            if (dy.shape[0] * dy.shape[1] * dy.shape[2]) % 64 == 0:
+                dwk = _conv_wgrad_lds(dy, xs, kt, 1, 1, 0, cv=kt * _S2D_CO).reshape(idx.shape)
+                valid = idx >= 0
+                dw = torch.zeros(int(torch.tensor(wshape).prod()), device=dwk.device, dtype=dwk.dtype)
+                dw.index_copy_(0, idx[valid], dwk[valid])
+                dw = dw.view(wshape)
+            else:   # the weight-gradient kernel walks the output pixels 64 at a time
+                _, dw, _ = torch.ops.aten.convolution_backward(
+                    dy.permute(0, 3, 1, 2), x.permute(0, 3, 1, 2), w, None, [2, 2], [pad, pad], [1, 1],
+                    False, [0, 0], 1, [False, True, False])
+        assert not ctx.needs_input_grad[0], "stem conv: input gradient not supported on this path"
+        return None, dw, None, None
+
+
+def stem_conv_nhwc(x, w, padding):
+    return StemConvFn.apply(x, w, int(padding), None)[0]
+
+
 def conv_bn_act_nhwc(x, w, stride, padding, bn_w, bn_b, rmean, rvar, training, momentum=0.9,
                      eps=1e-5, z=None, relu=True):
     """act(BN(conv(x)) [+ z]) for channels-last KxK convolutions with the BatchNorm statistics
@@ -1823,11 +1934,19 @@ def conv_bn_act_nhwc(x, w, stride, padding, bn_w, bn_b, rmean, rvar, training, m
         y, part = ConvKxKStatsFn.apply(x, w, None, int(stride), int(padding), rmean)
         return BatchNormActFn.apply(y, z, bn_w, bn_b, rmean, rvar, training, momentum, eps, relu,
                                     _join_for(z) if z is not None else None, (part, rmean))
+    if (_STEM_S2D and not x.requires_grad and stem_conv_supported(x, w, stride, padding)
+            and training and rmean is not None and rmean.dtype == torch.float32 and rmean.is_contiguous()
+            and R.select_backend(x, 'batch_norm_fwd') == 'hip'):
+        y, part = StemConvFn.apply(x, w, int(padding), rmean)
+        return BatchNormActFn.apply(y, z, bn_w, bn_b, rmean, rvar, training, momentum, eps, relu,
+                                    _join_for(z) if z is not None else None, (part, rmean))
     if conv1x1_bn_stats_ok(x, w, stride, padding, rmean, training):
         y, part = Conv1x1StatsFn.apply(x, w, int(stride), int(stride), _join_for(x), rmean)
         return BatchNormActFn.apply(y, z, bn_w, bn_b, rmean, rvar, training, momentum, eps, relu,
                                     _join_for(z) if z is not None else None, (part, rmean))
-    if w.shape[2] == w.shape[3] > 1 and conv_kxk_supported(x, w, stride, padding):
+    if _STEM_S2D and not x.requires_grad and stem_conv_supported(x, w, stride, padding):
+        y = stem_conv_nhwc(x, w, padding)
+    elif w.shape[2] == w.shape[3] > 1 and conv_kxk_supported(x, w, stride, padding):
         y = conv_kxk_nhwc(x, w, None, stride, padding)
     elif w.shape[2:] == (1, 1) and padding == 0 and x.is_cuda and x.dtype in _HALF:
         y = conv1x1_nhwc(x, w, None, (stride, stride))
@@ -1837,6 +1956,8 @@ def conv_bn_act_nhwc(x, w, stride, padding, bn_w, bn_b, rmean, rvar, training, m
 
 
 _CONV_BN_STATS = __import__('os').environ.get('PRA_CONV_BN_STATS', '1') == '1'
+# PRA_STEM_S2D=0: the narrow-input stride-2 stem through MIOpen instead (A/B)
+_STEM_S2D = __import__('os').environ.get('PRA_STEM_S2D', '1') == '1'
 
 
 def conv_bn_stats_ok(x, w, stride, padding, rmean, training):

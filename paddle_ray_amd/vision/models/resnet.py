@@ -151,7 +151,7 @@ class ResNet(nn.Layer):
         return nn.Sequential(*layers)
 
     def forward(self, x):
-        x = self.maxpool(_bn_act(self.bn1, self.conv1(x)))
+        x = self.maxpool(_conv_bn_act(self.conv1, self.bn1, x))
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         if self.with_pool:
             x = self.avgpool(x)

@@ -68,3 +68,47 @@ def test_conv_wgrad_lds(case):
         dy.float().permute(0, 3, 1, 2))
     err = (got - wr.grad).abs().max().item()
     assert err <= 1e-2 * wr.grad.abs().max().item() + 1e-2, err
+
+
+STEM_CASES = [
+    # n, h, w, cin, cout, k, pad
+    (2, 224, 224, 3, 64, 7, 3),     # ResNet stem
+    (3, 30, 26, 3, 64, 7, 3),
+    (2, 20, 18, 4, 32, 7, 3),
+    (1, 18, 14, 3, 16, 7, 3),       # 63 output pixels: weight gradient falls back
+]
+
+
+def test_stem_supported_cpu():
+    x = torch.zeros(1, 224, 224, 3, dtype=torch.bfloat16)
+    w = torch.zeros(64, 3, 7, 7, dtype=torch.bfloat16)
+    assert not K.stem_conv_supported(x, w, 2, 3)   # host tensors never reach the kernel
+    idx = K._stem_index(w)                         # every filter tap appears exactly once
+    v = idx[idx >= 0]
+    assert v.numel() == w.numel() and v.unique().numel() == w.numel()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", STEM_CASES)
+def test_stem_conv_s2d(case):
+    """Stride-2 narrow-input conv through space-to-depth + the pixel-pitch implicit GEMM: forward,
+    BN partial statistics and the weight gradient vs fp32 PyTorch."""
+    n, h, w_, cin, cout, k, p = case
+    torch.manual_seed(1)
+    x = torch.randn(n, h, w_, cin, device='cuda', dtype=torch.bfloat16)
+    w = (torch.randn(cout, cin, k, k, device='cuda') / (cin * k * k) ** 0.5).to(torch.bfloat16)
+    assert K.stem_conv_supported(x, w, 2, p)
+    shift = torch.randn(cout, device='cuda') * 0.1
+    wh = w.clone().requires_grad_()
+    y, part = K.StemConvFn.apply(x, wh, p, shift)
+    wr = w.float().requires_grad_()
+    yr = torch.nn.functional.conv2d(x.float().permute(0, 3, 1, 2), wr, None, 2, p).permute(0, 2, 3, 1)
+    assert y.shape == yr.shape
+    torch.testing.assert_close(y.float(), yr, atol=3e-2, rtol=3e-2)
+    d = y.float().reshape(-1, cout) - shift
+    torch.testing.assert_close(part[0].sum(0), d.sum(0), atol=0.5, rtol=1e-2)
+    torch.testing.assert_close(part[1].sum(0), (d * d).sum(0), atol=0.5, rtol=1e-2)
+    g = torch.randn_like(y)
+    y.backward(g)
+    yr.backward(g.float())
+    torch.testing.assert_close(wh.grad.float(), wr.grad, atol=5e-2 * wr.grad.abs().max().item(), rtol=3e-2)
