@@ -268,6 +268,8 @@ def bench_resnet(a, paddle, torch, dist, C, world, rank, dev):
         opt.clear_grad()
 
     dt = _timed(step, a, torch, dist, world, dev)
+    if a.profile_dir:
+        _op_profile(step, a, torch, rank)
     ips = bs * world * a.steps / dt
     return {"metric": "samples/sec ResNet50 bf16", "value": round(ips, 2), "unit": "images/s",
             "n_gpus": world, "steps": a.steps, "warmup": a.warmup,

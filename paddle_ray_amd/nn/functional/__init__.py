@@ -659,6 +659,10 @@ def adaptive_avg_pool1d(x, output_size, name=None):
 
 
 def adaptive_avg_pool2d(x, output_size, data_format='NCHW', name=None):
+    if data_format == 'NHWC' and output_size in (1, (1, 1), [1, 1]):
+        t = _t(x)
+        if K.global_avg_pool_nhwc_supported(t):
+            return _w(K.GlobalAvgPoolNHWCFn.apply(t))
     return _adaptive(TF.adaptive_avg_pool2d, x, output_size, data_format)
 
 

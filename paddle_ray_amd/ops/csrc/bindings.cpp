@@ -84,7 +84,7 @@ int pra_gemm_probe(int, int, const void*, const void*, void*, int, int, int, int
                    hipStream_t);
 int pra_gemm_get_w4();
 int pra_conv_lds(const void*, const void*, const void*, void*, int, int, int, int, int, int, int, int, int, int, int,
-                 int, float*, float*, const float*, int, hipStream_t);
+                 int, float*, float*, const float*, int, hipStream_t, const void*, const uint8_t*);
 int pra_conv_lds_stat_rows(int, int);
 int pra_conv_lds_splits(int, int, int);
 int pra_conv_wgrad_rows(int);
@@ -101,6 +101,10 @@ void pra_bn_fwd_infer(const void*, const void*, const void*, const void*, const 
                       int, int, float, int, int, int, hipStream_t);
 void pra_bn_bwd(const void*, const void*, const uint8_t*, const void*, const void*, const float*, const float*, void*,
                 void*, void*, void*, float*, float*, int, int, int, int, int, int, int, hipStream_t);
+void pra_bn_premerge(const float*, float*, int, int, hipStream_t);
+int pra_gap_bwd(const void*, void*, int, int, int, int, hipStream_t);
+void pra_bn_bwd_parts(const void*, const void*, const void*, const float*, const float*, void*, void*, void*,
+                      const float*, float*, int, int, int, int, int, int, hipStream_t);
 }
 
 #define V(x) reinterpret_cast<void*>(x)
@@ -124,10 +128,11 @@ PYBIND11_MODULE(_pra_hip, m) {
     check_launch("gemm_bias_act");
   });
   m.def("conv_lds", [](P x, P w, P bias, P y, int n, int h, int wd, int c, int cout, int kh, int kw, int st,
-                       int pad, int relu, int dt, int splits, P ws, P part, P kshift, int pp, P s) {
+                       int pad, int relu, int dt, int splits, P ws, P part, P kshift, int pp, P s, P bnx, P bnmask) {
     if (pra_conv_lds(CV(x), CV(w), CV(bias), V(y), n, h, wd, c, cout, kh, kw, st, pad, relu, dt, splits,
                      reinterpret_cast<float*>(ws), reinterpret_cast<float*>(part),
-                     reinterpret_cast<const float*>(kshift), pp, S(s)) != 0)
+                     reinterpret_cast<const float*>(kshift), pp, S(s), CV(bnx),
+                     reinterpret_cast<const uint8_t*>(bnmask)) != 0)
       throw std::invalid_argument("conv_lds: unsupported shape/dtype");
     check_launch("conv_lds");
   });
@@ -351,6 +356,20 @@ PYBIND11_MODULE(_pra_hip, m) {
     pra_bn_bwd(CV(dy), CV(y), reinterpret_cast<const uint8_t*>(mask), CV(x), CV(w), CF(mean), CF(invstd), V(dx), V(dz),
                V(dw), V(db), F(part), F(coef), M, C, nrb, relu, dt, dtw, acc, S(s));
     check_launch("bn_bwd");
+  });
+  m.def("gap_bwd", [](P dy, P dx, int n, int hw, int c, int dt, P s) {
+    if (pra_gap_bwd(CV(dy), V(dx), n, hw, c, dt, S(s)) != 0) throw std::invalid_argument("gap_bwd: unsupported shape");
+    check_launch("gap_bwd");
+  });
+  m.def("bn_premerge", [](P part, P out, int nrb, int C, P s) {
+    pra_bn_premerge(reinterpret_cast<const float*>(part), F(out), nrb, C, S(s));
+    check_launch("bn_premerge");
+  });
+  m.def("bn_bwd_parts", [](P g, P x, P w, P mean, P invstd, P dx, P dw, P db, P part, P coef, int M, int C, int nrb,
+                           int dt, int dtw, int acc, P s) {
+    pra_bn_bwd_parts(CV(g), CV(x), CV(w), CF(mean), CF(invstd), V(dx), V(dw), V(db),
+                     reinterpret_cast<const float*>(part), F(coef), M, C, nrb, dt, dtw, acc, S(s));
+    check_launch("bn_bwd_parts");
   });
   m.def("max_pool_fwd", [](P x, P y, P idx, int n, int h, int w, int c, int ho, int wo, int kh, int kw, int sh,
                            int sw, int ph, int pw, int dt, P s) {

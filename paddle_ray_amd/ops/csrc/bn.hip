@@ -156,9 +156,21 @@ __device__ __forceinline__ void merge_parts(const float* __restrict__ part, int 
                                             double& S2, double* red) {
   double a = 0.0, b = 0.0;
   if (c < C) {
-    for (int j = rl; j < nrb; j += 16) {
-      a += part[(size_t)j * C + c];
-      b += part[((size_t)nrb + j) * C + c];
+    // 16 loads in flight per lane (the conv-epilogue statistics arrive as up to ~1600 tile rows;
+    // one dependent load per row made the merge latency-bound); same summation order as a plain loop
+    const float* p1 = part + c;
+    const float* p2 = part + (size_t)nrb * C + c;
+    int j = rl;
+    for (; j + 16 * 7 < nrb; j += 16 * 8) {
+      float u[8], v[8];
+#pragma unroll
+      for (int t = 0; t < 8; ++t) { u[t] = p1[(size_t)(j + 16 * t) * C]; v[t] = p2[(size_t)(j + 16 * t) * C]; }
+#pragma unroll
+      for (int t = 0; t < 8; ++t) { a += u[t]; b += v[t]; }
+    }
+    for (; j < nrb; j += 16) {
+      a += p1[(size_t)j * C];
+      b += p2[(size_t)j * C];
     }
   }
   red[threadIdx.x] = a;
@@ -167,6 +179,37 @@ __device__ __forceinline__ void merge_parts(const float* __restrict__ part, int 
   S1 = 0.0; S2 = 0.0;
   if (rl == 0) {
     for (int j = 0; j < 16; ++j) { S1 += red[j * 64 + (threadIdx.x & 63)]; S2 += red[1024 + j * 64 + (threadIdx.x & 63)]; }
+  }
+}
+
+// Partial-row pre-merge for the statistics a convolution epilogue produced (one row per output
+// tile: up to ~6300 rows for the ResNet stem), so the finalize's single block per 64 channels
+// does not walk thousands of rows: [2][nrb][C] -> [2][ceil(nrb/64)][C], block (c64, r) sums rows
+// 64r .. 64r+63 (16 row lanes x 4 rows, fixed order: deterministic).
+__global__ void __launch_bounds__(1024) bn_premerge_k(const float* __restrict__ part, float* __restrict__ out,
+                                                      int nrb, int nrb2, int C) {
+  __shared__ float red[2][1024];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63), rl = threadIdx.x >> 6, r0 = blockIdx.y * 64;
+  float a = 0.f, b = 0.f;
+  if (c < C) {
+    float u[4], v[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int j = r0 + rl + 16 * t;
+      u[t] = j < nrb ? part[(size_t)j * C + c] : 0.f;
+      v[t] = j < nrb ? part[((size_t)nrb + j) * C + c] : 0.f;
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t) { a += u[t]; b += v[t]; }
+  }
+  red[0][threadIdx.x] = a;
+  red[1][threadIdx.x] = b;
+  __syncthreads();
+  if (rl == 0 && c < C) {
+    float sa = 0.f, sb = 0.f;
+    for (int j = 0; j < 16; ++j) { sa += red[0][j * 64 + threadIdx.x]; sb += red[1][j * 64 + threadIdx.x]; }
+    out[(size_t)blockIdx.y * C + c] = sa;
+    out[((size_t)nrb2 + blockIdx.y) * C + c] = sb;
   }
 }
 
@@ -415,6 +458,12 @@ void pra_bn_fwd_parts(const void* x, const void* z, const void* w, const void* b
   });
 }
 
+// out [2][ceil(nrb/64)][C] (see bn_premerge_k)
+void pra_bn_premerge(const float* part, float* out, int nrb, int C, hipStream_t s) {
+  const int nrb2 = (nrb + 63) / 64;
+  hipLaunchKernelGGL(bn_premerge_k, dim3((C + 63) / 64, nrb2), dim3(1024), 0, s, part, out, nrb, nrb2, C);
+}
+
 void pra_bn_fwd_infer(const void* x, const void* z, const void* w, const void* b, const float* rmean,
                       const float* rvar, void* y, float* coef, int M, int C, float eps, int relu, int dt, int dtw,
                       hipStream_t s) {
@@ -447,6 +496,22 @@ void pra_bn_bwd(const void* dy, const void* y, const uint8_t* mask, const void* 
     else
       hipLaunchKernelGGL((bn_bwd_apply_k<T, false>), dim3(g), dim3(kBnThreads), 0, s, (const T*)dy, nullptr, nullptr,
                          (const T*)x, coef, (T*)dx, (T*)dz, nvec, C);
+  });
+}
+
+// Backward from the reductions a convolution's dgrad epilogue already produced (gemm_core.h
+// kBnG): g is the ReLU-masked gradient, part [2][nrb][C] = per-tile sums of g and g * (x - mean).
+// Finalize + apply only; the reduction pass over (dy, x, mask) is gone.
+void pra_bn_bwd_parts(const void* g, const void* x, const void* w, const float* mean, const float* invstd, void* dx,
+                      void* dw, void* db, const float* part, float* coef, int M, int C, int nrb, int dt, int dtw,
+                      int acc, hipStream_t s) {
+  const uint32_t nvec = (uint32_t)((size_t)M * C / 8);
+  const unsigned gr = bn_apply_grid(nvec);
+  hipLaunchKernelGGL(bn_fin_bwd_k, dim3((C + 63) / 64), dim3(1024), 0, s, part, w, dtw, mean, invstd, dw, db, coef,
+                     nrb, M, C, acc);
+  PRA_DISPATCH_FLOAT(dt, T, {
+    hipLaunchKernelGGL((bn_bwd_apply_k<T, false>), dim3(gr), dim3(kBnThreads), 0, s, (const T*)g, nullptr, nullptr,
+                       (const T*)x, coef, (T*)dx, (T*)nullptr, nvec, C);
   });
 }
 }

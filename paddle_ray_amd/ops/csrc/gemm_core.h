@@ -58,8 +58,11 @@ template <> __device__ __forceinline__ uint32_t pack2<f16>(float a, float b) {
 // work: profiles/r4/fused_dgelu_epilogue.md measured that VALU serialised behind the K loop).
 enum Epi : int {
   kNone = 0, kGeluErf = 1, kGeluTanh = 2, kRelu = 3, kDGeluErf = 4, kDGeluTanh = 5,
-  kGeluErfD = 6, kGeluTanhD = 7, kMulZ = 8
+  kGeluErfD = 6, kGeluTanhD = 7, kMulZ = 8, kBnG = 9
 };
+// kBnG (implicit-GEMM conv dgrad feeding a BatchNorm+ReLU backward): C = acc masked by the ReLU
+// keep-bits (mbits, 1 bit per element), colsum = sum of that g, colsq = sum of g * (Z - cshift)
+// with Z the BN input and cshift its batch mean -- the BN backward's two reductions.
 // epilogues that read Z and scale the product by a per-element factor (the dgrad side)
 constexpr bool epi_scales(int E) { return E == kDGeluErf || E == kDGeluTanh || E == kMulZ; }
 // forward GELUs that store the derivative into Z
@@ -412,7 +415,8 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_lds_kernel(const uint16_t* __r
                                                           int M, int N, int K, int lda, int ldb, int ldc, int ldz,
                                                           int splits, float* __restrict__ ws, ConvGeom cg = {},
                                                           float* __restrict__ colsq = nullptr,
-                                                          const float* __restrict__ cshift = nullptr) {
+                                                          const float* __restrict__ cshift = nullptr,
+                                                          const uint8_t* __restrict__ mbits = nullptr) {
   constexpr int NT = CF::NT, TI = CF::TI, TJ = CF::TJ, NDA = CF::NDA, NDB = CF::NDB, WC = CF::WC;
   constexpr int BM = CF::BM, BN = CF::BN, IMGA = CF::IMGA, SLOT = CF::SLOT;
   constexpr int RW = TI * 16, CW = TJ * 16;  // rows / columns per wave
@@ -811,6 +815,23 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_lds_kernel(const uint16_t* __r
 #pragma unroll
     for (int e = 0; e < 8; ++e) ks[e] = cshift[n + e];
   }
+  // kBnG with few units per thread (the narrow conv tiles): every Z / keep-bit load of the whole
+  // epilogue is issued up front, so their latency overlaps the accumulator parking instead of
+  // being paid once per 128-row chunk
+  constexpr int NU = (BM / 128) * NQ;
+  constexpr bool ZPRE = E == kBnG && NU <= 8;
+  uint4 zp[ZPRE ? NU : 1];
+  uint32_t mp[ZPRE ? NU : 1];
+  if constexpr (ZPRE) {
+#pragma unroll
+    for (int q = 0; q < NU; ++q) {
+      const int m = m0 + (q / NQ) * 128 + urow + RSTEP * (q % NQ);
+      if (m < M && ncol_ok) {
+        zp[q] = *reinterpret_cast<const uint4*>(Z + (int64_t)m * ldz + n);
+        mp[q] = mbits[((int64_t)m * N + n) >> 3];
+      }
+    }
+  }
 #pragma unroll
   for (int h = 0; h < BM / 128; ++h) {
     __builtin_amdgcn_s_waitcnt(0xC07F);
@@ -831,6 +852,7 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_lds_kernel(const uint16_t* __r
     for (int bq = 0; bq < NQ; bq += QB) {
       f32x4 lo[QB], hi[QB];
       uint4 gz[QB];
+      uint32_t mb[QB];
       bool ok[QB];
       int64_t moff[QB];
 #pragma unroll
@@ -840,8 +862,12 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_lds_kernel(const uint16_t* __r
         moff[u] = (int64_t)(ok[u] ? m : 0);
         lo[u] = *reinterpret_cast<const f32x4*>(img + rr * PITCH + ucol);
         hi[u] = *reinterpret_cast<const f32x4*>(img + rr * PITCH + ucol + 4);
-        if (epi_scales(E)) {
+        if constexpr (ZPRE) {
+          gz[u] = zp[h * NQ + bq + u];
+          mb[u] = mp[h * NQ + bq + u];
+        } else if (epi_scales(E) || E == kBnG) {
           if (ok[u]) gz[u] = *reinterpret_cast<const uint4*>(Z + moff[u] * ldz + n);
+          if (E == kBnG && ok[u]) mb[u] = mbits[(moff[u] * N + n) >> 3];
         } else if (BETA) {
           if (ok[u]) gz[u] = *reinterpret_cast<const uint4*>(C + moff[u] * ldc + n);
         }
@@ -869,6 +895,9 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_lds_kernel(const uint16_t* __r
           o.x = pack2<T>(d[0], d[1]); o.y = pack2<T>(d[2], d[3]);
           o.z = pack2<T>(d[4], d[5]); o.w = pack2<T>(d[6], d[7]);
           *reinterpret_cast<uint4*>(Z + m * ldz + n) = o;
+        } else if constexpr (E == kBnG) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = (mb[u] >> e) & 1u ? v[e] : 0.f;
         } else if (E != kNone) {
           if (Z) {
             uint4 o;
@@ -879,7 +908,7 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_lds_kernel(const uint16_t* __r
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] = act<E>(v[e]);
         }
-        if (BETA && !epi_scales(E)) {
+        if (BETA && !epi_scales(E) && E != kBnG) {
           const uint32_t w4[4] = {gz[u].x, gz[u].y, gz[u].z, gz[u].w};
 #pragma unroll
           for (int e = 0; e < 4; ++e) { v[2 * e] += to_f<T>(w4[e] & 0xffff); v[2 * e + 1] += to_f<T>(w4[e] >> 16); }
@@ -891,12 +920,24 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_lds_kernel(const uint16_t* __r
         if (colsum) {
           // the bias gradient sums the ROUNDED output (what a separate reduction would read)
           const uint32_t w4[4] = {o.x, o.y, o.z, o.w};
+          if constexpr (E == kBnG) {
+            const uint32_t z4[4] = {gz[u].x, gz[u].y, gz[u].z, gz[u].w};
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const float d0 = to_f<T>(w4[e] & 0xffff) - ks[2 * e], d1 = to_f<T>(w4[e] >> 16) - ks[2 * e + 1];
-            cs[2 * e] += d0;
-            cs[2 * e + 1] += d1;
-            if (colsq) { cq[2 * e] += d0 * d0; cq[2 * e + 1] += d1 * d1; }
+            for (int e = 0; e < 4; ++e) {
+              const float g0 = to_f<T>(w4[e] & 0xffff), g1 = to_f<T>(w4[e] >> 16);
+              cs[2 * e] += g0;
+              cs[2 * e + 1] += g1;
+              cq[2 * e] += g0 * (to_f<T>(z4[e] & 0xffff) - ks[2 * e]);
+              cq[2 * e + 1] += g1 * (to_f<T>(z4[e] >> 16) - ks[2 * e + 1]);
+            }
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float d0 = to_f<T>(w4[e] & 0xffff) - ks[2 * e], d1 = to_f<T>(w4[e] >> 16) - ks[2 * e + 1];
+              cs[2 * e] += d0;
+              cs[2 * e + 1] += d1;
+              if (colsq) { cq[2 * e] += d0 * d0; cq[2 * e + 1] += d1 * d1; }
+            }
           }
         }
       }

@@ -197,25 +197,29 @@ int launch_t(int layout, const void* A, const void* B, const void* bias, void* C
 
 template <typename T, typename CF, int E>
 void launch_conv_cfg(const void* xpad, const void* W, const void* bias, void* Y, int M, int N, int K,
-                     const ConvGeom& cg, int splits, float* ws, float* part, const float* kshift, hipStream_t s) {
+                     const ConvGeom& cg, int splits, float* ws, float* part, const float* kshift, hipStream_t s,
+                     const void* bnx = nullptr, const uint8_t* bnmask = nullptr) {
   const int tiles_m = (M + CF::BM - 1) / CF::BM;
   const int tiles = tiles_m * ((N + CF::BN - 1) / CF::BN);
   auto px = static_cast<const uint16_t*>(xpad);
   auto pw = static_cast<const uint16_t*>(W);
   auto pb = static_cast<const uint16_t*>(bias);
   auto py = static_cast<uint16_t*>(Y);
-  if (splits > 1) {  // few output tiles (late ResNet stages): split the K = KH*KW*C loop
-    gemm_lds_kernel<T, CF, true, true, kNone, false, true, true><<<tiles * splits, CF::NT, 0, s>>>(
-        px, pw, nullptr, nullptr, nullptr, nullptr, M, N, K, 0, K, N, N, splits, ws, cg);
-    const int64_t quads = (int64_t)M * N / 4;
-    splitk_reduce_k<T, E, false><<<(int)((quads + 255) / 256), 256, 0, s>>>(ws, splits, pb, py, nullptr, M, N, N, N);
-    return;
+  if constexpr (E != kBnG) {
+    if (splits > 1) {  // few output tiles (late ResNet stages): split the K = KH*KW*C loop
+      gemm_lds_kernel<T, CF, true, true, kNone, false, true, true><<<tiles * splits, CF::NT, 0, s>>>(
+          px, pw, nullptr, nullptr, nullptr, nullptr, M, N, K, 0, K, N, N, splits, ws, cg);
+      const int64_t quads = (int64_t)M * N / 4;
+      splitk_reduce_k<T, E, false><<<(int)((quads + 255) / 256), 256, 0, s>>>(ws, splits, pb, py, nullptr, M, N, N, N);
+      return;
+    }
   }
   // part (optional): per-tile-row BatchNorm statistics of the output, [2][tiles_m][N] = sums of
-  // (y - kshift) and (y - kshift)^2 over each tile's rows (kshift: the running mean)
+  // (y - kshift) and (y - kshift)^2 over each tile's rows (kshift: the running mean).
+  // kBnG: Y = dgrad masked by bnmask, part = sums of Y and Y * (bnx - kshift) (kshift: BN batch mean)
   gemm_lds_kernel<T, CF, true, true, E, false, false, true><<<tiles, CF::NT, 0, s>>>(
-      px, pw, pb, py, nullptr, part, M, N, K, 0, K, N, N, 1, nullptr, cg,
-      part ? part + (int64_t)tiles_m * N : nullptr, kshift);
+      px, pw, pb, py, const_cast<uint16_t*>(static_cast<const uint16_t*>(bnx)), part, M, N, K, 0, K, N, N, 1, nullptr,
+      cg, part ? part + (int64_t)tiles_m * N : nullptr, kshift, bnmask);
 }
 
 inline int conv_wgrad_rows(int Cout) { return Cout <= 128 ? WG128::BM : W8::BM; }
@@ -252,10 +256,11 @@ inline int conv_tile_rows(int N) { return N <= 64 ? C64::BM : (N <= 128 ? C128::
 
 template <typename T, int E>
 int launch_conv(const void* xpad, const void* W, const void* bias, void* Y, int M, int N, int K, const ConvGeom& cg,
-                int splits, float* ws, float* part, const float* kshift, hipStream_t s) {
-  if (N <= 64) launch_conv_cfg<T, C64, E>(xpad, W, bias, Y, M, N, K, cg, 1, nullptr, part, kshift, s);
-  else if (N <= 128) launch_conv_cfg<T, C128, E>(xpad, W, bias, Y, M, N, K, cg, 1, nullptr, part, kshift, s);
-  else launch_conv_cfg<T, W8, E>(xpad, W, bias, Y, M, N, K, cg, part ? 1 : splits, ws, part, kshift, s);
+                int splits, float* ws, float* part, const float* kshift, hipStream_t s, const void* bnx = nullptr,
+                const uint8_t* bnmask = nullptr) {
+  if (N <= 64) launch_conv_cfg<T, C64, E>(xpad, W, bias, Y, M, N, K, cg, 1, nullptr, part, kshift, s, bnx, bnmask);
+  else if (N <= 128) launch_conv_cfg<T, C128, E>(xpad, W, bias, Y, M, N, K, cg, 1, nullptr, part, kshift, s, bnx, bnmask);
+  else launch_conv_cfg<T, W8, E>(xpad, W, bias, Y, M, N, K, cg, part ? 1 : splits, ws, part, kshift, s, bnx, bnmask);
   return 0;
 }
 
@@ -275,10 +280,15 @@ extern "C" int pra_conv_lds_stat_rows(int M, int Cout) { return (M + pra::conv_t
 
 // pp (0 = C): the input's pixel pitch when it is narrower than C (see ConvGeom::PP): then
 // KW == 1, P == 0, a tap row is C / pp adjacent pixels and Wo = (Wd - C / pp) / S + 1.
+// bnx / bnmask (optional, a dgrad feeding BatchNorm(+ReLU)'s backward): Y = the product masked by
+// the ReLU keep-bits bnmask ([M*Cout/8] bytes), part = per-tile sums of Y and of Y * (bnx - kshift)
+// with bnx the BN input [M][Cout] and kshift its batch mean; needs part, kshift, no relu/bias/split.
 extern "C" int pra_conv_lds(const void* x, const void* W, const void* bias, void* Y, int Nimg, int H, int Wd,
                             int C, int Cout, int KH, int KW, int S, int P, int relu, int dtype, int splits, float* ws,
-                            float* part, const float* kshift, int pp, hipStream_t s) {
+                            float* part, const float* kshift, int pp, hipStream_t s, const void* bnx = nullptr,
+                            const uint8_t* bnmask = nullptr) {
   if (pp <= 0) pp = C;
+  if (bnx && (!bnmask || !part || !kshift || relu || bias || splits > 1)) return -1;
   if (C % 64 || Cout % 8 || KH <= 0 || KW <= 0 || S <= 0 || P < 0 || H <= 0 || Wd <= 0) return -1;
   if (pp != C && (pp % 8 || C % pp || KW != 1 || P != 0)) return -1;
   if (H >= 32768 || Wd >= 32768 || (long long)Nimg * H * Wd * pp * 2 >= (1ll << 31)) return -1;
@@ -291,6 +301,13 @@ extern "C" int pra_conv_lds(const void* x, const void* W, const void* bias, void
   const int M = (int)Mll, K = KH * KW * C;
   if (splits > 1 && (Cout <= 128 || !ws)) return -1;
   pra::ConvGeom cg{Ho, Wo, H, Wd, C, KW, S, P, pp};
+  if (bnx) {
+    if (dtype == pra::kBF16)
+      return pra::launch_conv<pra::bf16, pra::kBnG>(x, W, nullptr, Y, M, Cout, K, cg, 1, nullptr, part, kshift, s, bnx, bnmask);
+    if (dtype == pra::kF16)
+      return pra::launch_conv<pra::f16, pra::kBnG>(x, W, nullptr, Y, M, Cout, K, cg, 1, nullptr, part, kshift, s, bnx, bnmask);
+    return -1;
+  }
   if (dtype == pra::kBF16) return relu ? pra::launch_conv<pra::bf16, pra::kRelu>(x, W, bias, Y, M, Cout, K, cg, splits, ws, part, kshift, s)
                                   : pra::launch_conv<pra::bf16, pra::kNone>(x, W, bias, Y, M, Cout, K, cg, splits, ws, part, kshift, s);
   if (dtype == pra::kF16) return relu ? pra::launch_conv<pra::f16, pra::kRelu>(x, W, bias, Y, M, Cout, K, cg, splits, ws, part, kshift, s)

@@ -136,7 +136,34 @@ extern "C" int pra_space_to_depth2(const void* x, void* y, int N, int H, int W, 
 }
 
 namespace pra {
+// Global average pooling backward, channels-last: dx[n][p][c] = dy[n][c] * scale for all HW
+// pixels p (a broadcast write; torch's expand + copy runs a non-vectorised strided kernel)
+template <typename T>
+__global__ void __launch_bounds__(256) gap_bwd_k(const T* __restrict__ dy, T* __restrict__ dx, int HW, int CV,
+                                                 float scale, int64_t nvec) {
+  for (int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x; v < nvec; v += (int64_t)gridDim.x * 256) {
+    const int cv = (int)(v % CV);
+    const int64_t n = v / ((int64_t)HW * CV);
+    float g[8];
+    load8<T>(dy + (n * CV + cv) * 8, g);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) g[e] *= scale;
+    store8<T>(dx + v * 8, g);
+  }
+}
 }  // namespace pra
+
+extern "C" int pra_gap_bwd(const void* dy, void* dx, int N, int HW, int C, int dt, hipStream_t s) {
+  if (N <= 0 || HW <= 0 || C % 8) return -1;
+  const int64_t nvec = (int64_t)N * HW * (C / 8);
+  const int64_t want = (nvec + 255) / 256;
+  const unsigned blocks = (unsigned)(want < 4096 ? want : 4096);
+  const float scale = 1.f / (float)HW;
+  PRA_DISPATCH_FLOAT(dt, T, {
+    hipLaunchKernelGGL(pra::gap_bwd_k<T>, dim3(blocks), dim3(256), 0, s, (const T*)dy, (T*)dx, HW, C / 8, scale, nvec);
+  });
+  return 0;
+}
 
 using pra::PoolGeom;
 

@@ -1496,10 +1496,10 @@ class GradJoin:
     initial buffer) and only the LAST contributor to run backward returns the total; the
     others return None. Contributors register in forward, so the count is exact."""
 
-    __slots__ = ('x', 'n', 'left', 'pending')
+    __slots__ = ('x', 'n', 'left', 'pending', 'deferred')
 
     def __init__(self, x):
-        self.x, self.n, self.left, self.pending = x, 0, None, None
+        self.x, self.n, self.left, self.pending, self.deferred = x, 0, None, None, []
 
     def _finish(self):
         if self.left is None:
@@ -1507,6 +1507,16 @@ class GradJoin:
         self.left -= 1
         if self.left == 0:
             out, self.pending = self.pending, None
+            # strided contributions that arrived before any full-size buffer existed are added
+            # into their sampled positions of the final buffer (no zero-filled full tensor
+            # unless every contributor was strided)
+            for dx2, xshape, sh, sw in self.deferred:
+                if out is None:
+                    out = torch.zeros(xshape, dtype=dx2.dtype, device=dx2.device)
+                    out[:, ::sh, ::sw, :] = dx2
+                else:
+                    out[:, ::sh, ::sw, :] += dx2
+            self.deferred = []
             self.left = None
             return out
         return None
@@ -1520,8 +1530,7 @@ class GradJoin:
 
     def add_strided(self, dx2, xshape, sh, sw):
         if self.pending is None:
-            self.pending = torch.zeros(xshape, dtype=dx2.dtype, device=dx2.device)
-            self.pending[:, ::sh, ::sw, :] = dx2
+            self.deferred.append((dx2, xshape, sh, sw))
         else:
             self.pending[:, ::sh, ::sw, :] += dx2
         return self._finish()
@@ -1564,10 +1573,61 @@ def _join_for(t):
     return None
 
 
+# BatchNorm(+ReLU) -> convolution gradient handoff. The BN backward's two reductions (sum of g and
+# of g * (x - mean), g = the ReLU-masked incoming gradient) are produced by the epilogue of the
+# convolution dgrad that computes that gradient (gemm_core.h kBnG), so the BN backward is the
+# finalize + apply kernels only. BatchNormActFn tags its output with a _BnHandoff; a consumer
+# conv whose backward runs on the implicit-GEMM kernel writes g and the partial sums into it; the
+# BN backward uses them only when the gradient it receives IS that g, unmodified (same storage and
+# version: a second consumer's gradient summed in by autograd lands in a new buffer or bumps the
+# version), and otherwise runs its own reduction (masking g again is idempotent).
+_BN_DGRAD_FUSE = __import__('os').environ.get('PRA_BN_DGRAD_FUSE', '1') == '1'
+_BN_DGRAD_SPLIT = __import__('os').environ.get('PRA_BN_DGRAD_SPLIT', '0') == '1'
+
+
+class _BnHandoff:
+    __slots__ = ('x2', 'mask', 'mean', 'g', 'gver', 'part', 'used')
+
+    def __init__(self, x2, mask, mean):
+        self.x2, self.mask, self.mean = x2, mask, mean
+        self.g = self.gver = self.part = None
+        self.used = 0
+
+    def take(self, dy2):
+        """The epilogue partial sums if dy2 is the produced g, else None (either way cleared)."""
+        g, part, ver = self.g, self.part, self.gver
+        self.g = self.part = self.gver = None
+        if (part is None or dy2.data_ptr() != g.data_ptr() or dy2._version != ver
+                or dy2.shape != self.x2.shape):
+            return None
+        self.used += 1
+        return part
+
+
+def _bn_handoff(x):
+    rec = getattr(x, '_pra_bn', None) if _BN_DGRAD_FUSE else None
+    return rec if isinstance(rec, _BnHandoff) else None
+
+
+def _bn_dgrad_ok(rec, m, cout_dgrad, k):
+    """The fused dgrad runs without split-K; shapes the split would have served keep the plain
+    dgrad unless PRA_BN_DGRAD_SPLIT=1."""
+    return (rec is not None and rec.x2.shape == (m, cout_dgrad) and rec.x2.is_contiguous()
+            and (_BN_DGRAD_SPLIT or _native.lib().conv_lds_splits(m, cout_dgrad, k) == 1))
+
+
+def _bn_dgrad(rec, dy4, wk, kh, kw, pad):
+    """dgrad on the implicit-GEMM kernel with the kBnG epilogue; stores g + partials in rec."""
+    g, part = _conv_lds(dy4, wk, None, kh, kw, 1, pad, bn=(rec.x2, rec.mask, rec.mean))
+    rec.g, rec.part, rec.gver = g, part, g._version
+    return g
+
+
 class Conv1x1Fn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, bias, sh, sw, join=None):
         ctx.join = join
+        ctx.bn = _bn_handoff(x) if (join is None and (sh, sw) == (1, 1) and bias is None) else None
         xs = x if (sh, sw) == (1, 1) else x[:, ::sh, ::sw, :]
         xs = xs.contiguous()
         n, h, wd, cin = xs.shape
@@ -1588,7 +1648,12 @@ class Conv1x1Fn(torch.autograd.Function):
             dy2 = dy2.contiguous()
         dy2 = _like(dy2, x2.dtype)
         dx = dw = db = None
-        if ctx.needs_input_grad[0]:
+        rec = getattr(ctx, 'bn', None)
+        m, cout = dy2.shape
+        if (ctx.needs_input_grad[0] and rec is not None and cout % 64 == 0 and w2.shape[1] % 8 == 0
+                and _bn_dgrad_ok(rec, m, w2.shape[1], cout)):
+            dx = _bn_dgrad(rec, dy2.view(*xsshape[:3], cout), w2.t().contiguous(), 1, 1, 0).view(xshape)
+        elif ctx.needs_input_grad[0]:
             j = ctx.join
             if j is not None and (sh, sw) == (1, 1):
                 dx = j.add_gemm(dy2, w2, xshape)
@@ -1634,14 +1699,18 @@ class Conv1x1StatsFn(torch.autograd.Function):
         cout = w.shape[0]
         w2 = w.reshape(cout, cin)
         y, part = _conv_lds(xs, w2, None, 1, 1, 1, 0, stats_shift=shift)
+        ctx.bn = _bn_handoff(x) if (join is None and (sh, sw) == (1, 1)) else None
         ctx.save_for_backward(xs.view(-1, cin), w2)
         ctx.w = w
         ctx.meta = (tuple(x.shape), tuple(xs.shape), tuple(w.shape), sh, sw, False)
         ctx.mark_non_differentiable(part)
+        ctx.set_materialize_grads(False)   # (no zero-filled [2, rows, C] gradient for part)
         return y, part
 
     @staticmethod
     def backward(ctx, dy, dpart):
+        if dy is None:
+            return None, None, None, None, None, None
         dx, dw, _, _, _, _ = Conv1x1Fn.backward(ctx, dy)
         return dx, dw, None, None, None, None
 
@@ -1687,11 +1756,14 @@ def conv_kxk_supported(x, w, stride, padding):
             and x.numel() * 2 < 2 ** 31 and max(x.shape[1], x.shape[2]) < 32768)
 
 
-def _conv_lds(x, wk, bias, kh, kw, stride, pad, relu=False, stats_shift=None, cv=None):
+def _conv_lds(x, wk, bias, kh, kw, stride, pad, relu=False, stats_shift=None, cv=None, bn=None):
     """y[N,Ho,Wo,Cout] = conv(x NHWC, wk [Cout, kh*kw*C] (OHWI)) via the implicit-GEMM kernel
     (zero padding applied by the kernel's DMA range check, the input is read in place).
     stats_shift (fp32 [Cout], e.g. the BN running mean): the epilogue also returns the per-tile
-    BatchNorm partial sums part [2, rows, Cout] of (y - shift) and (y - shift)^2."""
+    BatchNorm partial sums part [2, rows, Cout] of (y - shift) and (y - shift)^2.
+    bn = (x2, mask, mean) of a BatchNorm+ReLU whose output this conv's dgrad is the gradient of:
+    y = the product masked by the ReLU keep-bits, part = per-tile sums of y and y * (x2 - mean)
+    (gemm_core.h kBnG), returned as (y, part)."""
     n, h, wd, c = x.shape
     cout = wk.shape[0]
     x = x.contiguous()
@@ -1708,6 +1780,11 @@ def _conv_lds(x, wk, bias, kh, kw, stride, pad, relu=False, stats_shift=None, cv
     L = _native.lib()
     m = n * ho * wo
     part = None
+    bnx = bnm = 0
+    if bn is not None:
+        bx2, bmask, stats_shift = bn
+        assert bx2.shape == (n * ho * wo, cout) and bmask.numel() * 8 == bx2.numel() and bias is None
+        bnx, bnm = bx2.data_ptr(), bmask.data_ptr()
     if stats_shift is not None:
         splits = 1
         part = torch.empty((2, L.conv_lds_stat_rows(m, cout), cout), device=x.device, dtype=torch.float32)
@@ -1715,7 +1792,8 @@ def _conv_lds(x, wk, bias, kh, kw, stride, pad, relu=False, stats_shift=None, cv
         splits = L.conv_lds_splits(m, cout, kh * kw * c)
     ws = torch.empty((splits, m, cout), device=x.device, dtype=torch.float32) if splits > 1 else None
     L.conv_lds(x.data_ptr(), wk.data_ptr(), _ptr(bias), y.data_ptr(), n, h, wd, c, cout, kh, kw,
-               stride, pad, int(relu), _dt(x), splits, _ptr(ws), _ptr(part), _ptr(stats_shift), pp, _stream())
+               stride, pad, int(relu), _dt(x), splits, _ptr(ws), _ptr(part), _ptr(stats_shift), pp, _stream(),
+               bnx, bnm)
     return y if stats_shift is None else (y, part)
 
 
@@ -1767,6 +1845,7 @@ class ConvKxKFn(torch.autograd.Function):
         y = _conv_lds(x, wk, bias, kh, kw, stride, pad)
         ctx.save_for_backward(x, w)
         ctx.meta = (stride, pad, bias is not None)
+        ctx.bn = _bn_handoff(x) if stride == 1 else None
         return y
 
     @staticmethod
@@ -1780,7 +1859,11 @@ class ConvKxKFn(torch.autograd.Function):
         dx = dw = db = None
         if ours_dx:
             wf = w.flip(2, 3).permute(1, 2, 3, 0).reshape(cin, kh * kw * cout).contiguous()
-            dx = _conv_lds(dy, wf, None, kh, kw, 1, kh - 1 - pad)
+            rec = getattr(ctx, 'bn', None)
+            if _bn_dgrad_ok(rec, x.shape[0] * x.shape[1] * x.shape[2], cin, kh * kw * cout):
+                dx = _bn_dgrad(rec, dy, wf, kh, kw, kh - 1 - pad)
+            else:
+                dx = _conv_lds(dy, wf, None, kh, kw, 1, kh - 1 - pad)
         need_lib_dx = ctx.needs_input_grad[0] and not ours_dx
         ours_dw = ctx.needs_input_grad[1] and _conv_wgrad_ok(x, dy, cout)
         if ours_dw:
@@ -1812,11 +1895,15 @@ class ConvKxKStatsFn(ConvKxKFn):
         y, part = _conv_lds(x, wk, bias, kh, kw, stride, pad, stats_shift=shift)
         ctx.save_for_backward(x, w)
         ctx.meta = (stride, pad, bias is not None)
+        ctx.bn = _bn_handoff(x) if stride == 1 else None
         ctx.mark_non_differentiable(part)
+        ctx.set_materialize_grads(False)   # (no zero-filled [2, rows, C] gradient for part)
         return y, part
 
     @staticmethod
     def backward(ctx, dy, dpart):
+        if dy is None:
+            return (None,) * 6
         return ConvKxKFn.backward(ctx, dy) + (None,)
 
 
@@ -1895,10 +1982,13 @@ class StemConvFn(torch.autograd.Function):
             return r, None
         y, part = r
         ctx.mark_non_differentiable(part)
+        ctx.set_materialize_grads(False)   # (no zero-filled [2, rows, C] gradient for part)
         return y, part
 
     @staticmethod
     def backward(ctx, dy, dpart):
+        if dy is None:
+            return None, None, None, None
         xs, idx, x, w = ctx.saved_tensors
         kt, wshape, pad = ctx.meta
         dw = None
@@ -2504,11 +2594,26 @@ def _bn_fwd_hip(x2, z2, w, b, rmean, rvar, training, momentum, eps, relu):
     return y, mean, torch.rsqrt(rvar.float() + eps), None
 
 
+_BN_PREMERGE_ROWS = 256
+
+
+def _bn_premerge(part):
+    """[2, rows, C] conv-epilogue partials -> [2, ceil(rows/64), C] when there are many rows
+    (the finalize kernel walks the rows with one block per 64 channels)."""
+    rows, C = part.shape[1], part.shape[2]
+    if rows <= _BN_PREMERGE_ROWS:
+        return part
+    out = torch.empty((2, (rows + 63) // 64, C), device=part.device, dtype=torch.float32)
+    _native.lib().bn_premerge(part.data_ptr(), out.data_ptr(), rows, C, _stream())
+    return out
+
+
 def _bn_fwd_parts_hip(x2, z2, w, b, rmean, rvar, momentum, eps, relu, part, kshift):
     """Training BN forward from the per-tile partial sums a convolution epilogue produced
     (part [2, rows, C] around kshift): finalize + apply kernels only."""
     _check_dtypes('batch_norm', (x2, z2), (w, b))
     L = _native.lib()
+    part = _bn_premerge(part)
     M, C = x2.shape
     y = torch.empty_like(x2)
     stat = torch.empty((4, C), device=x2.device, dtype=torch.float32)  # mean | invstd | scale | shift
@@ -2552,6 +2657,30 @@ def _bn_bwd_hip(dy, y, mask, x2, w, mean, invstd, relu, need_dz, acc=None):
     return dx, dz, gw, gb
 
 
+def _bn_bwd_parts_hip(g, x2, w, mean, invstd, part, acc=None):
+    """BN backward from the masked gradient g and its partial sums part [2, rows, C] (sum g,
+    sum g * (x - mean)): returns (dx, dscale, dshift); with acc = (w.grad, b.grad) those are
+    accumulated in place and (dx, None, None) returned."""
+    L = _native.lib()
+    R._STATS[('batch_norm_bwd', 'hip_parts')] += 1
+    part = _bn_premerge(part)
+    M, C = x2.shape
+    dx = torch.empty_like(x2)
+    pdt = w.dtype if w is not None else torch.float32
+    if acc is not None:
+        gw, gb = acc
+    else:
+        dwb = torch.empty((2, C), device=x2.device, dtype=pdt)
+        gw, gb = dwb[0], dwb[1]
+    coef = torch.empty((3, C), device=x2.device, dtype=torch.float32)
+    L.bn_bwd_parts(g.data_ptr(), x2.data_ptr(), _ptr(w), mean.data_ptr(), invstd.data_ptr(), dx.data_ptr(),
+                   gw.data_ptr(), gb.data_ptr(), part.data_ptr(), coef.data_ptr(), M, C, part.shape[1], _dt(x2),
+                   _DT[pdt], int(acc is not None), _stream())
+    if acc is not None:
+        return dx, None, None
+    return dx, gw, gb
+
+
 class BatchNormActFn(torch.autograd.Function):
     """y = act(BN(x) + z) over channels-last x[..., C]; running stats updated in place."""
 
@@ -2575,7 +2704,12 @@ class BatchNormActFn(torch.autograd.Function):
         ctx.save_for_backward(x2, y if (relu and mask is None) else None, mask, w, mean, invstd)
         ctx.relu, ctx.shp, ctx.has_z = relu, shp, z is not None
         ctx.has_b, ctx.training, ctx.b = b is not None, training, b
-        return y.view(shp)
+        out = y.view(shp)
+        ctx.rec = None
+        if (_BN_DGRAD_FUSE and training and relu and z is None and mask is not None and x2.is_cuda
+                and mean.dtype == torch.float32 and x2.dtype in _HALF):
+            ctx.rec = out._pra_bn = _BnHandoff(x2, mask, mean)
+        return out
 
     @staticmethod
     def backward(ctx, dy):
@@ -2600,6 +2734,14 @@ class BatchNormActFn(torch.autograd.Function):
                 and ctx.needs_input_grad[3] and w.is_leaf and b.is_leaf and _acc_grad_ok(w.grad, w, w.dtype)
                 and _acc_grad_ok(b.grad, b, w.dtype) and R.select_backend(x2, 'batch_norm_bwd') == 'hip'):
             acc = (w.grad, b.grad)  # scale/shift grads accumulated in the finalize kernel
+        part = ctx.rec.take(dy2) if ctx.rec is not None else None
+        if part is not None:
+            # dy2 is the ReLU-masked gradient and part its reductions (the consumer conv's dgrad
+            # epilogue): finalize + apply only
+            dx, dw, db = _bn_bwd_parts_hip(dy2, x2, w, mean, invstd, part, acc)
+            return (dx.view(ctx.shp), None, dw if (w is not None and ctx.needs_input_grad[2]) else None,
+                    db if (ctx.has_b and ctx.needs_input_grad[3]) else None,
+                    None, None, None, None, None, None, None, None)
         if acc is not None:
             dx, dz, dw, db = _bn_bwd_hip(dy2, y, mask, x2, w, mean, invstd, ctx.relu,
                                          ctx.has_z and ctx.needs_input_grad[1], acc=acc)
@@ -2628,6 +2770,29 @@ def batch_norm_act(x, z, w, b, rmean, rvar, training, momentum=0.9, eps=1e-5, re
 # the winning tap per output element as one byte; the backward gathers (no atomics, no
 # zero-fill, no int64 index tensor)
 # =============================================================================
+class GlobalAvgPoolNHWCFn(torch.autograd.Function):
+    """Global average pooling over H, W of a channels-last tensor -> [N, 1, 1, C]; the backward
+    is one broadcast-write kernel (pool.hip gap_bwd_k). Parity: phi pool2d with adaptive=True,
+    output 1x1 (paddle/phi/kernels/funcs/pooling.cu)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        ctx.shp = tuple(x.shape)
+        return x.mean((1, 2), keepdim=True)
+
+    @staticmethod
+    def backward(ctx, dy):
+        n, h, w, c = ctx.shp
+        dy = dy.contiguous()
+        dx = torch.empty(ctx.shp, device=dy.device, dtype=dy.dtype)
+        _native.lib().gap_bwd(dy.data_ptr(), dx.data_ptr(), n, h * w, c, _dt(dy), _stream())
+        return dx
+
+
+def global_avg_pool_nhwc_supported(x):
+    return x.is_cuda and x.dim() == 4 and x.dtype in _FLOATS and x.shape[3] % 8 == 0 and x.is_contiguous()
+
+
 def max_pool_nhwc_supported(x, k, s, p):
     return (x.is_cuda and x.dim() == 4 and x.dtype in _FLOATS and x.shape[3] % 8 == 0
             and k[0] * k[1] <= 255 and p[0] < k[0] and p[1] < k[1] and min(s) >= 1 and min(p) >= 0)
