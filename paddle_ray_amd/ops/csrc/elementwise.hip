@@ -4,8 +4,6 @@
 //   multi-tensor Momentum, sum-of-squares (global-norm clipping), attention
 //   backward preprocess delta = rowsum(dO * O).
 #include "common.h"
-#include <stdlib.h>
-#include <type_traits>
 
 namespace pra {
 
@@ -231,69 +229,8 @@ __device__ __forceinline__ void adamw_vec4(float* __restrict__ master, const voi
   }
 }
 
-// 8 elements per lane per step: every load of the step (one 16-B bf16x8 gradient, two 16-B
-// vectors each of m, v, master) is issued before any math, and the streamed-once results are
-// written with nontemporal stores (no reuse: keep them from displacing L2 lines).
-typedef float f32x4e __attribute__((ext_vector_type(4)));
-typedef uint32_t u32x4e __attribute__((ext_vector_type(4)));
-typedef uint32_t u32x2e __attribute__((ext_vector_type(2)));
-template <typename V>
-__device__ __forceinline__ V ld_nt(const V* p, std::true_type) { return __builtin_nontemporal_load(p); }
-template <typename V>
-__device__ __forceinline__ V ld_nt(const V* p, std::false_type) { return *p; }
-template <typename V>
-__device__ __forceinline__ void st_nt(V v, V* p, std::true_type) { __builtin_nontemporal_store(v, p); }
-template <typename V>
-__device__ __forceinline__ void st_nt(V v, V* p, std::false_type) { *p = v; }
-template <bool LOWP, bool NTL, bool NTS>
-__device__ __forceinline__ void adamw_vec8(float* __restrict__ master, const uint16_t* __restrict__ grad,
-                                           float* __restrict__ m, float* __restrict__ v, uint16_t* __restrict__ lowp,
-                                           int64_t start, int64_t end, float b1, float b2, float eps, float decay,
-                                           float step, float rbc2, float gscale) {
-  for (int64_t i = start + 8 * threadIdx.x; i + 7 < end; i += 8 * blockDim.x) {
-    const std::integral_constant<bool, NTL> L{};
-    const std::integral_constant<bool, NTS> S{};
-    const u32x4e gu = ld_nt(reinterpret_cast<const u32x4e*>(grad + i), L);
-    f32x4e mv[2], vv[2], pv[2];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      mv[h] = ld_nt(reinterpret_cast<const f32x4e*>(m + i + 4 * h), L);
-      vv[h] = ld_nt(reinterpret_cast<const f32x4e*>(v + i + 4 * h), L);
-      pv[h] = ld_nt(reinterpret_cast<const f32x4e*>(master + i + 4 * h), L);
-    }
-    float g[8];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      g[2 * k] = __uint_as_float(gu[k] << 16) * gscale;
-      g[2 * k + 1] = __uint_as_float(gu[k] & 0xffff0000u) * gscale;
-    }
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const int h = k >> 2, e = k & 3;
-      const float mm = b1 * mv[h][e] + (1.f - b1) * g[k];
-      const float vq = b2 * vv[h][e] + (1.f - b2) * g[k] * g[k];
-      mv[h][e] = mm;
-      vv[h][e] = vq;
-      pv[h][e] = pv[h][e] * decay - step * mm / (sqrtf(vq * rbc2) + eps);
-    }
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      st_nt(mv[h], reinterpret_cast<f32x4e*>(m + i + 4 * h), S);
-      st_nt(vv[h], reinterpret_cast<f32x4e*>(v + i + 4 * h), S);
-      st_nt(pv[h], reinterpret_cast<f32x4e*>(master + i + 4 * h), S);
-    }
-    if (LOWP) {
-      const u32x4e o = {pack_bf2(pv[0][0], pv[0][1]), pack_bf2(pv[0][2], pv[0][3]), pack_bf2(pv[1][0], pv[1][1]),
-                        pack_bf2(pv[1][2], pv[1][3])};
-      st_nt(o, reinterpret_cast<u32x4e*>(lowp + i), S);
-    }
-  }
-}
-
 // gscale_ptr (device, nullable): global-norm clip coefficient read in-kernel, so the clip
-// needs no separate pass over the gradients. V8: the 8-wide nontemporal body for bf16 grads.
-// V8: 0 = the 4-wide body, 1 = 8-wide, 2 = 8-wide + nontemporal stores, 3 = 8-wide nontemporal
-template <int V8>
+// needs no separate pass over the gradients.
 __global__ void __launch_bounds__(256) adamw_mt_k(const int64_t* __restrict__ tab, const float* __restrict__ ftab,
                                                   const int64_t* __restrict__ chunks, float lr, float b1, float b2,
                                                   float eps, float bc1, float bc2, float gscale,
@@ -316,15 +253,7 @@ __global__ void __launch_bounds__(256) adamw_mt_k(const int64_t* __restrict__ ta
   if (end > n) end = n;
   const bool aligned = ((start & 3) == 0) && ((((uintptr_t)master | (uintptr_t)m | (uintptr_t)v) & 15) == 0) &&
                        ((((uintptr_t)grad | (uintptr_t)lowp) & 7) == 0);
-  if (V8 && aligned && mdt == kF32 && gdt == kBF16 && (!lowp || pdt == kBF16) && (start & 7) == 0 &&
-      ((((uintptr_t)grad | (uintptr_t)lowp) & 15) == 0)) {
-    const int64_t vend = start + ((end - start) & ~(int64_t)7);
-    if (lowp) adamw_vec8<true, V8 == 3, V8 >= 2>((float*)master, (const uint16_t*)grad, m, v, (uint16_t*)lowp, start,
-                                                 vend, b1, b2, eps, decay, step, rbc2, gscale);
-    else adamw_vec8<false, V8 == 3, V8 >= 2>((float*)master, (const uint16_t*)grad, m, v, nullptr, start, vend, b1,
-                                             b2, eps, decay, step, rbc2, gscale);
-    start = vend;
-  } else if (aligned && mdt == kF32 && (gdt == kBF16 || gdt == kF32) && (!lowp || pdt == kBF16)) {
+  if (aligned && mdt == kF32 && (gdt == kBF16 || gdt == kF32) && (!lowp || pdt == kBF16)) {
     const int64_t vend = start + ((end - start) & ~(int64_t)3);
     if (gdt == kBF16) {
       if (lowp) adamw_vec4<true, true>((float*)master, grad, m, v, (uint16_t*)lowp, start, vend, b1, b2, eps,
@@ -497,20 +426,8 @@ void pra_bias_gelu_bwd(const void* dy, const void* x, const void* b, void* dx, i
 void pra_adamw_mt(const int64_t* tab, const float* ftab, const int64_t* chunks, int nchunks, float lr, float b1,
                   float b2, float eps, float bc1, float bc2, float gscale, const float* gscale_ptr, hipStream_t s) {
   if (!nchunks) return;
-  static const int v8 = [] {
-    const char* e = getenv("PRA_ADAMW_V8");
-    return e ? atoi(e) : 0;
-  }();
-#define PRA_ADAMW_L(V)                                                                                              \
-  hipLaunchKernelGGL(adamw_mt_k<V>, dim3(nchunks), dim3(256), 0, s, tab, ftab, chunks, lr, b1, b2, eps, bc1, bc2, \
-                     gscale, gscale_ptr)
-  switch (v8) {
-    case 1: PRA_ADAMW_L(1); break;
-    case 2: PRA_ADAMW_L(2); break;
-    case 3: PRA_ADAMW_L(3); break;
-    default: PRA_ADAMW_L(0);
-  }
-#undef PRA_ADAMW_L
+  hipLaunchKernelGGL(adamw_mt_k, dim3(nchunks), dim3(256), 0, s, tab, ftab, chunks, lr, b1, b2, eps, bc1, bc2,
+                     gscale, gscale_ptr);
 }
 void pra_zero_mt(const int64_t* chunks, int nchunks, hipStream_t s) {
   if (nchunks > 0) hipLaunchKernelGGL(zero_mt_k, dim3(nchunks), dim3(256), 0, s, chunks);

@@ -1734,8 +1734,16 @@ def _conv1x1_stats_shape(x, w, stride):
     """Shapes where the fused path measured faster forward+backward than hipBLASLt + the separate
     statistics pass (profiles/r3g/conv1x1_bn_shapes.md, ResNet-50 bs 256): the 14x14 / 7x7 stages
     and the wide (>= 512 channel) 28x28 outputs; the 56x56 stage stays on the library GEMM."""
+    if _CONV1X1_STATS_ALL:
+        # round 5: with the finalize pre-merge and no zero-filled stats gradients the 56x56
+        # stage joins too (ResNet-50 bs 256: 9137 / 9154 vs 8936 / 8943 img/s with the 56x56
+        # forwards on hipBLASLt + the separate statistics pass, profiles/r5/resnet_conv1x1_all_ab.log)
+        return True
     m = x.shape[0] * ((x.shape[1] - 1) // stride + 1) * ((x.shape[2] - 1) // stride + 1)
     return m <= 65536 or (m <= 262144 and w.shape[0] >= 512)
+
+
+_CONV1X1_STATS_ALL = __import__('os').environ.get('PRA_CONV1X1_STATS_ALL', '1') == '1'
 
 
 # =============================================================================
