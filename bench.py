@@ -256,6 +256,14 @@ def bench_resnet(a, paddle, torch, dist, C, world, rank, dev):
                                     multi_precision=True)
     if world > 1:
         model = paddle.DataParallel(model)
+    elif dev.type == 'cuda' and not a.no_graph and os.environ.get('PRA_RESNET_GRAPH', '0') == '1':
+        # (opt-in, PRA_RESNET_GRAPH=1) jit.to_static training capture: forward and backward of the
+        # dygraph model replayed as two HIP graphs (jit/api.py _TrainGraph, accumulate mode).
+        # Measured slower than eager on the same box: 9300 / 9291 vs 9546 / 9590 img/s
+        # (profiles/r5/resnet_graph_ab.log) -- the eager queue already keeps the GPU busy
+        st = paddle.static.BuildStrategy()
+        st.use_hip_graph = True
+        model = paddle.jit.to_static(model, build_strategy=st)
     bs = a.micro_batch if a.micro_batch != 16 else 256
     x = paddle.Tensor(torch.randn(bs, 224, 224, 3, device=dev, dtype=torch.bfloat16))
     y = paddle.Tensor(torch.randint(0, 1000, (bs,), device=dev))
@@ -270,13 +278,20 @@ def bench_resnet(a, paddle, torch, dist, C, world, rank, dev):
     dt = _timed(step, a, torch, dist, world, dev)
     if a.profile_dir:
         _op_profile(step, a, torch, rank)
+    graphed = hasattr(model, 'forward') and hasattr(model.forward, 'graph_status')
+    if graphed:
+        st_ = model.forward.graph_status()
+        graphed = bool(st_) and all(v == 'graph' for v in st_.values())
+        if not graphed and rank == 0:
+            print(f"resnet: HIP-graph capture fell back to eager: {st_}", file=sys.stderr)
     ips = bs * world * a.steps / dt
     return {"metric": "samples/sec ResNet50 bf16", "value": round(ips, 2), "unit": "images/s",
             "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": round(dt / a.steps * 1000, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
             "config": {"model": "ResNet50", "global_batch": bs * world, "seq_len": None,
-                       "parallelism": f"dp{world}"},
+                       "parallelism": f"dp{world}",
+                       "executor": "HIP graph (jit.to_static capture)" if graphed else "eager"},
             "samples_per_sec_per_gpu": round(ips / world, 2)}
 
 

@@ -33,6 +33,7 @@ from ..framework.core import Tensor, _u
 from ..static.input import InputSpec
 
 _enabled = [True]
+_TRAIN_GRAPH_ACCUMULATE = os.environ.get('PRA_TRAIN_GRAPH_ACCUMULATE', '1') == '1'
 _graph_default = [os.environ.get('PRA_TO_STATIC_HIP_GRAPH', '1') == '1']
 
 
@@ -178,17 +179,33 @@ class _TrainGraph:
         ptens = [p._t for p in self.params]
         diff_in = [t for t in self.static_in if t.requires_grad]
         wrt = diff_in + ptens
+        # Accumulate mode (no differentiable inputs, no post-accumulate hooks on the parameters):
+        # the backward graph adds straight into the parameters' .grad buffers -- the fused
+        # kernels' in-place beta=1 / finalize accumulation and autograd's AccumulateGrad are
+        # captured -- so a replay hands no per-parameter gradient copies back to autograd. The
+        # .grad buffers must keep their storage (clear_grad(set_to_zero=True) zeroes in place).
+        self.accumulate = (_TRAIN_GRAPH_ACCUMULATE and not diff_in and all(
+            not getattr(p, '_post_accumulate_grad_hooks', None) for p in ptens))
         saved_grads = [p.grad for p in ptens]
-        for p in ptens:   # fused kernels add into an existing .grad in place: keep them pure
-            p.grad = None
+        if self.accumulate:
+            for p in ptens:
+                if p.grad is None:
+                    p.grad = torch.zeros_like(p)
+            saved_grads = [p.grad.clone() for p in ptens]
+        else:
+            for p in ptens:   # fused kernels add into an existing .grad in place: keep them pure
+                p.grad = None
         try:
             s = torch.cuda.Stream()
             s.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(s):
                 for _ in range(2):  # warm up allocator / lazy inits / autotuning
                     outs = [o._t for o in _flat_tensors(fn(*sargs, **skw), [])]
-                    torch.autograd.grad(outs, wrt, [torch.ones_like(o) for o in outs],
-                                        allow_unused=True)
+                    if self.accumulate:
+                        torch.autograd.backward(outs, [torch.ones_like(o) for o in outs], inputs=ptens)
+                    else:
+                        torch.autograd.grad(outs, wrt, [torch.ones_like(o) for o in outs],
+                                            allow_unused=True)
             torch.cuda.current_stream().wait_stream(s)
             pool = torch.cuda.graph_pool_handle()
             self.fwd_graph = torch.cuda.CUDAGraph()
@@ -203,12 +220,20 @@ class _TrainGraph:
             self.bwd_graph = torch.cuda.CUDAGraph()
             with managed_graph_rng():  # reads the forward's counter value, never advances it
                 with torch.cuda.graph(self.bwd_graph, pool=pool):
-                    grads = torch.autograd.grad(self.static_out, wrt, self.static_gout,
-                                                allow_unused=True)
+                    if self.accumulate:
+                        torch.autograd.backward(self.static_out, self.static_gout, inputs=ptens)
+                        grads = [None] * len(wrt)
+                    else:
+                        grads = torch.autograd.grad(self.static_out, wrt, self.static_gout,
+                                                    allow_unused=True)
             self.static_grads = [g if g is not None else None for g in grads]
         finally:
-            for p, g in zip(ptens, saved_grads):
-                p.grad = g
+            if self.accumulate:   # the warm-up added into the buffers: restore their values
+                for p, g in zip(ptens, saved_grads):
+                    p.grad.copy_(g)
+            else:
+                for p, g in zip(ptens, saved_grads):
+                    p.grad = g
         self.diff_mask = [t.requires_grad for t in self.static_in]
         entry = self
 
@@ -232,6 +257,8 @@ class _TrainGraph:
                     else:
                         buf.copy_(g, non_blocking=True)
                 entry.bwd_graph.replay()
+                if entry.accumulate:   # already added into the parameters' .grad
+                    return tuple(None for _ in range(len(entry.static_in) + len(entry.params)))
                 gi = iter(entry.static_grads)
                 res = []
                 for m in entry.diff_mask:

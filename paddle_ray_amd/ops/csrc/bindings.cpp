@@ -84,8 +84,10 @@ int pra_gemm_probe(int, int, const void*, const void*, void*, int, int, int, int
                    hipStream_t);
 int pra_gemm_get_w4();
 int pra_conv_lds(const void*, const void*, const void*, void*, int, int, int, int, int, int, int, int, int, int, int,
-                 int, float*, float*, const float*, int, hipStream_t, const void*, const uint8_t*);
+                 int, float*, float*, const float*, int, hipStream_t, const void*, const uint8_t*, int);
 int pra_conv_lds_stat_rows(int, int);
+int pra_conv_dgrad_phase(const void*, const void*, void*, int, int, int, int, int, int, int, int, int, float*,
+                         const float*, const void*, const uint8_t*, hipStream_t);
 int pra_conv_lds_splits(int, int, int);
 int pra_conv_wgrad_rows(int);
 int pra_conv_wgrad_lds(const void*, const void*, void*, int, int, int, int, int, int, int, int, int, int, int, float*,
@@ -128,13 +130,22 @@ PYBIND11_MODULE(_pra_hip, m) {
     check_launch("gemm_bias_act");
   });
   m.def("conv_lds", [](P x, P w, P bias, P y, int n, int h, int wd, int c, int cout, int kh, int kw, int st,
-                       int pad, int relu, int dt, int splits, P ws, P part, P kshift, int pp, P s, P bnx, P bnmask) {
+                       int pad, int relu, int dt, int splits, P ws, P part, P kshift, int pp, P s, P bnx, P bnmask,
+                       int beta) {
     if (pra_conv_lds(CV(x), CV(w), CV(bias), V(y), n, h, wd, c, cout, kh, kw, st, pad, relu, dt, splits,
                      reinterpret_cast<float*>(ws), reinterpret_cast<float*>(part),
                      reinterpret_cast<const float*>(kshift), pp, S(s), CV(bnx),
-                     reinterpret_cast<const uint8_t*>(bnmask)) != 0)
+                     reinterpret_cast<const uint8_t*>(bnmask), beta) != 0)
       throw std::invalid_argument("conv_lds: unsupported shape/dtype");
     check_launch("conv_lds");
+  });
+  m.def("conv_dgrad_phase", [](P dy, P wp, P dxp, int n, int ho, int wo, int co, int ci, int khp, int kwp, int os,
+                               int dt, P part, P kshift, P bnx, P bnmask, P s) {
+    if (pra_conv_dgrad_phase(CV(dy), CV(wp), V(dxp), n, ho, wo, co, ci, khp, kwp, os, dt, reinterpret_cast<float*>(part),
+                             reinterpret_cast<const float*>(kshift), CV(bnx), reinterpret_cast<const uint8_t*>(bnmask),
+                             S(s)) != 0)
+      throw std::invalid_argument("conv_dgrad_phase: unsupported shape/dtype");
+    check_launch("conv_dgrad_phase");
   });
   m.def("conv_wgrad_lds", [](P dy, P x, P dw, int n, int h, int wd, int c, int cout, int kh, int kw, int st, int pad,
                              int dt, int splits, P ws, int pp, P s) {

@@ -278,6 +278,10 @@ struct Dma {
 // contiguous 128-B segment), with taps counted in units of C columns.
 struct ConvGeom {
   int Ho, Wo, H, W, C, KW, S, P, PP;
+  // OS > 0 (sub-pixel phase of a stride-OS transposed convolution, the strided dgrad): output
+  // row m = (n, i, j) of the Ho x Wo phase grid is written to pixel (n, OS*i, OS*j) of an
+  // (OS*Ho) x (OS*Wo) image (the phase offset is folded into the output pointer)
+  int OS = 0;
 };
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -796,6 +800,13 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_lds_kernel(const uint16_t* __r
   constexpr int TPR = BN / 8, RSTEP = NT / TPR, NQ = 128 / RSTEP, QB = NQ < 4 ? NQ : 4;
   const int ucol = (tid % TPR) * 8, urow = tid / TPR;
   const int n = n0 + ucol;
+  // output / Z / keep-bit row of GEMM row m (identity unless a strided-dgrad phase)
+  auto orow = [&](int m) -> int64_t {
+    if constexpr (CONV) {
+      if (cg.OS) return (int64_t)cg.OS * cg.OS * m - (int64_t)cg.OS * (cg.OS - 1) * (m % cg.Wo);
+    }
+    return m;
+  };
   const bool ncol_ok = n < N;  // N % 8 == 0: a unit is all-in or all-out
   float bv[8];
 #pragma unroll
@@ -827,8 +838,9 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_lds_kernel(const uint16_t* __r
     for (int q = 0; q < NU; ++q) {
       const int m = m0 + (q / NQ) * 128 + urow + RSTEP * (q % NQ);
       if (m < M && ncol_ok) {
-        zp[q] = *reinterpret_cast<const uint4*>(Z + (int64_t)m * ldz + n);
-        mp[q] = mbits[((int64_t)m * N + n) >> 3];
+        const int64_t mo = orow(m);
+        zp[q] = *reinterpret_cast<const uint4*>(Z + mo * ldz + n);
+        mp[q] = mbits[(mo * N + n) >> 3];
       }
     }
   }
@@ -853,15 +865,19 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_lds_kernel(const uint16_t* __r
       f32x4 lo[QB], hi[QB];
       uint4 gz[QB];
       uint32_t mb[QB];
+      uint4 gc[(E == kBnG && BETA) ? QB : 1];   // kBnG + beta: the pending gradient C (added before the mask)
       bool ok[QB];
       int64_t moff[QB];
 #pragma unroll
       for (int u = 0; u < QB; ++u) {
         const int rr = urow + RSTEP * (bq + u), m = m0 + h * 128 + rr;
         ok[u] = m < M && ncol_ok;
-        moff[u] = (int64_t)(ok[u] ? m : 0);
+        moff[u] = ok[u] ? orow(m) : 0;
         lo[u] = *reinterpret_cast<const f32x4*>(img + rr * PITCH + ucol);
         hi[u] = *reinterpret_cast<const f32x4*>(img + rr * PITCH + ucol + 4);
+        if constexpr (E == kBnG && BETA) {
+          if (ok[u]) gc[u] = *reinterpret_cast<const uint4*>(C + moff[u] * ldc + n);
+        }
         if constexpr (ZPRE) {
           gz[u] = zp[h * NQ + bq + u];
           mb[u] = mp[h * NQ + bq + u];
@@ -896,6 +912,11 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_lds_kernel(const uint16_t* __r
           o.z = pack2<T>(d[4], d[5]); o.w = pack2<T>(d[6], d[7]);
           *reinterpret_cast<uint4*>(Z + m * ldz + n) = o;
         } else if constexpr (E == kBnG) {
+          if constexpr (BETA) {
+            const uint32_t c4[4] = {gc[u].x, gc[u].y, gc[u].z, gc[u].w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) { v[2 * e] += to_f<T>(c4[e] & 0xffff); v[2 * e + 1] += to_f<T>(c4[e] >> 16); }
+          }
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] = (mb[u] >> e) & 1u ? v[e] : 0.f;
         } else if (E != kNone) {

@@ -198,7 +198,7 @@ int launch_t(int layout, const void* A, const void* B, const void* bias, void* C
 template <typename T, typename CF, int E>
 void launch_conv_cfg(const void* xpad, const void* W, const void* bias, void* Y, int M, int N, int K,
                      const ConvGeom& cg, int splits, float* ws, float* part, const float* kshift, hipStream_t s,
-                     const void* bnx = nullptr, const uint8_t* bnmask = nullptr) {
+                     const void* bnx = nullptr, const uint8_t* bnmask = nullptr, int beta = 0) {
   const int tiles_m = (M + CF::BM - 1) / CF::BM;
   const int tiles = tiles_m * ((N + CF::BN - 1) / CF::BN);
   auto px = static_cast<const uint16_t*>(xpad);
@@ -217,6 +217,14 @@ void launch_conv_cfg(const void* xpad, const void* W, const void* bias, void* Y,
   // part (optional): per-tile-row BatchNorm statistics of the output, [2][tiles_m][N] = sums of
   // (y - kshift) and (y - kshift)^2 over each tile's rows (kshift: the running mean).
   // kBnG: Y = dgrad masked by bnmask, part = sums of Y and Y * (bnx - kshift) (kshift: BN batch mean)
+  if constexpr (E == kBnG) {
+    if (beta) {  // the pending gradient in Y is added before the ReLU mask (a residual join's last term)
+      gemm_lds_kernel<T, CF, true, true, E, true, false, true><<<tiles, CF::NT, 0, s>>>(
+          px, pw, pb, py, const_cast<uint16_t*>(static_cast<const uint16_t*>(bnx)), part, M, N, K, 0, K, N, N, 1,
+          nullptr, cg, part + (int64_t)tiles_m * N, kshift, bnmask);
+      return;
+    }
+  }
   gemm_lds_kernel<T, CF, true, true, E, false, false, true><<<tiles, CF::NT, 0, s>>>(
       px, pw, pb, py, const_cast<uint16_t*>(static_cast<const uint16_t*>(bnx)), part, M, N, K, 0, K, N, N, 1, nullptr,
       cg, part ? part + (int64_t)tiles_m * N : nullptr, kshift, bnmask);
@@ -257,10 +265,12 @@ inline int conv_tile_rows(int N) { return N <= 64 ? C64::BM : (N <= 128 ? C128::
 template <typename T, int E>
 int launch_conv(const void* xpad, const void* W, const void* bias, void* Y, int M, int N, int K, const ConvGeom& cg,
                 int splits, float* ws, float* part, const float* kshift, hipStream_t s, const void* bnx = nullptr,
-                const uint8_t* bnmask = nullptr) {
-  if (N <= 64) launch_conv_cfg<T, C64, E>(xpad, W, bias, Y, M, N, K, cg, 1, nullptr, part, kshift, s, bnx, bnmask);
-  else if (N <= 128) launch_conv_cfg<T, C128, E>(xpad, W, bias, Y, M, N, K, cg, 1, nullptr, part, kshift, s, bnx, bnmask);
-  else launch_conv_cfg<T, W8, E>(xpad, W, bias, Y, M, N, K, cg, part ? 1 : splits, ws, part, kshift, s, bnx, bnmask);
+                const uint8_t* bnmask = nullptr, int beta = 0) {
+  if (N <= 64) launch_conv_cfg<T, C64, E>(xpad, W, bias, Y, M, N, K, cg, 1, nullptr, part, kshift, s, bnx, bnmask, beta);
+  else if (N <= 128)
+    launch_conv_cfg<T, C128, E>(xpad, W, bias, Y, M, N, K, cg, 1, nullptr, part, kshift, s, bnx, bnmask, beta);
+  else
+    launch_conv_cfg<T, W8, E>(xpad, W, bias, Y, M, N, K, cg, part ? 1 : splits, ws, part, kshift, s, bnx, bnmask, beta);
   return 0;
 }
 
@@ -283,10 +293,11 @@ extern "C" int pra_conv_lds_stat_rows(int M, int Cout) { return (M + pra::conv_t
 // bnx / bnmask (optional, a dgrad feeding BatchNorm(+ReLU)'s backward): Y = the product masked by
 // the ReLU keep-bits bnmask ([M*Cout/8] bytes), part = per-tile sums of Y and of Y * (bnx - kshift)
 // with bnx the BN input [M][Cout] and kshift its batch mean; needs part, kshift, no relu/bias/split.
+// beta (bnx only): Y holds a pending gradient that is added to the product before the mask.
 extern "C" int pra_conv_lds(const void* x, const void* W, const void* bias, void* Y, int Nimg, int H, int Wd,
                             int C, int Cout, int KH, int KW, int S, int P, int relu, int dtype, int splits, float* ws,
                             float* part, const float* kshift, int pp, hipStream_t s, const void* bnx = nullptr,
-                            const uint8_t* bnmask = nullptr) {
+                            const uint8_t* bnmask = nullptr, int beta = 0) {
   if (pp <= 0) pp = C;
   if (bnx && (!bnmask || !part || !kshift || relu || bias || splits > 1)) return -1;
   if (C % 64 || Cout % 8 || KH <= 0 || KW <= 0 || S <= 0 || P < 0 || H <= 0 || Wd <= 0) return -1;
@@ -303,15 +314,49 @@ extern "C" int pra_conv_lds(const void* x, const void* W, const void* bias, void
   pra::ConvGeom cg{Ho, Wo, H, Wd, C, KW, S, P, pp};
   if (bnx) {
     if (dtype == pra::kBF16)
-      return pra::launch_conv<pra::bf16, pra::kBnG>(x, W, nullptr, Y, M, Cout, K, cg, 1, nullptr, part, kshift, s, bnx, bnmask);
+      return pra::launch_conv<pra::bf16, pra::kBnG>(x, W, nullptr, Y, M, Cout, K, cg, 1, nullptr, part, kshift, s, bnx,
+                                                   bnmask, beta);
     if (dtype == pra::kF16)
-      return pra::launch_conv<pra::f16, pra::kBnG>(x, W, nullptr, Y, M, Cout, K, cg, 1, nullptr, part, kshift, s, bnx, bnmask);
+      return pra::launch_conv<pra::f16, pra::kBnG>(x, W, nullptr, Y, M, Cout, K, cg, 1, nullptr, part, kshift, s, bnx,
+                                                  bnmask, beta);
     return -1;
   }
+  if (beta) return -1;
   if (dtype == pra::kBF16) return relu ? pra::launch_conv<pra::bf16, pra::kRelu>(x, W, bias, Y, M, Cout, K, cg, splits, ws, part, kshift, s)
                                   : pra::launch_conv<pra::bf16, pra::kNone>(x, W, bias, Y, M, Cout, K, cg, splits, ws, part, kshift, s);
   if (dtype == pra::kF16) return relu ? pra::launch_conv<pra::f16, pra::kRelu>(x, W, bias, Y, M, Cout, K, cg, splits, ws, part, kshift, s)
                                  : pra::launch_conv<pra::f16, pra::kNone>(x, W, bias, Y, M, Cout, K, cg, splits, ws, part, kshift, s);
+  return -1;
+}
+
+// One sub-pixel phase of a stride-OS transposed convolution (the input gradient of a strided
+// conv): dxp = conv_stride1(dy, Wp) over the Ho x Wo grid of dy with the phase's KHp x KWp taps
+// at non-negative offsets (taps past the image edge read zeros), row (n, i, j) written to pixel
+// (n, OS*i, OS*j) of dx_phase (dx + the phase's pixel offset, an (OS*Ho) x (OS*Wo) image).
+// dy [Nimg][Ho][Wo][Co], Wp [Ci][KHp*KWp*Co]; Co % 64 == 0, Ci % 8 == 0. No split-K.
+// bnx / bnmask / part / kshift: the kBnG epilogue as in pra_conv_lds (same phase offset applied
+// to bnx and bnmask by the caller).
+extern "C" int pra_conv_dgrad_phase(const void* dy, const void* Wp, void* dx_phase, int Nimg, int Ho, int Wo, int Co,
+                                    int Ci, int KHp, int KWp, int OS, int dtype, float* part, const float* kshift,
+                                    const void* bnx, const uint8_t* bnmask, hipStream_t s) {
+  if (Co % 64 || Ci % 8 || KHp <= 0 || KWp <= 0 || OS < 2 || Ho <= 0 || Wo <= 0 || Ho >= 32768 || Wo >= 32768)
+    return -1;
+  if ((long long)Nimg * Ho * Wo * Co * 2 >= (1ll << 31) || (long long)Nimg * Ho * Wo * OS * OS * Ci * 2 >= (1ll << 31))
+    return -1;
+  if (bnx && (!bnmask || !part || !kshift)) return -1;
+  const int M = Nimg * Ho * Wo, K = KHp * KWp * Co;
+  pra::ConvGeom cg{Ho, Wo, Ho, Wo, Co, KWp, 1, 0, Co};
+  cg.OS = OS;
+  if (dtype == pra::kBF16)
+    return bnx ? pra::launch_conv<pra::bf16, pra::kBnG>(dy, Wp, nullptr, dx_phase, M, Ci, K, cg, 1, nullptr, part, kshift,
+                                                        s, bnx, bnmask)
+               : pra::launch_conv<pra::bf16, pra::kNone>(dy, Wp, nullptr, dx_phase, M, Ci, K, cg, 1, nullptr, part,
+                                                         kshift, s);
+  if (dtype == pra::kF16)
+    return bnx ? pra::launch_conv<pra::f16, pra::kBnG>(dy, Wp, nullptr, dx_phase, M, Ci, K, cg, 1, nullptr, part, kshift,
+                                                       s, bnx, bnmask)
+               : pra::launch_conv<pra::f16, pra::kNone>(dy, Wp, nullptr, dx_phase, M, Ci, K, cg, 1, nullptr, part, kshift,
+                                                        s);
   return -1;
 }
 

@@ -1522,6 +1522,20 @@ class GradJoin:
         return None
 
     def add_gemm(self, dy2, w2, xshape):
+        # the join's LAST term with a BatchNorm+ReLU (+ residual) producing x: the 1x1 dgrad runs
+        # on the implicit-GEMM kernel with the kBnG epilogue, adding the pending sum first, so the
+        # BN backward receives the masked total and its reductions (no reduce pass over it)
+        left = self.n if self.left is None else self.left
+        rec = _bn_handoff(self.x) if left == 1 and not self.deferred else None
+        m, cout = dy2.shape
+        cin = w2.shape[1]
+        if (rec is not None and cout % 64 == 0 and cin % 8 == 0 and rec.x2.shape == (m, cin)
+                and rec.x2.is_contiguous() and len(xshape) == 4
+                and (self.pending is None or self.pending.is_contiguous()) and _bn_dgrad_ok(rec, m, cin, cout)):
+            dy4 = dy2.view(*xshape[:3], cout)
+            out = self.pending.view(xshape) if self.pending is not None else None
+            self.pending = _bn_dgrad(rec, dy4, w2.t().contiguous(), 1, 1, 0, out=out).view(xshape)
+            return self._finish()
         if self.pending is None:
             self.pending = gemm(GEMM_FWD, dy2, w2).view(xshape)
         else:
@@ -1616,9 +1630,10 @@ def _bn_dgrad_ok(rec, m, cout_dgrad, k):
             and (_BN_DGRAD_SPLIT or _native.lib().conv_lds_splits(m, cout_dgrad, k) == 1))
 
 
-def _bn_dgrad(rec, dy4, wk, kh, kw, pad):
-    """dgrad on the implicit-GEMM kernel with the kBnG epilogue; stores g + partials in rec."""
-    g, part = _conv_lds(dy4, wk, None, kh, kw, 1, pad, bn=(rec.x2, rec.mask, rec.mean))
+def _bn_dgrad(rec, dy4, wk, kh, kw, pad, out=None):
+    """dgrad on the implicit-GEMM kernel with the kBnG epilogue; stores g + partials in rec.
+    out: a pending gradient the product is added to (in place) before the mask."""
+    g, part = _conv_lds(dy4, wk, None, kh, kw, 1, pad, bn=(rec.x2, rec.mask, rec.mean), out=out)
     rec.g, rec.part, rec.gver = g, part, g._version
     return g
 
@@ -1764,14 +1779,15 @@ def conv_kxk_supported(x, w, stride, padding):
             and x.numel() * 2 < 2 ** 31 and max(x.shape[1], x.shape[2]) < 32768)
 
 
-def _conv_lds(x, wk, bias, kh, kw, stride, pad, relu=False, stats_shift=None, cv=None, bn=None):
+def _conv_lds(x, wk, bias, kh, kw, stride, pad, relu=False, stats_shift=None, cv=None, bn=None, out=None):
     """y[N,Ho,Wo,Cout] = conv(x NHWC, wk [Cout, kh*kw*C] (OHWI)) via the implicit-GEMM kernel
     (zero padding applied by the kernel's DMA range check, the input is read in place).
     stats_shift (fp32 [Cout], e.g. the BN running mean): the epilogue also returns the per-tile
     BatchNorm partial sums part [2, rows, Cout] of (y - shift) and (y - shift)^2.
     bn = (x2, mask, mean) of a BatchNorm+ReLU whose output this conv's dgrad is the gradient of:
     y = the product masked by the ReLU keep-bits, part = per-tile sums of y and y * (x2 - mean)
-    (gemm_core.h kBnG), returned as (y, part)."""
+    (gemm_core.h kBnG), returned as (y, part). out (bn only): y is written in place and its
+    current contents (a pending gradient) are added to the product before the mask."""
     n, h, wd, c = x.shape
     cout = wk.shape[0]
     x = x.contiguous()
@@ -1782,7 +1798,11 @@ def _conv_lds(x, wk, bias, kh, kw, stride, pad, relu=False, stats_shift=None, cv
         ho, wo = (h - kh) // stride + 1, (wd - c // pp) // stride + 1
     else:
         ho, wo = (h + 2 * pad - kh) // stride + 1, (wd + 2 * pad - kw) // stride + 1
-    y = torch.empty((n, ho, wo, cout), device=x.device, dtype=x.dtype)
+    if out is not None:
+        assert bn is not None and out.is_contiguous() and out.numel() == n * ho * wo * cout and out.dtype == x.dtype
+        y = out
+    else:
+        y = torch.empty((n, ho, wo, cout), device=x.device, dtype=x.dtype)
     if bias is not None and (bias.dtype != x.dtype or not bias.is_contiguous()):
         bias = bias.to(x.dtype).contiguous()
     L = _native.lib()
@@ -1801,7 +1821,7 @@ def _conv_lds(x, wk, bias, kh, kw, stride, pad, relu=False, stats_shift=None, cv
     ws = torch.empty((splits, m, cout), device=x.device, dtype=torch.float32) if splits > 1 else None
     L.conv_lds(x.data_ptr(), wk.data_ptr(), _ptr(bias), y.data_ptr(), n, h, wd, c, cout, kh, kw,
                stride, pad, int(relu), _dt(x), splits, _ptr(ws), _ptr(part), _ptr(stats_shift), pp, _stream(),
-               bnx, bnm)
+               bnx, bnm, int(out is not None))
     return y if stats_shift is None else (y, part)
 
 
@@ -1844,6 +1864,79 @@ _CONV_WGRAD = __import__('os').environ.get('PRA_CONV_WGRAD', 'mfma')
 _CONV_WGRAD_NARROW = __import__('os').environ.get('PRA_CONV_WGRAD_NARROW', '1') == '1'
 
 
+# Strided (stride-2, 3x3, pad 1) input gradient as four sub-pixel phases on the implicit-GEMM
+# kernel (gemm_lds.hip pra_conv_dgrad_phase): the transposed convolution's output pixel
+# (2i + ph, 2j + pw) only meets filter taps ky with (ph + 1 - ky) even, at dy row offset
+# (ph + 1 - ky) / 2 in {0, 1}; each phase is a stride-1 conv of dy with a 1x1 / 1x2 / 2x1 / 2x2
+# sub-filter whose epilogue writes the phase's pixels of dx directly (every pixel exactly once, no
+# zero fill, no interleave pass). Parity: the reference's strided conv2d_grad (phi gpudnn).
+# Off by default: ResNet-50 bs 256 measured 8991 vs 9178 img/s against MIOpen's igemm_bwd (the
+# per-phase K of 1-4 taps x Cout leaves each launch prologue/epilogue-bound; 56x56x128: 210 vs
+# 173 us, 28x28x256: 125 vs 149 us, 14x14x512: 189 vs 141 us, profiles/r5/strided_dgrad_probe.md)
+_STRIDED_DGRAD = __import__('os').environ.get('PRA_STRIDED_DGRAD', '0') == '1'
+_S2_TAPS = {0: [(0, 1)], 1: [(0, 2), (1, 0)]}   # phase -> [(dy offset, filter tap)]
+_S2_IDX = {}
+
+
+def _s2_phase_index(w):
+    """Gather index over w.flatten() of the four phase sub-filters (each [Cin, khp*kwp*Cout],
+    OHWI over the phase's taps) concatenated, and the phase table (ph, pw, khp, kwp, off, numel)."""
+    cout, cin, kh, kw = w.shape
+    key = (cout, cin, w.device)
+    if key not in _S2_IDX:
+        ci = torch.arange(cin).view(cin, 1, 1, 1)
+        co = torch.arange(cout).view(1, 1, 1, cout)
+        parts, table, off = [], [], 0
+        for ph in (0, 1):
+            for pw in (0, 1):
+                rows, cols = _S2_TAPS[ph], _S2_TAPS[pw]
+                ky = torch.tensor([k for _, k in rows]).view(1, -1, 1, 1)
+                kx = torch.tensor([k for _, k in cols]).view(1, 1, -1, 1)
+                idx = ((co * cin + ci) * 3 + ky) * 3 + kx          # [cin, khp, kwp, cout]
+                parts.append(idx.reshape(-1))
+                table.append((ph, pw, len(rows), len(cols), off, idx.numel()))
+                off += idx.numel()
+        _S2_IDX[key] = (torch.cat(parts).to(w.device), table)
+    return _S2_IDX[key]
+
+
+def strided_dgrad_ok(x, dy, w, stride, pad):
+    cout, cin, kh, kw = w.shape
+    return (_STRIDED_DGRAD and stride == 2 and kh == kw == 3 and pad == 1 and dy.is_cuda
+            and x.shape[1] == 2 * dy.shape[1] and x.shape[2] == 2 * dy.shape[2]
+            and cout % 64 == 0 and cin % 8 == 0 and dy.dtype in _HALF and w.dtype == dy.dtype
+            and dy.numel() * 2 < 2 ** 31 and x.numel() * 2 < 2 ** 31 and max(dy.shape[1], dy.shape[2]) < 32768)
+
+
+def _conv_dgrad_s2(dy, w, xshape, rec=None):
+    """dx [N, 2Ho, 2Wo, Cin] of a 3x3 / stride 2 / pad 1 conv from dy [N, Ho, Wo, Cout].
+    rec (_BnHandoff of the BatchNorm+ReLU producing the conv input): every phase's epilogue
+    applies the ReLU keep-bits and emits its BN partial sums (kBnG); stored into rec."""
+    idx, table = _s2_phase_index(w)
+    n, h, wd, cin = xshape
+    _, ho, wo, cout = dy.shape
+    dy = dy.contiguous()
+    wcat = w.reshape(-1)[idx]
+    dx = torch.empty(xshape, device=dy.device, dtype=dy.dtype)
+    L = _native.lib()
+    es = dx.element_size()
+    parts = []
+    for ph, pw, khp, kwp, off, cnt in table:
+        pix = ph * wd + pw
+        part = bnx = bnm = kshift = 0
+        if rec is not None:
+            pt = torch.empty((2, L.conv_lds_stat_rows(n * ho * wo, cin), cin), device=dy.device, dtype=torch.float32)
+            parts.append(pt)
+            part, kshift = pt.data_ptr(), rec.mean.data_ptr()
+            bnx = rec.x2.data_ptr() + pix * cin * es
+            bnm = rec.mask.data_ptr() + pix * cin // 8
+        L.conv_dgrad_phase(dy.data_ptr(), wcat[off:off + cnt].data_ptr(), dx.data_ptr() + pix * cin * es, n, ho, wo,
+                           cout, cin, khp, kwp, 2, _dt(dy), part, kshift, bnx, bnm, _stream())
+    if rec is not None:
+        rec.g, rec.part, rec.gver = dx, torch.cat(parts, 1), dx._version
+    return dx
+
+
 class ConvKxKFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, bias, stride, pad):
@@ -1853,7 +1946,7 @@ class ConvKxKFn(torch.autograd.Function):
         y = _conv_lds(x, wk, bias, kh, kw, stride, pad)
         ctx.save_for_backward(x, w)
         ctx.meta = (stride, pad, bias is not None)
-        ctx.bn = _bn_handoff(x) if stride == 1 else None
+        ctx.bn = _bn_handoff(x) if stride in (1, 2) else None
         return y
 
     @staticmethod
@@ -1872,6 +1965,12 @@ class ConvKxKFn(torch.autograd.Function):
                 dx = _bn_dgrad(rec, dy, wf, kh, kw, kh - 1 - pad)
             else:
                 dx = _conv_lds(dy, wf, None, kh, kw, 1, kh - 1 - pad)
+        if ctx.needs_input_grad[0] and not ours_dx and strided_dgrad_ok(x, dy, w, stride, pad):
+            rec = getattr(ctx, 'bn', None)
+            ok = (rec is not None and rec.x2.shape == (x.shape[0] * x.shape[1] * x.shape[2], cin)
+                  and rec.x2.is_contiguous())
+            dx = _conv_dgrad_s2(dy, w, x.shape, rec if ok else None)
+            ours_dx = True
         need_lib_dx = ctx.needs_input_grad[0] and not ours_dx
         ours_dw = ctx.needs_input_grad[1] and _conv_wgrad_ok(x, dy, cout)
         if ours_dw:
@@ -1903,7 +2002,7 @@ class ConvKxKStatsFn(ConvKxKFn):
         y, part = _conv_lds(x, wk, bias, kh, kw, stride, pad, stats_shift=shift)
         ctx.save_for_backward(x, w)
         ctx.meta = (stride, pad, bias is not None)
-        ctx.bn = _bn_handoff(x) if stride == 1 else None
+        ctx.bn = _bn_handoff(x) if stride in (1, 2) else None
         ctx.mark_non_differentiable(part)
         ctx.set_materialize_grads(False)   # (no zero-filled [2, rows, C] gradient for part)
         return y, part
@@ -1964,6 +2063,20 @@ def _stem_index(w):
     return idx
 
 
+def _stem_inverse(idx, numel):
+    """Position in idx of every filter element (each appears exactly once): the weight gradient
+    is then one gather, no boolean mask (graph-capturable, no host sync)."""
+    key = ('inv', idx.data_ptr(), numel)
+    inv = _STEM_IDX.get(key)
+    if inv is None:
+        flat = idx.reshape(-1).cpu()
+        pos = torch.nonzero(flat >= 0).squeeze(1)
+        inv_h = torch.empty(numel, dtype=torch.long)
+        inv_h[flat[pos]] = pos
+        inv = _STEM_IDX[key] = inv_h.to(idx.device)
+    return inv
+
+
 class StemConvFn(torch.autograd.Function):
     """y = conv2d(x, w, stride 2, padding p) for a narrow channels-last input, through the
     space-to-depth stride-1 form; optional BN partial statistics of y (epilogue column sums
@@ -1985,6 +2098,7 @@ class StemConvFn(torch.autograd.Function):
         wk = wk.reshape(cout, kt * kt * _S2D_CO).contiguous()
         r = _conv_lds(xs, wk, None, kt, 1, 1, 0, stats_shift=shift, cv=kt * _S2D_CO)
         ctx.save_for_backward(xs, idx, x, w)
+        ctx.inv = _stem_inverse(idx, w.numel())
         ctx.meta = (kt, w.shape, pad)
         if shift is None:
             return r, None
@@ -2003,11 +2117,8 @@ class StemConvFn(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             dy = dy.contiguous()
             if (dy.shape[0] * dy.shape[1] * dy.shape[2]) % 64 == 0:
-                dwk = _conv_wgrad_lds(dy, xs, kt, 1, 1, 0, cv=kt * _S2D_CO).reshape(idx.shape)
-                valid = idx >= 0
-                dw = torch.zeros(int(torch.tensor(wshape).prod()), device=dwk.device, dtype=dwk.dtype)
-                dw.index_copy_(0, idx[valid], dwk[valid])
-                dw = dw.view(wshape)
+                dwk = _conv_wgrad_lds(dy, xs, kt, 1, 1, 0, cv=kt * _S2D_CO).reshape(-1)
+                dw = dwk[ctx.inv].view(wshape)
             else:   # the weight-gradient kernel walks the output pixels 64 at a time
                 _, dw, _ = torch.ops.aten.convolution_backward(
                     dy.permute(0, 3, 1, 2), x.permute(0, 3, 1, 2), w, None, [2, 2], [pad, pad], [1, 1],
@@ -2714,7 +2825,7 @@ class BatchNormActFn(torch.autograd.Function):
         ctx.has_b, ctx.training, ctx.b = b is not None, training, b
         out = y.view(shp)
         ctx.rec = None
-        if (_BN_DGRAD_FUSE and training and relu and z is None and mask is not None and x2.is_cuda
+        if (_BN_DGRAD_FUSE and training and relu and mask is not None and x2.is_cuda
                 and mean.dtype == torch.float32 and x2.dtype in _HALF):
             ctx.rec = out._pra_bn = _BnHandoff(x2, mask, mean)
         return out
@@ -2747,7 +2858,14 @@ class BatchNormActFn(torch.autograd.Function):
             # dy2 is the ReLU-masked gradient and part its reductions (the consumer conv's dgrad
             # epilogue): finalize + apply only
             dx, dw, db = _bn_bwd_parts_hip(dy2, x2, w, mean, invstd, part, acc)
-            return (dx.view(ctx.shp), None, dw if (w is not None and ctx.needs_input_grad[2]) else None,
+            dz = None
+            if ctx.has_z and ctx.needs_input_grad[1]:
+                # the residual's gradient IS the masked g (produced for this BN by the dgrad
+                # epilogue; nothing else holds it, so the join may accumulate into it)
+                dz = dy2.view(ctx.shp)
+                if ctx.join is not None:
+                    dz = ctx.join.add_tensor(dz, owned=True)
+            return (dx.view(ctx.shp), dz, dw if (w is not None and ctx.needs_input_grad[2]) else None,
                     db if (ctx.has_b and ctx.needs_input_grad[3]) else None,
                     None, None, None, None, None, None, None, None)
         if acc is not None:

@@ -1,0 +1,19 @@
+#!/bin/bash
+# Round 5: strided dgrad phases; in-kernel split-K fixup (GPT / BERT A/B).
+OUT=gpurun_out/${1:-r5v}
+mkdir -p $OUT
+export TMPDIR=/tmp
+fatal() { case $1 in 124|137|134|139) return 0;; esac; return 1; }
+step() { local name=$1 t=$2; shift 2; timeout -k 10 "$t" "$@" > $OUT/$name.log 2>&1; local rc=$?;
+         echo "[$name rc=$rc]"; grep -v amdgpu.ids $OUT/$name.log | tail -n 3 | cut -c1-200; if fatal $rc; then exit $rc; fi; }
+step tests 400 python -u -m pytest tests/test_gemm_lds_gpu.py tests/test_conv_kxk.py tests/test_bn_dgrad_fuse.py -m gpu -x -q --timeout 120 --timeout-method thread
+step probe 200 python scripts/strided_dgrad_probe.py
+step gpt 300 python bench.py --steps 10 --warmup 3
+PRA_SPLIT_FIXUP_MAX=1 step gpt_old 300 python bench.py --steps 10 --warmup 3
+step gpt2 300 python bench.py --steps 10 --warmup 3
+step bert 300 python bench.py --model bert --steps 20 --warmup 5
+PRA_SPLIT_FIXUP_MAX=1 step bert_old 300 python bench.py --model bert --steps 20 --warmup 5
+PRA_SPLIT_FIXUP_MAX=32 step bert_32 300 python bench.py --model bert --steps 20 --warmup 5
+step rn 300 python bench.py --model resnet50 --steps 20 --warmup 5
+PRA_STRIDED_DGRAD=0 step rn_old 300 python bench.py --model resnet50 --steps 20 --warmup 5
+exit 0

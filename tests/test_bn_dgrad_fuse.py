@@ -31,6 +31,8 @@ def _chain(x, s, b, w, kind, extra_use):
     a = K.batch_norm_act(x, None, s, b, rm, rv, True, 0.9, 1e-5, True)
     if kind == '3x3':
         y = K.conv_kxk_nhwc(a, w, None, 1, 1)
+    elif kind == '3x3s2':   # strided dgrad: four sub-pixel phase convs, each with the kBnG epilogue
+        y = K.conv_kxk_nhwc(a, w, None, 2, 1)
     elif kind == '3x3_stats':
         co = w.shape[0]
         assert K.conv_bn_stats_ok(a, w, 1, 1, torch.zeros(co, device=x.device), True)
@@ -45,6 +47,7 @@ def _chain(x, s, b, w, kind, extra_use):
 
 
 CASES = [('3x3', 64, 64), ('3x3', 128, 128), ('3x3', 256, 64), ('3x3_stats', 64, 128),
+         ('3x3s2', 64, 64), ('3x3s2', 128, 256),
          ('1x1', 64, 256), ('1x1', 128, 512), ('1x1', 256, 256)]
 
 
@@ -54,6 +57,7 @@ CASES = [('3x3', 64, 64), ('3x3', 128, 128), ('3x3', 256, 64), ('3x3_stats', 64,
 def test_bn_dgrad_fused_matches(case, extra_use, monkeypatch):
     kind, c, cout = case
     monkeypatch.setattr(K, '_BN_DGRAD_SPLIT', True)   # cover the W8 (C > 128) tile too
+    monkeypatch.setattr(K, '_STRIDED_DGRAD', True)    # (off by default: MIOpen measured faster)
     torch.manual_seed(0)
     dev = 'cuda'
     n, hw = 4, 12
@@ -62,7 +66,8 @@ def test_bn_dgrad_fused_matches(case, extra_use, monkeypatch):
     w = (torch.randn(cout, c, kk, kk, device=dev) * (2.0 / (kk * kk * c)) ** 0.5).bfloat16()
     s = torch.rand(c, device=dev) + 0.5
     b = torch.randn(c, device=dev) * 0.1
-    g = torch.randn(n, hw, hw, cout, device=dev).bfloat16()
+    st = 2 if kind == '3x3s2' else 1
+    g = torch.randn(n, hw // st, hw // st, cout, device=dev).bfloat16()
 
     def run(fuse):
         monkeypatch.setattr(K, '_BN_DGRAD_FUSE', fuse)
@@ -92,7 +97,7 @@ def test_bn_dgrad_fused_matches(case, extra_use, monkeypatch):
     sf, bf = s.clone().requires_grad_(), b.clone().requires_grad_()
     xn = xf.permute(0, 3, 1, 2)
     a = torch.relu(torch.nn.functional.batch_norm(xn, None, None, sf, bf, True, 0.1, 1e-5))
-    y = torch.nn.functional.conv2d(a, wf, None, 1, kk // 2).permute(0, 2, 3, 1)
+    y = torch.nn.functional.conv2d(a, wf, None, st, kk // 2).permute(0, 2, 3, 1)
     if extra_use:
         (y.sum() + (a * 0.5).sum()).backward()
     else:

@@ -112,3 +112,36 @@ def test_stem_conv_s2d(case):
     y.backward(g)
     yr.backward(g.float())
     torch.testing.assert_close(wh.grad.float(), wr.grad, atol=5e-2 * wr.grad.abs().max().item(), rtol=3e-2)
+
+
+def test_strided_dgrad_phase_index_cpu():
+    """The four stride-2 phase sub-filters use the 9 taps 1 + 2 + 2 + 4 times in total, and each
+    phase's taps are the ones with (phase + 1 - k) even."""
+    w = torch.zeros(64, 8, 3, 3)
+    idx, table = K._s2_phase_index(w)
+    assert [t[2] * t[3] for t in table] == [1, 2, 2, 4]
+    assert idx.numel() == 9 * 64 * 8
+    assert idx.unique().numel() == 9 * 64 * 8        # every (co, ci, ky, kx) exactly once
+
+
+S2_CASES = [(2, 8, 8, 64, 64), (2, 14, 10, 128, 128), (1, 6, 6, 256, 256), (3, 12, 12, 64, 128)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", S2_CASES)
+def test_strided_dgrad_phases(case, monkeypatch):
+    """3x3 / stride 2 / pad 1 input gradient through the four sub-pixel phase convs vs fp32."""
+    monkeypatch.setattr(K, '_STRIDED_DGRAD', True)
+    n, h, w_, cin, cout = case
+    torch.manual_seed(2)
+    x = torch.randn(n, h, w_, cin, device='cuda', dtype=torch.bfloat16)
+    w = (torch.randn(cout, cin, 3, 3, device='cuda') / (9 * cin) ** 0.5).to(torch.bfloat16)
+    ho, wo = h // 2, w_ // 2
+    dy = torch.randn(n, ho, wo, cout, device='cuda', dtype=torch.bfloat16)
+    assert K.strided_dgrad_ok(x, dy, w, 2, 1)
+    got = K._conv_dgrad_s2(dy, w, x.shape)
+    xr = x.float().permute(0, 3, 1, 2).requires_grad_()
+    torch.nn.functional.conv2d(xr, w.float(), None, 2, 1).backward(dy.float().permute(0, 3, 1, 2))
+    want = xr.grad.permute(0, 2, 3, 1)
+    err = (got.float() - want).abs().max().item()
+    assert err <= 2e-2 * want.abs().max().item() + 1e-2, err

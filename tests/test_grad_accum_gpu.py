@@ -135,3 +135,49 @@ def test_linear_bias_grad_colsum_kernel(rows, cols):
     b2 = torch.zeros(cols, device='cuda', dtype=torch.bfloat16, requires_grad=True)
     K.linear(x, w, b2).backward(dy)
     torch.testing.assert_close(b2.grad.float(), ref, atol=tol, rtol=1e-2)
+
+
+@pytest.mark.gpu
+def test_residual_bn_reduce_in_join_dgrad(monkeypatch):
+    """Two stacked bottlenecks: block A's output BN (+ residual + ReLU) gets its backward
+    reductions from block B's joined input gradient (conv1 dgrad with the pending sum added before
+    the ReLU mask, kBnG epilogue). Gradients match the unfused path."""
+    import paddle_ray_amd as paddle
+    from paddle_ray_amd.vision.models import resnet as R
+    paddle.seed(0)
+    ds = paddle.nn.Sequential(
+        paddle.nn.Conv2D(64, 256, 1, stride=1, bias_attr=False, data_format='NHWC'),
+        paddle.nn.BatchNorm2D(256, data_format='NHWC'))
+    net = paddle.nn.Sequential(R.BottleneckBlock(64, 64, stride=1, downsample=ds, data_format='NHWC'),
+                               R.BottleneckBlock(256, 64, stride=1, data_format='NHWC'))
+    net = paddle.amp.decorate(net, level='O2', dtype='bfloat16')
+    x0 = torch.randn(4, 16, 16, 64, device='cuda', dtype=torch.bfloat16)
+    bufs0 = [b._t.clone() for b in net.buffers()]
+    outs, used = [], []
+    seen = []
+    orig = K._BnHandoff.take
+
+    def spy(self, dy2):
+        r = orig(self, dy2)
+        seen.append(r is not None)
+        return r
+    monkeypatch.setattr(K._BnHandoff, 'take', spy)
+    for fuse in (True, False):
+        monkeypatch.setattr(K, '_BN_DGRAD_FUSE', fuse)
+        for b, b0 in zip(net.buffers(), bufs0):
+            b._t.copy_(b0)
+        for p in net.parameters():
+            p._t.grad = None
+        seen.clear()
+        x = paddle.Tensor(x0.clone().requires_grad_())
+        y = net(x)
+        g = torch.randn(y.shape, device='cuda', generator=torch.Generator('cuda').manual_seed(1)).to(y._t.dtype)
+        y._t.backward(g)
+        used.append(sum(seen))
+        outs.append((x._t.grad.float().clone(), [p._t.grad.float().clone() for p in net.parameters()]))
+    # fused: block A's bn3, and both blocks' bn1 / bn2 (their conv consumers' dgrads)
+    assert used[0] >= 5 and used[1] == 0, used
+    (gx1, gp1), (gx2, gp2) = outs
+    torch.testing.assert_close(gx1, gx2, rtol=3e-2, atol=3e-2)
+    for a, b in zip(gp1, gp2):
+        torch.testing.assert_close(a, b, rtol=5e-2, atol=5e-2)
