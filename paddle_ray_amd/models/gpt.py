@@ -112,8 +112,15 @@ class GPTAttention(nn.Layer):
         self.attn_dropout = cfg.attention_dropout
         self.mp = cfg.mp_degree
 
-    def _core(self, x):
-        qkv = _u(self.qkv_proj(x))
+    def _core(self, x, pair=None):
+        if pair is not None:
+            # QKV projection as a paired Linear: its backward also issues the output
+            # projection's weight gradient, both in one grouped launch (ops/fused.py WgradPair)
+            qp = self.qkv_proj
+            qkv = K.linear(_u(x), qp.weight._t, qp.bias._t if qp.bias is not None else None, pair=pair,
+                           w_dep=self.out_proj.weight._t)
+        else:
+            qkv = _u(self.qkv_proj(x))
         B, S = qkv.shape[0], qkv.shape[1]
         qkv = qkv.view(B, S, 3, self.num_heads, self.head_dim)
         if self.attn_dropout > 0 and self.training:
@@ -127,7 +134,10 @@ class GPTAttention(nn.Layer):
     def forward_nobias(self, x):
         """attention output projection WITHOUT its bias (fused into the next kernel). Under
         TP the row-parallel partial sums are all-reduced here (bias added after, once)."""
-        a = K.linear(self._core(x), self.out_proj.weight._t)
+        pair = None
+        if self.mp == 1 and _u(x).is_cuda and self.training:
+            pair = K.WgradPair()
+        a = K.linear(self._core(x, pair), self.out_proj.weight._t, pair=pair)
         if self.mp > 1:
             a = _mp()._AllReduce.apply(a, self.out_proj.model_parallel_group)
         return Tensor(a)

@@ -77,6 +77,8 @@ int pra_gemm_bias_act(const void*, const void*, const void*, void*, void*, int, 
 int pra_gemm_lds(int, const void*, const void*, const void*, void*, void*, float*, int, int, int, int, int, int, int,
                  int, int, int, int, float*, hipStream_t);
 int pra_gemm_lds_splits(int, int, int);
+int pra_gemm_tn_grouped2(const void*, const void*, void*, int, int, int, int, const void*, const void*, void*, int, int,
+                         int, int, int, int, int, hipStream_t);
 void pra_gemm_set_w4(int);
 void pra_gemm_set_pts(int);
 int pra_gemm_get_pts();
@@ -178,6 +180,13 @@ PYBIND11_MODULE(_pra_hip, m) {
                      splits, F(ws), S(s)) != 0)
       throw std::invalid_argument("gemm_lds: unsupported shape/stride/dtype");
     check_launch("gemm_lds");
+  });
+  m.def("gemm_tn_grouped2", [](P a1, P b1, P c1, int n1, int lda1, int ldb1, int ldc1, P a2, P b2, P c2, int n2,
+                               int lda2, int ldb2, int ldc2, int M, int K, int beta, P s) {
+    if (pra_gemm_tn_grouped2(CV(a1), CV(b1), V(c1), n1, lda1, ldb1, ldc1, CV(a2), CV(b2), V(c2), n2, lda2, ldb2, ldc2,
+                             M, K, beta, S(s)) != 0)
+      throw std::invalid_argument("gemm_tn_grouped2: unsupported shape");
+    check_launch("gemm_tn_grouped2");
   });
   m.def("colsum_partials", [](P part, P out, int P_, int N, int dt, P s) {
     if (pra_colsum_partials(CF(part), V(out), P_, N, dt, S(s)) != 0)

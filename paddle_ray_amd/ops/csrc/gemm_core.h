@@ -411,6 +411,17 @@ __device__ __forceinline__ typename V8<T>::type frag(const char* img, int r0, in
   }
 }
 
+// Second problem of a two-problem grouped launch (same M, K and layout; workgroups with a
+// remapped id >= tiles1 run it): two weight gradients whose tile counts add up to one full wave
+// of the chip (GPT-1.3B: qkv 192 + out-projection 64 = 256 tiles, one round of the full K loop
+// instead of two split-K passes and their reductions).
+struct GemmG2 {
+  const uint16_t* A = nullptr;
+  const uint16_t* B = nullptr;
+  uint16_t* C = nullptr;
+  int N = 0, lda = 0, ldb = 0, ldc = 0, tiles1 = 0;
+};
+
 template <typename T, typename CF, bool AK, bool BK, int E, bool BETA, bool SPLIT, bool CONV = false,
           int DPSX = 0, bool CONVW = false>
 __global__ __launch_bounds__(CF::NT, 1) void gemm_lds_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
@@ -420,7 +431,8 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_lds_kernel(const uint16_t* __r
                                                           int splits, float* __restrict__ ws, ConvGeom cg = {},
                                                           float* __restrict__ colsq = nullptr,
                                                           const float* __restrict__ cshift = nullptr,
-                                                          const uint8_t* __restrict__ mbits = nullptr) {
+                                                          const uint8_t* __restrict__ mbits = nullptr,
+                                                          GemmG2 g2 = {}) {
   constexpr int NT = CF::NT, TI = CF::TI, TJ = CF::TJ, NDA = CF::NDA, NDB = CF::NDB, WC = CF::WC;
   constexpr int BM = CF::BM, BN = CF::BN, IMGA = CF::IMGA, SLOT = CF::SLOT;
   constexpr int RW = TI * 16, CW = TJ * 16;  // rows / columns per wave
@@ -439,13 +451,25 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_lds_kernel(const uint16_t* __r
   PRA_STAMP(6, (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4));
   PRA_STAMP(7, (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 20));
 
-  const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;
   const int nb = gridDim.x;
   int pid = blockIdx.x;
   {  // contiguous tile run per XCD (bijective for any grid size)
     const int q = nb >> 3, r = nb & 7, xcd = pid & 7;
     pid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (pid >> 3);
   }
+  if constexpr (!SPLIT && !CONV && !CONVW) {
+    if (g2.tiles1 > 0 && pid >= g2.tiles1) {  // (wave-uniform: a whole workgroup switches)
+      pid -= g2.tiles1;
+      A = g2.A;
+      B = g2.B;
+      C = g2.C;
+      N = g2.N;
+      lda = g2.lda;
+      ldb = g2.ldb;
+      ldc = g2.ldc;
+    }
+  }
+  const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;
   // split-K: the splits of one tile are adjacent ids (same XCD); each covers a K range and
   // writes an fp32 partial tile that splitk_reduce_k combines
   const int split = SPLIT ? pid % splits : 0;

@@ -2192,6 +2192,32 @@ def _acc_grad_ok(g, w, dt):
             and g.dtype == dt and g.is_contiguous())
 
 
+# Weight-gradient pairing of two Linears of one block (GPT attention: the QKV projection and the
+# output projection, whose weight gradients share M = hidden and K = tokens): the output
+# projection's backward (which runs first) leaves its xᵀ·dy job in the pair; the QKV
+# projection's backward runs both as ONE launch of the two-problem grouped kernel
+# (pra_gemm_tn_grouped2) when their tile counts fill one wave of the chip (GPT-1.3B: 192 + 64 =
+# 256 tiles over the full K, instead of a split-K pass + reduction each). The QKV Linear takes
+# the output-projection weight as an extra (unused) input, so that weight's AccumulateGrad --
+# and the post-accumulate hooks the DP / sharding reducers count on -- fires only after the
+# deferred accumulation has been issued.
+_WGRAD_PAIR = __import__('os').environ.get('PRA_WGRAD_PAIR', '1') == '1'
+
+
+class WgradPair:
+    __slots__ = ('job', 'used')
+
+    def __init__(self):
+        self.job = None
+        self.used = 0
+
+
+def _pair_fill(M, N1, N2):
+    t = ((M + 255) // 256)
+    tiles = t * ((N1 + 255) // 256) + t * ((N2 + 255) // 256)
+    return 224 <= tiles <= 256
+
+
 class LinearFn(torch.autograd.Function):
     """y = x @ W (+ b) with paddle's [in, out] weight, all three GEMMs on the MFMA kernel:
     forward x·W with the bias in its epilogue; dx = dy·Wᵀ; dW = xᵀ·dy accumulated straight into
@@ -2201,12 +2227,13 @@ class LinearFn(torch.autograd.Function):
     hooks that trigger the bucketed all-reduce / reduce-scatter."""
 
     @staticmethod
-    def forward(ctx, x, w, b):
+    def forward(ctx, x, w, b, pair=None, w_dep=None):
         x2 = x.reshape(-1, x.shape[-1])
         y = gemm(GEMM_FWD, x2, w, bias=b)
         ctx.save_for_backward(x)
         ctx.w, ctx.b = w, b
         ctx.has_b = b is not None
+        ctx.pair, ctx.collector = pair, w_dep is not None
         return y.view(*x.shape[:-1], w.shape[-1])
 
     @staticmethod
@@ -2222,16 +2249,45 @@ class LinearFn(torch.autograd.Function):
             acc = _dx_acc(ctx, x)
             dx = gemm(GEMM_NT, dy2, w, out=acc, beta=1 if acc is not None else 0).view(x.shape)
         dw = None
+        pair = ctx.pair
+        job = None
+        if pair is not None and ctx.collector:
+            job, pair.job = pair.job, None
         if ctx.needs_input_grad[1]:
             g = w.grad if w.is_leaf else None
             if _acc_grad_ok(g, w, dy2.dtype):
-                # returning None still runs W's AccumulateGrad node, which fires its
-                # post-accumulate hooks after this in-place accumulation
-                gemm(GEMM_TN, x2, dy2, out=g, beta=1)
+                if pair is not None and not ctx.collector and pair.job is None:
+                    pair.job = (x2, dy2, g)      # the collector's backward runs it (grouped)
+                elif job is not None and _grouped_wgrad(job, (x2, dy2, g)):
+                    job = None
+                    pair.used += 1
+                else:
+                    # returning None still runs W's AccumulateGrad node, which fires its
+                    # post-accumulate hooks after this in-place accumulation
+                    gemm(GEMM_TN, x2, dy2, out=g, beta=1)
             else:
                 dw = gemm(GEMM_TN, x2, dy2)
+        if job is not None:   # a deferred job that could not be grouped
+            gemm(GEMM_TN, job[0], job[1], out=job[2], beta=1)
         db = bias_grad(dy2, ctx.b) if ctx.has_b and ctx.needs_input_grad[2] else None
-        return dx, dw, db
+        return dx, dw, db, None, None
+
+
+def _grouped_wgrad(j1, j2):
+    """g (+)= xᵀ·dy for two jobs in one grouped launch; False (nothing launched) if they do not
+    share M / K or do not fill one wave of the chip."""
+    (x1, d1, g1), (x2, d2, g2) = j1, j2
+    M, K = x1.shape[1], x1.shape[0]
+    if not (x2.shape == (K, M) and d1.shape[0] == K and d2.shape[0] == K and x1.dtype == torch.bfloat16
+            and all(t.dtype == torch.bfloat16 and t.is_contiguous() for t in (x1, d1, g1, x2, d2, g2))
+            and _pair_fill(M, d1.shape[1], d2.shape[1]) and K % 64 == 0 and M % 8 == 0
+            and d1.shape[1] % 8 == 0 and d2.shape[1] % 8 == 0 and R.select_backend(x1, 'gemm') == 'hip'
+            and _GEMM_MODE != 'blas'):
+        return False
+    _native.lib().gemm_tn_grouped2(x1.data_ptr(), d1.data_ptr(), g1.data_ptr(), d1.shape[1], M, d1.shape[1],
+                                   d1.shape[1], x2.data_ptr(), d2.data_ptr(), g2.data_ptr(), d2.shape[1], M,
+                                   d2.shape[1], d2.shape[1], M, K, 1, _stream())
+    return True
 
 
 def _dx_acc(ctx, x):
@@ -2277,8 +2333,10 @@ def _no_autocast_change(x, w):
     return x.dtype == w.dtype == torch.get_autocast_dtype(dev)
 
 
-def linear(x, w, b=None):
-    """[.., in] @ [in, out] (+ b) with fused dW accumulation (see LinearFn)."""
+def linear(x, w, b=None, pair=None, w_dep=None):
+    """[.., in] @ [in, out] (+ b) with fused dW accumulation (see LinearFn). pair / w_dep: the
+    weight-gradient pairing of two Linears (WgradPair; w_dep on the one whose backward runs
+    last: the other Linear's weight)."""
     if b is not None and b.dtype != x.dtype and torch.is_autocast_enabled(x.device.type):
         b = b.to(x.dtype)
     if torch.is_grad_enabled() and (x.requires_grad or w.requires_grad or (b is not None and b.requires_grad)) \
@@ -2286,6 +2344,8 @@ def linear(x, w, b=None):
         # any operand that needs a gradient goes through the autograd Function (a frozen
         # weight with a trainable input, or a non-leaf weight, included: the raw GEMM below
         # records no graph)
+        if pair is not None and _WGRAD_PAIR:
+            return LinearFn.apply(x, w, b, pair, w_dep)
         return LinearFn.apply(x, w, b)
     x2 = x.reshape(-1, x.shape[-1])
     if x2.is_cuda and x.dtype == w.dtype and _no_autocast_change(x, w):
