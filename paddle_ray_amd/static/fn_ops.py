@@ -48,7 +48,7 @@ def _op(name, fn_cls, eager, pred=None):
 
 
 # -- linear --------------------------------------------------------------------------------------
-def _lin_ok(x, w, b=None):
+def _lin_ok(x, w, b=None, *_):
     return isinstance(w, torch.Tensor) and w.requires_grad and w.is_leaf and x.dtype == w.dtype and \
         K._no_autocast_change(x, w)
 
