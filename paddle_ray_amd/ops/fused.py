@@ -98,9 +98,12 @@ def _adl_ok(cols):
     return cols % 8 == 0 and cols <= 4096
 
 
+_ADL_NBLK = int(__import__('os').environ.get('PRA_ADL_NBLK', '768'))
+
+
 def _adl_nblk(rows):
     # 768 workgroups of 4 waves = 3 waves per SIMD on 256 CUs (the two-pass backward's occupancy)
-    return max(1, min(768, (rows + 7) // 8))
+    return max(1, min(_ADL_NBLK, (rows + 7) // 8))
 
 
 @R.register_kernel('layer_norm_fwd', 'hip', dtypes=_FLOATS)
@@ -2355,6 +2358,31 @@ def linear(x, w, b=None, pair=None, w_dep=None):
     return y.view(*x.shape[:-1], w.shape[-1])
 
 
+# Tile-count tail of a long-K weight gradient: a TN product with a few tiles past a multiple of
+# 256 (GPT's tied LM head: 50304 x 2048 -> 1576 tiles = 6 full waves + 40) runs its last tile
+# rows as a separate split-K launch, so the 40 stragglers do not hold the chip for a whole
+# seventh wave of the full K loop. PRA_GEMM_TN_TAIL=0 turns it off.
+_TN_TAIL = __import__('os').environ.get('PRA_GEMM_TN_TAIL', '1') == '1'
+
+
+def gemm_tn_balanced(a, b, out=None, beta=0):
+    """gemm(GEMM_TN, a, b, out, beta) with the tile-count tail split off (see _TN_TAIL)."""
+    K, M = a.shape
+    N = b.shape[1]
+    tm, tn = (M + 255) // 256, (N + 255) // 256
+    tiles = tm * tn
+    if (_TN_TAIL and a.is_cuda and tiles > 256 and 0 < tiles % 256 <= 64 and 256 % tn == 0
+            and R.select_backend(a, 'gemm') == 'hip'):
+        rows = (tiles // 256) * (256 // tn) * 256
+        if 0 < rows < M and (M - rows) % 8 == 0:
+            if out is None:
+                out = torch.empty((M, N), device=a.device, dtype=a.dtype)
+            gemm(GEMM_TN, a[:, :rows], b, out=out[:rows], beta=beta)
+            gemm(GEMM_TN, a[:, rows:], b, out=out[rows:], beta=beta)
+            return out
+    return gemm(GEMM_TN, a, b, out=out, beta=beta)
+
+
 class LinearNTFn(torch.autograd.Function):
     """y = x @ W^T for a [out, in] weight (the tied LM head: W is the [vocab, hidden] word
     embedding). dx = dy·W and dW += dyᵀ·x (beta=1 into W's grad) on the MFMA kernel."""
@@ -2376,9 +2404,9 @@ class LinearNTFn(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             g = w.grad if w.is_leaf else None
             if _acc_grad_ok(g, w, dy.dtype):
-                gemm(GEMM_TN, dy, x, out=g, beta=1)
+                gemm_tn_balanced(dy, x, out=g, beta=1)
             else:
-                dw = gemm(GEMM_TN, dy, x)
+                dw = gemm_tn_balanced(dy, x)
         return dx, dw
 
 

@@ -312,3 +312,19 @@ def test_paired_wgrad_grouped_launch(hidden, tokens):
     for got, want in ((wq.grad, wqf.grad), (wo.grad, wof.grad), (x.grad, xf.grad)):
         err = (got.float() - want).abs().max().item() / (want.abs().max().item() + 1e-6)
         assert err < 3e-2, err
+
+
+@pytest.mark.parametrize('beta', [0, 1])
+def test_tn_tail_split(beta):
+    """TN weight gradient with a 40-tile tail past 6 full waves (LM-head shape, K shortened):
+    the tail rows run as a separate split-K launch; result matches fp32."""
+    M, N, KD = 50304, 2048, 1024
+    g = torch.Generator(device='cuda').manual_seed(5)
+    a = ((torch.rand(KD, M, device='cuda', generator=g) * 2 - 1) * 0.5).to(torch.bfloat16)
+    b = ((torch.rand(KD, N, device='cuda', generator=g) * 2 - 1) * 0.5).to(torch.bfloat16)
+    c0 = (torch.rand(M, N, device='cuda', generator=g) - 0.5).to(torch.bfloat16)
+    out = c0.clone()
+    K.gemm_tn_balanced(a, b, out=out, beta=beta)
+    want = a.float().t() @ b.float() + (c0.float() if beta else 0)
+    err = (out.float() - want).abs().max().item()
+    assert err < 2e-2 * want.abs().max().item(), err
