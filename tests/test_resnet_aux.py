@@ -63,3 +63,31 @@ def test_global_avg_pool_nhwc_backward():
     yf.backward(g.float())
     torch.testing.assert_close(y.float(), yf, atol=2e-2, rtol=2e-2)
     torch.testing.assert_close(x.grad.float(), xf.grad, atol=1e-3, rtol=1e-2)
+
+
+def test_wgrad_pair_defers_and_hooks_fire_after_cpu():
+    """WgradPair on the host (no grouped kernel there): the output projection's weight gradient
+    is deferred to the QKV Linear's backward, and its post-accumulate hook fires only after the
+    deferred accumulation (the QKV Linear holds that weight as a dependency)."""
+    torch.manual_seed(0)
+    h, t = 16, 12
+    x = torch.randn(t, h, requires_grad=True)
+    wq = (torch.randn(h, 3 * h) * 0.1).requires_grad_()
+    wo = (torch.randn(h, h) * 0.1).requires_grad_()
+    for p in (wq, wo):
+        p.grad = torch.zeros_like(p)
+    seen = []
+    wo.register_post_accumulate_grad_hook(lambda p: seen.append(p.grad.clone()))
+    pair = K.WgradPair()
+    qkv = K.linear(x, wq, None, pair=pair, w_dep=wo)
+    a = qkv[:, :h] * qkv[:, h:2 * h] + qkv[:, 2 * h:]
+    y = K.linear(a, wo, pair=pair)
+    g = torch.randn_like(y)
+    y.backward(g)
+    assert pair.job is None and len(seen) == 1
+    xr, wqr, wor = (v.detach().clone().requires_grad_() for v in (x, wq, wo))
+    qr = xr @ wqr
+    ((qr[:, :h] * qr[:, h:2 * h] + qr[:, 2 * h:]) @ wor).backward(g)
+    torch.testing.assert_close(seen[0], wor.grad, rtol=1e-5, atol=1e-5)   # final value at hook time
+    torch.testing.assert_close(wo.grad, wor.grad, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(wq.grad, wqr.grad, rtol=1e-5, atol=1e-5)
