@@ -342,3 +342,41 @@ def test_transformer_encoder_mask_dropout_on_flash_ext():
     assert np.abs(yv - yrv).max() / np.abs(yrv).max() < 3e-2
     gx, gxr = xg.grad.astype('float32').numpy(), xc.grad.numpy()
     assert np.abs(gx - gxr).max() / np.abs(gxr).max() < 5e-2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('D', [80, 96])
+@pytest.mark.parametrize('causal', [False, True])
+def test_flash_ext_other_head_dims(D, causal):
+    """Head dims outside the flash kernel (80, 96) take torch's memory-efficient SDPA: values and
+    gradients match an fp32 reference, and no [B, H, S, S] fp32 score tensor is kept (the peak
+    allocation stays far below one)."""
+    torch.manual_seed(0)
+    B, S, H = 2, 1024, 4
+    q, k, v = (torch.randn(B, S, H, D, device='cuda', dtype=torch.bfloat16).requires_grad_() for _ in range(3))
+    mask = torch.zeros(B, 1, 1, S, device='cuda', dtype=torch.bfloat16)
+    mask[:, :, :, S - 64:] = float('-inf')            # key padding
+    before = K.R._STATS[('flash_attn_ext', 'sdpa')]
+    import paddle_ray_amd.device.cuda as dc    # (works with the native allocator too)
+    torch.cuda.synchronize()
+    dc.reset_max_memory_allocated()
+    base = dc.memory_allocated()
+    o = K.flash_attention_ext(q, k, v, causal=causal, attn_mask=mask)
+    g = torch.randn_like(o)
+    o.backward(g)
+    torch.cuda.synchronize()
+    peak = dc.max_memory_allocated() - base
+    assert K.R._STATS[('flash_attn_ext', 'sdpa')] == before + 1
+    scores_fp32 = B * H * S * S * 4
+    print(f"D={D} causal={causal}: peak {peak / 2**20:.1f} MiB vs fp32 scores {scores_fp32 / 2**20:.1f} MiB")
+    assert peak < scores_fp32 / 2, (peak, scores_fp32)   # measured 6-12 MiB vs 32 MiB
+    qf, kf, vf = (t.detach().float().requires_grad_() for t in (q, k, v))
+    s = torch.einsum('bqhd,bkhd->bhqk', qf, kf) / math.sqrt(D) + mask.float()
+    if causal:
+        s = s.masked_fill(torch.ones(S, S, dtype=torch.bool, device='cuda').triu(1), float('-inf'))
+    of = torch.einsum('bhqk,bkhd->bqhd', s.softmax(-1), vf)
+    of.backward(g.float())
+    torch.testing.assert_close(o.float(), of, atol=2e-2, rtol=2e-2)
+    for a, b in ((q.grad, qf.grad), (k.grad, kf.grad), (v.grad, vf.grad)):
+        err = (a.float() - b).abs().max().item() / (b.abs().max().item() + 1e-6)
+        assert err < 3e-2, err
