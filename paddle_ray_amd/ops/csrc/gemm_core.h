@@ -118,6 +118,15 @@ __device__ __forceinline__ float zfac(float z) {
 
 constexpr int BM = 256, BN = 256, BKT = 64;  // the GEMM tile (conv configs below narrow BN)
 
+// Lanes per output quad of splitk_reduce_k: enough to fill the chip when the output is small and
+// the split count large.
+inline int splitk_groups(int64_t quads, int splits) {
+  static const int gmax = getenv("PRA_SPLITK_GMAX") ? atoi(getenv("PRA_SPLITK_GMAX")) : 64;   // A/B knob
+  int G = 1;
+  while (2 * G <= gmax && 2 * G <= splits && quads * G < 262144) G *= 2;
+  return G;
+}
+
 // Phase stamps for diagnostic builds only (gemm_probe.hip defines PRA_GEMM_STAMPS 1; the
 // library's kernels compile them out): lane 0 of wave 0 of each workgroup writes 8 words into
 // the (otherwise unused) ws buffer of a non-split launch: shader clock at entry / loop start /
@@ -1026,18 +1035,48 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_lds_kernel(const uint16_t* __r
   PRA_STAMP(5, __builtin_amdgcn_s_memrealtime());
 }
 
-// split-K combine: C[m][n..n+3] = epi(sum_s ws[s][m][n..n+3] + bias) (+ C if BETA)
+// split-K combine: C[m][n..n+3] = epi(sum_s ws[s][m][n..n+3] + bias) (+ C if BETA).
+// G (power of two, <= 256) lanes per 4-column quad: lane g sums splits g, g+G, ... (4 loads in
+// flight), then the G partials are added in lane order through LDS. G > 1 for small outputs
+// with many splits (a ResNet 1x1 weight gradient: 64 x 256 outputs, 256 splits), which with one
+// lane per quad ran 4-32 workgroups of 256 dependent loads each (splitk_groups picks G).
+// G = 1 keeps the plain split order.
 template <typename T, int E, bool BETA>
-__global__ void splitk_reduce_k(const float* __restrict__ ws, int splits, const uint16_t* __restrict__ bias,
-                                uint16_t* __restrict__ C, uint16_t* __restrict__ Z, int M, int N, int ldc, int ldz) {
-  const int64_t idx = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
-  if (idx >= (int64_t)M * N) return;
-  const int m = (int)(idx / N), n = (int)(idx % N);
-  float4 a = *reinterpret_cast<const float4*>(ws + idx);
-  for (int s = 1; s < splits; ++s) {
-    const float4 b = *reinterpret_cast<const float4*>(ws + (int64_t)s * M * N + idx);
-    a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+__global__ void __launch_bounds__(256) splitk_reduce_k(const float* __restrict__ ws, int splits,
+                                                       const uint16_t* __restrict__ bias, uint16_t* __restrict__ C,
+                                                       uint16_t* __restrict__ Z, int M, int N, int ldc, int ldz,
+                                                       int G = 1) {
+  __shared__ float4 red[256];
+  const int g = threadIdx.x & (G - 1);
+  const int64_t MN = (int64_t)M * N;
+  const int64_t idx = (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / G) * 4;
+  const bool valid = idx < MN;
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (valid) {
+    int s = g;
+    for (; s + 3 * G < splits; s += 4 * G) {
+      float4 b[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) b[u] = *reinterpret_cast<const float4*>(ws + (int64_t)(s + u * G) * MN + idx);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) { a.x += b[u].x; a.y += b[u].y; a.z += b[u].z; a.w += b[u].w; }
+    }
+    for (; s < splits; s += G) {
+      const float4 b = *reinterpret_cast<const float4*>(ws + (int64_t)s * MN + idx);
+      a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+    }
   }
+  if (G > 1) {
+    red[threadIdx.x] = a;
+    __syncthreads();
+    if (g != 0) return;   // (no barrier after this point)
+    for (int j = 1; j < G; ++j) {
+      const float4 b = red[threadIdx.x + j];
+      a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+    }
+  }
+  if (!valid) return;
+  const int m = (int)(idx / N), n = (int)(idx % N);
   float v[4] = {a.x, a.y, a.z, a.w};
   if (bias) {
     const uint2 bb = *reinterpret_cast<const uint2*>(bias + n);

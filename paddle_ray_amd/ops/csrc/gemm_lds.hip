@@ -125,9 +125,10 @@ void launch_e(const void* A, const void* B, const void* bias, void* C, void* Z, 
       gemm_lds_kernel<T, W8, AK, BK, kNone, false, true><<<tiles * splits, W8::NT, 0, s>>>(
           pa, pb, nullptr, nullptr, nullptr, nullptr, M, N, K, lda, ldb, ldc, ldz, splits, ws);
     const int64_t quads = (int64_t)M * N / 4;
-    const int blocks = (int)((quads + 255) / 256);
-    if (beta) splitk_reduce_k<T, E, true><<<blocks, 256, 0, s>>>(ws, splits, pbias, pc, pz, M, N, ldc, ldz);
-    else splitk_reduce_k<T, E, false><<<blocks, 256, 0, s>>>(ws, splits, pbias, pc, pz, M, N, ldc, ldz);
+    const int G = splitk_groups(quads, splits);
+    const int blocks = (int)((quads * G + 255) / 256);
+    if (beta) splitk_reduce_k<T, E, true><<<blocks, 256, 0, s>>>(ws, splits, pbias, pc, pz, M, N, ldc, ldz, G);
+    else splitk_reduce_k<T, E, false><<<blocks, 256, 0, s>>>(ws, splits, pbias, pc, pz, M, N, ldc, ldz, G);
     return;
   }
   // (measured: front-loading the step's DMA into the first 2 / 4 segments of the half instead of
@@ -210,7 +211,9 @@ void launch_conv_cfg(const void* xpad, const void* W, const void* bias, void* Y,
       gemm_lds_kernel<T, CF, true, true, kNone, false, true, true><<<tiles * splits, CF::NT, 0, s>>>(
           px, pw, nullptr, nullptr, nullptr, nullptr, M, N, K, 0, K, N, N, splits, ws, cg);
       const int64_t quads = (int64_t)M * N / 4;
-      splitk_reduce_k<T, E, false><<<(int)((quads + 255) / 256), 256, 0, s>>>(ws, splits, pb, py, nullptr, M, N, N, N);
+      const int G = splitk_groups(quads, splits);
+      splitk_reduce_k<T, E, false><<<(int)((quads * G + 255) / 256), 256, 0, s>>>(ws, splits, pb, py, nullptr, M, N,
+                                                                                 N, N, G);
       return;
     }
   }
@@ -244,8 +247,9 @@ void launch_conv_wgrad_cfg(const void* dy, const void* x, void* dW, int Mpix, in
     gemm_lds_kernel<T, CF, false, false, kNone, false, true, false, 0, true><<<tiles * splits, CF::NT, 0, s>>>(
         pdy, px, nullptr, nullptr, nullptr, nullptr, Cout, Nk, Mpix, Cout, 0, Nk, Nk, splits, ws, cg);
     const int64_t quads = (int64_t)Cout * Nk / 4;
-    splitk_reduce_k<T, kNone, false><<<(int)((quads + 255) / 256), 256, 0, s>>>(ws, splits, nullptr, pw, nullptr, Cout,
-                                                                               Nk, Nk, Nk);
+    const int G = splitk_groups(quads, splits);
+    splitk_reduce_k<T, kNone, false><<<(int)((quads * G + 255) / 256), 256, 0, s>>>(ws, splits, nullptr, pw, nullptr,
+                                                                                   Cout, Nk, Nk, Nk, G);
     return;
   }
   gemm_lds_kernel<T, CF, false, false, kNone, false, false, false, 0, true><<<tiles, CF::NT, 0, s>>>(
