@@ -380,3 +380,19 @@ def test_flash_ext_other_head_dims(D, causal):
     for a, b in ((q.grad, qf.grad), (k.grad, kf.grad), (v.grad, vf.grad)):
         err = (a.float() - b).abs().max().item() / (b.abs().max().item() + 1e-6)
         assert err < 3e-2, err
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('shape', [(16, 1024, 16, 128), (3, 77, 5, 64), (2, 512, 12, 64)])
+def test_attn_delta_kernel(shape):
+    """delta[b, h, s] = sum_d dO * O (the flash backward's row term) vs fp32."""
+    from paddle_ray_amd.ops import _native
+    B, S, H, D = shape
+    torch.manual_seed(0)
+    o = torch.randn(B, S, H, D, device='cuda').bfloat16()
+    do = torch.randn(B, S, H, D, device='cuda').bfloat16()
+    delta = torch.full((B, H, S), float('nan'), device='cuda')
+    _native.lib().flash_bwd_pre(o.data_ptr(), do.data_ptr(), delta.data_ptr(), B, H, S, D, 2,
+                                torch.cuda.current_stream().cuda_stream)
+    want = (o.float() * do.float()).sum(-1).permute(0, 2, 1)
+    torch.testing.assert_close(delta, want, atol=1e-3, rtol=1e-3)
