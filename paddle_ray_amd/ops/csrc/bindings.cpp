@@ -72,6 +72,7 @@ int pra_max_pool_fwd(const void*, void*, uint8_t*, int, int, int, int, int, int,
                      hipStream_t);
 int pra_max_pool_bwd(const void*, const uint8_t*, void*, int, int, int, int, int, int, int, int, int, int, int, int,
                      int, hipStream_t);
+int pra_wflip_t(const void*, void*, int, int, int, int, int, hipStream_t);
 int pra_gemm_bias_act(const void*, const void*, const void*, void*, void*, int, int, int, int, int, int, int, int,
                       hipStream_t);
 int pra_gemm_lds(int, const void*, const void*, const void*, void*, void*, float*, int, int, int, int, int, int, int,
@@ -404,6 +405,11 @@ PYBIND11_MODULE(_pra_hip, m) {
                          pw, dt, S(s)) != 0)
       throw std::invalid_argument("max_pool_bwd: unsupported geometry");
     check_launch("max_pool_bwd");
+  });
+  m.def("wflip_t", [](P src, P dst, int o, int c, int kh, int kw, int dt, P s) {
+    if (pra_wflip_t(CV(src), V(dst), o, c, kh, kw, dt, S(s)) != 0)
+      throw std::invalid_argument("wflip_t: unsupported shape");
+    check_launch("wflip_t");
   });
   m.def("embedding_fwd", [](P ids, P w, P out, int64_t n, int D, int64_t V, int64_t pad, int dt, P s) {
     if (pra_embedding_fwd(I64(ids), CV(w), V(out), n, D, V, pad, dt, S(s)) != 0)

@@ -1940,6 +1940,16 @@ def _conv_dgrad_s2(dy, w, xshape, rec=None):
     return dx
 
 
+def _flip_t(w):
+    """[Cin, kh*kw*Cout] filter of the stride-1 input gradient: w flipped in both taps, IHWO."""
+    cout, cin, kh, kw = w.shape
+    if w.is_cuda and w.is_contiguous() and w.dtype in _HALF:
+        wf = torch.empty((cin, kh * kw * cout), device=w.device, dtype=w.dtype)
+        _native.lib().wflip_t(w.data_ptr(), wf.data_ptr(), cout, cin, kh, kw, _dt(w), _stream())
+        return wf
+    return w.flip(2, 3).permute(1, 2, 3, 0).reshape(cin, kh * kw * cout).contiguous()
+
+
 class ConvKxKFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, bias, stride, pad):
@@ -1962,7 +1972,7 @@ class ConvKxKFn(torch.autograd.Function):
                    and kh - 1 - pad >= 0 and kw - 1 - pad >= 0 and kh == kw)
         dx = dw = db = None
         if ours_dx:
-            wf = w.flip(2, 3).permute(1, 2, 3, 0).reshape(cin, kh * kw * cout).contiguous()
+            wf = _flip_t(w)
             rec = getattr(ctx, 'bn', None)
             if _bn_dgrad_ok(rec, x.shape[0] * x.shape[1] * x.shape[2], cin, kh * kw * cout):
                 dx = _bn_dgrad(rec, dy, wf, kh, kw, kh - 1 - pad)
@@ -1977,7 +1987,14 @@ class ConvKxKFn(torch.autograd.Function):
         need_lib_dx = ctx.needs_input_grad[0] and not ours_dx
         ours_dw = ctx.needs_input_grad[1] and _conv_wgrad_ok(x, dy, cout)
         if ours_dw:
-            dw = _conv_wgrad_lds(dy, x, kh, kw, stride, pad).permute(0, 3, 1, 2).contiguous()
+            dwk = _conv_wgrad_lds(dy, x, kh, kw, stride, pad)
+            g = w.grad
+            if _acc_grad_ok(g, w, dwk.dtype):
+                # accumulated straight from the OHWI product (no OIHW copy before the add); the
+                # AccumulateGrad node still fires its post-accumulate hooks
+                g.add_(dwk.permute(0, 3, 1, 2))
+            else:
+                dw = dwk.permute(0, 3, 1, 2).contiguous()
         need_lib_dw = ctx.needs_input_grad[1] and not ours_dw
         if need_lib_dx or need_lib_dw:
             # NCHW-shaped views of the channels-last tensors: MIOpen runs its NHWC kernels

@@ -45,6 +45,18 @@ def test_conv_kxk_fwd_bwd(case, dtype):
         err = (got.float() - ref).abs().max().item()
         scale = ref.abs().max().item() + 1e-6
         assert err <= 2e-2 * scale + 2e-2, (err, scale)
+    # second pass: the weight gradient is accumulated in place into the existing w.grad
+    K.conv_kxk_nhwc(xh, wh, bh, s, p).backward(dy.to(dtype))
+    err = (wh.grad.float() - 2 * wr.grad).abs().max().item()
+    assert err <= 4e-2 * wr.grad.abs().max().item() + 4e-2, err
+
+
+@pytest.mark.gpu
+def test_flip_t_filter():
+    torch.manual_seed(0)
+    w = torch.randn(96, 64, 3, 3, device='cuda', dtype=torch.bfloat16)
+    ref = w.flip(2, 3).permute(1, 2, 3, 0).reshape(64, 9 * 96)
+    assert torch.equal(K._flip_t(w), ref)
 
 
 @pytest.mark.gpu
