@@ -26,5 +26,6 @@ from . import io  # noqa
 from . import watchdog  # noqa: E402
 from . import models  # noqa: E402
 from . import utils  # noqa: E402
+from . import rpc  # noqa: E402
 from . import auto_parallel  # noqa: E402
 from .auto_parallel import ProcessMesh, shard_tensor, shard_op, reshard, Strategy, Engine  # noqa: E402
