@@ -7,6 +7,7 @@ the active mode (PipelineParallel / TensorParallel / sharded / DataParallel);
 ``distributed_optimizer`` returns the matching optimizer wrapper
 (HybridParallelOptimizer semantics: TP-aware global-norm clipping, sharding).
 """
+import os
 import copy
 
 import torch
@@ -135,6 +136,14 @@ class Fleet:
 
     def init(self, role_maker=None, is_collective=False, strategy=None, log_level="INFO"):
         self._strategy = strategy or DistributedStrategy()
+        self._ps_role = None
+        if not is_collective and os.environ.get('TRAINING_ROLE') and os.environ.get('PADDLE_PSERVERS_IP_PORT_LIST'):
+            # parameter-server mode (reference role_maker.py PaddleCloudRoleMaker environment):
+            # servers hold the tables, trainers pull / push over distributed.rpc (distributed/ps)
+            from .. import ps as _ps
+            self._ps_role = _ps.role_from_env()
+            self._is_collective = False
+            return self
         self._is_collective = True
         C.init_parallel_env()
         ws = C.get_world_size()
@@ -154,19 +163,34 @@ class Fleet:
 
     # -- info ----------------------------------------------------------------------------
     def is_first_worker(self):
+        r = getattr(self, '_ps_role', None)
+        if r is not None:
+            return not r.is_server and r.index == 0
         return C.get_rank() == 0
 
     def worker_index(self):
-        return C.get_rank()
+        r = getattr(self, '_ps_role', None)
+        return r.index if r is not None and not r.is_server else C.get_rank()
 
     def worker_num(self):
-        return C.get_world_size()
+        r = getattr(self, '_ps_role', None)
+        return r.n_trainers if r is not None else C.get_world_size()
 
     def is_worker(self):
-        return True
+        r = getattr(self, '_ps_role', None)
+        return r is None or not r.is_server
 
     def is_server(self):
-        return False
+        r = getattr(self, '_ps_role', None)
+        return r is not None and r.is_server
+
+    def server_num(self):
+        r = getattr(self, '_ps_role', None)
+        return r.n_servers if r is not None else 0
+
+    def server_index(self):
+        r = getattr(self, '_ps_role', None)
+        return r.index if r is not None and r.is_server else -1
 
     def worker_endpoints(self, to_string=False):
         eps = C.ParallelEnv().trainer_endpoints
@@ -176,16 +200,24 @@ class Fleet:
         C.barrier()
 
     def init_worker(self):
-        pass
+        if getattr(self, '_ps_role', None) is not None:
+            from .. import ps as _ps
+            _ps.init_worker(self._ps_role)
 
     def init_server(self, *a, **k):
-        pass
+        if getattr(self, '_ps_role', None) is not None:
+            from .. import ps as _ps
+            _ps.init_server(self._ps_role)
 
     def run_server(self):
-        pass
+        if getattr(self, '_ps_role', None) is not None:
+            from .. import ps as _ps
+            _ps.run_server()
 
     def stop_worker(self):
-        pass
+        if getattr(self, '_ps_role', None) is not None:
+            from .. import ps as _ps
+            _ps.stop_worker()
 
     def get_hybrid_communicate_group(self):
         return self._hcg
@@ -595,6 +627,15 @@ is_first_worker = fleet.is_first_worker
 worker_index = fleet.worker_index
 worker_num = fleet.worker_num
 barrier_worker = fleet.barrier_worker
+is_worker = fleet.is_worker
+is_server = fleet.is_server
+server_num = fleet.server_num
+server_index = fleet.server_index
+init_worker = fleet.init_worker
+init_server = fleet.init_server
+run_server = fleet.run_server
+stop_worker = fleet.stop_worker
+worker_endpoints = fleet.worker_endpoints
 util = fleet.util
 
 from . import meta_parallel, utils, layers, recompute  # noqa: E402,F401
