@@ -264,6 +264,8 @@ class SparseEmbedding(torch.nn.Module):
 
     def forward(self, ids):
         flat = ids.reshape(-1)
+        if flat.numel() == 0:
+            return torch.zeros(*ids.shape, self.dim, device=ids.device)
         uniq, inv = torch.unique(flat.cpu(), return_inverse=True)
         rows = pull_sparse(self.table, uniq.tolist()).to(ids.device).requires_grad_()
         table, uid = self.table, uniq.tolist()
