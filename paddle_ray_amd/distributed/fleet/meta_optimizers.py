@@ -370,8 +370,24 @@ def static_minimize(opt, loss, strategy, hcg, parameters=None):
         if stage != 1:
             raise NotImplementedError(f"static-mode sharding supports stage 1 (got stage {stage}); "
                                       "use dygraph group_sharded_parallel for stages 2/3")
+    if getattr(strategy, 'pipeline', False):
+        # (parity gap, raised rather than ignored: the reference's PipelineOptimizer splits the
+        # program by device_guard into per-stage sections, fluid/optimizer.py:4494)
+        raise NotImplementedError(
+            "strategy.pipeline is not supported for static-graph programs; use fleet dygraph "
+            "pipeline parallel (PipelineLayer + fleet.distributed_model)")
+    G.check_single_device(prog, 'fleet.distributed_optimizer(...).minimize')
+    ckpts = None
+    if getattr(strategy, 'recompute', False):
+        # recompute_optimizer.py:97 -> RecomputeOptimizer._set_checkpoints + backward with
+        # forward recomputation between the checkpoints
+        names = list((strategy.recompute_configs or {}).get('checkpoints') or [])
+        if not names:
+            raise ValueError("strategy.recompute needs recompute_configs['checkpoints'] (the "
+                             "static Variables or their names to keep in memory)")
+        ckpts = [blk.var(n) if isinstance(n, str) else n for n in names]
     n_before = len(blk.ops)
-    pg = G.append_backward(loss, parameters, loss_scale=loss_scale)
+    pg = G.append_backward(loss, parameters, loss_scale=loss_scale, checkpoints=ckpts)
     params = [p for p, _ in pg]
     if sharding:
         state.shard = _ShardPlan(params, hcg.get_sharding_parallel_group()

@@ -34,7 +34,7 @@ from .graph import (Program, Block, Variable, Executor, global_scope, scope_guar
                     xpu_places, npu_places, mlu_places, accuracy, auc, WeightNormParamAttr,
                     ExponentialMovingAverage, ipu_shard_guard, set_ipu_shard, IpuStrategy,
                     IpuCompiledProgram, exponential_decay, ctr_metric_bundle, _static_minimize,
-                    Scope)
+                    Scope, RecomputeOptimizer)
 from . import nn  # noqa: E402
 from .sequence_lod import create_lod_tensor  # noqa: E402,F401
 from . import amp  # noqa: E402

@@ -278,9 +278,43 @@ def name_scope(prefix=None):
     yield
 
 
+_DEVICE = [None]
+
+
 @contextlib.contextmanager
 def device_guard(device=None):
-    yield
+    """Ops recorded inside carry ``attrs['device']`` (parity: fluid/framework.py device_guard,
+    the op_device attribute PipelineOptimizer splits a program by). One device per program is
+    what the executor runs; ``minimize`` raises for a program spread over several devices (a
+    static pipeline split is not implemented: use fleet dygraph PipelineParallel)."""
+    prev = _DEVICE[0]
+    _DEVICE[0] = device
+    try:
+        yield
+    finally:
+        _DEVICE[0] = prev
+
+
+def _device_index(dev):
+    if dev is None:
+        return None
+    s = str(dev)
+    if ':' in s:
+        kind, idx = s.split(':', 1)
+        return (kind, idx)
+    return (s, '0') if s in ('gpu', 'cuda') else (s, None)
+
+
+def check_single_device(prog, what='minimize'):
+    """Raise for a program whose ops were recorded under device_guard on more than one device."""
+    devs = {op.attrs.get('device') for op in prog.global_block().ops if op.attrs.get('device')}
+    keys = {_device_index(d) for d in devs}
+    gpus = {k for k in keys if k and k[0] in ('gpu', 'cuda')}
+    if len(gpus) > 1:
+        raise NotImplementedError(
+            f"{what}: the program places ops on {len(gpus)} devices with static.device_guard "
+            f"({sorted(devs)}); a static-graph pipeline split is not implemented -- use "
+            "fleet dygraph pipeline parallel (PipelineLayer + fleet.distributed_model)")
 
 
 def data(name, shape, dtype=None, lod_level=0):
@@ -449,7 +483,10 @@ def record_op(op_type, fn, args, kwargs, out_specs=None):
 
 
 def _record_amp(op):
-    """Ops recorded inside ``paddle.amp.auto_cast`` replay under the same AMP policy."""
+    """Ops recorded inside ``paddle.amp.auto_cast`` replay under the same AMP policy (and
+    carry the enclosing device_guard's device)."""
+    if _DEVICE[0] is not None:
+        op.attrs['device'] = _DEVICE[0]
     from ..amp import amp_state
     st = amp_state()
     if st['enabled']:
@@ -627,13 +664,141 @@ def _new_var(blk, like_shape, dtype, name=None):
     return v
 
 
+# -----------------------------------------------------------------------------
+# forward recomputation (parity: python/paddle/fluid/backward.py:907
+# `_append_backward_ops_with_checkpoints_`, fluid/optimizer.py:6447 RecomputeOptimizer)
+# -----------------------------------------------------------------------------
+# Segments are op ranges between checkpoints (the reference's rule: with one checkpoint the ops up
+# to and including its producer; with several, the ops from the first consumer of checkpoint i to
+# the producer of checkpoint i+1, plus the head before the first segment). A segment's forward ops
+# run WITHOUT keeping their autograd contexts, so their intermediate outputs are freed at their
+# last forward use; when the backward reaches the segment, clones of its forward ops (role
+# 'recompute', fresh output vars) re-run from the held inputs and the segment's grad ops read the
+# clones' contexts. The host/device RNG state is saved at the segment's start and swapped in
+# around the clones, so dropout masks (seeded from the host generator) repeat bit for bit.
+_FWD_ROLES = ('forward', 'recompute')
+
+
+def _rng_save():
+    cpu = torch.get_rng_state()
+    dev = torch.cuda.get_rng_state() if torch.cuda.is_available() and torch.cuda.is_initialized() \
+        else torch.empty(0, dtype=torch.uint8)
+    return Tensor(cpu), Tensor(dev)
+
+
+def _rng_swap(cpu, dev):
+    cur = _rng_save()
+    torch.set_rng_state(_u(cpu))
+    d = _u(dev)
+    if d.numel():
+        torch.cuda.set_rng_state(d)
+    return cur
+
+
+def _rng_restore(cpu, dev):
+    _rng_swap(cpu, dev)
+
+
+for _n, _f in (('recompute_rng_save', _rng_save), ('recompute_rng_swap', _rng_swap),
+               ('recompute_rng_restore', _rng_restore)):
+    register_static_op(_n, _f)
+
+
+def _checkpoint_vids(checkpoints):
+    out = []
+    for c in checkpoints or ():
+        if isinstance(c, Variable):
+            out.append(c.vid)
+        else:
+            raise TypeError(f"checkpoints must be static Variables, got {type(c).__name__}")
+    return out
+
+
+def _recompute_segments(fwd, ck_vids):
+    """[(lo, hi)] op-index ranges of ``fwd`` to recompute (see the block comment above)."""
+    producer, first_use = {}, {}
+    for i, op in enumerate(fwd):
+        for v in op.in_vids:
+            first_use.setdefault(v, i)
+        for v in op.out_vids:
+            producer[v] = i
+    ck = sorted({v for v in ck_vids if v in producer}, key=lambda v: producer[v])
+    if not ck:
+        return []
+    if len(ck) == 1:
+        end = producer[ck[0]]
+        return [(0, end + 1)] if end > 0 else []
+    segs, prev_end = [], 0
+    for a, b in zip(ck, ck[1:]):
+        lo = max(first_use.get(a, producer[a] + 1), prev_end)
+        hi = producer[b] + 1
+        if lo < hi:
+            segs.append((lo, hi))
+            prev_end = hi
+    if segs and segs[0][0] > 0:
+        segs.insert(0, (0, segs[0][0]))
+    return segs
+
+
+def _remap_refs(obj, remap):
+    if isinstance(obj, _VarRef):
+        return _VarRef(remap.get(obj.vid, obj.vid))
+    if isinstance(obj, list):
+        return [_remap_refs(o, remap) for o in obj]
+    if isinstance(obj, tuple):
+        return tuple(_remap_refs(o, remap) for o in obj)
+    if isinstance(obj, dict):
+        return {k: _remap_refs(v, remap) for k, v in obj.items()}
+    return obj
+
+
+def _emit_recompute(blk, seg_ops, ctrl_vids):
+    """Append the RNG swap, the clones of ``seg_ops`` and the RNG restore; returns
+    (clones by id(original op), vid remap, the forward-side RNG save op)."""
+    cv = _new_var(blk, [-1], torch.uint8, 'recompute@RNG_CPU')
+    dv = _new_var(blk, [-1], torch.uint8, 'recompute@RNG_DEV')
+    save = OpDesc('recompute_rng_save', _rng_save, [], {}, [], [cv.vid, dv.vid],
+                  ('tuple', ['T', 'T']), role='forward')
+    sc = _new_var(blk, [-1], torch.uint8)
+    sd = _new_var(blk, [-1], torch.uint8)
+    blk.ops.append(OpDesc('recompute_rng_swap', _rng_swap, [_VarRef(cv.vid), _VarRef(dv.vid)], {},
+                          [cv.vid, dv.vid] + list(ctrl_vids), [sc.vid, sd.vid],
+                          ('tuple', ['T', 'T']), role='backward'))
+    remap, clones, last_outs = {}, {}, [sc.vid]
+    for op in seg_ops:
+        nop = OpDesc(op.type, op.fn, _remap_refs(op.args, remap), _remap_refs(op.kwargs, remap),
+                     [remap.get(v, v) for v in op.in_vids] + [sc.vid], [], op.out_template,
+                     role='recompute')
+        nop.attrs = {k: v for k, v in op.attrs.items() if k not in ('diff_in', 'diff_params')}
+        nop.attrs['recompute_of'] = op
+        for o in op.out_vids:
+            ov = blk.vars[o]
+            nv = _new_var(blk, list(ov._vshape), ov.dtype, ov.name + '@RECOMPUTE')
+            remap[o] = nv.vid
+            nop.out_vids.append(nv.vid)
+        if nop.out_vids:
+            last_outs = nop.out_vids
+        clones[id(op)] = nop
+        blk.ops.append(nop)
+    # (no outputs: the scheduler keeps an output-less op, in program order, instead of pruning it)
+    blk.ops.append(OpDesc('recompute_rng_restore', _rng_restore, [_VarRef(sc.vid), _VarRef(sd.vid)], {},
+                          [sc.vid, sd.vid] + list(last_outs), [], 'C', role='backward'))
+    return clones, remap, save
+
+
 def _build_backward(prog, targets, inputs=(), target_grads=None, no_grad_set=None,
-                    params=None, loss_scale=1.0):
+                    params=None, loss_scale=1.0, checkpoints=None):
     """Emit grad ops for ``targets`` w.r.t. ``inputs`` (Variables) and the trainable
     parameters. Returns ({input vid: grad var}, {param name: grad var})."""
     blk = prog.global_block()
     no_grad = {getattr(x, 'name', x) for x in (no_grad_set or ())}
     fwd = [op for op in blk.ops if op.role == 'forward']
+    segs = _recompute_segments(fwd, _checkpoint_vids(checkpoints)) if checkpoints else []
+    seg_of = {}
+    for si, (lo, hi) in enumerate(segs):
+        for op in fwd[lo:hi]:
+            seg_of[id(op)] = si
+    clones, seg_remap, rng_saves = {}, {}, []
     req = {v.vid for v in blk.vars.values() if v.is_data and not v.stop_gradient}
     req |= {x.vid for x in inputs}
     allowed = None if params is None else {id(p) for p in params}
@@ -697,12 +862,21 @@ def _build_backward(prog, targets, inputs=(), target_grads=None, no_grad_set=Non
         dps = diff_params(op)
         if not diff_in and not dps:
             continue
-        if op.ctx_vid is None:
+        si = seg_of.get(id(op))
+        if si is not None and si not in seg_remap:
+            lo, hi = segs[si]
+            cl, seg_remap[si], save = _emit_recompute(blk, fwd[lo:hi], [g for g in ogs if g is not None])
+            clones.update(cl)
+            rng_saves.append((fwd[lo], save))
+        xop = clones.get(id(op), op)    # the op whose context the grad op reads
+        remap = seg_remap.get(si, {}) if si is not None else {}
+        if xop.ctx_vid is None:
             cv = Variable(blk, [], 'float32', name=f'{op.type}@CTX')
             blk.vars[cv.vid] = cv
-            op.ctx_vid = cv.vid
-        op.attrs['diff_in'] = diff_in
-        op.attrs['diff_params'] = dps
+            xop.ctx_vid = cv.vid
+        xop.attrs['diff_in'] = [remap.get(i, i) for i in diff_in]
+        xop.attrs['diff_params'] = dps
+        fop, op = op, xop
         outs = []
         for i in diff_in:
             v = blk.vars[i]
@@ -714,8 +888,8 @@ def _build_backward(prog, targets, inputs=(), target_grads=None, no_grad_set=Non
         # gradient from a later consumer (a residual stream feeding both a Linear / MLP and an
         # add+LayerNorm), the grad op folds it into its input gradient (beta=1 GEMM) and the
         # separate `sum` op disappears
-        if op.type in _ACC_DX_OPS and op.type in _FN_OPS and diff_in and op.args and \
-                isinstance(op.args[0], _VarRef) and op.args[0].vid == diff_in[0] and \
+        if op.type in _ACC_DX_OPS and op.type in _FN_OPS and diff_in and fop.args and \
+                isinstance(fop.args[0], _VarRef) and fop.args[0].vid == diff_in[0] and \
                 diff_in[0] not in final and len(partial.get(diff_in[0], [])) == 1:
             acc_in = partial[diff_in[0]][0]
         gop = OpDesc(op.type + '_grad', _fn_grad if op.type in _FN_OPS else _vjp, args,
@@ -734,6 +908,9 @@ def _build_backward(prog, targets, inputs=(), target_grads=None, no_grad_set=Non
         for p, gv in zip(dps, outs[len(diff_in):]):
             add_partial(('param', p.name), gv)
             prog._register_param(p)
+    # each recomputed segment's RNG snapshot is taken in the forward, right before its first op
+    for first, save in rng_saves:
+        blk.ops.insert(blk.ops.index(first), save)
     in_grads = {x.vid: final_grad(x.vid, x.name + '@GRAD') for x in inputs}
     p_grads = {}
     for key in list(partial):
@@ -752,7 +929,9 @@ def append_backward(loss, parameter_list=None, no_grad_set=None, callbacks=None,
     if parameter_list:
         params = [prog._params[p] if isinstance(p, str) else p for p in parameter_list]
     _, p_grads = _build_backward(prog, [loss], no_grad_set=no_grad_set, params=params,
-                                 loss_scale=loss_scale)
+                                 loss_scale=loss_scale, checkpoints=checkpoints)
+    if checkpoints:
+        prog.__dict__['_recompute_checkpoints'] = [c.name for c in checkpoints]
     out = []
     for name, gvid in p_grads.items():
         if gvid is None:
@@ -806,15 +985,16 @@ def _optimize_fn(opt, params, *grads, scaler=None):
 register_static_op('optimize', _optimize_fn)
 
 
-def _static_minimize(opt, loss, parameters=None, scaler=None, loss_scale=1.0):
+def _static_minimize(opt, loss, parameters=None, scaler=None, loss_scale=1.0, checkpoints=None):
     prog = loss.block.program
+    check_single_device(prog)
     if not opt._parameter_list:
         ps = parameters or [p for p in prog.all_parameters() if not p.stop_gradient]
         opt._param_groups = []
         opt._add_param_group({'params': list(ps)})
     blk = prog.global_block()
     n_before = len(blk.ops)
-    pg = append_backward(loss, parameters, loss_scale=loss_scale)
+    pg = append_backward(loss, parameters, loss_scale=loss_scale, checkpoints=checkpoints)
     params = [p for p, _ in pg]
     gvars = [g for _, g in pg]
     sync = prog.__dict__.get('_ap_grad_sync')
@@ -829,6 +1009,106 @@ def _static_minimize(opt, loss, parameters=None, scaler=None, loss_scale=1.0):
     blk.ops.append(op)
     prog._bump()
     return None, pg
+
+
+class RecomputeOptimizer:
+    """Static-graph activation recomputation around an inner optimizer (parity:
+    python/paddle/fluid/optimizer.py:6447 RecomputeOptimizer; fleet meta_optimizers/
+    recompute_optimizer.py:97). ``_set_checkpoints`` names the Variables kept in memory; the
+    backward re-runs the forward ops between consecutive checkpoints (see _recompute_segments)."""
+
+    def __init__(self, optimizer):
+        from . import _static_mode_enabled
+        if not _static_mode_enabled():
+            raise Exception("In dygraph, don't support RecomputeOptimizer.")
+        self._optimizer = optimizer
+        self._checkpoints = None
+        self._learning_rate = getattr(optimizer, '_learning_rate', None)
+
+    def _set_checkpoints(self, checkpoints):
+        if not isinstance(checkpoints, (list, tuple)):
+            raise TypeError("_checkpoints should be a list of Variable or a list of String")
+        for c in checkpoints:
+            if not isinstance(c, (Variable, str)):
+                raise TypeError("_checkpoints should be a list of Variable or a list of String")
+        self._checkpoints = list(checkpoints)
+
+    def _resolve(self, prog):
+        if not self._checkpoints:
+            raise ValueError("RecomputeOptimizer: call _set_checkpoints() before minimize/backward")
+        blk = prog.global_block()
+        return [blk.var(c) if isinstance(c, str) else c for c in self._checkpoints]
+
+    def load(self, state_dict):
+        raise NotImplementedError("load function is not supported by Recompute Optimizer for now")
+
+    def backward(self, loss, startup_program=None, parameter_list=None, no_grad_set=None,
+                 callbacks=None):
+        return append_backward(loss, parameter_list, no_grad_set,
+                               checkpoints=self._resolve(loss.block.program))
+
+    def apply_gradients(self, params_grads):
+        prog = params_grads[0][1].block.program if params_grads else default_main_program()
+        opt = self._optimizer
+        params = [p for p, _ in params_grads]
+        if not opt._parameter_list:
+            opt._param_groups = []
+            opt._add_param_group({'params': list(params)})
+        blk = prog.global_block()
+        gvars = [g for _, g in params_grads]
+        blk.ops.append(OpDesc('optimize', _optimize_fn, [opt, params] + [_VarRef(g.vid) for g in gvars],
+                              {'scaler': None}, [g.vid for g in gvars], [], 'C', role='optimize'))
+        prog._bump()
+        return []
+
+    def apply_optimize(self, loss, startup_program, params_grads):
+        return self.apply_gradients(params_grads)
+
+    def minimize(self, loss, startup_program=None, parameter_list=None, no_grad_set=None):
+        from .amp import OptimizerWithMixedPrecision, _ScaleRef
+        opt, scaler, ls = self._optimizer, None, 1.0
+        ckpts = self._resolve(loss.block.program)
+        if isinstance(opt, OptimizerWithMixedPrecision):
+            opt._tag_program(loss.block.program)
+            if opt._use_scaling:
+                scaler, ls = opt._scaler, _ScaleRef(opt._scaler)
+            opt = opt._optimizer
+        return _static_minimize(opt, loss, parameter_list, scaler=scaler, loss_scale=ls,
+                                checkpoints=ckpts)
+
+    def __getattr__(self, k):
+        return getattr(self.__dict__['_optimizer'], k)
+
+
+def _tensor_bytes(t, seen):
+    if not isinstance(t, torch.Tensor) or t.device.type == 'meta':
+        return 0
+    try:
+        key = (t.untyped_storage().data_ptr(), t.device)
+        n = t.untyped_storage().nbytes()
+    except Exception:
+        return 0
+    if key in seen or not n:
+        return 0
+    seen.add(key)
+    return n
+
+
+def _live_bytes(env):
+    """Bytes held by an executor environment: tensors plus what op contexts keep for the
+    backward (a generic context's leaf inputs and outputs, a direct-grad context's saved
+    tensors), each storage counted once."""
+    seen, total = set(), 0
+    for v in list(env.values()):
+        if isinstance(v, Tensor):
+            total += _tensor_bytes(v._t, seen)
+        elif isinstance(v, _Ctx):
+            for t in list(v.leaves) + list(v.outs):
+                total += _tensor_bytes(t, seen)
+        elif isinstance(v, _FnCtx):
+            for t in v.saved_tensors:
+                total += _tensor_bytes(t, seen)
+    return total
 
 
 # =============================================================================
@@ -912,6 +1192,16 @@ class Executor:
     def __init__(self, place=None):
         self.place = place
         self._op_costs = None  # list of (op type, ms) when per-op timing is on (CostModel)
+        self._mem_trace = None  # peak bytes held by the run's environment (enable_memory_trace)
+
+    def enable_memory_trace(self, on=True):
+        """Track the peak bytes the executor's environment holds during ``run`` (activations
+        and backward contexts; parameters excluded): ``peak_live_bytes``."""
+        self._mem_trace = 0 if on else None
+
+    @property
+    def peak_live_bytes(self):
+        return self._mem_trace or 0
 
     def enable_op_timing(self, on=True):
         """Record every executed op's wall time (device-synchronized) in ``op_costs``."""
@@ -1005,12 +1295,12 @@ class Executor:
             amp_ctx = auto_cast(True, amp_cfg['white'], amp_cfg['black'], amp_cfg['level'],
                                 amp_cfg['dtype'])
         with amp_ctx:
-            if op.role == 'forward' and op.ctx_vid is not None and ctx_needed and \
+            if op.role in _FWD_ROLES and op.ctx_vid is not None and ctx_needed and \
                     op.type in _FN_OPS and not op.kwargs:
                 r = self._run_fn_op(op, env)
                 if r is not None:
                     return r
-            if op.role == 'forward' and op.ctx_vid is not None and ctx_needed:
+            if op.role in _FWD_ROLES and op.ctx_vid is not None and ctx_needed:
                 # run on leaf copies of the differentiable inputs and keep this op's own graph
                 diff_in = op.attrs.get('diff_in', [])
                 dps = op.attrs.get('diff_params', [])
@@ -1083,7 +1373,7 @@ class Executor:
         try:
             ops = blk.ops
             live = {v for oi in order for v in ops[oi].in_vids}
-            explicit_bwd = any(ops[oi].role == 'backward' for oi in order)
+            explicit_bwd = any(ops[oi].role in ('backward', 'recompute') for oi in order)
             timing = self._op_costs is not None
             sync = torch.cuda.synchronize if timing and torch.cuda.is_available() else \
                 (lambda: None)
@@ -1105,6 +1395,8 @@ class Executor:
                         flat, _ = _flatten_out(res)
                     for vid, t in zip(op.out_vids, flat):
                         env[vid] = t
+                if self._mem_trace is not None:
+                    self._mem_trace = max(self._mem_trace, _live_bytes(env))
                 for vid in free_after[pos]:
                     if vid not in required:
                         env.pop(vid, None)

@@ -127,6 +127,10 @@ def test_static_fleet_dp_matches_serial(tmp_path, world):
     ops = info['ops']
     first_ar = ops.index('c_allreduce_coalesced')
     last_grad = max(i for i, t in enumerate(ops) if t.endswith('_grad') or t == 'grad')
+    # one bucket holds all four gradients: its all-reduce is issued right behind the grad op
+    # that produces the bucket's last gradient, ahead of the join and the optimizer
+    assert first_ar == last_grad + 1, ops
+    assert first_ar < ops.index('c_sync_comm_stream') < ops.index('fleet_optimize')
     assert sum(info['buckets']) == 4
 
 
