@@ -384,7 +384,9 @@ fwd_kernel(const T* __restrict__ q, const T* __restrict__ k, const T* __restrict
 #pragma unroll
     for (int s = 0; s < NS; ++s) qf[s] = frag_global<T>(rowp, 16 * s + 8 * h, valid);
   }
-  wait_vmem_all();
+  // (no wait here: the Q fragment loads stay in flight under the first K/V tile's DMA below and
+  // are retired by the same vmcnt(0) before the first barrier -- one HBM round trip per block
+  // prologue instead of two; causal blocks at S = 1024 sweep only 2-16 tiles)
 
   f32x16 acc_o[ND];
 #pragma unroll

@@ -68,18 +68,22 @@ constexpr bool epi_scales(int E) { return E == kDGeluErf || E == kDGeluTanh || E
 // forward GELUs that store the derivative into Z
 constexpr bool epi_gd(int E) { return E == kGeluErfD || E == kGeluTanhD; }
 
-// tanh(u) = 1 - 2 / (exp(2u) + 1): one v_exp + one v_rcp (saturates cleanly at +-1)
-__device__ __forceinline__ float fast_tanh(float u) {
-  return 1.f - 2.f * __builtin_amdgcn_rcpf(__expf(2.f * u) + 1.f);
+// tanh-GELU in sigmoid form: 0.5 (1 + tanh(u)) = sigmoid(2u) with 2u = x (k1 + k3 x^2), so
+//   gelu(x) = x s,   gelu'(x) = s + x s (1 - s) (k1 + 3 k3 x^2),   s = 1 / (1 + 2^(-2u log2 e))
+// one v_exp + one v_rcp and ~9 FMA-class ops for BOTH values (the tanh form took ~19: the
+// derivative-saving forward epilogue runs serialised behind the K loop at one wave per SIMD,
+// profiles/r5/gemm_fwd_probe.log). Saturates cleanly: x -> -inf gives s = 0, x -> +inf s = 1.
+constexpr float kGT1 = 1.5957691216057308f;   // 2 sqrt(2 / pi)
+constexpr float kGT3 = 0.0713548162726009f;   // kGT1 * 0.044715
+constexpr float kLog2e = 1.4426950408889634f;
+__device__ __forceinline__ float gelu_tanh_sig(float x, float x2) {
+  const float e = __builtin_amdgcn_exp2f(-x * fmaf(kGT3 * kLog2e, x2, kGT1 * kLog2e));
+  return __builtin_amdgcn_rcpf(1.f + e);
 }
-__device__ __forceinline__ float gelu_tanh(float x) {
-  const float u = 0.79788456080286536f * (x + 0.044715f * x * x * x);
-  return 0.5f * x * (1.f + fast_tanh(u));
-}
+__device__ __forceinline__ float gelu_tanh(float x) { return x * gelu_tanh_sig(x, x * x); }
 __device__ __forceinline__ float dgelu_tanh(float x) {
-  const float u = 0.79788456080286536f * (x + 0.044715f * x * x * x);
-  const float t = fast_tanh(u);
-  return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * 0.79788456080286536f * (1.f + 0.134145f * x * x);
+  const float x2 = x * x, s = gelu_tanh_sig(x, x2);
+  return fmaf(x * s * (1.f - s), fmaf(3.f * kGT3, x2, kGT1), s);
 }
 __device__ __forceinline__ float gelu_erf(float x) { return gelu_erf_fast(x); }
 __device__ __forceinline__ float dgelu_erf(float x) { return dgelu_erf_fast(x); }
@@ -95,11 +99,9 @@ __device__ __forceinline__ float act(float x) {
 template <int E>
 __device__ __forceinline__ float act_d(float x, float& d) {
   if constexpr (E == kGeluTanhD) {
-    const float u = 0.79788456080286536f * (x + 0.044715f * x * x * x);
-    const float t = fast_tanh(u);
-    const float h = 0.5f * (1.f + t);
-    d = h + 0.5f * x * (1.f - t * t) * 0.79788456080286536f * (1.f + 0.134145f * x * x);
-    return x * h;
+    const float x2 = x * x, sg = gelu_tanh_sig(x, x2), y = x * sg;
+    d = fmaf(y * (1.f - sg), fmaf(3.f * kGT3, x2, kGT1), sg);
+    return y;
   } else {
     const float u = x * 0.70710678118654752f;
     const float e = __expf(-u * u);
