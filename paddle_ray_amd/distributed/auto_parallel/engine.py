@@ -422,7 +422,7 @@ class Engine:
         sd = load(path + '.pdparams')
         self._model.set_state_dict(sd)
         if getattr(self, '_dist', None) is not None:
-            by_name = {}
+            by_name, full_shape = {}, {}
             with torch.no_grad():
                 for k, p in self._model.state_dict().items():
                     lp = self._shard_of(p)
@@ -431,6 +431,7 @@ class Engine:
                     full = _u(p).detach()
                     _u(lp).copy_(self._slice_local(full, lp.__dict__.get('_dist_mapping')))
                     by_name[lp.name] = lp
+                    full_shape[lp.name] = tuple(full.shape)
             if load_optimizer and self._optimizer is not None and os.path.exists(path + '.pdopt'):
                 osd = load(path + '.pdopt')
                 local = {}
@@ -439,9 +440,12 @@ class Engine:
                         local[k] = {pn: Tensor(self._slice_local(_u(t), by_name[pn].__dict__.get('_dist_mapping')))
                                     if pn in by_name else t for pn, t in v.items()}
                         continue
-                    pn = next((n for n in by_name if k.startswith(n + '_')), None)
-                    if pn is not None and isinstance(v, Tensor) and _u(v).dim() == _u(by_name[pn]).dim() \
-                            and _u(v).dim() > 0 and _u(v).numel() > 1:
+                    # the LONGEST parameter name that prefixes the key ('w_1_moment1_0' belongs to
+                    # 'w_1', not 'w'), and only an accumulator with the parameter's FULL shape is
+                    # sliced like it (beta-pow scalars and foreign shapes pass through)
+                    pn = max((n for n in by_name if k.startswith(n + '_')), key=len, default=None)
+                    if pn is not None and isinstance(v, Tensor) and _u(v).dim() > 0 and \
+                            tuple(_u(v).shape) == full_shape[pn]:
                         v = Tensor(self._slice_local(_u(v), by_name[pn].__dict__.get('_dist_mapping')))
                     local[k] = v
                 self._optimizer.set_state_dict(local)

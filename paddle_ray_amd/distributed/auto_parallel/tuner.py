@@ -235,9 +235,15 @@ class Trial:
     def strategy(self):
         """Fleet hybrid_configs + the sharding / recompute switches of this trial."""
         v = self.space.values
-        return {'hybrid_configs': {'dp_degree': v['dp_degree'], 'mp_degree': v['mp_degree'],
-                                   'pp_degree': v['pp_degree'], 'sharding_degree': 1},
-                'sharding_stage': v['sharding_stage'], 'micro_batch_size': v['micro_batch_size'],
+        stage = int(v['sharding_stage'])
+        # evaluate() models optimizer state / gradients / parameters sharded over the data-parallel
+        # ranks when sharding_stage > 0: those ranks then form fleet's SHARDING group (sharding
+        # degree = dp, dp degree 1), so the emitted strategy shards exactly what was priced
+        dp = int(v['dp_degree'])
+        return {'hybrid_configs': {'dp_degree': 1 if stage > 0 else dp, 'mp_degree': v['mp_degree'],
+                                   'pp_degree': v['pp_degree'], 'sharding_degree': dp if stage > 0 else 1},
+                'sharding': stage > 0, 'sharding_configs': {'stage': stage} if stage > 0 else {},
+                'sharding_stage': stage, 'micro_batch_size': v['micro_batch_size'],
                 'recompute': v['recompute']}
 
     def __repr__(self):

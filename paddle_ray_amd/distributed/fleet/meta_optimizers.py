@@ -89,6 +89,7 @@ class _CommState:
         self.shard = None   # sharding stage 1: _ShardPlan
         self.localsgd = None
         self.steps = 0      # optimizer steps taken
+        self.last_comm = 0  # localsgd: the step of the last parameter averaging
 
     def final_micro(self):
         """This run completes a gradient-merge window (always True without merging)."""
@@ -208,26 +209,41 @@ def _fleet_optimize(state, opt, params, *grads, scaler=None):
     if state.shard is not None:
         sh = state.shard
         owned = set(id(p) for p in sh.owned(params))
+        own_p = [p for p in params if id(p) in owned]
+        own_g = [g for p, g in zip(params, grads) if id(p) in owned]
+        others = [(p, _u(g)) for p, g in zip(params, grads) if g is not None and id(p) not in owned]
+
+        # Every rank holds EVERY reduced gradient. The loss-scale unscale / found_inf check and
+        # the global clip norm must cover all of them (not just the owned ones): found_inf is
+        # then identical on every rank (all skip or all step, the scales never drift apart, a
+        # rank that owns nothing included) and the norm is taken over unscaled gradients.
+        def every_grad(clip_only=False):
+            gs = [p._t.grad for p in own_p if p._t.grad is not None and
+                  (not clip_only or getattr(p, 'need_clip', True))]
+            return gs + [g for p, g in others if not clip_only or getattr(p, 'need_clip', True)]
         clip = opt._grad_clip
         from ...nn.clip import ClipGradByGlobalNorm
+        from ...ops.fused import global_l2_norm_sq
         prev_hook = None
         if isinstance(clip, ClipGradByGlobalNorm):
-            # the norm is over EVERY parameter: all reduced gradients are on every rank
-            from ...ops.fused import global_l2_norm_sq
-            full = [_u(g) for p, g in zip(params, grads)
-                    if g is not None and getattr(p, 'need_clip', True)]
             prev_hook = clip._norm_hook
-            clip._norm_hook = lambda sq, _f=full: global_l2_norm_sq(_f).reshape(())
+            clip._norm_hook = lambda sq: global_l2_norm_sq(every_grad(True)).reshape(())
+        had_sg = '_scaler_grads' in opt.__dict__
+        prev_sg = opt.__dict__.get('_scaler_grads')
+        opt._scaler_grads = every_grad
         try:
-            own_p = [p for p in params if id(p) in owned]
-            own_g = [g for p, g in zip(params, grads) if id(p) in owned]
             if own_p:
                 _optimize_fn(opt, own_p, *own_g, scaler=scaler)
             elif scaler is not None:
+                scaler.unscale_(opt)     # found_inf over the reduced gradients like every rank
                 scaler.update()
         finally:
             if isinstance(clip, ClipGradByGlobalNorm):
                 clip._norm_hook = prev_hook
+            if had_sg:
+                opt._scaler_grads = prev_sg
+            else:
+                del opt.__dict__['_scaler_grads']
         sh.broadcast(params)
     else:
         _optimize_fn(opt, params, *grads, scaler=scaler)
@@ -236,9 +252,12 @@ def _fleet_optimize(state, opt, params, *grads, scaler=None):
         m.zero_()
     ls = state.localsgd
     if ls is not None:
+        # localsgd_optimizer.py:206: cond(step > begin_step, begin_localsgd, communicate) --
+        # average after EVERY step through begin_step, then k_steps after the last averaging
         k, begin = ls
-        if state.steps >= begin and (state.steps - begin) % k == 0:
+        if state.steps <= begin or state.steps - state.last_comm >= k:
             _average_params(state, params)
+            state.last_comm = state.steps
     return None
 
 

@@ -76,6 +76,15 @@ def _run_pod(a, devs, addr, port, restart):
     return code
 
 
+def _multi_node(a):
+    n = str(a.nnodes or '1')
+    try:
+        hi = int(n.split(':')[-1])
+    except ValueError:
+        hi = 1
+    return hi > 1
+
+
 def launch(argv=None):
     a = _parse(argv)
     if a.devices:
@@ -96,6 +105,13 @@ def launch(argv=None):
             sys.exit(130)
         # reference controllers/collective.py:208: the pod is rebuilt while restart <= max_restart
         if code == 0 or a.elastic_level < 1 or restart >= a.max_restart:
+            sys.exit(code)
+        if _multi_node(a):
+            # the other nodes' pods keep their rendezvous: rebuilding only this one would hang at
+            # init. A multi-node restart needs the peers restarted too (the reference coordinates
+            # it through its master store); report and exit with the failure instead
+            print(f'[launch] job {a.job_id}: a rank exited with {code}; in-place restart is '
+                  f'single-node only (--nnodes {a.nnodes}): not restarting', file=sys.stderr, flush=True)
             sys.exit(code)
         restart += 1
         print(f'[launch] job {a.job_id}: a rank exited with {code}; restart {restart}/{a.max_restart}',

@@ -34,7 +34,13 @@ def test_gpt13b_on_one_node_prefers_data_parallel():
     assert best.metrics['memory_gb'] < 288
     # every trial is either priced or carries the reason it was rejected
     assert all((t.status == T.TrialStatus.COMPLETED) == (t.reason is None) for t in tuner.trials)
-    assert best.strategy()['hybrid_configs']['dp_degree'] == 8
+    hc = best.strategy()['hybrid_configs']
+    # the 8 data-parallel ranks: plain dp, or fleet's sharding group when the trial shards
+    if v['sharding_stage'] > 0:
+        assert (hc['dp_degree'], hc['sharding_degree']) == (1, 8)
+        assert best.strategy()['sharding_configs'] == {'stage': v['sharding_stage']}
+    else:
+        assert (hc['dp_degree'], hc['sharding_degree']) == (8, 1)
 
 
 def test_175b_needs_more_than_one_node():

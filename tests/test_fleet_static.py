@@ -175,6 +175,76 @@ def test_static_fleet_localsgd(tmp_path):
     assert 'c_allreduce_coalesced' not in res[0][2]['ops']
 
 
+def _localsgd_steps(rank, world, begin, k, steps):
+    import paddle_ray_amd as paddle
+    from paddle_ray_amd import static
+    from paddle_ray_amd.distributed import fleet
+    paddle.enable_static()
+    main, startup, loss, params, opt = _program('sgd')
+    st = fleet.DistributedStrategy()
+    st.localsgd = True
+    st.localsgd_configs = {'k_steps': k, 'begin_step': begin}
+    fleet.init(is_collective=True, strategy=st)
+    with static.program_guard(main, startup):
+        fleet.distributed_optimizer(opt, strategy=st).minimize(loss)
+    exe = static.Executor()
+    xs, ys = _data(world, steps)
+    snaps = []
+    for s in range(steps):
+        exe.run(main, feed={'x': xs[s, 0, rank], 'y': ys[s, 0, rank]}, fetch_list=[loss])
+        snaps.append([p.numpy().copy() for p in params])
+    paddle.disable_static()
+    return snaps
+
+
+def test_static_fleet_localsgd_begin_step(tmp_path):
+    """Before begin_step every step averages (the ranks never drift during warm-up); after it,
+    averaging happens k_steps after the previous one (steps 1..3, then 5)."""
+    res = run_ranks(_localsgd_steps, 2, tmp_path, args=(3, 2, 5))
+    same = [all(np.array_equal(a, b) for a, b in zip(res[0][s], res[1][s])) for s in range(5)]
+    assert same == [True, True, True, False, True], same
+
+
+def _sharding_amp_clip(rank, world, sharding):
+    import paddle_ray_amd as paddle
+    from paddle_ray_amd import static
+    from paddle_ray_amd.distributed import fleet
+    paddle.enable_static()
+    main, startup, loss, params, _ = _program('adam')
+    opt = paddle.optimizer.Adam(0.05, parameters=params,
+                                grad_clip=paddle.nn.ClipGradByGlobalNorm(0.05))
+    st = fleet.DistributedStrategy()
+    st.amp = True
+    st.amp_configs = {'init_loss_scaling': 1024.0, 'use_dynamic_loss_scaling': True}
+    if sharding:
+        st.sharding = True
+        st.sharding_configs = {'stage': 1}
+        st.hybrid_configs = {'sharding_degree': 2, 'dp_degree': 1}
+    fleet.init(is_collective=True, strategy=st)
+    with static.program_guard(main, startup):
+        fleet.distributed_optimizer(opt, strategy=st).minimize(loss)
+    exe = static.Executor()
+    xs, ys = _data(world, 3)
+    for s in range(3):
+        exe.run(main, feed={'x': xs[s, 0, rank], 'y': ys[s, 0, rank]}, fetch_list=[loss])
+    out = [p.numpy().copy() for p in params]
+    paddle.disable_static()
+    return out
+
+
+def test_static_fleet_sharding_amp_clip_matches_dp(tmp_path):
+    """Sharding stage 1 + AMP loss scaling + global-norm clip: the owner-only update must see
+    the same unscaled gradients, clip coefficient and found_inf as plain data parallel."""
+    (tmp_path / 'sh').mkdir()
+    (tmp_path / 'dp').mkdir()
+    sh = run_ranks(_sharding_amp_clip, 2, tmp_path / 'sh', args=(True,))
+    dp = run_ranks(_sharding_amp_clip, 2, tmp_path / 'dp', args=(False,))
+    for a, b in zip(sh[0], sh[1]):
+        assert np.array_equal(a, b)
+    for a, b in zip(sh[0], dp[0]):
+        np.testing.assert_allclose(a, b, rtol=1e-5, atol=1e-6)
+
+
 def _lars_momentum(rank, world):
     import paddle_ray_amd as paddle
     from paddle_ray_amd.distributed import fleet
