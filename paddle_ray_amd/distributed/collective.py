@@ -276,24 +276,44 @@ def _ret(work, sync_op, post=None):
     return t
 
 
+def _comm_range(fn):
+    """While a profiler records, a collective's host call is a Communication range (the
+    profiler's Distributed view; the RCCL kernels themselves come from the device trace)."""
+    import functools
+
+    @functools.wraps(fn)
+    def wrapper(*a, **k):
+        from ..profiler import _hooks
+        if not _hooks.ACTIVE:
+            return fn(*a, **k)
+        from ..profiler import RecordEvent, TracerEventType
+        with RecordEvent(fn.__name__, TracerEventType.Communication):
+            return fn(*a, **k)
+    return wrapper
+
+
+@_comm_range
 def all_reduce(tensor, op=ReduceOp.SUM, group=None, sync_op=True, use_calc_stream=False):
     if _single(group):
         return _Task()
     return _ret(dist.all_reduce(_u(tensor), _op(op), _pg(group), async_op=True), sync_op)
 
 
+@_comm_range
 def broadcast(tensor, src, group=None, sync_op=True):
     if _single(group):
         return _Task()
     return _ret(dist.broadcast(_u(tensor), src, _pg(group), async_op=True), sync_op)
 
 
+@_comm_range
 def reduce(tensor, dst, op=ReduceOp.SUM, group=None, sync_op=True):
     if _single(group):
         return _Task()
     return _ret(dist.reduce(_u(tensor), dst, _op(op), _pg(group), async_op=True), sync_op)
 
 
+@_comm_range
 def all_gather(tensor_list, tensor, group=None, sync_op=True):
     t = _u(tensor)
     if _single(group):
@@ -311,6 +331,7 @@ def all_gather(tensor_list, tensor, group=None, sync_op=True):
     return _ret(w, sync_op, post)
 
 
+@_comm_range
 def all_gather_into_tensor(out_tensor, in_tensor, group=None, sync_op=True):
     if _single(group):
         _u(out_tensor).copy_(_u(in_tensor).reshape(_u(out_tensor).shape))
@@ -345,6 +366,7 @@ def scatter_object_list(out_object_list, in_object_list=None, src=0, group=None)
     out_object_list[:] = out
 
 
+@_comm_range
 def reduce_scatter(tensor, tensor_list, op=ReduceOp.SUM, group=None, sync_op=True):
     out = _u(tensor)
     if isinstance(tensor_list, (list, tuple)):
@@ -360,6 +382,7 @@ def reduce_scatter(tensor, tensor_list, op=ReduceOp.SUM, group=None, sync_op=Tru
     return _ret(w, sync_op)
 
 
+@_comm_range
 def scatter(tensor, tensor_list=None, src=0, group=None, sync_op=True):
     if _single(group):
         if tensor_list:
@@ -369,6 +392,7 @@ def scatter(tensor, tensor_list=None, src=0, group=None, sync_op=True):
     return _ret(dist.scatter(_u(tensor), ins, src, _pg(group), async_op=True), sync_op)
 
 
+@_comm_range
 def alltoall(in_tensor_list, out_tensor_list, group=None, sync_op=True):
     ins = [_u(t).contiguous() for t in in_tensor_list]
     if _single(group):
@@ -398,6 +422,7 @@ def alltoall(in_tensor_list, out_tensor_list, group=None, sync_op=True):
     return _ret(w, sync_op, post)
 
 
+@_comm_range
 def alltoall_single(in_tensor, out_tensor, in_split_sizes=None, out_split_sizes=None, group=None,
                     sync_op=True):
     if _single(group):
@@ -407,20 +432,24 @@ def alltoall_single(in_tensor, out_tensor, in_split_sizes=None, out_split_sizes=
                                        in_split_sizes, _pg(group), async_op=True), sync_op)
 
 
+@_comm_range
 def send(tensor, dst=0, group=None, sync_op=True):
     w = dist.isend(_u(tensor).contiguous(), dst, _pg(group))
     return _ret(w, sync_op)
 
 
+@_comm_range
 def recv(tensor, src=0, group=None, sync_op=True):
     w = dist.irecv(_u(tensor), src, _pg(group))
     return _ret(w, sync_op)
 
 
+@_comm_range
 def isend(tensor, dst, group=None):
     return send(tensor, dst, group, False)
 
 
+@_comm_range
 def irecv(tensor, src=None, group=None):
     return recv(tensor, src, group, False)
 
@@ -438,6 +467,7 @@ def batch_isend_irecv(p2p_op_list):
     return [_Task(w) for w in dist.batch_isend_irecv(ops)]
 
 
+@_comm_range
 def barrier(group=None):
     if _single(group):
         return

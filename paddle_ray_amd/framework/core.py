@@ -427,6 +427,12 @@ class Tensor:
         g = None if grad_tensor is None else _u(grad_tensor)
         if g is None and self._t.numel() != 1:
             g = torch.ones_like(self._t)
+        from ..profiler import _hooks
+        if _hooks.ACTIVE:
+            from ..profiler import RecordEvent, TracerEventType
+            with RecordEvent('backward', TracerEventType.Backward):
+                self._t.backward(g, retain_graph=retain_graph)
+            return
         self._t.backward(g, retain_graph=retain_graph)
 
     def clear_gradient(self, set_to_zero=True):

@@ -410,6 +410,9 @@ class DataLoader:
             yield collate([_np_tree(self.dataset[i]) for i in idx])
 
     def __iter__(self):
+        return _ReaderTimed(self, self._iter_batches())
+
+    def _iter_batches(self):
         dev = self._device()
         src = self._host_batches()
         if not (self.use_buffer_reader and dev.type == 'cuda'):
@@ -434,6 +437,37 @@ class DataLoader:
     def from_generator(feed_list=None, capacity=None, use_double_buffer=True, iterable=True,
                        return_list=False, use_multiprocess=False, drop_last=True):
         return _GeneratorLoader(return_list)
+
+
+class _ReaderTimed:
+    """Iterator over a DataLoader's batches that reports each batch's reader time to the
+    profiler benchmark (reader_cost in step_info; parity: fluid/dataloader/dataloader_iter.py
+    benchmark().before_reader / after_reader) and, while a profiler records, opens a
+    Dataloader range around it."""
+
+    def __init__(self, loader, it):
+        self._loader, self._it = loader, it
+
+    def __iter__(self):
+        return self
+
+    def __next__(self):
+        from ..profiler import _hooks
+        from ..profiler.timer import benchmark
+        bm = benchmark()
+        bm.check_if_need_record(self._loader)
+        bm.before_reader()
+        if _hooks.ACTIVE:
+            from ..profiler import RecordEvent, TracerEventType
+            with RecordEvent('Dataloader', TracerEventType.Dataloader):
+                b = next(self._it)
+        else:
+            b = next(self._it)
+        bm.after_reader()
+        return b
+
+    def __len__(self):
+        return len(self._loader)
 
 
 class _GeneratorLoader:

@@ -9,6 +9,7 @@ import torch
 from ...framework.core import (Tensor, Parameter, _u, convert_dtype, get_default_dtype,
                                _default_device, _to_torch_device, _unique_name)
 from .. import initializer as I
+from ...profiler import _hooks as _prof_hooks
 
 
 class ParamAttr:
@@ -275,6 +276,15 @@ class Layer:
             from ...static.graph import _has_var, record_layer_call
             if _has_var(inputs) or _has_var(kwargs):
                 return record_layer_call(self, inputs, kwargs)
+        if _prof_hooks.ACTIVE and not _prof_hooks.layer_depth():
+            # the outermost layer call of a recording profiler is the step's Forward range
+            from ...profiler import RecordEvent, TracerEventType
+            _prof_hooks.enter_layer()
+            try:
+                with RecordEvent(type(self).__name__, TracerEventType.Forward):
+                    return self._call_impl(*inputs, **kwargs)
+            finally:
+                _prof_hooks.exit_layer()
         return self._call_impl(*inputs, **kwargs)
 
     def _call_impl(self, *inputs, **kwargs):

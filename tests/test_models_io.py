@@ -133,7 +133,7 @@ def test_metrics():
 
 def test_profiler_record_event(tmp_path):
     import paddle_ray_amd.profiler as profiler
-    prof = profiler.Profiler(targets=[profiler.ProfilerTarget.CPU], timer_only=True)
+    prof = profiler.Profiler(targets=[profiler.ProfilerTarget.CPU])
     prof.start()
     for _ in range(3):
         with profiler.RecordEvent('my_op'):
