@@ -34,4 +34,5 @@ def is_compiled_with_cinn():
 Stream = cuda.Stream
 Event = cuda.Event
 current_stream = cuda.current_stream
+set_stream = cuda.set_stream
 stream_guard = cuda.stream_guard

@@ -141,6 +141,15 @@ def current_stream(device=None):
     return s
 
 
+def set_stream(stream):
+    """Make ``stream`` the current stream of its device; returns the previous current stream
+    (parity: python/paddle/device/__init__.py:900 set_stream)."""
+    ts = stream._s if isinstance(stream, Stream) else stream
+    prev = current_stream(ts.device)
+    torch.cuda.set_stream(ts)
+    return prev
+
+
 @contextlib.contextmanager
 def stream_guard(stream):
     with torch.cuda.stream(stream._s if isinstance(stream, Stream) else stream):

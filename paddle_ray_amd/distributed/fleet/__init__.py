@@ -10,6 +10,7 @@ the active mode (PipelineParallel / TensorParallel / sharded / DataParallel);
 import os
 import copy
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -52,7 +53,7 @@ class DistributedStrategy:
         self.tensor_parallel = False
         self.tensor_parallel_configs = {'tensor_parallel_degree': 1}
         self.without_graph_optimization = True
-        self.a_sync = False
+        self.a_sync = True      # parameter-server mode: asynchronous updates (reference default)
         self.a_sync_configs = {}
         self.heter_ccl_mode = False
         self.build_strategy = None
@@ -71,11 +72,19 @@ class DistributedStrategy:
 
 class UtilBase:
     def all_reduce(self, input, mode="sum", comm_world="worker"):
-        t = torch.as_tensor(input)
+        """Host all-reduce of a numpy array (a copy: the input is not modified); over RCCL the
+        values travel through the device."""
+        a = np.asarray(input)
+        t = torch.from_numpy(np.array(a, copy=True))
         if C.is_initialized() and C.get_world_size() > 1:
             op = {'sum': dist.ReduceOp.SUM, 'max': dist.ReduceOp.MAX,
                   'min': dist.ReduceOp.MIN}[mode]
-            dist.all_reduce(t, op)
+            if dist.get_backend() == 'nccl':
+                d = t.to(f'cuda:{torch.cuda.current_device()}')
+                dist.all_reduce(d, op)
+                t = d.cpu()
+            else:
+                dist.all_reduce(t, op)
         return t.numpy()
 
     def barrier(self, comm_world="worker"):
@@ -143,6 +152,7 @@ class Fleet:
             from .. import ps as _ps
             self._ps_role = _ps.role_from_env()
             self._is_collective = False
+            _ps.set_mode('async' if getattr(self._strategy, 'a_sync', True) else 'sync')
             return self
         self._is_collective = True
         C.init_parallel_env()
@@ -204,10 +214,12 @@ class Fleet:
             from .. import ps as _ps
             _ps.init_worker(self._ps_role)
 
-    def init_server(self, *a, **k):
+    def init_server(self, dirname=None, var_names=None, **kwargs):
+        """PS mode: join as a server; ``dirname`` preloads the tables save_persistables wrote
+        (the_one_ps.py:1340 _init_server)."""
         if getattr(self, '_ps_role', None) is not None:
             from .. import ps as _ps
-            _ps.init_server(self._ps_role)
+            _ps.init_server(self._ps_role, dirname=dirname)
 
     def run_server(self):
         if getattr(self, '_ps_role', None) is not None:
@@ -221,6 +233,135 @@ class Fleet:
 
     def get_hybrid_communicate_group(self):
         return self._hcg
+
+    # -- job geometry (fleet.py rank / nranks / world_size / local_rank / node_num ...) -------
+    def rank(self):
+        return self.worker_index()
+
+    def nranks(self):
+        return self.worker_num()
+
+    world_size = nranks
+
+    def local_rank(self):
+        return int(os.environ.get('PADDLE_LOCAL_RANK', os.environ.get('LOCAL_RANK', self.rank())))
+
+    def local_device_ids(self):
+        ids = os.environ.get('FLAGS_selected_gpus') or os.environ.get('PADDLE_LOCAL_DEVICE_IDS')
+        if ids:
+            return [int(i) for i in ids.split(',') if i != '']
+        return [self.local_rank()]
+
+    def world_device_ids(self):
+        ids = os.environ.get('PADDLE_WORLD_DEVICE_IDS')
+        if ids:
+            return [[int(i) for i in node.split(',') if i != ''] for node in ids.split(':')]
+        return [self.local_device_ids()]
+
+    def node_num(self):
+        r = getattr(self, '_ps_role', None)
+        if r is not None:
+            return len({e.split(':')[0] for e in r.server_endpoints})
+        n = os.environ.get('PADDLE_NNODES') or os.environ.get('PADDLE_TRAINERS_NUM_NODES')
+        if n:
+            return int(n)
+        eps = [e for e in os.environ.get('PADDLE_TRAINER_ENDPOINTS', '').split(',') if e]
+        return max(1, len({e.split(':')[0] for e in eps}))
+
+    def server_endpoints(self, to_string=False):
+        r = getattr(self, '_ps_role', None)
+        eps = list(r.server_endpoints) if r is not None else []
+        return ','.join(eps) if to_string else eps
+
+    def is_coordinator(self):
+        return False
+
+    def init_coordinator(self, *a, **k):
+        raise NotImplementedError("federated-learning coordinator (fleet.init_coordinator) is not supported")
+
+    def make_fl_strategy(self, *a, **k):
+        raise NotImplementedError("federated-learning strategies (fleet.make_fl_strategy) are not supported")
+
+    def get_fl_client(self, *a, **k):
+        raise NotImplementedError("federated-learning clients (fleet.get_fl_client) are not supported")
+
+    def _final_strategy(self):
+        return self._strategy
+
+    def _get_applied_meta_list(self):
+        return list(getattr(self, '_applied_meta', []))
+
+    def _get_applied_graph_list(self):
+        return []
+
+    # -- PS-mode table persistence (fleet.py:695,934; the_one_ps.py) ----------------------------
+    def _ps(self):
+        if getattr(self, '_ps_role', None) is None:
+            return None
+        from .. import ps as _ps
+        return _ps
+
+    def save_cache_model(self, dirname, **configs):
+        ps = self._ps()
+        if ps is None:
+            raise RuntimeError("save_cache_model is a parameter-server API")
+        return ps.save(dirname, int(configs.get('mode', 0)))
+
+    save_cache_table = save_cache_model
+
+    def check_save_pre_patch_done(self):
+        return True
+
+    def save_one_table(self, table_id, path, mode):
+        ps = self._ps()
+        if ps is None:
+            raise RuntimeError("save_one_table is a parameter-server API")
+        return ps.save(path, mode, table=str(table_id))
+
+    def save_dense_params(self, executor, dirname, scope, program, var_names=None):
+        ps = self._ps()
+        if ps is None:
+            from ..io import save_persistables
+            return save_persistables(executor, dirname, program)
+        return ps.save(dirname, 0)
+
+    def load_model(self, path, mode=0):
+        ps = self._ps()
+        if ps is None:
+            from ...framework.io import load
+            return load(path)
+        return ps.load(path)
+
+    def load_one_table(self, table_id, path, mode=0):
+        ps = self._ps()
+        if ps is None:
+            raise RuntimeError("load_one_table is a parameter-server API")
+        return ps.load(path, table=str(table_id))
+
+    def shrink(self, threshold=None):
+        raise NotImplementedError("fleet.shrink needs per-feature show/click statistics, which this "
+                                  "framework's sparse tables do not keep")
+
+    def save_inference_model(self, executor, dirname, feeded_var_names=None, target_vars=None,
+                             main_program=None, export_for_deployment=True, mode=0):
+        from ...static import save_inference_model, default_main_program
+        from ...static.graph import Variable
+        prog = main_program or default_main_program()
+        blk = prog.global_block()
+        feeds = [blk.var(n) if isinstance(n, str) else n for n in (feeded_var_names or [])]
+        fetches = list(target_vars or [])
+        os.makedirs(dirname, exist_ok=True)
+        save_inference_model(os.path.join(dirname, 'model'), feeds, fetches, executor, program=prog)
+        ps = self._ps()
+        if ps is not None:
+            ps.save(os.path.join(dirname, 'tables'), mode)
+
+    def load_inference_model(self, path, mode=0):
+        from ...static import load_inference_model
+        ps = self._ps()
+        if ps is not None and os.path.isdir(os.path.join(path, 'tables')):
+            ps.load(os.path.join(path, 'tables'))
+        return load_inference_model(os.path.join(path, 'model'))
 
     # -- wrapping ----------------------------------------------------------------------------
     def _sharding_level(self):
@@ -292,6 +433,12 @@ class Fleet:
         hybrid_parallel_optimizer.py:243-313); ``strategy.gradient_merge`` wraps the result."""
         if strategy is not None:
             self._strategy = strategy
+        if getattr(self, '_ps_role', None) is not None:
+            # PS mode: the strategy picks async / sync tables; dense parameters are trained on the
+            # servers through distributed.ps.DistributedOptimizer
+            from .. import ps as _ps
+            _ps.set_mode('async' if getattr(self._strategy, 'a_sync', True) else 'sync')
+            return optimizer
         if self._hcg is None:
             from ...static import _static_mode_enabled
             if not _static_mode_enabled():
@@ -361,6 +508,14 @@ class Fleet:
 
     # -- checkpoints ---------------------------------------------------------------------------
     def save_persistables(self, executor, dirname, main_program=None, mode=0):
+        """Collective: the program's persistables. PS mode (from a trainer): every server
+        writes its dense and sparse tables (mode 0 with optimizer state, 2 parameters only;
+        the_one_ps.py:1730 _save_persistables, :1459 _save_sparse_params)."""
+        if getattr(self, '_ps_role', None) is not None:
+            from .. import ps as _ps
+            if self._ps_role.is_server:
+                raise RuntimeError("fleet.save_persistables in PS mode is called on a trainer")
+            return _ps.save(dirname, mode)
         from ..io import save_persistables
         save_persistables(executor, dirname, main_program)
 
@@ -637,8 +792,36 @@ run_server = fleet.run_server
 stop_worker = fleet.stop_worker
 worker_endpoints = fleet.worker_endpoints
 util = fleet.util
+_final_strategy = fleet._final_strategy
+_get_applied_meta_list = fleet._get_applied_meta_list
+_get_applied_graph_list = fleet._get_applied_graph_list
+node_num = fleet.node_num
+rank = fleet.rank
+nranks = fleet.nranks
+world_size = fleet.world_size
+local_device_ids = fleet.local_device_ids
+world_device_ids = fleet.world_device_ids
+local_rank = fleet.local_rank
+is_coordinator = fleet.is_coordinator
+init_coordinator = fleet.init_coordinator
+make_fl_strategy = fleet.make_fl_strategy
+get_fl_client = fleet.get_fl_client
+server_endpoints = fleet.server_endpoints
+save_inference_model = fleet.save_inference_model
+save_persistables = fleet.save_persistables
+save_cache_model = fleet.save_cache_model
+save_cache_table = fleet.save_cache_table
+check_save_pre_patch_done = fleet.check_save_pre_patch_done
+save_one_table = fleet.save_one_table
+save_dense_params = fleet.save_dense_params
+load_model = fleet.load_model
+load_inference_model = fleet.load_inference_model
+load_one_table = fleet.load_one_table
+minimize = fleet.minimize
+shrink = fleet.shrink
 
-from . import meta_parallel, utils, layers, recompute  # noqa: E402,F401
+from . import meta_parallel, utils, layers, recompute, metrics, data_generator  # noqa: E402,F401
+from .data_generator import MultiSlotDataGenerator, MultiSlotStringDataGenerator  # noqa: E402,F401
 from .meta_parallel import (LayerDesc, SharedLayerDesc, PipelineLayer,  # noqa: E402,F401
                             ColumnParallelLinear, RowParallelLinear, VocabParallelEmbedding,
                             ParallelCrossEntropy, get_rng_state_tracker)

@@ -2,3 +2,4 @@
 from ....parallel.recompute import recompute  # noqa
 from . import hybrid_parallel_util  # noqa
 from .fs import LocalFS, HDFSClient  # noqa
+from .ps_util import DistributedInfer  # noqa

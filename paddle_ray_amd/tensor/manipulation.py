@@ -254,6 +254,13 @@ def index_add(x, index, axis, value, name=None):
     return Tensor(torch.index_add(_t(x), axis, _t(index).long(), _t(value)))
 
 
+def index_add_(x, index, axis, value, name=None):
+    """In-place index_add (parity: python/paddle/tensor/manipulation.py:4723)."""
+    t = _t(x)
+    t.index_add_(axis, _t(index).long(), _t(value).to(t.dtype))
+    return x
+
+
 def index_put(x, indices, value, accumulate=False, name=None):
     return Tensor(torch.index_put(_t(x), tuple(_t(i) for i in indices), _t(value), accumulate))
 
