@@ -163,14 +163,21 @@ class Predictor:
                 return [Tensor(o._t.clone()) for o in g(tuple(ins), {})]
             return self._replay(*ins)
 
+    def _io_types(self, outs):
+        mp = self._prog.__dict__.get('_mixed_precision')
+        if mp and mp.get('keep_io_types', True):
+            outs = [Tensor(o._t.float()) if o._t.dtype in (torch.float16, torch.bfloat16) else o
+                    for o in outs]
+        return outs
+
     def run(self, inputs=None):
         from ..framework.core import to_tensor
         if inputs is not None:  # new-style API: list of tensors in, list out
-            return self._run_tensors([x if isinstance(x, Tensor) else to_tensor(x)
-                                      for x in inputs])
+            return self._io_types(self._run_tensors([x if isinstance(x, Tensor) else to_tensor(x)
+                                                     for x in inputs]))
         ins = [to_tensor(self._inputs[n]) if not isinstance(self._inputs[n], Tensor)
                else self._inputs[n] for n in self._feed_names]
-        outs = self._run_tensors(ins)
+        outs = self._io_types(self._run_tensors(ins))
         self._outputs = {n: o.numpy() for n, o in zip(self._fetch_names, outs)}
         return True
 
@@ -187,6 +194,85 @@ class Predictor:
 
 def create_predictor(config):
     return Predictor(config)
+
+
+class PredictorPool:
+    """``size`` predictors over one config (parity: paddle.inference.PredictorPool): one per
+    serving thread, sharing nothing but the model files."""
+
+    def __init__(self, config, size=1):
+        if size < 1:
+            raise ValueError("PredictorPool size must be >= 1")
+        first = Predictor(config)
+        self._preds = [first] + [first.clone() for _ in range(size - 1)]
+
+    def retrive(self, idx):
+        return self._preds[idx]
+
+    retrieve = retrive
+
+    def __len__(self):
+        return len(self._preds)
+
+
+def convert_to_mixed_precision(model_file, params_file, mixed_model_file, mixed_params_file,
+                               mixed_precision, backend, keep_io_types=True, black_list=None):
+    """fp32 ``.pdmodel`` / ``.pdiparams`` -> a mixed-precision pair (parity:
+    python/paddle/inference/wrapper.py convert_to_mixed_precision): floating parameters are stored
+    in the half type (bf16 for PrecisionType.Bfloat16, fp16 for Half) except those read by an
+    op type in ``black_list``, which stay fp32, and the program is marked so that it replays
+    under O2 autocast with ``black_list`` op types in fp32; ``keep_io_types``: the predictor still
+    takes and returns fp32."""
+    import json
+    from ..framework.io import load, save
+    from ..static import program_desc as PD
+    from ..static.graph import MIXED_PRECISION_OP
+    if int(mixed_precision) not in (int(PrecisionType.Half), int(PrecisionType.Bfloat16)):
+        raise ValueError(f"mixed_precision must be PrecisionType.Half or Bfloat16, got {mixed_precision!r}")
+    if int(backend) != int(PlaceType.GPU):
+        raise ValueError("convert_to_mixed_precision targets PlaceType.GPU")
+    half = 'bfloat16' if int(mixed_precision) == int(PrecisionType.Bfloat16) else 'float16'
+    tdt = torch.bfloat16 if half == 'bfloat16' else torch.float16
+    black = sorted(set(black_list or ()))
+    with open(model_file, 'rb') as f:
+        desc = PD.decode('ProgramDesc', f.read())
+    ops = desc['blocks'][0].setdefault('ops', [])
+    def param_refs(obj, out):
+        if isinstance(obj, dict):
+            if '__param__' in obj:
+                out.add(obj['__param__'])
+            for v in obj.values():
+                param_refs(v, out)
+        elif isinstance(obj, list):
+            for v in obj:
+                param_refs(v, out)
+        return out
+    keep32 = set()
+    for od in ops:
+        if od.get('type') in black:
+            for slot in od.get('inputs', []):
+                keep32.update(slot.get('arguments', []))
+            for a in od.get('attrs', []):
+                if a.get('name') == '__pra_call__':
+                    param_refs(PD.loads_call(PD.attr_value(a)), keep32)
+    cfg = {'dtype': half, 'black_list': black, 'keep_io_types': bool(keep_io_types)}
+    marker = {'type': MIXED_PRECISION_OP, 'inputs': [], 'outputs': [],
+              'attrs': [{'name': 'config', 'type': PD.ATTR['STRING'], 's': json.dumps(cfg)}]}
+    nfeed = sum(1 for od in ops if od.get('type') == 'feed')
+    ops.insert(nfeed, marker)
+    params = load(params_file)
+    out = {}
+    for k, v in params.items():
+        t = v._t if isinstance(v, Tensor) else torch.as_tensor(v)
+        if t.is_floating_point() and k not in keep32:
+            t = t.to(tdt)
+        out[k] = Tensor(t)
+    for d in (os.path.dirname(mixed_model_file), os.path.dirname(mixed_params_file)):
+        if d:
+            os.makedirs(d, exist_ok=True)
+    with open(mixed_model_file, 'wb') as f:
+        f.write(PD.encode('ProgramDesc', desc))
+    save(out, mixed_params_file)
 
 
 def get_version():

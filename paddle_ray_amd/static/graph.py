@@ -1791,8 +1791,12 @@ def deserialize_program(data, params=None):
     def enc_block(idx):
         return [enc_op(od) for od in blocks[idx].get('ops', [])]
 
+    mixed = None
     for od in blocks[0].get('ops', []):
         attrs = {a['name']: a for a in od.get('attrs', [])}
+        if od['type'] == MIXED_PRECISION_OP:
+            mixed = json.loads(PD.attr_value(attrs['config']))
+            continue
         if od['type'] == 'feed':
             feeds[PD.attr_value(attrs['col'])] = od['outputs'][0]['arguments'][0]
             continue
@@ -1806,8 +1810,29 @@ def deserialize_program(data, params=None):
     for v in prog._feeds:
         v.__dict__['is_data'] = True
     prog._fetches = [blk.vars[vids[fetches[i]]] for i in sorted(fetches)]
+    if mixed is not None:
+        apply_mixed_precision(prog, mixed)
     prog._bump()
     return prog
+
+
+# A converted mixed-precision model (inference.convert_to_mixed_precision) carries one marker op
+# of this type in block 0 with a STRING attribute 'config' = {"dtype", "black_list",
+# "keep_io_types"}: on load every op replays under O2 autocast of that dtype, black-listed op
+# types in fp32.
+MIXED_PRECISION_OP = 'pra_mixed_precision'
+
+
+def apply_mixed_precision(prog, cfg):
+    from ..amp import BLACK_LIST
+    dt = {'float16': torch.float16, 'bfloat16': torch.bfloat16}[cfg['dtype']]
+    black = set(cfg.get('black_list', [])) | set(BLACK_LIST)
+    amp = {'dtype': dt, 'level': 'O2', 'white': set(), 'black': black}
+    for op in prog.global_block().ops:
+        if op.type in set(cfg.get('black_list', [])):
+            continue
+        op.attrs['amp'] = amp
+    prog.__dict__['_mixed_precision'] = dict(cfg)
 
 
 def load_inference_model(path_prefix, executor=None, **kwargs):

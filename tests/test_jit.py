@@ -290,3 +290,56 @@ def test_dy2static_nonlocal_closure():
     out = cg(paddle.ones([2]))
     np.testing.assert_allclose(out.numpy(), [2.0, 2.0])
     assert k == 3.0 and calls[0] == 1  # the nonlocal write reached the real cell
+
+
+class _MLPNorm(paddle.nn.Layer):
+    def __init__(self):
+        super().__init__()
+        self.l1 = paddle.nn.Linear(16, 32)
+        self.ln = paddle.nn.LayerNorm(32)
+        self.l2 = paddle.nn.Linear(32, 4)
+
+    def forward(self, x):
+        return self.l2(paddle.nn.functional.gelu(self.ln(self.l1(x))))
+
+
+def test_convert_to_mixed_precision_and_predictor_pool(tmp_path):
+    """inference.convert_to_mixed_precision (wrapper.py): bf16 parameters except those of
+    black-listed op types, O2 replay, fp32 I/O kept; PredictorPool hands out independent
+    predictors (reference: paddle.inference.PredictorPool)."""
+    from paddle_ray_amd import inference
+    from paddle_ray_amd.static import program_desc as PD
+    paddle.seed(3)
+    net = _MLPNorm()
+    net.eval()
+    path = str(tmp_path / 'm')
+    paddle.jit.save(net, path, input_spec=[InputSpec([None, 16], 'float32', 'x')])
+    ops = [od['type'] for od in PD.decode('ProgramDesc', open(path + '.pdmodel', 'rb').read())['blocks'][0]['ops']]
+    ln_type = next(t for t in ops if 'layer_norm' in t)
+    mixed = str(tmp_path / 'mixed' / 'm')
+    inference.convert_to_mixed_precision(path + '.pdmodel', path + '.pdiparams', mixed + '.pdmodel',
+                                         mixed + '.pdiparams', inference.PrecisionType.Bfloat16,
+                                         inference.PlaceType.GPU, keep_io_types=True, black_list={ln_type})
+    params = paddle.load(mixed + '.pdiparams')
+    dts = {k: v.dtype for k, v in params.items()}
+    assert any('bfloat16' in str(d) for d in dts.values())
+    ln_names = [k for k in params if params[k].shape == [32] and 'bfloat16' not in str(params[k].dtype)]
+    assert len(ln_names) >= 2          # the LayerNorm's scale and shift stay fp32
+    x = np.random.RandomState(1).rand(5, 16).astype('float32')
+    ref = net(paddle.to_tensor(x)).numpy()
+    pool = inference.PredictorPool(inference.Config(mixed + '.pdmodel', mixed + '.pdiparams'), 2)
+    assert len(pool) == 2 and pool.retrive(0) is not pool.retrive(1)
+    outs = []
+    for i in range(2):
+        p = pool.retrive(i)
+        p.get_input_handle('x').copy_from_cpu(x)
+        p.run()
+        outs.append(p.get_output_handle(p.get_output_names()[0]).copy_to_cpu())
+    assert outs[0].dtype == np.float32
+    np.testing.assert_allclose(outs[0], outs[1])
+    np.testing.assert_allclose(outs[0], ref, rtol=5e-2, atol=5e-2)
+    assert not np.array_equal(outs[0], ref)       # really ran in bf16
+    with pytest.raises(ValueError):
+        inference.convert_to_mixed_precision(path + '.pdmodel', path + '.pdiparams', mixed + '2.pdmodel',
+                                             mixed + '2.pdiparams', inference.PrecisionType.Int8,
+                                             inference.PlaceType.GPU)
