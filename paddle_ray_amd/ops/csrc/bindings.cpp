@@ -38,6 +38,10 @@ void pra_bias_gelu_fwd(const void*, const void*, void*, int64_t, int, int, int, 
 void pra_bias_gelu_bwd(const void*, const void*, const void*, void*, int64_t, int, int, int, hipStream_t);
 void pra_adamw_mt(const int64_t*, const float*, const int64_t*, int, float, float, float, float, float, float, float,
                   const float*, hipStream_t);
+void pra_lamb_shard_stage1(const int64_t*, int, const void*, int, const float*, float*, float*, float*, const float*,
+                           float*, int, float, float, float, float, float, float, const float*, hipStream_t);
+void pra_lamb_shard_stage2(const int64_t*, int, float*, const float*, const float*, int, float, void*, int,
+                           hipStream_t);
 void pra_zero_mt(const int64_t*, int, hipStream_t);
 void pra_momentum_mt(const int64_t*, const float*, const int64_t*, int, float, float, int, float, const float*,
                      hipStream_t);
@@ -282,6 +286,17 @@ PYBIND11_MODULE(_pra_hip, m) {
                           P gsp) {
     pra_momentum_mt(I64(tab), CF(ftab), I64(chunks), nch, lr, mu, nesterov, gs, CF(gsp), S(s));
     check_launch("momentum_mt");
+  });
+  m.def("lamb_shard_stage1", [](P pieces, int np_, P g, int gdt, P w, P m_, P v, P r, P wd, P norms, int nparams,
+                                float b1, float b2, float eps, float bc1, float bc2, float gs, P gsp, P s) {
+    pra_lamb_shard_stage1(I64(pieces), np_, CV(g), gdt, CF(w), F(m_), F(v), F(r), CF(wd), F(norms), nparams, b1, b2,
+                          eps, bc1, bc2, gs, CF(gsp), S(s));
+    check_launch("lamb_shard_stage1");
+  });
+  m.def("lamb_shard_stage2", [](P pieces, int np_, P w, P r, P norms, int nparams, float lr, P pout, int pdt, P s) {
+    pra_lamb_shard_stage2(I64(pieces), np_, F(w), CF(r), CF(norms), nparams, lr, reinterpret_cast<void*>(pout), pdt,
+                          S(s));
+    check_launch("lamb_shard_stage2");
   });
   m.def("sumsq_accum", [](P x, P out, int64_t n, int dt, P s) {
     pra_sumsq_accum(CV(x), F(out), n, dt, S(s));

@@ -9,6 +9,6 @@ step() { local name=$1 t=$2; shift 2; timeout -k 10 "$t" "$@" > $OUT/$name.log 2
 step fa_causal 120 python scripts/fa_probe.py --B 16 --S 1024 --H 16 --D 128 --causal 1
 step fa_nc 120 python scripts/fa_probe.py --B 8 --S 2048 --H 16 --D 128 --causal 0 --check 0
 step gemm 300 python scripts/r6_gemm_probe.py
-step tests 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gemm_lds_gpu.py tests/test_flash_ext.py tests/test_kernels_gpu.py -m gpu
-step bench 300 python bench.py --steps 10 --warmup 3
+step tests 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gemm_lds_gpu.py tests/test_flash_ext.py tests/test_kernels_gpu.py -m gpu
+step bench 240 python bench.py --steps 10 --warmup 3
 exit 0
