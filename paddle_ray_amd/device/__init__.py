@@ -3,7 +3,9 @@ import torch
 
 from ..framework.core import (set_device, get_device, is_compiled_with_cuda, is_compiled_with_rocm,  # noqa
                               is_compiled_with_xpu)
+from ..framework.core import XPUPlace, IPUPlace, MLUPlace  # noqa: F401
 from . import cuda  # noqa
+from . import xpu  # noqa: F401
 
 
 def get_all_device_type():
@@ -29,6 +31,26 @@ def synchronize(device=None):
 
 def is_compiled_with_cinn():
     return False
+
+
+def is_compiled_with_ipu():
+    return False
+
+
+def is_compiled_with_npu():
+    return False
+
+
+def is_compiled_with_mlu():
+    return False
+
+
+def is_compiled_with_custom_device(device_type):
+    return False
+
+
+def get_available_custom_device():
+    return []
 
 
 Stream = cuda.Stream

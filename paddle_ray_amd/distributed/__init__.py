@@ -27,5 +27,6 @@ from . import watchdog  # noqa: E402
 from . import models  # noqa: E402
 from . import utils  # noqa: E402
 from . import rpc  # noqa: E402
+from . import communication  # noqa: E402
 from . import auto_parallel  # noqa: E402
 from .auto_parallel import ProcessMesh, shard_tensor, shard_op, reshard, Strategy, Engine  # noqa: E402

@@ -161,8 +161,16 @@ def CUDAPinnedPlace():
     return Place('cpu')
 
 
-def XPUPlace(i=0):  # no XPU on MI355X; kept for API surface
-    raise RuntimeError("XPUPlace is not available in the MI355X build")
+def _foreign_place(kind):
+    def make(i=0):  # no such device on an MI355X build; kept for API surface
+        raise RuntimeError(f"{kind} is not available in the MI355X build (devices: CPUPlace, CUDAPlace = HIP)")
+    make.__name__ = kind
+    return make
+
+
+XPUPlace = _foreign_place('XPUPlace')
+IPUPlace = _foreign_place('IPUPlace')
+MLUPlace = _foreign_place('MLUPlace')
 
 
 NPUPlace = XPUPlace

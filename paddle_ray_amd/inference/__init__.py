@@ -275,6 +275,28 @@ def convert_to_mixed_precision(model_file, params_file, mixed_model_file, mixed_
     save(out, mixed_params_file)
 
 
+def get_num_bytes_of_data_type(dtype):
+    """Bytes per element of an inference DataType."""
+    return {DataType.FLOAT32: 4, DataType.INT64: 8, DataType.INT32: 4, DataType.UINT8: 1, DataType.INT8: 1,
+            DataType.FLOAT16: 2, DataType.BFLOAT16: 2, DataType.BOOL: 1}[DataType(int(dtype))]
+
+
+def get_trt_compile_version():
+    """TensorRT is not part of an MI355X build: (0, 0, 0) as the reference reports without it."""
+    return (0, 0, 0)
+
+
+def get_trt_runtime_version():
+    return (0, 0, 0)
+
+
+def _get_phi_kernel_name(op_name):
+    """The kernel-registry name an op type dispatches to (ops/registry.py keys)."""
+    from ..ops import registry as R
+    names = {k[0] for k in R.list_kernels()}
+    return op_name if op_name in names else op_name
+
+
 def get_version():
     from .. import __version__
     return __version__

@@ -35,7 +35,7 @@ def _from_dense(dense_ndhwc, active):
     return Tensor(torch.sparse_coo_tensor(idx, vals, dense_ndhwc.shape).coalesce())
 
 
-class functional:
+class _Functional:
     @staticmethod
     def relu(x, name=None):
         t = _coo(x)
@@ -75,12 +75,12 @@ class functional:
     @staticmethod
     def conv3d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1,
                data_format='NDHWC', name=None):
-        return functional._conv(x, weight, bias, stride, padding, dilation, groups, False)
+        return _Functional._conv(x, weight, bias, stride, padding, dilation, groups, False)
 
     @staticmethod
     def subm_conv3d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1,
                     data_format='NDHWC', key=None, name=None):
-        return functional._conv(x, weight, bias, stride, padding, dilation, groups, True)
+        return _Functional._conv(x, weight, bias, stride, padding, dilation, groups, True)
 
     @staticmethod
     def max_pool3d(x, kernel_size, stride=None, padding=0, ceil_mode=False,
@@ -108,12 +108,12 @@ class functional:
 
 class ReLU(Layer):
     def forward(self, x):
-        return functional.relu(x)
+        return _Functional.relu(x)
 
 
 class ReLU6(Layer):
     def forward(self, x):
-        return functional.relu6(x)
+        return _Functional.relu6(x)
 
 
 class LeakyReLU(Layer):
@@ -122,7 +122,7 @@ class LeakyReLU(Layer):
         self._slope = negative_slope
 
     def forward(self, x):
-        return functional.leaky_relu(x, self._slope)
+        return _Functional.leaky_relu(x, self._slope)
 
 
 class Softmax(Layer):
@@ -131,7 +131,7 @@ class Softmax(Layer):
         self._axis = axis
 
     def forward(self, x):
-        return functional.softmax(x, self._axis)
+        return _Functional.softmax(x, self._axis)
 
 
 class _Conv3DBase(Layer):
@@ -152,7 +152,7 @@ class _Conv3DBase(Layer):
             [out_channels], attr=bias_attr, is_bias=True)
 
     def forward(self, x):
-        fn = functional.subm_conv3d if self._subm else functional.conv3d
+        fn = _Functional.subm_conv3d if self._subm else _Functional.conv3d
         return fn(x, self.weight, self.bias, self._stride, self._padding, self._dilation,
                   self._groups)
 
@@ -172,7 +172,7 @@ class MaxPool3D(Layer):
         self._k, self._s, self._p, self._ceil = kernel_size, stride, padding, ceil_mode
 
     def forward(self, x):
-        return functional.max_pool3d(x, self._k, self._s, self._p, self._ceil)
+        return _Functional.max_pool3d(x, self._k, self._s, self._p, self._ceil)
 
 
 class BatchNorm(Layer):
@@ -197,3 +197,6 @@ class SyncBatchNorm(BatchNorm):
         Layer.__init__(self)
         from ...nn import SyncBatchNorm as _Sync
         self._bn = _Sync(num_features, momentum, epsilon, weight_attr, bias_attr, 'NCL')
+
+
+from . import functional  # noqa: E402,F401
