@@ -29,4 +29,5 @@ from . import utils  # noqa: E402
 from . import rpc  # noqa: E402
 from . import communication  # noqa: E402
 from . import auto_parallel  # noqa: E402
+from . import passes  # noqa: E402
 from .auto_parallel import ProcessMesh, shard_tensor, shard_op, reshard, Strategy, Engine  # noqa: E402

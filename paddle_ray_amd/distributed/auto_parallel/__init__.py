@@ -334,8 +334,15 @@ def shard_op(op, process_mesh=None, in_shard_specs=None, out_shard_specs=None):
     return wrapped
 
 
+_RC_IDS = iter(range(1, 1 << 62))
+
+
 def recompute(op):
-    """Activation recomputation of `op` (a callable or Layer) in the backward pass."""
+    """Activation recomputation of `op` (a callable or Layer) in the backward pass. Eagerly it
+    runs under ``parallel.recompute``; while a static program records, the ops of each call are
+    tagged as one recompute region (``recompute_id``), which the static Engine's
+    ``auto_parallel_recompute`` pass turns into a recompute segment (reference
+    auto_parallel/interface.py recompute -> op attr 'recompute_id')."""
     from ...parallel.recompute import recompute as _rc
 
     class _RC:
@@ -343,6 +350,15 @@ def recompute(op):
             self.f = f
 
         def __call__(self, *args, **kwargs):
+            from ...static import _STATIC
+            if _STATIC[0]:
+                from ...static import graph as G
+                prev = G._RECOMPUTE_ID[0]
+                G._RECOMPUTE_ID[0] = next(_RC_IDS)
+                try:
+                    return self.f(*args, **kwargs)
+                finally:
+                    G._RECOMPUTE_ID[0] = prev
             return _rc(self.f, *args, **kwargs)
 
         def __getattr__(self, name):

@@ -182,12 +182,6 @@ class Engine:
         from .static_passes import parallelize
         assert inputs_spec, "a static Engine needs inputs_spec (paddle.static.InputSpec list)"
         st = self._strategy
-        for opt_name in ('amp', 'recompute', 'gradient_merge'):
-            cfg = getattr(st, opt_name, None) if st is not None else None
-            if cfg is not None and getattr(cfg, 'enable', False):
-                raise NotImplementedError(
-                    f"auto_parallel.Engine in static mode: strategy.{opt_name} is not applied to the "
-                    "partitioned program; run the Engine in dygraph mode for it")
         serial = static.Program()
         with static.program_guard(serial):
             ins = [static.data(sp.name or f'input{i}', list(sp.shape), sp.dtype)
@@ -198,6 +192,8 @@ class Engine:
             loss = self._compute_loss(outs, lbs)
         dist, vmap, part = parallelize(serial)
         local = [part.local_param(p) for p in self._model.parameters() if id(p) in part.params]
+        if self._optimizer is not None:
+            self._apply_passes(dist, serial, vmap, part, ins, outs)
         self._dist = {'program': dist, 'feeds': [v.name for v in ins + lbs], 'n_in': len(ins),
                       'label_specs': list(_to_list(labels_spec)),
                       'loss': vmap[loss], 'outs': [vmap[o] for o in _to_list(outs)],
@@ -211,6 +207,52 @@ class Engine:
                 opt.minimize(vmap[loss], parameters=[p for p in local if not p.stop_gradient])
         self._dist['eval_program'] = eval_prog
         self._exe = static.Executor()
+
+    def _apply_passes(self, dist, serial, vmap, part, ins, outs):
+        """strategy.{amp, recompute, gradient_merge, sharding, fused_passes} as program passes on
+        the partitioned program, before its minimize (reference engine.py _apply_pre_optimization
+        / _apply_post_optimization -> distributed/passes); the distributed global-norm clip
+        whenever the optimizer clips by global norm."""
+        from ..passes import new_pass, PassManager
+        from ...nn.clip import ClipGradByGlobalNorm
+        st = self._strategy
+        passes = []
+        if st is not None and st.amp.enable:
+            lvl = str(st.amp.level).lower()
+            passes.append(new_pass('auto_parallel_fp16' if lvl in ('o2', 'o3') else 'auto_parallel_amp', {
+                'dtype': st.amp.dtype, 'custom_white_list': st.amp.custom_white_list,
+                'custom_black_list': st.amp.custom_black_list,
+                'init_loss_scaling': st.amp.init_loss_scaling,
+                'use_dynamic_loss_scaling': st.amp.use_dynamic_loss_scaling,
+                'incr_every_n_steps': st.amp.incr_every_n_steps,
+                'decr_every_n_nan_or_inf': st.amp.decr_every_n_nan_or_inf,
+                'incr_ratio': st.amp.incr_ratio, 'decr_ratio': st.amp.decr_ratio,
+                'use_optimizer_fp16': lvl == 'o3'}))
+        if st is not None and st.recompute.enable:
+            blk = serial.global_block()
+            ck = [vmap[blk.var(c) if isinstance(c, str) else c].name for c in st.recompute.checkpoints or []]
+            if not ck and not any('recompute_id' in op.attrs for op in dist.global_block().ops):
+                # no checkpoints, no auto_parallel.recompute regions: the whole model is one
+                # segment (what the dygraph Engine's recompute(model) does)
+                ck = [vmap[o].name for o in _to_list(outs)]
+            passes.append(new_pass('auto_parallel_recompute', {
+                'checkpoints': ck or None, 'no_recompute_segments': st.recompute.no_recompute_segments}))
+        if st is not None and st.gradient_merge.enable and int(st.gradient_merge.k_steps) > 1:
+            passes.append(new_pass('auto_parallel_gradient_merge_pass', {
+                'k_steps': int(st.gradient_merge.k_steps), 'avg': bool(st.gradient_merge.avg)}))
+        if st is not None and st.sharding.enable:
+            group = None
+            if ins:
+                m = part.ctx.get(ins[0])
+                if m and m[0] >= 0:
+                    group = part.ctx.mesh.axis_group(m[0])
+            passes.append(new_pass('auto_parallel_sharding', {'stage': int(st.sharding.stage), 'group': group}))
+        if isinstance(getattr(self._optimizer, '_grad_clip', None), ClipGradByGlobalNorm):
+            passes.append(new_pass('auto_parallel_grad_clip'))
+        if st is not None and st.fused_passes.enable:
+            passes += [new_pass(n) for n in st.fused_passes.fused_passes_list or []]
+        if passes:
+            self._pass_context = PassManager(passes).apply([dist], [None])
 
     def _static_feed(self, batch, split):
         inputs, labels = self._split(batch, split)

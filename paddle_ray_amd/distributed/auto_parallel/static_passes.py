@@ -383,6 +383,7 @@ class Partitioner:
     def __init__(self, ctx, rank=None):
         self.ctx = ctx
         self.params = {}
+        self.param_dims = {}   # local parameter name -> its serial parameter's dims mapping
 
     def local_param(self, p):
         """The local shard of serial Parameter `p` in the partitioned program."""
@@ -391,6 +392,7 @@ class Partitioner:
     def _param(self, p):
         if id(p) not in self.params:
             self.params[id(p)] = _local_param(p, self.ctx.get(p), self.ctx.mesh)
+            self.param_dims[self.params[id(p)].name] = list(self.ctx.get(p))
         return self.params[id(p)]
 
     def _reshard(self, val, have, want):
@@ -457,7 +459,10 @@ class Partitioner:
                     if isinstance(a, Parameter) and _needs_grad(a):
                         uses.setdefault(id(a), set()).add(grad_dims(op, partial, outs, pos, want))
             deferred = {pid: next(iter(ds)) for pid, ds in uses.items() if len(ds) == 1 and next(iter(ds))}
+            prev_rc = G._RECOMPUTE_ID[0]
             for op, req, outs, partial in ctx.plans:
+                # the op's recompute region covers its resharding / partial-sum communication too
+                G._RECOMPUTE_ID[0] = op.attrs.get('recompute_id')
                 name = op.type.rsplit(':', 1)[-1]
                 top = (G._VarRef, Tensor)            # top-level operands: placed by the plan below
                 args = [a if isinstance(a, top) else self._nested(a, vmap) for a in op.args]
@@ -488,7 +493,10 @@ class Partitioner:
                     flat = [f + bias for f in flat]
                 for ov, nv in zip(op.out_vids, flat):
                     vmap[ov] = nv
+            G._RECOMPUTE_ID[0] = prev_rc
         dist.__dict__['_dist_context'] = ctx
+        dist.__dict__['_ap_param_dims'] = dict(self.param_dims)
+        dist.__dict__['_ap_mesh'] = mesh
         if sync:
             groups = {d: mesh.axis_group(d) for ds in sync.values() for d in ds}
             dist.__dict__['_ap_grad_sync'] = {n: [groups[d] for d in ds if groups[d] is not None]

@@ -90,6 +90,7 @@ class _CommState:
         self.localsgd = None
         self.steps = 0      # optimizer steps taken
         self.last_comm = 0  # localsgd: the step of the last parameter averaging
+        self.linked = []    # bucket states whose merge window this (optimize) state drives
 
     def final_micro(self):
         """This run completes a gradient-merge window (always True without merging)."""
@@ -162,13 +163,15 @@ class _ShardPlan:
             load[r] += _u(p).numel()
 
     def owned(self, params):
-        return [p for p in params if self.owner[p.name] == self.local]
+        """This rank's parameters: the ones it owns plus any outside the plan (updated by every
+        rank, e.g. parameters not replicated over the sharding group)."""
+        return [p for p in params if self.owner.get(p.name, self.local) == self.local]
 
     def broadcast(self, params):
         """Every owner sends its updated parameters (one flat broadcast per owner)."""
         pend = []
         for r in range(self.nranks):
-            ps = [p for p in params if self.owner[p.name] == r]
+            ps = [p for p in params if self.owner.get(p.name) == r]
             if not ps:
                 continue
             flat = torch.cat([_u(p).detach().reshape(-1) for p in ps])
@@ -204,6 +207,8 @@ def _fleet_optimize(state, opt, params, *grads, scaler=None):
     from ...static.graph import _optimize_fn
     final = state.final_micro()
     state.micro += 1
+    for s in state.linked:
+        s.micro += 1
     if not final:
         return None
     if state.shard is not None:
@@ -227,7 +232,14 @@ def _fleet_optimize(state, opt, params, *grads, scaler=None):
         prev_hook = None
         if isinstance(clip, ClipGradByGlobalNorm):
             prev_hook = clip._norm_hook
-            clip._norm_hook = lambda sq: global_l2_norm_sq(every_grad(True)).reshape(())
+            if getattr(prev_hook, 'dist_norm', None) is not None:
+                # a partitioned program's distributed clip: per parameter class over its mesh
+                # axes, reading the owned gradients and the reduced ones of the other owners
+                gmap = {id(p): g for p, g in others}
+                clip._norm_hook = lambda sq: prev_hook.dist_norm(
+                    lambda p: p._t.grad if id(p) in owned else gmap.get(id(p)), sq)
+            else:
+                clip._norm_hook = lambda sq: global_l2_norm_sq(every_grad(True)).reshape(())
         had_sg = '_scaler_grads' in opt.__dict__
         prev_sg = opt.__dict__.get('_scaler_grads')
         opt._scaler_grads = every_grad
@@ -248,8 +260,9 @@ def _fleet_optimize(state, opt, params, *grads, scaler=None):
     else:
         _optimize_fn(opt, params, *grads, scaler=scaler)
     state.steps += 1
-    for m in state.merged.values():
-        m.zero_()
+    for s in [state] + state.linked:
+        for m in s.merged.values():
+            m.zero_()
     ls = state.localsgd
     if ls is not None:
         # localsgd_optimizer.py:206: cond(step > begin_step, begin_localsgd, communicate) --
@@ -316,12 +329,14 @@ def _insert_bucketed(blk, n_before, pg, state, bucket_bytes, tag=''):
     return order, outs
 
 
-def insert_grad_sync(prog, n_before, pg, sync, bucket_mb=_DEFAULT_BUCKET_MB):
+def insert_grad_sync(prog, n_before, pg, sync, bucket_mb=_DEFAULT_BUCKET_MB, k_steps=1, avg=True):
     """Static auto-parallel: the gradients of parameters replicated over mesh axes (data
     parallel) are SUMMED over those axes' groups (the loss's own 1/n already scales them) in
     flat buckets, asynchronously inside the backward (parity: auto_parallel_data_parallel_
     optimization.py:57,132 `_fuse_allreduce`, GradientsGroup :727). ``sync``: local parameter
-    name -> [Group, ...]. Returns (params, grad vars) for the optimize op."""
+    name -> [Group, ...]. With ``k_steps`` > 1 each bucket accumulates locally and is reduced on
+    the merge window's last micro-step only. Returns (params, grad vars) for the optimize op;
+    the bucket states are ``prog._ap_grad_states``."""
     blk = prog.global_block()
     byname = {p.name: (p, g) for p, g in pg}
     keyed = {}
@@ -331,7 +346,7 @@ def insert_grad_sync(prog, n_before, pg, sync, bucket_mb=_DEFAULT_BUCKET_MB):
     states = []
     done = {}
     for t, (key, (groups, items)) in enumerate(sorted(keyed.items(), key=lambda kv: kv[0])):
-        st = _CommState(groups[0].process_group, groups[0].nranks, rank_avg=False,
+        st = _CommState(groups[0].process_group, groups[0].nranks, k_steps, avg, rank_avg=False,
                         extra_pgs=[g.process_group for g in groups[1:]])
         ps, gs = _insert_bucketed(blk, n_before, items, st, int(bucket_mb * (1 << 20)), tag=f'_{t}')
         for p, g in zip(ps, gs):
@@ -343,16 +358,107 @@ def insert_grad_sync(prog, n_before, pg, sync, bucket_mb=_DEFAULT_BUCKET_MB):
     return params, [done.get(p.name, g) for p, g in pg]
 
 
+def _majority_group(sync):
+    """The group most parameters reduce over (the data-parallel axis of a partitioned program)."""
+    count = {}
+    for groups in (sync or {}).values():
+        for g in groups:
+            count.setdefault(id(g), [g, 0])[1] += 1
+    return max(count.values(), key=lambda gc: gc[1])[0] if count else None
+
+
+def build_sync_optimize(prog, n_before, pg, opt, scaler, sync, k_steps, avg, shard, bucket_mb):
+    """The training tail of a program built by ``paddle.static`` minimize when a gradient all-reduce
+    (auto-parallel ``sync``), a gradient-merge window or sharding stage 1 applies (the
+    distributed passes auto_parallel_data_parallel_optimization / gradient_merge / sharding):
+    bucketed reductions inside the backward, then one ``fleet_optimize`` op that steps on the
+    window's last micro-step (the owners update, then broadcast, under sharding)."""
+    from ...static import graph as G
+    blk = prog.global_block()
+    k_steps = max(1, int(k_steps))
+    linked = []
+    params = [p for p, _ in pg]
+    gvars = [g for _, g in pg]
+    if sync:
+        params, gvars = insert_grad_sync(prog, n_before, pg, sync, bucket_mb, k_steps, avg)
+        linked += prog.__dict__['_ap_grad_states']
+    if k_steps > 1:
+        # gradients no group reduces still accumulate over the window (a local bucket state)
+        synced = {p.name for p in params if sync and p.name in sync and sync[p.name]}
+        local = [(p, g) for p, g in zip(params, gvars) if p.name not in synced]
+        if local:
+            st = _CommState(None, 1, k_steps, avg, rank_avg=False)
+            order, outs = _insert_bucketed(blk, n_before, local, st, int(bucket_mb * (1 << 20)),
+                                           tag='_local')
+            red = {p.name: g for p, g in zip(order, outs)}
+            gvars = [red.get(p.name, g) for p, g in zip(params, gvars)]
+            linked.append(st)
+    state = _CommState(None, 1, k_steps, avg)
+    state.linked = linked
+    if shard is not None and dist.is_initialized() and dist.get_world_size() > 1:
+        group = shard if shard != 'auto' else _majority_group(sync)
+        if group is None and not sync:
+            raise ValueError("sharding stage 1 needs the program's data-parallel gradient all-reduce "
+                             "(a partitioned program with replicated parameters); none was found")
+        members = [p for p in params if not sync or (p.name in sync and any(g is group for g in sync[p.name]))] \
+            if group is not None else params
+        state.shard = _ShardPlan(members, group)
+        opt._param_groups = []
+        opt._add_param_group({'params': state.shard.owned(params)})
+    op = G.OpDesc('fleet_optimize', _fleet_optimize, [state, opt, params] + [G._VarRef(g.vid) for g in gvars],
+                  {'scaler': scaler}, [g.vid for g in gvars], [], 'C', role='optimize')
+    blk.ops.append(op)
+    prog.__dict__['_no_graph'] = True
+    prog.__dict__['_fleet_state'] = state
+
+
+def strategy_with_pass_cfg(strategy, cfg):
+    """A copy of a fleet DistributedStrategy with the settings the distributed passes recorded."""
+    import copy
+    s = copy.copy(strategy)
+    for k, v in list(vars(s).items()):
+        if isinstance(v, dict):
+            s.__dict__[k] = dict(v)
+    if cfg.get('checkpoints'):
+        s.__dict__['recompute'] = True
+        s.__dict__['recompute_configs'] = {'checkpoints': list(cfg['checkpoints'])}
+    amp = cfg.get('amp')
+    if amp is not None:
+        s.__dict__['amp'] = True
+        s.__dict__['amp_configs'] = {
+            'init_loss_scaling': amp.get('init_loss_scaling', 32768.0),
+            'use_dynamic_loss_scaling': amp.get('use_dynamic_loss_scaling', True),
+            'use_bf16': amp['dtype'] == 'bfloat16', 'use_pure_fp16': amp.get('level') == 'O2',
+            'custom_white_list': list(amp.get('white') or ()),
+            'custom_black_list': list(amp.get('black') or ())}
+    k, avg = cfg.get('gradient_merge', (1, True))
+    if k > 1:
+        s.__dict__['gradient_merge'] = True
+        s.__dict__['gradient_merge_configs'] = {'k_steps': k, 'avg': avg}
+    if cfg.get('sharding') is not None:
+        s.__dict__['sharding'] = True
+        s.__dict__['sharding_configs'] = dict(s.sharding_configs, stage=1)
+    if 'bucket_mb' in cfg:
+        s.__dict__['fuse_grad_size_in_MB'] = cfg['bucket_mb']
+    return s
+
+
 def static_minimize(opt, loss, strategy, hcg, parameters=None):
     """Rewrite the program of ``loss`` for collective training (see the module docstring)."""
     from ...static import graph as G
     from ...static.amp import OptimizerWithMixedPrecision, decorate as amp_decorate
     prog = loss.block.program
     blk = prog.global_block()
+    orig_opt, orig_strategy = opt, strategy
+    if prog.__dict__.get('_pass_cfg'):
+        strategy = strategy_with_pass_cfg(strategy, prog.__dict__['_pass_cfg'])
+    fwd_vids = set(blk.vars)
     scaler, loss_scale = None, 1.0
     if getattr(strategy, 'amp', False) and not isinstance(opt, OptimizerWithMixedPrecision):
         cfg = dict(strategy.amp_configs or {})
-        opt = amp_decorate(opt, init_loss_scaling=cfg.get('init_loss_scaling', 32768),
+        from ...static.amp import AutoMixedPrecisionLists
+        lists = AutoMixedPrecisionLists(cfg.get('custom_white_list'), cfg.get('custom_black_list'))
+        opt = amp_decorate(opt, lists, init_loss_scaling=cfg.get('init_loss_scaling', 32768),
                            use_pure_fp16=cfg.get('use_pure_fp16', False),
                            use_bf16=cfg.get('use_bf16', False),
                            use_dynamic_loss_scaling=cfg.get('use_dynamic_loss_scaling', True))
@@ -370,6 +476,7 @@ def static_minimize(opt, loss, strategy, hcg, parameters=None):
         ps = parameters or [p for p in prog.all_parameters() if not p.stop_gradient]
         opt._param_groups = []
         opt._add_param_group({'params': list(ps)})
+    groups = G.save_param_groups(opt)
     if hcg is not None and (hcg.get_model_parallel_world_size() > 1 or
                             hcg.get_pipe_parallel_world_size() > 1):
         raise NotImplementedError(
@@ -405,9 +512,16 @@ def static_minimize(opt, loss, strategy, hcg, parameters=None):
             raise ValueError("strategy.recompute needs recompute_configs['checkpoints'] (the "
                              "static Variables or their names to keep in memory)")
         ckpts = [blk.var(n) if isinstance(n, str) else n for n in names]
+    pcfg = prog.__dict__.get('_pass_cfg') or {}
+    segments_fn = None
+    if ckpts is None and pcfg.get('recompute_annotated') is not None:
+        skip = list(pcfg['recompute_annotated'])
+        segments_fn = lambda fwd: G.annotated_segments(fwd, skip)  # noqa: E731
     n_before = len(blk.ops)
-    pg = G.append_backward(loss, parameters, loss_scale=loss_scale, checkpoints=ckpts)
+    pg = G.append_backward(loss, parameters, loss_scale=loss_scale, checkpoints=ckpts,
+                           segments_fn=segments_fn)
     params = [p for p, _ in pg]
+    prog.__dict__['_minimize_params'] = list(params)
     if sharding:
         state.shard = _ShardPlan(params, hcg.get_sharding_parallel_group()
                                  if hcg is not None and hcg.get_sharding_parallel_world_size() > 1
@@ -434,5 +548,11 @@ def static_minimize(opt, loss, strategy, hcg, parameters=None):
     # broadcasts) and async work handles are kept out of HIP-graph capture
     prog.__dict__['_no_graph'] = True
     prog.__dict__['_fleet_state'] = state
+    for hook in pcfg.get('minimize_hooks', ()):
+        hook(prog, opt)
+    prog.__dict__['_train_meta'] = {
+        'fwd_vids': fwd_vids, 'kind': 'fleet',
+        'rebuild': lambda: (G.restore_param_groups(opt, groups),
+                            static_minimize(orig_opt, loss, orig_strategy, hcg, parameters))}
     prog._bump()
     return None, pg

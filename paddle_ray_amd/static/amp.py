@@ -45,13 +45,8 @@ class OptimizerWithMixedPrecision:
         return self._scaler.get_loss_scaling()
 
     def _tag_program(self, prog):
-        import torch
-        dt = torch.bfloat16 if self._dtype == 'bfloat16' else torch.float16
-        cfg = {'dtype': dt, 'level': self._level, 'white': set(self._amp_lists.white_list),
-               'black': set(self._amp_lists.black_list)}
-        for op in prog.global_block().ops:
-            if op.role == 'forward':
-                op.attrs['amp'] = cfg
+        tag_program(prog, {'dtype': self._dtype, 'level': self._level,
+                           'white': self._amp_lists.white_list, 'black': self._amp_lists.black_list})
 
     def minimize(self, loss, startup_program=None, parameters=None, no_grad_set=None):
         from .graph import _static_minimize
@@ -64,6 +59,24 @@ class OptimizerWithMixedPrecision:
 
     def __getattr__(self, k):
         return getattr(self._optimizer, k)
+
+
+def tag_program(prog, amp):
+    """Tag every forward op (and the grad op built from it) with the AMP policy ``amp`` =
+    {dtype: 'float16' | 'bfloat16', level: 'O1' | 'O2', white, black}: the Executor replays each
+    op under ``auto_cast`` with it."""
+    import torch
+    dt = amp['dtype']
+    if isinstance(dt, str):
+        dt = torch.bfloat16 if dt == 'bfloat16' else torch.float16
+    cfg = {'dtype': dt, 'level': amp.get('level', 'O1'), 'white': set(amp.get('white') or ()),
+           'black': set(amp.get('black') or ())}
+    for op in prog.global_block().ops:
+        if op.role == 'forward' or op.role == 'recompute':
+            op.attrs['amp'] = cfg
+        elif op.role == 'backward' and 'fwd' in op.attrs:
+            op.attrs['amp'] = cfg
+    prog._bump()
 
 
 class _ScaleRef:

@@ -482,11 +482,16 @@ def record_op(op_type, fn, args, kwargs, out_specs=None):
     return _rebuild(tmpl, iter(out_vars))
 
 
+_RECOMPUTE_ID = [None]   # set while an auto_parallel.recompute(...)-wrapped callable records
+
+
 def _record_amp(op):
     """Ops recorded inside ``paddle.amp.auto_cast`` replay under the same AMP policy (and
-    carry the enclosing device_guard's device)."""
+    carry the enclosing device_guard's device and auto_parallel.recompute region)."""
     if _DEVICE[0] is not None:
         op.attrs['device'] = _DEVICE[0]
+    if _RECOMPUTE_ID[0] is not None:
+        op.attrs['recompute_id'] = _RECOMPUTE_ID[0]
     from ..amp import amp_state
     st = amp_state()
     if st['enabled']:
@@ -740,6 +745,29 @@ def _recompute_segments(fwd, ck_vids):
     return segs
 
 
+def annotated_segments(fwd, skip=()):
+    """[(lo, hi)] recompute segments from ``auto_parallel.recompute`` regions: each maximal run of
+    forward ops carrying one ``recompute_id`` (single-op runs are not worth recomputing); the
+    ``skip`` indices (``no_recompute_segments``) are dropped (reference auto_parallel_recompute.py
+    :94 get_recompute_segments)."""
+    segs, i = [], 0
+    while i < len(fwd):
+        rid = fwd[i].attrs.get('recompute_id')
+        j = i + 1
+        if rid is not None:
+            while j < len(fwd) and fwd[j].attrs.get('recompute_id') == rid:
+                j += 1
+            if j - i > 1:
+                segs.append((i, j))
+        i = j
+    for k in sorted(set(skip), reverse=True):
+        if not 0 <= k < len(segs):
+            raise ValueError(f"no_recompute_segments index {k} out of range: the program has "
+                             f"{len(segs)} recompute segments")
+        segs.pop(k)
+    return segs
+
+
 def _remap_refs(obj, remap):
     if isinstance(obj, _VarRef):
         return _VarRef(remap.get(obj.vid, obj.vid))
@@ -787,13 +815,16 @@ def _emit_recompute(blk, seg_ops, ctrl_vids):
 
 
 def _build_backward(prog, targets, inputs=(), target_grads=None, no_grad_set=None,
-                    params=None, loss_scale=1.0, checkpoints=None):
+                    params=None, loss_scale=1.0, checkpoints=None, segments_fn=None):
     """Emit grad ops for ``targets`` w.r.t. ``inputs`` (Variables) and the trainable
     parameters. Returns ({input vid: grad var}, {param name: grad var})."""
     blk = prog.global_block()
     no_grad = {getattr(x, 'name', x) for x in (no_grad_set or ())}
     fwd = [op for op in blk.ops if op.role == 'forward']
-    segs = _recompute_segments(fwd, _checkpoint_vids(checkpoints)) if checkpoints else []
+    if segments_fn is not None:
+        segs = segments_fn(fwd)
+    else:
+        segs = _recompute_segments(fwd, _checkpoint_vids(checkpoints)) if checkpoints else []
     seg_of = {}
     for si, (lo, hi) in enumerate(segs):
         for op in fwd[lo:hi]:
@@ -921,15 +952,17 @@ def _build_backward(prog, targets, inputs=(), target_grads=None, no_grad_set=Non
 
 
 def append_backward(loss, parameter_list=None, no_grad_set=None, callbacks=None,
-                    checkpoints=None, loss_scale=1.0):
-    """Append grad ops for ``loss``; returns [(param, param@GRAD var)]."""
+                    checkpoints=None, loss_scale=1.0, segments_fn=None):
+    """Append grad ops for ``loss``; returns [(param, param@GRAD var)]. ``segments_fn(forward
+    ops) -> [(lo, hi)]`` picks the recompute segments directly (annotated regions)."""
     prog = loss.block.program
     blk = prog.global_block()
     params = None
     if parameter_list:
         params = [prog._params[p] if isinstance(p, str) else p for p in parameter_list]
     _, p_grads = _build_backward(prog, [loss], no_grad_set=no_grad_set, params=params,
-                                 loss_scale=loss_scale, checkpoints=checkpoints)
+                                 loss_scale=loss_scale, checkpoints=checkpoints,
+                                 segments_fn=segments_fn)
     if checkpoints:
         prog.__dict__['_recompute_checkpoints'] = [c.name for c in checkpoints]
     out = []
@@ -986,29 +1019,116 @@ register_static_op('optimize', _optimize_fn)
 
 
 def _static_minimize(opt, loss, parameters=None, scaler=None, loss_scale=1.0, checkpoints=None):
+    """Backward + optimize op for ``loss``'s program. Settings recorded on the program by
+    ``paddle.distributed.passes`` (``prog._pass_cfg``: amp, recompute checkpoints, gradient
+    merge, sharding stage 1, gradient bucket size) are honoured here; the arguments are kept so
+    a pass applied AFTER minimize can strip the training ops and rebuild them."""
     prog = loss.block.program
     check_single_device(prog)
+    args = dict(opt=opt, loss=loss, parameters=parameters, scaler=scaler, loss_scale=loss_scale,
+                checkpoints=checkpoints)
+    cfg = prog.__dict__.get('_pass_cfg') or {}
+    blk = prog.global_block()
+    segments_fn = None
+    if checkpoints is None and cfg.get('checkpoints'):
+        checkpoints = [blk.var(c) if isinstance(c, str) else c for c in cfg['checkpoints']]
+    elif checkpoints is None and cfg.get('recompute_annotated') is not None:
+        skip = list(cfg['recompute_annotated'])
+        segments_fn = lambda fwd: annotated_segments(fwd, skip)  # noqa: E731
+    amp = cfg.get('amp')
+    if amp is not None:
+        from .amp import tag_program, _ScaleRef
+        tag_program(prog, amp)
+        if scaler is None and amp.get('scaler') is not None:
+            scaler, loss_scale = amp['scaler'], _ScaleRef(amp['scaler'])
+        if amp.get('level') == 'O2':
+            opt._multi_precision = True
     if not opt._parameter_list:
         ps = parameters or [p for p in prog.all_parameters() if not p.stop_gradient]
         opt._param_groups = []
         opt._add_param_group({'params': list(ps)})
-    blk = prog.global_block()
+    groups = save_param_groups(opt)
+    fwd_vids = set(blk.vars)
     n_before = len(blk.ops)
-    pg = append_backward(loss, parameters, loss_scale=loss_scale, checkpoints=checkpoints)
+    pg = append_backward(loss, parameters, loss_scale=loss_scale, checkpoints=checkpoints,
+                         segments_fn=segments_fn)
     params = [p for p, _ in pg]
     gvars = [g for _, g in pg]
+    prog.__dict__['_minimize_params'] = list(params)
     sync = prog.__dict__.get('_ap_grad_sync')
-    if sync:
+    k_steps, avg = cfg.get('gradient_merge', (1, True))
+    shard = cfg.get('sharding')
+    if sync or k_steps > 1 or shard is not None:
         # auto-parallel partitioned program: bucketed async gradient all-reduce over the mesh
-        # axes the parameters are replicated on (static_passes.Partitioner records them)
-        from ..distributed.fleet.meta_optimizers import insert_grad_sync
-        params, gvars = insert_grad_sync(prog, n_before, pg, sync,
-                                         prog.__dict__.get('_ap_bucket_mb', 32))
-    op = OpDesc('optimize', _optimize_fn, [opt, params] + [_VarRef(g.vid) for g in gvars],
-                {'scaler': scaler}, [g.vid for g in gvars], [], 'C', role='optimize')
-    blk.ops.append(op)
+        # axes the parameters are replicated on (static_passes.Partitioner records them), the
+        # merge window and the stage-1 owner update + broadcast (meta_optimizers)
+        from ..distributed.fleet.meta_optimizers import build_sync_optimize
+        build_sync_optimize(prog, n_before, pg, opt, scaler, sync, k_steps, avg, shard,
+                            cfg.get('bucket_mb', prog.__dict__.get('_ap_bucket_mb', 32)))
+    else:
+        op = OpDesc('optimize', _optimize_fn, [opt, params] + [_VarRef(g.vid) for g in gvars],
+                    {'scaler': scaler}, [g.vid for g in gvars], [], 'C', role='optimize')
+        blk.ops.append(op)
+    for hook in cfg.get('minimize_hooks', ()):
+        hook(prog, opt)
+    prog.__dict__['_train_meta'] = {'fwd_vids': fwd_vids, 'kind': 'plain',
+                                    'rebuild': lambda: (restore_param_groups(opt, groups),
+                                                        _static_minimize(**args))}
     prog._bump()
     return None, pg
+
+
+def _inner_opt(opt):
+    while '_optimizer' in getattr(opt, '__dict__', {}):
+        opt = opt.__dict__['_optimizer']
+    return opt
+
+
+def save_param_groups(opt):
+    """The optimizer's parameter groups as minimize saw them (sharding later narrows them to the
+    owned parameters; a rebuild restores them first)."""
+    return [dict(g, params=list(g['params'])) for g in _inner_opt(opt)._param_groups]
+
+
+def restore_param_groups(opt, groups):
+    o = _inner_opt(opt)
+    o._param_groups = [dict(g, params=list(g['params'])) for g in groups]
+    o._fused_plan = None
+
+
+def strip_training(prog):
+    """Undo append_backward / minimize: drop the grad, recompute, communication and optimize ops,
+    the RNG snapshots, the forward ops' autograd-context links and the vars only those ops made.
+    The program is its forward again (``_train_meta['rebuild']`` re-creates the training ops)."""
+    blk = prog.global_block()
+    meta = prog.__dict__.get('_train_meta') or {}
+    keep = [op for op in blk.ops if op.role == 'forward' and op.type != 'recompute_rng_save']
+    for op in keep:
+        op.ctx_vid = None
+        op.attrs.pop('diff_in', None)
+        op.attrs.pop('diff_params', None)
+    blk.ops[:] = keep
+    fwd_vids = meta.get('fwd_vids')
+    if fwd_vids is not None:
+        for vid in [v for v in blk.vars if v not in fwd_vids]:
+            del blk.vars[vid]
+    for k in ('_param_grads', '_recompute_checkpoints', '_fleet_state', '_ap_grad_states',
+              '_no_graph', '_train_meta'):
+        prog.__dict__.pop(k, None)
+    prog._plans = {}
+    prog._bump()
+
+
+def rebuild_training(prog):
+    """Re-run the program's minimize (after a pass changed ``_pass_cfg``). False when the program
+    has no training ops yet (the settings then apply at its minimize)."""
+    meta = prog.__dict__.get('_train_meta')
+    if meta is None:
+        return False
+    rebuild = meta['rebuild']
+    strip_training(prog)
+    rebuild()
+    return True
 
 
 class RecomputeOptimizer:
