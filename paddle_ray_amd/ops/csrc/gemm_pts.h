@@ -48,7 +48,9 @@ __device__ __forceinline__ float row16_sum(float x) {
   return x;
 }
 
-template <typename T, typename CF, bool AK, bool BK, int E, bool BETA>
+// SPO: MFMA slots between two refill pieces of a K-step (0: spread the pieces over the whole
+// window between the two barriers; smaller values issue the refill earlier in the step)
+template <typename T, typename CF, bool AK, bool BK, int E, bool BETA, int SPO = 0>
 __global__ __launch_bounds__(CF::NT, 1) void gemm_pts_kernel(const uint16_t* __restrict__ A,
                                                              const uint16_t* __restrict__ B,
                                                              const uint16_t* __restrict__ bias,
@@ -157,7 +159,8 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_pts_kernel(const uint16_t* __r
     constexpr bool ZPRE = decltype(zpre_c)::value && ZOP;
     constexpr int NRD = TI + TJ, NDMA = NDA + NDB, NM = TI * TJ, F = 2 * NM;
     constexpr int BA = NRD + 4, BB = F - NRD - 3;
-    constexpr int SP = (BB - BA - 1) / NDMA > 0 ? (BB - BA - 1) / NDMA : 1;
+    constexpr int SP0 = (BB - BA - 1) / NDMA > 0 ? (BB - BA - 1) / NDMA : 1;
+    constexpr int SP = SPO > 0 ? SPO : SP0;
     static_assert(BB >= NM && BA + 1 + (NDMA - 1) * SP < BB, "pts: fillers exceed the K-step's MFMAs");
     if constexpr (STEADY) {
       dcur = true;

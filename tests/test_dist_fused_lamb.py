@@ -122,7 +122,7 @@ def test_lamb_shard_kernels_match_fp32_reference():
         torch.cuda.synchronize()
         np.testing.assert_allclose(dn.cpu().numpy(), rn.numpy(), rtol=1e-4)
         np.testing.assert_allclose(dm.cpu().numpy(), rm.numpy(), rtol=1e-5, atol=1e-7)
-        np.testing.assert_allclose(dv.cpu().numpy(), rv.numpy(), rtol=1e-5, atol=1e-9)
+        np.testing.assert_allclose(dv.cpu().numpy(), rv.numpy(), rtol=5e-5, atol=1e-9)
         np.testing.assert_allclose(dw.cpu().numpy(), rw.numpy(), rtol=1e-5, atol=1e-6)
         np.testing.assert_allclose(dout.cpu().float().numpy(), rout.float().numpy(), rtol=1e-2, atol=1e-2)
         untouched = torch.ones(n, dtype=torch.bool)

@@ -515,3 +515,45 @@ def test_engine_static_strategy_passes(tmp_path):
         assert o['passes'] == ['auto_parallel_recompute', 'auto_parallel_gradient_merge_pass',
                                'auto_parallel_grad_clip'], o['passes']
         assert 'recompute_rng_swap' in o['ops'] and o['k'] == 2
+
+
+@pytest.mark.gpu
+def test_fused_feedforward_pass_on_gpu_bf16():
+    """On the MI355X the fused ops run the in-tree HIP kernels (MLP GEMM epilogues, add +
+    dropout + LayerNorm): the fused bf16 program trains like the unfused one."""
+    import torch
+    import paddle_ray_amd as paddle
+    import paddle_ray_amd.nn as nn
+    import paddle_ray_amd.nn.functional as F
+    from paddle_ray_amd import static
+    from paddle_ray_amd.distributed.passes import new_pass
+    paddle.set_device('gpu:0')
+    paddle.enable_static()
+    try:
+        def build(fuse):
+            paddle.seed(5)
+            paddle.set_default_dtype('bfloat16')
+            main = static.Program()
+            with static.program_guard(main):
+                x = static.data('x', [256, 512], 'bfloat16')
+                l1, l2, ln = nn.Linear(512, 2048), nn.Linear(2048, 512), nn.LayerNorm(512)
+                z = ln(x + F.dropout(l2(F.gelu(l1(x), approximate=True)), 0.0))
+                loss = paddle.mean(z.astype('float32') ** 2)
+                if fuse:
+                    new_pass('fused_feedforward').apply([main], [None])
+                paddle.optimizer.AdamW(1e-3, multi_precision=True).minimize(loss)
+            paddle.set_default_dtype('float32')
+            return main, loss
+        xv = np.random.RandomState(0).randn(256, 512).astype('float32')
+        feed = {'x': torch.from_numpy(xv).to(torch.bfloat16).cuda()}
+        out = []
+        for fuse in (False, True):
+            m, l = build(fuse)
+            exe = static.Executor()
+            out.append([float(exe.run(m, feed=feed, fetch_list=[l])[0]) for _ in range(4)])
+            if fuse:
+                assert _fwd_types(m)[:2] == ['fused_mlp_gelu', 'fused_add_dropout_ln']
+        np.testing.assert_allclose(out[1], out[0], rtol=2e-2, atol=2e-3)
+        assert out[1][-1] < out[1][0]
+    finally:
+        paddle.disable_static()
