@@ -42,6 +42,9 @@ extern "C" int pra_gemm_alt(int cfg, int layout, const void* A, const void* B, c
 extern "C" int pra_gemm_pts_w4(int layout, const void* A, const void* B, const void* bias, void* C, void* Z,
                                float* colsum, int M, int N, int K, int lda, int ldb, int ldc, int ldz, int dtype,
                                int epi, int beta, hipStream_t s);
+extern "C" int pra_gemm_pts_w4b(int layout, const void* A, const void* B, const void* bias, void* C, void* Z,
+                                float* colsum, int M, int N, int K, int lda, int ldb, int ldc, int ldz, int dtype,
+                                int epi, int beta, hipStream_t s);
 extern "C" int pra_gemm_pts_w8(int layout, const void* A, const void* B, const void* bias, void* C, void* Z,
                                float* colsum, int M, int N, int K, int lda, int ldb, int ldc, int ldz, int dtype,
                                int epi, int beta, hipStream_t s);
@@ -143,7 +146,8 @@ void launch_e(const void* A, const void* B, const void* bias, void* C, void* Z, 
     // with mask bit 32 or a per-call persistent request (the fused GELU forward: 486 vs 517 us
     // per-tile at 16384 x 8192 x 2048, profiles/r5/gemm_fwd_probe.log); 8 waves otherwise
     const bool w4 = (layout == 1 && !(pts_mask() & 16)) || (layout == 0 && ((pts_mask() & 32) || g_force_pts));
-    if ((w4 ? pra_gemm_pts_w4 : pra_gemm_pts_w8)(layout, A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, kBF16,
+    static const bool buf = getenv("PRA_PTS_BUF") && atoi(getenv("PRA_PTS_BUF")) == 1;
+    if ((w4 ? (buf ? pra_gemm_pts_w4b : pra_gemm_pts_w4) : pra_gemm_pts_w8)(layout, A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, kBF16,
                                                  E, beta, s) == 0)
       return;
   }

@@ -67,6 +67,17 @@ class DeviceEvent:
     def dur_ns(self):
         return self.end_ns - self.start_ns
 
+    # a kernel's "thread" in the statistics tables is its stream; its device time is itself
+    @property
+    def tid(self):
+        return self.stream
+
+    @property
+    def gpu_ns(self):
+        return self.end_ns - self.start_ns
+
+    kernels = None
+
 
 class MemEvent:
     __slots__ = ('name', 'place', 'bytes', 'type', 'ts_ns')

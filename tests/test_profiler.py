@@ -148,3 +148,25 @@ def test_timer_only_and_nested_reader_pause():
     assert 'batch_cost' in info and 'reader_cost' not in info
     assert prof.profiler_result is None and prof.summary() == ''
     assert benchmark().current_event is None
+
+
+def test_statistics_with_device_events_synthetic():
+    """Kernel / Device / Distributed views over device records (what a GPU run merges in):
+    kernel totals, GPU sort keys and the communication overlap, checked on synthetic events."""
+    from paddle_ray_amd.profiler.result import ProfilerResult, HostEvent, DeviceEvent, TracerEventType as TT
+    from paddle_ray_amd.profiler.statistic import StatisticData, build_table, SortedKeys
+    host = [HostEvent('ProfileStep#0', TT.ProfileStep, 0, 1000, 1)]
+    dev = [DeviceEvent('pra::gemm_a', TT.Kernel, 0, 300), DeviceEvent('pra::gemm_a', TT.Kernel, 400, 500),
+           DeviceEvent('pra::small', TT.Kernel, 500, 520), DeviceEvent('ncclDevKernel_AllReduce', TT.Kernel, 250, 450)]
+    res = ProfilerResult(host, dev, steps=[(0, 0, 1000)])
+    data = StatisticData(res)
+    tot = {k[0]: it.gpu for k, it in data.kernel_items.items()}
+    assert tot == {'pra::gemm_a': 400, 'pra::small': 20, 'ncclDevKernel_AllReduce': 200}
+    busy, _ = data.device_union(data.kernels)
+    assert busy == 520
+    t_total = build_table(data, SortedKeys.GPUTotal, views=[profiler.SummaryView.KernelView], time_unit='ns')
+    t_min = build_table(data, SortedKeys.GPUMin, views=[profiler.SummaryView.KernelView], time_unit='ns')
+    rows = lambda t: [l.split()[0] for l in t.splitlines() if l.startswith(('pra::', 'nccl'))]  # noqa: E731
+    assert rows(t_total)[0] == 'pra::gemm_a' and rows(t_min)[0] == 'pra::small'
+    dist = build_table(data, SortedKeys.CPUTotal, views=[profiler.SummaryView.DistributedView], time_unit='ns')
+    assert 'Communication' in dist or 'communication' in dist.lower()
