@@ -412,6 +412,28 @@ def build_sync_optimize(prog, n_before, pg, opt, scaler, sync, k_steps, avg, sha
     prog.__dict__['_fleet_state'] = state
 
 
+def _static_pipeline(opt, loss, strategy, hcg, parameters, scaler):
+    """strategy.pipeline: the program split by device_guard into one stage per rank of the
+    pipeline group (static/pipeline.py; reference meta_optimizers/pipeline_optimizer.py:198)."""
+    from ...static.pipeline import build_pipeline
+    for flag in ('sharding', 'localsgd', 'gradient_merge', 'recompute', 'lamb', 'lars'):
+        if getattr(strategy, flag, False):
+            raise NotImplementedError(f"static pipeline together with strategy.{flag} is not supported")
+    if scaler is not None:
+        raise NotImplementedError("static pipeline with fp16 loss scaling is not supported (use bf16)")
+    cfg = dict(strategy.pipeline_configs or {})
+    n_micro = int(cfg.get('accumulate_steps', 1))
+    pp_group = dp_group = None
+    if hcg is not None:
+        if hcg.get_model_parallel_world_size() > 1:
+            raise NotImplementedError("static pipeline with tensor parallelism is not supported")
+        if hcg.get_pipe_parallel_world_size() > 1:
+            pp_group = hcg.get_pipe_parallel_group()
+        if hcg.get_data_parallel_world_size() > 1:
+            dp_group = hcg.get_data_parallel_group()
+    return build_pipeline(opt, loss, n_micro, cfg.get('schedule_mode', '1F1B'), parameters, pp_group, dp_group)
+
+
 def strategy_with_pass_cfg(strategy, cfg):
     """A copy of a fleet DistributedStrategy with the settings the distributed passes recorded."""
     import copy
@@ -477,11 +499,13 @@ def static_minimize(opt, loss, strategy, hcg, parameters=None):
         opt._param_groups = []
         opt._add_param_group({'params': list(ps)})
     groups = G.save_param_groups(opt)
+    if getattr(strategy, 'pipeline', False):
+        return _static_pipeline(opt, loss, strategy, hcg, parameters, scaler)
     if hcg is not None and (hcg.get_model_parallel_world_size() > 1 or
                             hcg.get_pipe_parallel_world_size() > 1):
         raise NotImplementedError(
-            "static-mode fleet supports data parallel, sharding stage 1, gradient merge and "
-            "localsgd; for tensor / pipeline parallel static programs use "
+            "static-mode fleet supports data parallel, pipeline (strategy.pipeline), sharding "
+            "stage 1, gradient merge and localsgd; for tensor-parallel static programs use "
             "paddle.distributed.auto_parallel (static Engine)")
     world = dist.get_world_size() if dist.is_initialized() else 1
     k = 1
@@ -496,12 +520,6 @@ def static_minimize(opt, loss, strategy, hcg, parameters=None):
         if stage != 1:
             raise NotImplementedError(f"static-mode sharding supports stage 1 (got stage {stage}); "
                                       "use dygraph group_sharded_parallel for stages 2/3")
-    if getattr(strategy, 'pipeline', False):
-        # (parity gap, raised rather than ignored: the reference's PipelineOptimizer splits the
-        # program by device_guard into per-stage sections, fluid/optimizer.py:4494)
-        raise NotImplementedError(
-            "strategy.pipeline is not supported for static-graph programs; use fleet dygraph "
-            "pipeline parallel (PipelineLayer + fleet.distributed_model)")
     G.check_single_device(prog, 'fleet.distributed_optimizer(...).minimize')
     ckpts = None
     if getattr(strategy, 'recompute', False):

@@ -38,3 +38,4 @@ from .graph import (Program, Block, Variable, Executor, global_scope, scope_guar
 from . import nn  # noqa: E402
 from .sequence_lod import create_lod_tensor  # noqa: E402,F401
 from . import amp  # noqa: E402
+from .pipeline import PipelineOptimizer  # noqa: E402,F401

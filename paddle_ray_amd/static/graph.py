@@ -284,9 +284,9 @@ _DEVICE = [None]
 @contextlib.contextmanager
 def device_guard(device=None):
     """Ops recorded inside carry ``attrs['device']`` (parity: fluid/framework.py device_guard,
-    the op_device attribute PipelineOptimizer splits a program by). One device per program is
-    what the executor runs; ``minimize`` raises for a program spread over several devices (a
-    static pipeline split is not implemented: use fleet dygraph PipelineParallel)."""
+    the op_device attribute PipelineOptimizer splits a program by). A program spread over
+    several GPUs trains through the static pipeline (PipelineOptimizer / fleet
+    strategy.pipeline: one stage per rank, static/pipeline.py); a plain ``minimize`` raises."""
     prev = _DEVICE[0]
     _DEVICE[0] = device
     try:
@@ -313,8 +313,8 @@ def check_single_device(prog, what='minimize'):
     if len(gpus) > 1:
         raise NotImplementedError(
             f"{what}: the program places ops on {len(gpus)} devices with static.device_guard "
-            f"({sorted(devs)}); a static-graph pipeline split is not implemented -- use "
-            "fleet dygraph pipeline parallel (PipelineLayer + fleet.distributed_model)")
+            f"({sorted(devs)}); train it as a pipeline (paddle.static.PipelineOptimizer or fleet "
+            "strategy.pipeline, one rank per stage)")
 
 
 def data(name, shape, dtype=None, lod_level=0):
@@ -1356,6 +1356,9 @@ class Executor:
             use_graph = program._build_strategy.use_hip_graph
             program = program._program
         prog = program or default_main_program()
+        if prog.__dict__.get('_pipeline') is not None:
+            # a pipeline stage (static/pipeline.py): micro-batched schedule with p2p transfers
+            return prog._pipeline.run(self, feed or {}, list(fetch_list or []), return_numpy)
         if prog.__dict__.get('_no_graph'):
             use_graph = False   # fleet collective programs (meta_optimizers.static_minimize)
         if prog._is_startup or not prog.global_block().ops and not fetch_list:

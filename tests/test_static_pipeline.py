@@ -1,0 +1,186 @@
+"""Static-graph pipeline parallelism (reference: fluid/optimizer.py PipelineOptimizer, fleet
+pipeline_optimizer.py; test/collective/fleet/pipeline_mnist*.py style: a pipelined run must
+train like the single-process run of the same program). gloo ranks on CPU."""
+import numpy as np
+import pytest
+
+from dist_utils import run_ranks
+
+B, H, F_, C = 8, 6, 16, 4
+
+
+def _program(guard, clip=None, skip=False, three=False):
+    """x -> [gpu:0] Linear -> tanh -> [gpu:1] Linear -> gelu (-> [gpu:2] Linear) -> CE loss."""
+    import paddle_ray_amd as paddle
+    import paddle_ray_amd.nn as nn
+    import paddle_ray_amd.nn.functional as F
+    from paddle_ray_amd import static
+    import contextlib
+    paddle.seed(11)
+    g = static.device_guard if guard else (lambda d: contextlib.nullcontext())
+    main = static.Program()
+    with static.program_guard(main):
+        x = static.data('x', [-1, H], 'float32')
+        y = static.data('y', [-1, 1], 'int64')
+        with g('gpu:0'):
+            l1 = nn.Linear(H, F_)
+            h0 = paddle.tanh(l1(x))
+        with g('gpu:1'):
+            l2 = nn.Linear(F_, F_ if three else C)
+            h1 = F.gelu(l2(h0))
+            if skip:
+                h1 = h1 + h0[:, :h1.shape[1]] * 0.5        # a skip edge 0 -> 1 used twice
+        params = [l1.weight, l1.bias, l2.weight, l2.bias]
+        if three:
+            with g('gpu:2'):
+                l3 = nn.Linear(F_, C)
+                h1 = l3(h1) + 0.1 * paddle.sum(h0, axis=1, keepdim=True)   # skip edge 0 -> 2
+            params += [l3.weight, l3.bias]
+        loss = F.cross_entropy(h1, y)            # unguarded: follows its inputs' stage
+    return main, loss, params
+
+
+def _data(steps, bs):
+    rs = np.random.RandomState(5)
+    return [{'x': rs.randn(bs, H).astype('float32'), 'y': rs.randint(0, C, (bs, 1)).astype('int64')}
+            for _ in range(steps)]
+
+
+def _serial(clip, skip, three, opt_name='momentum'):
+    import paddle_ray_amd as paddle
+    from paddle_ray_amd import static
+    paddle.enable_static()
+    main, loss, params = _program(False, clip, skip, three)
+    with static.program_guard(main):
+        _opt(opt_name, clip).minimize(loss)
+    exe = static.Executor()
+    losses = [float(exe.run(main, feed=f, fetch_list=[loss])[0]) for f in _data(3, B)]
+    out = [p.numpy() for p in params]
+    paddle.disable_static()
+    return losses, out
+
+
+def _opt(name, clip):
+    import paddle_ray_amd as paddle
+    c = paddle.nn.ClipGradByGlobalNorm(clip) if clip else None
+    if name == 'adam':
+        return paddle.optimizer.AdamW(0.01, grad_clip=c)
+    return paddle.optimizer.Momentum(0.3, momentum=0.9, grad_clip=c)
+
+
+def _pipe(rank, world, n_micro, schedule, clip, skip, three, use_fleet, opt_name, dp=1):
+    import paddle_ray_amd as paddle
+    from paddle_ray_amd import static
+    paddle.enable_static()
+    main, loss, params = _program(True, clip, skip, three)
+    with static.program_guard(main):
+        if use_fleet:
+            from paddle_ray_amd.distributed import fleet
+            st = fleet.DistributedStrategy()
+            st.pipeline = True
+            st.pipeline_configs = {'accumulate_steps': n_micro, 'micro_batch_size': B // n_micro,
+                                   'schedule_mode': schedule}
+            st.hybrid_configs = {'dp_degree': dp, 'mp_degree': 1, 'pp_degree': world // dp}
+            fleet.init(is_collective=True, strategy=st)
+            fleet.distributed_optimizer(_opt(opt_name, clip)).minimize(loss)
+        else:
+            static.PipelineOptimizer(_opt(opt_name, clip), num_microbatches=n_micro,
+                                     schedule_mode=schedule).minimize(loss)
+    exe = static.Executor()
+    losses = [float(exe.run(main, feed=f, fetch_list=[loss])[0]) for f in _data(3, B)]
+    pipe = main._pipeline
+    mine = {p.name for p in pipe.params}
+    out = {i: p.numpy() for i, p in enumerate(params) if p.name in mine}
+    n_ops = (len(pipe.fwd_ops), len(pipe.bwd_ops))
+    paddle.disable_static()
+    return {'losses': losses, 'params': out, 'stage': pipe.stage, 'ops': n_ops,
+            'sends': len(pipe.fsend) + len(pipe.bsend)}
+
+
+@pytest.mark.parametrize('n_micro,schedule,use_fleet', [(1, 'F-then-B', False), (4, 'F-then-B', False),
+                                                        (4, '1F1B', True), (2, '1F1B', False)])
+def test_static_pipeline_matches_serial_2stages(tmp_path, n_micro, schedule, use_fleet):
+    ref_losses, ref = _serial(None, False, False)
+    res = run_ranks(_pipe, 2, tmp_path, args=(n_micro, schedule, None, False, False, use_fleet, 'momentum'))
+    got = {}
+    for o in res:
+        np.testing.assert_allclose(o['losses'], ref_losses, rtol=1e-5, atol=1e-6)
+        got.update(o['params'])
+        assert o['ops'][0] > 0 and o['ops'][1] > 0 and o['sends'] >= 1
+    assert sorted(got) == [0, 1, 2, 3]
+    for i, p in got.items():
+        np.testing.assert_allclose(p, ref[i], rtol=1e-5, atol=1e-6)
+    assert ref_losses[-1] < ref_losses[0]
+
+
+def test_static_pipeline_with_data_parallel_2x2(tmp_path):
+    """fleet hybrid dp 2 x pp 2: each stage's gradients are averaged over its data-parallel
+    replica (same batch on both replicas here: the serial run is the reference)."""
+    ref_losses, ref = _serial(0.05, False, False)
+    res = run_ranks(_pipe, 4, tmp_path, args=(2, '1F1B', 0.05, False, False, True, 'momentum', 2))
+    for o in res:
+        np.testing.assert_allclose(o['losses'], ref_losses, rtol=1e-5, atol=1e-6)
+        for i, p in o['params'].items():
+            np.testing.assert_allclose(p, ref[i], rtol=1e-5, atol=1e-6)
+    assert sorted({o['stage'] for o in res}) == [0, 1]
+
+
+def test_static_pipeline_skip_edges_clip_adam_3stages(tmp_path):
+    """Three stages with activations used on two later stages (skip edges) and gradients summed
+    across stages, AdamW, a global-norm clip over all stages."""
+    ref_losses, ref = _serial(0.05, True, True, 'adam')
+    res = run_ranks(_pipe, 3, tmp_path, args=(4, '1F1B', 0.05, True, True, False, 'adam'))
+    got = {}
+    for o in res:
+        np.testing.assert_allclose(o['losses'], ref_losses, rtol=1e-5, atol=1e-6)
+        got.update(o['params'])
+    assert sorted(got) == list(range(6))
+    for i, p in got.items():
+        np.testing.assert_allclose(p, ref[i], rtol=1e-4, atol=1e-6)
+
+
+def _bad(rank, world, what):
+    import paddle_ray_amd as paddle
+    import paddle_ray_amd.nn as nn
+    from paddle_ray_amd import static
+    paddle.enable_static()
+    main = static.Program()
+    err = None
+    with static.program_guard(main):
+        x = static.data('x', [-1, H], 'float32')
+        lin = nn.Linear(H, H)
+        with static.device_guard('gpu:0'):
+            h = lin(x)
+        with static.device_guard('gpu:1'):
+            out = lin(h) if what == 'shared' else h * 2.0
+        loss = paddle.mean(out)
+        try:
+            static.PipelineOptimizer(paddle.optimizer.SGD(0.1), 2).minimize(loss)
+        except (NotImplementedError, ValueError) as e:
+            err = type(e).__name__
+    paddle.disable_static()
+    return err
+
+
+def test_static_pipeline_rejects_shared_params(tmp_path):
+    res = run_ranks(_bad, 2, tmp_path, args=('shared',))
+    assert res == ['NotImplementedError', 'NotImplementedError']
+
+
+def test_plain_minimize_still_raises_for_multi_device():
+    import paddle_ray_amd as paddle
+    import paddle_ray_amd.nn as nn
+    from paddle_ray_amd import static
+    paddle.enable_static()
+    try:
+        main = static.Program()
+        with static.program_guard(main):
+            x = static.data('x', [-1, H], 'float32')
+            with static.device_guard('gpu:0'):
+                h = nn.Linear(H, H)(x)
+            with static.device_guard('gpu:1'):
+                loss = paddle.mean(nn.Linear(H, H)(h))
+            with pytest.raises(NotImplementedError):
+                paddle.optimizer.SGD(0.1).minimize(loss)
+    finally:
+        paddle.disable_static()
