@@ -255,6 +255,25 @@ def merge_torch_events(res, tp_events, own_names):
             h.kernels = _kernels_of(e)
     offsets.sort()
     off = offsets[len(offsets) // 2] if offsets else 0
+    # 1b) kernels launched straight through the HIP runtime (the in-tree kernels: no aten op
+    # around them) are credited to every one of our ranges their launch call falls in, by the
+    # runtime API event's time (its .kernels are linked by correlation id)
+    own = sorted(res.host_events, key=lambda h: h.start_ns)
+    starts = [h.start_ns for h in own]
+    launched = {}
+    import bisect
+    for e in cpu_evs:
+        ks = getattr(e, 'kernels', None)
+        if not ks or e.name.startswith('aten::') or e.name in own_names:
+            continue
+        t = int(e.time_range.start * 1000) + off
+        dur = sum(int(getattr(k, 'duration', 0) * 1000) for k in ks)
+        for h in own[:bisect.bisect_right(starts, t)]:
+            if h.end_ns >= t:
+                launched[id(h)] = launched.get(id(h), 0) + dur
+    for h in own:
+        if launched.get(id(h), 0) > h.gpu_ns:
+            h.gpu_ns = launched[id(h)]
     # 2) operators: top-level aten ops (an op nested in another aten op is its inner detail)
     for e in cpu_evs:
         if not e.name.startswith('aten::'):

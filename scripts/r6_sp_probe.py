@@ -1,5 +1,5 @@
-"""Persistent W4 GEMM refill spacing (PRA_PTS_SP, read once per process) on the GPT shapes:
-interleaved medians vs hipBLASLt.   PRA_PTS_SP=n python scripts/r6_sp_probe.py"""
+"""Persistent W4 GEMM refill spacing (PRA_PTS_VAR, read once per process) on the GPT shapes:
+interleaved medians vs hipBLASLt.   PRA_PTS_VAR=n python scripts/r6_sp_probe.py"""
 import os
 import statistics
 import sys
@@ -25,7 +25,7 @@ def timeit(fn, iters):
 def main():
     L = _native.lib()
     F._GEMM_MODE = 'mfma'
-    sp = os.environ.get('PRA_PTS_SP', '0')
+    sp = os.environ.get("PRA_PTS_VAR", "0") + "/buf" + os.environ.get("PRA_PTS_BUF", "0")
     g = torch.Generator(device='cuda').manual_seed(0)
     r = lambda *s: ((torch.rand(*s, device='cuda', generator=g) * 2 - 1) * 0.5).to(torch.bfloat16)  # noqa
     cases = [('fc1.fwd', 0, T, 8192, 2048), ('fc2.dgrad', 1, T, 8192, 2048), ('qkv.dgrad', 1, T, 2048, 6144),
