@@ -228,12 +228,17 @@ def merge_torch_events(res, tp_events, own_names):
     them occurrence by occurrence gives the clock offset and each range's device time."""
     import torch
     cuda = torch.autograd.DeviceType.CUDA
-    cpu_evs, dev_evs, mem_evs = [], [], []
+    cpu_evs, dev_evs, mem_evs, dev_ann = [], [], [], {}
     for e in tp_events:
         if e.name == '[memory]':
             mem_evs.append(e)
         elif getattr(e, 'device_type', None) == cuda:
-            dev_evs.append(e)
+            if e.name in own_names:
+                # the device-side mirror of one of our ranges (gpu_user_annotation): the span of
+                # the kernels launched inside it, natively launched ones included
+                dev_ann.setdefault(e.name, []).append(e)
+            else:
+                dev_evs.append(e)
         else:
             cpu_evs.append(e)
     # 1) clock: pair our ranges with torch's annotation events of the same name, k-th with k-th
@@ -255,6 +260,11 @@ def merge_torch_events(res, tp_events, own_names):
             h.kernels = _kernels_of(e)
     offsets.sort()
     off = offsets[len(offsets) // 2] if offsets else 0
+    for name, dl in dev_ann.items():
+        dl.sort(key=lambda e: e.time_range.start)
+        for h, e in zip(sorted(ours.get(name, []), key=lambda h: h.start_ns), dl):
+            g = int(getattr(e, 'device_time_total', 0) * 1000) or int((e.time_range.end - e.time_range.start) * 1000)
+            h.gpu_ns = max(h.gpu_ns, g)
     # 1b) kernels launched straight through the HIP runtime (the in-tree kernels: no aten op
     # around them) are credited to every one of our ranges their launch call falls in, by the
     # runtime API event's time (its .kernels are linked by correlation id)
