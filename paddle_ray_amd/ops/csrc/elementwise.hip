@@ -229,60 +229,8 @@ __device__ __forceinline__ void adamw_vec4(float* __restrict__ master, const voi
   }
 }
 
-// Two 4-element groups per thread per iteration (i and i + 4 * blockDim): both groups' five
-// loads are in flight before the first update, twice the bytes per wave in flight of the
-// one-group loop (the update is HBM-bound: 30 B per parameter).
-template <bool BF16G, bool LOWP>
-__device__ __forceinline__ void adamw_vec4x2(float* __restrict__ master, const void* __restrict__ grad,
-                                             float* __restrict__ m, float* __restrict__ v,
-                                             uint16_t* __restrict__ lowp, int64_t start, int64_t end, float b1,
-                                             float b2, float eps, float decay, float step, float rbc2, float gscale) {
-  const int64_t stride = 4 * (int64_t)blockDim.x;
-  int64_t i = start + 4 * threadIdx.x;
-  for (; i + stride + 3 < end; i += 2 * stride) {
-    float g[2][4];
-    float4 mv[2], vv[2], pv[2];
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int64_t j = i + u * stride;
-      if (BF16G) {
-        const uint2 w = *reinterpret_cast<const uint2*>((const uint16_t*)grad + j);
-        g[u][0] = __uint_as_float(w.x << 16); g[u][1] = __uint_as_float(w.x & 0xffff0000u);
-        g[u][2] = __uint_as_float(w.y << 16); g[u][3] = __uint_as_float(w.y & 0xffff0000u);
-      } else {
-        const float4 w = *reinterpret_cast<const float4*>((const float*)grad + j);
-        g[u][0] = w.x; g[u][1] = w.y; g[u][2] = w.z; g[u][3] = w.w;
-      }
-      mv[u] = *reinterpret_cast<const float4*>(m + j);
-      vv[u] = *reinterpret_cast<const float4*>(v + j);
-      pv[u] = *reinterpret_cast<const float4*>(master + j);
-    }
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int64_t j = i + u * stride;
-      float mm[4] = {mv[u].x, mv[u].y, mv[u].z, mv[u].w}, vq[4] = {vv[u].x, vv[u].y, vv[u].z, vv[u].w},
-            pp[4] = {pv[u].x, pv[u].y, pv[u].z, pv[u].w};
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const float gk = g[u][k] * gscale;
-        mm[k] = b1 * mm[k] + (1.f - b1) * gk;
-        vq[k] = b2 * vq[k] + (1.f - b2) * gk * gk;
-        pp[k] = pp[k] * decay - step * mm[k] / (sqrtf(vq[k] * rbc2) + eps);
-      }
-      *reinterpret_cast<float4*>(m + j) = make_float4(mm[0], mm[1], mm[2], mm[3]);
-      *reinterpret_cast<float4*>(v + j) = make_float4(vq[0], vq[1], vq[2], vq[3]);
-      *reinterpret_cast<float4*>(master + j) = make_float4(pp[0], pp[1], pp[2], pp[3]);
-      if (LOWP) *reinterpret_cast<uint2*>(lowp + j) = make_uint2(pack_bf2(pp[0], pp[1]), pack_bf2(pp[2], pp[3]));
-    }
-  }
-  // the last (single) group of this thread
-  adamw_vec4<BF16G, LOWP>(master, grad, m, v, lowp, i - 4 * (int64_t)threadIdx.x, end, b1, b2, eps, decay, step,
-                          rbc2, gscale);
-}
-
 // gscale_ptr (device, nullable): global-norm clip coefficient read in-kernel, so the clip
 // needs no separate pass over the gradients.
-template <bool X2>
 __global__ void __launch_bounds__(256) adamw_mt_k(const int64_t* __restrict__ tab, const float* __restrict__ ftab,
                                                   const int64_t* __restrict__ chunks, float lr, float b1, float b2,
                                                   float eps, float bc1, float bc2, float gscale,
@@ -307,12 +255,7 @@ __global__ void __launch_bounds__(256) adamw_mt_k(const int64_t* __restrict__ ta
                        ((((uintptr_t)grad | (uintptr_t)lowp) & 7) == 0);
   if (aligned && mdt == kF32 && (gdt == kBF16 || gdt == kF32) && (!lowp || pdt == kBF16)) {
     const int64_t vend = start + ((end - start) & ~(int64_t)3);
-    if (gdt == kBF16 && X2) {
-      if (lowp) adamw_vec4x2<true, true>((float*)master, grad, m, v, (uint16_t*)lowp, start, vend, b1, b2, eps,
-                                         decay, step, rbc2, gscale);
-      else adamw_vec4x2<true, false>((float*)master, grad, m, v, nullptr, start, vend, b1, b2, eps, decay, step,
-                                     rbc2, gscale);
-    } else if (gdt == kBF16) {
+    if (gdt == kBF16) {
       if (lowp) adamw_vec4<true, true>((float*)master, grad, m, v, (uint16_t*)lowp, start, vend, b1, b2, eps,
                                        decay, step, rbc2, gscale);
       else adamw_vec4<true, false>((float*)master, grad, m, v, nullptr, start, vend, b1, b2, eps, decay, step,
@@ -483,14 +426,8 @@ void pra_bias_gelu_bwd(const void* dy, const void* x, const void* b, void* dx, i
 void pra_adamw_mt(const int64_t* tab, const float* ftab, const int64_t* chunks, int nchunks, float lr, float b1,
                   float b2, float eps, float bc1, float bc2, float gscale, const float* gscale_ptr, hipStream_t s) {
   if (!nchunks) return;
-  // PRA_ADAMW_X2=0: the one-group loop (A/B)
-  static const bool x2 = !(getenv("PRA_ADAMW_X2") && atoi(getenv("PRA_ADAMW_X2")) == 0);
-  if (x2)
-    hipLaunchKernelGGL(adamw_mt_k<true>, dim3(nchunks), dim3(256), 0, s, tab, ftab, chunks, lr, b1, b2, eps, bc1,
-                       bc2, gscale, gscale_ptr);
-  else
-    hipLaunchKernelGGL(adamw_mt_k<false>, dim3(nchunks), dim3(256), 0, s, tab, ftab, chunks, lr, b1, b2, eps, bc1,
-                       bc2, gscale, gscale_ptr);
+  hipLaunchKernelGGL(adamw_mt_k, dim3(nchunks), dim3(256), 0, s, tab, ftab, chunks, lr, b1, b2, eps, bc1, bc2,
+                     gscale, gscale_ptr);
 }
 void pra_zero_mt(const int64_t* chunks, int nchunks, hipStream_t s) {
   if (nchunks > 0) hipLaunchKernelGGL(zero_mt_k, dim3(nchunks), dim3(256), 0, s, chunks);
