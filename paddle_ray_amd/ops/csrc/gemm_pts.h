@@ -48,9 +48,11 @@ __device__ __forceinline__ float row16_sum(float x) {
   return x;
 }
 
-// SPO: MFMA slots between two refill pieces of a K-step (0: spread the pieces over the whole
-// window between the two barriers; smaller values issue the refill earlier in the step)
-template <typename T, typename CF, bool AK, bool BK, int E, bool BETA, int SPO = 0>
+// VAR (measurement variants): bits 0-7 = MFMA slots between two refill pieces of a K-step (0:
+// spread them over the whole window between the two barriers); bit 8 = read the next step's
+// first A fragment ahead of the B fragments (every first-use gets the same MFMA slack); bits
+// 12-15 = move the second barrier this many MFMA slots earlier.
+template <typename T, typename CF, bool AK, bool BK, int E, bool BETA, int VAR = 0>
 __global__ __launch_bounds__(CF::NT, 1) void gemm_pts_kernel(const uint16_t* __restrict__ A,
                                                              const uint16_t* __restrict__ B,
                                                              const uint16_t* __restrict__ bias,
@@ -158,7 +160,9 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_pts_kernel(const uint16_t* __r
     constexpr bool STEADY = decltype(steady_c)::value, FIRST = decltype(first_c)::value;
     constexpr bool ZPRE = decltype(zpre_c)::value && ZOP;
     constexpr int NRD = TI + TJ, NDMA = NDA + NDB, NM = TI * TJ, F = 2 * NM;
-    constexpr int BA = NRD + 4, BB = F - NRD - 3;
+    constexpr int SPO = VAR & 255, BSH = (VAR >> 12) & 15;
+    constexpr bool AFIRST = (VAR >> 8) & 1;
+    constexpr int BA = NRD + 4, BB = F - NRD - 3 - BSH;
     constexpr int SP0 = (BB - BA - 1) / NDMA > 0 ? (BB - BA - 1) / NDMA : 1;
     constexpr int SP = SPO > 0 ? SPO : SP0;
     static_assert(BB >= NM && BA + 1 + (NDMA - 1) * SP < BB, "pts: fillers exceed the K-step's MFMAs");
@@ -214,8 +218,15 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_pts_kernel(const uint16_t* __r
             __builtin_amdgcn_s_barrier();  // ... for every wave
           } else if (rd1 && f > BB && f - BB - 1 < NRD) {
             const int r = f - BB - 1;
-            if (r < TJ) fb0[r] = frag<T, BK>(bn, wc * CW + r * 16, 0, lane);
-            else fa0[r - TJ] = frag<T, AK, (AK ? 256 : BM)>(an, wr * RW + (r - TJ) * 16, 0, lane);
+            if constexpr (AFIRST) {
+              // A0, B0..B(TJ-1), A1.. : the first MFMA's operands are the first two reads
+              if (r == 0) fa0[0] = frag<T, AK, (AK ? 256 : BM)>(an, wr * RW, 0, lane);
+              else if (r <= TJ) fb0[r - 1] = frag<T, BK>(bn, wc * CW + (r - 1) * 16, 0, lane);
+              else fa0[r - TJ] = frag<T, AK, (AK ? 256 : BM)>(an, wr * RW + (r - TJ) * 16, 0, lane);
+            } else {
+              if (r < TJ) fb0[r] = frag<T, BK>(bn, wc * CW + r * 16, 0, lane);
+              else fa0[r - TJ] = frag<T, AK, (AK ? 256 : BM)>(an, wr * RW + (r - TJ) * 16, 0, lane);
+            }
           } else if (ZPRE && f > BB) {
             // the ring's first ZR - 1 pass-rows, spread over the slots after the barrier
             constexpr int LPS = ((ZR - 1) * JH + (F - BB - 2)) / (F - BB - 1);  // loads per slot

@@ -17,22 +17,22 @@ int num_cus() {
   return n;
 }
 
-// refill spacing of the plain (no epilogue) kernel: PRA_PTS_SP (0 = default spread)
-int pts_sp() {
+// measurement variant of the plain (no epilogue) kernel: PRA_PTS_VAR (gemm_pts.h VAR; 0 = default)
+int pts_var() {
   static int v = -1;
   if (v < 0) {
-    const char* e = getenv("PRA_PTS_SP");
+    const char* e = getenv("PRA_PTS_VAR");
     v = e ? atoi(e) : 0;
   }
   return v;
 }
 
-template <typename CF, typename T, bool AK, bool BK, int E, bool BETA, int SPO = 0>
+template <typename CF, typename T, bool AK, bool BK, int E, bool BETA, int VAR = 0>
 void launch_pts(const void* A, const void* B, const void* bias, void* C, void* Z, float* colsum, int M, int N, int K,
                 int lda, int ldb, int ldc, int ldz, hipStream_t s) {
   const int tiles = ((M + 255) / 256) * ((N + 255) / 256);
   const int grid = tiles < num_cus() ? tiles : num_cus();
-  gemm_pts_kernel<T, CF, AK, BK, E, BETA, SPO><<<grid, CF::NT, 0, s>>>(
+  gemm_pts_kernel<T, CF, AK, BK, E, BETA, VAR><<<grid, CF::NT, 0, s>>>(
       static_cast<const uint16_t*>(A), static_cast<const uint16_t*>(B), static_cast<const uint16_t*>(bias),
       static_cast<uint16_t*>(C), static_cast<uint16_t*>(Z), colsum, M, N, K, lda, ldb, ldc, ldz);
 }
@@ -44,10 +44,12 @@ int launch_pts_e(const void* A, const void* B, const void* bias, void* C, void* 
   switch (epi) {
     case kNone:
       if (beta) launch_pts<CF, T, AK, BK, kNone, true>(A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, s);
-      else if (CF::NT == 256 && pts_sp() == 2)
-        launch_pts<CF, T, AK, BK, kNone, false, 2>(A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, s);
-      else if (CF::NT == 256 && pts_sp() == 3)
-        launch_pts<CF, T, AK, BK, kNone, false, 3>(A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, s);
+      else if (CF::NT == 256 && pts_var() == 256)
+        launch_pts<CF, T, AK, BK, kNone, false, 256>(A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, s);
+      else if (CF::NT == 256 && pts_var() == (256 | (4 << 12)))
+        launch_pts<CF, T, AK, BK, kNone, false, 256 | (4 << 12)>(A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, s);
+      else if (CF::NT == 256 && pts_var() == (4 << 12))
+        launch_pts<CF, T, AK, BK, kNone, false, (4 << 12)>(A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, s);
       else launch_pts<CF, T, AK, BK, kNone, false>(A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, s);
       return 0;
     case kGeluErf: launch_pts<CF, T, AK, BK, kGeluErf, false>(A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, s); return 0;
