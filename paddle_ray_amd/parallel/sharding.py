@@ -35,8 +35,6 @@ from .data_parallel import GradBucketReducer, _avg_supported
 from .flat import FlatGroup, group_params_into_buckets
 from ..distributed import watchdog as _watchdog
 
-_ZERO_SIDE = __import__('os').environ.get('PRA_ZERO_SIDE', '1') == '1'
-
 LEVELS = {'os': 1, 'os_g': 2, 'p_g_os': 3}
 
 
@@ -113,7 +111,6 @@ class ShardedState:
                  release_after_forward=True):
         from ..distributed import collective as C
         self.layer = layer
-        self._zero_stream, self._zero_event = None, None   # side-stream gradient zeroing
         self.stage = LEVELS[level] if isinstance(level, str) else int(level)
         self.group = group
         self.pg = None if group is None else group.process_group
@@ -394,39 +391,20 @@ class ShardedState:
             self._release_unit(u)
 
     def zero_grad(self):
-        """Zero the flat gradient slabs. On the GPU the fill runs on a side stream behind the
-        optimizer's reads and overlaps the next forward (the slabs are first written by the
-        backward, which ``join_zero`` -- called when the forward returns -- orders after it):
-        ~2.6 GB of stores per GPT-1.3B step off the critical path (PRA_ZERO_SIDE=0: inline)."""
+        """Zero the flat gradient slabs in ONE multi-tensor launch. (Running the fill on a side
+        stream under the next forward measured 131.0 vs 126.2 ms per GPT-1.3B step: the fill's
+        workgroups take CU slots from the one-workgroup-per-CU persistent GEMMs,
+        profiles/r6/zero_side_stream_ab.md.)"""
         bufs = [g.grad_buf for g in self.groups if not g.grads_released]
         if self.stage > 1 and self.world > 1:
             bufs += list(self.shard_grads)
-        if bufs and bufs[0].is_cuda and _ZERO_SIDE:
-            self.join_zero()
-            cur = torch.cuda.current_stream(bufs[0].device)
-            if self._zero_stream is None:
-                self._zero_stream = torch.cuda.Stream(bufs[0].device)
-            side = self._zero_stream
-            side.wait_stream(cur)      # the optimizer finished reading the gradients
-            with torch.cuda.stream(side):
-                K.zero_tensors(bufs)
-            for b in bufs:
-                b.record_stream(side)
-            self._zero_event = side.record_event()
-        elif bufs:
+        if bufs:
             K.zero_tensors(bufs)
         for g in self.groups:
             if not g.grads_released:
                 g.reattach_grads()
         if self.reducer is not None:
             self.reducer.reset_accumulation()
-
-    def join_zero(self):
-        """Make the current stream wait for a side-stream gradient zeroing (no-op if none)."""
-        ev = self._zero_event
-        if ev is not None:
-            self._zero_event = None
-            torch.cuda.current_stream(self.groups[0].device if self.groups else None).wait_event(ev)
 
     def params_loaded(self):
         """Full parameter values were written into the gathered buffers (set_state_dict):
@@ -833,7 +811,6 @@ class ShardedOptimizer:
     @torch.no_grad()
     def step(self):
         st = self.state
-        st.join_zero()
         self._step += 1
         o = self._inner
         o._step_count = self._step
@@ -1110,9 +1087,7 @@ class ShardedModel(Layer):
 
     def forward(self, *inputs, **kwargs):
         self._state.before_forward()
-        out = self._layer(*inputs, **kwargs)
-        self._state.join_zero()    # the backward (after this) writes the gradient slabs
-        return out
+        return self._layer(*inputs, **kwargs)
 
     def state_dict(self, *a, **k):
         st = self._state
