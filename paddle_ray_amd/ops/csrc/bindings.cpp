@@ -87,6 +87,7 @@ int pra_gemm_tn_grouped2(const void*, const void*, void*, int, int, int, int, co
 void pra_gemm_set_w4(int);
 void pra_gemm_set_pts(int);
 int pra_gemm_get_pts();
+void pra_spin_hog(int, long long, float*, hipStream_t);
 int pra_gemm_probe(int, int, const void*, const void*, void*, int, int, int, int, int, int, unsigned long long*,
                    hipStream_t);
 int pra_gemm_get_w4();
@@ -173,6 +174,7 @@ PYBIND11_MODULE(_pra_hip, m) {
   m.def("gemm_set_w4", [](int mask) { pra_gemm_set_w4(mask); });
   m.def("gemm_set_pts", [](int mask) { pra_gemm_set_pts(mask); });
   m.def("gemm_get_pts", []() { return pra_gemm_get_pts(); });
+  m.def("spin_hog", [](int nwg, long long cycles, P sink, P stream) { pra_spin_hog(nwg, cycles, (float*)sink, (hipStream_t)stream); });
   m.def("gemm_probe", [](int cfg, int layout, P a, P b, P c, int M, int N, int K, int lda, int ldb, int ldc, P st,
                          P stream) {
     return pra_gemm_probe(cfg, layout, CV(a), CV(b), V(c), M, N, K, lda, ldb, ldc,

@@ -51,3 +51,26 @@ extern "C" int pra_gemm_probe(int cfg, int layout, const void* A, const void* B,
   }
   return tiles;
 }
+
+// Co-residence load for scheduling experiments: nwg workgroups of 256 threads running
+// dependent FMA chains on the CUs they land on for `cycles` shader clocks (the stand-in for the
+// RCCL channel workgroups that share CUs with the GEMMs during overlapped communication). Every
+// wave leaves after at most `cycles` clocks or 1<<24 iterations, whichever comes first.
+namespace pra {
+namespace {
+__global__ void __launch_bounds__(256) spin_hog_k(float* __restrict__ sink, long long cycles) {
+  const long long t0 = clock64();
+  float a = (float)threadIdx.x, b = 1.0000001f;
+  for (int it = 0; it < (1 << 24); ++it) {
+#pragma unroll
+    for (int u = 0; u < 64; ++u) a = fmaf(a, b, 0.5f);
+    if (clock64() - t0 > cycles) break;
+  }
+  if (a == 12345.f) sink[threadIdx.x] = a;  // keeps the chain alive (never true in practice)
+}
+}  // namespace
+}  // namespace pra
+
+extern "C" void pra_spin_hog(int nwg, long long cycles, float* sink, hipStream_t s) {
+  if (nwg > 0) hipLaunchKernelGGL(pra::spin_hog_k, dim3(nwg), dim3(256), 0, s, sink, cycles);
+}

@@ -58,24 +58,29 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_pts_kernel(const uint16_t* __r
                                                              const uint16_t* __restrict__ bias,
                                                              uint16_t* __restrict__ C, uint16_t* __restrict__ Z,
                                                              float* __restrict__ colsum, int M, int N, int K, int lda,
-                                                             int ldb, int ldc, int ldz) {
+                                                             int ldb, int ldc, int ldz, int* __restrict__ tctr) {
   constexpr int NT = CF::NT, TI = CF::TI, TJ = CF::TJ, NDA = CF::NDA, NDB = CF::NDB, WC = CF::WC;
   constexpr int BM = CF::BM, BN = CF::BN, IMGA = CF::IMGA, SLOT = CF::SLOT;
   constexpr int RW = TI * 16, CW = TJ * 16;
   constexpr bool AGPR_ACC = CF::WR * CF::WC == 4;
   static_assert(BM == 256 && BN == 256 && TJ % 2 == 0 && CF::WR == 2, "pts: 256x256 tiles, 2 wave rows");
-  __shared__ __attribute__((aligned(1024))) char lds[2 * SLOT + 2 * BN * 4];
+  __shared__ __attribute__((aligned(1024))) char lds[2 * SLOT + 2 * BN * 4 + 16];
   typedef typename V8<T>::type v8;
   const uint32_t lds_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)lds;
 
   const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN, ntiles = tiles_m * tiles_n;
   const int G = gridDim.x;
-  int pid;
-  {  // XCD-major rank of this workgroup (bijective for any G)
-    const int q = G >> 3, r = G & 7, xcd = blockIdx.x & 7;
-    pid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (blockIdx.x >> 3);
-  }
+  // XCD-major rank of this workgroup (bijective for any G): the workgroups of XCD x own the
+  // ranks [x0, x0 + nx); round k of the static order gives them tiles k * G + [x0, x0 + nx)
+  const int xq = G >> 3, xr = G & 7, xcd = blockIdx.x & 7;
+  const int nx = xcd < xr ? xq + 1 : xq, x0 = xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq;
+  int pid = x0 + (blockIdx.x >> 3);
   if (pid >= ntiles) return;
+  // tctr (dynamic order): the same per-XCD tile runs, but which workgroup of the XCD takes the
+  // next one is decided by a per-XCD counter (one vector atomic per tile, fetched a K-step
+  // ahead): a workgroup slowed by a co-resident kernel (RCCL channels during overlapped
+  // communication) takes fewer tiles instead of stretching the whole GEMM
+  int* nxt_lds = reinterpret_cast<int*>(lds + 2 * SLOT + 2 * BN * 4);
   auto tile_mn = [&](int p, int& tm, int& tn) {
     const int group = 8 * tiles_n, gi = p / group, first_m = gi * 8;
     const int gm = min(tiles_m - first_m, 8);
@@ -241,12 +246,26 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_pts_kernel(const uint16_t* __r
 
   float* xlds = reinterpret_cast<float*>(lds + 2 * SLOT);  // [2][BN] column sums per wave row
   while (true) {
-    const int npid = pid + G;
-    const bool has_next = npid < ntiles;
+    // the counter atomic is issued from inline asm (like the LDS-DMA) so the compiler's waitcnt
+    // model never drains the in-flight refills for it: step 0's counted vmcnt wait retires it
+    // (it is older than that step's refills) before its result is read below
+    int fetched = 0;
+    if (tctr && wave == 0 && lane == 0) {
+      const uint64_t ca = (uint64_t)(tctr + xcd);
+      asm volatile("global_atomic_add %0, %1, %2, off sc0" : "=v"(fetched) : "v"(ca), "v"(1) : "memory");
+    }
     int ntm = 0, ntn = 0;
     kstep(0, std::true_type{}, std::true_type{}, true, false, true, std::false_type{});
+    if (tctr && wave == 0 && lane == 0) {
+      const int f = nx + fetched;
+      nxt_lds[0] = (f / nx) * G + x0 + f % nx;
+    }
     for (int kt = 1; kt + 2 < nk; ++kt)
       kstep(kt, std::true_type{}, std::false_type{}, true, false, true, std::false_type{});
+    // (the LDS slot was written before step 1's barriers and is rewritten only after the next
+    // tile's step 0, two barriers after every wave read it here)
+    const int npid = tctr ? __builtin_amdgcn_readfirstlane(nxt_lds[0]) : pid + G;
+    const bool has_next = (unsigned)npid < (unsigned)ntiles;  // (a bad dynamic fetch exits instead of faulting)
     // this tile's last refill was step nk-1 (issued in step nk-3): the DMA state moves to the next tile
     if (has_next) {
       tile_mn(npid, ntm, ntn);

@@ -1,5 +1,9 @@
 // Launch side of the persistent TS GEMM (gemm_pts.h): one translation unit per wave configuration.
 #pragma once
+#include <mutex>
+#include <utility>
+#include <vector>
+
 #include "gemm_pts.h"
 
 namespace pra {
@@ -27,14 +31,43 @@ int pts_var() {
   return v;
 }
 
+// Dynamic tile order (gemm_pts.h tctr), default on (PRA_PTS_DYN=0: the static order). Under a
+// 32-workgroup co-resident load the fused fc1 GEMM took 1.60x its time with the static order and
+// 1.17x with the dynamic one, alone 553 vs 557 us (profiles/r6/pts_dynamic_order.md). One
+// 8-counter block per stream, zeroed by a memset node ahead of each launch (graph-capture safe).
+int pts_dyn() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("PRA_PTS_DYN");
+    v = e ? atoi(e) : 1;
+  }
+  return v;
+}
+int* pts_counters(hipStream_t s) {
+  static std::mutex mu;
+  static std::vector<std::pair<hipStream_t, int*>> pool;
+  std::lock_guard<std::mutex> lk(mu);
+  for (auto& e : pool)
+    if (e.first == s) return e.second;
+  int* p = nullptr;
+  if (hipMalloc(&p, 8 * sizeof(int)) != hipSuccess) return nullptr;
+  pool.emplace_back(s, p);
+  return p;
+}
+
 template <typename CF, typename T, bool AK, bool BK, int E, bool BETA, int VAR = 0>
 void launch_pts(const void* A, const void* B, const void* bias, void* C, void* Z, float* colsum, int M, int N, int K,
                 int lda, int ldb, int ldc, int ldz, hipStream_t s) {
   const int tiles = ((M + 255) / 256) * ((N + 255) / 256);
   const int grid = tiles < num_cus() ? tiles : num_cus();
+  int* ctr = nullptr;
+  if (pts_dyn() && tiles > grid) {
+    ctr = pts_counters(s);
+    if (ctr && hipMemsetAsync(ctr, 0, 8 * sizeof(int), s) != hipSuccess) ctr = nullptr;
+  }
   gemm_pts_kernel<T, CF, AK, BK, E, BETA, VAR><<<grid, CF::NT, 0, s>>>(
       static_cast<const uint16_t*>(A), static_cast<const uint16_t*>(B), static_cast<const uint16_t*>(bias),
-      static_cast<uint16_t*>(C), static_cast<uint16_t*>(Z), colsum, M, N, K, lda, ldb, ldc, ldz);
+      static_cast<uint16_t*>(C), static_cast<uint16_t*>(Z), colsum, M, N, K, lda, ldb, ldc, ldz, ctr);
 }
 
 template <typename CF, typename T, bool AK, bool BK>
