@@ -246,14 +246,12 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_pts_kernel(const uint16_t* __r
 
   float* xlds = reinterpret_cast<float*>(lds + 2 * SLOT);  // [2][BN] column sums per wave row
   while (true) {
-    // the counter atomic is issued from inline asm (like the LDS-DMA) so the compiler's waitcnt
-    // model never drains the in-flight refills for it: step 0's counted vmcnt wait retires it
-    // (it is older than that step's refills) before its result is read below
+    // the counter atomic is a plain (compiler-tracked) vector atomic: its result is consumed
+    // after step 0, where the compiler's vmcnt(0) for it also retires step 2's refills a little
+    // early. (An inline-asm atomic whose result the waitcnt model cannot see was spilled to
+    // scratch before it returned by the register-heavy xᵀ·dy instantiations.)
     int fetched = 0;
-    if (tctr && wave == 0 && lane == 0) {
-      const uint64_t ca = (uint64_t)(tctr + xcd);
-      asm volatile("global_atomic_add %0, %1, %2, off sc0" : "=v"(fetched) : "v"(ca), "v"(1) : "memory");
-    }
+    if (tctr && wave == 0 && lane == 0) fetched = atomicAdd(tctr + xcd, 1);
     int ntm = 0, ntn = 0;
     kstep(0, std::true_type{}, std::true_type{}, true, false, true, std::false_type{});
     if (tctr && wave == 0 && lane == 0) {
