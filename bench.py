@@ -38,8 +38,9 @@ def parse():
     p.add_argument('--no-graph', action='store_true',
                    help='BERT: run the static Executor op by op (no HIP-graph replay)')
     p.add_argument('--profile-dir', default=None)
-    p.add_argument('--no-tuned-gemms', action='store_true',
-                   help='skip the committed MI355X TunableOp GEMM solutions')
+    p.add_argument('--tuned-gemms', action='store_true',
+                   help='load the committed MI355X TunableOp solutions for the library GEMMs (off by '
+                        'default: measured 126.93 vs 126.93 ms per GPT step, profiles/r6/tunableop_ab.md)')
     return p.parse_args()
 
 
@@ -128,7 +129,7 @@ def main():
     if dev.type == 'cuda':
         paddle.set_device(f'gpu:{dev.index}')
     paddle.seed(1234 + rank)
-    if dev.type == 'cuda' and not a.no_tuned_gemms:
+    if dev.type == 'cuda' and a.tuned_gemms:
         from paddle_ray_amd.incubate import autotune
         autotune.use_tuned_gemms()  # paddle_ray_amd/tuning/gemm_gfx950.csv (if present)
 
