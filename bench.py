@@ -41,6 +41,7 @@ def parse():
     p.add_argument('--tuned-gemms', action='store_true',
                    help='load the committed MI355X TunableOp solutions for the library GEMMs (off by '
                         'default: measured 126.93 vs 126.93 ms per GPT step, profiles/r6/tunableop_ab.md)')
+    p.add_argument('--no-tuned-gemms', action='store_true', help=argparse.SUPPRESS)  # (the old default)
     return p.parse_args()
 
 
