@@ -52,6 +52,10 @@ __device__ __forceinline__ float row16_sum(float x) {
 // spread them over the whole window between the two barriers); bit 8 = read the next step's
 // first A fragment ahead of the B fragments (every first-use gets the same MFMA slack); bits
 // 12-15 = move the second barrier this many MFMA slots earlier.
+// dynamic-order counters: one per XCD + the exit count, each in its own 256-B line (a shared line
+// serialises the 256 workgroups' fetches at every tile boundary)
+constexpr int kPtsCtrStride = 64;
+
 template <typename T, typename CF, bool AK, bool BK, int E, bool BETA, int VAR = 0>
 __global__ __launch_bounds__(CF::NT, 1) void gemm_pts_kernel(const uint16_t* __restrict__ A,
                                                              const uint16_t* __restrict__ B,
@@ -251,18 +255,37 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_pts_kernel(const uint16_t* __r
     // early. (An inline-asm atomic whose result the waitcnt model cannot see was spilled to
     // scratch before it returned by the register-heavy xᵀ·dy instantiations.)
     int fetched = 0;
-    if (tctr && wave == 0 && lane == 0) fetched = atomicAdd(tctr + xcd, 1);
+    if (tctr && wave == 0 && lane == 0) fetched = atomicAdd(tctr + xcd * kPtsCtrStride, 1);
     int ntm = 0, ntn = 0;
     kstep(0, std::true_type{}, std::true_type{}, true, false, true, std::false_type{});
-    if (tctr && wave == 0 && lane == 0) {
-      const int f = nx + fetched;
-      nxt_lds[0] = (f / nx) * G + x0 + f % nx;
+    if constexpr (!(VAR & (1 << 20))) {
+      if (tctr && wave == 0 && lane == 0) {
+        const int f = nx + fetched;
+        nxt_lds[0] = (f / nx) * G + x0 + f % nx;
+      }
     }
     for (int kt = 1; kt + 2 < nk; ++kt)
       kstep(kt, std::true_type{}, std::false_type{}, true, false, true, std::false_type{});
-    // (the LDS slot was written before step 1's barriers and is rewritten only after the next
-    // tile's step 0, two barriers after every wave read it here)
-    const int npid = tctr ? __builtin_amdgcn_readfirstlane(nxt_lds[0]) : pid + G;
+    int npid;
+    if constexpr (VAR & (1 << 20)) {
+      // measurement variant: the fetched value is used after the steady loop (one vmcnt(0) there,
+      // in wave 0), broadcast through LDS under an extra barrier
+      if (tctr) {
+        if (wave == 0 && lane == 0) {
+          const int f = nx + fetched;
+          nxt_lds[0] = (f / nx) * G + x0 + f % nx;
+        }
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        __builtin_amdgcn_s_barrier();
+        npid = __builtin_amdgcn_readfirstlane(nxt_lds[0]);
+      } else {
+        npid = pid + G;
+      }
+    } else {
+      // (the LDS slot was written before step 1's barriers and is rewritten only after the next
+      // tile's step 0, two barriers after every wave read it here)
+      npid = tctr ? __builtin_amdgcn_readfirstlane(nxt_lds[0]) : pid + G;
+    }
     const bool has_next = (unsigned)npid < (unsigned)ntiles;  // (a bad dynamic fetch exits instead of faulting)
     // this tile's last refill was step nk-1 (issued in step nk-3): the DMA state moves to the next tile
     if (has_next) {
@@ -430,6 +453,15 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_pts_kernel(const uint16_t* __r
     pid = npid;
     tm = ntm;
     tn = ntn;
+  }
+  if (tctr && tid == 0) {
+    // the last workgroup out returns the counters to zero for the next launch on this stream
+    // (each workgroup's final fetch precedes its exit count; vector atomics only)
+    __threadfence();
+    if (atomicAdd(tctr + 8 * kPtsCtrStride, 1) == G - 1) {
+#pragma unroll
+      for (int c = 0; c < 9; ++c) atomicExch(tctr + c * kPtsCtrStride, 0);
+    }
   }
 }
 

@@ -33,8 +33,9 @@ int pts_var() {
 
 // Dynamic tile order (gemm_pts.h tctr), default on (PRA_PTS_DYN=0: the static order). Under a
 // 32-workgroup co-resident load the fused fc1 GEMM took 1.60x its time with the static order and
-// 1.17x with the dynamic one, alone 553 vs 557 us (profiles/r6/pts_dynamic_order.md). One
-// 8-counter block per stream, zeroed by a memset node ahead of each launch (graph-capture safe).
+// 1.17x with the dynamic one, alone 553 vs 557 us (profiles/r6/pts_dynamic_order.md). A block
+// holds 8 per-XCD counters + an exit count; it starts zeroed and the kernel's last workgroup
+// re-zeroes it, so no memset is launched per GEMM and graph replays find it ready.
 int pts_dyn() {
   static int v = -1;
   if (v < 0) {
@@ -43,16 +44,49 @@ int pts_dyn() {
   }
   return v;
 }
+// Counter blocks come from one zeroed pool per device, allocated at the first launch outside a
+// stream capture (hipMalloc would invalidate a capture). Eager launches use one block per stream
+// (launches on a stream are ordered, so they can share it); every captured launch takes a block
+// of its own, so graphs replayed concurrently never share counters. With no pool yet, or the
+// pool used up, a captured launch falls back to the static order.
+constexpr int kPtsSlotInts = 10 * kPtsCtrStride, kPtsSlots = 1024;
 int* pts_counters(hipStream_t s) {
+  struct Pool {
+    int dev;
+    int* base;
+    int used;
+    std::vector<std::pair<hipStream_t, int>> eager;
+  };
   static std::mutex mu;
-  static std::vector<std::pair<hipStream_t, int*>> pool;
+  static std::vector<Pool> pools;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &cs) != hipSuccess) return nullptr;
+  const bool capturing = cs != hipStreamCaptureStatusNone;
   std::lock_guard<std::mutex> lk(mu);
-  for (auto& e : pool)
-    if (e.first == s) return e.second;
-  int* p = nullptr;
-  if (hipMalloc(&p, 8 * sizeof(int)) != hipSuccess) return nullptr;
-  pool.emplace_back(s, p);
-  return p;
+  Pool* p = nullptr;
+  for (auto& q : pools)
+    if (q.dev == dev) p = &q;
+  if (!p) {
+    if (capturing) return nullptr;
+    int* base = nullptr;
+    const size_t bytes = size_t(kPtsSlots) * kPtsSlotInts * sizeof(int);
+    if (hipMalloc(&base, bytes) != hipSuccess) return nullptr;
+    if (hipMemset(base, 0, bytes) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+      (void)hipFree(base);
+      return nullptr;
+    }
+    pools.push_back(Pool{dev, base, 0, {}});
+    p = &pools.back();
+  }
+  if (!capturing)
+    for (auto& e : p->eager)
+      if (e.first == s) return p->base + size_t(e.second) * kPtsSlotInts;
+  if (p->used >= kPtsSlots) return nullptr;
+  const int slot = p->used++;
+  if (!capturing) p->eager.emplace_back(s, slot);
+  return p->base + size_t(slot) * kPtsSlotInts;
 }
 
 template <typename CF, typename T, bool AK, bool BK, int E, bool BETA, int VAR = 0>
@@ -61,10 +95,7 @@ void launch_pts(const void* A, const void* B, const void* bias, void* C, void* Z
   const int tiles = ((M + 255) / 256) * ((N + 255) / 256);
   const int grid = tiles < num_cus() ? tiles : num_cus();
   int* ctr = nullptr;
-  if (pts_dyn() && tiles > grid) {
-    ctr = pts_counters(s);
-    if (ctr && hipMemsetAsync(ctr, 0, 8 * sizeof(int), s) != hipSuccess) ctr = nullptr;
-  }
+  if (pts_dyn() && tiles > grid) ctr = pts_counters(s);
   gemm_pts_kernel<T, CF, AK, BK, E, BETA, VAR><<<grid, CF::NT, 0, s>>>(
       static_cast<const uint16_t*>(A), static_cast<const uint16_t*>(B), static_cast<const uint16_t*>(bias),
       static_cast<uint16_t*>(C), static_cast<uint16_t*>(Z), colsum, M, N, K, lda, ldb, ldc, ldz, ctr);
@@ -81,6 +112,8 @@ int launch_pts_e(const void* A, const void* B, const void* bias, void* C, void* 
         launch_pts<CF, T, AK, BK, kNone, false, 256>(A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, s);
       else if (CF::NT == 256 && pts_var() == (256 | (4 << 12)))
         launch_pts<CF, T, AK, BK, kNone, false, 256 | (4 << 12)>(A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, s);
+      else if (pts_var() == (1 << 20))
+        launch_pts<CF, T, AK, BK, kNone, false, (1 << 20)>(A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, s);
       else if (CF::NT == 256 && pts_var() == (4 << 12))
         launch_pts<CF, T, AK, BK, kNone, false, (4 << 12)>(A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, s);
       else launch_pts<CF, T, AK, BK, kNone, false>(A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, s);

@@ -13,7 +13,7 @@ from paddle_ray_amd.ops import fused as F, _native  # noqa: E402
 T = 16384
 L = _native.lib()
 F._GEMM_MODE = 'mfma'
-dyn = os.environ.get('PRA_PTS_DYN', '0')
+dyn = os.environ.get('PRA_PTS_DYN', '1')
 g = torch.Generator(device='cuda').manual_seed(0)
 r = lambda *s: ((torch.rand(*s, device='cuda', generator=g) * 2 - 1) * 0.5).to(torch.bfloat16)  # noqa
 sink = torch.zeros(256, device='cuda')

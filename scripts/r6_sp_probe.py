@@ -25,7 +25,8 @@ def timeit(fn, iters):
 def main():
     L = _native.lib()
     F._GEMM_MODE = 'mfma'
-    sp = os.environ.get("PRA_PTS_VAR", "0") + "/buf" + os.environ.get("PRA_PTS_BUF", "0")
+    sp = (os.environ.get("PRA_PTS_VAR", "0") + "/buf" + os.environ.get("PRA_PTS_BUF", "0")
+          + "/stg" + os.environ.get("PRA_PTS_STG", "0"))
     g = torch.Generator(device='cuda').manual_seed(0)
     r = lambda *s: ((torch.rand(*s, device='cuda', generator=g) * 2 - 1) * 0.5).to(torch.bfloat16)  # noqa
     cases = [('fc1.fwd', 0, T, 8192, 2048), ('fc2.dgrad', 1, T, 8192, 2048), ('qkv.dgrad', 1, T, 2048, 6144),

@@ -240,6 +240,31 @@ def test_many_tiles_per_workgroup(layout):
     _close(c, ref + c0.float())
 
 
+def test_many_tiles_graph_replay():
+    """The persistent kernel's dynamic tile counters reset themselves (the last workgroup out
+    zeroes them): back-to-back launches and hipGraph replays, with no memset between them, must
+    each cover every tile exactly once."""
+    torch.manual_seed(9)
+    M, N, Kd = 4168, 4360, 256
+    a, b = _operands(0, M, N, Kd)
+    ref = _ref(0, a, b)
+    for _ in range(3):
+        _close(K._gemm_hip(0, a, b), ref)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        out = K._gemm_hip(0, a, b)
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        out = K._gemm_hip(0, a, b)
+    for _ in range(4):
+        out.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        _close(out, ref)
+
+
 def test_many_tiles_epilogues():
     """bias + GELU with the pre-activation, and dGELU + column sums, over 306 tiles."""
     torch.manual_seed(8)
