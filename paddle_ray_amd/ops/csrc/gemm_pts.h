@@ -52,8 +52,7 @@ __device__ __forceinline__ float row16_sum(float x) {
 // spread them over the whole window between the two barriers); bit 8 = read the next step's
 // first A fragment ahead of the B fragments (every first-use gets the same MFMA slack); bits
 // 12-15 = move the second barrier this many MFMA slots earlier.
-// dynamic-order counters: one per XCD + the exit count, each in its own 256-B line (a shared line
-// serialises the 256 workgroups' fetches at every tile boundary)
+// dynamic-order counters: one per XCD, each in its own 256-B line
 constexpr int kPtsCtrStride = 64;
 
 template <typename T, typename CF, bool AK, bool BK, int E, bool BETA, int VAR = 0>
@@ -85,6 +84,8 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_pts_kernel(const uint16_t* __r
   // ahead): a workgroup slowed by a co-resident kernel (RCCL channels during overlapped
   // communication) takes fewer tiles instead of stretching the whole GEMM
   int* nxt_lds = reinterpret_cast<int*>(lds + 2 * SLOT + 2 * BN * 4);
+  // tiles of this XCD's runs (ranks r with (r / nx) * G + x0 + r % nx < ntiles: a prefix)
+  const int tx = (ntiles / G) * nx + min(max(ntiles % G - x0, 0), nx);
   auto tile_mn = [&](int p, int& tm, int& tn) {
     const int group = 8 * tiles_n, gi = p / group, first_m = gi * 8;
     const int gm = min(tiles_m - first_m, 8);
@@ -258,34 +259,18 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_pts_kernel(const uint16_t* __r
     if (tctr && wave == 0 && lane == 0) fetched = atomicAdd(tctr + xcd * kPtsCtrStride, 1);
     int ntm = 0, ntn = 0;
     kstep(0, std::true_type{}, std::true_type{}, true, false, true, std::false_type{});
-    if constexpr (!(VAR & (1 << 20))) {
-      if (tctr && wave == 0 && lane == 0) {
-        const int f = nx + fetched;
-        nxt_lds[0] = (f / nx) * G + x0 + f % nx;
-      }
+    if (tctr && wave == 0 && lane == 0) {
+      const int f = nx + fetched;
+      nxt_lds[0] = (f / nx) * G + x0 + f % nx;
+      // the XCD's last fetch (its workgroups fetch once per tile they run: tx in all) returns the
+      // counter to zero for the next launch on this stream; no workgroup fetches after it
+      if (fetched == tx - 1) atomicExch(tctr + xcd * kPtsCtrStride, 0);
     }
     for (int kt = 1; kt + 2 < nk; ++kt)
       kstep(kt, std::true_type{}, std::false_type{}, true, false, true, std::false_type{});
-    int npid;
-    if constexpr (VAR & (1 << 20)) {
-      // measurement variant: the fetched value is used after the steady loop (one vmcnt(0) there,
-      // in wave 0), broadcast through LDS under an extra barrier
-      if (tctr) {
-        if (wave == 0 && lane == 0) {
-          const int f = nx + fetched;
-          nxt_lds[0] = (f / nx) * G + x0 + f % nx;
-        }
-        __builtin_amdgcn_s_waitcnt(0xC07F);
-        __builtin_amdgcn_s_barrier();
-        npid = __builtin_amdgcn_readfirstlane(nxt_lds[0]);
-      } else {
-        npid = pid + G;
-      }
-    } else {
-      // (the LDS slot was written before step 1's barriers and is rewritten only after the next
-      // tile's step 0, two barriers after every wave read it here)
-      npid = tctr ? __builtin_amdgcn_readfirstlane(nxt_lds[0]) : pid + G;
-    }
+    // (the LDS slot was written before step 1's barriers and is rewritten only after the next
+    // tile's step 0, two barriers after every wave read it here)
+    const int npid = tctr ? __builtin_amdgcn_readfirstlane(nxt_lds[0]) : pid + G;
     const bool has_next = (unsigned)npid < (unsigned)ntiles;  // (a bad dynamic fetch exits instead of faulting)
     // this tile's last refill was step nk-1 (issued in step nk-3): the DMA state moves to the next tile
     if (has_next) {
@@ -453,15 +438,6 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_pts_kernel(const uint16_t* __r
     pid = npid;
     tm = ntm;
     tn = ntn;
-  }
-  if (tctr && tid == 0) {
-    // the last workgroup out returns the counters to zero for the next launch on this stream
-    // (each workgroup's final fetch precedes its exit count; vector atomics only)
-    __threadfence();
-    if (atomicAdd(tctr + 8 * kPtsCtrStride, 1) == G - 1) {
-#pragma unroll
-      for (int c = 0; c < 9; ++c) atomicExch(tctr + c * kPtsCtrStride, 0);
-    }
   }
 }
 

@@ -33,9 +33,9 @@ int pts_var() {
 
 // Dynamic tile order (gemm_pts.h tctr), default on (PRA_PTS_DYN=0: the static order). Under a
 // 32-workgroup co-resident load the fused fc1 GEMM took 1.60x its time with the static order and
-// 1.17x with the dynamic one, alone 553 vs 557 us (profiles/r6/pts_dynamic_order.md). A block
-// holds 8 per-XCD counters + an exit count; it starts zeroed and the kernel's last workgroup
-// re-zeroes it, so no memset is launched per GEMM and graph replays find it ready.
+// 1.17x with the dynamic one (profiles/r6/pts_dynamic_order.md). A block holds the 8 per-XCD
+// counters; it starts zeroed and each XCD's last fetch re-zeroes its counter, so no memset is
+// launched per GEMM and graph replays find it ready.
 int pts_dyn() {
   static int v = -1;
   if (v < 0) {
@@ -49,7 +49,7 @@ int pts_dyn() {
 // (launches on a stream are ordered, so they can share it); every captured launch takes a block
 // of its own, so graphs replayed concurrently never share counters. With no pool yet, or the
 // pool used up, a captured launch falls back to the static order.
-constexpr int kPtsSlotInts = 10 * kPtsCtrStride, kPtsSlots = 1024;
+constexpr int kPtsSlotInts = 8 * kPtsCtrStride, kPtsSlots = 1024;
 int* pts_counters(hipStream_t s) {
   struct Pool {
     int dev;
@@ -112,8 +112,6 @@ int launch_pts_e(const void* A, const void* B, const void* bias, void* C, void* 
         launch_pts<CF, T, AK, BK, kNone, false, 256>(A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, s);
       else if (CF::NT == 256 && pts_var() == (256 | (4 << 12)))
         launch_pts<CF, T, AK, BK, kNone, false, 256 | (4 << 12)>(A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, s);
-      else if (pts_var() == (1 << 20))
-        launch_pts<CF, T, AK, BK, kNone, false, (1 << 20)>(A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, s);
       else if (CF::NT == 256 && pts_var() == (4 << 12))
         launch_pts<CF, T, AK, BK, kNone, false, (4 << 12)>(A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, s);
       else launch_pts<CF, T, AK, BK, kNone, false>(A, B, bias, C, Z, colsum, M, N, K, lda, ldb, ldc, ldz, s);
