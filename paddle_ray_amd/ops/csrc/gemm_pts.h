@@ -61,7 +61,8 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_pts_kernel(const uint16_t* __r
                                                              const uint16_t* __restrict__ bias,
                                                              uint16_t* __restrict__ C, uint16_t* __restrict__ Z,
                                                              float* __restrict__ colsum, int M, int N, int K, int lda,
-                                                             int ldb, int ldc, int ldz, int* __restrict__ tctr) {
+                                                             int ldb, int ldc, int ldz, int* __restrict__ tctr,
+                                                             int nts) {
   constexpr int NT = CF::NT, TI = CF::TI, TJ = CF::TJ, NDA = CF::NDA, NDB = CF::NDB, WC = CF::WC;
   constexpr int BM = CF::BM, BN = CF::BN, IMGA = CF::IMGA, SLOT = CF::SLOT;
   constexpr int RW = TI * 16, CW = TJ * 16;
@@ -388,15 +389,21 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_pts_kernel(const uint16_t* __r
           {
             auto r0 = __builtin_amdgcn_permlane16_swap(pc[0][0], pc[1][0], false, false);
             auto r1 = __builtin_amdgcn_permlane16_swap(pc[0][1], pc[1][1], false, false);
-            if (mok && nc < N)
-              *reinterpret_cast<uint4*>(C + mr * ldc + nc) = make_uint4(r0[0], r1[0], r0[1], r1[1]);
+            if (mok && nc < N) {
+              const u32x4 w = {r0[0], r1[0], r0[1], r1[1]};
+              if (nts & 1) asm volatile("global_store_dwordx4 %0, %1, off nt" ::"v"(C + mr * ldc + nc), "v"(w) : "memory");
+              else *reinterpret_cast<u32x4*>(C + mr * ldc + nc) = w;
+            }
           }
           if constexpr (!DG && E != kNone) {
             if (Z) {
               auto r0 = __builtin_amdgcn_permlane16_swap(pz[0][0], pz[1][0], false, false);
               auto r1 = __builtin_amdgcn_permlane16_swap(pz[0][1], pz[1][1], false, false);
-              if (mok && nc < N)
-                *reinterpret_cast<uint4*>(Z + mr * ldz + nc) = make_uint4(r0[0], r1[0], r0[1], r1[1]);
+              if (mok && nc < N) {
+                const u32x4 w = {r0[0], r1[0], r0[1], r1[1]};
+                if (nts & 2) asm volatile("global_store_dwordx4 %0, %1, off nt" ::"v"(Z + mr * ldz + nc), "v"(w) : "memory");
+                else *reinterpret_cast<u32x4*>(Z + mr * ldz + nc) = w;
+              }
             }
           }
         }

@@ -36,6 +36,18 @@ int pts_var() {
 // 1.17x with the dynamic one (profiles/r6/pts_dynamic_order.md). A block holds the 8 per-XCD
 // counters; it starts zeroed and each XCD's last fetch re-zeroes its counter, so no memset is
 // launched per GEMM and graph replays find it ready.
+// PRA_PTS_NT: which epilogue stores carry the non-temporal hint (see launch_pts). Default 3: the
+// fused-epilogue GEMMs' C and Z (fc1 forward + gelu' 562 -> 544 us, fc2 dgrad * gelu' 546 -> 535 us
+// alone); plain GEMMs keep L2-allocating stores (their outputs are read next: nt on the dy·Wᵀ
+// out-projection dgrad cost 101 -> 108 us). GPT step 125.8 -> 125.6 ms (profiles/r6/pts_nt_stores.md).
+int pts_nt() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("PRA_PTS_NT");
+    v = e ? atoi(e) : 3;
+  }
+  return v;
+}
 int pts_dyn() {
   static int v = -1;
   if (v < 0) {
@@ -96,9 +108,19 @@ void launch_pts(const void* A, const void* B, const void* bias, void* C, void* Z
   const int grid = tiles < num_cus() ? tiles : num_cus();
   int* ctr = nullptr;
   if (pts_dyn() && tiles > grid) ctr = pts_counters(s);
+  // non-temporal epilogue stores: bit 0 = C, bit 1 = Z
+  int nts = 0;
+  switch (pts_nt()) {
+    case 1: nts = 3; break;
+    case 2: nts = 2; break;
+    case 3: nts = (E != kNone) ? 3 : 0; break;
+    case 4: nts = (E != kNone) ? 3 : (BETA ? 1 : 0); break;
+    case 5: nts = (E != kNone) ? 2 : 0; break;
+    default: break;
+  }
   gemm_pts_kernel<T, CF, AK, BK, E, BETA, VAR><<<grid, CF::NT, 0, s>>>(
       static_cast<const uint16_t*>(A), static_cast<const uint16_t*>(B), static_cast<const uint16_t*>(bias),
-      static_cast<uint16_t*>(C), static_cast<uint16_t*>(Z), colsum, M, N, K, lda, ldb, ldc, ldz, ctr);
+      static_cast<uint16_t*>(C), static_cast<uint16_t*>(Z), colsum, M, N, K, lda, ldb, ldc, ldz, ctr, nts);
 }
 
 template <typename CF, typename T, bool AK, bool BK>
