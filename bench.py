@@ -110,6 +110,11 @@ def main():
     a = parse()
     if a.gpus > 1 and 'WORLD_SIZE' not in os.environ:
         sys.exit(_spawn_ranks(a.gpus))
+    if os.environ.get('PRA_BENCH_TRACE'):
+        # diagnosing a stuck rank: every rank dumps all its threads' stacks periodically
+        import faulthandler
+        v = float(os.environ['PRA_BENCH_TRACE'])
+        faulthandler.dump_traceback_later(v if v > 1 else 120.0, repeat=True)
     import torch
     import torch.distributed as dist
     import paddle_ray_amd as paddle
