@@ -3,7 +3,6 @@ process per rank, or self-spawning its ranks from ``--gpus N``, bench.py prints 
 line (rank 0) with the whole-job value, n_gpus = N, and ZeRO-3 active at N > 1."""
 import json
 import os
-import socket
 import subprocess
 import sys
 
@@ -11,12 +10,6 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ARGS = ['--steps', '1', '--warmup', '1', '--model', 'gpt3-tiny', '--micro-batch', '2', '--seq', '64']
-
-
-def _port():
-    with socket.socket() as s:
-        s.bind(('127.0.0.1', 0))
-        return s.getsockname()[1]
 
 
 def _json_lines(out):
@@ -42,8 +35,9 @@ def _check(lines, n):
 
 @pytest.mark.timeout(300)
 def test_bench_under_torchrun_two_ranks():
-    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', '2',
-           '--master-addr', '127.0.0.1', '--master-port', str(_port()), 'bench.py', '--gpus', '2'] + ARGS
+    # (--standalone: torchrun picks a free rendezvous port itself, no race with parallel tests)
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--standalone', '--local-addr', '127.0.0.1',
+           '--nnodes=1', '--nproc-per-node', '2', 'bench.py', '--gpus', '2'] + ARGS
     p = subprocess.run(cmd, cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=280)
     assert p.returncode == 0, p.stderr[-3000:]
     _check(_json_lines(p.stdout), 2)
