@@ -345,11 +345,14 @@ def _emit(b, func, args, kwargs, out):
             v = b.node('Mul', [v, b.scalar(n / max(1, n - corr), x)])
         return b.node('Sqrt', [v]) if op == 'std' else v
     if op == 'convolution':
-        x, w, bias, stride, pad, dil, transposed, _, groups = a[:9]
-        if transposed:
-            raise NotImplementedError('onnx export: transposed convolution')
+        x, w, bias, stride, pad, dil, transposed, opad, groups = a[:9]
         ins = [t(x), t(w)] + ([t(bias)] if bias is not None else [])
         nd = w.dim() - 2
+        if transposed:
+            # weight [Cin, Cout/groups, k...]: ONNX ConvTranspose's W layout as is
+            return b.node('ConvTranspose', ins, strides=list(stride), pads=list(pad) * 2, dilations=list(dil),
+                          group=int(groups), kernel_shape=list(w.shape[2:2 + nd]),
+                          output_padding=[int(v) for v in opad])
         return b.node('Conv', ins, strides=list(stride), pads=list(pad) * 2, dilations=list(dil), group=int(groups),
                       kernel_shape=list(w.shape[2:2 + nd]))
     if op in ('_native_batch_norm_legit_no_training', 'native_batch_norm', '_native_batch_norm_legit'):
@@ -526,6 +529,32 @@ def _conv2d(x, w, b, strides, pads, dil, group):
     return y
 
 
+def _conv_transpose2d(x, w, b, strides, pads, dil, group, opad):
+    """ONNX ConvTranspose (2-D) as a stride-1 convolution of the zero-upsampled input with the
+    flipped, in/out-swapped filter: w [Cin, Cout/group, kh, kw]."""
+    n, c, h, wd = x.shape
+    cin, ocg, kh, kw = w.shape
+    up = np.zeros((n, c, (h - 1) * strides[0] + 1, (wd - 1) * strides[1] + 1), dtype=np.float32)
+    up[:, :, ::strides[0], ::strides[1]] = x
+    # per side: dil*(k-1) - pad (+ output_padding at the end); a negative amount crops
+    amounts = [(dil[0] * (kh - 1) - pads[0], dil[0] * (kh - 1) - pads[2] + opad[0]),
+               (dil[1] * (kw - 1) - pads[1], dil[1] * (kw - 1) - pads[3] + opad[1])]
+    for ax, (lo, hi) in zip((2, 3), amounts):
+        if lo < 0:
+            up = np.take(up, range(-lo, up.shape[ax]), axis=ax)
+            lo = 0
+        if hi < 0:
+            up = np.take(up, range(0, up.shape[ax] + hi), axis=ax)
+            hi = 0
+        pw = [(0, 0)] * 4
+        pw[ax] = (lo, hi)
+        up = np.pad(up, pw)
+    icg = cin // group
+    wc = w.reshape(group, icg, ocg, kh, kw).transpose(0, 2, 1, 3, 4).reshape(group * ocg, icg, kh, kw)
+    wc = np.ascontiguousarray(wc[:, :, ::-1, ::-1])
+    return _conv2d(up, wc, b, [1, 1], [0, 0, 0, 0], dil, group)
+
+
 def _pool(x, k, s, p, kind, ceil=0, incl=1):
     n, c, h, w = x.shape
     fill = -np.inf if kind == 'max' else 0.0
@@ -631,6 +660,9 @@ def run(model, inputs):
         elif op == 'Conv':
             y = _conv2d(x, ins[1], ins[2] if len(ins) > 2 else None, A('strides'), A('pads'), A('dilations'),
                         A('group', 1))
+        elif op == 'ConvTranspose':
+            y = _conv_transpose2d(x, ins[1], ins[2] if len(ins) > 2 else None, A('strides'), A('pads'),
+                                  A('dilations'), A('group', 1), A('output_padding', [0, 0]))
         elif op == 'BatchNormalization':
             sh = (1, -1) + (1,) * (x.ndim - 2)
             y = (x - ins[3].reshape(sh)) / np.sqrt(ins[4].reshape(sh) + A('epsilon', 1e-5)) * ins[1].reshape(sh) + \

@@ -59,6 +59,25 @@ def test_embedding_layernorm_gelu_softmax(tmp_path):
            gen=lambda: np.random.RandomState(3).randint(0, 50, (3, 7)).astype(np.int64))
 
 
+class _Up(nn.Layer):
+    """Decoder-style upsampling: transposed convolutions with stride, padding, output padding,
+    dilation and groups (ONNX ConvTranspose)."""
+
+    def __init__(self):
+        super().__init__()
+        self.a = nn.Conv2DTranspose(4, 6, 3, stride=2, padding=1, output_padding=1)
+        self.b = nn.Conv2DTranspose(6, 4, 4, stride=2, padding=1, groups=2)
+        self.c = nn.Conv2DTranspose(4, 3, 3, stride=1, padding=2, dilation=2, bias_attr=False)
+
+    def forward(self, x):
+        return self.c(nn.functional.relu(self.b(nn.functional.relu(self.a(x)))))
+
+
+def test_conv_transpose(tmp_path):
+    paddle.seed(4)
+    _check(_Up(), [2, 4, 5, 7], tmp_path)
+
+
 def test_unsupported_op_is_named(tmp_path):
     class Odd(nn.Layer):
         def forward(self, x):
