@@ -1430,12 +1430,12 @@ static void launch_fwd(const void* q, const void* k, const void* v, void* o, flo
   else launch_fwd_nw<T, D, C, 8>(q, k, v, o, lse, B, H, Sq, Sk, st, scale, s);
 }
 
-// dQ = dS K launch shape: waves per block x ring depth. PRA_FA_DQ = "8x3" (default: 256 queries
+// dQ = dS K launch shape: waves per block x ring depth. PRA_FA_DQ_SHAPE = "8x3" (default: 256 queries
 // per block, two tiles in flight), "8x2", "4x3", "4x4" (128 queries, three in flight) -- A/B knob.
 static int dq_variant() {
   static int v = -1;
   if (v < 0) {
-    const char* e = getenv("PRA_FA_DQ");
+    const char* e = getenv("PRA_FA_DQ_SHAPE");
     v = 0;
     if (e && !strcmp(e, "8x2")) v = 1;
     else if (e && !strcmp(e, "4x3")) v = 2;
