@@ -416,7 +416,7 @@ def _static_pipeline(opt, loss, strategy, hcg, parameters, scaler):
     """strategy.pipeline: the program split by device_guard into one stage per rank of the
     pipeline group (static/pipeline.py; reference meta_optimizers/pipeline_optimizer.py:198)."""
     from ...static.pipeline import build_pipeline
-    for flag in ('sharding', 'localsgd', 'gradient_merge', 'recompute', 'lamb', 'lars'):
+    for flag in ('sharding', 'localsgd', 'gradient_merge', 'lamb', 'lars'):
         if getattr(strategy, flag, False):
             raise NotImplementedError(f"static pipeline together with strategy.{flag} is not supported")
     if scaler is not None:
@@ -431,7 +431,13 @@ def _static_pipeline(opt, loss, strategy, hcg, parameters, scaler):
             pp_group = hcg.get_pipe_parallel_group()
         if hcg.get_data_parallel_world_size() > 1:
             dp_group = hcg.get_data_parallel_group()
-    return build_pipeline(opt, loss, n_micro, cfg.get('schedule_mode', '1F1B'), parameters, pp_group, dp_group)
+    ckpts = None
+    if getattr(strategy, 'recompute', False):
+        ckpts = list((strategy.recompute_configs or {}).get('checkpoints') or [])
+        if not ckpts:
+            raise ValueError("strategy.recompute needs recompute_configs['checkpoints']")
+    return build_pipeline(opt, loss, n_micro, cfg.get('schedule_mode', '1F1B'), parameters, pp_group, dp_group,
+                          checkpoints=ckpts)
 
 
 def strategy_with_pass_cfg(strategy, cfg):

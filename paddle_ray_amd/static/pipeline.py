@@ -101,16 +101,36 @@ class _Pipeline:
         self.pstage = pstage
 
     # -- backward ----------------------------------------------------------------------------------
-    def build_backward(self, parameters=None):
+    def build_backward(self, parameters=None, checkpoints=None):
+        """checkpoints (RecomputeOptimizer / strategy.recompute): the recompute segments' clones
+        run on their forward ops' stages; a segment's intermediates are dropped from the micro-
+        batch's state after its forward (only what the stage's backward reads stays)."""
         prog, blk = self.prog, self.prog.global_block()
-        n_before = len(blk.ops)
-        pg = G.append_backward(self.loss, parameters, loss_scale=1.0 / self.n_micro)
+        before = {id(op) for op in blk.ops}
+        pg = G.append_backward(self.loss, parameters, loss_scale=1.0 / self.n_micro, checkpoints=checkpoints)
         st = dict(self.fwd_stage)
+        # forward ops the backward builder inserted (each recompute segment's RNG snapshot, placed
+        # right before the segment's first op): the stage of the next forward op
+        ops = blk.ops
+        for k in range(len(ops) - 1, -1, -1):
+            op = ops[k]
+            if op.role == 'forward' and id(op) not in st:
+                nxt = next((st[id(o)] for o in ops[k + 1:] if o.role == 'forward' and id(o) in st), 0)
+                st[id(op)] = nxt
         grad_of = {}   # grad-op output vid -> ('v', forward vid) | ('p', param name)
-        bwd = blk.ops[n_before:]
+        bwd = [op for op in blk.ops if id(op) not in before and op.role != 'forward']
+        producer_any = {}
+        for op in blk.ops:
+            for v in op.out_vids:
+                producer_any[v] = op
         for op in bwd:
-            if op.role == 'recompute' or op.type.startswith('recompute_'):
-                raise NotImplementedError("pipeline + recompute checkpoints is not supported")
+            if op.role == 'recompute':
+                st[id(op)] = st[id(op.attrs['recompute_of'])]
+                continue
+            if op.type in ('recompute_rng_swap', 'recompute_rng_restore'):
+                # swap: its RNG-snapshot input's stage (the segment's); restore: the swap's
+                st[id(op)] = st[id(producer_any[op.in_vids[0]])]
+                continue
             f = op.attrs.get('fwd')
             if f is not None:
                 st[id(op)] = st[id(f)]
@@ -133,7 +153,7 @@ class _Pipeline:
                 raise NotImplementedError(f"pipeline: unexpected backward op {op.type}")
         self.st = st
         me = self.stage
-        self.fwd_ops = [op for op in blk.ops[:n_before] if op.role == 'forward' and st[id(op)] == me]
+        self.fwd_ops = [op for op in blk.ops if op.role == 'forward' and st[id(op)] == me]
         self.bwd_ops = [op for op in bwd if st[id(op)] == me]
         # -- transfers ----------------------------------------------------------------------------
         prod_all = {}
@@ -156,7 +176,9 @@ class _Pipeline:
                         fsend.add(edge)
                     if t == me:
                         frecv.add(edge)
-                elif op.role == 'backward' and p.role == 'backward' and s > t:
+                elif op.role == 'recompute' and p.role == 'forward':
+                    continue   # a segment input from another stage: received in the forward, kept
+                elif op.role in ('backward', 'recompute') and p.role in ('backward', 'recompute') and s > t:
                     edge = (s, t, v)
                     if s == me:
                         bsend.add(edge)
@@ -174,6 +196,13 @@ class _Pipeline:
         self.grad_vid = {p.name: g.vid for p, g in pg}
         self.ctx_needed = {id(op) for op in self.fwd_ops if op.ctx_vid is not None and
                            any(op.ctx_vid in b.in_vids for b in self.bwd_ops)}
+        # recompute clones whose autograd contexts the segment's grad ops read
+        self.bctx_needed = {id(op) for op in self.bwd_ops if op.role == 'recompute' and op.ctx_vid is not None
+                            and any(op.ctx_vid in b.in_vids for b in self.bwd_ops)}
+        # a recomputed segment's forward outputs no later op of this stage reads: dropped per micro-batch
+        seg = {id(op.attrs['recompute_of']) for op in self.bwd_ops if op.role == 'recompute'}
+        keep = {v for op in self.bwd_ops for v in op.in_vids} | {v for _, _, v in self.fsend} | {self.loss.vid}
+        self.drop_after_fwd = [v for op in self.fwd_ops if id(op) in seg for v in op.out_vids if v not in keep]
         data = {v.vid: v for v in blk.vars.values() if v.__dict__.get('is_data')}
         used = {v for op in self.fwd_ops + self.bwd_ops for v in op.in_vids}
         self.feeds = {data[v].name: v for v in used if v in data}
@@ -238,7 +267,7 @@ class _Pipeline:
 
     def _backward(self, exe, env, acc):
         for op in self.bwd_ops:
-            self._apply(exe, op, env, False)
+            self._apply(exe, op, env, id(op) in self.bctx_needed)
         for p in self.params:
             g = env.get(self.grad_vid[p.name])
             if g is None:
@@ -294,6 +323,8 @@ class _Pipeline:
             for f in fetch_vars:
                 if f.vid in env and f.vid != self.loss.vid:
                     fetched[id(f)].append(_u(env[f.vid]).detach())
+            for v in self.drop_after_fwd:   # recomputed segments' intermediates
+                env.pop(v, None)
             envs[i] = env
         sig = tuple((vid, tuple(chunks[vid][0]._t.shape), str(chunks[vid][0]._t.dtype)) for vid in sorted(chunks))
         known = self._shapes.get(sig)
@@ -408,9 +439,17 @@ class _Pipeline:
                 clip._norm_hook = prev
 
 
-def build_pipeline(opt, loss, n_micro=1, schedule='1F1B', parameters=None, pp_group=None, dp_group=None):
-    """Turn ``loss``'s program into this rank's pipeline stage (see the module docstring)."""
+def build_pipeline(opt, loss, n_micro=1, schedule='1F1B', parameters=None, pp_group=None, dp_group=None,
+                   checkpoints=None):
+    """Turn ``loss``'s program into this rank's pipeline stage (see the module docstring).
+    checkpoints / a RecomputeOptimizer ``opt``: recompute segments inside the stages."""
     prog = loss.block.program
+    if isinstance(opt, G.RecomputeOptimizer):
+        checkpoints = opt._resolve(prog)
+        opt = opt._optimizer
+    if checkpoints:
+        blk = prog.global_block()
+        checkpoints = [blk.var(c) if isinstance(c, str) else c for c in checkpoints]
     from .amp import OptimizerWithMixedPrecision
     if isinstance(opt, OptimizerWithMixedPrecision):
         if opt._use_scaling:
@@ -431,7 +470,7 @@ def build_pipeline(opt, loss, n_micro=1, schedule='1F1B', parameters=None, pp_gr
     stage = pp_ranks.index(dist.get_rank())
     pipe = _Pipeline(prog, loss, opt, n_micro, '1F1B' if schedule == '1F1B' else 'FThenB', stage,
                      len(pp_ranks), pg, pp_ranks, dp_group.process_group if dp_group is not None else None)
-    pg_list = pipe.build_backward(parameters)
+    pg_list = pipe.build_backward(parameters, checkpoints)
     prog.__dict__['_pipeline'] = pipe
     prog.__dict__['_no_graph'] = True
     prog._bump()

@@ -27,7 +27,8 @@ def _program(guard, clip=None, skip=False, three=False):
             h0 = paddle.tanh(l1(x))
         with g('gpu:1'):
             l2 = nn.Linear(F_, F_ if three else C)
-            h1 = F.gelu(l2(h0))
+            z1 = l2(h0)
+            h1 = F.gelu(z1)
             if skip:
                 h1 = h1 + h0[:, :h1.shape[1]] * 0.5        # a skip edge 0 -> 1 used twice
         params = [l1.weight, l1.bias, l2.weight, l2.bias]
@@ -37,6 +38,7 @@ def _program(guard, clip=None, skip=False, three=False):
                 h1 = l3(h1) + 0.1 * paddle.sum(h0, axis=1, keepdim=True)   # skip edge 0 -> 2
             params += [l3.weight, l3.bias]
         loss = F.cross_entropy(h1, y)            # unguarded: follows its inputs' stage
+    main.__dict__['_test_vars'] = {'h0': h0, 'z1': z1}
     return main, loss, params
 
 
@@ -68,7 +70,7 @@ def _opt(name, clip):
     return paddle.optimizer.Momentum(0.3, momentum=0.9, grad_clip=c)
 
 
-def _pipe(rank, world, n_micro, schedule, clip, skip, three, use_fleet, opt_name, dp=1):
+def _pipe(rank, world, n_micro, schedule, clip, skip, three, use_fleet, opt_name, dp=1, recompute=False):
     import paddle_ray_amd as paddle
     from paddle_ray_amd import static
     paddle.enable_static()
@@ -81,20 +83,28 @@ def _pipe(rank, world, n_micro, schedule, clip, skip, three, use_fleet, opt_name
             st.pipeline_configs = {'accumulate_steps': n_micro, 'micro_batch_size': B // n_micro,
                                    'schedule_mode': schedule}
             st.hybrid_configs = {'dp_degree': dp, 'mp_degree': 1, 'pp_degree': world // dp}
+            if recompute:
+                st.recompute = True
+                st.recompute_configs = {'checkpoints': [v.name for v in main._test_vars.values()]}
             fleet.init(is_collective=True, strategy=st)
             fleet.distributed_optimizer(_opt(opt_name, clip)).minimize(loss)
         else:
-            static.PipelineOptimizer(_opt(opt_name, clip), num_microbatches=n_micro,
-                                     schedule_mode=schedule).minimize(loss)
+            inner = _opt(opt_name, clip)
+            if recompute:
+                inner = static.RecomputeOptimizer(inner)
+                inner._set_checkpoints(list(main._test_vars.values()))
+            static.PipelineOptimizer(inner, num_microbatches=n_micro, schedule_mode=schedule).minimize(loss)
     exe = static.Executor()
     losses = [float(exe.run(main, feed=f, fetch_list=[loss])[0]) for f in _data(3, B)]
     pipe = main._pipeline
     mine = {p.name for p in pipe.params}
     out = {i: p.numpy() for i, p in enumerate(params) if p.name in mine}
     n_ops = (len(pipe.fwd_ops), len(pipe.bwd_ops))
+    n_rc = sum(op.role == 'recompute' for op in pipe.bwd_ops)
     paddle.disable_static()
     return {'losses': losses, 'params': out, 'stage': pipe.stage, 'ops': n_ops,
-            'sends': len(pipe.fsend) + len(pipe.bsend)}
+            'sends': len(pipe.fsend) + len(pipe.bsend), 'recompute_ops': n_rc,
+            'dropped': len(pipe.drop_after_fwd)}
 
 
 @pytest.mark.parametrize('n_micro,schedule,use_fleet', [(1, 'F-then-B', False), (4, 'F-then-B', False),
@@ -111,6 +121,23 @@ def test_static_pipeline_matches_serial_2stages(tmp_path, n_micro, schedule, use
     for i, p in got.items():
         np.testing.assert_allclose(p, ref[i], rtol=1e-5, atol=1e-6)
     assert ref_losses[-1] < ref_losses[0]
+
+
+@pytest.mark.parametrize('use_fleet,schedule', [(False, '1F1B'), (True, 'F-then-B')])
+def test_static_pipeline_with_recompute(tmp_path, use_fleet, schedule):
+    """Pipeline + recompute (RecomputeOptimizer inside PipelineOptimizer, or fleet strategy.pipeline
+    + strategy.recompute): each stage re-runs its segment in the backward and matches the serial
+    run; the segments' intermediates are dropped per micro-batch."""
+    ref_losses, ref = _serial(None, False, False)
+    res = run_ranks(_pipe, 2, tmp_path, args=(4, schedule, None, False, False, use_fleet, 'momentum', 1, True))
+    got = {}
+    for o in res:
+        np.testing.assert_allclose(o['losses'], ref_losses, rtol=1e-5, atol=1e-6)
+        got.update(o['params'])
+        assert o['recompute_ops'] > 0, o
+    assert sum(o['dropped'] for o in res) > 0
+    for i, p in got.items():
+        np.testing.assert_allclose(p, ref[i], rtol=1e-5, atol=1e-6)
 
 
 def test_static_pipeline_with_data_parallel_2x2(tmp_path):
