@@ -416,7 +416,7 @@ def _static_pipeline(opt, loss, strategy, hcg, parameters, scaler):
     """strategy.pipeline: the program split by device_guard into one stage per rank of the
     pipeline group (static/pipeline.py; reference meta_optimizers/pipeline_optimizer.py:198)."""
     from ...static.pipeline import build_pipeline
-    for flag in ('sharding', 'localsgd', 'gradient_merge', 'lamb', 'lars'):
+    for flag in ('sharding', 'localsgd', 'lamb', 'lars'):
         if getattr(strategy, flag, False):
             raise NotImplementedError(f"static pipeline together with strategy.{flag} is not supported")
     if scaler is not None:
@@ -436,8 +436,12 @@ def _static_pipeline(opt, loss, strategy, hcg, parameters, scaler):
         ckpts = list((strategy.recompute_configs or {}).get('checkpoints') or [])
         if not ckpts:
             raise ValueError("strategy.recompute needs recompute_configs['checkpoints']")
+    gm = None
+    if getattr(strategy, 'gradient_merge', False):
+        gcfg = strategy.gradient_merge_configs or {}
+        gm = (int(gcfg.get('k_steps', 1)), bool(gcfg.get('avg', True)))
     return build_pipeline(opt, loss, n_micro, cfg.get('schedule_mode', '1F1B'), parameters, pp_group, dp_group,
-                          checkpoints=ckpts)
+                          checkpoints=ckpts, gradient_merge=gm)
 
 
 def strategy_with_pass_cfg(strategy, cfg):

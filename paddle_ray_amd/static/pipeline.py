@@ -389,7 +389,7 @@ class _Pipeline:
                     del benv
                 if known is None:
                     self._shapes[sig] = {'f': seen['f'] or [], 'b': seen['b'] or []}
-            self._step(acc, dev)
+            self._merge_or_step(acc, dev)
         finally:
             G._STATIC[0] = prev
         # the loss: micro-batch mean on the last stage, broadcast over the pipeline
@@ -407,6 +407,30 @@ class _Pipeline:
             else:
                 outs.append(None)
         return [(o.numpy() if return_numpy else o) if o is not None else None for o in outs]
+
+    def _merge_or_step(self, acc, dev):
+        """Gradient merge (strategy.gradient_merge over the pipeline): the micro-batch-accumulated
+        gradients of gm_k consecutive runs are summed (averaged with gm_avg) and the optimizer
+        steps on the k-th run only (reference gradient_merge_optimizer.py / pipeline: the merge
+        window spans whole pipeline runs)."""
+        k = getattr(self, 'gm_k', 1)
+        if k <= 1:
+            self._step(acc, dev)
+            return
+        gm = self.__dict__.setdefault('_gm', {})
+        for name, g in acc.items():
+            if name in gm:
+                gm[name].add_(g)
+            else:
+                gm[name] = g
+        self._gm_n = getattr(self, '_gm_n', 0) + 1
+        if self._gm_n < k:
+            return
+        if getattr(self, 'gm_avg', True):
+            for g in gm.values():
+                g.div_(k)
+        self._gm, self._gm_n = {}, 0
+        self._step(gm, dev)
 
     def _step(self, acc, dev):
         from ..nn.clip import ClipGradByGlobalNorm
@@ -440,7 +464,7 @@ class _Pipeline:
 
 
 def build_pipeline(opt, loss, n_micro=1, schedule='1F1B', parameters=None, pp_group=None, dp_group=None,
-                   checkpoints=None):
+                   checkpoints=None, gradient_merge=None):
     """Turn ``loss``'s program into this rank's pipeline stage (see the module docstring).
     checkpoints / a RecomputeOptimizer ``opt``: recompute segments inside the stages."""
     prog = loss.block.program
@@ -471,6 +495,8 @@ def build_pipeline(opt, loss, n_micro=1, schedule='1F1B', parameters=None, pp_gr
     pipe = _Pipeline(prog, loss, opt, n_micro, '1F1B' if schedule == '1F1B' else 'FThenB', stage,
                      len(pp_ranks), pg, pp_ranks, dp_group.process_group if dp_group is not None else None)
     pg_list = pipe.build_backward(parameters, checkpoints)
+    if gradient_merge is not None:
+        pipe.gm_k, pipe.gm_avg = int(gradient_merge[0]), bool(gradient_merge[1])
     prog.__dict__['_pipeline'] = pipe
     prog.__dict__['_no_graph'] = True
     prog._bump()

@@ -140,6 +140,59 @@ def test_static_pipeline_with_recompute(tmp_path, use_fleet, schedule):
         np.testing.assert_allclose(p, ref[i], rtol=1e-5, atol=1e-6)
 
 
+def _pipe_gm(rank, world, k):
+    import paddle_ray_amd as paddle
+    from paddle_ray_amd import static
+    from paddle_ray_amd.distributed import fleet
+    paddle.enable_static()
+    main, loss, params = _program(True)
+    with static.program_guard(main):
+        st = fleet.DistributedStrategy()
+        st.pipeline = True
+        st.pipeline_configs = {'accumulate_steps': 2, 'micro_batch_size': B // 2, 'schedule_mode': '1F1B'}
+        st.gradient_merge = True
+        st.gradient_merge_configs = {'k_steps': k, 'avg': True}
+        st.hybrid_configs = {'dp_degree': 1, 'mp_degree': 1, 'pp_degree': world}
+        fleet.init(is_collective=True, strategy=st)
+        fleet.distributed_optimizer(_opt('momentum', None)).minimize(loss)
+    exe = static.Executor()
+    losses = [float(exe.run(main, feed=f, fetch_list=[loss])[0]) for f in _data(2 * k, B)]
+    mine = {p.name for p in main._pipeline.params}
+    out = {i: p.numpy() for i, p in enumerate(params) if p.name in mine}
+    paddle.disable_static()
+    return {'losses': losses, 'params': out}
+
+
+def test_static_pipeline_with_gradient_merge(tmp_path):
+    """strategy.pipeline + gradient_merge (k = 2, avg): two pipeline runs, one optimizer step --
+    the serial program stepping once per concatenated pair of batches."""
+    import paddle_ray_amd as paddle
+    from paddle_ray_amd import static
+    k = 2
+    data = _data(2 * k, B)
+    paddle.enable_static()
+    main, loss, params = _program(False)
+    with static.program_guard(main):
+        _opt('momentum', None).minimize(loss)
+    exe = static.Executor()
+    ref_losses = []
+    for j in range(2):
+        pair = data[j * k:(j + 1) * k]
+        feed = {n: np.concatenate([f[n] for f in pair]) for n in ('x', 'y')}
+        ref_losses.append(float(exe.run(main, feed=feed, fetch_list=[loss])[0]))
+    ref = [p.numpy() for p in params]
+    paddle.disable_static()
+    res = run_ranks(_pipe_gm, 2, tmp_path, args=(k,))
+    got = {}
+    for o in res:
+        pl = np.asarray(o['losses']).reshape(2, k).mean(1)
+        np.testing.assert_allclose(pl, ref_losses, rtol=1e-5, atol=1e-6)
+        got.update(o['params'])
+    assert sorted(got) == [0, 1, 2, 3]
+    for i, p in got.items():
+        np.testing.assert_allclose(p, ref[i], rtol=1e-5, atol=1e-6)
+
+
 def test_static_pipeline_with_data_parallel_2x2(tmp_path):
     """fleet hybrid dp 2 x pp 2: each stage's gradients are averaged over its data-parallel
     replica (same batch on both replicas here: the serial run is the reference)."""
