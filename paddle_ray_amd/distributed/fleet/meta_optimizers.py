@@ -416,9 +416,11 @@ def _static_pipeline(opt, loss, strategy, hcg, parameters, scaler):
     """strategy.pipeline: the program split by device_guard into one stage per rank of the
     pipeline group (static/pipeline.py; reference meta_optimizers/pipeline_optimizer.py:198)."""
     from ...static.pipeline import build_pipeline
-    for flag in ('sharding', 'localsgd', 'lamb', 'lars'):
+    for flag in ('sharding', 'localsgd'):
         if getattr(strategy, flag, False):
             raise NotImplementedError(f"static pipeline together with strategy.{flag} is not supported")
+    # (strategy.lamb / lars: fleet.distributed_optimizer already swapped the inner optimizer;
+    # every stage steps it on its own parameters)
     if scaler is not None:
         raise NotImplementedError("static pipeline with fp16 loss scaling is not supported (use bf16)")
     cfg = dict(strategy.pipeline_configs or {})

@@ -193,6 +193,54 @@ def test_static_pipeline_with_gradient_merge(tmp_path):
         np.testing.assert_allclose(p, ref[i], rtol=1e-5, atol=1e-6)
 
 
+def _pipe_lars(rank, world):
+    import paddle_ray_amd as paddle
+    from paddle_ray_amd import static
+    from paddle_ray_amd.distributed import fleet
+    paddle.enable_static()
+    main, loss, params = _program(True)
+    with static.program_guard(main):
+        st = fleet.DistributedStrategy()
+        st.pipeline = True
+        st.pipeline_configs = {'accumulate_steps': 2, 'micro_batch_size': B // 2, 'schedule_mode': '1F1B'}
+        st.lars = True
+        st.lars_configs = {'lars_coeff': 0.01, 'lars_weight_decay': 0.001}
+        st.hybrid_configs = {'dp_degree': 1, 'mp_degree': 1, 'pp_degree': world}
+        fleet.init(is_collective=True, strategy=st)
+        fleet.distributed_optimizer(_opt('momentum', None)).minimize(loss)
+    exe = static.Executor()
+    losses = [float(exe.run(main, feed=f, fetch_list=[loss])[0]) for f in _data(3, B)]
+    pipe = main._pipeline
+    mine = {p.name for p in pipe.params}
+    out = {i: p.numpy() for i, p in enumerate(params) if p.name in mine}
+    kind = type(pipe.opt).__name__
+    paddle.disable_static()
+    return {'losses': losses, 'params': out, 'opt': kind}
+
+
+def test_static_pipeline_with_lars_swap(tmp_path):
+    """strategy.lars under the pipeline: every stage steps LarsMomentum (per-parameter trust
+    ratios on its own parameters), as the serial program minimized with LarsMomentum."""
+    import paddle_ray_amd as paddle
+    from paddle_ray_amd import static
+    paddle.enable_static()
+    main, loss, params = _program(False)
+    with static.program_guard(main):
+        paddle.optimizer.LarsMomentum(0.3, momentum=0.9, lars_coeff=0.01, lars_weight_decay=0.001).minimize(loss)
+    exe = static.Executor()
+    ref_losses = [float(exe.run(main, feed=f, fetch_list=[loss])[0]) for f in _data(3, B)]
+    ref = [p.numpy() for p in params]
+    paddle.disable_static()
+    res = run_ranks(_pipe_lars, 2, tmp_path)
+    got = {}
+    for o in res:
+        assert o['opt'] == 'LarsMomentum'
+        np.testing.assert_allclose(o['losses'], ref_losses, rtol=1e-5, atol=1e-6)
+        got.update(o['params'])
+    for i, p in got.items():
+        np.testing.assert_allclose(p, ref[i], rtol=1e-5, atol=1e-6)
+
+
 def test_static_pipeline_with_data_parallel_2x2(tmp_path):
     """fleet hybrid dp 2 x pp 2: each stage's gradients are averaged over its data-parallel
     replica (same batch on both replicas here: the serial run is the reference)."""
