@@ -416,9 +416,13 @@ def _static_pipeline(opt, loss, strategy, hcg, parameters, scaler):
     """strategy.pipeline: the program split by device_guard into one stage per rank of the
     pipeline group (static/pipeline.py; reference meta_optimizers/pipeline_optimizer.py:198)."""
     from ...static.pipeline import build_pipeline
-    for flag in ('sharding', 'localsgd'):
-        if getattr(strategy, flag, False):
-            raise NotImplementedError(f"static pipeline together with strategy.{flag} is not supported")
+    if getattr(strategy, 'localsgd', False):
+        raise NotImplementedError("static pipeline together with strategy.localsgd is not supported")
+    shard = bool(getattr(strategy, 'sharding', False))
+    if shard:
+        stage = int((strategy.sharding_configs or {}).get('stage', 1))
+        if stage != 1:
+            raise NotImplementedError(f"static pipeline with sharding supports stage 1 (got stage {stage})")
     # (strategy.lamb / lars: fleet.distributed_optimizer already swapped the inner optimizer;
     # every stage steps it on its own parameters)
     if scaler is not None:
@@ -443,7 +447,7 @@ def _static_pipeline(opt, loss, strategy, hcg, parameters, scaler):
         gcfg = strategy.gradient_merge_configs or {}
         gm = (int(gcfg.get('k_steps', 1)), bool(gcfg.get('avg', True)))
     return build_pipeline(opt, loss, n_micro, cfg.get('schedule_mode', '1F1B'), parameters, pp_group, dp_group,
-                          checkpoints=ckpts, gradient_merge=gm)
+                          checkpoints=ckpts, gradient_merge=gm, shard=shard)
 
 
 def strategy_with_pass_cfg(strategy, cfg):

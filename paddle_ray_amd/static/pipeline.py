@@ -445,26 +445,38 @@ class _Pipeline:
         clip = getattr(opt, '_grad_clip', None)
         prev = None
         is_gn = isinstance(clip, ClipGradByGlobalNorm)
-        if is_gn and self.n_stages > 1:
+        plan = getattr(self, 'shard_plan', None)
+        hook = is_gn and (self.n_stages > 1 or plan is not None)
+        if hook:
             # every stage joins the one all-reduce of the squared norms (a stage without
             # gradients contributes zero), the clip then uses the pipeline-wide norm
             from ..ops.fused import global_l2_norm_sq
             gs = [g for p, g in zip(ps, grads) if getattr(p, 'need_clip', True)]
             sq = global_l2_norm_sq(gs) if gs else None
             tot = sq.reshape(()).float().clone() if sq is not None else torch.zeros((), device=dev)
-            dist.all_reduce(tot, group=self.pp_group)
+            if self.n_stages > 1:
+                dist.all_reduce(tot, group=self.pp_group)
             prev = clip._norm_hook
             clip._norm_hook = lambda _sq: tot
         try:
-            if ps:
+            if plan is not None:
+                # sharding stage 1 over the stage's data-parallel replicas: each steps the
+                # parameters it owns (the norm above covered every gradient), then the owners
+                # broadcast them
+                own = {p.name for p in plan.owned(ps)}
+                sel = [(p, g) for p, g in zip(ps, grads) if p.name in own]
+                if sel:
+                    G._optimize_fn(opt, [p for p, _ in sel], *[Tensor(g) for _, g in sel])
+                plan.broadcast(self.params)
+            elif ps:
                 G._optimize_fn(opt, ps, *[Tensor(g) for g in grads])
         finally:
-            if is_gn and self.n_stages > 1:
+            if hook:
                 clip._norm_hook = prev
 
 
 def build_pipeline(opt, loss, n_micro=1, schedule='1F1B', parameters=None, pp_group=None, dp_group=None,
-                   checkpoints=None, gradient_merge=None):
+                   checkpoints=None, gradient_merge=None, shard=False):
     """Turn ``loss``'s program into this rank's pipeline stage (see the module docstring).
     checkpoints / a RecomputeOptimizer ``opt``: recompute segments inside the stages."""
     prog = loss.block.program
@@ -497,6 +509,10 @@ def build_pipeline(opt, loss, n_micro=1, schedule='1F1B', parameters=None, pp_gr
     pg_list = pipe.build_backward(parameters, checkpoints)
     if gradient_merge is not None:
         pipe.gm_k, pipe.gm_avg = int(gradient_merge[0]), bool(gradient_merge[1])
+    if shard and dp_group is not None and dp_group.nranks > 1:
+        # sharding stage 1 inside each stage, over its data-parallel replicas
+        from ..distributed.fleet.meta_optimizers import _ShardPlan
+        pipe.shard_plan = _ShardPlan(pipe.params, dp_group)
     prog.__dict__['_pipeline'] = pipe
     prog.__dict__['_no_graph'] = True
     prog._bump()

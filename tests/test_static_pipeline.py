@@ -70,7 +70,8 @@ def _opt(name, clip):
     return paddle.optimizer.Momentum(0.3, momentum=0.9, grad_clip=c)
 
 
-def _pipe(rank, world, n_micro, schedule, clip, skip, three, use_fleet, opt_name, dp=1, recompute=False):
+def _pipe(rank, world, n_micro, schedule, clip, skip, three, use_fleet, opt_name, dp=1, recompute=False,
+          shard=False):
     import paddle_ray_amd as paddle
     from paddle_ray_amd import static
     paddle.enable_static()
@@ -83,6 +84,9 @@ def _pipe(rank, world, n_micro, schedule, clip, skip, three, use_fleet, opt_name
             st.pipeline_configs = {'accumulate_steps': n_micro, 'micro_batch_size': B // n_micro,
                                    'schedule_mode': schedule}
             st.hybrid_configs = {'dp_degree': dp, 'mp_degree': 1, 'pp_degree': world // dp}
+            if shard:
+                st.sharding = True
+                st.sharding_configs = {'stage': 1}
             if recompute:
                 st.recompute = True
                 st.recompute_configs = {'checkpoints': [v.name for v in main._test_vars.values()]}
@@ -101,10 +105,12 @@ def _pipe(rank, world, n_micro, schedule, clip, skip, three, use_fleet, opt_name
     out = {i: p.numpy() for i, p in enumerate(params) if p.name in mine}
     n_ops = (len(pipe.fwd_ops), len(pipe.bwd_ops))
     n_rc = sum(op.role == 'recompute' for op in pipe.bwd_ops)
+    n_states = len(getattr(pipe.opt, '_accumulators', {}).get('moment1', {}))
+    n_params = len(pipe.params)
     paddle.disable_static()
     return {'losses': losses, 'params': out, 'stage': pipe.stage, 'ops': n_ops,
             'sends': len(pipe.fsend) + len(pipe.bsend), 'recompute_ops': n_rc,
-            'dropped': len(pipe.drop_after_fwd)}
+            'dropped': len(pipe.drop_after_fwd), 'n_states': n_states, 'n_params': n_params}
 
 
 @pytest.mark.parametrize('n_micro,schedule,use_fleet', [(1, 'F-then-B', False), (4, 'F-then-B', False),
@@ -251,6 +257,23 @@ def test_static_pipeline_with_data_parallel_2x2(tmp_path):
         for i, p in o['params'].items():
             np.testing.assert_allclose(p, ref[i], rtol=1e-5, atol=1e-6)
     assert sorted({o['stage'] for o in res}) == [0, 1]
+
+
+def test_static_pipeline_with_sharding_2x2(tmp_path):
+    """pp 2 x dp 2 with sharding stage 1 inside each stage: a replica steps only the parameters it
+    owns (AdamW states 1/2 per replica), the global-norm clip still sees every gradient, the owners
+    broadcast the updates."""
+    ref_losses, ref = _serial(0.05, False, False, 'adam')
+    res = run_ranks(_pipe, 4, tmp_path, args=(2, '1F1B', 0.05, False, False, True, 'adam', 2, False, True))
+    for o in res:
+        np.testing.assert_allclose(o['losses'], ref_losses, rtol=1e-5, atol=1e-6)
+        for i, p in o['params'].items():
+            np.testing.assert_allclose(p, ref[i], rtol=1e-4, atol=1e-6)
+    assert sorted({o['stage'] for o in res}) == [0, 1]
+    for stage in (0, 1):
+        reps = [o for o in res if o['stage'] == stage]
+        assert sum(o['n_states'] for o in reps) == reps[0]['n_params']
+        assert all(0 < o['n_states'] < o['n_params'] for o in reps)
 
 
 def test_static_pipeline_skip_edges_clip_adam_3stages(tmp_path):
