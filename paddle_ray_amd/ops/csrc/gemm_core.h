@@ -95,6 +95,24 @@ __device__ __forceinline__ float act(float x) {
   if (E == kRelu) return fmaxf(x, 0.f);
   return x;
 }
+// tanh-GELU and its derivative for two elements as packed f32 math (v_pk_mul / v_pk_fma / v_pk_add:
+// two lanes' worth per instruction in the serialised GEMM epilogue; the exp / rcp stay scalar)
+typedef float pf32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ pf32x2 gelu_tanh_d2(pf32x2 x, pf32x2& d) {
+  const pf32x2 x2 = x * x;
+  const pf32x2 u = -x * (x2 * (kGT3 * kLog2e) + (kGT1 * kLog2e));
+  pf32x2 e;
+  e.x = __builtin_amdgcn_exp2f(u.x);
+  e.y = __builtin_amdgcn_exp2f(u.y);
+  const pf32x2 den = e + 1.f;
+  pf32x2 sg;
+  sg.x = __builtin_amdgcn_rcpf(den.x);
+  sg.y = __builtin_amdgcn_rcpf(den.y);
+  const pf32x2 y = x * sg;
+  d = (y * (1.f - sg)) * (x2 * (3.f * kGT3) + kGT1) + sg;
+  return y;
+}
+
 // gelu(x) and gelu'(x) sharing the one transcendental
 template <int E>
 __device__ __forceinline__ float act_d(float x, float& d) {

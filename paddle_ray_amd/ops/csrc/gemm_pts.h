@@ -364,8 +364,17 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_pts_kernel(const uint16_t* __r
               }
             } else if constexpr (epi_gd(E)) {
               float d[4];
+              // (nts bit 2: the scalar form, A/B)
+              if (E == kGeluTanhD && !(nts & 4)) {
+                pf32x2 d01, d23;
+                const pf32x2 y01 = gelu_tanh_d2(pf32x2{v[0], v[1]}, d01);
+                const pf32x2 y23 = gelu_tanh_d2(pf32x2{v[2], v[3]}, d23);
+                v[0] = y01.x, v[1] = y01.y, v[2] = y23.x, v[3] = y23.y;
+                d[0] = d01.x, d[1] = d01.y, d[2] = d23.x, d[3] = d23.y;
+              } else {
 #pragma unroll
-              for (int r = 0; r < 4; ++r) v[r] = act_d<E>(v[r], d[r]);
+                for (int r = 0; r < 4; ++r) v[r] = act_d<E>(v[r], d[r]);
+              }
               pz[u][0] = pack2<T>(d[0], d[1]);
               pz[u][1] = pack2<T>(d[2], d[3]);
             } else if constexpr (E != kNone) {

@@ -118,6 +118,8 @@ void launch_pts(const void* A, const void* B, const void* bias, void* C, void* Z
     case 5: nts = (E != kNone) ? 2 : 0; break;
     default: break;
   }
+  static const bool pk = !getenv("PRA_PTS_PK") || atoi(getenv("PRA_PTS_PK")) != 0;
+  if (!pk) nts |= 4;  // scalar tanh-GELU' epilogue (packed-f32 form by default)
   gemm_pts_kernel<T, CF, AK, BK, E, BETA, VAR><<<grid, CF::NT, 0, s>>>(
       static_cast<const uint16_t*>(A), static_cast<const uint16_t*>(B), static_cast<const uint16_t*>(bias),
       static_cast<uint16_t*>(C), static_cast<uint16_t*>(Z), colsum, M, N, K, lda, ldb, ldc, ldz, ctr, nts);
