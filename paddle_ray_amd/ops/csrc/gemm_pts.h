@@ -320,6 +320,7 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_pts_kernel(const uint16_t* __r
         __builtin_amdgcn_sched_barrier(0);  // one 16-row block at a time (ring loads stay in place; no accumulator hoisting)
         const int m = rb + i * 16;
         const bool mok = m < M;
+        const float mk = (mok || (nts & 4)) ? 1.f : 0.f;
         const int64_t mr = mok ? m : 0;
         if constexpr (ZOP) {
           // ring: pass-row q + ZR - 1's loads go out before pass-row q is consumed
@@ -357,10 +358,17 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_pts_kernel(const uint16_t* __r
                                   to_f<T>(gz[u].y >> 16)};
 #pragma unroll
               for (int r = 0; r < 4; ++r) v[r] *= zfac<E>(z[r]);
-              // bias-gradient column sums of the fp32 products (rows past M contribute zeros)
-              if (mok) {
+              // bias-gradient column sums of the fp32 products (rows past M contribute zeros:
+              // a 0 / 1 factor per row block instead of a select per element; those rows hold
+              // finite copies of row M-1, the operand DMA clamps them)
+              if (nts & 4) {  // (A/B: the per-element select form)
+                if (mok) {
 #pragma unroll
-                for (int r = 0; r < 4; ++r) cs[jq + u][r] += v[r];
+                  for (int r = 0; r < 4; ++r) cs[jq + u][r] += v[r];
+                }
+              } else {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) cs[jq + u][r] = fmaf(v[r], mk, cs[jq + u][r]);
               }
             } else if constexpr (epi_gd(E)) {
               float d[4];

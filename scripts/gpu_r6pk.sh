@@ -6,7 +6,7 @@ export TMPDIR=/tmp
 fatal() { case $1 in 124|137|134|139) return 0;; esac; return 1; }
 step() { local name=$1 t=$2; shift 2; timeout -k 10 "$t" "$@" > $OUT/$name.log 2>&1; local rc=$?;
          echo "[$name rc=$rc]"; grep -v amdgpu.ids $OUT/$name.log | tail -n 3 | cut -c1-200; if fatal $rc; then exit $rc; fi; }
-step gemmtests 600 python -u -m pytest tests/test_gemm_lds_gpu.py tests/test_gemm_gpu.py tests/test_fused_mlp_gpu.py -m gpu -q -x --timeout 120 --timeout-method thread -p no:cacheprovider
+step gemmtests 600 python -u -m pytest tests/test_gemm_lds_gpu.py tests/test_gemm_gpu.py -m gpu -q -x --timeout 120 --timeout-method thread -p no:cacheprovider
 step e1 200 env PRA_PTS_PK=1 python scripts/r6_dyn_probe.py
 step e0 200 env PRA_PTS_PK=0 python scripts/r6_dyn_probe.py
 step e1b 200 env PRA_PTS_PK=1 python scripts/r6_dyn_probe.py
