@@ -75,7 +75,10 @@ def test_overlap_state_reads_see_finished_update(monkeypatch):
     _train(monkeypatch, True, steps=2, extra=extra)
     # parameter names differ between the two models (global counters): compare in order
     assert len(seen['m1']) == len(seen['m1_ref']) > 0 and len(seen['w']) == len(seen['w_ref'])
+    # (the two runs differ only by the clip norm's atomic order; after the first update a bf16
+    # rounding flip can move an element's second gradient, so near-zero moment entries get an
+    # absolute tolerance scaled to the tensor: a stale read would miss a whole update)
     for i, (a, b) in enumerate(zip(seen['m1'], seen['m1_ref'])):
-        assert torch.allclose(a, b, rtol=2e-2, atol=1e-6), i
+        assert torch.allclose(a, b, rtol=2e-2, atol=2e-3 * b.abs().max().item() + 1e-6), i
     for i, (a, b) in enumerate(zip(seen['w'], seen['w_ref'])):
         assert torch.allclose(a, b, rtol=2e-2, atol=2e-3), i
