@@ -416,8 +416,12 @@ def _static_pipeline(opt, loss, strategy, hcg, parameters, scaler):
     """strategy.pipeline: the program split by device_guard into one stage per rank of the
     pipeline group (static/pipeline.py; reference meta_optimizers/pipeline_optimizer.py:198)."""
     from ...static.pipeline import build_pipeline
+    ls = None
     if getattr(strategy, 'localsgd', False):
-        raise NotImplementedError("static pipeline together with strategy.localsgd is not supported")
+        if getattr(strategy, 'sharding', False):
+            raise NotImplementedError("static pipeline: localsgd together with sharding is not supported")
+        lcfg = strategy.localsgd_configs or {}
+        ls = (int(lcfg.get('k_steps', 1)), int(lcfg.get('begin_step', 1)))
     shard = bool(getattr(strategy, 'sharding', False))
     if shard:
         stage = int((strategy.sharding_configs or {}).get('stage', 1))
@@ -447,7 +451,7 @@ def _static_pipeline(opt, loss, strategy, hcg, parameters, scaler):
         gcfg = strategy.gradient_merge_configs or {}
         gm = (int(gcfg.get('k_steps', 1)), bool(gcfg.get('avg', True)))
     return build_pipeline(opt, loss, n_micro, cfg.get('schedule_mode', '1F1B'), parameters, pp_group, dp_group,
-                          checkpoints=ckpts, gradient_merge=gm, shard=shard)
+                          checkpoints=ckpts, gradient_merge=gm, shard=shard, localsgd=ls)
 
 
 def strategy_with_pass_cfg(strategy, cfg):

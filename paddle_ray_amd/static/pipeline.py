@@ -436,7 +436,8 @@ class _Pipeline:
         from ..nn.clip import ClipGradByGlobalNorm
         ps = [p for p in self.params if p.name in acc]
         grads = [acc[p.name] for p in ps]
-        if self.dp_group is not None and dist.get_world_size(self.dp_group) > 1:
+        local = getattr(self, 'localsgd', None)
+        if local is None and self.dp_group is not None and dist.get_world_size(self.dp_group) > 1:
             n = dist.get_world_size(self.dp_group)
             for g in grads:
                 dist.all_reduce(g, group=self.dp_group)
@@ -473,10 +474,29 @@ class _Pipeline:
         finally:
             if hook:
                 clip._norm_hook = prev
+        if local is not None and self.dp_group is not None and dist.get_world_size(self.dp_group) > 1:
+            # localsgd over the stage's data-parallel replicas (no gradient all-reduce): parameters
+            # averaged after every step through begin_step, then k_steps after the last averaging
+            # (reference localsgd_optimizer.py:206)
+            k, begin = local
+            self._ls_steps = getattr(self, '_ls_steps', 0) + 1
+            last = getattr(self, '_ls_last', 0)
+            if self._ls_steps <= begin or self._ls_steps - last >= k:
+                n = dist.get_world_size(self.dp_group)
+                ts = [_u(p) for p in self.params]
+                flat = torch.cat([t.detach().reshape(-1) for t in ts])
+                dist.all_reduce(flat, group=self.dp_group)
+                flat.div_(n)
+                off = 0
+                with torch.no_grad():
+                    for t in ts:
+                        t.copy_(flat[off:off + t.numel()].view(t.shape))
+                        off += t.numel()
+                self._ls_last = self._ls_steps
 
 
 def build_pipeline(opt, loss, n_micro=1, schedule='1F1B', parameters=None, pp_group=None, dp_group=None,
-                   checkpoints=None, gradient_merge=None, shard=False):
+                   checkpoints=None, gradient_merge=None, shard=False, localsgd=None):
     """Turn ``loss``'s program into this rank's pipeline stage (see the module docstring).
     checkpoints / a RecomputeOptimizer ``opt``: recompute segments inside the stages."""
     prog = loss.block.program
@@ -509,6 +529,8 @@ def build_pipeline(opt, loss, n_micro=1, schedule='1F1B', parameters=None, pp_gr
     pg_list = pipe.build_backward(parameters, checkpoints)
     if gradient_merge is not None:
         pipe.gm_k, pipe.gm_avg = int(gradient_merge[0]), bool(gradient_merge[1])
+    if localsgd is not None:
+        pipe.localsgd = (max(1, int(localsgd[0])), max(1, int(localsgd[1])))
     if shard and dp_group is not None and dp_group.nranks > 1:
         # sharding stage 1 inside each stage, over its data-parallel replicas
         from ..distributed.fleet.meta_optimizers import _ShardPlan

@@ -276,6 +276,47 @@ def test_static_pipeline_with_sharding_2x2(tmp_path):
         assert all(0 < o['n_states'] < o['n_params'] for o in reps)
 
 
+def _pipe_local(rank, world, localsgd):
+    import paddle_ray_amd as paddle
+    from paddle_ray_amd import static
+    from paddle_ray_amd.distributed import fleet
+    paddle.enable_static()
+    main, loss, params = _program(True)
+    with static.program_guard(main):
+        st = fleet.DistributedStrategy()
+        st.pipeline = True
+        st.pipeline_configs = {'accumulate_steps': 2, 'micro_batch_size': B // 2, 'schedule_mode': '1F1B'}
+        st.hybrid_configs = {'dp_degree': 2, 'mp_degree': 1, 'pp_degree': 2}
+        if localsgd:
+            st.localsgd = True
+            st.localsgd_configs = {'k_steps': 1, 'begin_step': 1}
+        fleet.init(is_collective=True, strategy=st)
+        fleet.distributed_optimizer(paddle.optimizer.SGD(0.3)).minimize(loss)
+    dp_rank = fleet.get_hybrid_communicate_group().get_data_parallel_rank()
+    exe = static.Executor()
+    data = _data(6, B)[dp_rank::2]          # a different batch on each data-parallel replica
+    for f in data:
+        exe.run(main, feed=f, fetch_list=[loss])
+    pipe = main._pipeline
+    mine = {p.name for p in pipe.params}
+    out = {i: p.numpy() for i, p in enumerate(params) if p.name in mine}
+    paddle.disable_static()
+    return {'params': out, 'stage': pipe.stage}
+
+
+def test_static_pipeline_with_localsgd_2x2(tmp_path):
+    """pp 2 x dp 2 with localsgd (k_steps 1): replicas step on their own batches and average the
+    parameters, which for SGD equals the data-parallel gradient all-reduce."""
+    (tmp_path / 'a').mkdir()
+    (tmp_path / 'b').mkdir()
+    loc = run_ranks(_pipe_local, 4, tmp_path / 'a', args=(True,))
+    ref = run_ranks(_pipe_local, 4, tmp_path / 'b', args=(False,))
+    for o, r in zip(loc, ref):
+        assert o['stage'] == r['stage']
+        for i, p in o['params'].items():
+            np.testing.assert_allclose(p, r['params'][i], rtol=1e-5, atol=1e-6)
+
+
 def test_static_pipeline_skip_edges_clip_adam_3stages(tmp_path):
     """Three stages with activations used on two later stages (skip edges) and gradients summed
     across stages, AdamW, a global-norm clip over all stages."""
