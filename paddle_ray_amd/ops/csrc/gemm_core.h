@@ -113,6 +113,26 @@ __device__ __forceinline__ pf32x2 gelu_tanh_d2(pf32x2 x, pf32x2& d) {
   return y;
 }
 
+// erf-GELU and its derivative for two elements, packed f32 (erf_from_exp's rational
+// approximation; exp / rcp / sign transfer per element)
+__device__ __forceinline__ pf32x2 gelu_erf_d2(pf32x2 x, pf32x2& d) {
+  const pf32x2 u = x * 0.70710678118654752f;
+  const pf32x2 w = -(u * u) * kLog2e;
+  pf32x2 e, t;
+  e.x = __builtin_amdgcn_exp2f(w.x);
+  e.y = __builtin_amdgcn_exp2f(w.y);
+  const pf32x2 den = pf32x2{fabsf(u.x), fabsf(u.y)} * 0.3275911f + 1.f;
+  t.x = __builtin_amdgcn_rcpf(den.x);
+  t.y = __builtin_amdgcn_rcpf(den.y);
+  const pf32x2 p =
+      t * (t * (t * (t * (t * 1.061405429f + -1.453152027f) + 1.421413741f) + -0.284496736f) + 0.254829592f);
+  const pf32x2 m = 1.f - p * e;  // erf(|u|)
+  const pf32x2 er = pf32x2{copysignf(m.x, u.x), copysignf(m.y, u.y)};
+  const pf32x2 h = er * 0.5f + 0.5f;
+  d = (x * 0.3989422804014327f) * e + h;
+  return x * h;
+}
+
 // gelu(x) and gelu'(x) sharing the one transcendental
 template <int E>
 __device__ __forceinline__ float act_d(float x, float& d) {

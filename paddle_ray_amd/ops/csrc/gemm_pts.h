@@ -373,10 +373,12 @@ __global__ __launch_bounds__(CF::NT, 1) void gemm_pts_kernel(const uint16_t* __r
             } else if constexpr (epi_gd(E)) {
               float d[4];
               // (nts bit 2: the scalar form, A/B)
-              if (E == kGeluTanhD && !(nts & 4)) {
+              if (!(nts & 4)) {
                 pf32x2 d01, d23;
-                const pf32x2 y01 = gelu_tanh_d2(pf32x2{v[0], v[1]}, d01);
-                const pf32x2 y23 = gelu_tanh_d2(pf32x2{v[2], v[3]}, d23);
+                const pf32x2 y01 = E == kGeluTanhD ? gelu_tanh_d2(pf32x2{v[0], v[1]}, d01)
+                                                   : gelu_erf_d2(pf32x2{v[0], v[1]}, d01);
+                const pf32x2 y23 = E == kGeluTanhD ? gelu_tanh_d2(pf32x2{v[2], v[3]}, d23)
+                                                   : gelu_erf_d2(pf32x2{v[2], v[3]}, d23);
                 v[0] = y01.x, v[1] = y01.y, v[2] = y23.x, v[3] = y23.y;
                 d[0] = d01.x, d[1] = d01.y, d[2] = d23.x, d[3] = d23.y;
               } else {
