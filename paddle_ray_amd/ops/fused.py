@@ -1380,7 +1380,8 @@ def _gemm_hip(layout, a, b, out=None, bias=None, z=None, epi=None, beta=0, want_
         return None
     persist = (layout == GEMM_NT and ((_GEMM_MODE == 'auto' and _nt_in_tree(a, b)) or
                                       (epi == 'mulz' and _MLP_MULZ_PTS))) or \
-        (layout == GEMM_FWD and epi in ('gelu_d', 'gelu_tanh_d') and _MLP_MULZ_PTS)
+        (layout == GEMM_FWD and epi in ('gelu_d', 'gelu_tanh_d') and _MLP_MULZ_PTS) or \
+        (layout == GEMM_FWD and epi is None and _FWD_LONGK_PTS and a.shape[1] >= 4096)
     if _GEMM_MODE == 'auto' and layout == GEMM_NT and not persist and epi != 'mulz' and \
             not (_MLP_DGELU_EPI and epi in ('dgelu', 'dgelu_tanh')):
         return None
@@ -1439,6 +1440,9 @@ def _gemm_hip(layout, a, b, out=None, bias=None, z=None, epi=None, beta=0, want_
 # hipBLASLt: 22.5 / 61.6 / 98.5 us vs 24.5 / 63.6 / 130.9 us (profiles/r4/gemm_pts_bert.log);
 # at GPT-1.3B's K = 2048..8192 hipBLASLt's stream-K kernel stays ahead (gemm_pts_15shapes.log).
 _NT_SHORTK = __import__('os').environ.get('PRA_GEMM_NT_SHORTK', '1') == '1'
+# long-K x·W (GPT's fc2 forward, K = 8192) on the persistent 4-wave kernel: 385.1 vs 394.5 us per-tile
+# (scripts/r6_fwd_policy_probe.py); PRA_GEMM_FWD_LONGK_PTS=0 keeps the per-tile kernel (A/B)
+_FWD_LONGK_PTS = __import__('os').environ.get('PRA_GEMM_FWD_LONGK_PTS', '1') == '1'
 _PERSIST_BIT = 256
 
 
